@@ -1,0 +1,279 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident fingerprint-hash throughput of the reconcile-rs hot path on MI355X.
+
+One step = one pass of the path over one batch resident in HBM:
+  lift every record of this GPU's key-range shard (BLAKE3 over the synthesised canonical
+  encoding, fused with the 256-row block sums) -> super-block sums -> the R = 16 range
+  aggregates of rbsr's default fan-out (rbsr/src/protocol.rs:40) -> (N > 1) all_gather of the
+  per-shard (R x 40 B) aggregates over RCCL + carry-add combine.
+
+Workload (BASELINE.json configs[1]): 10 M records per GPU, 16 B key / 64 B value, dated
+(FingerprintTreeMap<[u8;16], Entry<Timestamp, Vec<u8>>>, 120 canonical bytes per record).
+Weak scaling: every GPU holds its own 10 M-record shard of one globally key-sorted set.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config2|config3|bench_u32]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "reconcile-rs_amd"))
+
+import torch  # noqa: E402
+
+CONFIGS = {
+    # name: (key, value, record kind, records per GPU, canonical bytes hashed, HBM bytes / record, description)
+    "config2": ("bytes16", "bytes64", "dated", 10_000_000,
+                "BASELINE configs[1]: 10M records/GPU, 16 B key / 64 B value, dated Entry<Timestamp,Vec<u8>>"),
+    "config3": ("bytes16", "bytes1024", "dated", 10_000_000,
+                "BASELINE configs[2] shape: 16 B key / 1 KiB value, dated (10M/GPU bench sample of the 100M set)"),
+    "config3_full": ("bytes16", "bytes1024", "dated", 100_000_000,
+                     "BASELINE configs[2]: 100M records, 16 B key / 1 KiB value, dated, 1 GPU"),
+    "config4": ("bytes16", "bytes64", "dated", 12_500_000,
+                "BASELINE configs[3] per-GPU shard: 100M records over 8 GPUs, 16 B key / 64 B value"),
+    "bench_u32": ("u32", "u32", "plain", 10_000_000,
+                  "benches/bench.rs fill shape: FingerprintTreeMap<u32,u32>"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    p.add_argument("--records", type=int, default=0, help="override records per GPU")
+    p.add_argument("--ranges", type=int, default=16)
+    p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
+    p.add_argument("--cpu-sample", type=int, default=2_000_000, help="records in the CPU baseline sample")
+    p.add_argument("--e2e", action="store_true", help="also time host->device->host end to end (DESIGN.md)")
+    p.add_argument("--check", type=int, default=1, help="oracle spot-check of a sample before timing")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import rsos_hip
+    from rsos_hip import RecordSchema, lift_records, range_aggregates, reduce_blocks, combine_aggregates
+    from rsos_hip.synth import make_records
+
+    kname, vname, kind, n_default, desc = CONFIGS[args.config]
+    n = args.records or n_default
+    schema = getattr(RecordSchema, kind)(kname, vname)
+    rec_bytes = schema.record_len()                     # canonical bytes BLAKE3 absorbs
+    read_bytes = schema.key_row + schema.value_row + (20 if schema.dated_kind else 0)
+    hbm_bytes = read_bytes + 32                          # + fingerprint write
+
+    # this rank's shard of the globally sorted key space: global rows [rank*n, (rank+1)*n)
+    cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n)
+    base = rank * n
+    total = n * world
+    R = args.ranges
+    glo = [total * j // R for j in range(R)]
+    ghi = [total * (j + 1) // R for j in range(R)]
+    lo = torch.tensor([min(max(g - base, 0), n) for g in glo], dtype=torch.int64, device=dev)
+    hi = torch.tensor([min(max(g - base, 0), n) for g in ghi], dtype=torch.int64, device=dev)
+
+    nb = (n + 255) // 256
+    fps = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    bs = torch.empty((nb, 32), dtype=torch.uint8, device=dev)
+    out = torch.empty((R, 5), dtype=torch.int64, device=dev)
+    gathered = torch.empty((world, R, 5), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    # correctness gate before timing: sampled rows vs the oracle (rank 0)
+    checked = None
+    if args.check and rank == 0:
+        checked = spot_check(schema, cols, n)
+
+    lift_ms = []
+
+    def step(timed: bool):
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        lift_records(schema, cols, fps=fps, bsums=bs)
+        if timed:
+            e1.record(stream)
+            lift_ms.append((e0, e1))
+        ss = reduce_blocks(bs)
+        range_aggregates(fps, bs, ss, lo, hi, out=out)
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, out)
+            return combine_aggregates(gathered)
+        return out
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step(True)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lift_avg_s = sum(a.elapsed_time(b) for a, b in lift_ms) / len(lift_ms) / 1e3
+
+    root = res.cpu().numpy()  # the step's result: R combined range aggregates over all shards
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    recs = total * args.steps
+    gib_s = recs * rec_bytes / elapsed / 2**30
+    achieved = hbm_bytes * n / lift_avg_s / 1e9
+    traffic = load_traffic(args.config, n)
+    line = {
+        "metric": "fingerprint-hash GiB/s + M records/s (device-resident) at 1/2/4/8 MI355X",
+        "value": round(gib_s, 2),
+        "unit": "GiB/s",
+        "mrec_per_s": round(recs / elapsed / 1e6, 1),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded, SURVEY §8d generator), resident in HBM before timing",
+        "config": {"workload": desc, "records_per_gpu": n, "records_total": total, "ranges": R,
+                   "canonical_bytes_per_record": rec_bytes, "hbm_bytes_per_record": hbm_bytes,
+                   "parallelism": f"key-range shards x{world}" + (" + RCCL all_gather" if world > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "rh::k_lift (lift + block sums)", "kernel_avg_us": round(lift_avg_s * 1e6, 2)},
+        "oracle_spot_check": checked,
+        "total_aggregate_size": int(root[:, 4].sum()),
+    }
+    if args.cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample)
+    if args.e2e:
+        line["end_to_end"] = end_to_end(schema, cols, n)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def spot_check(schema, cols, n):
+    """Lift a few thousand rows and compare with the C oracle (test infrastructure)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import oracle as O
+        O.lib()
+    except Exception as e:  # the checker is optional; the product path never needs it
+        return f"skipped: {e}"
+    from rsos_hip import lift_records
+    from rsos_hip.synth import to_host
+    m = min(n, 4096)
+    sub = {k: v[:m] for k, v in cols.items()}
+    fps, _ = lift_records(schema, sub, block_sums=False)
+    torch.cuda.synchronize()
+    h = to_host(cols, 0, m)
+    sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+    want = O.Records(sc, h["keys"], h.get("values"), h.get("phys"), h.get("logical"), h.get("node"),
+                     h.get("tags")).lift(threads=8)
+    ok = bool(np.array_equal(fps.cpu().numpy(), want))
+    if not ok:
+        raise SystemExit("bench: GPU fingerprints differ from the oracle -- refusing to report a number")
+    return f"bit-exact on {m} rows"
+
+
+def cpu_baseline(schema, cols, sample):
+    """The reference's CPU path restated (oracle/oracle.c): FingerprintTreeMap fill -- one lift per
+    insert into an order-6 B-tree with per-node Aggregate caches, serial (one writer holds the map's
+    write lock, src/replica/write.rs:117-120), over a bounded sample of the same records."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from rsos_hip.synth import to_host
+    m = min(sample, next(iter(cols.values())).shape[0])
+    h = to_host(cols, 0, m)
+    sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+    recs = O.Records(sc, h["keys"], h.get("values"), h.get("phys"), h.get("logical"), h.get("node"), h.get("tags"))
+    rec_bytes = schema.record_len()
+    t = O.FingerprintTreeMap(recs)
+    t0 = time.perf_counter()
+    t.fill(0, m)
+    dt = time.perf_counter() - t0
+    fill = {"value": round(m * rec_bytes / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "mrec_per_s": round(m / dt / 1e6, 3),
+            "sample": f"FingerprintTreeMap fill (oracle/oracle.c restatement, serial inserts) of the first "
+                      f"{m} records of the benchmark shard, {dt:.2f} s"}
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    recs.lift(threads=threads)
+    dt2 = time.perf_counter() - t0
+    fill["batch_lift_all_cores"] = {"value": round(m * rec_bytes / dt2 / 2**30, 4), "unit": "GiB/s",
+                                    "cores": threads, "mrec_per_s": round(m / dt2 / 1e6, 3)}
+    return fill
+
+
+def end_to_end(schema, cols, n):
+    """Host records -> H2D -> lift -> D2H of the fingerprints (pinned host buffers)."""
+    from rsos_hip import lift_records
+    host = {k: v.cpu().pin_memory() for k, v in cols.items()}
+    fps_h = torch.empty((n, 32), dtype=torch.uint8).pin_memory()
+    best = None
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dcols = {k: v.to("cuda", non_blocking=True) for k, v in host.items()}
+        fps, _ = lift_records(schema, dcols, block_sums=False)
+        fps_h.copy_(fps, non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+        del dcols, fps
+    return {"records": n, "seconds": round(best, 5), "mrec_per_s": round(n / best / 1e6, 1),
+            "gib_s_hashed": round(n * schema.record_len() / best / 2**30, 2)}
+
+
+def load_traffic(config, n):
+    """HBM bytes per lift launch from the committed rocprofv3 PMC summary, if one exists for this
+    config and size (profiles/traffic_<config>.json; FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+        if int(t.get("records", -1)) == n:
+            return t.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,199 @@
+/*
+ * rsos_hip.h -- C ABI of librsos_hip.so, the MI355X (gfx950) fingerprint-hash path of
+ * reconcile-rs.
+ *
+ * What it replaces (citations relative to the reference checkout, Akvize/reconcile-rs 0.3.0):
+ *   - rsos::lift / rsos::digest                      rsos/src/fingerprint.rs:270-292
+ *     (BLAKE3 over the canonical encoding, rsos/src/encoding.rs:17-35)
+ *   - Fingerprint + / - (mod 2^256, LE u64 limbs)    rsos/src/fingerprint.rs:145-173
+ *   - Aggregate (fingerprint, size) monoid           rsos/src/aggregate.rs:38-89
+ *   - FingerprintTreeMap's cached subtree aggregates rsos/src/fingerprint_tree_map/node.rs:54-91
+ *     and its range query                            rsos/src/fingerprint_tree_map/query.rs:25-76
+ *   - the Rsos<K> trait surface (size / aggregate / rank / select / insert / delete)
+ *                                                    rsos/src/rsos_trait.rs:39-90
+ *     which rbsr consumes through RsosView<K>        rbsr/src/rsos_view.rs:55-91
+ *
+ * Conventions
+ *   - Every call returns rh_status (0 = ok, negative = error); rh_last_error() gives a
+ *     thread-local message.  No exceptions, no callbacks cross this boundary.
+ *   - A fingerprint is 32 bytes: the BLAKE3 digest read as four little-endian u64 limbs,
+ *     limb 0 least significant (rsos/src/fingerprint.rs:106-124).  On the wire and in these
+ *     buffers the 32 bytes are exactly the digest bytes.
+ *   - rh_aggregate mirrors rsos::Aggregate's field order (fingerprint, then size;
+ *     rsos/src/aggregate.rs:38-42).
+ *   - *_async calls take DEVICE pointers and enqueue on `stream` (a hipStream_t, or NULL for
+ *     the null stream); they never synchronise, allocate or copy to the host.
+ *   - rh_store_* calls take HOST pointers and are synchronous: the stream is drained before
+ *     return, so a caller holding the map's read lock never observes an in-flight batch
+ *     (the one-snapshot-per-round law, rbsr/src/rsos_view.rs:36).
+ */
+#ifndef RSOS_HIP_H
+#define RSOS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RH_ABI_VERSION 1
+
+typedef enum rh_status {
+    RH_OK = 0,
+    RH_ERR_ARG = -1,         /* bad argument (null pointer, misaligned buffer, bad range)     */
+    RH_ERR_HIP = -2,         /* a HIP runtime call failed (message in rh_last_error)           */
+    RH_ERR_OOM = -3,         /* device allocation failed                                       */
+    RH_ERR_UNSUPPORTED = -4, /* schema has no specialised kernel: encode on the host and use
+                                rh_lift_encoded_async (the generic canonical-bytes path)       */
+    RH_ERR_STATE = -5        /* call not valid in the store's current state                   */
+} rh_status;
+
+/* Key encodings (rsos/src/encoding/serializer.rs):
+ *   UNIT  : `()`            -> no bytes (digest = lift with a unit key, fingerprint.rs:288-292)
+ *   U32   : u32 / i32       -> 4 bytes LE              (:76-79)
+ *   U64   : u64 / i64/usize -> 8 bytes LE              (:81-84)
+ *   BYTES : [u8; L] / Vec<u8> / String of fixed byte length L
+ *                           -> u64 LE length L, then the L bytes (:105-113,162-179)        */
+typedef enum rh_key_kind { RH_KEY_UNIT = 0, RH_KEY_U32 = 1, RH_KEY_U64 = 2, RH_KEY_BYTES = 3 } rh_key_kind;
+typedef enum rh_value_kind { RH_VAL_UNIT = 0, RH_VAL_U32 = 1, RH_VAL_U64 = 2, RH_VAL_BYTES = 3 } rh_value_kind;
+
+/* What is hashed per record:
+ *   PLAIN      : lift(k, v)                                   FingerprintTreeMap<K, V>
+ *   DATED      : lift(k, Entry<Timestamp, V>{stamp, state})   Replica.map   (src/replica.rs:69)
+ *   PROJECTION : lift(k, State<V>)                            Replica.projection (:74)
+ * Entry/State/Timestamp: lww-register/src/entry.rs:24-29,88-94; clock.rs:143-181.        */
+typedef enum rh_record_kind { RH_REC_PLAIN = 0, RH_REC_DATED = 1, RH_REC_PROJECTION = 2 } rh_record_kind;
+
+typedef struct rh_schema {
+    int32_t  key_kind;    /* rh_key_kind                                  */
+    uint32_t key_len;     /* bytes per key in the key column (4, 8 or L)  */
+    int32_t  value_kind;  /* rh_value_kind                                */
+    uint32_t value_len;   /* bytes per value in the value column          */
+    int32_t  record_kind; /* rh_record_kind                               */
+    uint32_t reserved;    /* must be 0                                    */
+} rh_schema;
+
+/* Records in column (SoA) layout, row i = record i.  Columns a schema does not use may be NULL.
+ * Device columns must be 16-byte aligned (hipMalloc / torch allocations are).             */
+typedef struct rh_columns {
+    const void     *keys;    /* n * key_len bytes                                        */
+    const uint64_t *phys;    /* DATED: Timestamp.hlc.physical (PhysicalTime, ms)         */
+    const uint32_t *logical; /* DATED: Timestamp.hlc.logical  (LogicalCounter)           */
+    const uint64_t *node;    /* DATED: Timestamp.node_id      (NodeId)                   */
+    const uint8_t  *tags;    /* DATED/PROJECTION, nullable: 0 = State::Present, 1 = Tombstone */
+    const void     *values;  /* n * value_len bytes                                      */
+} rh_columns;
+
+typedef struct rh_aggregate {
+    uint64_t fingerprint[4]; /* Aggregate.fingerprint, LE limbs */
+    uint64_t size;           /* Aggregate.size                  */
+} rh_aggregate;
+
+/* ---- library ------------------------------------------------------------------------- */
+int         rh_abi_version(void);
+const char *rh_last_error(void);
+/* 1 if a specialised kernel exists for this schema, 0 if it needs the encoded path, <0 bad */
+int         rh_schema_supported(const rh_schema *schema);
+/* canonical-encoding length of a present / tombstone record of this schema (host helper)   */
+int64_t     rh_schema_record_len(const rh_schema *schema, int tombstone);
+
+/* ---- device-resident batch API (all pointers are device pointers) -------------------- */
+/* Records are grouped in blocks of RH_BLOCK = 256 consecutive rows, blocks in
+ * super-blocks of 256 blocks (65536 rows); these are the cached "subtree" aggregates. */
+#define RH_BLOCK 256
+#define RH_SUPER 65536
+size_t rh_num_blocks(size_t n);      /* ceil(n / 256)   */
+size_t rh_num_superblocks(size_t n); /* ceil(n / 65536) */
+
+/* lift every record: fps[i] = lift(key_i, record_i)  (32 B each, rsos/src/fingerprint.rs:270);
+ * block_sums (nullable) receives Σ fps over each 256-row block (32 B per block).
+ * Replaces the per-insert lift of FingerprintTreeMap::insert (mutate.rs:34,61) and
+ * Replica::map_insert's two lifts (src/replica/write.rs:44-45).                           */
+int rh_lift_records_async(const rh_schema *schema, const rh_columns *dev_cols, size_t n,
+                          uint8_t *dev_fps, uint8_t *dev_block_sums, void *stream);
+
+/* Both lifts of Replica::map_insert in one pass (src/replica/write.rs:44-45): the dated
+ * fingerprint lift(k, Entry<Timestamp,V>) and the projection lift(k, State<V>).
+ * schema->record_kind must be RH_REC_DATED.  Either block-sum pointer may be NULL.        */
+int rh_lift_dual_async(const rh_schema *schema, const rh_columns *dev_cols, size_t n,
+                       uint8_t *dev_fps_dated, uint8_t *dev_block_sums_dated,
+                       uint8_t *dev_fps_proj, uint8_t *dev_block_sums_proj, void *stream);
+
+/* Generic path: BLAKE3 of pre-encoded canonical bytes (rsos::encoding::encode_to_vec of
+ * k then v, public-api/rsos.txt:61), record i = bytes[offsets[i] .. offsets[i+1]).
+ * `bytes` must be readable up to offsets[n] rounded up to a multiple of 4.               */
+int rh_lift_encoded_async(const uint8_t *dev_bytes, const uint64_t *dev_offsets, size_t n,
+                          uint8_t *dev_fps, uint8_t *dev_block_sums, void *stream);
+
+/* out[g] = Σ in[256 g .. 256 g + 255]  (32-byte fingerprints, mod 2^256) */
+int rh_reduce_blocks_async(const uint8_t *dev_in, size_t n_in, uint8_t *dev_out, void *stream);
+
+/* Range aggregates over rank ranges [lo[j], hi[j]) of a lifted, rank-ordered array:
+ * out[j] = (Σ fps[lo..hi), hi - lo).  Uses the block and super-block sums, so the cost per
+ * range is O(n / 65536 + 512) reads -- the cached-subtree walk of query.rs:25-76.
+ * An inverted or empty range yields the zero aggregate (rbsr/src/protocol.rs:230-232).   */
+int rh_range_aggregates_async(const uint8_t *dev_fps, const uint8_t *dev_block_sums,
+                              const uint8_t *dev_super_sums, size_t n, const uint64_t *dev_lo,
+                              const uint64_t *dev_hi, size_t r, rh_aggregate *dev_out, void *stream);
+
+/* out[j] = Σ_p in[p * r + j]  (the combine step after a cross-GPU gather of per-shard
+ * aggregates; Aggregate's Add, rsos/src/aggregate.rs:79-89)                               */
+int rh_combine_aggregates_async(const rh_aggregate *dev_in, size_t parts, size_t r,
+                                rh_aggregate *dev_out, void *stream);
+
+/* ---- host helpers --------------------------------------------------------------------- */
+/* End-to-end lift of host records: H2D copy, lift on `device`, D2H of the fingerprints.
+ * The PCIe-inclusive path a host caller (the Rust shim) uses for a one-shot batch.        */
+int rh_lift_host(int device, const rh_schema *schema, const rh_columns *host_cols, size_t n,
+                 uint8_t *host_fps);
+
+/* Fingerprint group on the host (rsos/src/fingerprint.rs:145-173), for callers' combines */
+void rh_fp_add(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
+void rh_fp_sub(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
+
+/* ---- GPU-resident RSOS store ---------------------------------------------------------
+ * A rank-ordered set of records resident in HBM with per-record fingerprints and block /
+ * super-block sums; the host keeps the key column for rank / select (rbsr's `select`
+ * returns &K, so keys must stay host-addressable).
+ * Realises Rsos<K> (rsos/src/rsos_trait.rs:39-90) for fixed-width keys:
+ *   size -> rh_store_len, aggregate -> rh_store_aggregate[_keys], rank -> rh_store_rank,
+ *   select -> rh_store_select, insert/delete -> rh_store_apply.                          */
+typedef struct rh_store rh_store;
+
+int rh_store_create(int device, const rh_schema *schema, rh_store **out);
+int rh_store_destroy(rh_store *store);
+/* Replace the contents with n records (host columns), which must be sorted by key in the
+ * key type's Ord and free of duplicates.  Bulk fill: the GPU form of FromIterator /
+ * ReplicatedMap::load_bulk (rsos/src/fingerprint_tree_map_iter/into_iter.rs:22-33,
+ * src/replicated_map/write.rs:184).                                                      */
+int rh_store_load(rh_store *store, const rh_columns *host_cols, size_t n);
+int rh_store_len(const rh_store *store, uint64_t *out);
+/* Aggregate over rank range [lo, hi) */
+int rh_store_aggregate(rh_store *store, uint64_t lo, uint64_t hi, rh_aggregate *out);
+/* r rank ranges in one launch (the ≤ 16 child ranges of one rbsr SPLIT, protocol.rs:299-307) */
+int rh_store_aggregates(rh_store *store, const uint64_t *lo, const uint64_t *hi, size_t r,
+                        rh_aggregate *out);
+/* Aggregate over the key range given by two bounds.  kind: 0 = unbounded, 1 = included,
+ * 2 = excluded (std::ops::Bound).  Inverted ranges give ZERO.                            */
+int rh_store_aggregate_keys(rh_store *store, int lo_kind, const void *lo_key, int hi_kind,
+                            const void *hi_key, rh_aggregate *out);
+/* Rank(z) = number of keys strictly below z (query.rs:93-121) */
+int rh_store_rank(const rh_store *store, const void *key, uint64_t *out);
+/* Select(r): copies the r-th key into key_out (key_len bytes); RH_ERR_ARG if r >= size  */
+int rh_store_select(const rh_store *store, uint64_t r, void *key_out);
+/* Copy fingerprints of ranks [lo, hi) to the host (32 B each) */
+int rh_store_fingerprints(rh_store *store, uint64_t lo, uint64_t hi, uint8_t *host_out);
+
+/* Batched insert / overwrite / delete (FingerprintTreeMap::insert / remove, mutate.rs:23-154).
+ * ops[i]: 0 = insert-or-overwrite record i of `host_cols`, 1 = delete key i (value columns
+ * ignored).  Keys within one batch must be distinct.  On return every aggregate reflects
+ * the whole batch (no half-applied state is observable).  n_new / n_overwritten / n_deleted
+ * (nullable) report what happened.                                                       */
+int rh_store_apply(rh_store *store, const rh_columns *host_cols, const uint8_t *ops, size_t n,
+                   uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSOS_HIP_H */

@@ -1,0 +1,222 @@
+// aggregate_kernels.hip -- the generic (pre-encoded bytes) lift, the 256-bit block reducer,
+// the rank-range aggregate query and the cross-shard combine.
+//
+//   k_lift_encoded      rsos::lift over bytes from rsos::encoding::encode_to_vec (any schema),
+//                       rsos/src/fingerprint.rs:270-275, rsos/src/encoding.rs:117-128
+//   k_reduce            per-256 sums: the cached subtree Aggregate of node.rs:54-91
+//   k_range_query       FingerprintTreeMap::aggregate, query.rs:25-76, over rank ranges
+//   k_combine           Aggregate's Add (rsos/src/aggregate.rs:79-89) over gathered shards
+#include "internal.hpp"
+#include "lift_kernels.hpp"
+
+namespace rh {
+
+// ---- generic encoded-bytes lift -------------------------------------------------------------
+
+// 16 message words of the block starting at byte `addr`, `blen` (0..64) valid bytes; bytes
+// past blen are zero.  Dwords at or beyond `limit` (buffer size rounded up to 4) are not read.
+__device__ __forceinline__ void load_block_bytes(const uint8_t *base, uint64_t addr, uint32_t blen,
+                                                 uint64_t limit, uint32_t m[16]) {
+    const uint64_t a4 = addr & ~3ull;
+    const uint32_t sh = (uint32_t)(addr & 3) * 8u;
+    uint32_t d[17];
+#pragma unroll
+    for (int k = 0; k < 17; k++) {
+        const uint64_t at = a4 + 4ull * k;
+        d[k] = (at < limit && (uint32_t)(4 * k) < blen + 4) ? *reinterpret_cast<const uint32_t *>(base + at) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint32_t w = __builtin_amdgcn_alignbit(d[j + 1], d[j], sh);
+        const int valid = (int)blen - 4 * j;
+        const uint32_t mask = valid >= 4 ? 0xFFFFFFFFu : valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u);
+        m[j] = w & mask;
+    }
+}
+
+constexpr int ENC_STACK = 40;
+
+__global__ __launch_bounds__(256) void k_lift_encoded(const uint8_t *bytes, const uint64_t *offs,
+                                                      uint64_t n, uint64_t limit, uint8_t *fps,
+                                                      uint8_t *bsums) {
+    __shared__ SumTile tile;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n) {
+        const uint64_t start = offs[i];
+        const uint64_t len = offs[i + 1] - start;
+        const uint64_t nchunks = len == 0 ? 1 : (len + CHUNK_LEN - 1) / CHUNK_LEN;
+        uint32_t stk[ENC_STACK][8];
+        int sp = 0;
+        uint32_t cv[8];
+        for (uint64_t c = 0; c < nchunks; c++) {
+            const uint64_t cbeg = c * CHUNK_LEN;
+            const uint64_t clen = len - cbeg < (uint64_t)CHUNK_LEN ? len - cbeg : (uint64_t)CHUNK_LEN;
+            const uint32_t nb = clen == 0 ? 1u : (uint32_t)((clen + 63) / 64);
+            cv_iv(cv);
+            for (uint32_t b = 0; b < nb; b++) {
+                const uint64_t boff = cbeg + 64ull * b;
+                const uint32_t blen = (uint32_t)(len - boff < 64 ? len - boff : 64);
+                uint32_t m[16];
+                load_block_bytes(bytes, start + boff, blen, limit, m);
+                uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b == nb - 1 ? CHUNK_END : 0u);
+                if (nchunks == 1 && b == nb - 1) flags |= ROOT;
+                compress(cv, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
+            }
+            if (c + 1 < nchunks) {
+                uint64_t total = c + 1;
+                while ((total & 1) == 0) {
+                    sp--;
+                    uint32_t p[8];
+                    parent(p, stk[sp], cv, 0u);
+                    for (int q = 0; q < 8; q++) cv[q] = p[q];
+                    total >>= 1;
+                }
+                for (int q = 0; q < 8; q++) stk[sp][q] = cv[q];
+                sp++;
+            }
+        }
+        for (int s = sp - 1; s >= 0; s--) {
+            uint32_t p[8];
+            parent(p, stk[s], cv, s == 0 ? ROOT : 0u);
+            for (int q = 0; q < 8; q++) cv[q] = p[q];
+        }
+        for (int q = 0; q < 8; q++) h[q] = cv[q];
+        store_fp(fps, i, h);
+    }
+    if (bsums) {
+        uint32_t f[8];
+        block_sum_fps256(h, tile, f);
+        if (threadIdx.x == 0) store_sum(bsums, blockIdx.x, f);
+    }
+}
+
+// ---- reductions ------------------------------------------------------------------------------
+
+__device__ __forceinline__ void load_fp(const uint8_t *src, uint64_t i, uint32_t f[8]) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(src + 32 * i);
+    uint4 a = p[0], b = p[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+__global__ __launch_bounds__(256) void k_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out) {
+    __shared__ SumTile tile;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n_in) load_fp(in, i, h);
+    uint32_t f[8];
+    block_sum_fps256(h, tile, f);
+    if (threadIdx.x == 0) store_sum(out, blockIdx.x, f);
+}
+
+__device__ __forceinline__ void acc_span(Acc &a, const uint8_t *src, uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        uint32_t f[8];
+        load_fp(src, i, f);
+        acc_add_fp(a, f);
+    }
+}
+
+// One workgroup per query.  [lo, hi) = head rows + whole blocks + tail rows, the whole blocks
+// = head blocks + whole super-blocks + tail blocks.  Each thread sums at most a few hundred
+// entries into carry-save u64 limbs, then one block reduction.
+__global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, const uint8_t *bsums,
+                                                     const uint8_t *ssums, uint64_t n,
+                                                     const uint64_t *qlo, const uint64_t *qhi,
+                                                     uint64_t r, uint64_t *out) {
+    __shared__ uint64_t lds[4 * 8];
+    const uint64_t j = blockIdx.x;
+    if (j >= r) return;  // uniform per block
+    uint64_t lo = qlo[j], hi = qhi[j];
+    if (hi > n) hi = n;
+    if (lo > hi) lo = hi;
+    Acc a;
+    acc_zero(a);
+    const uint64_t B = 256, S = 65536;
+    const uint64_t b1 = (lo + B - 1) / B, b2 = hi / B;  // whole blocks [b1, b2)
+    if (b1 >= b2 || bsums == nullptr) {
+        acc_span(a, fps, lo, hi);
+    } else {
+        acc_span(a, fps, lo, b1 * B);
+        acc_span(a, fps, b2 * B, hi);
+        const uint64_t s1 = (b1 + B - 1) / B, s2 = b2 / B;  // whole super-blocks [s1, s2)
+        if (s1 >= s2 || ssums == nullptr) {
+            acc_span(a, bsums, b1, b2);
+        } else {
+            acc_span(a, bsums, b1, s1 * B);
+            acc_span(a, bsums, s2 * B, b2);
+            acc_span(a, ssums, s1, s2);
+        }
+    }
+    (void)S;
+    uint32_t f[8];
+    acc_block_reduce<256>(a, lds, f);
+    if (threadIdx.x == 0) {
+        uint64_t *o = out + 5 * j;
+        o[0] = (uint64_t)f[0] | ((uint64_t)f[1] << 32);
+        o[1] = (uint64_t)f[2] | ((uint64_t)f[3] << 32);
+        o[2] = (uint64_t)f[4] | ((uint64_t)f[5] << 32);
+        o[3] = (uint64_t)f[6] | ((uint64_t)f[7] << 32);
+        o[4] = hi - lo;
+    }
+}
+
+// out[j] = Σ_p in[p*r + j] over rh_aggregate {u64 fp[4]; u64 size}
+__global__ void k_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64_t *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= r) return;
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, sz = 0;
+    for (uint64_t p = 0; p < parts; p++) {
+        const uint64_t *a = in + 5 * (p * r + j);
+        uint64_t t0 = s0 + a[0];
+        uint64_t c = t0 < s0;
+        uint64_t t1 = s1 + a[1];
+        uint64_t c1 = t1 < s1;
+        t1 += c;
+        c1 |= (t1 < c);
+        uint64_t t2 = s2 + a[2];
+        uint64_t c2 = t2 < s2;
+        t2 += c1;
+        c2 |= (t2 < c1);
+        uint64_t t3 = s3 + a[3] + c2;
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        sz += a[4];
+    }
+    uint64_t *o = out + 5 * j;
+    o[0] = s0; o[1] = s1; o[2] = s2; o[3] = s3; o[4] = sz;
+}
+
+// ---- launchers --------------------------------------------------------------------------------
+
+hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint64_t n, uint64_t limit,
+                               uint8_t *fps, uint8_t *bsums, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(k_lift_encoded, dim3((uint32_t)g), dim3(256), 0, st, bytes, offs, n, limit, fps, bsums);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st) {
+    if (n_in == 0) return hipSuccess;
+    const uint64_t g = (n_in + 255) / 256;
+    hipLaunchKernelGGL(k_reduce, dim3((uint32_t)g), dim3(256), 0, st, in, n_in, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
+                              const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
+                              hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_range_query, dim3((uint32_t)r), dim3(256), 0, st, fps, bsums, ssums, n, lo, hi, r, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64_t *out, hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    const uint64_t g = (r + 255) / 256;
+    hipLaunchKernelGGL(k_combine, dim3((uint32_t)g), dim3(256), 0, st, in, parts, r, out);
+    return hipGetLastError();
+}
+
+}  // namespace rh

@@ -1,0 +1,25 @@
+// internal.hpp -- declarations shared by the kernel translation units and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rh {
+
+struct DevCols;
+
+// Schema-specialised lift; returns hipErrorInvalidValue-free status, or sets *supported = false
+// when no instantiation matches (the caller then reports RH_ERR_UNSUPPORTED).
+hipError_t launch_lift_schema(int kk, int kl, int vk, int vl, int rk, bool tags, bool dual,
+                              const DevCols &c, uint64_t n, uint8_t *fps, uint8_t *bsums,
+                              uint8_t *fps2, uint8_t *bsums2, hipStream_t st, bool *supported);
+bool schema_instantiated(int kk, int kl, int vk, int vl);
+
+hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint64_t n, uint64_t limit,
+                               uint8_t *fps, uint8_t *bsums, hipStream_t st);
+hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st);
+hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
+                              const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
+                              hipStream_t st);
+hipError_t launch_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64_t *out, hipStream_t st);
+
+}  // namespace rh

@@ -1,0 +1,199 @@
+"""GpuFingerprintStore -- an rsos::Rsos<K> realisation resident on one MI355X.
+
+Mirrors rsos/src/rsos_trait.rs:39-90 (method names, argument meaning, panics-as-errors):
+
+  size()                 -> |X|
+  aggregate(range)       -> Aggregate over X ∩ range   (summary-folds-lift: computed with lift)
+  rank(z)                -> number of keys strictly below z
+  select(r)              -> r-th key; IndexError if r >= size()  (the reference panics)
+  enumerate(range)       -> (key, record index) pairs in key order
+  insert(k, v) / delete(k)
+
+Records are held in rank order in HBM with their fingerprints and block / super-block sums;
+the key column stays on the host for rank/select.  Keys are fixed-width: bytes of
+schema.key_len for byte keys (memcmp order = Ord of [u8; L]), ints for u32/u64 keys.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Iterator, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import _abi as A
+from .fingerprint import Aggregate, Fingerprint
+from .schema import RecordSchema
+
+Key = Union[bytes, int]
+HOST_COLS = ("keys", "phys", "logical", "node", "tags", "values")
+
+
+def _np_ptr(a: Optional[np.ndarray]) -> Optional[int]:
+    return None if a is None else a.ctypes.data
+
+
+class KeyRange:
+    """std::ops range with Bound semantics: kinds 'unbounded' | 'included' | 'excluded'."""
+
+    _K = {"unbounded": 0, "included": 1, "excluded": 2}
+
+    def __init__(self, start: Optional[Key] = None, end: Optional[Key] = None,
+                 start_kind: str = "included", end_kind: str = "excluded"):
+        self.start, self.end = start, end
+        self.start_kind = "unbounded" if start is None else start_kind
+        self.end_kind = "unbounded" if end is None else end_kind
+
+    @staticmethod
+    def full() -> "KeyRange":  # `..`
+        return KeyRange()
+
+
+class GpuFingerprintStore:
+    def __init__(self, schema: RecordSchema, device: int = 0):
+        self.schema = schema
+        self._s = schema.c()
+        h = C.c_void_p()
+        A.check(A.lib().rh_store_create(device, C.byref(self._s), C.byref(h)), "rh_store_create")
+        self._h = h
+        self._hold: Dict[str, np.ndarray] = {}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            A.lib().rh_store_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- key encoding --------------------------------------------------------------------
+    def _key_bytes(self, k: Key) -> bytes:
+        s = self.schema
+        if s.key_kind == A.KEY_U32:
+            return int(k).to_bytes(4, "little")
+        if s.key_kind == A.KEY_U64:
+            return int(k).to_bytes(8, "little")
+        b = bytes(k)
+        if len(b) != s.key_row:
+            raise ValueError(f"key must be {s.key_row} bytes")
+        return b
+
+    def _key_out(self, b: bytes) -> Key:
+        if self.schema.key_kind in (A.KEY_U32, A.KEY_U64):
+            return int.from_bytes(b, "little")
+        return b
+
+    @staticmethod
+    def _columns(cols: Dict[str, np.ndarray]) -> Tuple[A.Columns, Dict[str, np.ndarray]]:
+        held = {k: np.ascontiguousarray(v) for k, v in cols.items() if v is not None}
+        for k in held:
+            if k not in HOST_COLS:
+                raise ValueError(f"unknown column {k!r}")
+        return A.Columns(*[_np_ptr(held.get(k)) for k in HOST_COLS]), held
+
+    # ---- fill ----------------------------------------------------------------------------
+    def load_bulk(self, cols: Dict[str, np.ndarray]) -> None:
+        """Replace the contents with records sorted by key, without duplicates."""
+        c, held = self._columns(cols)
+        n = len(held["keys"]) if "keys" in held else len(held["values"])
+        A.check(A.lib().rh_store_load(self._h, C.byref(c), n), "rh_store_load")
+
+    # ---- Rsos<K> -------------------------------------------------------------------------
+    def size(self) -> int:
+        out = C.c_uint64()
+        A.check(A.lib().rh_store_len(self._h, C.byref(out)), "rh_store_len")
+        return int(out.value)
+
+    __len__ = size
+
+    def aggregate(self, rng: Optional[KeyRange] = None) -> Aggregate:
+        rng = rng or KeyRange.full()
+        lo = None if rng.start is None else C.create_string_buffer(self._key_bytes(rng.start))
+        hi = None if rng.end is None else C.create_string_buffer(self._key_bytes(rng.end))
+        out = A.Aggregate()
+        A.check(A.lib().rh_store_aggregate_keys(self._h, KeyRange._K[rng.start_kind], lo,
+                                                KeyRange._K[rng.end_kind], hi, C.byref(out)),
+                "rh_store_aggregate_keys")
+        return Aggregate.from_c(out)
+
+    def aggregate_ranks(self, lo: int, hi: int) -> Aggregate:
+        out = A.Aggregate()
+        A.check(A.lib().rh_store_aggregate(self._h, lo, hi, C.byref(out)), "rh_store_aggregate")
+        return Aggregate.from_c(out)
+
+    def aggregates_ranks(self, lo: Sequence[int], hi: Sequence[int]):
+        lo_a = np.ascontiguousarray(lo, dtype=np.uint64)
+        hi_a = np.ascontiguousarray(hi, dtype=np.uint64)
+        r = len(lo_a)
+        out = (A.Aggregate * max(r, 1))()
+        A.check(A.lib().rh_store_aggregates(self._h, _np_ptr(lo_a), _np_ptr(hi_a), r, out),
+                "rh_store_aggregates")
+        return [Aggregate.from_c(out[j]) for j in range(r)]
+
+    def rank(self, z: Key) -> int:
+        out = C.c_uint64()
+        A.check(A.lib().rh_store_rank(self._h, C.create_string_buffer(self._key_bytes(z)), C.byref(out)),
+                "rh_store_rank")
+        return int(out.value)
+
+    def select(self, r: int) -> Key:
+        if r < 0 or r >= self.size():
+            raise IndexError("select: r >= size()")
+        buf = C.create_string_buffer(max(self.schema.key_row, 1))
+        A.check(A.lib().rh_store_select(self._h, r, buf), "rh_store_select")
+        return self._key_out(buf.raw[: self.schema.key_row])
+
+    def enumerate(self, rng: Optional[KeyRange] = None) -> Iterator[Tuple[Key, int]]:
+        """Keys in X ∩ range with their ranks, in key order."""
+        rng = rng or KeyRange.full()
+        n = self.size()
+        lo = 0 if rng.start is None else self.rank(rng.start)
+        if rng.start is not None and rng.start_kind == "excluded" and lo < n and self.select(lo) == rng.start:
+            lo += 1
+        hi = n if rng.end is None else self.rank(rng.end)
+        if rng.end is not None and rng.end_kind == "included" and hi < n and self.select(hi) == rng.end:
+            hi += 1
+        for r in range(lo, hi):
+            yield self.select(r), r
+
+    def fingerprints(self, lo: int = 0, hi: Optional[int] = None) -> np.ndarray:
+        hi = self.size() if hi is None else hi
+        out = np.zeros((max(hi - lo, 0), 32), np.uint8)
+        A.check(A.lib().rh_store_fingerprints(self._h, lo, hi, _np_ptr(out) if hi > lo else None),
+                "rh_store_fingerprints")
+        return out
+
+    def apply(self, cols: Dict[str, np.ndarray], ops: np.ndarray) -> Tuple[int, int, int]:
+        """Batched insert (op 0) / delete (op 1); returns (new, overwritten, deleted)."""
+        c, held = self._columns(cols)
+        ops_a = np.ascontiguousarray(ops, dtype=np.uint8)
+        a, b, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        A.check(A.lib().rh_store_apply(self._h, C.byref(c), _np_ptr(ops_a), len(ops_a), C.byref(a), C.byref(b),
+                                       C.byref(d)), "rh_store_apply")
+        return int(a.value), int(b.value), int(d.value)
+
+    def insert(self, key: Key, value: bytes = b"", phys: int = 0, logical: int = 0, node: int = 0,
+               tombstone: bool = False) -> bool:
+        """Insert-or-overwrite one record; True if the key was new (Rsos::insert returns the old V)."""
+        s = self.schema
+        cols = {"keys": np.frombuffer(self._key_bytes(key), np.uint8).copy()}
+        if s.value_row:
+            v = value if isinstance(value, (bytes, bytearray)) else int(value).to_bytes(s.value_row, "little")
+            if len(v) != s.value_row:
+                raise ValueError(f"value must be {s.value_row} bytes")
+            cols["values"] = np.frombuffer(bytes(v), np.uint8).copy()
+        if s.dated_kind:
+            cols["phys"] = np.array([phys], np.uint64)
+            cols["logical"] = np.array([logical], np.uint32)
+            cols["node"] = np.array([node], np.uint64)
+        if s.record_kind != A.REC_PLAIN:
+            cols["tags"] = np.array([1 if tombstone else 0], np.uint8)
+        new, _, _ = self.apply(cols, np.zeros(1, np.uint8))
+        return new == 1
+
+    def delete(self, key: Key) -> bool:
+        cols = {"keys": np.frombuffer(self._key_bytes(key), np.uint8).copy()}
+        _, _, d = self.apply(cols, np.ones(1, np.uint8))
+        return d == 1

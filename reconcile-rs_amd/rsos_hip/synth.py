@@ -1,0 +1,74 @@
+"""Seeded synthetic records of the BASELINE shapes, generated directly in HBM.
+
+Follows SURVEY.md §8(d): keys are unique and sorted by memcmp (the Ord of [u8; L]); stamps
+follow benches/bench.rs:286-293's pattern (physical = 1_700_000_000_000 + i, logical 0,
+node_id 1); values are random bytes; optional tombstones at a given fraction.  Keys: the
+first 8 bytes are the big-endian u64 (i << 24 | r24) -- strictly increasing, hence unique
+and memcmp-sorted -- and the remaining key bytes are random.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+
+from .schema import RecordSchema
+from . import _abi as A
+
+
+def _rand_bytes(gen: torch.Generator, shape, device) -> torch.Tensor:
+    # int64 random words viewed as bytes (fast on device)
+    n = 1
+    for s in shape:
+        n *= s
+    words = (n + 7) // 8
+    w = torch.randint(-2**63, 2**63 - 1, (words,), generator=gen, device=device, dtype=torch.int64)
+    return w.view(torch.uint8)[:n].view(*shape)
+
+
+def make_records(schema: RecordSchema, n: int, seed: int = 42, device="cuda",
+                 tombstone_fraction: float = 0.0, first_index: int = 0) -> Dict[str, torch.Tensor]:
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    cols: Dict[str, torch.Tensor] = {}
+    idx = torch.arange(first_index, first_index + n, device=dev, dtype=torch.int64)
+    if schema.key_kind == A.KEY_BYTES:
+        kl = schema.key_len
+        keys = _rand_bytes(gen, (n, kl), dev).clone()
+        r24 = torch.randint(0, 1 << 24, (n,), generator=gen, device=dev, dtype=torch.int64)
+        head = (idx << 24) | r24
+        # big-endian bytes of head into keys[:, :8]
+        shifts = torch.arange(56, -8, -8, device=dev, dtype=torch.int64)
+        if kl >= 8:
+            keys[:, :8] = ((head[:, None] >> shifts[None, :]) & 0xFF).to(torch.uint8)
+        cols["keys"] = keys.contiguous()
+    elif schema.key_kind == A.KEY_U64:
+        r = torch.randint(0, 1 << 20, (n,), generator=gen, device=dev, dtype=torch.int64)
+        cols["keys"] = ((idx << 20) | r).contiguous().view(torch.uint8).view(n, 8)
+    elif schema.key_kind == A.KEY_U32:
+        cols["keys"] = idx.to(torch.int32).contiguous().view(torch.uint8).view(n, 4)
+    if schema.value_row:
+        cols["values"] = _rand_bytes(gen, (n, schema.value_row), dev).contiguous()
+    if schema.record_kind == A.REC_DATED:
+        cols["phys"] = (1_700_000_000_000 + idx).contiguous()
+        cols["logical"] = torch.zeros(n, dtype=torch.int32, device=dev)
+        cols["node"] = torch.ones(n, dtype=torch.int64, device=dev)
+    if schema.record_kind != A.REC_PLAIN and tombstone_fraction > 0:
+        u = torch.rand(n, generator=gen, device=dev)
+        cols["tags"] = (u < tombstone_fraction).to(torch.uint8)
+    return cols
+
+
+def to_host(cols: Dict[str, torch.Tensor], lo: int = 0, hi=None):
+    """numpy copies of rows [lo, hi) with the dtypes the oracle binding expects."""
+    import numpy as np
+    out = {}
+    for k, t in cols.items():
+        a = t[lo:hi].cpu().numpy()
+        if k in ("phys", "node"):
+            a = a.view(np.uint64)
+        elif k == "logical":
+            a = a.view(np.uint32)
+        out[k] = np.ascontiguousarray(a)
+    return out

@@ -1,0 +1,228 @@
+"""Generate tests/golden/vectors.json -- the committed parity fixtures.
+
+Sources, in order of authority:
+  1. the reference's own golden vectors (copied as DATA: inputs + expected limbs):
+       rsos/src/fingerprint/tests.rs:68-93            lift(&50u64,&"Hello"), the 3-element sum
+       tests/timestamp_wire_format.rs:41-49,105-121   lift(&7u32, &Entry::present(stamp, 12345u32))
+       rsos/src/fingerprint/tests.rs:45-64            carry / borrow known answers
+       rsos/src/encoding/tests.rs:19-247              byte-exact encodings (a representative subset)
+  2. BLAKE3 specification test vectors (input byte i = i % 251), the 32-byte prefix of the
+     published extended output; the reference's hash is crate blake3 1.8.5 (Cargo.lock:197-200)
+     and its own vectors stop at 64-byte inputs, so these pin multi-block / multi-chunk hashing.
+  3. per-shape record vectors for the GPU parity tests, computed by the pure-Python
+     restatement (oracle/pyref.py) and cross-checked here against the C oracle
+     (oracle/oracle.c) -- two independent restatements that must agree byte for byte.
+
+Run:  python tests/golden/make_golden.py   (rewrites vectors.json; deterministic)
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import pyref as P  # noqa: E402
+import oracle as O  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "vectors.json")
+
+
+def limbs_hex(b: bytes):
+    return [f"0x{x:016x}" for x in struct.unpack("<4Q", b)]
+
+
+def reference_goldens():
+    g1 = P.lift(P.U64(50), P.Str(b"Hello"))
+    g2 = P.fp_add(P.lift(P.U64(25), P.Str(b"World!")), g1, P.lift(P.U64(75), P.Str(b"Everyone!")))
+    stamp = P.timestamp(0x0123456789ABCDEF, 0x11223344, 0xFEEDFACEDEADBEEF)
+    g3_bytes = P.encode(P.U32(7)) + P.encode(P.entry(stamp, P.present(P.U32(12345))))
+    g3 = P.blake3(g3_bytes)
+    expect = {
+        "lift_50u64_Hello": ["0x5983c0894de2aacf", "0xa3b75857a517c2a4", "0xf30c219dd2d5d655", "0xc269e4a2cb9e3aa1"],
+        "combined_25_50_75": ["0x44d88232ba37b808", "0x39174386159c3900", "0xd744127365092edc", "0x0d4af5d85402598c"],
+        "entry_fingerprint_7u32": ["0xbaa4af17b48b79a7", "0x7ac363a554df3f18", "0x6d7e6ffeace1e413", "0xec7f5fadea960d52"],
+    }
+    got = {"lift_50u64_Hello": limbs_hex(g1), "combined_25_50_75": limbs_hex(g2),
+           "entry_fingerprint_7u32": limbs_hex(g3)}
+    assert got == expect, (got, expect)
+    return {
+        "source": "rsos/src/fingerprint/tests.rs:68-93; tests/timestamp_wire_format.rs:41-49,105-121",
+        "vectors": [
+            {"name": "lift_50u64_Hello", "encoded_hex": (P.encode(P.U64(50)) + P.encode(P.Str(b"Hello"))).hex(),
+             "limbs": expect["lift_50u64_Hello"]},
+            {"name": "combined_25_50_75",
+             "encoded_hex_parts": [(P.encode(P.U64(k)) + P.encode(P.Str(v))).hex()
+                                   for k, v in ((25, b"World!"), (50, b"Hello"), (75, b"Everyone!"))],
+             "limbs": expect["combined_25_50_75"]},
+            {"name": "entry_fingerprint_7u32", "encoded_hex": g3_bytes.hex(),
+             "record": {"key_u32": 7, "phys": "0x0123456789abcdef", "logical": "0x11223344",
+                        "node": "0xfeedfacedeadbeef", "value_u32": 12345, "state": "present"},
+             "limbs": expect["entry_fingerprint_7u32"]},
+        ],
+        "carry_borrow": [
+            {"op": "add", "a": ["0xffffffffffffffff"] * 4, "b": ["0x1", "0x0", "0x0", "0x0"], "out": ["0x0"] * 4},
+            {"op": "add", "a": ["0xffffffffffffffff", "0x0", "0x0", "0x0"], "b": ["0x1", "0x0", "0x0", "0x0"],
+             "out": ["0x0", "0x1", "0x0", "0x0"]},
+            {"op": "sub", "a": ["0x0"] * 4, "b": ["0x1", "0x0", "0x0", "0x0"], "out": ["0xffffffffffffffff"] * 4},
+        ],
+        "encodings": [
+            {"what": "1u32", "hex": "01000000"},
+            {"what": "1u64", "hex": "0100000000000000"},
+            {"what": "\"ab\"", "hex": "0200000000000000" + "6162"},
+            {"what": "None::<u8>", "hex": "00"},
+            {"what": "Some(0u8)", "hex": "0100"},
+            {"what": "E::A(1) (newtype variant 0)", "hex": "00000000" + "01000000"},
+            {"what": "U::B (unit variant 1)", "hex": "01000000"},
+            {"what": "Pair(1u32, 2u32) (tuple struct)", "hex": "0200000000000000" + "01000000" + "02000000"},
+        ],
+    }
+
+
+# Recalled from the BLAKE3 repository's test_vectors.json (input i % 251, first 32 output bytes).
+BLAKE3_SPEC = {
+    0: "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262",
+    1: "2d3adedff11b61f14c886e35afa036736dcd87a74d27b5c1510225d0f592e213",
+    1023: "10108970eeda3eb932baac1428c7a2163b0e924c9a9e25b35bba72b28f70bd11",
+    1024: "42214739f095a406f3fc83deb889744ac00df831c10daa55189b5d121c855af7",
+    1025: "d00278ae47eb27b34faecf67b4fe263f82d5412916c1ffd97c8cb7fb814b8444",
+    2048: "e776b6028c7cd22a4d0ba182a8bf62205d2ef576467e838ed6f2529b85fba24a",
+    2049: "5f4d72f40d7a5f82b15ca2b2e44b1de3c2ef86c426c95c1af0b6879522563030",
+    3072: "b98cb0ff3623be03326b373de6b9095218513e64f1ee2edd2525c7ad1e5cffd2",
+}
+
+
+def blake3_spec():
+    out = []
+    for n, h in BLAKE3_SPEC.items():
+        data = bytes(i % 251 for i in range(n))
+        assert P.blake3(data).hex() == h, n
+        assert O.blake3(data).hex() == h, n
+        out.append({"len": n, "hash": h})
+    assert P.blake3(b"abc").hex() == "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"
+    return {"source": "BLAKE3 test_vectors.json, input byte i = i % 251", "vectors": out,
+            "abc": "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"}
+
+
+SHAPES = [
+    # name, key kind/len, value kind/len, record kind, tombstone fraction, n
+    ("u32_u32_plain", "u32", "u32", O.REC_PLAIN, 0.0, 16),
+    ("u32_u32_dated", "u32", "u32", O.REC_DATED, 0.25, 16),
+    ("u64_u64_plain", "u64", "u64", O.REC_PLAIN, 0.0, 16),
+    ("u64_b64_plain", "u64", "bytes64", O.REC_PLAIN, 0.0, 16),
+    ("u64_b64_dated", "u64", "bytes64", O.REC_DATED, 0.0, 16),
+    ("b16_b64_dated", "bytes16", "bytes64", O.REC_DATED, 0.25, 24),
+    ("b16_b64_projection", "bytes16", "bytes64", O.REC_PROJECTION, 0.25, 16),
+    ("b16_b64_plain", "bytes16", "bytes64", O.REC_PLAIN, 0.0, 16),
+    ("b16_b1024_dated", "bytes16", "bytes1024", O.REC_DATED, 0.25, 8),
+    ("b16_b1024_projection", "bytes16", "bytes1024", O.REC_PROJECTION, 0.0, 8),
+    ("b16_u64_dated", "bytes16", "u64", O.REC_DATED, 0.0, 8),
+    ("b32_b64_dated", "bytes32", "bytes64", O.REC_DATED, 0.25, 8),
+]
+
+KIND = {"u32": (O.KEY_U32, 4), "u64": (O.KEY_U64, 8)}
+
+
+def _kind(name):
+    if name in KIND:
+        return KIND[name]
+    return O.KEY_BYTES, int(name[5:])
+
+
+def _pyvalue(kind, raw: bytes):
+    if kind == "u32":
+        return P.U32(int.from_bytes(raw, "little"))
+    if kind == "u64":
+        return P.U64(int.from_bytes(raw, "little"))
+    return P.Str(raw)  # Vec<u8>: u64 length then bytes
+
+
+def _pykey(kind, raw: bytes):
+    if kind in ("u32", "u64"):
+        return _pyvalue(kind, raw)
+    return P.Seq(tuple(P.U8(b) for b in raw))  # [u8; L] is a serde tuple: u64 count then bytes
+
+
+def shape_vectors():
+    rng = np.random.default_rng(20260817)
+    out = []
+    for name, kname, vname, rk, tomb, n in SHAPES:
+        kk, kl = _kind(kname)
+        vk, vl = _kind(vname)
+        schema = O.Schema(kk, kl, vk, vl, rk, 0)
+        keys = rng.integers(0, 256, (n, kl), dtype=np.uint8)
+        values = rng.integers(0, 256, (n, vl), dtype=np.uint8)
+        phys = rng.integers(0, 2**63, n, dtype=np.uint64)
+        logical = rng.integers(0, 2**32, n, dtype=np.uint32)
+        node = rng.integers(0, 2**63, n, dtype=np.uint64)
+        tags = (rng.random(n) < tomb).astype(np.uint8) if rk != O.REC_PLAIN else None
+        if tags is not None and n > 1:
+            tags[0], tags[1] = 0, 1 if tomb > 0 else 0
+        recs = O.Records(schema, keys, values, phys if rk == O.REC_DATED else None,
+                         logical if rk == O.REC_DATED else None, node if rk == O.REC_DATED else None, tags)
+        fps_c = recs.lift()
+        rows = []
+        for i in range(n):
+            k = _pykey(kname, keys[i].tobytes())
+            is_tomb = bool(tags[i]) if tags is not None else False
+            state = P.TOMBSTONE if is_tomb else P.present(_pyvalue(vname, values[i].tobytes()))
+            if rk == O.REC_PLAIN:
+                v = _pyvalue(vname, values[i].tobytes())
+            elif rk == O.REC_DATED:
+                v = P.entry(P.timestamp(int(phys[i]), int(logical[i]), int(node[i])), state)
+            else:
+                v = state
+            enc = P.encode(k) + P.encode(v)
+            assert recs.encode(i) == enc, (name, i)
+            fp = P.blake3(enc)
+            assert fp == fps_c[i].tobytes(), (name, i)
+            rows.append(fp.hex())
+        out.append({
+            "name": name, "key_kind": kk, "key_len": kl, "value_kind": vk, "value_len": vl,
+            "record_kind": rk, "n": n,
+            "keys": keys.tobytes().hex(), "values": values.tobytes().hex(),
+            "phys": [int(x) for x in phys] if rk == O.REC_DATED else None,
+            "logical": [int(x) for x in logical] if rk == O.REC_DATED else None,
+            "node": [int(x) for x in node] if rk == O.REC_DATED else None,
+            "tags": tags.tolist() if tags is not None else None,
+            "record_len": len(recs.encode(0)),
+            "fps": rows,
+            "sum": P.fp_add(*[bytes.fromhex(r) for r in rows]).hex(),
+        })
+    return out
+
+
+def encoded_vectors():
+    """Ragged pre-encoded records, including empty, 1-block, block- and chunk-boundary and
+    multi-chunk lengths (the generic path)."""
+    rng = np.random.default_rng(7)
+    lens = [0, 1, 3, 63, 64, 65, 120, 127, 128, 1023, 1024, 1025, 1080, 2048, 2049, 3073, 4097, 5000]
+    blobs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    fps_c = O.lift_encoded(blobs)
+    rows = []
+    for b, f in zip(blobs, fps_c):
+        h = P.blake3(b)
+        assert h == f.tobytes()
+        rows.append({"hex": b.hex(), "fp": h.hex()})
+    return rows
+
+
+def main():
+    doc = {
+        "_comment": "generated by tests/golden/make_golden.py -- data only (inputs and expected outputs)",
+        "reference": reference_goldens(),
+        "blake3_spec": blake3_spec(),
+        "shapes": shape_vectors(),
+        "encoded": encoded_vectors(),
+    }
+    with open(OUT, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(f"wrote {OUT}")
+
+
+if __name__ == "__main__":
+    main()

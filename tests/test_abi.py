@@ -1,0 +1,102 @@
+"""CPU tests of the drop-in boundary: librsos_hip.so loads, exports every entry point
+include/rsos_hip.h declares, and its host-only helpers behave (no GPU compute here)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rsos_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = set(re.findall(r"\b(rh_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
+
+
+def test_header_declares_the_boundary():
+    names = declared_symbols()
+    for must in ["rh_lift_records_async", "rh_lift_dual_async", "rh_lift_encoded_async",
+                 "rh_range_aggregates_async", "rh_combine_aggregates_async", "rh_store_create",
+                 "rh_store_aggregate", "rh_store_rank", "rh_store_select", "rh_store_apply", "rh_last_error"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(rsos_hip_lib):
+    from rsos_hip import _abi
+    L = _abi.lib()
+    missing = [n for n in declared_symbols() if not hasattr(L, n)]
+    assert not missing, missing
+    # and the python binding declares a signature for each of them
+    bound = {name for name, _, _ in _abi.SIGNATURES}
+    assert set(declared_symbols()) <= bound
+
+
+def test_abi_version_and_enums(rsos_hip_lib, oracle_lib):
+    from rsos_hip import _abi as A
+    assert A.lib().rh_abi_version() == 1
+    O = oracle_lib
+    assert (A.KEY_UNIT, A.KEY_U32, A.KEY_U64, A.KEY_BYTES) == (O.KEY_UNIT, O.KEY_U32, O.KEY_U64, O.KEY_BYTES)
+    assert (A.REC_PLAIN, A.REC_DATED, A.REC_PROJECTION) == (O.REC_PLAIN, O.REC_DATED, O.REC_PROJECTION)
+    text = open(HEADER).read()
+    assert "#define RH_BLOCK 256" in text and "#define RH_SUPER 65536" in text
+
+
+def test_schema_support_and_lengths(rsos_hip_lib):
+    from rsos_hip import RecordSchema
+    s = RecordSchema.dated("bytes16", "bytes64")
+    assert s.supported()
+    assert s.record_len() == 120 and s.record_len(tombstone=True) == 48
+    assert RecordSchema.projection("bytes16", "bytes64").record_len() == 100
+    assert RecordSchema.dated("bytes16", "bytes1024").record_len() == 1080
+    assert RecordSchema.plain("u32", "u32").record_len() == 8
+    assert not RecordSchema.plain("bytes12", "bytes100").supported()
+
+
+def test_bad_schema_is_an_error_not_a_crash(rsos_hip_lib):
+    from rsos_hip import _abi as A
+    bad = A.Schema(9, 4, 1, 4, 0, 0)
+    assert A.lib().rh_schema_supported(C.byref(bad)) == A.ERR_ARG
+    assert b"key_kind" in A.lib().rh_last_error()
+    with pytest.raises(A.RsosHipError):
+        A.check(A.lib().rh_schema_supported(C.byref(bad)), "x")
+
+
+def test_host_fingerprint_group(rsos_hip_lib, golden):
+    from rsos_hip import _abi as A
+    L = A.lib()
+    for kat in golden["reference"]["carry_borrow"]:
+        a = np.array([int(x, 16) for x in kat["a"]], np.uint64)
+        b = np.array([int(x, 16) for x in kat["b"]], np.uint64)
+        out = np.zeros(4, np.uint64)
+        fn = L.rh_fp_add if kat["op"] == "add" else L.rh_fp_sub
+        fn(a.ctypes.data, b.ctypes.data, out.ctypes.data)
+        assert [int(x) for x in out] == [int(x, 16) for x in kat["out"]]
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        a = rng.integers(0, 2**64, 4, dtype=np.uint64, endpoint=False)
+        b = rng.integers(0, 2**64, 4, dtype=np.uint64, endpoint=False)
+        s, d, back = np.zeros(4, np.uint64), np.zeros(4, np.uint64), np.zeros(4, np.uint64)
+        L.rh_fp_add(a.ctypes.data, b.ctypes.data, s.ctypes.data)
+        L.rh_fp_sub(s.ctypes.data, b.ctypes.data, back.ctypes.data)
+        assert (back == a).all()
+        ai = sum(int(x) << (64 * i) for i, x in enumerate(a))
+        bi = sum(int(x) << (64 * i) for i, x in enumerate(b))
+        assert sum(int(x) << (64 * i) for i, x in enumerate(s)) == (ai + bi) % (1 << 256)
+
+
+def test_python_value_types_mirror_reference(rsos_hip_lib):
+    from rsos_hip import Aggregate, Fingerprint
+    all_ones = Fingerprint((2**64 - 1,) * 4)
+    assert all_ones + Fingerprint((1, 0, 0, 0)) == Fingerprint.ZERO
+    assert Fingerprint.ZERO - Fingerprint((1, 0, 0, 0)) == all_ones
+    f = Fingerprint((1, 2, 3, 4))
+    assert -(-f) == f and f + (-f) == Fingerprint.ZERO
+    assert Fingerprint.from_le_bytes(f.to_le_bytes()) == f
+    assert str(f) == "0000000000000004000000000000000300000000000000020000000000000001"
+    z = Aggregate(2, f + (-f))
+    assert not z.is_empty() and Aggregate.ZERO.is_empty()

@@ -1,0 +1,364 @@
+"""GPU parity: the HIP path (librsos_hip.so, through its C ABI) against the oracle.
+
+Bit-exact for everything (integer / byte work).  Golden fixtures first, then seeded random
+batches against the C oracle, then size-independent properties at full size.
+Mirrors the reference's own strategy: golden vectors (rsos/src/fingerprint/tests.rs:68-93,
+tests/timestamp_wire_format.rs:105-121), fold-of-lift oracles
+(tests/proptest_fingerprint_tree_map/btreemap_oracle.rs:132-162,
+rsos/src/fingerprint_tree_map/tests/aggregate.rs:59-78), duplicate delivery (:195-231).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+M256 = 1 << 256
+
+
+def fp_int(b) -> int:
+    return int.from_bytes(bytes(b), "little")
+
+
+def limbs_int(l) -> int:
+    return sum(int(x) << (64 * i) for i, x in enumerate(l))
+
+
+def agg_int(row) -> int:
+    """row of an (r, 5) int64 aggregate tensor -> fingerprint as int"""
+    return sum((int(x) & (2**64 - 1)) << (64 * i) for i, x in enumerate(row[:4]))
+
+
+def dev_cols(torch, schema_d, n, keys, values, phys=None, logical=None, node=None, tags=None):
+    cols = {"keys": torch.from_numpy(np.ascontiguousarray(keys)).cuda()}
+    if values is not None and schema_d["value_len"]:
+        cols["values"] = torch.from_numpy(np.ascontiguousarray(values)).cuda()
+    if phys is not None:
+        cols["phys"] = torch.from_numpy(np.asarray(phys, np.uint64).view(np.int64)).cuda()
+        cols["logical"] = torch.from_numpy(np.asarray(logical, np.uint32).view(np.int32)).cuda()
+        cols["node"] = torch.from_numpy(np.asarray(node, np.uint64).view(np.int64)).cuda()
+    if tags is not None:
+        cols["tags"] = torch.from_numpy(np.asarray(tags, np.uint8)).cuda()
+    return cols
+
+
+def schema_of(s):
+    from rsos_hip import RecordSchema
+    return RecordSchema(s["key_kind"], s["key_len"], s["value_kind"], s["value_len"], s["record_kind"])
+
+
+# ---- golden fixtures -------------------------------------------------------------------------
+
+def test_reference_golden_entry_fingerprint_on_gpu(gpu, golden):
+    """lift(&7u32, &Entry::present(stamp, 12345u32)) == tests/timestamp_wire_format.rs:105-121"""
+    import torch
+    from rsos_hip import RecordSchema, lift_records
+    v = golden["reference"]["vectors"][2]
+    r = v["record"]
+    s = RecordSchema.dated("u32", "u32")
+    cols = {"keys": torch.tensor([r["key_u32"]], dtype=torch.int32).view(torch.uint8).view(1, 4).cuda(),
+            "values": torch.tensor([r["value_u32"]], dtype=torch.int32).view(torch.uint8).view(1, 4).cuda(),
+            "phys": torch.tensor([int(r["phys"], 16)], dtype=torch.int64).cuda(),
+            "logical": torch.tensor([int(r["logical"], 16)], dtype=torch.int32).cuda(),
+            "node": torch.from_numpy(np.array([int(r["node"], 16)], np.uint64).view(np.int64)).cuda()}
+    fps, bs = lift_records(s, cols)
+    torch.cuda.synchronize()
+    got = [f"0x{x:016x}" for x in np.frombuffer(fps.cpu().numpy().tobytes(), np.uint64)]
+    assert got == v["limbs"]
+    assert bytes(bs.cpu().numpy()[0]) == bytes(fps.cpu().numpy()[0])
+
+
+def test_reference_golden_u64_str_via_encoded_path(gpu, golden):
+    """lift(&50u64, &"Hello") and the 3-element sum through the generic encoded-bytes kernel."""
+    import torch
+    from rsos_hip import lift_encoded
+    v0, v1 = golden["reference"]["vectors"][0], golden["reference"]["vectors"][1]
+    blobs = [bytes.fromhex(v0["encoded_hex"])] + [bytes.fromhex(h) for h in v1["encoded_hex_parts"]]
+    offs = np.zeros(len(blobs) + 1, np.int64)
+    offs[1:] = np.cumsum([len(b) for b in blobs])
+    data = torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).cuda()
+    fps, _ = lift_encoded(data, torch.from_numpy(offs).cuda())
+    fps = fps.cpu().numpy()
+    assert [f"0x{x:016x}" for x in np.frombuffer(fps[0].tobytes(), np.uint64)] == v0["limbs"]
+    s = sum(fp_int(fps[i]) for i in (1, 2, 3)) % M256
+    assert s == limbs_int([int(x, 16) for x in v1["limbs"]])
+
+
+@pytest.mark.parametrize("idx", range(12))
+def test_shape_golden_vectors(gpu, golden, idx):
+    import torch
+    from rsos_hip import lift_records
+    s = golden["shapes"][idx]
+    n = s["n"]
+    keys = np.frombuffer(bytes.fromhex(s["keys"]), np.uint8).reshape(n, s["key_len"])
+    vals = np.frombuffer(bytes.fromhex(s["values"]), np.uint8).reshape(n, s["value_len"])
+    dated = s["record_kind"] == 1
+    cols = dev_cols(torch, s, n, keys, vals, s["phys"] if dated else None, s["logical"] if dated else None,
+                    s["node"] if dated else None, s["tags"])
+    fps, bs = lift_records(schema_of(s), cols)
+    torch.cuda.synchronize()
+    assert [bytes(f).hex() for f in fps.cpu().numpy()] == s["fps"], s["name"]
+    assert bytes(bs.cpu().numpy()[0]).hex() == s["sum"]
+
+
+def test_encoded_golden_ragged(gpu, golden):
+    import torch
+    from rsos_hip import lift_encoded
+    blobs = [bytes.fromhex(r["hex"]) for r in golden["encoded"]]
+    offs = np.zeros(len(blobs) + 1, np.int64)
+    offs[1:] = np.cumsum([len(b) for b in blobs])
+    data = torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).cuda()
+    fps, bs = lift_encoded(data, torch.from_numpy(offs).cuda())
+    got = [bytes(f).hex() for f in fps.cpu().numpy()]
+    assert got == [r["fp"] for r in golden["encoded"]]
+    assert fp_int(bs.cpu().numpy()[0]) == sum(fp_int(bytes.fromhex(r["fp"])) for r in golden["encoded"]) % M256
+
+
+# ---- seeded random batches vs the C oracle ---------------------------------------------------
+
+SHAPES = [("u32", "u32"), ("u64", "u64"), ("u64", "bytes64"), ("bytes16", "bytes64"),
+          ("bytes16", "bytes1024"), ("bytes16", "u64"), ("bytes32", "bytes64")]
+
+
+def oracle_records(O, schema, h):
+    sch = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+    return O.Records(sch, h["keys"], h.get("values"), h.get("phys"), h.get("logical"), h.get("node"), h.get("tags"))
+
+
+@pytest.mark.parametrize("kind", ["plain", "dated", "projection"])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_random_batches_bit_exact(gpu, oracle_lib, shape, kind):
+    import torch
+    from rsos_hip import RecordSchema, lift_records
+    from rsos_hip.synth import make_records, to_host
+    schema = getattr(RecordSchema, kind)(*shape)
+    n = 3001 if shape[1] != "bytes1024" else 1201  # ragged last block
+    cols = make_records(schema, n, seed=11, tombstone_fraction=0.2 if kind != "plain" else 0.0)
+    fps, bs = lift_records(schema, cols)
+    torch.cuda.synchronize()
+    want = oracle_records(oracle_lib, schema, to_host(cols)).lift(threads=8)
+    got = fps.cpu().numpy()
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} mismatching rows, first {bad[:5]}"
+    bsn = bs.cpu().numpy()
+    for g in range(bsn.shape[0]):
+        s = sum(fp_int(want[i]) for i in range(256 * g, min(n, 256 * g + 256))) % M256
+        assert fp_int(bsn[g]) == s, g
+
+
+def test_dual_lift_equals_two_lifts(gpu):
+    import torch
+    from rsos_hip import RecordSchema, lift_dual, lift_records
+    from rsos_hip.synth import make_records
+    for vshape in ("bytes64", "bytes1024"):
+        d = RecordSchema.dated("bytes16", vshape)
+        cols = make_records(d, 2000, seed=3, tombstone_fraction=0.3)
+        fd, bd, fpj, bpj = lift_dual(d, cols)
+        a, ab = lift_records(d, cols)
+        b, bb = lift_records(d.with_kind(2), cols)
+        torch.cuda.synchronize()
+        assert torch.equal(fd, a) and torch.equal(fpj, b) and torch.equal(bd, ab) and torch.equal(bpj, bb)
+
+
+def test_encoded_random_ragged(gpu, oracle_lib):
+    import torch
+    from rsos_hip import lift_encoded
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 3000, 1500)
+    lens[:6] = [0, 0, 1, 1024, 1025, 2048]
+    blobs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
+    offs = np.zeros(len(blobs) + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    data = torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).cuda()
+    fps, _ = lift_encoded(data, torch.from_numpy(offs).cuda())
+    want = oracle_lib.lift_encoded(blobs, threads=8)
+    assert np.array_equal(fps.cpu().numpy(), want)
+
+
+def test_empty_batches(gpu):
+    import torch
+    from rsos_hip import RecordSchema, lift_records, range_aggregates
+    from rsos_hip.synth import make_records
+    s = RecordSchema.dated("bytes16", "bytes64")
+    cols = make_records(s, 0)
+    fps, bs = lift_records(s, cols)
+    assert fps.shape == (0, 32) and bs.shape == (0, 32)
+    lo = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = range_aggregates(fps, bs, None, lo, lo)
+    torch.cuda.synchronize()
+    assert out.cpu().tolist() == [[0, 0, 0, 0, 0]]
+
+
+# ---- range aggregates -------------------------------------------------------------------------
+
+def test_range_aggregates_match_prefix_sums(gpu, oracle_lib):
+    import torch
+    from rsos_hip import RecordSchema, lift_records, range_aggregates, reduce_blocks
+    from rsos_hip.synth import make_records, to_host
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 300_007  # > 4 super-blocks, ragged
+    cols = make_records(s, n, seed=9)
+    fps, bs = lift_records(s, cols)
+    ss = reduce_blocks(bs)
+    want = oracle_records(oracle_lib, s, to_host(cols)).lift(threads=8)
+    assert np.array_equal(fps.cpu().numpy(), want)
+    pref = [0]
+    for f in want:
+        pref.append(pref[-1] + fp_int(f))
+    rng = np.random.default_rng(2)
+    lo = list(rng.integers(0, n, 200)) + [0, 0, 5, n - 1, 65536, 65535, 256, 100, n]
+    hi = list(rng.integers(0, n + 50, 200)) + [n, 0, 5, n, 3 * 65536 + 7, 65536 * 4, 512, 50, n]
+    lo_t = torch.tensor(lo, dtype=torch.int64, device="cuda")
+    hi_t = torch.tensor(hi, dtype=torch.int64, device="cuda")
+    for b, sup in ((bs, ss), (bs, None), (None, None)):
+        out = range_aggregates(fps, b, sup, lo_t, hi_t).cpu().numpy()
+        for j, (l, h) in enumerate(zip(lo, hi)):
+            h2 = min(int(h), n)
+            l2 = min(int(l), h2)
+            assert int(out[j][4]) == h2 - l2
+            assert agg_int(out[j]) == (pref[h2] - pref[l2]) % M256, (j, l, h)
+
+
+def test_combine_aggregates(gpu):
+    import torch
+    from rsos_hip import combine_aggregates
+    rng = np.random.default_rng(4)
+    parts = rng.integers(-2**63, 2**63 - 1, (8, 16, 5), dtype=np.int64)
+    parts[..., 4] = rng.integers(0, 10**9, (8, 16))
+    parts[0, 0, :4] = -1  # all-ones limbs: carries everywhere
+    parts[1, 0, :4] = [1, 0, 0, 0]
+    out = combine_aggregates(torch.from_numpy(parts).cuda()).cpu().numpy()
+    for j in range(16):
+        want = sum(agg_int(parts[p, j]) for p in range(8)) % M256
+        assert agg_int(out[j]) == want
+        assert int(out[j][4]) == int(parts[:, j, 4].sum())
+
+
+# ---- the store (Rsos<K> realisation) -----------------------------------------------------
+
+def _store_fixture(oracle_lib, n=5000, seed=1):
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    rng = np.random.default_rng(seed)
+    keys = np.unique(rng.integers(0, 2**40, n, dtype=np.uint64))
+    n = len(keys)
+    vals = rng.integers(0, 2**63, n, dtype=np.uint64)
+    schema = RecordSchema.plain("u64", "u64")
+    st = GpuFingerprintStore(schema)
+    st.load_bulk({"keys": keys.view(np.uint8).reshape(n, 8), "values": vals.view(np.uint8).reshape(n, 8)})
+    O = oracle_lib
+    recs = O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0), keys.view(np.uint8).reshape(n, 8),
+                     vals.view(np.uint8).reshape(n, 8))
+    return st, keys, vals, recs
+
+
+def test_store_rsos_surface(gpu, oracle_lib):
+    from rsos_hip.store import KeyRange
+    st, keys, vals, recs = _store_fixture(oracle_lib)
+    n = len(keys)
+    t = oracle_lib.FingerprintTreeMap(recs)
+    t.fill(0, n)
+    root = st.aggregate()
+    assert root.size == n == st.size()
+    assert root.fingerprint.to_int() == limbs_int(t.root()[0])
+    assert np.array_equal(st.fingerprints(), recs.lift())
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        a, b = (int(x) for x in rng.integers(0, 2**40, 2))
+        got = st.aggregate(KeyRange(a, b))
+        fp, size = t.aggregate(np.uint64(a).tobytes(), np.uint64(b).tobytes())
+        assert got.size == size and got.fingerprint.to_int() == limbs_int(fp)
+        assert st.rank(a) == t.rank(np.uint64(a).tobytes())
+    # count-agreement and rank/select inverse laws (rbsr/src/rsos_view.rs:30-36)
+    for r in rng.integers(0, n, 50):
+        k = st.select(int(r))
+        assert k == int(keys[r]) and st.rank(k) == r
+    with pytest.raises(IndexError):
+        st.select(n)
+    k0, k1 = int(keys[10]), int(keys[20])
+    assert st.aggregate(KeyRange(k0, k1)).size == st.rank(k1) - st.rank(k0) == 10
+    assert st.aggregate(KeyRange(k0, k1, "included", "included")).size == 11
+    assert st.aggregate(KeyRange(k0, k1, "excluded", "excluded")).size == 9
+    assert st.aggregate(KeyRange(k1, k0)).is_empty()  # inverted -> ZERO
+    assert [k for k, _ in st.enumerate(KeyRange(k0, k1))] == [int(x) for x in keys[10:20]]
+    st.close()
+
+
+def test_store_apply_insert_overwrite_delete(gpu, oracle_lib):
+    st, keys, vals, recs = _store_fixture(oracle_lib, n=3000, seed=8)
+    O = oracle_lib
+    content = {int(k): int(v) for k, v in zip(keys, vals)}
+    rng = np.random.default_rng(12)
+    for rnd in range(3):
+        new_keys = rng.integers(0, 2**40, 300, dtype=np.uint64)
+        over = rng.choice(np.array(list(content.keys()), np.uint64), 100, replace=False)
+        dels = rng.choice(np.array(list(content.keys()), np.uint64), 50, replace=False)
+        bk = np.unique(np.concatenate([new_keys, over]))
+        bk = np.setdiff1d(bk, dels)
+        bv = rng.integers(0, 2**63, len(bk), dtype=np.uint64)
+        allk = np.concatenate([bk, dels])
+        allv = np.concatenate([bv, np.zeros(len(dels), np.uint64)])
+        ops = np.concatenate([np.zeros(len(bk), np.uint8), np.ones(len(dels), np.uint8)])
+        n_new, n_over, n_del = st.apply({"keys": allk.view(np.uint8).reshape(-1, 8),
+                                         "values": allv.view(np.uint8).reshape(-1, 8)}, ops)
+        exp_new = sum(1 for k in bk if int(k) not in content)
+        assert (n_new, n_over, n_del) == (exp_new, len(bk) - exp_new, len(dels))
+        for k, v in zip(bk, bv):
+            content[int(k)] = int(v)
+        for k in dels:
+            content.pop(int(k))
+        ks = np.array(sorted(content), np.uint64)
+        vs = np.array([content[int(k)] for k in ks], np.uint64)
+        r2 = O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0), ks.view(np.uint8).reshape(-1, 8),
+                       vs.view(np.uint8).reshape(-1, 8))
+        want = sum(fp_int(f) for f in r2.lift()) % M256
+        root = st.aggregate()
+        assert root.size == len(content) and root.fingerprint.to_int() == want
+    # duplicate delivery moves the aggregate by 0 (btreemap_oracle.rs:195-231)
+    before = st.aggregate()
+    k = int(ks[7]); v = content[k]
+    assert st.insert(k, v.to_bytes(8, "little")) is False
+    assert st.aggregate() == before
+    assert st.delete(k) is True and st.aggregate().size == before.size - 1
+    assert st.insert(k, v.to_bytes(8, "little")) is True and st.aggregate() == before
+    st.close()
+
+
+def test_lift_host_end_to_end(gpu, oracle_lib):
+    import ctypes as C
+    from rsos_hip import RecordSchema, _abi as A
+    from rsos_hip.synth import make_records, to_host
+    s = RecordSchema.dated("bytes16", "bytes64")
+    h = to_host(make_records(s, 4000, seed=21, tombstone_fraction=0.1))
+    cols = A.Columns(*[None if h.get(k) is None else h[k].ctypes.data for k in
+                       ("keys", "phys", "logical", "node", "tags", "values")])
+    out = np.zeros((4000, 32), np.uint8)
+    sc = s.c()
+    A.check(A.lib().rh_lift_host(0, C.byref(sc), C.byref(cols), 4000, out.ctypes.data), "rh_lift_host")
+    assert np.array_equal(out, oracle_records(oracle_lib, s, h).lift(threads=8))
+
+
+# ---- full size: size-independent properties ------------------------------------------------------
+
+def test_full_size_config2_properties(gpu, oracle_lib):
+    """10 M records, 16 B key / 64 B value, dated (BASELINE config 2): sampled bit-exactness,
+    block sums == an independent torch reduction, partition additivity of range aggregates."""
+    import torch
+    from rsos_hip import RecordSchema, lift_records, range_aggregates, reduce_blocks
+    from rsos_hip.synth import make_records, to_host
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 10_000_000
+    cols = make_records(s, n, seed=42)
+    fps, bs = lift_records(s, cols)
+    ss = reduce_blocks(bs)
+    # sampled rows vs the oracle: a contiguous window at each end + the middle
+    for lo in (0, n // 2 - 1000, n - 3000):
+        want = oracle_records(oracle_lib, s, to_host(cols, lo, lo + 3000)).lift(threads=8)
+        assert np.array_equal(fps[lo:lo + 3000].cpu().numpy(), want)
+    # root via the kernels vs an independent torch reduction over u16 limbs
+    limbs16 = fps.view(torch.int16).to(torch.int64) & 0xFFFF  # (n, 16)
+    col = limbs16.sum(dim=0).cpu().tolist()
+    want_root = sum(int(c) << (16 * i) for i, c in enumerate(col)) % M256
+    lo_t = torch.tensor([0, 0, 1234567], dtype=torch.int64, device="cuda")
+    hi_t = torch.tensor([n, 1234567, n], dtype=torch.int64, device="cuda")
+    out = range_aggregates(fps, bs, ss, lo_t, hi_t).cpu().numpy()
+    assert agg_int(out[0]) == want_root and int(out[0][4]) == n
+    assert (agg_int(out[1]) + agg_int(out[2])) % M256 == want_root

@@ -7,6 +7,7 @@ namespace rh {
 
 struct DevCols;
 
+
 // Schema-specialised lift; returns hipErrorInvalidValue-free status, or sets *supported = false
 // when no instantiation matches (the caller then reports RH_ERR_UNSUPPORTED).
 hipError_t launch_lift_schema(int kk, int kl, int vk, int vl, int rk, bool tags, bool dual,

@@ -93,7 +93,7 @@ __device__ __forceinline__ void lift_pipe_body(const DevCols &c, uint64_t n, uin
 
 // occupancy target: 6 waves per SIMD (<= 80 VGPRs) -- two records' words live per lane
 template <int KK, int KL, int VK, int VL, int RK, bool TAGS, bool DUAL>
-__global__ __launch_bounds__(LIFT_THREADS) __attribute__((amdgpu_waves_per_eu(RH_PIPE_WAVES, 8)))
+__global__ __launch_bounds__(LIFT_THREADS) __attribute__((amdgpu_waves_per_eu(6, 8)))
 void k_lift_pipe(DevCols c, uint64_t n, uint8_t *fps, uint8_t *bsums, uint8_t *fps2, uint8_t *bsums2,
                  uint64_t nblk, uint64_t per) {
     lift_pipe_body<KK, KL, VK, VL, RK, TAGS, DUAL>(c, n, fps, bsums, fps2, bsums2, nblk, per);

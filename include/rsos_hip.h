@@ -153,45 +153,55 @@ void rh_fp_add(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
 void rh_fp_sub(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
 
 /* ---- GPU-resident RSOS store ---------------------------------------------------------
- * A rank-ordered set of records resident in HBM with per-record fingerprints and block /
- * super-block sums; the host keeps the key column for rank / select (rbsr's `select`
- * returns &K, so keys must stay host-addressable).
- * Realises Rsos<K> (rsos/src/rsos_trait.rs:39-90) for fixed-width keys:
- *   size -> rh_store_len, aggregate -> rh_store_aggregate[_keys], rank -> rh_store_rank,
- *   select -> rh_store_select, insert/delete -> rh_store_apply.                          */
+ * A rank-ordered set resident in HBM: keys, per-record fingerprints, and the 256-row block /
+ * 65536-row super-block sums (the GPU form of FingerprintTreeMap's cached subtree
+ * Aggregates, rsos/src/fingerprint_tree_map/node.rs:54-91).  Record payloads are lifted on
+ * ingest and not kept on the device; the caller owns K and V in host memory, as the
+ * reference's map does (Rsos::enumerate / select return borrows, rsos_trait.rs:66-80).
+ * Realises Rsos<K> (rsos/src/rsos_trait.rs:39-90) for u32 / u64 / 8-, 16-, 32-byte keys:
+ *   size -> rh_store_len, aggregate -> rh_store_aggregate[s|_keys], rank -> rh_store_rank[s],
+ *   select -> rh_store_select, insert / delete -> rh_store_apply[_device].
+ * Every call drains the store's stream before returning.                                   */
 typedef struct rh_store rh_store;
 
 int rh_store_create(int device, const rh_schema *schema, rh_store **out);
 int rh_store_destroy(rh_store *store);
-/* Replace the contents with n records (host columns), which must be sorted by key in the
- * key type's Ord and free of duplicates.  Bulk fill: the GPU form of FromIterator /
- * ReplicatedMap::load_bulk (rsos/src/fingerprint_tree_map_iter/into_iter.rs:22-33,
- * src/replicated_map/write.rs:184).                                                      */
+/* Replace the contents with n records, sorted by key in the key type's Ord and free of
+ * duplicates (checked on the device; RH_ERR_ARG otherwise).  Bulk fill: the GPU form of
+ * FromIterator / ReplicatedMap::load_bulk (rsos/src/fingerprint_tree_map_iter/into_iter.rs:22-33,
+ * src/replicated_map/write.rs:184).  _device: the columns are already in HBM.             */
 int rh_store_load(rh_store *store, const rh_columns *host_cols, size_t n);
+int rh_store_load_device(rh_store *store, const rh_columns *dev_cols, size_t n);
 int rh_store_len(const rh_store *store, uint64_t *out);
 /* Aggregate over rank range [lo, hi) */
 int rh_store_aggregate(rh_store *store, uint64_t lo, uint64_t hi, rh_aggregate *out);
-/* r rank ranges in one launch (the ≤ 16 child ranges of one rbsr SPLIT, protocol.rs:299-307) */
+/* r rank ranges in one launch (the <= 16 child ranges of one rbsr SPLIT, protocol.rs:299-307) */
 int rh_store_aggregates(rh_store *store, const uint64_t *lo, const uint64_t *hi, size_t r,
                         rh_aggregate *out);
 /* Aggregate over the key range given by two bounds.  kind: 0 = unbounded, 1 = included,
- * 2 = excluded (std::ops::Bound).  Inverted ranges give ZERO.                            */
+ * 2 = excluded (std::ops::Bound).  Inverted ranges give ZERO (rbsr/src/protocol.rs:230-232). */
 int rh_store_aggregate_keys(rh_store *store, int lo_kind, const void *lo_key, int hi_kind,
                             const void *hi_key, rh_aggregate *out);
-/* Rank(z) = number of keys strictly below z (query.rs:93-121) */
-int rh_store_rank(const rh_store *store, const void *key, uint64_t *out);
-/* Select(r): copies the r-th key into key_out (key_len bytes); RH_ERR_ARG if r >= size  */
-int rh_store_select(const rh_store *store, uint64_t r, void *key_out);
-/* Copy fingerprints of ranks [lo, hi) to the host (32 B each) */
+/* Rank(z) = number of keys strictly below z (query.rs:93-121); _ranks: m keys at once      */
+int rh_store_rank(rh_store *store, const void *key, uint64_t *out);
+int rh_store_ranks(rh_store *store, const void *keys, size_t m, uint64_t *out);
+/* Select(r): copies the r-th key into key_out (key_len bytes); RH_ERR_ARG if r >= size      */
+int rh_store_select(rh_store *store, uint64_t r, void *key_out);
+/* Copy the keys / fingerprints of ranks [lo, hi) to the host (Enumerate's key order)       */
+int rh_store_keys(rh_store *store, uint64_t lo, uint64_t hi, void *host_out);
 int rh_store_fingerprints(rh_store *store, uint64_t lo, uint64_t hi, uint8_t *host_out);
 
 /* Batched insert / overwrite / delete (FingerprintTreeMap::insert / remove, mutate.rs:23-154).
- * ops[i]: 0 = insert-or-overwrite record i of `host_cols`, 1 = delete key i (value columns
- * ignored).  Keys within one batch must be distinct.  On return every aggregate reflects
- * the whole batch (no half-applied state is observable).  n_new / n_overwritten / n_deleted
- * (nullable) report what happened.                                                       */
+ * ops[i]: 0 = insert-or-overwrite record i, 1 = delete key i (its value columns are ignored).
+ * Keys within one batch must be distinct (RH_ERR_ARG, store unchanged).  On return every
+ * aggregate reflects the whole batch; an overwrite replaces the element's fingerprint (the
+ * `new - old` delta of mutate.rs:31-41), so re-delivering a record changes nothing.
+ * n_new / n_overwritten / n_deleted (nullable) report what happened.
+ * _device: columns and ops already in HBM (the on-GPU incremental update of config 5).    */
 int rh_store_apply(rh_store *store, const rh_columns *host_cols, const uint8_t *ops, size_t n,
                    uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted);
+int rh_store_apply_device(rh_store *store, const rh_columns *dev_cols, const uint8_t *dev_ops, size_t n,
+                          uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted);
 
 #ifdef __cplusplus
 }

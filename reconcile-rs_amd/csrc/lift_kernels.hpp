@@ -188,12 +188,18 @@ struct Streamer {
         }
         constexpr int b_start = C == 0 ? 1 : 16 * C;
         constexpr int b_end = C == NC - 1 ? NB - 1 : 16 * C + 16;
+        // software-pipelined: block b+1's words are in flight while block b is compressed
+        uint32_t m[16];
+        if (b_start < b_end) block_mid(b_start, m);
 #pragma unroll 1
         for (int b = b_start; b < b_end; b++) {
-            uint32_t m[16];
-            block_mid(b, m);
+            uint32_t mn[16];
+            block_mid(b + 1 < b_end ? b + 1 : b, mn);  // unconditional (stays ahead of the
+                                                       // compression); never past the row
             const uint32_t flags = (b == 16 * C ? CHUNK_START : 0u) | (b == 16 * C + 15 ? CHUNK_END : 0u);
             compress(cv, m, (uint32_t)C, 0, 64, flags);
+#pragma unroll
+            for (int j = 0; j < 16; j++) m[j] = mn[j];
         }
         if constexpr (C == NC - 1) {
             uint32_t m[16];

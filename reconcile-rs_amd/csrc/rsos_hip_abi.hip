@@ -21,6 +21,7 @@
 #include "../../include/rsos_hip.h"
 #include "internal.hpp"
 #include "lift_kernels.hpp"
+#include "store_kernels.hpp"
 
 namespace {
 
@@ -361,63 +362,93 @@ extern "C" int rh_lift_host(int device, const rh_schema *schema, const rh_column
 }
 
 // =================================================================================================
-// The GPU-resident store
+// The GPU-resident store: keys + fingerprints + block / super-block sums in HBM, rank order.
 struct rh_store {
     int device = 0;
     rh_schema schema{};
     hipStream_t stream = nullptr;
     std::mutex mu;  // serialises callers sharing one store (readers under a RwLock read guard)
-    size_t n = 0;
-    size_t krow = 0, vrow = 0;
-    // host mirror (rank order): key column for rank/select, full columns for rebuilds
-    std::vector<uint8_t> h_keys, h_values, h_tags;
-    std::vector<uint64_t> h_phys, h_node;
-    std::vector<uint32_t> h_logical;
-    bool has_tags = false;
-    // device
-    DevColumns cols;
-    DevBuf<uint8_t> fps, bsums, ssums;
-    DevBuf<uint64_t> q_lo, q_hi;
+    rh::StoreKeyOps *kops = nullptr;
+    size_t kl = 0;
+    uint64_t n = 0;
+    int cur = 0;
+    DevBuf<uint8_t> keys[2], fps[2];  // double-buffered: a batch merges from one into the other
+    DevBuf<uint8_t> bsums, ssums;
+    DevColumns staging;               // host batches land here
+    DevBuf<uint8_t> bfps, skeys, sfps, sops, hops;
+    DevBuf<uint64_t> q_lo, q_hi, counts;
     DevBuf<rh_aggregate> q_out;
+    DevBuf<uint8_t> q_keys;
+    DevBuf<uint32_t> flag, q_rank;
+    rh::Scratch scratch;
 
-    int cmp_keys(const uint8_t *a, const uint8_t *b) const {
-        switch (schema.key_kind) {
-        case RH_KEY_U32: { uint32_t x, y; memcpy(&x, a, 4); memcpy(&y, b, 4); return (x > y) - (x < y); }
-        case RH_KEY_U64: { uint64_t x, y; memcpy(&x, a, 8); memcpy(&y, b, 8); return (x > y) - (x < y); }
-        case RH_KEY_UNIT: return 0;
-        default: return memcmp(a, b, krow);
-        }
-    }
-    // number of keys strictly below key (query.rs:93-121)
-    size_t rank_of(const uint8_t *key) const {
-        size_t lo = 0, hi = n;
-        while (lo < hi) {
-            size_t mid = (lo + hi) / 2;
-            if (cmp_keys(&h_keys[mid * krow], key) < 0) lo = mid + 1;
-            else hi = mid;
-        }
-        return lo;
-    }
-    int rebuild() {
-        int rc;
-        rh_columns h;
-        h.keys = h_keys.data();
-        h.values = h_values.data();
-        h.phys = h_phys.data();
-        h.node = h_node.data();
-        h.logical = h_logical.data();
-        h.tags = has_tags ? h_tags.data() : nullptr;
-        if ((rc = cols.upload(schema, h, n, stream))) return rc;
-        const size_t nb = rh_num_blocks(n), ns = rh_num_superblocks(n);
-        if ((rc = fps.ensure(n * 32 + 32)) || (rc = bsums.ensure(nb * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)))
-            return rc;
-        if (n) {
-            rh_columns v = cols.view(schema);
-            if ((rc = lift_dispatch(schema, v, n, fps.p, bsums.p, nullptr, nullptr, false, stream))) return rc;
-            RH_HIP(rh::launch_reduce(bsums.p, nb, ssums.p, stream));
-        }
+    int sync() {
         RH_HIP(hipStreamSynchronize(stream));
         return RH_OK;
+    }
+    int resum() {  // block + super-block sums of the current contents
+        int rc;
+        const size_t nb = rh_num_blocks(n), ns = rh_num_superblocks(n);
+        if ((rc = bsums.ensure(nb * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32))) return rc;
+        if (n) {
+            RH_HIP(rh::launch_reduce(fps[cur].p, n, bsums.p, stream));
+            RH_HIP(rh::launch_reduce(bsums.p, nb, ssums.p, stream));
+        }
+        return RH_OK;
+    }
+    int load_device(const rh_columns &c, size_t m) {
+        int rc;
+        const int nxt = cur;  // contents are replaced in place
+        if ((rc = keys[nxt].ensure(m * kl + 64)) || (rc = fps[nxt].ensure(m * 32 + 64)) || (rc = flag.ensure(4))) return rc;
+        if (m) {
+            RH_HIP(hipMemcpyAsync(keys[nxt].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
+            if ((rc = lift_dispatch(schema, c, m, fps[nxt].p, nullptr, nullptr, nullptr, false, stream))) return rc;
+            RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
+            RH_HIP(kops->check_sorted(keys[nxt].p, m, flag.p, stream));
+        }
+        uint32_t bad = 0;
+        if (m) RH_HIP(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        if (bad) {
+            n = 0;
+            return fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
+        }
+        n = m;
+        if ((rc = resum())) return rc;
+        return sync();
+    }
+    int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3]) {
+        int rc;
+        out[0] = out[1] = out[2] = 0;
+        if (m == 0) return RH_OK;
+        if (n + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if ((rc = bfps.ensure(m * 32 + 64)) || (rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) ||
+            (rc = sops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
+            return rc;
+        // 1. lift the batch (deletes are lifted too and ignored: their value columns may be garbage
+        //    but are never read past their own rows)
+        if ((rc = lift_dispatch(schema, c, m, bfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
+        // 2. key order + duplicate check
+        RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
+        RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), bfps.p, ops, m, scratch, skeys.p, sfps.p,
+                                sops.p, flag.p, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        uint32_t dup = 0;
+        RH_HIP(hipMemcpyAsync(&dup, flag.p, 4, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        if (dup) return fail(RH_ERR_ARG, "duplicate key within one batch");
+        // 3. merge into the other buffer, then swap
+        const int nxt = 1 - cur;
+        if ((rc = keys[nxt].ensure((n + m) * kl + 64)) || (rc = fps[nxt].ensure((n + m) * 32 + 64))) return rc;
+        RH_HIP(kops->merge(keys[cur].p, fps[cur].p, n, skeys.p, sfps.p, sops.p, m, scratch, keys[nxt].p, fps[nxt].p,
+                           counts.p, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        RH_HIP(hipMemcpyAsync(out, counts.p, 24, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        cur = nxt;
+        n = n + out[0] - out[2];
+        if ((rc = resum())) return rc;
+        return sync();
     }
     int query(const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {
         int rc;
@@ -425,13 +456,25 @@ struct rh_store {
         if ((rc = q_lo.ensure(r)) || (rc = q_hi.ensure(r)) || (rc = q_out.ensure(r))) return rc;
         RH_HIP(hipMemcpyAsync(q_lo.p, lo, r * 8, hipMemcpyHostToDevice, stream));
         RH_HIP(hipMemcpyAsync(q_hi.p, hi, r * 8, hipMemcpyHostToDevice, stream));
-        RH_HIP(rh::launch_range_query(fps.p, bsums.p, ssums.p, n, q_lo.p, q_hi.p, r,
+        RH_HIP(rh::launch_range_query(fps[cur].p, bsums.p, ssums.p, n, q_lo.p, q_hi.p, r,
                                       reinterpret_cast<uint64_t *>(q_out.p), stream));
         RH_HIP(hipMemcpyAsync(out, q_out.p, r * sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipStreamSynchronize(stream));
-        return RH_OK;
+        return sync();
+    }
+    void release() {
+        (void)hipStreamSynchronize(stream);
+        for (int k = 0; k < 2; k++) { keys[k].release(); fps[k].release(); }
+        bsums.release(); ssums.release(); staging.release();
+        bfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release();
+        q_lo.release(); q_hi.release(); counts.release(); q_out.release(); q_keys.release();
+        flag.release(); q_rank.release();
+        scratch.release();
     }
 };
+
+#define RH_LOCK(s)                                  \
+    std::lock_guard<std::mutex> guard_((s)->mu);    \
+    RH_HIP(hipSetDevice((s)->device))
 
 extern "C" {
 
@@ -441,17 +484,20 @@ int rh_store_create(int device, const rh_schema *schema, rh_store **out) {
     if (!out) return fail(RH_ERR_ARG, "out is NULL");
     if (rh_schema_supported(schema) != 1)
         return fail(RH_ERR_UNSUPPORTED, "store needs a schema with a specialised lift kernel");
+    rh::StoreKeyOps *kops = rh::store_key_ops(schema->key_kind, key_row(*schema));
+    if (!kops) return fail(RH_ERR_UNSUPPORTED, "store keys must be u32, u64 or 8/16/32-byte arrays");
     RH_HIP(hipSetDevice(device));
     rh_store *s = new rh_store();
     s->device = device;
     s->schema = *schema;
-    s->krow = key_row(*schema);
-    s->vrow = value_row(*schema);
+    s->kops = kops;
+    s->kl = key_row(*schema);
     hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete s;
         return fail(RH_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
+    s->scratch.stream = s->stream;
     *out = s;
     return RH_OK;
 }
@@ -459,48 +505,26 @@ int rh_store_create(int device, const rh_schema *schema, rh_store **out) {
 int rh_store_destroy(rh_store *s) {
     if (!s) return RH_OK;
     (void)hipSetDevice(s->device);
-    (void)hipStreamSynchronize(s->stream);
-    s->cols.release();
-    s->fps.release();
-    s->bsums.release();
-    s->ssums.release();
-    s->q_lo.release();
-    s->q_hi.release();
-    s->q_out.release();
+    s->release();
     (void)hipStreamDestroy(s->stream);
     delete s;
     return RH_OK;
 }
 
 int rh_store_load(rh_store *s, const rh_columns *h, size_t n) {
-    if (!s) return fail(RH_ERR_ARG, "store is NULL");
-    if (!h) return fail(RH_ERR_ARG, "columns is NULL");
-    std::lock_guard<std::mutex> g(s->mu);
-    RH_HIP(hipSetDevice(s->device));
-    const rh_schema &sc = s->schema;
-    if (n) {
-        if (s->krow && !h->keys) return fail(RH_ERR_ARG, "keys NULL");
-        if (s->vrow && !h->values) return fail(RH_ERR_ARG, "values NULL");
-        if (sc.record_kind == RH_REC_DATED && (!h->phys || !h->node || !h->logical))
-            return fail(RH_ERR_ARG, "DATED needs stamp columns");
-    }
-    const uint8_t *k = static_cast<const uint8_t *>(h->keys);
-    for (size_t i = 1; i < n; i++)
-        if (s->cmp_keys(k + (i - 1) * s->krow, k + i * s->krow) >= 0)
-            return fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
-    s->n = n;
-    s->h_keys.assign(k, k + n * s->krow);
-    const uint8_t *v = static_cast<const uint8_t *>(h->values);
-    s->h_values.assign(v, v + n * s->vrow);
-    if (sc.record_kind == RH_REC_DATED) {
-        s->h_phys.assign(h->phys, h->phys + n);
-        s->h_node.assign(h->node, h->node + n);
-        s->h_logical.assign(h->logical, h->logical + n);
-    }
-    s->has_tags = h->tags != nullptr && sc.record_kind != RH_REC_PLAIN;
-    if (s->has_tags) s->h_tags.assign(h->tags, h->tags + n);
-    else s->h_tags.clear();
-    return s->rebuild();
+    if (!s || !h) return fail(RH_ERR_ARG, "NULL");
+    RH_LOCK(s);
+    int rc;
+    if ((rc = s->staging.upload(s->schema, *h, n, s->stream))) return rc;
+    return s->load_device(s->staging.view(s->schema), n);
+}
+
+int rh_store_load_device(rh_store *s, const rh_columns *dev_cols, size_t n) {
+    if (!s) return fail(RH_ERR_ARG, "NULL");
+    int rc = check_cols(s->schema, dev_cols, n);
+    if (rc) return rc;
+    RH_LOCK(s);
+    return s->load_device(*dev_cols, n);
 }
 
 int rh_store_len(const rh_store *s, uint64_t *out) {
@@ -512,8 +536,7 @@ int rh_store_len(const rh_store *s, uint64_t *out) {
 int rh_store_aggregates(rh_store *s, const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     if (r && (!lo || !hi || !out)) return fail(RH_ERR_ARG, "NULL buffer");
-    std::lock_guard<std::mutex> g(s->mu);
-    RH_HIP(hipSetDevice(s->device));
+    RH_LOCK(s);
     return s->query(lo, hi, r, out);
 }
 
@@ -521,28 +544,38 @@ int rh_store_aggregate(rh_store *s, uint64_t lo, uint64_t hi, rh_aggregate *out)
     return rh_store_aggregates(s, &lo, &hi, 1, out);
 }
 
-int rh_store_rank(const rh_store *s, const void *key, uint64_t *out) {
-    if (!s || !key || !out) return fail(RH_ERR_ARG, "NULL");
-    *out = s->rank_of(static_cast<const uint8_t *>(key));
+int rh_store_ranks(rh_store *s, const void *keys, size_t m, uint64_t *out) {
+    if (!s || (m && (!keys || !out))) return fail(RH_ERR_ARG, "NULL");
+    if (m == 0) return RH_OK;
+    RH_LOCK(s);
+    int rc;
+    if ((rc = s->q_keys.ensure(m * s->kl + 64)) || (rc = s->q_rank.ensure(m))) return rc;
+    RH_HIP(hipMemcpyAsync(s->q_keys.p, keys, m * s->kl, hipMemcpyHostToDevice, s->stream));
+    RH_HIP(s->kops->search(s->keys[s->cur].p, s->n, s->q_keys.p, m, s->q_rank.p, nullptr, s->stream));
+    std::vector<uint32_t> r32(m);
+    RH_HIP(hipMemcpyAsync(r32.data(), s->q_rank.p, m * 4, hipMemcpyDeviceToHost, s->stream));
+    if ((rc = s->sync())) return rc;
+    for (size_t j = 0; j < m; j++) out[j] = r32[j];
     return RH_OK;
 }
 
-int rh_store_select(const rh_store *s, uint64_t r, void *key_out) {
+int rh_store_rank(rh_store *s, const void *key, uint64_t *out) { return rh_store_ranks(s, key, 1, out); }
+
+int rh_store_keys(rh_store *s, uint64_t lo, uint64_t hi, void *host_out) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    if (lo > hi || hi > s->n) return fail(RH_ERR_ARG, "bad rank range");
+    if (hi == lo) return RH_OK;
+    if (!host_out) return fail(RH_ERR_ARG, "host_out NULL");
+    RH_LOCK(s);
+    RH_HIP(hipMemcpyAsync(host_out, s->keys[s->cur].p + lo * s->kl, (hi - lo) * s->kl, hipMemcpyDeviceToHost,
+                          s->stream));
+    return s->sync();
+}
+
+int rh_store_select(rh_store *s, uint64_t r, void *key_out) {
     if (!s || !key_out) return fail(RH_ERR_ARG, "NULL");
     if (r >= s->n) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
-    memcpy(key_out, &s->h_keys[r * s->krow], s->krow);
-    return RH_OK;
-}
-
-// Bound -> rank: Included(k) lower = rank(k); Excluded(k) lower = rank(k) + [k present];
-// Included(k) upper = rank(k) + [k present]; Excluded(k) upper = rank(k).
-static size_t bound_rank(const rh_store *s, int kind, const uint8_t *key, bool lower) {
-    if (kind == 0) return lower ? 0 : s->n;
-    size_t r = s->rank_of(key);
-    bool present = r < s->n && s->cmp_keys(&s->h_keys[r * s->krow], key) == 0;
-    bool incl = kind == 1;
-    if (lower) return (!incl && present) ? r + 1 : r;
-    return (incl && present) ? r + 1 : r;
+    return rh_store_keys(s, r, r + 1, key_out);
 }
 
 int rh_store_aggregate_keys(rh_store *s, int lo_kind, const void *lo_key, int hi_kind, const void *hi_key,
@@ -550,98 +583,58 @@ int rh_store_aggregate_keys(rh_store *s, int lo_kind, const void *lo_key, int hi
     if (!s || !out) return fail(RH_ERR_ARG, "NULL");
     if (lo_kind < 0 || lo_kind > 2 || hi_kind < 0 || hi_kind > 2) return fail(RH_ERR_ARG, "bad bound kind");
     if ((lo_kind && !lo_key) || (hi_kind && !hi_key)) return fail(RH_ERR_ARG, "bound key is NULL");
-    uint64_t lo = bound_rank(s, lo_kind, static_cast<const uint8_t *>(lo_key), true);
-    uint64_t hi = bound_rank(s, hi_kind, static_cast<const uint8_t *>(hi_key), false);
-    if (hi < lo) hi = lo;  // inverted range -> ZERO (rbsr/src/protocol.rs:230-232)
-    return rh_store_aggregates(s, &lo, &hi, 1, out);
+    RH_LOCK(s);
+    int rc;
+    if ((rc = s->q_keys.ensure(2 * s->kl + 64)) || (rc = s->q_lo.ensure(1)) || (rc = s->q_hi.ensure(1)) ||
+        (rc = s->q_out.ensure(1)))
+        return rc;
+    if (lo_kind) RH_HIP(hipMemcpyAsync(s->q_keys.p, lo_key, s->kl, hipMemcpyHostToDevice, s->stream));
+    if (hi_kind) RH_HIP(hipMemcpyAsync(s->q_keys.p + s->kl, hi_key, s->kl, hipMemcpyHostToDevice, s->stream));
+    RH_HIP(s->kops->bounds(s->keys[s->cur].p, s->n, s->q_keys.p, lo_kind, s->q_keys.p + s->kl, hi_kind, s->q_lo.p,
+                           s->q_hi.p, s->stream));
+    RH_HIP(rh::launch_range_query(s->fps[s->cur].p, s->bsums.p, s->ssums.p, s->n, s->q_lo.p, s->q_hi.p, 1,
+                                  reinterpret_cast<uint64_t *>(s->q_out.p), s->stream));
+    RH_HIP(hipMemcpyAsync(out, s->q_out.p, sizeof(rh_aggregate), hipMemcpyDeviceToHost, s->stream));
+    return s->sync();
 }
 
 int rh_store_fingerprints(rh_store *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     if (lo > hi || hi > s->n) return fail(RH_ERR_ARG, "bad rank range");
     if (hi > lo && !host_out) return fail(RH_ERR_ARG, "host_out NULL");
-    std::lock_guard<std::mutex> g(s->mu);
-    RH_HIP(hipSetDevice(s->device));
-    if (hi > lo) {
-        RH_HIP(hipMemcpyAsync(host_out, s->fps.p + lo * 32, (hi - lo) * 32, hipMemcpyDeviceToHost, s->stream));
-        RH_HIP(hipStreamSynchronize(s->stream));
-    }
-    return RH_OK;
+    RH_LOCK(s);
+    if (hi > lo)
+        RH_HIP(hipMemcpyAsync(host_out, s->fps[s->cur].p + lo * 32, (hi - lo) * 32, hipMemcpyDeviceToHost, s->stream));
+    return s->sync();
 }
 
-// Batched insert / overwrite / delete.  Host merge of the sorted batch into the rank-ordered
-// mirror, then a device rebuild (re-lift + re-sum).  Semantics follow FingerprintTreeMap::insert
-// (overwrite = new fp replaces old: the `new - old` delta of mutate.rs:31-41) and ::remove
-// (mutate.rs:93-154): the resulting aggregates equal a fold of lift over the final contents.
 int rh_store_apply(rh_store *s, const rh_columns *h, const uint8_t *ops, size_t m, uint64_t *n_new,
                    uint64_t *n_over, uint64_t *n_del) {
     if (!s || !h || (m && !ops)) return fail(RH_ERR_ARG, "NULL");
-    std::lock_guard<std::mutex> g(s->mu);
-    RH_HIP(hipSetDevice(s->device));
-    const rh_schema &sc = s->schema;
-    const size_t kr = s->krow, vr = s->vrow;
-    const uint8_t *bk = static_cast<const uint8_t *>(h->keys);
-    const uint8_t *bv = static_cast<const uint8_t *>(h->values);
-    bool any_insert = false;
-    for (size_t i = 0; i < m; i++) any_insert |= ops[i] == 0;
-    if (m && !bk) return fail(RH_ERR_ARG, "keys NULL");
-    if (any_insert && vr && !bv) return fail(RH_ERR_ARG, "values NULL");
-    if (any_insert && sc.record_kind == RH_REC_DATED && (!h->phys || !h->node || !h->logical))
-        return fail(RH_ERR_ARG, "DATED needs stamp columns");
-    // order the batch by key
-    std::vector<size_t> order(m);
-    for (size_t i = 0; i < m; i++) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return s->cmp_keys(bk + a * kr, bk + b * kr) < 0; });
-    for (size_t i = 1; i < m; i++)
-        if (s->cmp_keys(bk + order[i - 1] * kr, bk + order[i] * kr) == 0)
-            return fail(RH_ERR_ARG, "duplicate key within one batch");
-    const bool tags_out = s->has_tags || (h->tags != nullptr && sc.record_kind != RH_REC_PLAIN);
-    std::vector<uint8_t> nk, nv, nt;
-    std::vector<uint64_t> np, nn;
-    std::vector<uint32_t> nl;
-    nk.reserve((s->n + m) * kr);
-    nv.reserve((s->n + m) * vr);
-    const bool dated = sc.record_kind == RH_REC_DATED;
-    uint64_t c_new = 0, c_over = 0, c_del = 0;
-    auto push_old = [&](size_t i) {
-        nk.insert(nk.end(), &s->h_keys[i * kr], &s->h_keys[i * kr] + kr);
-        nv.insert(nv.end(), s->h_values.data() + i * vr, s->h_values.data() + (i + 1) * vr);
-        if (dated) { np.push_back(s->h_phys[i]); nn.push_back(s->h_node[i]); nl.push_back(s->h_logical[i]); }
-        if (tags_out) nt.push_back(s->has_tags ? s->h_tags[i] : 0);
-    };
-    auto push_new = [&](size_t j) {
-        nk.insert(nk.end(), bk + j * kr, bk + (j + 1) * kr);
-        if (vr) nv.insert(nv.end(), bv + j * vr, bv + (j + 1) * vr);
-        if (dated) { np.push_back(h->phys[j]); nn.push_back(h->node[j]); nl.push_back(h->logical[j]); }
-        if (tags_out) nt.push_back(h->tags ? h->tags[j] : 0);
-    };
-    size_t i = 0;
-    for (size_t t = 0; t < m; t++) {
-        const size_t j = order[t];
-        const uint8_t *key = bk + j * kr;
-        while (i < s->n && s->cmp_keys(&s->h_keys[i * kr], key) < 0) push_old(i++);
-        const bool present = i < s->n && s->cmp_keys(&s->h_keys[i * kr], key) == 0;
-        if (ops[j] == 0) {
-            push_new(j);
-            if (present) { c_over++; i++; } else c_new++;
-        } else {
-            if (present) { c_del++; i++; }
-        }
-    }
-    while (i < s->n) push_old(i++);
-    s->n = nk.size() / (kr ? kr : 1);
-    if (!kr) s->n = nv.size() / (vr ? vr : 1);
-    s->h_keys.swap(nk);
-    s->h_values.swap(nv);
-    s->h_phys.swap(np);
-    s->h_node.swap(nn);
-    s->h_logical.swap(nl);
-    s->h_tags.swap(nt);
-    s->has_tags = tags_out;
-    if (n_new) *n_new = c_new;
-    if (n_over) *n_over = c_over;
-    if (n_del) *n_del = c_del;
-    return s->rebuild();
+    RH_LOCK(s);
+    int rc;
+    if ((rc = s->staging.upload(s->schema, *h, m, s->stream)) || (rc = s->hops.ensure(m + 64))) return rc;
+    if (m) RH_HIP(hipMemcpyAsync(s->hops.p, ops, m, hipMemcpyHostToDevice, s->stream));
+    uint64_t c[3];
+    if ((rc = s->apply_device(s->staging.view(s->schema), s->hops.p, m, c))) return rc;
+    if (n_new) *n_new = c[0];
+    if (n_over) *n_over = c[1];
+    if (n_del) *n_del = c[2];
+    return RH_OK;
+}
+
+int rh_store_apply_device(rh_store *s, const rh_columns *dev_cols, const uint8_t *dev_ops, size_t m,
+                          uint64_t *n_new, uint64_t *n_over, uint64_t *n_del) {
+    if (!s) return fail(RH_ERR_ARG, "NULL");
+    int rc = check_cols(s->schema, dev_cols, m);
+    if (rc) return rc;
+    RH_LOCK(s);
+    uint64_t c[3];
+    if ((rc = s->apply_device(*dev_cols, dev_ops, m, c))) return rc;
+    if (n_new) *n_new = c[0];
+    if (n_over) *n_over = c[1];
+    if (n_del) *n_del = c[2];
+    return RH_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,81 @@
+// store_kernels.hpp -- interface between the store (rsos_hip_abi.hip) and its device kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "lift_kernels.hpp"
+
+namespace rh {
+
+// Growable device scratch buffers in numbered slots, reused across calls.  Growing a slot
+// drains `stream` first, so no in-flight kernel still reads the freed buffer.
+struct Scratch {
+    hipStream_t stream = nullptr;
+    struct Slot {
+        void *p = nullptr;
+        size_t bytes = 0;
+    };
+    std::vector<Slot> slots;
+    hipError_t err = hipSuccess;
+
+    void *get(size_t idx, size_t bytes) {
+        if (slots.size() <= idx) slots.resize(idx + 1);
+        Slot &s = slots[idx];
+        bytes = std::max<size_t>(bytes, 256);
+        if (s.bytes < bytes) {
+            if (s.p) {
+                (void)hipStreamSynchronize(stream);
+                (void)hipFree(s.p);
+            }
+            s.p = nullptr;
+            s.bytes = 0;
+            const size_t want = (bytes + (bytes >> 3) + 255) & ~size_t(255);  // +12.5% headroom
+            hipError_t e = hipMalloc(&s.p, want);
+            if (e != hipSuccess) {
+                err = e;
+                return nullptr;
+            }
+            s.bytes = want;
+        }
+        return s.p;
+    }
+    uint32_t *u32(int k, size_t n) { return static_cast<uint32_t *>(get(0 + k, n * 4)); }
+    uint64_t *u64(int k, size_t n) { return static_cast<uint64_t *>(get(16 + k, n * 8)); }
+    uint8_t *u8(int k, size_t n) { return static_cast<uint8_t *>(get(32 + k, n)); }
+    int32_t *i32(int k, size_t n) { return static_cast<int32_t *>(get(48 + k, n * 4)); }
+    void *bytes(size_t n) { return get(63, n); }
+    void release() {
+        (void)hipStreamSynchronize(stream);
+        for (auto &s : slots)
+            if (s.p) (void)hipFree(s.p);
+        slots.clear();
+    }
+};
+
+// Key-type-specialised device operations of the store.
+struct StoreKeyOps {
+    virtual ~StoreKeyOps() = default;
+    // sort a batch by key (LSD radix over u64 digits), gather keys / fingerprints / ops into key
+    // order; *dup |= 1 if two batch keys are equal
+    virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
+                                  Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *dup,
+                                  hipStream_t st) = 0;
+    // lower-bound rank of each query key (and whether it is present)
+    virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
+                              uint8_t *present, hipStream_t st) = 0;
+    // merge a key-sorted batch into (keys, fps) -> (okeys, ofps); counts = {new, overwritten, deleted}
+    virtual hipError_t merge(const uint8_t *keys, const uint8_t *fps, uint64_t n, const uint8_t *skeys,
+                             const uint8_t *sfps, const uint8_t *sops, uint64_t m, Scratch &s, uint8_t *okeys,
+                             uint8_t *ofps, uint64_t *counts, hipStream_t st) = 0;
+    virtual hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) = 0;
+    virtual hipError_t bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key, int lo_kind,
+                              const uint8_t *hi_key, int hi_kind, uint64_t *qlo, uint64_t *qhi, hipStream_t st) = 0;
+};
+
+// nullptr if the store does not support this key type
+StoreKeyOps *store_key_ops(int key_kind, int key_len);
+
+}  // namespace rh

@@ -55,15 +55,20 @@ SIGNATURES = [
     ("rh_store_create", C.c_int, [C.c_int, C.POINTER(Schema), C.POINTER(C.c_void_p)]),
     ("rh_store_destroy", C.c_int, [P]),
     ("rh_store_load", C.c_int, [P, C.POINTER(Columns), SZ]),
+    ("rh_store_load_device", C.c_int, [P, C.POINTER(Columns), SZ]),
     ("rh_store_len", C.c_int, [P, C.POINTER(C.c_uint64)]),
     ("rh_store_aggregate", C.c_int, [P, C.c_uint64, C.c_uint64, C.POINTER(Aggregate)]),
     ("rh_store_aggregates", C.c_int, [P, U64P, U64P, SZ, P]),
     ("rh_store_aggregate_keys", C.c_int, [P, C.c_int, VP, C.c_int, VP, C.POINTER(Aggregate)]),
     ("rh_store_rank", C.c_int, [P, VP, C.POINTER(C.c_uint64)]),
+    ("rh_store_ranks", C.c_int, [P, VP, SZ, U64P]),
+    ("rh_store_keys", C.c_int, [P, C.c_uint64, C.c_uint64, VP]),
     ("rh_store_select", C.c_int, [P, C.c_uint64, VP]),
     ("rh_store_fingerprints", C.c_int, [P, C.c_uint64, C.c_uint64, U8P]),
     ("rh_store_apply", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("rh_store_apply_device", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 ]
 
 _lib = None

@@ -9,9 +9,11 @@ Mirrors rsos/src/rsos_trait.rs:39-90 (method names, argument meaning, panics-as-
   enumerate(range)       -> (key, record index) pairs in key order
   insert(k, v) / delete(k)
 
-Records are held in rank order in HBM with their fingerprints and block / super-block sums;
-the key column stays on the host for rank/select.  Keys are fixed-width: bytes of
-schema.key_len for byte keys (memcmp order = Ord of [u8; L]), ints for u32/u64 keys.
+Keys and fingerprints are held in rank order in HBM with the block / super-block sums; rank,
+select and range bounds are answered on the device.  Record payloads are lifted on ingest and
+not kept on the device (the caller owns K and V, as the reference's map does).  Keys are
+fixed-width: bytes of schema.key_len for byte keys (memcmp order = Ord of [u8; L]), ints for
+u32/u64 keys.
 """
 from __future__ import annotations
 
@@ -55,7 +57,6 @@ class GpuFingerprintStore:
         h = C.c_void_p()
         A.check(A.lib().rh_store_create(device, C.byref(self._s), C.byref(h)), "rh_store_create")
         self._h = h
-        self._hold: Dict[str, np.ndarray] = {}
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -99,6 +100,25 @@ class GpuFingerprintStore:
         c, held = self._columns(cols)
         n = len(held["keys"]) if "keys" in held else len(held["values"])
         A.check(A.lib().rh_store_load(self._h, C.byref(c), n), "rh_store_load")
+
+    def load_bulk_device(self, cols) -> None:
+        """load_bulk from device (torch) columns already resident in HBM."""
+        from .device import _check_cols, _columns
+        n = _check_cols(self.schema, cols)
+        c = _columns(cols)
+        A.check(A.lib().rh_store_load_device(self._h, C.byref(c), n), "rh_store_load_device")
+
+    def apply_device(self, cols, ops=None) -> Tuple[int, int, int]:
+        """apply() with device (torch) columns / ops; returns (new, overwritten, deleted)."""
+        from .device import _check_cols, _columns
+        m = _check_cols(self.schema, cols)
+        if ops is not None and (ops.numel() != m or not ops.is_cuda):
+            raise ValueError("ops must be m device bytes")
+        c = _columns(cols)
+        a, b, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        A.check(A.lib().rh_store_apply_device(self._h, C.byref(c), None if ops is None else ops.data_ptr(), m,
+                                              C.byref(a), C.byref(b), C.byref(d)), "rh_store_apply_device")
+        return int(a.value), int(b.value), int(d.value)
 
     # ---- Rsos<K> -------------------------------------------------------------------------
     def size(self) -> int:
@@ -146,7 +166,7 @@ class GpuFingerprintStore:
         return self._key_out(buf.raw[: self.schema.key_row])
 
     def enumerate(self, rng: Optional[KeyRange] = None) -> Iterator[Tuple[Key, int]]:
-        """Keys in X ∩ range with their ranks, in key order."""
+        """Keys in X ∩ range with their ranks, in key order (Rsos::enumerate's key half)."""
         rng = rng or KeyRange.full()
         n = self.size()
         lo = 0 if rng.start is None else self.rank(rng.start)
@@ -155,8 +175,20 @@ class GpuFingerprintStore:
         hi = n if rng.end is None else self.rank(rng.end)
         if rng.end is not None and rng.end_kind == "included" and hi < n and self.select(hi) == rng.end:
             hi += 1
+        if hi <= lo:
+            return
+        kl = self.schema.key_row
+        buf = np.zeros((hi - lo) * kl, np.uint8)
+        A.check(A.lib().rh_store_keys(self._h, lo, hi, _np_ptr(buf)), "rh_store_keys")
         for r in range(lo, hi):
-            yield self.select(r), r
+            yield self._key_out(buf[(r - lo) * kl:(r - lo + 1) * kl].tobytes()), r
+
+    def ranks(self, keys: np.ndarray) -> np.ndarray:
+        """Rank of each of m keys (rows of key_len bytes) in one device search."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, self.schema.key_row)
+        out = np.zeros(k.shape[0], np.uint64)
+        A.check(A.lib().rh_store_ranks(self._h, _np_ptr(k), k.shape[0], _np_ptr(out)), "rh_store_ranks")
+        return out
 
     def fingerprints(self, lo: int = 0, hi: Optional[int] = None) -> np.ndarray:
         hi = self.size() if hi is None else hi

@@ -362,3 +362,102 @@ def test_full_size_config2_properties(gpu, oracle_lib):
     out = range_aggregates(fps, bs, ss, lo_t, hi_t).cpu().numpy()
     assert agg_int(out[0]) == want_root and int(out[0][4]) == n
     assert (agg_int(out[1]) + agg_int(out[2])) % M256 == want_root
+
+
+def test_store_device_batches_bytes16_dated(gpu, oracle_lib):
+    """Batched insert / overwrite / delete on the device merge path (16 B keys, dated records),
+    checked against a fold of the oracle's lift over the expected contents after each batch."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    from rsos_hip.synth import make_records, to_host
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 200_000
+    base = make_records(s, n, seed=5)
+    st = GpuFingerprintStore(s)
+    st.load_bulk_device(base)
+    hb = to_host(base)
+    content = {}  # key bytes -> record row (dict of numpy rows)
+
+    def rows(h, i):
+        return {k: h[k][i] for k in h}
+    for i in range(n):
+        content[hb["keys"][i].tobytes()] = rows(hb, i)
+    O = oracle_lib
+    sc = O.Schema(s.key_kind, s.key_len, s.value_kind, s.value_len, s.record_kind, 0)
+
+    def expected_root():
+        ks = sorted(content)
+        cols = {c: np.stack([content[k][c] for k in ks]) for c in hb}
+        fps = O.Records(sc, cols["keys"], cols["values"], cols["phys"], cols["logical"], cols["node"]).lift(threads=8)
+        return len(ks), sum(int.from_bytes(f.tobytes(), "little") for f in fps) % M256, ks
+
+    rng = np.random.default_rng(77)
+    for rnd in range(3):
+        m = 20_000
+        fresh = make_records(s, m, seed=100 + rnd)  # keys interleave with the stored ones
+        hf = to_host(fresh)
+        existing = list(content)
+        pick = rng.choice(len(existing), 6000, replace=False)
+        over_keys, del_keys = [existing[i] for i in pick[:4000]], [existing[i] for i in pick[4000:]]
+        # batch = fresh inserts + overwrites (new values/stamps) + deletes, shuffled
+        keys = np.concatenate([hf["keys"], np.frombuffer(b"".join(over_keys + del_keys), np.uint8).reshape(-1, 16)])
+        tot = len(keys)
+        vals = rng.integers(0, 256, (tot, 64), dtype=np.uint8)
+        phys = rng.integers(0, 2**62, tot, dtype=np.uint64)
+        logical = rng.integers(0, 2**31, tot, dtype=np.uint32)
+        node = rng.integers(0, 2**62, tot, dtype=np.uint64)
+        ops = np.zeros(tot, np.uint8)
+        ops[m + 4000:] = 1
+        perm = rng.permutation(tot)
+        keys, vals, phys, logical, node, ops = keys[perm], vals[perm], phys[perm], logical[perm], node[perm], ops[perm]
+        dev = {"keys": torch.from_numpy(keys.copy()).cuda(), "values": torch.from_numpy(vals.copy()).cuda(),
+               "phys": torch.from_numpy(phys.view(np.int64).copy()).cuda(),
+               "logical": torch.from_numpy(logical.view(np.int32).copy()).cuda(),
+               "node": torch.from_numpy(node.view(np.int64).copy()).cuda()}
+        exp_new = sum(1 for k in hf["keys"] if k.tobytes() not in content)
+        got = st.apply_device(dev, torch.from_numpy(ops).cuda())
+        assert got == (exp_new, 4000 + (m - exp_new), 2000)
+        for j in range(tot):
+            k = keys[j].tobytes()
+            if ops[j]:
+                content.pop(k, None)
+            else:
+                content[k] = {"keys": keys[j], "values": vals[j], "phys": phys[j], "logical": logical[j],
+                              "node": node[j]}
+        size, root, ks = expected_root()
+        agg = st.aggregate()
+        assert agg.size == size == st.size()
+        assert agg.fingerprint.to_int() == root
+        # rank / select / enumerate against the expected key order
+        for r in rng.integers(0, size, 20):
+            assert st.select(int(r)) == ks[r] and st.rank(ks[r]) == r
+        lo_k, hi_k = ks[1000], ks[1100]
+        assert [k for k, _ in st.enumerate(KeyRange(lo_k, hi_k))] == ks[1000:1100]
+    st.close()
+
+
+def test_store_rejects_bad_batches_unchanged(gpu):
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema, RsosHipError
+    from rsos_hip.synth import make_records
+    s = RecordSchema.plain("bytes16", "bytes64")
+    st = GpuFingerprintStore(s)
+    base = make_records(s, 5000, seed=1)
+    st.load_bulk_device(base)
+    before = st.aggregate()
+    batch = make_records(s, 10, seed=2)
+    batch["keys"][3] = batch["keys"][7]  # duplicate within one batch
+    with pytest.raises(RsosHipError):
+        st.apply_device(batch)
+    assert st.aggregate() == before
+    # deleting absent keys is a no-op; an empty batch is a no-op
+    absent = make_records(s, 10, seed=3)
+    assert st.apply_device(absent, torch.ones(10, dtype=torch.uint8, device="cuda")) == (0, 0, 0)
+    assert st.aggregate() == before
+    # unsorted load is refused
+    bad = make_records(s, 100, seed=4)
+    bad["keys"] = bad["keys"].flip(0).contiguous()
+    with pytest.raises(RsosHipError):
+        st.load_bulk_device(bad)
+    st.close()

@@ -297,15 +297,18 @@ struct DevColumns {
         const size_t kr = key_row(s), vr = value_row(s);
         if ((rc = keys.ensure(n * kr + 16))) return rc;
         if ((rc = values.ensure(n * vr + 16))) return rc;
-        if (n && kr) RH_HIP(hipMemcpyAsync(keys.p, h.keys, n * kr, hipMemcpyHostToDevice, st));
-        if (n && vr) RH_HIP(hipMemcpyAsync(values.p, h.values, n * vr, hipMemcpyHostToDevice, st));
+        // a NULL host column (e.g. the values of a delete-only batch) is zero-filled
+        auto put = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+            if (!bytes) return hipSuccess;
+            return src ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) : hipMemsetAsync(dst, 0, bytes, st);
+        };
+        RH_HIP(put(keys.p, h.keys, n * kr));
+        RH_HIP(put(values.p, h.values, n * vr));
         if (s.record_kind == RH_REC_DATED) {
             if ((rc = phys.ensure(n)) || (rc = node.ensure(n)) || (rc = logical.ensure(n))) return rc;
-            if (n) {
-                RH_HIP(hipMemcpyAsync(phys.p, h.phys, n * 8, hipMemcpyHostToDevice, st));
-                RH_HIP(hipMemcpyAsync(node.p, h.node, n * 8, hipMemcpyHostToDevice, st));
-                RH_HIP(hipMemcpyAsync(logical.p, h.logical, n * 4, hipMemcpyHostToDevice, st));
-            }
+            RH_HIP(put(phys.p, h.phys, n * 8));
+            RH_HIP(put(node.p, h.node, n * 8));
+            RH_HIP(put(logical.p, h.logical, n * 4));
         }
         has_tags = h.tags != nullptr && s.record_kind != RH_REC_PLAIN;
         if (has_tags) {

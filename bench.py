@@ -41,6 +41,8 @@ CONFIGS = {
                 "BASELINE configs[3] per-GPU shard: 100M records over 8 GPUs, 16 B key / 64 B value"),
     "bench_u32": ("u32", "u32", "plain", 10_000_000,
                   "benches/bench.rs fill shape: FingerprintTreeMap<u32,u32>"),
+    "config5": ("bytes16", "bytes64", "dated", 100_000_000,
+                "BASELINE configs[4]: 1M random inserts per batch into a 100M-record resident map"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec)
 
@@ -54,7 +56,8 @@ def parse():
     p.add_argument("--records", type=int, default=0, help="override records per GPU")
     p.add_argument("--ranges", type=int, default=16)
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
-    p.add_argument("--cpu-sample", type=int, default=2_000_000, help="records in the CPU baseline sample")
+    p.add_argument("--cpu-sample", type=int, default=0, help="records in the CPU baseline sample (0: the whole shard)")
+    p.add_argument("--batch", type=int, default=1_000_000, help="config5: records per update batch")
     p.add_argument("--e2e", action="store_true", help="also time host->device->host end to end (DESIGN.md)")
     p.add_argument("--check", type=int, default=1, help="oracle spot-check of a sample before timing")
     return p.parse_args()
@@ -67,8 +70,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BENCH_BACKEND", "nccl")  # gloo: functional rehearsal only
+        ngpu = torch.cuda.device_count()
+        torch.cuda.set_device(local % max(ngpu, 1))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -77,7 +85,10 @@ def main():
     import rsos_hip
     from rsos_hip import RecordSchema, lift_records, range_aggregates, reduce_blocks, combine_aggregates
     from rsos_hip.synth import make_records
+    from rsos_hip.shard import equal_count_ranges, gather, local_ranges
 
+    if args.config == "config5":
+        return incremental(args, world, rank, dev, dist)
     kname, vname, kind, n_default, desc = CONFIGS[args.config]
     n = args.records or n_default
     schema = getattr(RecordSchema, kind)(kname, vname)
@@ -86,20 +97,19 @@ def main():
     hbm_bytes = read_bytes + 32                          # + fingerprint write
 
     # this rank's shard of the globally sorted key space: global rows [rank*n, (rank+1)*n)
-    cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n)
+    cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
     base = rank * n
     total = n * world
     R = args.ranges
-    glo = [total * j // R for j in range(R)]
-    ghi = [total * (j + 1) // R for j in range(R)]
-    lo = torch.tensor([min(max(g - base, 0), n) for g in glo], dtype=torch.int64, device=dev)
-    hi = torch.tensor([min(max(g - base, 0), n) for g in ghi], dtype=torch.int64, device=dev)
+    lo_l, hi_l = local_ranges(equal_count_ranges(total, R), base, n)
+    lo = torch.tensor(lo_l, dtype=torch.int64, device=dev)
+    hi = torch.tensor(hi_l, dtype=torch.int64, device=dev)
 
     nb = (n + 255) // 256
     fps = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     bs = torch.empty((nb, 32), dtype=torch.uint8, device=dev)
     out = torch.empty((R, 5), dtype=torch.int64, device=dev)
-    gathered = torch.empty((world, R, 5), dtype=torch.int64, device=dev)
+    gathered = torch.empty((world, R, 5), dtype=torch.int64, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream()
 
     # correctness gate before timing: sampled rows vs the oracle (rank 0)
@@ -121,8 +131,7 @@ def main():
         ss = reduce_blocks(bs)
         range_aggregates(fps, bs, ss, lo, hi, out=out)
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, out)
-            return combine_aggregates(gathered)
+            return combine_aggregates(gather(dist, out, gathered))
         return out
 
     for _ in range(args.warmup):
@@ -187,6 +196,64 @@ def main():
         dist.destroy_process_group()
 
 
+def incremental(args, world, rank, dev, dist):
+    """config5: GPU-resident store of N records; each step applies one batch of `--batch` random
+    records (insert-or-overwrite; fresh random 128-bit keys are essentially all new) through the
+    device sort / search / merge / re-sum path.  Timed: apply_device, which ends synchronised."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.synth import make_records
+    kname, vname, kind, n_default, desc = CONFIGS["config5"]
+    n = args.records or n_default
+    schema = getattr(RecordSchema, kind)(kname, vname)
+    st = GpuFingerprintStore(schema, device=dev.index)
+    base = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
+    t0 = time.perf_counter()
+    st.load_bulk_device(base)
+    load_s = time.perf_counter() - t0
+    del base
+    torch.cuda.empty_cache()
+    m = args.batch
+    batches = [make_records(schema, m, seed=1000 * (rank + 1) + k, device=dev, random_keys=True)
+               for k in range(args.warmup + args.steps)]
+    for k in range(args.warmup):
+        st.apply_device(batches[k])
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    counts = [0, 0, 0]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        c = st.apply_device(batches[args.warmup + k])
+        counts = [a + b for a, b in zip(counts, c)]
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    root = st.aggregate()
+    if rank == 0:
+        recs = m * args.steps * world
+        line = {
+            "metric": "incremental update: batched inserts into a GPU-resident map (M records/s)",
+            "value": round(recs / elapsed / 1e6, 2), "unit": "M records/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded): sorted resident set + uniformly random update keys",
+            "config": {"workload": desc, "resident_records_per_gpu": n, "batch": m,
+                       "parallelism": f"key-range shards x{world}"},
+            "batch_counts": {"new": counts[0], "overwritten": counts[1], "deleted": counts[2]},
+            "final_size": root.size, "bulk_load_s": round(load_s, 3),
+        }
+        print(json.dumps(line), flush=True)
+    st.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def spot_check(schema, cols, n):
     """Lift a few thousand rows and compare with the C oracle (test infrastructure)."""
     import numpy as np
@@ -219,7 +286,8 @@ def cpu_baseline(schema, cols, sample):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from rsos_hip.synth import to_host
-    m = min(sample, next(iter(cols.values())).shape[0])
+    m = next(iter(cols.values())).shape[0]
+    m = min(sample, m) if sample else m
     h = to_host(cols, 0, m)
     sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
     recs = O.Records(sc, h["keys"], h.get("values"), h.get("phys"), h.get("logical"), h.get("node"), h.get("tags"))

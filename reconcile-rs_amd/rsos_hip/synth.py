@@ -27,7 +27,13 @@ def _rand_bytes(gen: torch.Generator, shape, device) -> torch.Tensor:
 
 
 def make_records(schema: RecordSchema, n: int, seed: int = 42, device="cuda",
-                 tombstone_fraction: float = 0.0, first_index: int = 0) -> Dict[str, torch.Tensor]:
+                 tombstone_fraction: float = 0.0, first_index: int = 0,
+                 random_keys: bool = False, key_space: int = 0) -> Dict[str, torch.Tensor]:
+    """Rows [first_index, first_index + n) of a key-sorted set of `key_space` records
+    (default first_index + n) whose keys spread evenly over the whole key space: row i's
+    first 8 key bytes are the big-endian u64 i * stride + r, r < stride = 2^64 / key_space.
+    random_keys: uniformly random keys instead (unsorted; update batches that land anywhere
+    in an existing key range)."""
     dev = torch.device(device)
     gen = torch.Generator(device=dev)
     gen.manual_seed(seed)
@@ -36,12 +42,14 @@ def make_records(schema: RecordSchema, n: int, seed: int = 42, device="cuda",
     if schema.key_kind == A.KEY_BYTES:
         kl = schema.key_len
         keys = _rand_bytes(gen, (n, kl), dev).clone()
-        r24 = torch.randint(0, 1 << 24, (n,), generator=gen, device=dev, dtype=torch.int64)
-        head = (idx << 24) | r24
+        space = max(key_space or (first_index + n), 2)
+        stride = min((1 << 64) // space, (1 << 63) - 1)
+        r = torch.randint(0, stride, (n,), generator=gen, device=dev, dtype=torch.int64)
+        head = idx * stride + r  # wraps in int64; the bit pattern is the unsigned value
         # big-endian bytes of head into keys[:, :8]
         shifts = torch.arange(56, -8, -8, device=dev, dtype=torch.int64)
-        if kl >= 8:
-            keys[:, :8] = ((head[:, None] >> shifts[None, :]) & 0xFF).to(torch.uint8)
+        if kl >= 8 and not random_keys:
+            keys[:, :8] = ((head[:, None] >> shifts[None, :]) & 0xFF).to(torch.uint8)  # arithmetic >> ok: & 0xFF
         cols["keys"] = keys.contiguous()
     elif schema.key_kind == A.KEY_U64:
         r = torch.randint(0, 1 << 20, (n,), generator=gen, device=dev, dtype=torch.int64)

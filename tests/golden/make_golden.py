@@ -122,9 +122,11 @@ SHAPES = [
     ("b16_b1024_projection", "bytes16", "bytes1024", O.REC_PROJECTION, 0.0, 8),
     ("b16_u64_dated", "bytes16", "u64", O.REC_DATED, 0.0, 8),
     ("b32_b64_dated", "bytes32", "bytes64", O.REC_DATED, 0.25, 8),
+    ("unit_b64_dated", "unit", "bytes64", O.REC_DATED, 0.25, 8),   # digest(&Entry): version_hash
+    ("unit_u32_plain", "unit", "u32", O.REC_PLAIN, 0.0, 8),        # digest(&u32)
 ]
 
-KIND = {"u32": (O.KEY_U32, 4), "u64": (O.KEY_U64, 8)}
+KIND = {"u32": (O.KEY_U32, 4), "u64": (O.KEY_U64, 8), "unit": (O.KEY_UNIT, 0)}
 
 
 def _kind(name):
@@ -142,6 +144,8 @@ def _pyvalue(kind, raw: bytes):
 
 
 def _pykey(kind, raw: bytes):
+    if kind == "unit":
+        return P.Unit()  # digest(v) == lift(&(), v), rsos/src/fingerprint.rs:288-292
     if kind in ("u32", "u64"):
         return _pyvalue(kind, raw)
     return P.Seq(tuple(P.U8(b) for b in raw))  # [u8; L] is a serde tuple: u64 count then bytes

@@ -14,3 +14,6 @@ step stats_$CONFIG rocprofv3 --kernel-trace --stats --output-format csv -d gpuru
 step fetch_$CONFIG rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_lift --output-format csv -d gpurun_out/fetch_$CONFIG -o run -- $B
 step write_$CONFIG rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_lift --output-format csv -d gpurun_out/write_$CONFIG -o run -- $B
 python3 scripts/pmc_traffic.py gpurun_out/fetch_$CONFIG/run_counter_collection.csv gpurun_out/write_$CONFIG/run_counter_collection.csv $CONFIG $RECORDS gpurun_out/traffic_$CONFIG.json
+# VALU instruction counts and cycles of the lift kernel (for the VALU roofline)
+step valu_$CONFIG rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex k_lift --output-format csv -d gpurun_out/valu_$CONFIG -o run -- $B
+python3 scripts/pmc_valu.py gpurun_out/valu_$CONFIG/run_counter_collection.csv gpurun_out/stats_$CONFIG/run_kernel_stats.csv $CONFIG $RECORDS gpurun_out/valu_$CONFIG.json

@@ -185,8 +185,16 @@ __device__ __forceinline__ void block_sum_fps256(const uint32_t h[8], SumTile &t
     const uint4 a = *reinterpret_cast<const uint4 *>(&t.limb[l][s * 8]);
     const uint4 b = *reinterpret_cast<const uint4 *>(&t.limb[l][s * 8 + 4]);
     uint64_t p = (uint64_t)a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) p += shfl_xor_u64(p, m);
+    // butterfly over the 32 lanes of this half-wave: ds_swizzle in bit mode
+    // (and_mask 0x1f, xor_mask m) needs no per-lane address arithmetic
+#define RH_SWZ(m)                                                                               \
+    {                                                                                           \
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)p, ((m) << 10) | 0x1f);        \
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(p >> 32), ((m) << 10) | 0x1f); \
+        p += ((uint64_t)hi << 32) | lo;                                                         \
+    }
+    RH_SWZ(16) RH_SWZ(8) RH_SWZ(4) RH_SWZ(2) RH_SWZ(1)
+#undef RH_SWZ
     if (s == 0) t.total[l] = p;
     __syncthreads();
     if (tid == 0) {

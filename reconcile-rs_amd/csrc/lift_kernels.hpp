@@ -80,8 +80,8 @@ __device__ __forceinline__ void ldw(const uint8_t *p, uint32_t *out) {
 }
 
 // key encoding words: u32 / u64 raw LE; bytes -> [len lo, len hi, bytes...]
-template <int KK, int KL>
-__device__ __forceinline__ void load_key(const uint8_t *keys, uint64_t i, uint32_t *kw) {
+template <int KK, int KL, class I = uint64_t>
+__device__ __forceinline__ void load_key(const uint8_t *keys, I i, uint32_t *kw) {
     if constexpr (KK == KEY_U32) {
         kw[0] = reinterpret_cast<const uint32_t *>(keys)[i];
     } else if constexpr (KK == KEY_U64) {
@@ -90,12 +90,13 @@ __device__ __forceinline__ void load_key(const uint8_t *keys, uint64_t i, uint32
     } else if constexpr (KK == KEY_BYTES) {
         kw[0] = (uint32_t)KL;
         kw[1] = 0;
-        ldw<KL / 4, cmin(16, lowbit(KL))>(keys + i * (uint64_t)KL, kw + 2);
+        ldw<KL / 4, cmin(16, lowbit(KL))>(keys + i * (I)KL, kw + 2);
     }
 }
 
 // Timestamp{hlc{physical u64, logical u32}, node_id u64}: 5 words (clock.rs:143-181)
-__device__ __forceinline__ void load_stamp(const DevCols &c, uint64_t i, uint32_t *sw) {
+template <class I = uint64_t>
+__device__ __forceinline__ void load_stamp(const DevCols &c, I i, uint32_t *sw) {
     uint64_t ph = c.phys[i], nd = c.node[i];
     sw[0] = (uint32_t)ph; sw[1] = (uint32_t)(ph >> 32);
     sw[2] = c.logical[i];
@@ -262,8 +263,9 @@ __device__ __forceinline__ void hash_present(const uint32_t *pw, const uint8_t *
     }
 }
 
-__device__ __forceinline__ void store_fp(uint8_t *fps, uint64_t i, const uint32_t h[8]) {
-    uint4 *o = reinterpret_cast<uint4 *>(fps + 32 * i);
+template <class I = uint64_t>
+__device__ __forceinline__ void store_fp(uint8_t *fps, I i, const uint32_t h[8]) {
+    uint4 *o = reinterpret_cast<uint4 *>(fps + (I)32 * i);
     o[0] = make_uint4(h[0], h[1], h[2], h[3]);
     o[1] = make_uint4(h[4], h[5], h[6], h[7]);
 }
@@ -307,17 +309,28 @@ __global__ __launch_bounds__(LIFT_THREADS) void k_lift(DevCols c, uint64_t n, ui
     uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t h2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (valid) {
+        // Column pointers rebased to this block in scalar registers, so every per-lane
+        // address is a 32-bit offset (global_load ... saddr): no 64-bit VALU address math.
+        const uint64_t b0 = (uint64_t)blockIdx.x * LIFT_THREADS;
+        const uint32_t t = threadIdx.x;
+        DevCols cb;
+        cb.keys = c.keys + b0 * L::KEY_ROW;
+        cb.phys = c.phys + b0;
+        cb.logical = c.logical + b0;
+        cb.node = c.node + b0;
+        cb.tags = c.tags + b0;
+        cb.values = c.values + b0 * L::VAL_ROW;
         uint32_t kw[L::KEY_ENC / 4 > 0 ? L::KEY_ENC / 4 : 1];
         uint32_t sw[5];
-        load_key<KK, KL>(c.keys, i, kw);
-        if constexpr (RK == REC_DATED) load_stamp(c, i, sw);
-        const bool tomb = TAGS ? (c.tags[i] != 0) : false;
-        const uint8_t *vrow = c.values + i * (uint64_t)L::VAL_ROW;
+        load_key<KK, KL>(cb.keys, t, kw);
+        if constexpr (RK == REC_DATED) load_stamp(cb, t, sw);
+        const bool tomb = TAGS ? (cb.tags[t] != 0) : false;
+        const uint8_t *vrow = cb.values + t * (uint32_t)L::VAL_ROW;
         lift_record<KK, KL, VK, VL, RK>(kw, sw, tomb, vrow, h);
-        store_fp(fps, i, h);
+        store_fp(fps + b0 * 32, t, h);
         if constexpr (DUAL) {
             lift_record<KK, KL, VK, VL, REC_PROJECTION>(kw, sw, tomb, vrow, h2);
-            store_fp(fps2, i, h2);
+            store_fp(fps2 + b0 * 32, t, h2);
         }
     }
     if (bsums) {

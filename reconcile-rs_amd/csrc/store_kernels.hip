@@ -118,45 +118,68 @@ __global__ void k_classify(const uint8_t *sops, const uint8_t *present, uint64_t
     del[j] = (isdel && p) ? 1u : 0u;
 }
 
-// c[r] += 1 per insert before old element r; c[r+1] -= 1 and gone[r] = 1 per delete of old r
-__global__ void k_mark(const uint32_t *rank, const uint32_t *ins, const uint32_t *del, uint64_t m, int32_t *c,
-                       uint8_t *gone) {
+// compact the ranks of inserts and deletes (both come out sorted: the batch is key-sorted)
+__global__ void k_compact(const uint32_t *rank, const uint32_t *ins, const uint32_t *del, const uint32_t *cum_ins,
+                          const uint32_t *cum_del, uint64_t m, uint32_t *ins_rank, uint32_t *del_rank) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
-    if (ins[j]) atomicAdd(&c[rank[j]], 1);
-    if (del[j]) {
-        gone[rank[j]] = 1;
-        atomicAdd(&c[rank[j] + 1], -1);
+    if (ins[j]) ins_rank[cum_ins[j]] = rank[j];
+    if (del[j]) del_rank[cum_del[j]] = rank[j];
+}
+
+__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t *a, uint64_t lo, uint64_t hi, uint64_t x) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Survivors move to i + #inserts(rank <= i) - #deletes(rank < i); deleted rows are skipped.
+// One workgroup covers MOVE_TILE consecutive rows: one lane finds the slice of the (sorted)
+// insert / delete rank lists that falls inside the tile, then every row binary-searches only
+// that slice -- no n-sized scratch arrays, no n-sized scan.
+constexpr int MOVE_TILE = 1024;
+template <int KK, int KL>
+__global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const uint8_t *fps, uint64_t n,
+                                                    const uint32_t *ins_rank, const uint32_t *del_rank,
+                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *ofps) {
+    __shared__ uint64_t bounds[4];
+    const uint64_t i0 = (uint64_t)blockIdx.x * MOVE_TILE;
+    if (threadIdx.x == 0) {
+        const uint64_t a = counts[0], d = counts[2];  // list lengths: #inserts, #deletes
+        bounds[0] = lower_bound_u32(ins_rank, 0, a, i0);              // inserts with rank < i0
+        bounds[1] = lower_bound_u32(ins_rank, 0, a, i0 + MOVE_TILE);  // ... < tile end
+        bounds[2] = lower_bound_u32(del_rank, 0, d, i0);
+        bounds[3] = lower_bound_u32(del_rank, 0, d, i0 + MOVE_TILE);
+    }
+    __syncthreads();
+    const uint64_t ia = bounds[0], ib = bounds[1], da = bounds[2], db = bounds[3];
+#pragma unroll
+    for (int k = 0; k < MOVE_TILE / 256; k++) {
+        const uint64_t i = i0 + threadIdx.x + 256 * k;
+        if (i >= n) break;
+        const uint64_t ins_le = lower_bound_u32(ins_rank, ia, ib, i + 1);  // rank <= i
+        const uint64_t del_lt = lower_bound_u32(del_rank, da, db, i);      // rank < i
+        if (del_lt < db && del_rank[del_lt] == i) continue;                 // deleted
+        const uint64_t pos = i + ins_le - del_lt;
+        copy_key<KK, KL>(okeys + pos * KL, keys + i * KL);
+        copy_fp(ofps + 32 * pos, fps + 32 * i);
     }
 }
 
-// survivors: new position = i + S[i] (S = inclusive prefix of c)
-template <int KK, int KL>
-__global__ void k_move(const uint8_t *keys, const uint8_t *fps, const uint8_t *gone, const int32_t *S, uint64_t n,
-                       uint8_t *okeys, uint8_t *ofps) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || gone[i]) return;
-    const uint64_t pos = (uint64_t)((int64_t)i + S[i]);
-    copy_key<KK, KL>(okeys + pos * KL, keys + i * KL);
-    copy_fp(ofps + 32 * pos, fps + 32 * i);
-}
-
-// inserts at r + (#inserts before) - (#deletes before); overwrites replace the fingerprint of
-// their surviving element at r + S[r]
+// inserts and overwrites land at r + (#inserts before j) - (#deletes before j): for an insert
+// that is its slot; for an overwrite it is where its surviving element moved (the inserts with
+// rank <= r and the deletes with rank < r are exactly the batch entries before j in key order)
 template <int KK, int KL>
 __global__ void k_scatter(const uint8_t *skeys, const uint8_t *sfps, const uint8_t *present, const uint8_t *sops,
-                          const uint32_t *rank, const uint32_t *cum_ins, const uint32_t *cum_del, const int32_t *S,
-                          uint64_t m, uint8_t *okeys, uint8_t *ofps) {
+                          const uint32_t *rank, const uint32_t *cum_ins, const uint32_t *cum_del, uint64_t m,
+                          uint8_t *okeys, uint8_t *ofps) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m || sops[j] != 0) return;
-    const uint64_t r = rank[j];
-    uint64_t pos;
-    if (present[j]) {
-        pos = (uint64_t)((int64_t)r + S[r]);
-    } else {
-        pos = r + cum_ins[j] - cum_del[j];
-        copy_key<KK, KL>(okeys + pos * KL, skeys + j * KL);
-    }
+    const uint64_t pos = (uint64_t)rank[j] + cum_ins[j] - cum_del[j];
+    if (!present[j]) copy_key<KK, KL>(okeys + pos * KL, skeys + j * KL);
     copy_fp(ofps + 32 * pos, sfps + 32 * j);
 }
 
@@ -252,9 +275,9 @@ struct KeyOps final : StoreKeyOps {
                      hipStream_t st) override {
         hipError_t e;
         uint32_t *rank = s.u32(2, m), *ins = s.u32(3, m), *del = s.u32(4, m);
-        uint32_t *cins = s.u32(5, m), *cdel = s.u32(6, m);
-        uint8_t *present = s.u8(0, m), *gone = s.u8(1, n + 1);
-        int32_t *c = s.i32(0, n + 2);
+        uint32_t *cins = s.u32(5, m), *cdel = s.u32(6, m), *ins_rank = s.u32(7, m), *del_rank = s.u32(8, m);
+        uint8_t *present = s.u8(0, m);
+        if (s.err) return s.err;
         if ((e = search(keys, n, skeys, m, rank, present, st))) return e;
         hipLaunchKernelGGL(k_classify, g1(m), dim3(256), 0, st, sops, present, m, ins, del);
         size_t tb = 0;
@@ -262,17 +285,16 @@ struct KeyOps final : StoreKeyOps {
         void *tmp = s.bytes(tb);
         if ((e = rocprim::exclusive_scan(tmp, tb, ins, cins, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
         if ((e = rocprim::exclusive_scan(tmp, tb, del, cdel, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
-        if ((e = hipMemsetAsync(c, 0, (n + 2) * sizeof(int32_t), st))) return e;
-        if ((e = hipMemsetAsync(gone, 0, n + 1, st))) return e;
-        hipLaunchKernelGGL(k_mark, g1(m), dim3(256), 0, st, rank, ins, del, m, c, gone);
-        tb = 0;
-        if ((e = rocprim::inclusive_scan(nullptr, tb, c, c, n + 1, rocprim::plus<int32_t>(), st))) return e;
-        tmp = s.bytes(tb);
-        if ((e = rocprim::inclusive_scan(tmp, tb, c, c, n + 1, rocprim::plus<int32_t>(), st))) return e;
-        if (n) hipLaunchKernelGGL((k_move<KK, KL>), g1(n), dim3(256), 0, st, keys, fps, gone, c, n, okeys, ofps);
-        hipLaunchKernelGGL((k_scatter<KK, KL>), g1(m), dim3(256), 0, st, skeys, sfps, present, sops, rank, cins, cdel, c,
-                           m, okeys, ofps);
+        hipLaunchKernelGGL(k_compact, g1(m), dim3(256), 0, st, rank, ins, del, cins, cdel, m, ins_rank, del_rank);
+        // totals of inserts / deletes (counts[0], counts[2]) are read by the tile kernel on the device
         hipLaunchKernelGGL(k_counts, dim3(1), dim3(64), 0, st, ins, del, cins, cdel, sops, present, m, counts);
+        if (n) {
+            const uint64_t tiles = (n + MOVE_TILE - 1) / MOVE_TILE;
+            hipLaunchKernelGGL((k_move_tiles<KK, KL>), dim3((uint32_t)tiles), dim3(256), 0, st, keys, fps, n, ins_rank,
+                               del_rank, counts, okeys, ofps);
+        }
+        hipLaunchKernelGGL((k_scatter<KK, KL>), g1(m), dim3(256), 0, st, skeys, sfps, present, sops, rank, cins, cdel,
+                           m, okeys, ofps);
         if ((e = hipMemsetAsync(counts + 1, 0, 8, st))) return e;
         hipLaunchKernelGGL(k_count_ovr, g1(m), dim3(256), 0, st, sops, present, m,
                            reinterpret_cast<unsigned long long *>(counts + 1));

@@ -55,8 +55,16 @@ __device__ __forceinline__ uint64_t key_digit(const uint8_t *k, int d) {
 
 template <int KK, int KL>
 __device__ __forceinline__ void copy_key(uint8_t *dst, const uint8_t *src) {
+    if constexpr (KL % 16 == 0) {
 #pragma unroll
-    for (int o = 0; o < KL; o += 4) *reinterpret_cast<uint32_t *>(dst + o) = *reinterpret_cast<const uint32_t *>(src + o);
+        for (int o = 0; o < KL; o += 16) *reinterpret_cast<uint4 *>(dst + o) = *reinterpret_cast<const uint4 *>(src + o);
+    } else if constexpr (KL % 8 == 0) {
+#pragma unroll
+        for (int o = 0; o < KL; o += 8) *reinterpret_cast<uint2 *>(dst + o) = *reinterpret_cast<const uint2 *>(src + o);
+    } else {
+#pragma unroll
+        for (int o = 0; o < KL; o += 4) *reinterpret_cast<uint32_t *>(dst + o) = *reinterpret_cast<const uint32_t *>(src + o);
+    }
 }
 
 __device__ __forceinline__ void copy_fp(uint8_t *dst, const uint8_t *src) {

@@ -203,6 +203,14 @@ int rh_store_apply(rh_store *store, const rh_columns *host_cols, const uint8_t *
 int rh_store_apply_device(rh_store *store, const rh_columns *dev_cols, const uint8_t *dev_ops, size_t n,
                           uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted);
 
+/* LSM maintenance.  A batch merges into a sorted signed-delta run (O(batch + delta)); the delta
+ * run merges into the base run when it exceeds max(base / divisor, min_rows) rows (default
+ * 8, 65536), and before rank-order queries (select, rank-range aggregates, key / fingerprint
+ * dumps).  Results never depend on the policy, only timings do.                            */
+int rh_store_compact(rh_store *store);
+int rh_store_set_compaction(rh_store *store, uint64_t divisor, uint64_t min_rows);
+int rh_store_stats(const rh_store *store, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions);
+
 #ifdef __cplusplus
 }
 #endif

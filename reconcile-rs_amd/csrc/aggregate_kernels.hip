@@ -93,27 +93,29 @@ __global__ __launch_bounds__(256) void k_lift_encoded(const uint8_t *bytes, cons
 
 // ---- reductions ------------------------------------------------------------------------------
 
-__device__ __forceinline__ void load_fp(const uint8_t *src, uint64_t i, uint32_t f[8]) {
-    const uint4 *p = reinterpret_cast<const uint4 *>(src + 32 * i);
+// fingerprint i of an array whose entries are `stride` bytes apart (32 for plain fingerprint
+// arrays; the store's delta records carry their 32-byte contribution first, stride 80)
+__device__ __forceinline__ void load_fp(const uint8_t *src, uint64_t i, uint32_t f[8], uint32_t stride = 32) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(src + (uint64_t)stride * i);
     uint4 a = p[0], b = p[1];
     f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
     f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
-__global__ __launch_bounds__(256) void k_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out) {
+__global__ __launch_bounds__(256) void k_reduce(const uint8_t *in, uint32_t stride, uint64_t n_in, uint8_t *out) {
     __shared__ SumTile tile;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (i < n_in) load_fp(in, i, h);
+    if (i < n_in) load_fp(in, i, h, stride);
     uint32_t f[8];
     block_sum_fps256(h, tile, f);
     if (threadIdx.x == 0) store_sum(out, blockIdx.x, f);
 }
 
-__device__ __forceinline__ void acc_span(Acc &a, const uint8_t *src, uint64_t lo, uint64_t hi) {
+__device__ __forceinline__ void acc_span(Acc &a, const uint8_t *src, uint64_t lo, uint64_t hi, uint32_t stride = 32) {
     for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         uint32_t f[8];
-        load_fp(src, i, f);
+        load_fp(src, i, f, stride);
         acc_add_fp(a, f);
     }
 }
@@ -121,7 +123,7 @@ __device__ __forceinline__ void acc_span(Acc &a, const uint8_t *src, uint64_t lo
 // One workgroup per query.  [lo, hi) = head rows + whole blocks + tail rows, the whole blocks
 // = head blocks + whole super-blocks + tail blocks.  Each thread sums at most a few hundred
 // entries into carry-save u64 limbs, then one block reduction.
-__global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, const uint8_t *bsums,
+__global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
                                                      const uint8_t *ssums, uint64_t n,
                                                      const uint64_t *qlo, const uint64_t *qhi,
                                                      uint64_t r, uint64_t *out) {
@@ -136,10 +138,10 @@ __global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, const u
     const uint64_t B = 256, S = 65536;
     const uint64_t b1 = (lo + B - 1) / B, b2 = hi / B;  // whole blocks [b1, b2)
     if (b1 >= b2 || bsums == nullptr) {
-        acc_span(a, fps, lo, hi);
+        acc_span(a, fps, lo, hi, stride);
     } else {
-        acc_span(a, fps, lo, b1 * B);
-        acc_span(a, fps, b2 * B, hi);
+        acc_span(a, fps, lo, b1 * B, stride);
+        acc_span(a, fps, b2 * B, hi, stride);
         const uint64_t s1 = (b1 + B - 1) / B, s2 = b2 / B;  // whole super-blocks [s1, s2)
         if (s1 >= s2 || ssums == nullptr) {
             acc_span(a, bsums, b1, b2);
@@ -197,18 +199,18 @@ hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint6
     return hipGetLastError();
 }
 
-hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st) {
+hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st, uint32_t stride) {
     if (n_in == 0) return hipSuccess;
     const uint64_t g = (n_in + 255) / 256;
-    hipLaunchKernelGGL(k_reduce, dim3((uint32_t)g), dim3(256), 0, st, in, n_in, out);
+    hipLaunchKernelGGL(k_reduce, dim3((uint32_t)g), dim3(256), 0, st, in, stride, n_in, out);
     return hipGetLastError();
 }
 
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
-                              hipStream_t st) {
+                              hipStream_t st, uint32_t stride) {
     if (r == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_range_query, dim3((uint32_t)r), dim3(256), 0, st, fps, bsums, ssums, n, lo, hi, r, out);
+    hipLaunchKernelGGL(k_range_query, dim3((uint32_t)r), dim3(256), 0, st, fps, stride, bsums, ssums, n, lo, hi, r, out);
     return hipGetLastError();
 }
 

@@ -17,10 +17,11 @@ bool schema_instantiated(int kk, int kl, int vk, int vl);
 
 hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint64_t n, uint64_t limit,
                                uint8_t *fps, uint8_t *bsums, hipStream_t st);
-hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st);
+// stride: bytes between consecutive level-0 entries (32 = a fingerprint array)
+hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st, uint32_t stride = 32);
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
-                              hipStream_t st);
+                              hipStream_t st, uint32_t stride = 32);
 hipError_t launch_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64_t *out, hipStream_t st);
 
 }  // namespace rh

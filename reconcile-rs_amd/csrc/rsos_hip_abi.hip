@@ -365,7 +365,11 @@ extern "C" int rh_lift_host(int device, const rh_schema *schema, const rh_column
 }
 
 // =================================================================================================
-// The GPU-resident store: keys + fingerprints + block / super-block sums in HBM, rank order.
+// The GPU-resident store: an LSM of a sorted base run and a sorted signed-delta run (see
+// store_kernels.hip).  Batches merge into the delta run in O(batch + delta); the delta run is
+// merged into the base when it passes base / compact_div, and before any rank-order query
+// (select, rank-range aggregates, key / fingerprint dumps).  Key-range aggregates and ranks
+// are answered from base + delta without compaction.
 struct rh_store {
     int device = 0;
     rh_schema schema{};
@@ -373,104 +377,210 @@ struct rh_store {
     std::mutex mu;  // serialises callers sharing one store (readers under a RwLock read guard)
     rh::StoreKeyOps *kops = nullptr;
     size_t kl = 0;
-    uint64_t n = 0;
-    int cur = 0;
-    DevBuf<uint8_t> keys[2], fps[2];  // double-buffered: a batch merges from one into the other
-    DevBuf<uint8_t> bsums, ssums;
-    DevColumns staging;               // host batches land here
-    DevBuf<uint8_t> bfps, skeys, sfps, sops, hops;
-    DevBuf<uint64_t> q_lo, q_hi, counts;
-    DevBuf<rh_aggregate> q_out;
+    // base run
+    uint64_t nb = 0;
+    int cb = 0;
+    DevBuf<uint8_t> bkeys[2], bfps[2], bsums, ssums;
+    // delta run
+    uint64_t nd = 0;
+    int cd = 0;
+    int64_t dtotal = 0;  // Σ count deltas
+    DevBuf<uint8_t> dkeys[2], dpay[2], dbsums, dssums;
+    DevBuf<int32_t> dcnt;  // inclusive prefix of the count deltas
+    uint64_t compact_div = 8, compact_min = 65536, compactions = 0;
+    // batch scratch
+    DevColumns staging;
+    DevBuf<uint8_t> lfps, skeys, sfps, sops, hops, bpay, dops, cfps, cops;
+    DevBuf<uint64_t> counts, counts2;
+    DevBuf<uint32_t> flag;
+    // query scratch
+    DevBuf<uint64_t> q_lo, q_hi, q_dlo, q_dhi, q_merged;
+    DevBuf<rh_aggregate> q_out, q_bout, q_dout;
     DevBuf<uint8_t> q_keys;
-    DevBuf<uint32_t> flag, q_rank;
+    DevBuf<uint32_t> q_rank, q_drank;
     rh::Scratch scratch;
 
+    uint64_t size() const { return (uint64_t)((int64_t)nb + dtotal); }
     int sync() {
         RH_HIP(hipStreamSynchronize(stream));
         return RH_OK;
     }
-    int resum() {  // block + super-block sums of the current contents
+    int resum_base() {
         int rc;
-        const size_t nb = rh_num_blocks(n), ns = rh_num_superblocks(n);
-        if ((rc = bsums.ensure(nb * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32))) return rc;
-        if (n) {
-            RH_HIP(rh::launch_reduce(fps[cur].p, n, bsums.p, stream));
-            RH_HIP(rh::launch_reduce(bsums.p, nb, ssums.p, stream));
+        const size_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
+        if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32))) return rc;
+        if (nb) {
+            RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
+            RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
         }
+        return RH_OK;
+    }
+    int resum_delta() {  // contribution sums + count prefix; leaves dtotal on the host
+        int rc;
+        const size_t nbk = rh_num_blocks(nd), ns = rh_num_superblocks(nd);
+        if ((rc = dbsums.ensure(nbk * 32 + 32)) || (rc = dssums.ensure(ns * 32 + 32)) || (rc = dcnt.ensure(nd + 16)))
+            return rc;
+        dtotal = 0;
+        if (!nd) return RH_OK;
+        RH_HIP(rh::launch_reduce(dpay[cd].p, nd, dbsums.p, stream, sizeof(rh::DeltaRec)));
+        RH_HIP(rh::launch_reduce(dbsums.p, nbk, dssums.p, stream));
+        RH_HIP(rh::launch_delta_prefix(dpay[cd].p, nd, dcnt.p, scratch, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        int32_t t = 0;
+        RH_HIP(hipMemcpyAsync(&t, dcnt.p + nd - 1, 4, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        dtotal = t;
         return RH_OK;
     }
     int load_device(const rh_columns &c, size_t m) {
         int rc;
-        const int nxt = cur;  // contents are replaced in place
-        if ((rc = keys[nxt].ensure(m * kl + 64)) || (rc = fps[nxt].ensure(m * 32 + 64)) || (rc = flag.ensure(4))) return rc;
+        if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)))
+            return rc;
+        nd = 0;
+        dtotal = 0;
         if (m) {
-            RH_HIP(hipMemcpyAsync(keys[nxt].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
-            if ((rc = lift_dispatch(schema, c, m, fps[nxt].p, nullptr, nullptr, nullptr, false, stream))) return rc;
+            RH_HIP(hipMemcpyAsync(bkeys[cb].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
+            if ((rc = lift_dispatch(schema, c, m, bfps[cb].p, nullptr, nullptr, nullptr, false, stream))) return rc;
             RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
-            RH_HIP(kops->check_sorted(keys[nxt].p, m, flag.p, stream));
+            RH_HIP(kops->check_sorted(bkeys[cb].p, m, flag.p, stream));
         }
         uint32_t bad = 0;
         if (m) RH_HIP(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
         if (bad) {
-            n = 0;
+            nb = 0;
             return fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
         }
-        n = m;
-        if ((rc = resum())) return rc;
+        nb = m;
+        if ((rc = resum_base())) return rc;
+        return sync();
+    }
+    int compact() {  // merge the delta run into the base run
+        int rc;
+        if (nd == 0) return RH_OK;
+        if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64)) || (rc = counts2.ensure(4))) return rc;
+        RH_HIP(rh::launch_delta_cur(dpay[cd].p, nd, cfps.p, cops.p, stream));
+        const int nxt = 1 - cb;
+        if ((rc = bkeys[nxt].ensure((nb + nd) * kl + 64)) || (rc = bfps[nxt].ensure((nb + nd) * 32 + 64))) return rc;
+        RH_HIP(kops->merge(bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, cfps.p, cops.p, nd, 32, scratch, bkeys[nxt].p,
+                           bfps[nxt].p, counts2.p, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        uint64_t c[3];
+        RH_HIP(hipMemcpyAsync(c, counts2.p, 24, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        const uint64_t want = size();
+        cb = nxt;
+        nb = nb + c[0] - c[2];
+        nd = 0;
+        dtotal = 0;
+        compactions++;
+        if (nb != want) return fail(RH_ERR_STATE, "compaction size mismatch (internal error)");
+        if ((rc = resum_base())) return rc;
         return sync();
     }
     int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3]) {
         int rc;
         out[0] = out[1] = out[2] = 0;
         if (m == 0) return RH_OK;
-        if (n + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
-        if ((rc = bfps.ensure(m * 32 + 64)) || (rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) ||
-            (rc = sops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
+        if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if ((rc = lfps.ensure(m * 32 + 64)) || (rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) ||
+            (rc = sops.ensure(m + 64)) || (rc = bpay.ensure(m * sizeof(rh::DeltaRec) + 64)) ||
+            (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)) || (rc = counts2.ensure(4)))
             return rc;
-        // 1. lift the batch (deletes are lifted too and ignored: their value columns may be garbage
-        //    but are never read past their own rows)
-        if ((rc = lift_dispatch(schema, c, m, bfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
+        // 1. lift the batch (delete rows are lifted too and ignored)
+        if ((rc = lift_dispatch(schema, c, m, lfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
         // 2. key order + duplicate check
         RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
-        RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), bfps.p, ops, m, scratch, skeys.p, sfps.p,
-                                sops.p, flag.p, stream));
+        RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, scratch, skeys.p, sfps.p, sops.p,
+                                flag.p, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         uint32_t dup = 0;
         RH_HIP(hipMemcpyAsync(&dup, flag.p, 4, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
         if (dup) return fail(RH_ERR_ARG, "duplicate key within one batch");
-        // 3. merge into the other buffer, then swap
-        const int nxt = 1 - cur;
-        if ((rc = keys[nxt].ensure((n + m) * kl + 64)) || (rc = fps[nxt].ensure((n + m) * 32 + 64))) return rc;
-        RH_HIP(kops->merge(keys[cur].p, fps[cur].p, n, skeys.p, sfps.p, sops.p, m, scratch, keys[nxt].p, fps[nxt].p,
-                           counts.p, stream));
+        // 3. where each key is now: base and delta runs
+        uint32_t *rank_b = scratch.u32(9, m), *rank_d = scratch.u32(10, m);
+        uint8_t *present_b = scratch.u8(2, m), *present_d = scratch.u8(3, m);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        RH_HIP(kops->search(bkeys[cb].p, nb, skeys.p, m, rank_b, present_b, stream));
+        RH_HIP(kops->search(dkeys[cd].p, nd, skeys.p, m, rank_d, present_d, stream));
+        // 4. the batch's delta records, then merge them into the delta run
+        RH_HIP(hipMemsetAsync(counts.p, 0, 24, stream));
+        RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d, dpay[cd].p,
+                                      bpay.p, dops.p, counts.p, stream));
+        const int nxt = 1 - cd;
+        if ((rc = dkeys[nxt].ensure((nd + m) * kl + 64)) || (rc = dpay[nxt].ensure((nd + m) * sizeof(rh::DeltaRec) + 64)))
+            return rc;
+        RH_HIP(kops->merge(dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p, dops.p, m, sizeof(rh::DeltaRec), scratch,
+                           dkeys[nxt].p, dpay[nxt].p, counts2.p, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        uint64_t c2[3];
         RH_HIP(hipMemcpyAsync(out, counts.p, 24, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(c2, counts2.p, 24, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
-        cur = nxt;
-        n = n + out[0] - out[2];
-        if ((rc = resum())) return rc;
-        return sync();
+        cd = nxt;
+        nd = nd + c2[0] - c2[2];
+        if ((rc = resum_delta())) return rc;
+        if (nd > std::max<uint64_t>(nb / compact_div, compact_min)) return compact();
+        return RH_OK;
     }
-    int query(const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {
+    int query(const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {  // rank ranges
         int rc;
         if (r == 0) return RH_OK;
+        if ((rc = compact())) return rc;
         if ((rc = q_lo.ensure(r)) || (rc = q_hi.ensure(r)) || (rc = q_out.ensure(r))) return rc;
         RH_HIP(hipMemcpyAsync(q_lo.p, lo, r * 8, hipMemcpyHostToDevice, stream));
         RH_HIP(hipMemcpyAsync(q_hi.p, hi, r * 8, hipMemcpyHostToDevice, stream));
-        RH_HIP(rh::launch_range_query(fps[cur].p, bsums.p, ssums.p, n, q_lo.p, q_hi.p, r,
+        RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, r,
                                       reinterpret_cast<uint64_t *>(q_out.p), stream));
         RH_HIP(hipMemcpyAsync(out, q_out.p, r * sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
         return sync();
     }
+    int aggregate_keys(int lo_kind, const void *lo_key, int hi_kind, const void *hi_key, rh_aggregate *out) {
+        int rc;
+        if ((rc = q_keys.ensure(2 * kl + 64)) || (rc = q_lo.ensure(1)) || (rc = q_hi.ensure(1)) ||
+            (rc = q_dlo.ensure(1)) || (rc = q_dhi.ensure(1)) || (rc = q_out.ensure(1)) || (rc = q_bout.ensure(1)) ||
+            (rc = q_dout.ensure(1)))
+            return rc;
+        if (lo_kind) RH_HIP(hipMemcpyAsync(q_keys.p, lo_key, kl, hipMemcpyHostToDevice, stream));
+        if (hi_kind) RH_HIP(hipMemcpyAsync(q_keys.p + kl, hi_key, kl, hipMemcpyHostToDevice, stream));
+        RH_HIP(kops->bounds(bkeys[cb].p, nb, q_keys.p, lo_kind, q_keys.p + kl, hi_kind, q_lo.p, q_hi.p, stream));
+        rh_aggregate *res = nd ? q_bout.p : q_out.p;
+        RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, 1,
+                                      reinterpret_cast<uint64_t *>(res), stream));
+        if (nd) {
+            RH_HIP(kops->bounds(dkeys[cd].p, nd, q_keys.p, lo_kind, q_keys.p + kl, hi_kind, q_dlo.p, q_dhi.p, stream));
+            RH_HIP(rh::launch_range_query(dpay[cd].p, dbsums.p, dssums.p, nd, q_dlo.p, q_dhi.p, 1,
+                                          reinterpret_cast<uint64_t *>(q_dout.p), stream, sizeof(rh::DeltaRec)));
+            RH_HIP(rh::launch_agg_merge(reinterpret_cast<uint64_t *>(q_bout.p), reinterpret_cast<uint64_t *>(q_dout.p),
+                                        q_dlo.p, q_dhi.p, dcnt.p, reinterpret_cast<uint64_t *>(q_out.p), stream));
+        }
+        RH_HIP(hipMemcpyAsync(out, q_out.p, sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
+        return sync();
+    }
+    int ranks(const void *keys, size_t m, uint64_t *out) {
+        int rc;
+        if ((rc = q_keys.ensure(m * kl + 64)) || (rc = q_rank.ensure(m)) || (rc = q_drank.ensure(m)) ||
+            (rc = q_merged.ensure(m)))
+            return rc;
+        RH_HIP(hipMemcpyAsync(q_keys.p, keys, m * kl, hipMemcpyHostToDevice, stream));
+        RH_HIP(kops->search(bkeys[cb].p, nb, q_keys.p, m, q_rank.p, nullptr, stream));
+        if (nd) RH_HIP(kops->search(dkeys[cd].p, nd, q_keys.p, m, q_drank.p, nullptr, stream));
+        RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, dcnt.p, m, q_merged.p, stream));
+        RH_HIP(hipMemcpyAsync(out, q_merged.p, m * 8, hipMemcpyDeviceToHost, stream));
+        return sync();
+    }
     void release() {
         (void)hipStreamSynchronize(stream);
-        for (int k = 0; k < 2; k++) { keys[k].release(); fps[k].release(); }
-        bsums.release(); ssums.release(); staging.release();
-        bfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release();
-        q_lo.release(); q_hi.release(); counts.release(); q_out.release(); q_keys.release();
-        flag.release(); q_rank.release();
+        for (int k = 0; k < 2; k++) {
+            bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
+        }
+        bsums.release(); ssums.release(); dbsums.release(); dssums.release(); dcnt.release();
+        staging.release();
+        lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); bpay.release();
+        dops.release(); cfps.release(); cops.release(); counts.release(); counts2.release(); flag.release();
+        q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
+        q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
         scratch.release();
     }
 };
@@ -532,7 +642,7 @@ int rh_store_load_device(rh_store *s, const rh_columns *dev_cols, size_t n) {
 
 int rh_store_len(const rh_store *s, uint64_t *out) {
     if (!s || !out) return fail(RH_ERR_ARG, "NULL");
-    *out = s->n;
+    *out = s->size();
     return RH_OK;
 }
 
@@ -551,33 +661,27 @@ int rh_store_ranks(rh_store *s, const void *keys, size_t m, uint64_t *out) {
     if (!s || (m && (!keys || !out))) return fail(RH_ERR_ARG, "NULL");
     if (m == 0) return RH_OK;
     RH_LOCK(s);
-    int rc;
-    if ((rc = s->q_keys.ensure(m * s->kl + 64)) || (rc = s->q_rank.ensure(m))) return rc;
-    RH_HIP(hipMemcpyAsync(s->q_keys.p, keys, m * s->kl, hipMemcpyHostToDevice, s->stream));
-    RH_HIP(s->kops->search(s->keys[s->cur].p, s->n, s->q_keys.p, m, s->q_rank.p, nullptr, s->stream));
-    std::vector<uint32_t> r32(m);
-    RH_HIP(hipMemcpyAsync(r32.data(), s->q_rank.p, m * 4, hipMemcpyDeviceToHost, s->stream));
-    if ((rc = s->sync())) return rc;
-    for (size_t j = 0; j < m; j++) out[j] = r32[j];
-    return RH_OK;
+    return s->ranks(keys, m, out);
 }
 
 int rh_store_rank(rh_store *s, const void *key, uint64_t *out) { return rh_store_ranks(s, key, 1, out); }
 
 int rh_store_keys(rh_store *s, uint64_t lo, uint64_t hi, void *host_out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
-    if (lo > hi || hi > s->n) return fail(RH_ERR_ARG, "bad rank range");
+    RH_LOCK(s);
+    int rc;
+    if (lo > hi || hi > s->size()) return fail(RH_ERR_ARG, "bad rank range");
     if (hi == lo) return RH_OK;
     if (!host_out) return fail(RH_ERR_ARG, "host_out NULL");
-    RH_LOCK(s);
-    RH_HIP(hipMemcpyAsync(host_out, s->keys[s->cur].p + lo * s->kl, (hi - lo) * s->kl, hipMemcpyDeviceToHost,
+    if ((rc = s->compact())) return rc;
+    RH_HIP(hipMemcpyAsync(host_out, s->bkeys[s->cb].p + lo * s->kl, (hi - lo) * s->kl, hipMemcpyDeviceToHost,
                           s->stream));
     return s->sync();
 }
 
 int rh_store_select(rh_store *s, uint64_t r, void *key_out) {
     if (!s || !key_out) return fail(RH_ERR_ARG, "NULL");
-    if (r >= s->n) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+    if (r >= s->size()) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
     return rh_store_keys(s, r, r + 1, key_out);
 }
 
@@ -587,28 +691,40 @@ int rh_store_aggregate_keys(rh_store *s, int lo_kind, const void *lo_key, int hi
     if (lo_kind < 0 || lo_kind > 2 || hi_kind < 0 || hi_kind > 2) return fail(RH_ERR_ARG, "bad bound kind");
     if ((lo_kind && !lo_key) || (hi_kind && !hi_key)) return fail(RH_ERR_ARG, "bound key is NULL");
     RH_LOCK(s);
-    int rc;
-    if ((rc = s->q_keys.ensure(2 * s->kl + 64)) || (rc = s->q_lo.ensure(1)) || (rc = s->q_hi.ensure(1)) ||
-        (rc = s->q_out.ensure(1)))
-        return rc;
-    if (lo_kind) RH_HIP(hipMemcpyAsync(s->q_keys.p, lo_key, s->kl, hipMemcpyHostToDevice, s->stream));
-    if (hi_kind) RH_HIP(hipMemcpyAsync(s->q_keys.p + s->kl, hi_key, s->kl, hipMemcpyHostToDevice, s->stream));
-    RH_HIP(s->kops->bounds(s->keys[s->cur].p, s->n, s->q_keys.p, lo_kind, s->q_keys.p + s->kl, hi_kind, s->q_lo.p,
-                           s->q_hi.p, s->stream));
-    RH_HIP(rh::launch_range_query(s->fps[s->cur].p, s->bsums.p, s->ssums.p, s->n, s->q_lo.p, s->q_hi.p, 1,
-                                  reinterpret_cast<uint64_t *>(s->q_out.p), s->stream));
-    RH_HIP(hipMemcpyAsync(out, s->q_out.p, sizeof(rh_aggregate), hipMemcpyDeviceToHost, s->stream));
-    return s->sync();
+    return s->aggregate_keys(lo_kind, lo_key, hi_kind, hi_key, out);
 }
 
 int rh_store_fingerprints(rh_store *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
-    if (lo > hi || hi > s->n) return fail(RH_ERR_ARG, "bad rank range");
-    if (hi > lo && !host_out) return fail(RH_ERR_ARG, "host_out NULL");
     RH_LOCK(s);
+    int rc;
+    if (lo > hi || hi > s->size()) return fail(RH_ERR_ARG, "bad rank range");
+    if (hi > lo && !host_out) return fail(RH_ERR_ARG, "host_out NULL");
+    if ((rc = s->compact())) return rc;
     if (hi > lo)
-        RH_HIP(hipMemcpyAsync(host_out, s->fps[s->cur].p + lo * 32, (hi - lo) * 32, hipMemcpyDeviceToHost, s->stream));
+        RH_HIP(hipMemcpyAsync(host_out, s->bfps[s->cb].p + lo * 32, (hi - lo) * 32, hipMemcpyDeviceToHost, s->stream));
     return s->sync();
+}
+
+int rh_store_compact(rh_store *s) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    RH_LOCK(s);
+    return s->compact();
+}
+
+int rh_store_stats(const rh_store *s, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    if (base_rows) *base_rows = s->nb;
+    if (delta_rows) *delta_rows = s->nd;
+    if (compactions) *compactions = s->compactions;
+    return RH_OK;
+}
+
+int rh_store_set_compaction(rh_store *s, uint64_t divisor, uint64_t min_rows) {
+    if (!s || divisor == 0) return fail(RH_ERR_ARG, "bad compaction policy");
+    s->compact_div = divisor;
+    s->compact_min = min_rows;
+    return RH_OK;
 }
 
 int rh_store_apply(rh_store *s, const rh_columns *h, const uint8_t *ops, size_t m, uint64_t *n_new,

@@ -1,19 +1,22 @@
 // store_kernels.hip -- device side of the GPU-resident RSOS store: key order, rank search,
-// batch sort, and the batched insert / overwrite / delete merge.
+// batch sort, the sorted-run merge, and the signed-delta run of the LSM layout.
 //
-// Store layout in HBM (rank order): keys[n][KL] + fps[n][32] + block sums [n/256][32] +
-// super-block sums [n/65536][32].  Record payloads are not kept on the device: a record's
-// only role after its lift is its fingerprint (the host owns K and V, as the reference's
-// map does -- rsos_trait.rs:70-80 returns borrows into host memory).
+// Store layout in HBM (rank order):
+//   base  : keys[nB][KL] + fps[nB][32] + block sums [nB/256][32] + super sums [nB/65536][32]
+//   delta : keys[nD][KL] + DeltaRec[nD] (80 B) + block / super sums of the contributions +
+//           an inclusive prefix of the count deltas
+// A DeltaRec for key k says what the batches since the last compaction did to k:
+//   contrib = cur_fp - base_fp   (cur_fp = 0 if k is now deleted; base_fp = 0 if k not in base)
+//   in_base, live                 (so the count delta is live - in_base, in {-1, 0, +1})
+// so every aggregate over a key range is   base part + Σ contrib over the delta part,
+// exactly as FingerprintTreeMap composes signed deltas into its cached aggregates
+// (rsos/src/fingerprint_tree_map/mutate.rs:31-41 overwrite delta, :93-154 remove).
+// Record payloads are not kept on the device (the host owns K and V, rsos_trait.rs:66-80).
 //
 // Batched update = FingerprintTreeMap::insert / remove applied to a whole batch at once
-// (rsos/src/fingerprint_tree_map/mutate.rs:23-154):
-//   sort batch by key -> rank of each batch key in the store -> classify INS / OVR / DEL
-//   -> positions by prefix sums -> move survivors + scatter inserts / overwrites
-//   -> recompute block / super-block sums.
-// An overwrite replaces the fingerprint (new - old delta, mutate.rs:31-41); a delete removes
-// the element (its fingerprint leaves every enclosing sum, mutate.rs:93-154); re-delivering
-// an identical record changes nothing (btreemap_oracle.rs:195-231).
+// (mutate.rs:23-154): sort the batch by key, find every key in base and delta, build the
+// batch's DeltaRecs, merge them into the delta run (O(m + nD)); when the delta run passes
+// nB / 8 it is merged into the base (O(nB)) -- amortised, and on demand before rank / select.
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -53,28 +56,71 @@ __device__ __forceinline__ uint64_t key_digit(const uint8_t *k, int d) {
     else return __builtin_bswap64(*reinterpret_cast<const uint64_t *>(k + 8 * d));
 }
 
-template <int KK, int KL>
-__device__ __forceinline__ void copy_key(uint8_t *dst, const uint8_t *src) {
-    if constexpr (KL % 16 == 0) {
+// copy N bytes (N a multiple of 4) with the widest aligned accesses
+template <int N>
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src) {
+    if constexpr (N % 16 == 0) {
 #pragma unroll
-        for (int o = 0; o < KL; o += 16) *reinterpret_cast<uint4 *>(dst + o) = *reinterpret_cast<const uint4 *>(src + o);
-    } else if constexpr (KL % 8 == 0) {
+        for (int o = 0; o < N; o += 16) *reinterpret_cast<uint4 *>(dst + o) = *reinterpret_cast<const uint4 *>(src + o);
+    } else if constexpr (N % 8 == 0) {
 #pragma unroll
-        for (int o = 0; o < KL; o += 8) *reinterpret_cast<uint2 *>(dst + o) = *reinterpret_cast<const uint2 *>(src + o);
+        for (int o = 0; o < N; o += 8) *reinterpret_cast<uint2 *>(dst + o) = *reinterpret_cast<const uint2 *>(src + o);
     } else {
 #pragma unroll
-        for (int o = 0; o < KL; o += 4) *reinterpret_cast<uint32_t *>(dst + o) = *reinterpret_cast<const uint32_t *>(src + o);
+        for (int o = 0; o < N; o += 4) *reinterpret_cast<uint32_t *>(dst + o) = *reinterpret_cast<const uint32_t *>(src + o);
     }
 }
 
-__device__ __forceinline__ void copy_fp(uint8_t *dst, const uint8_t *src) {
-    const uint4 *s = reinterpret_cast<const uint4 *>(src);
-    uint4 *d = reinterpret_cast<uint4 *>(dst);
-    d[0] = s[0];
-    d[1] = s[1];
+template <int KK, int KL>
+__device__ __forceinline__ uint64_t lower_bound_keys(const uint8_t *keys, uint64_t n, const uint8_t *key) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (key_cmp<KK, KL>(keys + mid * KL, key) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
 }
 
-// ---- kernels --------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t *a, uint64_t lo, uint64_t hi, uint64_t x) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// ---- 256-bit helpers (the Fingerprint group, rsos/src/fingerprint.rs:145-173) ----------------
+
+__device__ __forceinline__ void fp_load(const uint8_t *p, uint32_t f[8]) {
+    const uint4 a = reinterpret_cast<const uint4 *>(p)[0], b = reinterpret_cast<const uint4 *>(p)[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void fp_store(uint8_t *p, const uint32_t f[8]) {
+    reinterpret_cast<uint4 *>(p)[0] = make_uint4(f[0], f[1], f[2], f[3]);
+    reinterpret_cast<uint4 *>(p)[1] = make_uint4(f[4], f[5], f[6], f[7]);
+}
+__device__ __forceinline__ void fp_add(const uint32_t a[8], const uint32_t b[8], uint32_t o[8]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t t = (uint64_t)a[i] + b[i] + c;
+        o[i] = (uint32_t)t;
+        c = t >> 32;
+    }
+}
+__device__ __forceinline__ void fp_sub(const uint32_t a[8], const uint32_t b[8], uint32_t o[8]) {
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t t = (uint64_t)a[i] - b[i] - br;
+        o[i] = (uint32_t)t;
+        br = (t >> 63) & 1;  // borrow out
+    }
+}
+
+// ---- batch sort ------------------------------------------------------------------------------
 
 template <int KK, int KL>
 __global__ void k_digit(const uint8_t *keys, const uint32_t *perm, uint64_t m, int d, uint64_t *out) {
@@ -94,30 +140,31 @@ __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t 
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const uint64_t s = perm[j];
-    copy_key<KK, KL>(skeys + j * KL, keys + s * KL);
-    copy_fp(sfps + 32 * j, fps + 32 * s);
+    copy_bytes<KL>(skeys + j * KL, keys + s * KL);
+    copy_bytes<32>(sfps + 32 * j, fps + 32 * s);
     sops[j] = ops ? ops[s] : 0;
     if (j > 0 && key_cmp<KK, KL>(keys + s * KL, keys + (uint64_t)perm[j - 1] * KL) == 0) atomicOr(dup, 1u);
 }
 
-// lower_bound rank of each query key in the sorted store keys; present = key at rank equals
+// ---- search ---------------------------------------------------------------------------------
+
+// lower_bound rank of each query key in a sorted key array; present = key at rank equals
 template <int KK, int KL>
 __global__ void k_search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                          uint8_t *present) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const uint8_t *key = q + j * KL;
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (key_cmp<KK, KL>(keys + mid * KL, key) < 0) lo = mid + 1;
-        else hi = mid;
-    }
+    const uint64_t lo = lower_bound_keys<KK, KL>(keys, n, key);
     rank[j] = (uint32_t)lo;
     if (present) present[j] = (lo < n && key_cmp<KK, KL>(keys + lo * KL, key) == 0) ? 1 : 0;
 }
 
-// classify: op 0 = insert-or-overwrite, 1 = delete.  ins/del as 0/1 for the scans.
+// ---- sorted-run merge (payload P bytes per row) ------------------------------------------
+
+// classify: op 0 = upsert, 1 = delete.  INS = upsert of an absent key, DEL = delete of a
+// present key; an upsert of a present key overwrites its payload; deleting an absent key is a
+// no-op (FingerprintTreeMap::remove returns None).
 __global__ void k_classify(const uint8_t *sops, const uint8_t *present, uint64_t m, uint32_t *ins, uint32_t *del) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
@@ -135,13 +182,20 @@ __global__ void k_compact(const uint32_t *rank, const uint32_t *ins, const uint3
     if (del[j]) del_rank[cum_del[j]] = rank[j];
 }
 
-__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t *a, uint64_t lo, uint64_t hi, uint64_t x) {
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (a[mid] < x) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
+// counts[0] = inserts, counts[2] = deletes (counts[1], overwrites, by k_count_ovr)
+__global__ void k_counts(const uint32_t *ins, const uint32_t *del, const uint32_t *cum_ins, const uint32_t *cum_del,
+                         uint64_t m, uint64_t *counts) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    counts[0] = m ? (uint64_t)cum_ins[m - 1] + ins[m - 1] : 0;
+    counts[1] = 0;
+    counts[2] = m ? (uint64_t)cum_del[m - 1] + del[m - 1] : 0;
+}
+
+__global__ void k_count_ovr(const uint8_t *sops, const uint8_t *present, uint64_t m, unsigned long long *ovr) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool o = j < m && sops[j] == 0 && present[j];
+    const unsigned long long b = __ballot(o);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(ovr, (unsigned long long)__popcll(b));
 }
 
 // Survivors move to i + #inserts(rank <= i) - #deletes(rank < i); deleted rows are skipped.
@@ -149,10 +203,10 @@ __device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t *a, uint64_t 
 // insert / delete rank lists that falls inside the tile, then every row binary-searches only
 // that slice -- no n-sized scratch arrays, no n-sized scan.
 constexpr int MOVE_TILE = 1024;
-template <int KK, int KL>
-__global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const uint8_t *fps, uint64_t n,
+template <int KL, int P>
+__global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const uint8_t *pay, uint64_t n,
                                                     const uint32_t *ins_rank, const uint32_t *del_rank,
-                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *ofps) {
+                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay) {
     __shared__ uint64_t bounds[4];
     const uint64_t i0 = (uint64_t)blockIdx.x * MOVE_TILE;
     if (threadIdx.x == 0) {
@@ -172,38 +226,23 @@ __global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const u
         const uint64_t del_lt = lower_bound_u32(del_rank, da, db, i);      // rank < i
         if (del_lt < db && del_rank[del_lt] == i) continue;                 // deleted
         const uint64_t pos = i + ins_le - del_lt;
-        copy_key<KK, KL>(okeys + pos * KL, keys + i * KL);
-        copy_fp(ofps + 32 * pos, fps + 32 * i);
+        copy_bytes<KL>(okeys + pos * KL, keys + i * KL);
+        copy_bytes<P>(opay + (uint64_t)P * pos, pay + (uint64_t)P * i);
     }
 }
 
 // inserts and overwrites land at r + (#inserts before j) - (#deletes before j): for an insert
-// that is its slot; for an overwrite it is where its surviving element moved (the inserts with
+// that is its slot; for an overwrite it is where its surviving row moved (the inserts with
 // rank <= r and the deletes with rank < r are exactly the batch entries before j in key order)
-template <int KK, int KL>
-__global__ void k_scatter(const uint8_t *skeys, const uint8_t *sfps, const uint8_t *present, const uint8_t *sops,
+template <int KL, int P>
+__global__ void k_scatter(const uint8_t *skeys, const uint8_t *spay, const uint8_t *present, const uint8_t *sops,
                           const uint32_t *rank, const uint32_t *cum_ins, const uint32_t *cum_del, uint64_t m,
-                          uint8_t *okeys, uint8_t *ofps) {
+                          uint8_t *okeys, uint8_t *opay) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m || sops[j] != 0) return;
     const uint64_t pos = (uint64_t)rank[j] + cum_ins[j] - cum_del[j];
-    if (!present[j]) copy_key<KK, KL>(okeys + pos * KL, skeys + j * KL);
-    copy_fp(ofps + 32 * pos, sfps + 32 * j);
-}
-
-// counts[0..3] = inserted, overwritten, deleted, (dup flag is separate)
-__global__ void k_counts(const uint32_t *ins, const uint32_t *del, const uint32_t *cum_ins, const uint32_t *cum_del,
-                         const uint8_t *sops, const uint8_t *present, uint64_t m, uint64_t *counts) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    counts[0] = m ? (uint64_t)cum_ins[m - 1] + ins[m - 1] : 0;
-    counts[2] = m ? (uint64_t)cum_del[m - 1] + del[m - 1] : 0;
-}
-
-__global__ void k_count_ovr(const uint8_t *sops, const uint8_t *present, uint64_t m, unsigned long long *ovr) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool o = j < m && sops[j] == 0 && present[j];
-    const unsigned long long b = __ballot(o);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(ovr, (unsigned long long)__popcll(b));
+    if (!present[j]) copy_bytes<KL>(okeys + pos * KL, skeys + j * KL);
+    copy_bytes<P>(opay + (uint64_t)P * pos, spay + (uint64_t)P * j);
 }
 
 // 1 if keys are not strictly increasing
@@ -213,33 +252,115 @@ __global__ void k_check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad) {
     if (i < n && key_cmp<KK, KL>(keys + (i - 1) * KL, keys + i * KL) >= 0) atomicOr(bad, 1u);
 }
 
-// rank bounds of a key range (std::ops::Bound kinds 0 unbounded / 1 included / 2 excluded)
+// rank bounds of a key range in a sorted key array (std::ops::Bound: 0 unbounded, 1 included,
+// 2 excluded); an inverted range gives an empty one (rbsr/src/protocol.rs:230-232)
 template <int KK, int KL>
 __global__ void k_bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key, int lo_kind, const uint8_t *hi_key,
                          int hi_kind, uint64_t *qlo, uint64_t *qhi) {
     if (threadIdx.x != 0) return;
-    auto lb = [&](const uint8_t *k) {
-        uint64_t lo = 0, hi = n;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (key_cmp<KK, KL>(keys + mid * KL, k) < 0) lo = mid + 1;
-            else hi = mid;
-        }
-        return lo;
-    };
-    auto present = [&](uint64_t r, const uint8_t *k) { return r < n && key_cmp<KK, KL>(keys + r * KL, k) == 0; };
     uint64_t a = 0, b = n;
     if (lo_kind) {
-        a = lb(lo_key);
-        if (lo_kind == 2 && present(a, lo_key)) a++;
+        a = lower_bound_keys<KK, KL>(keys, n, lo_key);
+        if (lo_kind == 2 && a < n && key_cmp<KK, KL>(keys + a * KL, lo_key) == 0) a++;
     }
     if (hi_kind) {
-        b = lb(hi_key);
-        if (hi_kind == 1 && present(b, hi_key)) b++;
+        b = lower_bound_keys<KK, KL>(keys, n, hi_key);
+        if (hi_kind == 1 && b < n && key_cmp<KK, KL>(keys + b * KL, hi_key) == 0) b++;
     }
-    if (b < a) b = a;  // inverted range -> ZERO (rbsr/src/protocol.rs:230-232)
+    if (b < a) b = a;
     *qlo = a;
     *qhi = b;
+}
+
+// ---- the delta run ------------------------------------------------------------------------
+
+// Build the batch's DeltaRecs (key order) from its fingerprints, what base and delta hold for
+// each key, and the op; dops: 0 = upsert into the delta run, 1 = drop the key's delta entry.
+// counts (vs the merged view): [0] new keys, [1] overwritten, [2] deleted.
+__global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
+                              const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
+                              const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
+                              unsigned long long *counts) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool c_new = false, c_over = false, c_del = false;
+    if (j < m) {
+        const bool isdel = sops[j] != 0, in_b = present_b[j], in_d = present_d[j];
+        bool was_live = in_b;
+        if (in_d) was_live = (reinterpret_cast<const DeltaRec *>(dpay)[rank_d[j]].flags & DeltaRec::LIVE) != 0;
+        uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (in_b) fp_load(base_fps + 32ull * rank_b[j], base);
+        DeltaRec r;
+        r.flags = (in_b ? DeltaRec::IN_BASE : 0u);
+        r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        uint32_t cur[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (!isdel) {
+            fp_load(sfps + 32 * j, cur);
+            r.flags |= DeltaRec::LIVE;
+            c_new = !was_live;
+            c_over = was_live;
+        } else {
+            c_del = was_live;
+        }
+        fp_sub(cur, base, r.contrib);
+#pragma unroll
+        for (int i = 0; i < 8; i++) r.base[i] = base[i];
+        // deleting a key the base does not hold needs no entry (drop any delta entry it has)
+        dops[j] = (isdel && !in_b) ? 1 : 0;
+        reinterpret_cast<DeltaRec *>(bpay)[j] = r;
+    }
+    const unsigned long long bn = __ballot(c_new), bo = __ballot(c_over), bd = __ballot(c_del);
+    if ((threadIdx.x & 63) == 0) {
+        if (bn) atomicAdd(counts + 0, (unsigned long long)__popcll(bn));
+        if (bo) atomicAdd(counts + 1, (unsigned long long)__popcll(bo));
+        if (bd) atomicAdd(counts + 2, (unsigned long long)__popcll(bd));
+    }
+}
+
+// count delta of each delta entry: live - in_base
+__global__ void k_delta_cnt(const uint8_t *dpay, uint64_t n, int32_t *cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t f = reinterpret_cast<const DeltaRec *>(dpay)[i].flags;
+    cnt[i] = (int32_t)((f & DeltaRec::LIVE) ? 1 : 0) - (int32_t)((f & DeltaRec::IN_BASE) ? 1 : 0);
+}
+
+// compaction input: cur fp = contrib + base, op = live ? upsert : delete
+__global__ void k_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
+    uint32_t cur[8];
+    fp_add(r.contrib, r.base, cur);
+    fp_store(fps + 32 * i, cur);
+    ops[i] = (r.flags & DeltaRec::LIVE) ? 0 : 1;
+}
+
+// aggregate over a key range of the merged view = base part + delta part; the delta part's
+// size is the sum of its count deltas (prefix difference), not its entry count
+__global__ void k_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
+                            const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out) {
+    if (threadIdx.x != 0) return;
+    const uint64_t lo = *dlo, hi = *dhi;
+    const int64_t c = (int64_t)(hi ? cnt_prefix[hi - 1] : 0) - (int64_t)(lo ? cnt_prefix[lo - 1] : 0);
+    uint64_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint64_t a = base_agg[i], b = delta_agg[i];
+        const uint64_t s = a + b;
+        const uint64_t s2 = s + carry;
+        carry = (s < a ? 1u : 0u) | (s2 < s ? 1u : 0u);
+        out[i] = s2;
+    }
+    out[4] = (uint64_t)((int64_t)base_agg[4] + c);
+}
+
+// rank in the merged view = rank in base + Σ count deltas of the delta keys below
+__global__ void k_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, const int32_t *cnt_prefix, uint64_t m,
+                             uint64_t *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t rd = rank_d ? rank_d[j] : 0;
+    out[j] = (uint64_t)((int64_t)rank_b[j] + (rd ? cnt_prefix[rd - 1] : 0));
 }
 
 // ---- host-side drivers --------------------------------------------------------------------------
@@ -258,12 +379,14 @@ struct KeyOps final : StoreKeyOps {
         hipError_t e;
         uint32_t *perm = s.u32(0, m), *perm2 = s.u32(1, m);
         uint64_t *dig = s.u64(0, m), *dig2 = s.u64(1, m);
+        if (s.err) return s.err;
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
         for (int d = D - 1; d >= 0; d--) {  // LSD: least significant digit first, stable passes
             hipLaunchKernelGGL((k_digit<KK, KL>), g1(m), dim3(256), 0, st, keys, perm, m, d, dig);
             size_t tb = 0;
             if ((e = rocprim::radix_sort_pairs(nullptr, tb, dig, dig2, perm, perm2, m, 0, BITS, st))) return e;
             void *tmp = s.bytes(tb);
+            if (s.err) return s.err;
             if ((e = rocprim::radix_sort_pairs(tmp, tb, dig, dig2, perm, perm2, m, 0, BITS, st))) return e;
             std::swap(perm, perm2);
         }
@@ -278,9 +401,10 @@ struct KeyOps final : StoreKeyOps {
         return hipGetLastError();
     }
 
-    hipError_t merge(const uint8_t *keys, const uint8_t *fps, uint64_t n, const uint8_t *skeys, const uint8_t *sfps,
-                     const uint8_t *sops, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *ofps, uint64_t *counts,
-                     hipStream_t st) override {
+    template <int P>
+    hipError_t merge_p(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys, const uint8_t *spay,
+                       const uint8_t *sops, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay, uint64_t *counts,
+                       hipStream_t st) {
         hipError_t e;
         uint32_t *rank = s.u32(2, m), *ins = s.u32(3, m), *del = s.u32(4, m);
         uint32_t *cins = s.u32(5, m), *cdel = s.u32(6, m), *ins_rank = s.u32(7, m), *del_rank = s.u32(8, m);
@@ -291,22 +415,32 @@ struct KeyOps final : StoreKeyOps {
         size_t tb = 0;
         if ((e = rocprim::exclusive_scan(nullptr, tb, ins, cins, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
         void *tmp = s.bytes(tb);
+        if (s.err) return s.err;
         if ((e = rocprim::exclusive_scan(tmp, tb, ins, cins, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
         if ((e = rocprim::exclusive_scan(tmp, tb, del, cdel, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
         hipLaunchKernelGGL(k_compact, g1(m), dim3(256), 0, st, rank, ins, del, cins, cdel, m, ins_rank, del_rank);
-        // totals of inserts / deletes (counts[0], counts[2]) are read by the tile kernel on the device
-        hipLaunchKernelGGL(k_counts, dim3(1), dim3(64), 0, st, ins, del, cins, cdel, sops, present, m, counts);
+        // list lengths (counts[0], counts[2]) are read by the tile kernel on the device
+        hipLaunchKernelGGL(k_counts, dim3(1), dim3(64), 0, st, ins, del, cins, cdel, m, counts);
         if (n) {
             const uint64_t tiles = (n + MOVE_TILE - 1) / MOVE_TILE;
-            hipLaunchKernelGGL((k_move_tiles<KK, KL>), dim3((uint32_t)tiles), dim3(256), 0, st, keys, fps, n, ins_rank,
-                               del_rank, counts, okeys, ofps);
+            hipLaunchKernelGGL((k_move_tiles<KL, P>), dim3((uint32_t)tiles), dim3(256), 0, st, keys, pay, n, ins_rank,
+                               del_rank, counts, okeys, opay);
         }
-        hipLaunchKernelGGL((k_scatter<KK, KL>), g1(m), dim3(256), 0, st, skeys, sfps, present, sops, rank, cins, cdel,
-                           m, okeys, ofps);
-        if ((e = hipMemsetAsync(counts + 1, 0, 8, st))) return e;
+        hipLaunchKernelGGL((k_scatter<KL, P>), g1(m), dim3(256), 0, st, skeys, spay, present, sops, rank, cins, cdel,
+                           m, okeys, opay);
         hipLaunchKernelGGL(k_count_ovr, g1(m), dim3(256), 0, st, sops, present, m,
                            reinterpret_cast<unsigned long long *>(counts + 1));
         return hipGetLastError();
+    }
+
+    hipError_t merge(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys, const uint8_t *spay,
+                     const uint8_t *sops, uint64_t m, int payload, Scratch &s, uint8_t *okeys, uint8_t *opay,
+                     uint64_t *counts, hipStream_t st) override {
+        if (m == 0) return hipMemsetAsync(counts, 0, 24, st);
+        if (payload == 32) return merge_p<32>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st);
+        if (payload == (int)sizeof(DeltaRec))
+            return merge_p<sizeof(DeltaRec)>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st);
+        return hipErrorInvalidValue;
     }
 
     hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) override {
@@ -320,6 +454,20 @@ struct KeyOps final : StoreKeyOps {
         hipLaunchKernelGGL((k_bounds<KK, KL>), dim3(1), dim3(64), 0, st, keys, n, lo_key, lo_kind, hi_key, hi_kind, qlo,
                            qhi);
         return hipGetLastError();
+    }
+
+    int compare_keys_host(const uint8_t *a, const uint8_t *b) const override {
+        if constexpr (KK == KEY_U32) {
+            uint32_t x, y;
+            memcpy(&x, a, 4); memcpy(&y, b, 4);
+            return (x > y) - (x < y);
+        } else if constexpr (KK == KEY_U64) {
+            uint64_t x, y;
+            memcpy(&x, a, 8); memcpy(&y, b, 8);
+            return (x > y) - (x < y);
+        } else {
+            return memcmp(a, b, KL);
+        }
     }
 };
 
@@ -335,6 +483,48 @@ StoreKeyOps *store_key_ops(int kk, int kl) {
     if (kk == KEY_BYTES && kl == 32) return &b32;
     if (kk == KEY_BYTES && kl == 8) return &b8;
     return nullptr;
+}
+
+// ---- delta launchers (key-type independent) -------------------------------------------------
+
+hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
+                              const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
+                              const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
+                              uint64_t *counts, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delta_build, g1(m), dim3(256), 0, st, sfps, sops, m, rank_b, present_b, base_fps, rank_d,
+                       present_d, dpay, bpay, dops, reinterpret_cast<unsigned long long *>(counts));
+    return hipGetLastError();
+}
+
+hipError_t launch_delta_prefix(const uint8_t *dpay, uint64_t n, int32_t *cnt, Scratch &s, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delta_cnt, g1(n), dim3(256), 0, st, dpay, n, cnt);
+    size_t tb = 0;
+    hipError_t e;
+    if ((e = rocprim::inclusive_scan(nullptr, tb, cnt, cnt, n, rocprim::plus<int32_t>(), st))) return e;
+    void *tmp = s.bytes(tb);
+    if (s.err) return s.err;
+    return rocprim::inclusive_scan(tmp, tb, cnt, cnt, n, rocprim::plus<int32_t>(), st);
+}
+
+hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delta_cur, g1(n), dim3(256), 0, st, dpay, n, fps, ops);
+    return hipGetLastError();
+}
+
+hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
+                            const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_agg_merge, dim3(1), dim3(64), 0, st, base_agg, delta_agg, dlo, dhi, cnt_prefix, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, const int32_t *cnt_prefix, uint64_t m,
+                             uint64_t *out, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rank_merge, g1(m), dim3(256), 0, st, rank_b, rank_d, cnt_prefix, m, out);
+    return hipGetLastError();
 }
 
 }  // namespace rh

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "lift_kernels.hpp"
@@ -55,6 +56,17 @@ struct Scratch {
     }
 };
 
+// One entry of the store's delta run (80 B): what the batches since the last compaction did to
+// a key.  contrib = cur - base (mod 2^256); count delta = live - in_base.
+struct DeltaRec {
+    enum : uint32_t { IN_BASE = 1, LIVE = 2 };
+    uint32_t contrib[8];
+    uint32_t base[8];
+    uint32_t flags;
+    uint32_t pad[3];
+};
+static_assert(sizeof(DeltaRec) == 80, "DeltaRec layout");
+
 // Key-type-specialised device operations of the store.
 struct StoreKeyOps {
     virtual ~StoreKeyOps() = default;
@@ -66,14 +78,30 @@ struct StoreKeyOps {
     // lower-bound rank of each query key (and whether it is present)
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;
-    // merge a key-sorted batch into (keys, fps) -> (okeys, ofps); counts = {new, overwritten, deleted}
-    virtual hipError_t merge(const uint8_t *keys, const uint8_t *fps, uint64_t n, const uint8_t *skeys,
-                             const uint8_t *sfps, const uint8_t *sops, uint64_t m, Scratch &s, uint8_t *okeys,
-                             uint8_t *ofps, uint64_t *counts, hipStream_t st) = 0;
+    // merge a key-sorted batch (ops: 0 upsert, 1 delete) into a sorted run of (key, payload)
+    // rows -> (okeys, opay); payload 32 (fingerprints) or 80 (DeltaRec);
+    // counts = {inserted, overwritten, deleted}
+    virtual hipError_t merge(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys,
+                             const uint8_t *spay, const uint8_t *sops, uint64_t m, int payload, Scratch &s,
+                             uint8_t *okeys, uint8_t *opay, uint64_t *counts, hipStream_t st) = 0;
     virtual hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) = 0;
     virtual hipError_t bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key, int lo_kind,
                               const uint8_t *hi_key, int hi_kind, uint64_t *qlo, uint64_t *qhi, hipStream_t st) = 0;
+    // the key type's Ord on the host (for argument checks)
+    virtual int compare_keys_host(const uint8_t *a, const uint8_t *b) const = 0;
 };
+
+// delta-run kernels (store_kernels.hip)
+hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
+                              const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
+                              const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
+                              uint64_t *counts, hipStream_t st);
+hipError_t launch_delta_prefix(const uint8_t *dpay, uint64_t n, int32_t *cnt, Scratch &s, hipStream_t st);
+hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops, hipStream_t st);
+hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
+                            const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out, hipStream_t st);
+hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, const int32_t *cnt_prefix, uint64_t m,
+                             uint64_t *out, hipStream_t st);
 
 // nullptr if the store does not support this key type
 StoreKeyOps *store_key_ops(int key_kind, int key_len);

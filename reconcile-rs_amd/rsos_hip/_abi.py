@@ -69,6 +69,9 @@ SIGNATURES = [
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rh_store_apply_device", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("rh_store_compact", C.c_int, [P]),
+    ("rh_store_set_compaction", C.c_int, [P, C.c_uint64, C.c_uint64]),
+    ("rh_store_stats", C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 ]
 
 _lib = None

@@ -120,6 +120,17 @@ class GpuFingerprintStore:
                                               C.byref(a), C.byref(b), C.byref(d)), "rh_store_apply_device")
         return int(a.value), int(b.value), int(d.value)
 
+    def compact(self) -> None:
+        A.check(A.lib().rh_store_compact(self._h), "rh_store_compact")
+
+    def set_compaction(self, divisor: int, min_rows: int) -> None:
+        A.check(A.lib().rh_store_set_compaction(self._h, divisor, min_rows), "rh_store_set_compaction")
+
+    def stats(self) -> Dict[str, int]:
+        b, d, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        A.check(A.lib().rh_store_stats(self._h, C.byref(b), C.byref(d), C.byref(c)), "rh_store_stats")
+        return {"base_rows": int(b.value), "delta_rows": int(d.value), "compactions": int(c.value)}
+
     # ---- Rsos<K> -------------------------------------------------------------------------
     def size(self) -> int:
         out = C.c_uint64()

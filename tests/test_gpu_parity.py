@@ -467,3 +467,74 @@ def test_store_rejects_bad_batches_unchanged(gpu):
     with pytest.raises(RsosHipError):
         st.load_bulk_device(bad)
     st.close()
+
+
+def test_store_lsm_policies_agree(gpu, oracle_lib):
+    """The LSM store answers identically whether the delta run is compacted after every batch
+    or never: key-range aggregates, ranks and sizes over base + delta equal the compacted base,
+    and both equal a fold of the oracle's lift over the expected contents."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    s = RecordSchema.plain("u64", "u64")
+    O = oracle_lib
+    rng = np.random.default_rng(31)
+    keys = np.unique(rng.integers(0, 2**40, 50_000, dtype=np.uint64))
+    vals = rng.integers(0, 2**63, len(keys), dtype=np.uint64)
+    content = {int(k): int(v) for k, v in zip(keys, vals)}
+    lazy, eager = GpuFingerprintStore(s), GpuFingerprintStore(s)
+    lazy.set_compaction(1 << 40, 1 << 40)   # never compacts on its own
+    eager.set_compaction(1, 0)              # compacts after every batch
+    for st in (lazy, eager):
+        st.load_bulk({"keys": keys.view(np.uint8).reshape(-1, 8), "values": vals.view(np.uint8).reshape(-1, 8)})
+    sc = O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0)
+    inserted = []
+    for rnd in range(6):
+        present = np.array(list(content.keys()), np.uint64)
+        new = rng.integers(0, 2**40, 3000, dtype=np.uint64)
+        over = rng.choice(present, 1000, replace=False)
+        dele = rng.choice(np.setdiff1d(present, over), 800, replace=False)
+        if inserted:  # delete some keys that only ever lived in the delta run
+            dele = np.unique(np.concatenate([dele, np.array(inserted[-300:], np.uint64)]))
+        bk = np.setdiff1d(np.unique(np.concatenate([new, over])), dele)
+        bv = rng.integers(0, 2**63, len(bk), dtype=np.uint64)
+        allk = np.concatenate([bk, dele])
+        allv = np.concatenate([bv, np.zeros(len(dele), np.uint64)])
+        ops = np.concatenate([np.zeros(len(bk), np.uint8), np.ones(len(dele), np.uint8)])
+        perm = rng.permutation(len(allk))
+        cols = {"keys": allk[perm].view(np.uint8).reshape(-1, 8), "values": allv[perm].view(np.uint8).reshape(-1, 8)}
+        exp = (sum(1 for k in bk if int(k) not in content), sum(1 for k in bk if int(k) in content),
+               sum(1 for k in dele if int(k) in content))
+        assert lazy.apply(cols, ops[perm]) == exp
+        assert eager.apply(cols, ops[perm]) == exp
+        for k, v in zip(bk, bv):
+            if int(k) not in content:
+                inserted.append(int(k))
+            content[int(k)] = int(v)
+        for k in dele:
+            content.pop(int(k), None)
+        assert lazy.stats()["delta_rows"] > 0 and eager.stats()["delta_rows"] == 0
+        ks = np.array(sorted(content), np.uint64)
+        fps = O.Records(sc, ks.view(np.uint8).reshape(-1, 8),
+                        np.array([content[int(k)] for k in ks], np.uint64).view(np.uint8).reshape(-1, 8)).lift(threads=8)
+        pref = [0]
+        for f in fps:
+            pref.append(pref[-1] + fp_int(f))
+        assert lazy.size() == eager.size() == len(ks)
+        assert lazy.aggregate().fingerprint.to_int() == eager.aggregate().fingerprint.to_int() == pref[-1] % M256
+        for _ in range(25):
+            a, b = sorted(int(x) for x in rng.integers(0, 2**40, 2))
+            ra, rb = np.searchsorted(ks, a), np.searchsorted(ks, b)
+            for st in (lazy, eager):
+                agg = st.aggregate(KeyRange(a, b))
+                assert agg.size == rb - ra and agg.fingerprint.to_int() == (pref[rb] - pref[ra]) % M256
+        probes = rng.integers(0, 2**40, 64, dtype=np.uint64)
+        want = np.searchsorted(ks, probes)
+        assert (lazy.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
+        assert (eager.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
+    # a rank-order query compacts the lazy store; afterwards both agree row for row
+    assert lazy.select(100) == int(ks[100])
+    assert lazy.stats()["delta_rows"] == 0
+    assert np.array_equal(lazy.fingerprints(), eager.fingerprints())
+    lazy.close()
+    eager.close()

@@ -483,8 +483,8 @@ def test_store_lsm_policies_agree(gpu, oracle_lib):
     vals = rng.integers(0, 2**63, len(keys), dtype=np.uint64)
     content = {int(k): int(v) for k, v in zip(keys, vals)}
     lazy, eager = GpuFingerprintStore(s), GpuFingerprintStore(s)
-    lazy.set_compaction(1 << 40, 1 << 40)   # never compacts on its own
-    eager.set_compaction(1, 0)              # compacts after every batch
+    lazy.set_compaction(1, 1 << 40)         # threshold max(base / 1, 2^40): never on its own
+    eager.set_compaction(1 << 40, 0)        # threshold max(base / 2^40, 0) = 0: after every batch
     for st in (lazy, eager):
         st.load_bulk({"keys": keys.view(np.uint8).reshape(-1, 8), "values": vals.view(np.uint8).reshape(-1, 8)})
     sc = O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0)

@@ -221,10 +221,12 @@ def incremental(args, world, rank, dev, dist):
         dist.barrier()
     torch.cuda.synchronize()
     counts = [0, 0, 0]
+    comp0 = st.stats()["compactions"]
     t0 = time.perf_counter()
     for k in range(args.steps):
         c = st.apply_device(batches[args.warmup + k])
         counts = [a + b for a, b in zip(counts, c)]
+        root_agg = st.aggregate()  # the updated root fingerprint (initial_ranges, rbsr/src/protocol.rs:100)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -234,6 +236,8 @@ def incremental(args, world, rank, dev, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     root = st.aggregate()
+    stats = st.stats()
+    assert root == root_agg
     if rank == 0:
         recs = m * args.steps * world
         line = {
@@ -247,11 +251,40 @@ def incremental(args, world, rank, dev, dist):
                        "parallelism": f"key-range shards x{world}"},
             "batch_counts": {"new": counts[0], "overwritten": counts[1], "deleted": counts[2]},
             "final_size": root.size, "bulk_load_s": round(load_s, 3),
+            "step": "apply_device (lift + sort + base/delta search + delta merge; amortised compaction) "
+                    "+ root aggregate",
+            "compactions_in_timed_steps": stats["compactions"] - comp0, "delta_rows_at_end": stats["delta_rows"],
         }
+        if args.cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline_incremental(schema, m, args.cpu_sample or 10_000_000)
         print(json.dumps(line), flush=True)
     st.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def cpu_baseline_incremental(schema, m, resident):
+    """The reference's update path restated (oracle/oracle.c FingerprintTreeMap): a resident map
+    of `resident` records filled untimed, then `m` random-key inserts timed, serially (one writer
+    under the map's write lock, src/replica/dispatch.rs:188-196)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from rsos_hip.synth import make_records, to_host
+    base = to_host(make_records(schema, resident, seed=7, device="cuda"))
+    batch = to_host(make_records(schema, m, seed=8, device="cuda", random_keys=True))
+    cols = {k: np.concatenate([base[k], batch[k]]) for k in base}
+    sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+    recs = O.Records(sc, cols["keys"], cols.get("values"), cols.get("phys"), cols.get("logical"), cols.get("node"),
+                     cols.get("tags"))
+    t = O.FingerprintTreeMap(recs)
+    t.fill(0, resident)
+    t0 = time.perf_counter()
+    t.fill(resident, resident + m)
+    dt = time.perf_counter() - t0
+    return {"value": round(m / dt / 1e6, 3), "unit": "M records/s", "cores": 1, "kind": "port",
+            "sample": f"{m} random-key inserts into a {resident}-record FingerprintTreeMap "
+                      f"(oracle/oracle.c restatement, serial), {dt:.2f} s"}
 
 
 def spot_check(schema, cols, n):

@@ -46,7 +46,9 @@ typedef enum rh_status {
     RH_ERR_OOM = -3,         /* device allocation failed                                       */
     RH_ERR_UNSUPPORTED = -4, /* schema has no specialised kernel: encode on the host and use
                                 rh_lift_encoded_async (the generic canonical-bytes path)       */
-    RH_ERR_STATE = -5        /* call not valid in the store's current state                   */
+    RH_ERR_STATE = -5,       /* call not valid in the store's current state                   */
+    RH_ERR_DATA = -6         /* malformed snapshot / wire bytes (the reference's
+                                io::ErrorKind::InvalidData / bincode error)                    */
 } rh_status;
 
 /* Key encodings (rsos/src/encoding/serializer.rs):
@@ -210,6 +212,66 @@ int rh_store_apply_device(rh_store *store, const rh_columns *dev_cols, const uin
 int rh_store_compact(rh_store *store);
 int rh_store_set_compaction(rh_store *store, uint64_t divisor, uint64_t min_rows);
 int rh_store_stats(const rh_store *store, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions);
+
+/* ---- snapshot reload ------------------------------------------------------------------
+ * FileSnapshot (src/snapshot.rs:30-58): "RCNL", u32 LE format version 1, then bincode 1.3.3
+ * (fixint, LE) of PersistedState<K, V> (lww-register/src/persistence.rs:62-70), whose first
+ * field is entries: Vec<(K, Entry<Timestamp, V>)> (:32).  Reload replays the entries through
+ * just_insert_bulk (src/replicated_map/persistence.rs:143): every entry goes into the dated map
+ * and its projection (src/replica/write.rs:26-46,107-121), in file order, so a repeated key keeps
+ * its last entry.  The entries are located and decoded on the device; PersistedState.members
+ * and .tombstone_acks follow them at entries_end and stay with the host.
+ * Keys in the file: u32 / u64 as fixed LE; byte keys as [u8; L] (RH_FORM_ARRAY, a bincode tuple:
+ * the raw bytes) or Vec<u8> / String (RH_FORM_VEC: u64 length L, then the bytes).  Values of
+ * kind BYTES are Vec<u8> (u64 length, then the bytes).  Key and value lengths must be
+ * multiples of 4 (RH_ERR_UNSUPPORTED otherwise).                                            */
+typedef enum rh_key_form { RH_FORM_ARRAY = 0, RH_FORM_VEC = 1 } rh_key_form;
+
+typedef struct rh_snapshot_info {
+    uint64_t entries;     /* PersistedState.entries.len()                                  */
+    uint64_t tombstones;  /* entries holding State::Tombstone                               */
+    uint64_t entries_end; /* file offset of PersistedState.members (just past the entries)  */
+    uint64_t keys;        /* distinct keys loaded (< entries when a key repeats)            */
+} rh_snapshot_info;
+
+/* Check the 8-byte header (magic, version) and read the entry count; host bytes, len >= 16.
+ * RH_ERR_DATA with the reference's message on a short file, wrong magic or version.        */
+int rh_snapshot_header(const void *bytes, size_t len, uint64_t *entries);
+/* Decode the entries of a device-resident snapshot into device columns with room for `cap`
+ * rows.  keys / phys / logical / node / tags / values are all written (a tombstone's value
+ * row is zero-filled; tags = the State variant).  Synchronous on `stream`.                */
+int rh_snapshot_decode_device(const rh_schema *schema, int key_form, const void *dev_bytes, size_t len,
+                              const rh_columns *dev_out, size_t cap, rh_snapshot_info *info, void *stream);
+/* Reload: replace the contents of `dated` (record_kind DATED) and / or `projection`
+ * (PROJECTION) with a snapshot's entries; either store may be NULL, and both must have the
+ * same key and value kinds on the same device.  bytes_on_device: 0 = host bytes (copied to
+ * the device), 1 = device bytes.  info (nullable) reports what was read.                  */
+int rh_store_load_snapshot(rh_store *dated, rh_store *projection, int key_form, const void *bytes, size_t len,
+                           int bytes_on_device, rh_snapshot_info *info);
+
+/* ---- RangeAggregate wire codec ---------------------------------------------------------
+ * RangeAggregate<K> (rbsr/src/protocol.rs:63-88) under the gossip codec: bincode 1.3.3
+ * DefaultOptions, i.e. varint integers (gossip/src/bincode.rs:65-70; golden vector
+ * tests/wire_format.rs:37-62).  Per item: start bound (varint tag 0 = Unbounded,
+ * 1 = Included, then the key), end bound (0 = Unbounded, 1 = Excluded, then the key), the 32
+ * fingerprint bytes (rsos/src/fingerprint.rs:74-83), the size as a varint.  Keys: u32 / u64
+ * varint, [u8; L] raw bytes (RH_FORM_ARRAY), Vec<u8> varint length + bytes (RH_FORM_VEC).
+ * msg_tag >= 0 prefixes every item with that Message variant (0 = ComparisonItem,
+ * 3 = ValueComparisonItem, src/replica.rs:184-199), giving the byte stream send_messages_to
+ * packs into datagrams (src/replica/pacing.rs:200); msg_tag = -1 encodes bare items.
+ * Bound kinds are arrays of r bytes; keys are r * key_len bytes (rows of unbounded sides are
+ * ignored on encode and zeroed on decode).                                                 */
+/* out == NULL: only *out_len = the encoded length.  RH_ERR_ARG if cap < that length.      */
+int rh_wire_encode_range_aggregates(const rh_schema *schema, int key_form, int msg_tag, const uint8_t *start_kinds,
+                                    const void *start_keys, const uint8_t *end_kinds, const void *end_keys,
+                                    const rh_aggregate *aggregates, size_t r, uint8_t *out, size_t cap,
+                                    size_t *out_len);
+/* Decode items until the input ends or r_cap items are read (gossip::bincode::decode_stream,
+ * gossip/src/bincode.rs:79-100); *r_out items, *consumed bytes.  RH_ERR_DATA on malformed
+ * bytes (unknown tag, bad varint, truncated item, Vec length != key_len).                  */
+int rh_wire_decode_range_aggregates(const rh_schema *schema, int key_form, int msg_tag, const uint8_t *in, size_t len,
+                                    size_t r_cap, uint8_t *start_kinds, void *start_keys, uint8_t *end_kinds,
+                                    void *end_keys, rh_aggregate *aggregates, size_t *r_out, size_t *consumed);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,7 @@
 #include "../../include/rsos_hip.h"
 #include "internal.hpp"
 #include "lift_kernels.hpp"
+#include "snapshot_kernels.hpp"
 #include "store_kernels.hpp"
 
 namespace {
@@ -134,6 +135,10 @@ struct DevBuf {
 };
 
 }  // namespace
+
+namespace rh {
+int set_error(int code, const std::string &msg) { return fail(code, msg); }
+}  // namespace rh
 
 // ---- dispatch table over the instantiated shapes (schemas.def) -------------------------------
 namespace rh {
@@ -398,6 +403,7 @@ struct rh_store {
     DevBuf<rh_aggregate> q_out, q_bout, q_dout;
     DevBuf<uint8_t> q_keys;
     DevBuf<uint32_t> q_rank, q_drank;
+    DevBuf<uint8_t> snap;  // a host snapshot's bytes while it is decoded
     rh::Scratch scratch;
 
     uint64_t size() const { return (uint64_t)((int64_t)nb + dtotal); }
@@ -432,12 +438,17 @@ struct rh_store {
         dtotal = t;
         return RH_OK;
     }
-    int load_device(const rh_columns &c, size_t m) {
+    // Replace the contents with m records.  Sorted, duplicate-free input is required unless
+    // last_wins, which sorts on the device and keeps the last record of each repeated key --
+    // the result of inserting the records one by one (just_insert_bulk, src/replica/write.rs:107-121).
+    int load_device(const rh_columns &c, size_t m, bool last_wins = false) {
         int rc;
-        if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)))
+        if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
+            (rc = counts.ensure(4)))
             return rc;
         nd = 0;
         dtotal = 0;
+        nb = 0;
         if (m) {
             RH_HIP(hipMemcpyAsync(bkeys[cb].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
             if ((rc = lift_dispatch(schema, c, m, bfps[cb].p, nullptr, nullptr, nullptr, false, stream))) return rc;
@@ -447,11 +458,30 @@ struct rh_store {
         uint32_t bad = 0;
         if (m) RH_HIP(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
+        uint64_t kept = m;
         if (bad) {
-            nb = 0;
-            return fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
+            if (!last_wins) return fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
+            const int nxt = 1 - cb;
+            if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)))
+                return rc;
+            RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
+            RH_HIP(kops->sort_batch(bkeys[cb].p, bfps[cb].p, nullptr, m, scratch, bkeys[nxt].p, bfps[nxt].p, sops.p,
+                                    flag.p, stream));
+            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            uint32_t dup = 0;
+            RH_HIP(hipMemcpyAsync(&dup, flag.p, 4, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+            if (dup) {  // stable sort: within a run of equal keys the last record is last
+                RH_HIP(kops->dedup_last(bkeys[nxt].p, bfps[nxt].p, m, scratch, bkeys[cb].p, bfps[cb].p, counts.p,
+                                        stream));
+                if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+                RH_HIP(hipMemcpyAsync(&kept, counts.p, 8, hipMemcpyDeviceToHost, stream));
+                if ((rc = sync())) return rc;
+            } else {
+                cb = nxt;
+            }
         }
-        nb = m;
+        nb = kept;
         if ((rc = resum_base())) return rc;
         return sync();
     }
@@ -581,6 +611,7 @@ struct rh_store {
         dops.release(); cfps.release(); cops.release(); counts.release(); counts2.release(); flag.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
+        snap.release();
         scratch.release();
     }
 };
@@ -753,6 +784,191 @@ int rh_store_apply_device(rh_store *s, const rh_columns *dev_cols, const uint8_t
     if (n_new) *n_new = c[0];
     if (n_over) *n_over = c[1];
     if (n_del) *n_del = c[2];
+    return RH_OK;
+}
+
+}  // extern "C"
+
+// =================================================================================================
+// Snapshot reload (src/snapshot.rs:30-58; reload = just_insert_bulk, src/replicated_map/persistence.rs:143)
+namespace {
+
+int snapshot_header(const uint8_t *h, size_t len, uint64_t *n) {
+    // the checks and messages of decode_snapshot, src/snapshot.rs:60-98
+    if (len < 8)
+        return fail(RH_ERR_DATA, "snapshot is " + std::to_string(len) +
+                                     " bytes, shorter than the 8-byte format header (truncated, or a "
+                                     "pre-Entry/State snapshot without the versioned header)");
+    if (memcmp(h, "RCNL", 4) != 0) {
+        char m[64];
+        snprintf(m, sizeof m, "[%02x, %02x, %02x, %02x]", h[0], h[1], h[2], h[3]);
+        return fail(RH_ERR_DATA, std::string("snapshot magic ") + m +
+                                     " does not match [52, 43, 4e, 4c]; the file is not a reconcile snapshot, "
+                                     "or predates the versioned format");
+    }
+    uint32_t version;
+    memcpy(&version, h + 4, 4);
+    if (version != 1)
+        return fail(RH_ERR_DATA, "snapshot format version " + std::to_string(version) +
+                                     " is not supported by this build (expected 1); it was written by a "
+                                     "different reconcile version and must be migrated or discarded");
+    if (len < 16) return fail(RH_ERR_DATA, "snapshot body is truncated (io error: unexpected end of file)");
+    memcpy(n, h + 8, 8);
+    return RH_OK;
+}
+
+uint32_t gcd32(uint32_t a, uint32_t b) {
+    while (b) {
+        const uint32_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+int snapshot_format(const rh_schema &s, int key_form, size_t len, uint64_t n, rh::SnapFmt *f) {
+    if (key_form != RH_FORM_ARRAY && key_form != RH_FORM_VEC) return fail(RH_ERR_ARG, "bad key_form");
+    if (key_form == RH_FORM_VEC && s.key_kind != RH_KEY_BYTES) return fail(RH_ERR_ARG, "RH_FORM_VEC needs byte keys");
+    f->key_pre = key_form == RH_FORM_VEC ? 8 : 0;
+    f->key_len = key_row(s);
+    f->val_pre = s.value_kind == RH_VAL_BYTES ? 8 : 0;
+    f->val_len = value_row(s);
+    if (f->key_len % 4 || f->val_len % 4)
+        return fail(RH_ERR_UNSUPPORTED, "snapshot decode needs key and value lengths that are multiples of 4");
+    f->lt = f->key_pre + f->key_len + 20 + 4;  // key, Timestamp (u64 + u32 + u64), State variant
+    f->lp = f->lt + f->val_pre + f->val_len;
+    f->g = gcd32(f->lt, f->lp);
+    f->phases = f->lp / f->g;
+    f->seg = (uint64_t)f->g * ((32ull * f->lp + f->g - 1) / f->g);  // ~32 entries per segment
+    f->len = len;
+    f->base = 16;
+    if (n >= (1ull << 31)) return fail(RH_ERR_UNSUPPORTED, "snapshot has more than 2^31 entries");
+    if (n > (len - 16) / f->lt)
+        return fail(RH_ERR_DATA, "snapshot entry count " + std::to_string(n) + " exceeds what its " +
+                                     std::to_string(len) + " bytes can hold (io error: unexpected end of file)");
+    return RH_OK;
+}
+
+int snapshot_decode_into(const rh_schema &s, int key_form, const uint8_t *dev, size_t len, uint64_t n,
+                         const rh_columns &o, rh::Scratch &scr, hipStream_t st, rh_snapshot_info *info) {
+    rh::SnapFmt f;
+    int rc = snapshot_format(s, key_form, len, n, &f);
+    if (rc) return rc;
+    rh::SnapResult res;
+    int corrupt = 0;
+    RH_HIP(rh::snapshot_decode(f, dev, n, (uint8_t *)o.keys, (uint64_t *)o.phys, (uint32_t *)o.logical,
+                               (uint64_t *)o.node, (uint8_t *)o.tags, (uint8_t *)o.values, scr, st, &res, &corrupt));
+    if (scr.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+    if (corrupt)
+        return fail(RH_ERR_DATA, "snapshot entries are corrupt: " + std::to_string(res.parsed) + " of " +
+                                     std::to_string(n) + " entries parse (bad State variant, Vec length or "
+                                     "end of file)");
+    info->entries = n;
+    info->tombstones = res.tombstones;
+    info->entries_end = res.entries_end;
+    info->keys = n;
+    return RH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rh_snapshot_header(const void *bytes, size_t len, uint64_t *entries) {
+    if ((!bytes && len) || !entries) return fail(RH_ERR_ARG, "NULL");
+    return snapshot_header(static_cast<const uint8_t *>(bytes), len, entries);
+}
+
+int rh_snapshot_decode_device(const rh_schema *schema, int key_form, const void *dev_bytes, size_t len,
+                              const rh_columns *o, size_t cap, rh_snapshot_info *info, void *stream) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    if ((!dev_bytes && len) || !o) return fail(RH_ERR_ARG, "NULL");
+    if (!aligned16(dev_bytes)) return fail(RH_ERR_ARG, "snapshot bytes must be 16-byte aligned");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint8_t h[16] = {0};
+    const size_t hl = std::min<size_t>(len, 16);
+    if (hl) RH_HIP(hipMemcpyAsync(h, dev_bytes, hl, hipMemcpyDeviceToHost, st));
+    RH_HIP(hipStreamSynchronize(st));
+    uint64_t n = 0;
+    if ((rc = snapshot_header(h, len, &n))) return rc;
+    if (n > cap) return fail(RH_ERR_ARG, "snapshot has " + std::to_string(n) + " entries, more than cap");
+    if (n && ((key_row(*schema) && !o->keys) || (value_row(*schema) && !o->values) || !o->phys || !o->logical ||
+              !o->node || !o->tags))
+        return fail(RH_ERR_ARG, "output columns are NULL");
+    if (!aligned16(o->keys) || !aligned16(o->values) || !aligned16(o->phys) || !aligned16(o->node) ||
+        !aligned16(o->logical))
+        return fail(RH_ERR_ARG, "device columns must be 16-byte aligned");
+    rh::Scratch scr;
+    scr.stream = st;
+    rh_snapshot_info inf{};
+    rc = snapshot_decode_into(*schema, key_form, static_cast<const uint8_t *>(dev_bytes), len, n, *o, scr, st, &inf);
+    scr.release();
+    if (!rc && info) *info = inf;
+    return rc;
+}
+
+int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const void *bytes, size_t len,
+                           int on_device, rh_snapshot_info *info) {
+    if (!dated && !proj) return fail(RH_ERR_ARG, "no store given");
+    if (!bytes && len) return fail(RH_ERR_ARG, "bytes is NULL");
+    if (dated && dated->schema.record_kind != RH_REC_DATED) return fail(RH_ERR_ARG, "dated store must be DATED");
+    if (proj && proj->schema.record_kind != RH_REC_PROJECTION)
+        return fail(RH_ERR_ARG, "projection store must be PROJECTION");
+    if (dated && proj &&
+        (dated->schema.key_kind != proj->schema.key_kind || dated->schema.key_len != proj->schema.key_len ||
+         dated->schema.value_kind != proj->schema.value_kind || dated->schema.value_len != proj->schema.value_len ||
+         dated->device != proj->device))
+        return fail(RH_ERR_ARG, "dated and projection stores differ in key / value kind or device");
+    rh_store *a = dated ? dated : proj;
+    std::unique_lock<std::mutex> la(a->mu, std::defer_lock), lb;
+    if (dated && proj) {
+        lb = std::unique_lock<std::mutex>(proj->mu, std::defer_lock);
+        std::lock(la, lb);
+    } else {
+        la.lock();
+    }
+    RH_HIP(hipSetDevice(a->device));
+    int rc;
+    uint8_t h[16] = {0};
+    const size_t hl = std::min<size_t>(len, 16);
+    if (on_device) {
+        if (!aligned16(bytes)) return fail(RH_ERR_ARG, "snapshot bytes must be 16-byte aligned");
+        if (hl) RH_HIP(hipMemcpyAsync(h, bytes, hl, hipMemcpyDeviceToHost, a->stream));
+        RH_HIP(hipStreamSynchronize(a->stream));
+    } else if (hl) {
+        memcpy(h, bytes, hl);
+    }
+    uint64_t n = 0;
+    if ((rc = snapshot_header(h, len, &n))) return rc;
+    rh_schema ds = a->schema;
+    ds.record_kind = RH_REC_DATED;
+    rh::SnapFmt f;
+    if ((rc = snapshot_format(ds, key_form, len, n, &f))) return rc;
+    const uint8_t *dev = static_cast<const uint8_t *>(bytes);
+    if (!on_device) {
+        if ((rc = a->snap.ensure(len + 16))) return rc;
+        RH_HIP(hipMemcpyAsync(a->snap.p, bytes, len, hipMemcpyHostToDevice, a->stream));
+        dev = a->snap.p;
+    }
+    DevColumns &stg = a->staging;
+    const size_t kr = key_row(ds), vr = value_row(ds);
+    if ((rc = stg.keys.ensure(n * kr + 16)) || (rc = stg.values.ensure(n * vr + 16)) || (rc = stg.phys.ensure(n + 1)) ||
+        (rc = stg.node.ensure(n + 1)) || (rc = stg.logical.ensure(n + 1)) || (rc = stg.tags.ensure(n + 16)))
+        return rc;
+    stg.has_tags = true;
+    const rh_columns cols = stg.view(ds);
+    rh_snapshot_info inf{};
+    rc = snapshot_decode_into(ds, key_form, dev, len, n, cols, a->scratch, a->stream, &inf);
+    if (!on_device) a->snap.release();
+    if (rc) return rc;
+    for (rh_store *x : {dated, proj}) {
+        if (!x) continue;
+        RH_HIP(hipSetDevice(x->device));
+        if ((rc = x->load_device(cols, n, true))) return rc;
+        inf.keys = x->nb;
+    }
+    if (info) *info = inf;
     return RH_OK;
 }
 

@@ -254,6 +254,26 @@ __global__ void k_check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad) {
 
 // rank bounds of a key range in a sorted key array (std::ops::Bound: 0 unbounded, 1 included,
 // 2 excluded); an inverted range gives an empty one (rbsr/src/protocol.rs:230-232)
+// dedup_last: keep[j] = 1 unless row j + 1 has the same key
+template <int KK, int KL>
+__global__ void k_last_flags(const uint8_t *keys, uint64_t n, uint32_t *keep) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    keep[j] = (j + 1 == n || key_cmp<KK, KL>(keys + j * KL, keys + (j + 1) * KL) != 0) ? 1u : 0u;
+}
+
+template <int KL>
+__global__ void k_dedup_scatter(const uint8_t *keys, const uint8_t *fps, const uint32_t *keep, const uint32_t *pos,
+                                uint64_t n, uint8_t *okeys, uint8_t *ofps, uint64_t *counts) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    if (keep[j]) {
+        copy_bytes<KL>(okeys + (uint64_t)pos[j] * KL, keys + j * KL);
+        copy_bytes<32>(ofps + 32ull * pos[j], fps + 32 * j);
+    }
+    if (j + 1 == n) counts[0] = (uint64_t)pos[j] + keep[j];
+}
+
 template <int KK, int KL>
 __global__ void k_bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key, int lo_kind, const uint8_t *hi_key,
                          int hi_kind, uint64_t *qlo, uint64_t *qhi) {
@@ -446,6 +466,22 @@ struct KeyOps final : StoreKeyOps {
     hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) override {
         if (n < 2) return hipSuccess;
         hipLaunchKernelGGL((k_check_sorted<KK, KL>), g1(n), dim3(256), 0, st, keys, n, bad);
+        return hipGetLastError();
+    }
+
+    hipError_t dedup_last(const uint8_t *keys, const uint8_t *fps, uint64_t n, Scratch &s, uint8_t *okeys,
+                          uint8_t *ofps, uint64_t *counts, hipStream_t st) override {
+        if (n == 0) return hipMemsetAsync(counts, 0, 8, st);
+        hipError_t e;
+        uint32_t *keep = s.u32(11, n), *pos = s.u32(12, n);
+        if (s.err) return s.err;
+        hipLaunchKernelGGL((k_last_flags<KK, KL>), g1(n), dim3(256), 0, st, keys, n, keep);
+        size_t tb = 0;
+        if ((e = rocprim::exclusive_scan(nullptr, tb, keep, pos, 0u, n, rocprim::plus<uint32_t>(), st))) return e;
+        void *tmp = s.bytes(tb);
+        if (s.err) return s.err;
+        if ((e = rocprim::exclusive_scan(tmp, tb, keep, pos, 0u, n, rocprim::plus<uint32_t>(), st))) return e;
+        hipLaunchKernelGGL((k_dedup_scatter<KL>), g1(n), dim3(256), 0, st, keys, fps, keep, pos, n, okeys, ofps, counts);
         return hipGetLastError();
     }
 

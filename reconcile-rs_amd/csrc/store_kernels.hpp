@@ -85,6 +85,10 @@ struct StoreKeyOps {
                              const uint8_t *spay, const uint8_t *sops, uint64_t m, int payload, Scratch &s,
                              uint8_t *okeys, uint8_t *opay, uint64_t *counts, hipStream_t st) = 0;
     virtual hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) = 0;
+    // keep the last row of every run of equal keys of a key-sorted run (a stable sort keeps
+    // input order within a run, so this is "the last insert wins"); counts[0] = rows kept
+    virtual hipError_t dedup_last(const uint8_t *keys, const uint8_t *fps, uint64_t n, Scratch &s, uint8_t *okeys,
+                                  uint8_t *ofps, uint64_t *counts, hipStream_t st) = 0;
     virtual hipError_t bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key, int lo_kind,
                               const uint8_t *hi_key, int hi_kind, uint64_t *qlo, uint64_t *qhi, hipStream_t st) = 0;
     // the key type's Ord on the host (for argument checks)

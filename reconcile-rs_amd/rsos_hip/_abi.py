@@ -12,12 +12,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librsos_hip.so")
 
 # rh_status
-OK, ERR_ARG, ERR_HIP, ERR_OOM, ERR_UNSUPPORTED, ERR_STATE = 0, -1, -2, -3, -4, -5
+OK, ERR_ARG, ERR_HIP, ERR_OOM, ERR_UNSUPPORTED, ERR_STATE, ERR_DATA = 0, -1, -2, -3, -4, -5, -6
 # schema enums (rsos_hip.h)
 KEY_UNIT, KEY_U32, KEY_U64, KEY_BYTES = 0, 1, 2, 3
 VAL_UNIT, VAL_U32, VAL_U64, VAL_BYTES = 0, 1, 2, 3
 REC_PLAIN, REC_DATED, REC_PROJECTION = 0, 1, 2
 BLOCK, SUPER = 256, 65536
+FORM_ARRAY, FORM_VEC = 0, 1  # rh_key_form: [u8; L] | Vec<u8> / String
 
 
 class Schema(C.Structure):
@@ -32,6 +33,11 @@ class Columns(C.Structure):
 
 class Aggregate(C.Structure):
     _fields_ = [("fingerprint", C.c_uint64 * 4), ("size", C.c_uint64)]
+
+
+class SnapshotInfo(C.Structure):
+    _fields_ = [("entries", C.c_uint64), ("tombstones", C.c_uint64), ("entries_end", C.c_uint64),
+                ("keys", C.c_uint64)]
 
 
 # (name, restype, argtypes) -- every entry point include/rsos_hip.h declares
@@ -72,6 +78,14 @@ SIGNATURES = [
     ("rh_store_compact", C.c_int, [P]),
     ("rh_store_set_compaction", C.c_int, [P, C.c_uint64, C.c_uint64]),
     ("rh_store_stats", C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("rh_snapshot_header", C.c_int, [VP, SZ, C.POINTER(C.c_uint64)]),
+    ("rh_snapshot_decode_device", C.c_int, [C.POINTER(Schema), C.c_int, VP, SZ, C.POINTER(Columns), SZ,
+                                            C.POINTER(SnapshotInfo), VP]),
+    ("rh_store_load_snapshot", C.c_int, [P, P, C.c_int, VP, SZ, C.c_int, C.POINTER(SnapshotInfo)]),
+    ("rh_wire_encode_range_aggregates", C.c_int, [C.POINTER(Schema), C.c_int, C.c_int, U8P, VP, U8P, VP, P, SZ,
+                                                  U8P, SZ, C.POINTER(C.c_size_t)]),
+    ("rh_wire_decode_range_aggregates", C.c_int, [C.POINTER(Schema), C.c_int, C.c_int, U8P, SZ, SZ, U8P, VP, U8P,
+                                                  VP, P, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
 ]
 
 _lib = None

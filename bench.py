@@ -43,6 +43,9 @@ CONFIGS = {
                   "benches/bench.rs fill shape: FingerprintTreeMap<u32,u32>"),
     "config5": ("bytes16", "bytes64", "dated", 100_000_000,
                 "BASELINE configs[4]: 1M random inserts per batch into a 100M-record resident map"),
+    "snapshot": ("bytes16", "bytes64", "dated", 10_000_000,
+                 "snapshot reload (SURVEY 8f row 4): RCNL v1 file of 10M entries (16 B key / 64 B value, "
+                 "10% tombstones) resident in HBM -> dated + projection stores"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec)
 
@@ -89,6 +92,8 @@ def main():
 
     if args.config == "config5":
         return incremental(args, world, rank, dev, dist)
+    if args.config == "snapshot":
+        return reload(args, world, rank, dev, dist)
     kname, vname, kind, n_default, desc = CONFIGS[args.config]
     n = args.records or n_default
     schema = getattr(RecordSchema, kind)(kname, vname)
@@ -261,6 +266,111 @@ def incremental(args, world, rank, dev, dist):
     st.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def reload(args, world, rank, dev, dist):
+    """Snapshot reload: one step = rh_store_load_snapshot of a device-resident RCNL file into the
+    dated and the projection store (entry walk + decode + two lifts + sort check + sums), i.e.
+    ReplicatedMap::with_persistence's replay (src/replicated_map/persistence.rs:108-143)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, lift_records, range_aggregates, reduce_blocks
+    from rsos_hip.snapshot import decode_entries_device, load_snapshot
+    from rsos_hip.synth import make_records, make_snapshot
+    kname, vname, kind, n_default, desc = CONFIGS["snapshot"]
+    n = args.records or n_default
+    sd, sp = RecordSchema.dated(kname, vname), RecordSchema.projection(kname, vname)
+    cols = make_records(sd, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world,
+                        tombstone_fraction=0.1)
+    blob = make_snapshot(cols, sd)
+    file_bytes = blob.numel()
+    # the expected dated root: Σ GPU lifts of the source rows (checked after timing)
+    fps, bs = lift_records(sd, cols)
+    want = range_aggregates(fps, bs, reduce_blocks(bs), torch.tensor([0], device=dev),
+                            torch.tensor([n], device=dev)).cpu()
+    del fps, bs
+    dated, proj = GpuFingerprintStore(sd, device=dev.index), GpuFingerprintStore(sp, device=dev.index)
+    for _ in range(args.warmup):
+        load_snapshot(blob, dated, proj)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        info = load_snapshot(blob, dated, proj)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    root = dated.aggregate()
+    ok = root.size == n == info.keys and root.fingerprint.limbs == tuple(int(x) & (2**64 - 1) for x in want[0, :4])
+    if not ok:
+        raise SystemExit("bench: reloaded root aggregate differs from the lifted source rows")
+    # roofline of the entry decode (walk + offsets + column scatter), timed on torch's stream:
+    # algorithmic bytes = the file read once + the decoded columns written once
+    ev = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        got, _ = decode_entries_device(sd, blob)
+        e1.record()
+        ev.append((e0, e1))
+        del got
+    torch.cuda.synchronize()
+    dec_s = min(a.elapsed_time(b) for a, b in ev) / 1e3
+    col_bytes = n * (sd.key_row + 8 + 4 + 8 + 1 + sd.value_row)
+    achieved = (file_bytes + col_bytes) / dec_s / 1e9
+    if rank == 0:
+        recs = n * args.steps * world
+        line = {
+            "metric": "snapshot reload into dated + projection GPU stores (M entries/s)",
+            "value": round(recs / elapsed / 1e6, 2), "unit": "M entries/s",
+            "gib_s_file": round(file_bytes * args.steps * world / elapsed / 2**30, 2),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded): sorted unique keys, 10% tombstones, file bytes resident in HBM",
+            "config": {"workload": desc, "entries_per_gpu": n, "file_bytes": file_bytes,
+                       "parallelism": f"key-range shards x{world}"},
+            "tombstones": info.tombstones,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "snapshot decode (k_snap_walk/up/down/offsets + k_snap_decode)",
+                         "kernel_avg_us": round(dec_s * 1e6, 1)},
+            "root_check": "dated root == Σ lift(source rows)",
+        }
+        if args.cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline_reload(sd, sp, cols, args.cpu_sample or 1_000_000)
+        print(json.dumps(line), flush=True)
+    dated.close()
+    proj.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_reload(sd, sp, cols, m):
+    """The reference's replay restated (oracle/oracle.c FingerprintTreeMap): just_insert_bulk
+    inserts every entry into the dated map and into the projection, serially under the write
+    lock (src/replica/write.rs:26-46,107-121).  The bincode decode is not timed."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from rsos_hip.synth import to_host
+    h = to_host(cols, 0, m)
+    dt = 0.0
+    for s in (sd, sp):
+        sc = O.Schema(s.key_kind, s.key_len, s.value_kind, s.value_len, s.record_kind, 0)
+        dated = s.record_kind == O.REC_DATED
+        recs = O.Records(sc, h["keys"], h["values"], h["phys"] if dated else None, h["logical"] if dated else None,
+                         h["node"] if dated else None, h["tags"])
+        t = O.FingerprintTreeMap(recs)
+        t0 = time.perf_counter()
+        t.fill(0, m)
+        dt += time.perf_counter() - t0
+    return {"value": round(m / dt / 1e6, 3), "unit": "M entries/s", "cores": 1, "kind": "port",
+            "sample": f"replay of the first {m} entries into two FingerprintTreeMaps (dated + projection; "
+                      f"oracle/oracle.c restatement, serial, decode not timed), {dt:.2f} s"}
 
 
 def cpu_baseline_incremental(schema, m, resident):

@@ -276,12 +276,49 @@ __device__ __forceinline__ void store_sum(uint8_t *dst, uint64_t g, const uint32
     o[1] = make_uint4(f[4], f[5], f[6], f[7]);
 }
 
-// lift one record (present or tombstone) of schema (KK,KL,VK,VL,RK)
-template <int KK, int KL, int VK, int VL, int RK>
+// A present record and a tombstone of the same key share block 0 up to the State variant word
+// (the tombstone's last word), so when the tombstone fits one block the two are hashed with
+// one block-0 compression whose words, length and flags are chosen per lane; only present
+// lanes go on to the value blocks.  A wave mixing both kinds then runs NB compressions, not
+// NB + 1 as two divergent paths would.
+template <class L, int KK, int RK>
+__device__ __forceinline__ void hash_merged(const uint32_t *kw, const uint32_t *sw, bool tomb, const uint8_t *vrow,
+                                            uint32_t h[8]) {
+    constexpr int NW = L::LEN / 4, NB = (L::LEN + 63) / 64, TW = L::LEN_TOMB / 4;
+    static_assert(L::SMALL && L::LEN_TOMB <= 64 && TW >= 1, "tombstone must fit block 0");
+    uint32_t w[NW];
+    build_prefix<L, KK, RK>(kw, sw, false, w);  // present words: variant 0 at TW - 1
+    if constexpr (L::VW > 0) ldw<L::VW, L::ROW_ALIGN>(vrow, w + L::PW);
+    uint32_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t pres = j < NW ? w[j] : 0u;
+        m[j] = j < TW - 1 ? pres : j == TW - 1 ? (tomb ? 1u : 0u) : (tomb ? 0u : pres);
+    }
+    cv_iv(h);
+    const uint32_t blen0 = tomb ? (uint32_t)L::LEN_TOMB : (uint32_t)(NB == 1 ? L::LEN : 64);
+    const uint32_t fl0 = CHUNK_START | ((tomb || NB == 1) ? (CHUNK_END | ROOT) : 0u);
+    compress(h, m, 0, 0, blen0, fl0);
+    if (!tomb) {
+#pragma unroll
+        for (int b = 1; b < NB; b++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) m[j] = (16 * b + j < NW) ? w[16 * b + j] : 0u;
+            const uint32_t flags = b == NB - 1 ? (CHUNK_END | ROOT) : 0u;
+            const uint32_t blen = b == NB - 1 ? (uint32_t)(L::LEN - 64 * b) : 64u;
+            compress(h, m, 0, 0, blen, flags);
+        }
+    }
+}
+
+// lift one record (present or tombstone) of schema (KK,KL,VK,VL,RK); TAGS: tomb varies per lane
+template <int KK, int KL, int VK, int VL, int RK, bool TAGS = true>
 __device__ __forceinline__ void lift_record(const uint32_t *kw, const uint32_t *sw, bool tomb,
                                             const uint8_t *vrow, uint32_t h[8]) {
     using L = Layout<KK, KL, VK, VL, RK>;
-    if (RK != REC_PLAIN && tomb) {
+    if constexpr (TAGS && RK != REC_PLAIN && L::SMALL && L::LEN_TOMB <= 64) {
+        hash_merged<L, KK, RK>(kw, sw, tomb, vrow, h);
+    } else if (RK != REC_PLAIN && tomb) {
         constexpr int TW = L::LEN_TOMB / 4;
         uint32_t w[TW];
         build_prefix<L, KK, RK>(kw, sw, true, w);
@@ -326,10 +363,10 @@ __global__ __launch_bounds__(LIFT_THREADS) void k_lift(DevCols c, uint64_t n, ui
         if constexpr (RK == REC_DATED) load_stamp(cb, t, sw);
         const bool tomb = TAGS ? (cb.tags[t] != 0) : false;
         const uint8_t *vrow = cb.values + t * (uint32_t)L::VAL_ROW;
-        lift_record<KK, KL, VK, VL, RK>(kw, sw, tomb, vrow, h);
+        lift_record<KK, KL, VK, VL, RK, TAGS>(kw, sw, tomb, vrow, h);
         store_fp(fps + b0 * 32, t, h);
         if constexpr (DUAL) {
-            lift_record<KK, KL, VK, VL, REC_PROJECTION>(kw, sw, tomb, vrow, h2);
+            lift_record<KK, KL, VK, VL, REC_PROJECTION, TAGS>(kw, sw, tomb, vrow, h2);
             store_fp(fps2 + b0 * 32, t, h2);
         }
     }

@@ -535,14 +535,14 @@ struct rh_store {
         RH_HIP(kops->search(bkeys[cb].p, nb, skeys.p, m, rank_b, present_b, stream));
         RH_HIP(kops->search(dkeys[cd].p, nd, skeys.p, m, rank_d, present_d, stream));
         // 4. the batch's delta records, then merge them into the delta run
-        RH_HIP(hipMemsetAsync(counts.p, 0, 24, stream));
         RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d, dpay[cd].p,
-                                      bpay.p, dops.p, counts.p, stream));
+                                      bpay.p, dops.p, counts.p, scratch, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         const int nxt = 1 - cd;
         if ((rc = dkeys[nxt].ensure((nd + m) * kl + 64)) || (rc = dpay[nxt].ensure((nd + m) * sizeof(rh::DeltaRec) + 64)))
             return rc;
         RH_HIP(kops->merge(dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p, dops.p, m, sizeof(rh::DeltaRec), scratch,
-                           dkeys[nxt].p, dpay[nxt].p, counts2.p, stream));
+                           dkeys[nxt].p, dpay[nxt].p, counts2.p, stream, rank_d, present_d));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         uint64_t c2[3];
         RH_HIP(hipMemcpyAsync(out, counts.p, 24, hipMemcpyDeviceToHost, stream));
@@ -839,7 +839,11 @@ int snapshot_format(const rh_schema &s, int key_form, size_t len, uint64_t n, rh
     f->lp = f->lt + f->val_pre + f->val_len;
     f->g = gcd32(f->lt, f->lp);
     f->phases = f->lp / f->g;
-    f->seg = (uint64_t)f->g * ((32ull * f->lp + f->g - 1) / f->g);  // ~32 entries per segment
+    // ~16 entries per segment, and a run of segments + one entry must fit the 32 KiB LDS stage
+    f->seg = (uint64_t)f->g * ((16ull * f->lp + f->g - 1) / f->g);
+    if (f->seg + f->lp + 48 > 32768) f->seg = (uint64_t)f->g * ((32768ull - f->lp - 48) / f->g);
+    if (f->lp + 48 > 32768 || f->seg < f->g || f->phases > 256)
+        return fail(RH_ERR_UNSUPPORTED, "snapshot entries too long for the device decoder");
     f->len = len;
     f->base = 16;
     if (n >= (1ull << 31)) return fail(RH_ERR_UNSUPPORTED, "snapshot has more than 2^31 entries");
@@ -899,11 +903,19 @@ int rh_snapshot_decode_device(const rh_schema *schema, int key_form, const void 
     if (!aligned16(o->keys) || !aligned16(o->values) || !aligned16(o->phys) || !aligned16(o->node) ||
         !aligned16(o->logical))
         return fail(RH_ERR_ARG, "device columns must be 16-byte aligned");
-    rh::Scratch scr;
+    // the decode tables are kept per device between calls (the call is synchronous, so the
+    // next call may reuse them on any stream)
+    static std::mutex scr_mu;
+    static std::vector<rh::Scratch> scr_by_dev;
+    int dev = 0;
+    RH_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(scr_mu);
+    if ((int)scr_by_dev.size() <= dev) scr_by_dev.resize(dev + 1);
+    rh::Scratch &scr = scr_by_dev[dev];
     scr.stream = st;
+    scr.err = hipSuccess;
     rh_snapshot_info inf{};
     rc = snapshot_decode_into(*schema, key_form, static_cast<const uint8_t *>(dev_bytes), len, n, *o, scr, st, &inf);
-    scr.release();
     if (!rc && info) *info = inf;
     return rc;
 }

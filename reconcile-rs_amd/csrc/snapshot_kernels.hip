@@ -6,17 +6,21 @@
 // (:32): u64 count, then the entries back to back.  An entry's length depends on its State
 // variant (a tombstone carries no value), so entry i's offset depends on every variant before
 // it -- a serial chain through the whole file.  It is broken up like this:
-//   1. the body is cut into segments of `seg` bytes.  Entry starts are multiples of
-//      g = gcd(tombstone len, present len) past the body start, and the first entry starting
-//      in a segment lies within one present-entry length of its start, so there are only
-//      P = lp / g candidate positions.  One thread per (segment, candidate) walks the segment
-//      and records where the chain leaves it and how many entries it crossed (or that no
-//      valid entry starts there: bad variant, wrong Vec length, past the end of the file);
+//   1. the body is cut into segments of `seg` bytes (~16 entries).  Entry starts are multiples
+//      of g = gcd(tombstone len, present len) past the body start, and the first entry starting
+//      in a segment lies within one present-entry length of the segment start, so there are
+//      only P = lp / g candidate positions.  A workgroup stages a run of segments in LDS
+//      (16-byte coalesced loads) and one lane per (segment, candidate) walks its segment in LDS,
+//      recording where the chain leaves the segment and how many entries it crossed (or that
+//      no valid entry starts there: bad variant, wrong Vec length, past the end of the file);
 //   2. the per-segment transfer functions are composed up a tree (fan-out 32) and the true
-//      entry position of every segment is pushed back down from the file's first entry;
-//   3. one thread per segment re-walks from its true position writing entry offsets, and a
-//      wide copy kernel scatters the entries' dwords into the store's columns.
-// Steps 1 and 3 read the body twice at HBM rate; step 2 touches P words per segment.
+//      first-entry position and entry index of every segment are pushed back down from the
+//      file's first entry;
+//   3. a workgroup stages a run of segments in LDS again, one lane per segment re-walks it from
+//      the true position listing entry offsets in LDS, and the workgroup writes its contiguous
+//      range of entries into every column with coalesced stores (the AoS -> SoA transpose).
+// HBM traffic: the body is read twice (steps 1 and 3) and the columns written once; step 2
+// touches P words per segment.
 #include <algorithm>
 #include <vector>
 
@@ -28,38 +32,78 @@ namespace {
 
 constexpr uint32_t SNAP_BAD = 0xffffffffu;
 constexpr uint32_t SNAP_FAN = 32;
+constexpr uint32_t SNAP_LDS = 32768;  // staged bytes per workgroup
 
-__device__ __forceinline__ uint32_t ld32(const uint8_t *b, uint64_t p) { return *reinterpret_cast<const uint32_t *>(b + p); }
-__device__ __forceinline__ uint64_t ld64(const uint8_t *b, uint64_t p) {
-    return (uint64_t)ld32(b, p) | ((uint64_t)ld32(b, p + 4) << 32);
+// A run of the blob staged in LDS: bytes [a, a + 4 * words) (a 16-aligned), zero past the end.
+struct Img {
+    const uint32_t *w;
+    uint64_t a;
+    __device__ __forceinline__ uint32_t ld32(uint64_t p) const { return w[(p - a) >> 2]; }
+    __device__ __forceinline__ uint64_t ld64(uint64_t p) const {
+        return (uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32);
+    }
+};
+
+// stage blob bytes [a, b) (a 16-aligned) into lds; bytes at or past `len` read as 0
+__device__ __forceinline__ void stage(const uint8_t *blob, uint64_t len, uint64_t a, uint64_t b, uint32_t *lds) {
+    for (uint64_t q = a + 16ull * threadIdx.x; q < b; q += 16ull * blockDim.x) {
+        uint4 v;
+        if (q + 16 <= len) {
+            v = *reinterpret_cast<const uint4 *>(blob + q);
+        } else {
+            uint32_t t[4];
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                uint32_t x = 0;
+                for (int k = 0; k < 4; k++) {
+                    const uint64_t o = q + 4 * d + k;
+                    if (o < len) x |= (uint32_t)blob[o] << (8 * k);
+                }
+                t[d] = x;
+            }
+            v = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+        *reinterpret_cast<uint4 *>(lds + ((q - a) >> 2)) = v;
+    }
 }
 
-// length of the entry starting at p, or 0 if no valid entry starts there
-__device__ __forceinline__ uint32_t entry_len(const uint8_t *b, const SnapFmt &f, uint64_t p) {
+// length of the entry starting at p, or 0 if no valid entry starts there.  The image must
+// cover p + lp or the end of the file.
+__device__ __forceinline__ uint32_t entry_len(const Img &m, const SnapFmt &f, uint64_t p) {
     if (p + f.lt > f.len) return 0;
-    if (f.key_pre && ld64(b, p) != f.key_len) return 0;
-    const uint32_t v = ld32(b, p + f.key_pre + f.key_len + 20);
+    if (f.key_pre && m.ld64(p) != f.key_len) return 0;
+    const uint32_t v = m.ld32(p + f.key_pre + f.key_len + 20);
     if (v == 1) return f.lt;
     if (v != 0 || p + f.lp > f.len) return 0;
-    if (f.val_pre && ld64(b, p + f.lt) != f.val_len) return 0;
+    if (f.val_pre && m.ld64(p + f.lt) != f.val_len) return 0;
     return f.lp;
 }
 
-// step 1: transfer function of every (segment, candidate first-entry position)
-__global__ void k_snap_walk(const uint8_t *b, SnapFmt f, uint64_t nseg, uint32_t *ex, uint32_t *cnt) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nseg * f.phases) return;
-    const uint64_t s = t / f.phases;
-    const uint32_t ph = (uint32_t)(t - s * f.phases);
-    const uint64_t end = f.base + (s + 1) * f.seg;
-    uint64_t p = f.base + s * f.seg + (uint64_t)ph * f.g;
+__device__ __forceinline__ uint64_t seg_start(const SnapFmt &f, uint64_t s) { return f.base + s * f.seg; }
+
+// step 1: transfer function of every (segment, candidate first-entry position); G segments
+// per workgroup, lane = segment * P + candidate
+__global__ __launch_bounds__(256) void k_snap_walk(const uint8_t *blob, SnapFmt f, uint64_t nseg, uint32_t G,
+                                                   uint32_t *ex, uint32_t *cnt) {
+    extern __shared__ uint32_t lds[];
+    const uint64_t s0 = (uint64_t)blockIdx.x * G;
+    const uint32_t nG = (uint32_t)std::min<uint64_t>(G, nseg - s0);
+    const uint64_t a = seg_start(f, s0) & ~15ull;
+    const uint64_t b = std::min<uint64_t>(seg_start(f, s0 + nG) + f.lp, f.len);
+    stage(blob, f.len, a, b, lds);
+    __syncthreads();
+    const uint32_t gs = threadIdx.x / f.phases, ph = threadIdx.x - gs * f.phases;
+    if (gs >= nG) return;
+    const Img m{lds, a};
+    const uint64_t s = s0 + gs, end = seg_start(f, s + 1);
+    uint64_t p = seg_start(f, s) + (uint64_t)ph * f.g;
     uint32_t c = 0, x;
     for (;;) {
         if (p >= end) {
             x = (uint32_t)((p - end) / f.g);
             break;
         }
-        const uint32_t L = entry_len(b, f, p);
+        const uint32_t L = entry_len(m, f, p);
         if (!L) {
             x = SNAP_BAD;
             break;
@@ -67,8 +111,8 @@ __global__ void k_snap_walk(const uint8_t *b, SnapFmt f, uint64_t nseg, uint32_t
         p += L;
         c++;
     }
-    ex[t] = x;
-    cnt[t] = c;
+    ex[s * f.phases + ph] = x;
+    cnt[s * f.phases + ph] = c;
 }
 
 // step 2 (up): compose the transfer functions of SNAP_FAN consecutive groups
@@ -113,65 +157,106 @@ __global__ void k_snap_down(const uint32_t *ex, const CIn *cnt, uint64_t nl, uin
     }
 }
 
-// step 3a: entry offsets.  res[0] = end of entry n-1, res[1] = inconsistency flag
-__global__ void k_snap_offsets(const uint8_t *b, SnapFmt f, uint64_t nseg, const uint32_t *start,
-                               const uint64_t *basev, uint64_t n, uint64_t *off, unsigned long long *res) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg) return;
-    const uint32_t x = start[s];
-    uint64_t i = basev[s];
-    if (x == SNAP_BAD || i >= n) return;
-    const uint64_t end = f.base + (s + 1) * f.seg;
-    uint64_t p = f.base + s * f.seg + (uint64_t)x * f.g;
-    while (p < end && i < n) {
-        const uint32_t L = entry_len(b, f, p);
-        if (!L) {
-            atomicOr(res + 1, 1ull);
-            return;
-        }
-        off[i] = p;
-        if (i == n - 1) res[0] = p + L;
-        p += L;
-        i++;
-    }
-}
-
-// step 3b: scatter entry dwords into the columns.  Word w of an entry's W:
-//   [0, K4) key | phys lo, phys hi, logical, node lo, node hi | variant | [0, V4) value
-__global__ __launch_bounds__(256) void k_snap_decode(const uint8_t *b, SnapFmt f, const uint64_t *off, uint64_t n,
-                                                     uint32_t R, uint32_t *keys, uint32_t *phys, uint32_t *logical,
+// step 3: G segments per workgroup -> their entries [r0, r1) into the columns.
+// res[0] = end of entry n-1, res[1] = inconsistency flag, res[2] = tombstones
+__global__ __launch_bounds__(256) void k_snap_decode(const uint8_t *blob, SnapFmt f, uint64_t nseg, uint32_t G,
+                                                     uint32_t list_cap, const uint32_t *start, const uint64_t *basev,
+                                                     uint64_t n, uint32_t *keys, uint32_t *phys, uint32_t *logical,
                                                      uint32_t *node, uint8_t *tags, uint32_t *values,
-                                                     unsigned long long *tomb) {
-    const uint32_t K4 = f.key_len / 4, V4 = f.val_len / 4, W = K4 + 6 + V4;
-    uint32_t my_tomb = 0;
-    for (uint64_t r0 = (uint64_t)blockIdx.x * R; r0 < n; r0 += (uint64_t)gridDim.x * R) {
-        const uint32_t rows = (uint32_t)std::min<uint64_t>(R, n - r0);
-        for (uint32_t k = threadIdx.x; k < rows * W; k += blockDim.x) {
-            const uint32_t lr = k / W, w = k - lr * W;
-            const uint64_t i = r0 + lr, p = off[i];
-            const uint64_t stamp = p + f.key_pre + f.key_len;
-            if (w < K4) {
-                keys[i * K4 + w] = ld32(b, p + f.key_pre + 4ull * w);
-            } else if (w < K4 + 5) {
-                const uint32_t q = w - K4, v = ld32(b, stamp + 4ull * q);
-                if (q < 2) phys[2 * i + q] = v;
-                else if (q == 2) logical[i] = v;
-                else node[2 * i + (q - 3)] = v;
-            } else if (w == K4 + 5) {
-                const uint32_t v = ld32(b, stamp + 20);
-                tags[i] = (uint8_t)v;
-                my_tomb += v;
-            } else {
-                const uint32_t q = w - K4 - 6;
-                uint32_t v = 0;
-                if (ld32(b, stamp + 20) == 0) v = ld32(b, p + f.lt + f.val_pre + 4ull * q);
-                values[i * V4 + q] = v;
+                                                     unsigned long long *res, uint32_t *tomb_part) {
+    extern __shared__ uint32_t lds[];
+    const uint64_t s0 = (uint64_t)blockIdx.x * G;
+    const uint32_t nG = (uint32_t)std::min<uint64_t>(G, nseg - s0);
+    const uint64_t r0 = basev[s0];
+    if (start[s0] == SNAP_BAD || r0 >= n) {  // the whole group is past entry n-1
+        if (threadIdx.x == 0) tomb_part[blockIdx.x] = 0;
+        return;
+    }
+    const uint64_t r1 = std::min<uint64_t>(s0 + nG < nseg ? basev[s0 + nG] : n, n);
+    const uint64_t a = seg_start(f, s0) & ~15ull;
+    const uint64_t b = std::min<uint64_t>(seg_start(f, s0 + nG) + f.lp, f.len);
+    const uint32_t img_words = (uint32_t)(((b - a) + 15) / 16 * 4);
+    uint32_t *list = lds + img_words;  // entry offsets relative to a
+    stage(blob, f.len, a, b, lds);
+    __syncthreads();
+    const Img m{lds, a};
+    if (threadIdx.x < nG) {  // one lane per segment lists its entries (nG <= blockDim)
+        const uint64_t s = s0 + threadIdx.x;
+        const uint32_t x = start[s];
+        uint64_t i = basev[s];
+        if (x != SNAP_BAD) {
+            const uint64_t end = seg_start(f, s + 1);
+            uint64_t p = seg_start(f, s) + (uint64_t)x * f.g;
+            while (p < end && i < r1) {
+                const uint32_t L = entry_len(m, f, p);
+                if (!L || i - r0 >= list_cap) {
+                    atomicOr(res + 1, 1ull);
+                    break;
+                }
+                list[i - r0] = (uint32_t)(p - a);
+                if (i == n - 1) res[0] = p + L;
+                p += L;
+                i++;
             }
         }
     }
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)(r1 - r0);
+    const uint32_t K4 = f.key_len / 4, V4 = f.val_len / 4;
+    const uint32_t o_key = f.key_pre, o_stamp = f.key_pre + f.key_len, o_var = o_stamp + 20, o_val = f.lt + f.val_pre;
+    // every column's rows [r0, r1) are contiguous: lane j writes dword j of the range
+    for (uint32_t j = threadIdx.x; j < cnt * K4; j += blockDim.x) {
+        const uint32_t e = j / K4, q = j - e * K4;
+        keys[r0 * K4 + j] = lds[(list[e] + o_key) / 4 + q];
+    }
+    for (uint32_t j = threadIdx.x; j < cnt * 2; j += blockDim.x) {
+        const uint32_t e = j >> 1, q = j & 1;
+        phys[r0 * 2 + j] = lds[(list[e] + o_stamp) / 4 + q];
+        node[r0 * 2 + j] = lds[(list[e] + o_stamp + 12) / 4 + q];
+    }
+    uint32_t my_tomb = 0;
+    for (uint32_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+        logical[r0 + e] = lds[(list[e] + o_stamp + 8) / 4];
+        const uint32_t v = lds[(list[e] + o_var) / 4];
+        tags[r0 + e] = (uint8_t)v;
+        my_tomb += v;
+    }
+    for (uint32_t j = threadIdx.x; j < cnt * V4; j += blockDim.x) {
+        const uint32_t e = j / V4, q = j - e * V4;
+        const uint32_t base = list[e];
+        values[r0 * V4 + j] = lds[(base + o_var) / 4] == 0 ? lds[(base + o_val) / 4 + q] : 0u;
+    }
+    // per-workgroup tombstone count (a same-address atomic per workgroup would serialise
+    // ~10^5 workgroups in the L2 atomic unit); summed by k_snap_sum
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) my_tomb += __shfl_xor(my_tomb, m, 64);
-    if ((threadIdx.x & 63) == 0 && my_tomb) atomicAdd(tomb, (unsigned long long)my_tomb);
+    for (int k = 32; k >= 1; k >>= 1) my_tomb += __shfl_xor(my_tomb, k, 64);
+    __shared__ uint32_t wsum[4];
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = my_tomb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < (blockDim.x + 63) / 64; w++) t += wsum[w];
+        tomb_part[blockIdx.x] = t;
+    }
+}
+
+// res[2] = Σ part[0 .. m)
+__global__ __launch_bounds__(1024) void k_snap_sum(const uint32_t *part, uint64_t m, unsigned long long *res) {
+    __shared__ unsigned long long w[16];
+    unsigned long long t = 0;
+    for (uint64_t i = threadIdx.x; i < m; i += blockDim.x) t += part[i];
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)t, k, 64), hi = __shfl_xor((uint32_t)(t >> 32), k, 64);
+        t += ((unsigned long long)hi << 32) | lo;
+    }
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; k++) s += w[k];
+        res[2] = s;
+    }
 }
 
 inline dim3 grid_for(uint64_t threads) { return dim3((uint32_t)((threads + 255) / 256)); }
@@ -189,6 +274,7 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
     }
     hipError_t e;
     const uint32_t P = f.phases;
+    if (P > 256 || f.seg + f.lp + 32 > SNAP_LDS) return hipErrorInvalidValue;
     const uint64_t body = f.len > f.base ? f.len - f.base : 0;
     const uint64_t nseg = std::max<uint64_t>(1, (body + f.seg - 1) / f.seg);
     std::vector<uint64_t> sizes{nseg};
@@ -204,13 +290,21 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
         start[l] = static_cast<uint32_t *>(s.get(66 + 4 * l, sizes[l] * 4));
         basev[l] = static_cast<uint64_t *>(s.get(67 + 4 * l, sizes[l] * 8));
     }
-    uint64_t *off = static_cast<uint64_t *>(s.get(96, n * 8));
     unsigned long long *words = static_cast<unsigned long long *>(s.get(97, 64));
     if (s.err) return s.err;
+    // staged bytes of a run of G segments: G * seg + lp (+ 16 for the aligned start)
+    auto img_bytes = [&](uint32_t G) { return ((uint64_t)G * f.seg + f.lp + 16 + 15) / 16 * 16; };
 
-    // 1. transfer functions
-    hipLaunchKernelGGL(k_snap_walk, grid_for(nseg * P), dim3(256), 0, st, blob, f, nseg, ex[0],
-                       static_cast<uint32_t *>(cnt[0]));
+    // 1. transfer functions.  Small workgroups (one wave when P <= 64) keep the LDS stage small,
+    // so many workgroups per CU overlap their dependent walks
+    {
+        const uint32_t bd = P <= 64 ? 64 : 256;
+        uint32_t G = std::max<uint32_t>(1, bd / P);
+        while (G > 1 && img_bytes(G) > SNAP_LDS) G--;
+        const uint64_t groups = (nseg + G - 1) / G;
+        hipLaunchKernelGGL(k_snap_walk, dim3((uint32_t)groups), dim3(bd), (size_t)img_bytes(G), st, blob, f, nseg, G,
+                           ex[0], static_cast<uint32_t *>(cnt[0]));
+    }
     // 2. compose up to one group, then push the true positions down
     for (size_t l = 0; l + 1 < L; l++) {
         if (l == 0)
@@ -251,28 +345,34 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
                                static_cast<const uint64_t *>(cnt[l]), sizes[l], P, start[l + 1], basev[l + 1],
                                sizes[l + 1], start[l], basev[l]);
     }
-    // 3. offsets, then the column scatter
-    hipLaunchKernelGGL(k_snap_offsets, grid_for(nseg), dim3(256), 0, st, blob, f, nseg, start[0], basev[0], n, off,
-                       words);
-    unsigned long long w[2] = {0, 0};
-    if ((e = hipMemcpyAsync(w, words, 16, hipMemcpyDeviceToHost, st))) return e;
+    // 3. list + scatter: one wave per run of G segments (G walker lanes, then all 64 lanes scatter)
+    {
+        uint32_t G = 4;
+        auto lds_bytes = [&](uint32_t g) {
+            const uint64_t cap = (uint64_t)g * (f.seg / f.lt + 1);
+            return img_bytes(g) + cap * 4;
+        };
+        while (G > 1 && lds_bytes(G) > SNAP_LDS) G--;
+        const uint32_t cap = G * (uint32_t)(f.seg / f.lt + 1);
+        const uint64_t groups = (nseg + G - 1) / G;
+        uint32_t *part = static_cast<uint32_t *>(s.get(98, groups * 4));
+        if (s.err) return s.err;
+        hipLaunchKernelGGL(k_snap_decode, dim3((uint32_t)groups), dim3(64), (size_t)lds_bytes(G), st, blob, f, nseg,
+                           G, cap, start[0], basev[0], n, reinterpret_cast<uint32_t *>(keys),
+                           reinterpret_cast<uint32_t *>(phys), logical, reinterpret_cast<uint32_t *>(node), tags,
+                           reinterpret_cast<uint32_t *>(values), words, part);
+        hipLaunchKernelGGL(k_snap_sum, dim3(1), dim3(1024), 0, st, part, groups, words);
+    }
+    if ((e = hipGetLastError())) return e;
+    unsigned long long w[3] = {0, 0, 0};
+    if ((e = hipMemcpyAsync(w, words, 24, hipMemcpyDeviceToHost, st))) return e;
     if ((e = hipStreamSynchronize(st))) return e;
     if (w[1]) {  // cannot happen for a chain that parsed in step 1
         *corrupt = 2;
         return hipSuccess;
     }
     res->entries_end = w[0];
-    const uint32_t W = f.key_len / 4 + 6 + f.val_len / 4;
-    const uint32_t R = std::max<uint32_t>(1, 2048 / W);
-    const uint64_t groups = (n + R - 1) / R;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(groups, 1u << 16);
-    hipLaunchKernelGGL(k_snap_decode, dim3(grid), dim3(256), 0, st, blob, f, off, n, R,
-                       reinterpret_cast<uint32_t *>(keys), reinterpret_cast<uint32_t *>(phys), logical,
-                       reinterpret_cast<uint32_t *>(node), tags, reinterpret_cast<uint32_t *>(values), words + 2);
-    if ((e = hipGetLastError())) return e;
-    if ((e = hipMemcpyAsync(w, words + 2, 8, hipMemcpyDeviceToHost, st))) return e;
-    if ((e = hipStreamSynchronize(st))) return e;
-    res->tombstones = w[0];
+    res->tombstones = w[2];
     return hipSuccess;
 }
 

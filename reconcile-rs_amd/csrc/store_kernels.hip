@@ -17,6 +17,8 @@
 // (mutate.rs:23-154): sort the batch by key, find every key in base and delta, build the
 // batch's DeltaRecs, merge them into the delta run (O(m + nD)); when the delta run passes
 // nB / 8 it is merged into the base (O(nB)) -- amortised, and on demand before rank / select.
+#include <type_traits>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -200,14 +202,42 @@ __global__ void k_count_ovr(const uint8_t *sops, const uint8_t *present, uint64_
 
 // Survivors move to i + #inserts(rank <= i) - #deletes(rank < i); deleted rows are skipped.
 // One workgroup covers MOVE_TILE consecutive rows: one lane finds the slice of the (sorted)
-// insert / delete rank lists that falls inside the tile, then every row binary-searches only
-// that slice -- no n-sized scratch arrays, no n-sized scan.
+// insert / delete rank lists that falls inside the tile, every row binary-searches only that
+// slice for its shift (kept in LDS), and then the tile's key and payload bytes are copied as
+// flat dword streams -- consecutive lanes read consecutive dwords of the source run and write
+// consecutive dwords of the destination (a shifted memmove between insert / delete points).
+// No n-sized scratch arrays, no n-sized scan.
 constexpr int MOVE_TILE = 1024;
+
+template <int B>
+struct Unit {  // the widest access that divides a B-byte row
+    static constexpr int SIZE = B % 16 == 0 ? 16 : B % 8 == 0 ? 8 : 4;
+    using T = typename std::conditional<SIZE == 16, uint4, typename std::conditional<SIZE == 8, uint2, uint32_t>::type>::type;
+};
+
+// rows [i0, i0 + rows) of a B-byte-row run to row i + shift[i - i0] of dst, as a flat stream of
+// the widest units (consecutive lanes: consecutive source units)
+template <int B>
+__device__ __forceinline__ void move_rows(const uint8_t *src, uint8_t *dst, uint64_t i0, uint32_t rows,
+                                          const int32_t *shift) {
+    using U = typename Unit<B>::T;
+    constexpr int NU = B / Unit<B>::SIZE;
+    const U *s = reinterpret_cast<const U *>(src) + i0 * NU;
+    U *d = reinterpret_cast<U *>(dst);
+    for (uint32_t w = threadIdx.x; w < rows * NU; w += blockDim.x) {
+        const uint32_t r = w / NU;
+        const int32_t sh = shift[r];
+        if (sh != INT32_MIN) d[(uint64_t)((int64_t)(i0 + r) + sh) * NU + (w - r * NU)] = s[w];
+    }
+}
+
 template <int KL, int P>
 __global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const uint8_t *pay, uint64_t n,
                                                     const uint32_t *ins_rank, const uint32_t *del_rank,
                                                     const uint64_t *counts, uint8_t *okeys, uint8_t *opay) {
+    static_assert(KL % 4 == 0 && P % 4 == 0, "dword rows");
     __shared__ uint64_t bounds[4];
+    __shared__ int32_t shift[MOVE_TILE];  // pos - i, or INT32_MIN for a deleted row
     const uint64_t i0 = (uint64_t)blockIdx.x * MOVE_TILE;
     if (threadIdx.x == 0) {
         const uint64_t a = counts[0], d = counts[2];  // list lengths: #inserts, #deletes
@@ -218,17 +248,17 @@ __global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const u
     }
     __syncthreads();
     const uint64_t ia = bounds[0], ib = bounds[1], da = bounds[2], db = bounds[3];
-#pragma unroll
-    for (int k = 0; k < MOVE_TILE / 256; k++) {
-        const uint64_t i = i0 + threadIdx.x + 256 * k;
-        if (i >= n) break;
+    const uint32_t rows = (uint32_t)(n - i0 < (uint64_t)MOVE_TILE ? n - i0 : MOVE_TILE);
+    for (uint32_t r = threadIdx.x; r < rows; r += 256) {
+        const uint64_t i = i0 + r;
         const uint64_t ins_le = lower_bound_u32(ins_rank, ia, ib, i + 1);  // rank <= i
         const uint64_t del_lt = lower_bound_u32(del_rank, da, db, i);      // rank < i
-        if (del_lt < db && del_rank[del_lt] == i) continue;                 // deleted
-        const uint64_t pos = i + ins_le - del_lt;
-        copy_bytes<KL>(okeys + pos * KL, keys + i * KL);
-        copy_bytes<P>(opay + (uint64_t)P * pos, pay + (uint64_t)P * i);
+        const bool gone = del_lt < db && del_rank[del_lt] == i;
+        shift[r] = gone ? INT32_MIN : (int32_t)((int64_t)ins_le - (int64_t)del_lt);
     }
+    __syncthreads();
+    move_rows<KL>(keys, okeys, i0, rows, shift);
+    move_rows<P>(pay, opay, i0, rows, shift);
 }
 
 // inserts and overwrites land at r + (#inserts before j) - (#deletes before j): for an insert
@@ -300,7 +330,7 @@ __global__ void k_bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key,
 __global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
                               const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
                               const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
-                              unsigned long long *counts) {
+                              uint32_t *part) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool c_new = false, c_over = false, c_del = false;
     if (j < m) {
@@ -328,11 +358,46 @@ __global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
         dops[j] = (isdel && !in_b) ? 1 : 0;
         reinterpret_cast<DeltaRec *>(bpay)[j] = r;
     }
+    // per-workgroup counts (same-address atomics from every wave would serialise in L2);
+    // k_sum_parts3 adds them up
+    __shared__ uint32_t wc[4][3];
     const unsigned long long bn = __ballot(c_new), bo = __ballot(c_over), bd = __ballot(c_del);
     if ((threadIdx.x & 63) == 0) {
-        if (bn) atomicAdd(counts + 0, (unsigned long long)__popcll(bn));
-        if (bo) atomicAdd(counts + 1, (unsigned long long)__popcll(bo));
-        if (bd) atomicAdd(counts + 2, (unsigned long long)__popcll(bd));
+        wc[threadIdx.x >> 6][0] = (uint32_t)__popcll(bn);
+        wc[threadIdx.x >> 6][1] = (uint32_t)__popcll(bo);
+        wc[threadIdx.x >> 6][2] = (uint32_t)__popcll(bd);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) t += wc[w][threadIdx.x];
+        part[3ull * blockIdx.x + threadIdx.x] = t;
+    }
+}
+
+// counts[k] = Σ_g part[3 g + k], one workgroup
+__global__ __launch_bounds__(1024) void k_sum_parts3(const uint32_t *part, uint64_t groups, uint64_t *counts) {
+    __shared__ unsigned long long w[16][3];
+    unsigned long long t[3] = {0, 0, 0};
+    for (uint64_t g = threadIdx.x; g < groups; g += blockDim.x) {
+        t[0] += part[3 * g];
+        t[1] += part[3 * g + 1];
+        t[2] += part[3 * g + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)t[k], m, 64), hi = __shfl_xor((uint32_t)(t[k] >> 32), m, 64);
+            t[k] += ((unsigned long long)hi << 32) | lo;
+        }
+        if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6][k] = t[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long s = 0;
+        for (uint32_t q = 0; q < blockDim.x / 64; q++) s += w[q][threadIdx.x];
+        counts[threadIdx.x] = s;
     }
 }
 
@@ -424,13 +489,21 @@ struct KeyOps final : StoreKeyOps {
     template <int P>
     hipError_t merge_p(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys, const uint8_t *spay,
                        const uint8_t *sops, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay, uint64_t *counts,
-                       hipStream_t st) {
+                       hipStream_t st, const uint32_t *rank_in, const uint8_t *present_in) {
         hipError_t e;
-        uint32_t *rank = s.u32(2, m), *ins = s.u32(3, m), *del = s.u32(4, m);
+        uint32_t *ins = s.u32(3, m), *del = s.u32(4, m);
         uint32_t *cins = s.u32(5, m), *cdel = s.u32(6, m), *ins_rank = s.u32(7, m), *del_rank = s.u32(8, m);
-        uint8_t *present = s.u8(0, m);
+        const uint32_t *rank = rank_in;
+        const uint8_t *present = present_in;
+        if (!rank_in || !present_in) {  // where each batch key sits in the run
+            uint32_t *r = s.u32(2, m);
+            uint8_t *pr = s.u8(0, m);
+            if (s.err) return s.err;
+            if ((e = search(keys, n, skeys, m, r, pr, st))) return e;
+            rank = r;
+            present = pr;
+        }
         if (s.err) return s.err;
-        if ((e = search(keys, n, skeys, m, rank, present, st))) return e;
         hipLaunchKernelGGL(k_classify, g1(m), dim3(256), 0, st, sops, present, m, ins, del);
         size_t tb = 0;
         if ((e = rocprim::exclusive_scan(nullptr, tb, ins, cins, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
@@ -455,11 +528,13 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t merge(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys, const uint8_t *spay,
                      const uint8_t *sops, uint64_t m, int payload, Scratch &s, uint8_t *okeys, uint8_t *opay,
-                     uint64_t *counts, hipStream_t st) override {
+                     uint64_t *counts, hipStream_t st, const uint32_t *rank, const uint8_t *present) override {
         if (m == 0) return hipMemsetAsync(counts, 0, 24, st);
-        if (payload == 32) return merge_p<32>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st);
+        if (payload == 32)
+            return merge_p<32>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st, rank, present);
         if (payload == (int)sizeof(DeltaRec))
-            return merge_p<sizeof(DeltaRec)>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st);
+            return merge_p<sizeof(DeltaRec)>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st, rank,
+                                             present);
         return hipErrorInvalidValue;
     }
 
@@ -526,10 +601,14 @@ StoreKeyOps *store_key_ops(int kk, int kl) {
 hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
                               const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
                               const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
-                              uint64_t *counts, hipStream_t st) {
-    if (m == 0) return hipSuccess;
+                              uint64_t *counts, Scratch &s, hipStream_t st) {
+    if (m == 0) return hipMemsetAsync(counts, 0, 24, st);
+    const uint64_t groups = (m + 255) / 256;
+    uint32_t *part = s.u32(13, groups * 3);
+    if (s.err) return s.err;
     hipLaunchKernelGGL(k_delta_build, g1(m), dim3(256), 0, st, sfps, sops, m, rank_b, present_b, base_fps, rank_d,
-                       present_d, dpay, bpay, dops, reinterpret_cast<unsigned long long *>(counts));
+                       present_d, dpay, bpay, dops, part);
+    hipLaunchKernelGGL(k_sum_parts3, dim3(1), dim3(1024), 0, st, part, groups, counts);
     return hipGetLastError();
 }
 

@@ -80,10 +80,12 @@ struct StoreKeyOps {
                               uint8_t *present, hipStream_t st) = 0;
     // merge a key-sorted batch (ops: 0 upsert, 1 delete) into a sorted run of (key, payload)
     // rows -> (okeys, opay); payload 32 (fingerprints) or 80 (DeltaRec);
-    // counts = {inserted, overwritten, deleted}
+    // counts = {inserted, overwritten, deleted}.  rank / present: the batch keys' search result
+    // in the run if the caller already has it (else searched here)
     virtual hipError_t merge(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys,
                              const uint8_t *spay, const uint8_t *sops, uint64_t m, int payload, Scratch &s,
-                             uint8_t *okeys, uint8_t *opay, uint64_t *counts, hipStream_t st) = 0;
+                             uint8_t *okeys, uint8_t *opay, uint64_t *counts, hipStream_t st,
+                             const uint32_t *rank = nullptr, const uint8_t *present = nullptr) = 0;
     virtual hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) = 0;
     // keep the last row of every run of equal keys of a key-sorted run (a stable sort keeps
     // input order within a run, so this is "the last insert wins"); counts[0] = rows kept
@@ -99,7 +101,7 @@ struct StoreKeyOps {
 hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
                               const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
                               const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
-                              uint64_t *counts, hipStream_t st);
+                              uint64_t *counts, Scratch &s, hipStream_t st);
 hipError_t launch_delta_prefix(const uint8_t *dpay, uint64_t n, int32_t *cnt, Scratch &s, hipStream_t st);
 hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops, hipStream_t st);
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,

@@ -80,3 +80,55 @@ def to_host(cols: Dict[str, torch.Tensor], lo: int = 0, hi=None):
             a = a.view(np.uint32)
         out[k] = np.ascontiguousarray(a)
     return out
+
+
+def make_snapshot(cols: Dict[str, torch.Tensor], schema: RecordSchema, key_form: str = "array",
+                  chunk: int = 1 << 20) -> torch.Tensor:
+    """The RCNL v1 file (src/snapshot.rs:30-58) of a PersistedState whose entries are the rows
+    of `cols` (dated records; tags 1 = tombstone) and whose members / tombstone_acks are empty,
+    built on the device as bench / test input: b"RCNL", u32 1, then bincode fixint of
+    Vec<(K, Entry<Timestamp, V>)> (lww-register/src/persistence.rs:32,62-70)."""
+    dev = cols["keys"].device if "keys" in cols else cols["values"].device
+    n = (cols["keys"] if "keys" in cols else cols["values"]).shape[0]
+    kr, vr = schema.key_row, schema.value_row
+    kp = 8 if key_form == "vec" else 0
+    vp = 8 if schema.value_kind == A.VAL_BYTES else 0
+    lt = kp + kr + 24
+    lp = lt + vp + vr
+    tags = cols.get("tags")
+    tags = torch.zeros(n, dtype=torch.uint8, device=dev) if tags is None else tags
+    lens = torch.where(tags == 1, lt, lp).to(torch.int64)
+    offs = torch.cumsum(lens, 0) - lens + 16
+    body = 16 + int(lens.sum().item())
+    buf = torch.zeros(body + 16, dtype=torch.uint8, device=dev)  # + empty members, empty acks
+    head = b"RCNL" + (1).to_bytes(4, "little") + int(n).to_bytes(8, "little")
+    buf[:16] = torch.tensor(list(head), dtype=torch.uint8, device=dev)
+
+    def u8(t: torch.Tensor, w: int) -> torch.Tensor:
+        return t.contiguous().view(torch.uint8).view(-1, w)
+
+    def const(v: int, w: int, m: int) -> torch.Tensor:
+        return torch.tensor(list(v.to_bytes(w, "little")), dtype=torch.uint8, device=dev).expand(m, w)
+
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        o = offs[lo:hi]
+        present = tags[lo:hi] == 0
+        fields = []
+        if kp:
+            fields.append((0, const(kr, 8, hi - lo), None))
+        if kr:
+            fields.append((kp, cols["keys"][lo:hi], None))
+        fields += [(kp + kr, u8(cols["phys"][lo:hi], 8), None), (kp + kr + 8, u8(cols["logical"][lo:hi], 4), None),
+                   (kp + kr + 12, u8(cols["node"][lo:hi], 8), None),
+                   (kp + kr + 20, u8(tags[lo:hi].to(torch.int32), 4), None)]
+        if vp:
+            fields.append((lt, const(vr, 8, hi - lo), present))
+        if vr:
+            fields.append((lt + vp, cols["values"][lo:hi], present))
+        for rel, data, mask in fields:
+            w = data.shape[1]
+            oo, dd = (o, data) if mask is None else (o[mask], data[mask])
+            idx = (oo + rel)[:, None] + torch.arange(w, device=dev)[None, :]
+            buf[idx.reshape(-1)] = dd.reshape(-1)
+    return buf

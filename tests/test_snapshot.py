@@ -252,3 +252,19 @@ def test_reload_full_size_properties(gpu):
     total %= 1 << 256
     agg = dated.aggregate()
     assert agg.size == n and agg.fingerprint.to_int() == total
+
+
+@pytest.mark.parametrize("kv,form", [(("bytes16", "bytes64"), "array"), (("bytes16", "bytes64"), "vec"),
+                                     (("u32", "u32"), "array"), (("u64", "u64"), "array")])
+def test_device_snapshot_builder_matches_oracle(rsos_hip_lib, kv, form):
+    """synth.make_snapshot (the bench's input builder, torch) writes the oracle's bytes."""
+    from rsos_hip import RecordSchema
+    from rsos_hip.synth import make_records, make_snapshot, to_host
+    s = RecordSchema.dated(*kv)
+    c = make_records(s, 3000, seed=1, device="cpu", tombstone_fraction=0.3)
+    got = make_snapshot(c, s, form, chunk=1000).numpy().tobytes()
+    h = to_host(c)
+    ints = {"u32": "u32", "u64": "u64"}
+    want = OS.encode_snapshot(h["keys"], h["phys"], h["logical"], h["node"], h["tags"], h["values"],
+                              ints.get(kv[0], form), ints.get(kv[1], "bytes"))
+    assert got == want

@@ -428,9 +428,8 @@ struct rh_store {
             return rc;
         dtotal = 0;
         if (!nd) return RH_OK;
-        RH_HIP(rh::launch_reduce(dpay[cd].p, nd, dbsums.p, stream, sizeof(rh::DeltaRec)));
+        RH_HIP(rh::launch_delta_sums(dpay[cd].p, nd, dbsums.p, dcnt.p, scratch, stream));
         RH_HIP(rh::launch_reduce(dbsums.p, nbk, dssums.p, stream));
-        RH_HIP(rh::launch_delta_prefix(dpay[cd].p, nd, dcnt.p, scratch, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         int32_t t = 0;
         RH_HIP(hipMemcpyAsync(&t, dcnt.p + nd - 1, 4, hipMemcpyDeviceToHost, stream));

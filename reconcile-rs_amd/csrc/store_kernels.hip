@@ -135,6 +135,14 @@ __global__ void k_iota(uint32_t *p, uint64_t m) {
     if (j < m) p[j] = (uint32_t)j;
 }
 
+// *tie = 1 if two keys adjacent in perm order share their most significant digit
+template <int KK, int KL>
+__global__ void k_prefix_ties(const uint8_t *keys, const uint32_t *perm, uint64_t m, uint32_t *tie) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (j < m && key_digit<KK, KL>(keys + (uint64_t)perm[j] * KL, 0) == key_digit<KK, KL>(keys + (uint64_t)perm[j - 1] * KL, 0))
+        atomicOr(tie, 1u);
+}
+
 // gather the batch into key order; flag adjacent duplicates
 template <int KK, int KL>
 __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, const uint32_t *perm,
@@ -401,12 +409,21 @@ __global__ __launch_bounds__(1024) void k_sum_parts3(const uint32_t *part, uint6
     }
 }
 
-// count delta of each delta entry: live - in_base
-__global__ void k_delta_cnt(const uint8_t *dpay, uint64_t n, int32_t *cnt) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t f = reinterpret_cast<const DeltaRec *>(dpay)[i].flags;
-    cnt[i] = (int32_t)((f & DeltaRec::LIVE) ? 1 : 0) - (int32_t)((f & DeltaRec::IN_BASE) ? 1 : 0);
+// one pass over the delta run: the 256-row block sums of the contributions and each entry's
+// count delta (live - in_base), which the caller then prefix-sums
+__global__ __launch_bounds__(256) void k_delta_sums(const uint8_t *dpay, uint64_t n, uint8_t *bsums, int32_t *cnt) {
+    __shared__ SumTile tile;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n) {
+        const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
+        fp_load(reinterpret_cast<const uint8_t *>(r.contrib), h);
+        const uint32_t f = r.flags;
+        cnt[i] = (int32_t)((f & DeltaRec::LIVE) ? 1 : 0) - (int32_t)((f & DeltaRec::IN_BASE) ? 1 : 0);
+    }
+    uint32_t f8[8];
+    block_sum_fps256(h, tile, f8);
+    if (threadIdx.x == 0) store_sum(bsums, blockIdx.x, f8);
 }
 
 // compaction input: cur fp = contrib + base, op = live ? upsert : delete
@@ -465,15 +482,37 @@ struct KeyOps final : StoreKeyOps {
         uint32_t *perm = s.u32(0, m), *perm2 = s.u32(1, m);
         uint64_t *dig = s.u64(0, m), *dig2 = s.u64(1, m);
         if (s.err) return s.err;
-        hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
-        for (int d = D - 1; d >= 0; d--) {  // LSD: least significant digit first, stable passes
+        // Multi-digit keys: sort on the most significant digit alone first.  If no two keys then
+        // share that digit the order is already final (random and spread keys: always); else
+        // fall back to the full LSD sort (least significant digit first, stable passes).
+        auto pass = [&](int d) -> hipError_t {
+            hipError_t e2;
             hipLaunchKernelGGL((k_digit<KK, KL>), g1(m), dim3(256), 0, st, keys, perm, m, d, dig);
             size_t tb = 0;
-            if ((e = rocprim::radix_sort_pairs(nullptr, tb, dig, dig2, perm, perm2, m, 0, BITS, st))) return e;
+            if ((e2 = rocprim::radix_sort_pairs(nullptr, tb, dig, dig2, perm, perm2, m, 0, BITS, st))) return e2;
             void *tmp = s.bytes(tb);
             if (s.err) return s.err;
-            if ((e = rocprim::radix_sort_pairs(tmp, tb, dig, dig2, perm, perm2, m, 0, BITS, st))) return e;
+            if ((e2 = rocprim::radix_sort_pairs(tmp, tb, dig, dig2, perm, perm2, m, 0, BITS, st))) return e2;
             std::swap(perm, perm2);
+            return hipSuccess;
+        };
+        hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
+        if (D > 1) {
+            uint32_t *tie = s.u32(14, 1);
+            if (s.err) return s.err;
+            if ((e = hipMemsetAsync(tie, 0, 4, st))) return e;
+            if ((e = pass(0))) return e;
+            hipLaunchKernelGGL((k_prefix_ties<KK, KL>), g1(m), dim3(256), 0, st, keys, perm, m, tie);
+            uint32_t tie_h = 0;
+            if ((e = hipMemcpyAsync(&tie_h, tie, 4, hipMemcpyDeviceToHost, st))) return e;
+            if ((e = hipStreamSynchronize(st))) return e;
+            if (tie_h) {
+                hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
+                for (int d = D - 1; d >= 0; d--)
+                    if ((e = pass(d))) return e;
+            }
+        } else {
+            if ((e = pass(0))) return e;
         }
         hipLaunchKernelGGL((k_gather<KK, KL>), g1(m), dim3(256), 0, st, keys, fps, ops, perm, m, skeys, sfps, sops, dup);
         return hipGetLastError();
@@ -612,9 +651,10 @@ hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
     return hipGetLastError();
 }
 
-hipError_t launch_delta_prefix(const uint8_t *dpay, uint64_t n, int32_t *cnt, Scratch &s, hipStream_t st) {
+hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n, uint8_t *bsums, int32_t *cnt, Scratch &s,
+                             hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_delta_cnt, g1(n), dim3(256), 0, st, dpay, n, cnt);
+    hipLaunchKernelGGL(k_delta_sums, g1(n), dim3(256), 0, st, dpay, n, bsums, cnt);
     size_t tb = 0;
     hipError_t e;
     if ((e = rocprim::inclusive_scan(nullptr, tb, cnt, cnt, n, rocprim::plus<int32_t>(), st))) return e;

@@ -538,3 +538,29 @@ def test_store_lsm_policies_agree(gpu, oracle_lib):
     assert np.array_equal(lazy.fingerprints(), eager.fingerprints())
     lazy.close()
     eager.close()
+
+
+def test_store_batch_keys_sharing_leading_bytes(gpu, oracle_lib):
+    """16 B keys whose first 8 bytes repeat (the batch sort's most-significant-digit pass alone
+    cannot order them, so it falls back to the full sort): applied batches, and a reload with
+    repeated keys, still give the oracle's key order and fingerprints."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    O = oracle_lib
+    s = RecordSchema.plain("bytes16", "bytes64")
+    rng = np.random.default_rng(21)
+    heads = rng.integers(0, 256, (40, 8), dtype=np.uint8)
+    n = 4000
+    keys = np.concatenate([heads[rng.integers(0, 40, n)], rng.integers(0, 256, (n, 8), dtype=np.uint8)], axis=1)
+    keys = np.unique(keys.view("V16"), axis=0).view(np.uint8).reshape(-1, 16)
+    keys = keys[rng.permutation(len(keys))]
+    vals = rng.integers(0, 256, (len(keys), 64), dtype=np.uint8)
+    st = GpuFingerprintStore(s)
+    half = len(keys) // 2
+    for lo, hi in [(0, half), (half, len(keys))]:
+        st.apply({"keys": keys[lo:hi], "values": vals[lo:hi]}, np.zeros(hi - lo, np.uint8))
+    order = np.lexsort(keys.T[::-1])
+    sch = O.Schema(O.KEY_BYTES, 16, O.VAL_BYTES, 64, O.REC_PLAIN, 0)
+    want = O.Records(sch, np.ascontiguousarray(keys[order]), np.ascontiguousarray(vals[order])).lift()
+    assert np.array_equal(st.fingerprints(), want)
+    assert [k for k, _ in st.enumerate()] == [keys[i].tobytes() for i in order]
+    st.close()

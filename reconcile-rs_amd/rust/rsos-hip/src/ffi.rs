@@ -51,23 +51,83 @@ pub struct rh_store {
     _private: [u8; 0],
 }
 
+#[repr(C)]
+#[derive(Default, Clone, Copy, Debug)]
+pub struct rh_snapshot_info {
+    pub entries: u64,
+    pub tombstones: u64,
+    pub entries_end: u64,
+    pub keys: u64,
+}
+
+pub const RH_ERR_ARG: c_int = -1;
+pub const RH_ERR_HIP: c_int = -2;
+pub const RH_ERR_OOM: c_int = -3;
+pub const RH_ERR_UNSUPPORTED: c_int = -4;
+pub const RH_ERR_STATE: c_int = -5;
+pub const RH_ERR_DATA: c_int = -6;
+pub const RH_FORM_ARRAY: c_int = 0;
+pub const RH_FORM_VEC: c_int = 1;
+
+// Every entry point of include/rsos_hip.h, in header order.
 extern "C" {
     pub fn rh_abi_version() -> c_int;
     pub fn rh_last_error() -> *const c_char;
     pub fn rh_schema_supported(schema: *const rh_schema) -> c_int;
     pub fn rh_schema_record_len(schema: *const rh_schema, tombstone: c_int) -> i64;
+    pub fn rh_num_blocks(n: usize) -> usize;
+    pub fn rh_num_superblocks(n: usize) -> usize;
+    pub fn rh_lift_records_async(schema: *const rh_schema, dev_cols: *const rh_columns, n: usize, dev_fps: *mut u8,
+                                 dev_block_sums: *mut u8, stream: *mut c_void) -> c_int;
+    pub fn rh_lift_dual_async(schema: *const rh_schema, dev_cols: *const rh_columns, n: usize, fps_dated: *mut u8,
+                              bsums_dated: *mut u8, fps_proj: *mut u8, bsums_proj: *mut u8,
+                              stream: *mut c_void) -> c_int;
+    pub fn rh_lift_encoded_async(dev_bytes: *const u8, dev_offsets: *const u64, n: usize, dev_fps: *mut u8,
+                                 dev_block_sums: *mut u8, stream: *mut c_void) -> c_int;
+    pub fn rh_reduce_blocks_async(dev_in: *const u8, n_in: usize, dev_out: *mut u8, stream: *mut c_void) -> c_int;
+    pub fn rh_range_aggregates_async(dev_fps: *const u8, dev_block_sums: *const u8, dev_super_sums: *const u8,
+                                     n: usize, dev_lo: *const u64, dev_hi: *const u64, r: usize,
+                                     dev_out: *mut rh_aggregate, stream: *mut c_void) -> c_int;
+    pub fn rh_combine_aggregates_async(dev_in: *const rh_aggregate, parts: usize, r: usize, dev_out: *mut rh_aggregate,
+                                       stream: *mut c_void) -> c_int;
     pub fn rh_lift_host(device: c_int, schema: *const rh_schema, cols: *const rh_columns, n: usize, fps: *mut u8) -> c_int;
     pub fn rh_fp_add(a: *const u64, b: *const u64, out: *mut u64);
     pub fn rh_fp_sub(a: *const u64, b: *const u64, out: *mut u64);
     pub fn rh_store_create(device: c_int, schema: *const rh_schema, out: *mut *mut rh_store) -> c_int;
     pub fn rh_store_destroy(store: *mut rh_store) -> c_int;
     pub fn rh_store_load(store: *mut rh_store, cols: *const rh_columns, n: usize) -> c_int;
+    pub fn rh_store_load_device(store: *mut rh_store, dev_cols: *const rh_columns, n: usize) -> c_int;
     pub fn rh_store_len(store: *const rh_store, out: *mut u64) -> c_int;
     pub fn rh_store_aggregate(store: *mut rh_store, lo: u64, hi: u64, out: *mut rh_aggregate) -> c_int;
     pub fn rh_store_aggregates(store: *mut rh_store, lo: *const u64, hi: *const u64, r: usize, out: *mut rh_aggregate) -> c_int;
     pub fn rh_store_aggregate_keys(store: *mut rh_store, lo_kind: c_int, lo_key: *const c_void, hi_kind: c_int,
                                    hi_key: *const c_void, out: *mut rh_aggregate) -> c_int;
     pub fn rh_store_rank(store: *mut rh_store, key: *const c_void, out: *mut u64) -> c_int;
+    pub fn rh_store_ranks(store: *mut rh_store, keys: *const c_void, m: usize, out: *mut u64) -> c_int;
+    pub fn rh_store_select(store: *mut rh_store, r: u64, key_out: *mut c_void) -> c_int;
+    pub fn rh_store_keys(store: *mut rh_store, lo: u64, hi: u64, host_out: *mut c_void) -> c_int;
+    pub fn rh_store_fingerprints(store: *mut rh_store, lo: u64, hi: u64, host_out: *mut u8) -> c_int;
     pub fn rh_store_apply(store: *mut rh_store, cols: *const rh_columns, ops: *const u8, n: usize,
                           n_new: *mut u64, n_over: *mut u64, n_del: *mut u64) -> c_int;
+    pub fn rh_store_apply_device(store: *mut rh_store, dev_cols: *const rh_columns, dev_ops: *const u8, n: usize,
+                                 n_new: *mut u64, n_over: *mut u64, n_del: *mut u64) -> c_int;
+    pub fn rh_store_compact(store: *mut rh_store) -> c_int;
+    pub fn rh_store_set_compaction(store: *mut rh_store, divisor: u64, min_rows: u64) -> c_int;
+    pub fn rh_store_stats(store: *const rh_store, base_rows: *mut u64, delta_rows: *mut u64,
+                          compactions: *mut u64) -> c_int;
+    pub fn rh_snapshot_header(bytes: *const c_void, len: usize, entries: *mut u64) -> c_int;
+    pub fn rh_snapshot_decode_device(schema: *const rh_schema, key_form: c_int, dev_bytes: *const c_void, len: usize,
+                                     dev_out: *const rh_columns, cap: usize, info: *mut rh_snapshot_info,
+                                     stream: *mut c_void) -> c_int;
+    pub fn rh_store_load_snapshot(dated: *mut rh_store, projection: *mut rh_store, key_form: c_int,
+                                  bytes: *const c_void, len: usize, bytes_on_device: c_int,
+                                  info: *mut rh_snapshot_info) -> c_int;
+    pub fn rh_wire_encode_range_aggregates(schema: *const rh_schema, key_form: c_int, msg_tag: c_int,
+                                           start_kinds: *const u8, start_keys: *const c_void, end_kinds: *const u8,
+                                           end_keys: *const c_void, aggregates: *const rh_aggregate, r: usize,
+                                           out: *mut u8, cap: usize, out_len: *mut usize) -> c_int;
+    pub fn rh_wire_decode_range_aggregates(schema: *const rh_schema, key_form: c_int, msg_tag: c_int, input: *const u8,
+                                           len: usize, r_cap: usize, start_kinds: *mut u8, start_keys: *mut c_void,
+                                           end_kinds: *mut u8, end_keys: *mut c_void, aggregates: *mut rh_aggregate,
+                                           r_out: *mut usize, consumed: *mut usize) -> c_int;
 }

@@ -36,6 +36,14 @@ def test_library_exports_every_declared_symbol(rsos_hip_lib):
     assert set(declared_symbols()) <= bound
 
 
+def test_rust_ffi_declares_every_symbol():
+    """The Rust crate's FFI block (source only here) transcribes the whole header."""
+    ffi = open(os.path.join(ROOT, "reconcile-rs_amd", "rust", "rsos-hip", "src", "ffi.rs")).read()
+    declared = set(re.findall(r"pub fn (rh_[a-z0-9_]+)\s*\(", ffi))
+    missing = [n for n in declared_symbols() if n not in declared]
+    assert not missing, missing
+
+
 def test_abi_version_and_enums(rsos_hip_lib, oracle_lib):
     from rsos_hip import _abi as A
     assert A.lib().rh_abi_version() == 1

@@ -240,11 +240,12 @@ __global__ __launch_bounds__(256) void k_snap_decode(const uint8_t *blob, SnapFm
     }
 }
 
-// res[2] = Σ part[0 .. m)
+// res[2] += Σ part[0 .. m): a grid-stride pass, one atomic per workgroup (gridDim <= 256)
 __global__ __launch_bounds__(1024) void k_snap_sum(const uint32_t *part, uint64_t m, unsigned long long *res) {
     __shared__ unsigned long long w[16];
     unsigned long long t = 0;
-    for (uint64_t i = threadIdx.x; i < m; i += blockDim.x) t += part[i];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
+        t += part[i];
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) {
         const uint32_t lo = __shfl_xor((uint32_t)t, k, 64), hi = __shfl_xor((uint32_t)(t >> 32), k, 64);
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(1024) void k_snap_sum(const uint32_t *part, uint64_
     if (threadIdx.x == 0) {
         unsigned long long s = 0;
         for (uint32_t k = 0; k < blockDim.x / 64; k++) s += w[k];
-        res[2] = s;
+        if (s) atomicAdd(res + 2, s);
     }
 }
 
@@ -361,7 +362,8 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
                            G, cap, start[0], basev[0], n, reinterpret_cast<uint32_t *>(keys),
                            reinterpret_cast<uint32_t *>(phys), logical, reinterpret_cast<uint32_t *>(node), tags,
                            reinterpret_cast<uint32_t *>(values), words, part);
-        hipLaunchKernelGGL(k_snap_sum, dim3(1), dim3(1024), 0, st, part, groups, words);
+        const uint32_t sum_grid = (uint32_t)std::min<uint64_t>(256, (groups + 1023) / 1024);
+        hipLaunchKernelGGL(k_snap_sum, dim3(sum_grid), dim3(1024), 0, st, part, groups, words);
     }
     if ((e = hipGetLastError())) return e;
     unsigned long long w[3] = {0, 0, 0};

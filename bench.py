@@ -192,6 +192,9 @@ def main():
         "oracle_spot_check": checked,
         "total_aggregate_size": int(root[:, 4].sum()),
     }
+    valu = load_valu(args.config, n, lift_avg_s)
+    if valu:
+        line["valu"] = valu
     if args.cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample)
     if args.e2e:
@@ -470,6 +473,31 @@ def end_to_end(schema, cols, n):
         del dcols, fps
     return {"records": n, "seconds": round(best, 5), "mrec_per_s": round(n / best / 1e6, 1),
             "gib_s_hashed": round(n * schema.record_len() / best / 2**30, 2)}
+
+
+def load_valu(config, n, lift_s):
+    """The lift's VALU-issue roofline from the committed PMC pass (profiles/r01_valu_<config>.json:
+    SQ_INSTS_VALU / SQ_WAVES / GRBM_GUI_ACTIVE, scripts/pmc_valu.py): VALU instructions per
+    launch over this run's measured lift time, against the rate gfx950 sustains for this mix --
+    one wave64 instruction per 4 cycles per SIMD (DESIGN.md §4) at the clock the PMC pass saw;
+    peak_nominal: the full-rate 2-operand rate, one per 2 cycles per SIMD at 2.4 GHz."""
+    p = os.path.join(ROOT, "profiles", f"r01_valu_{config}.json")
+    try:
+        with open(p) as f:
+            v = json.load(f)
+        if int(v.get("records", -1)) != n:
+            return None
+        instr = float(v["valu_wave_instructions_per_launch"])
+        clock = float(v["effective_clock_ghz"]) * 1e9
+        sustained = 256 * 4 * clock / 4
+        achieved = instr / lift_s
+        return {"bound": "valu", "achieved": round(achieved / 1e9, 1), "peak_sustained": round(sustained / 1e9, 1),
+                "peak_nominal": 256 * 4 * 2.4 / 2, "unit": "G wave-instr/s", "frac": round(achieved / sustained, 4),
+                "frac_nominal": round(achieved / (256 * 4 * 2.4e9 / 2), 4),
+                "valu_per_wave": round(float(v["valu_per_wave"]), 1), "clock_ghz": round(clock / 1e9, 3),
+                "source": os.path.relpath(p, ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def load_traffic(config, n):

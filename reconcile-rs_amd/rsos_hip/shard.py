@@ -56,3 +56,23 @@ def gather(dist, out, gathered=None):
     parts = [torch.empty_like(out) for _ in range(world)]
     dist.all_gather(parts, out)
     return torch.stack(parts)
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+def gather_async(dist, out, gathered):
+    """Start the all-gather of `out` into `gathered` (world, R, 5) without blocking the compute
+    stream: (work, gathered).  nccl: RCCL runs it on its own stream and work.wait() only makes
+    the current stream wait, so the next step's lift overlaps the collective.  gloo: done
+    synchronously (CPU rehearsal)."""
+    import torch
+    if dist.get_backend() == "nccl":
+        return dist.all_gather_into_tensor(gathered, out, async_op=True), gathered
+    parts = [torch.empty_like(out) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, out)
+    gathered.copy_(torch.stack(parts))
+    return _Done(), gathered
+

@@ -11,7 +11,7 @@ Workload (BASELINE.json configs[1]): 10 M records per GPU, 16 B key / 64 B value
 (FingerprintTreeMap<[u8;16], Entry<Timestamp, Vec<u8>>>, 120 canonical bytes per record).
 Weak scaling: every GPU holds its own 10 M-record shard of one globally key-sorted set.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config2|config3|bench_u32]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config1|config2|config3|config3_full|config4|config5|snapshot|bench_u32]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Prints ONE JSON line on rank 0.
@@ -30,7 +30,10 @@ sys.path.insert(0, os.path.join(ROOT, "reconcile-rs_amd"))
 import torch  # noqa: E402
 
 CONFIGS = {
-    # name: (key, value, record kind, records per GPU, canonical bytes hashed, HBM bytes / record, description)
+    # name: (key, value, record kind, records per GPU, description)
+    "config1": ("u64", "bytes64", "plain", 1_000_000,
+                "BASELINE configs[0]: the reference's CPU case, FingerprintTreeMap<u64, Vec<u8>> of 1M "
+                "u64-key / 64 B-value records (GPU lift beside the CPU fill)"),
     "config2": ("bytes16", "bytes64", "dated", 10_000_000,
                 "BASELINE configs[1]: 10M records/GPU, 16 B key / 64 B value, dated Entry<Timestamp,Vec<u8>>"),
     "config3": ("bytes16", "bytes1024", "dated", 10_000_000,

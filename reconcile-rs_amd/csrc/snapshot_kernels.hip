@@ -44,26 +44,40 @@ struct Img {
     }
 };
 
-// stage blob bytes [a, b) (a 16-aligned) into lds; bytes at or past `len` read as 0
-__device__ __forceinline__ void stage(const uint8_t *blob, uint64_t len, uint64_t a, uint64_t b, uint32_t *lds) {
-    for (uint64_t q = a + 16ull * threadIdx.x; q < b; q += 16ull * blockDim.x) {
-        uint4 v;
-        if (q + 16 <= len) {
-            v = *reinterpret_cast<const uint4 *>(blob + q);
-        } else {
-            uint32_t t[4];
+// the 16 bytes at q, zero past `len`
+__device__ __forceinline__ uint4 load16(const uint8_t *blob, uint64_t len, uint64_t q) {
+    if (q + 16 <= len) return *reinterpret_cast<const uint4 *>(blob + q);
+    uint32_t t[4];
 #pragma unroll
-            for (int d = 0; d < 4; d++) {
-                uint32_t x = 0;
-                for (int k = 0; k < 4; k++) {
-                    const uint64_t o = q + 4 * d + k;
-                    if (o < len) x |= (uint32_t)blob[o] << (8 * k);
-                }
-                t[d] = x;
-            }
-            v = make_uint4(t[0], t[1], t[2], t[3]);
+    for (int d = 0; d < 4; d++) {
+        uint32_t x = 0;
+        for (int k = 0; k < 4; k++) {
+            const uint64_t o = q + 4 * d + k;
+            if (o < len) x |= (uint32_t)blob[o] << (8 * k);
         }
-        *reinterpret_cast<uint4 *>(lds + ((q - a) >> 2)) = v;
+        t[d] = x;
+    }
+    return make_uint4(t[0], t[1], t[2], t[3]);
+}
+
+// stage blob bytes [a, b) (a 16-aligned) into lds; bytes at or past `len` read as 0.  Each lane
+// issues up to STAGE_U 16-byte loads before its first LDS store, so a one-wave workgroup keeps
+// several KiB in flight instead of one load per round trip.
+constexpr int STAGE_U = 8;
+__device__ __forceinline__ void stage(const uint8_t *blob, uint64_t len, uint64_t a, uint64_t b, uint32_t *lds) {
+    const uint64_t step = 16ull * blockDim.x;
+    for (uint64_t q0 = a + 16ull * threadIdx.x; q0 < b; q0 += step * STAGE_U) {
+        uint4 v[STAGE_U];
+#pragma unroll
+        for (int u = 0; u < STAGE_U; u++) {
+            const uint64_t q = q0 + step * u;
+            if (q < b) v[u] = load16(blob, len, q);
+        }
+#pragma unroll
+        for (int u = 0; u < STAGE_U; u++) {
+            const uint64_t q = q0 + step * u;
+            if (q < b) *reinterpret_cast<uint4 *>(lds + ((q - a) >> 2)) = v[u];
+        }
     }
 }
 
@@ -80,6 +94,24 @@ __device__ __forceinline__ uint32_t entry_len(const Img &m, const SnapFmt &f, ui
 }
 
 __device__ __forceinline__ uint64_t seg_start(const SnapFmt &f, uint64_t s) { return f.base + s * f.seg; }
+
+// lane-strided walk over cnt rows of W dwords: fn(j, row, dword) with j = row * W + dword; the
+// (row, dword) pair is advanced incrementally -- one division per lane, not one per dword
+template <class Fn>
+__device__ __forceinline__ void for_dwords(uint32_t cnt, uint32_t W, Fn fn) {
+    if (W == 0) return;
+    uint32_t e = threadIdx.x / W, q = threadIdx.x - e * W;
+    const uint32_t de = blockDim.x / W, dq = blockDim.x - de * W;
+    for (uint32_t j = threadIdx.x; j < cnt * W; j += blockDim.x) {
+        fn(j, e, q);
+        q += dq;
+        e += de;
+        if (q >= W) {
+            q -= W;
+            e++;
+        }
+    }
+}
 
 // step 1: transfer function of every (segment, candidate first-entry position); G segments
 // per workgroup, lane = segment * P + candidate
@@ -180,19 +212,27 @@ __global__ __launch_bounds__(256) void k_snap_decode(const uint8_t *blob, SnapFm
     stage(blob, f.len, a, b, lds);
     __syncthreads();
     const Img m{lds, a};
+    __shared__ uint32_t bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
     if (threadIdx.x < nG) {  // one lane per segment lists its entries (nG <= blockDim)
+        // The chain was validated by k_snap_walk; here only the State variant picks the length.
+        // (For a corrupt file the chain is short -- the call reports it -- and this walk stays
+        // inside the segment and the LDS image whatever it reads.)
         const uint64_t s = s0 + threadIdx.x;
         const uint32_t x = start[s];
         uint64_t i = basev[s];
         if (x != SNAP_BAD) {
             const uint64_t end = seg_start(f, s + 1);
+            const uint32_t o_var = f.key_pre + f.key_len + 20;
             uint64_t p = seg_start(f, s) + (uint64_t)x * f.g;
             while (p < end && i < r1) {
-                const uint32_t L = entry_len(m, f, p);
-                if (!L || i - r0 >= list_cap) {
+                if (i - r0 >= list_cap) {
                     atomicOr(res + 1, 1ull);
+                    bad = 1;
                     break;
                 }
+                const uint32_t L = m.ld32(p + o_var) == 1 ? f.lt : f.lp;
                 list[i - r0] = (uint32_t)(p - a);
                 if (i == n - 1) res[0] = p + L;
                 p += L;
@@ -201,31 +241,32 @@ __global__ __launch_bounds__(256) void k_snap_decode(const uint8_t *blob, SnapFm
         }
     }
     __syncthreads();
+    if (bad) {
+        if (threadIdx.x == 0) tomb_part[blockIdx.x] = 0;
+        return;
+    }
     const uint32_t cnt = (uint32_t)(r1 - r0);
     const uint32_t K4 = f.key_len / 4, V4 = f.val_len / 4;
     const uint32_t o_key = f.key_pre, o_stamp = f.key_pre + f.key_len, o_var = o_stamp + 20, o_val = f.lt + f.val_pre;
     // every column's rows [r0, r1) are contiguous: lane j writes dword j of the range
-    for (uint32_t j = threadIdx.x; j < cnt * K4; j += blockDim.x) {
-        const uint32_t e = j / K4, q = j - e * K4;
-        keys[r0 * K4 + j] = lds[(list[e] + o_key) / 4 + q];
-    }
-    for (uint32_t j = threadIdx.x; j < cnt * 2; j += blockDim.x) {
-        const uint32_t e = j >> 1, q = j & 1;
-        phys[r0 * 2 + j] = lds[(list[e] + o_stamp) / 4 + q];
-        node[r0 * 2 + j] = lds[(list[e] + o_stamp + 12) / 4 + q];
-    }
+    for_dwords(cnt, K4, [&](uint32_t j, uint32_t e, uint32_t q) { keys[r0 * K4 + j] = lds[(list[e] + o_key) / 4 + q]; });
+    for_dwords(cnt, 2, [&](uint32_t j, uint32_t e, uint32_t q) {
+        const uint32_t b4 = (list[e] + o_stamp) / 4 + q;
+        phys[r0 * 2 + j] = lds[b4];
+        node[r0 * 2 + j] = lds[b4 + 3];
+    });
     uint32_t my_tomb = 0;
     for (uint32_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-        logical[r0 + e] = lds[(list[e] + o_stamp + 8) / 4];
-        const uint32_t v = lds[(list[e] + o_var) / 4];
+        const uint32_t b4 = (list[e] + o_stamp) / 4;
+        logical[r0 + e] = lds[b4 + 2];
+        const uint32_t v = lds[b4 + 5];
         tags[r0 + e] = (uint8_t)v;
         my_tomb += v;
     }
-    for (uint32_t j = threadIdx.x; j < cnt * V4; j += blockDim.x) {
-        const uint32_t e = j / V4, q = j - e * V4;
+    for_dwords(cnt, V4, [&](uint32_t j, uint32_t e, uint32_t q) {
         const uint32_t base = list[e];
         values[r0 * V4 + j] = lds[(base + o_var) / 4] == 0 ? lds[(base + o_val) / 4 + q] : 0u;
-    }
+    });
     // per-workgroup tombstone count (a same-address atomic per workgroup would serialise
     // ~10^5 workgroups in the L2 atomic unit); summed by k_snap_sum
 #pragma unroll
@@ -321,20 +362,14 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
     if ((e = hipMemsetAsync(start[L - 1], 0, 4, st)) || (e = hipMemsetAsync(basev[L - 1], 0, 8, st)) ||
         (e = hipMemsetAsync(words, 0, 64, st)))
         return e;
+    // entries on the chain from the file's first entry (checked against n at the end: a short
+    // chain only leaves rows unwritten, every access stays inside the blob and the columns)
     uint64_t parsed = 0;
+    uint32_t parsed32 = 0;
     if (L == 1) {
-        uint32_t c32 = 0;
-        if ((e = hipMemcpyAsync(&c32, cnt[0], 4, hipMemcpyDeviceToHost, st))) return e;
-        if ((e = hipStreamSynchronize(st))) return e;
-        parsed = c32;
+        if ((e = hipMemcpyAsync(&parsed32, cnt[0], 4, hipMemcpyDeviceToHost, st))) return e;
     } else {
         if ((e = hipMemcpyAsync(&parsed, cnt[L - 1], 8, hipMemcpyDeviceToHost, st))) return e;
-        if ((e = hipStreamSynchronize(st))) return e;
-    }
-    res->parsed = parsed;
-    if (parsed < n) {  // the file ends, or stops parsing, before entry n
-        *corrupt = 1;
-        return hipSuccess;
     }
     for (size_t l = L - 1; l-- > 0;) {
         if (l == 0)
@@ -369,6 +404,12 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
     unsigned long long w[3] = {0, 0, 0};
     if ((e = hipMemcpyAsync(w, words, 24, hipMemcpyDeviceToHost, st))) return e;
     if ((e = hipStreamSynchronize(st))) return e;
+    if (L == 1) parsed = parsed32;
+    res->parsed = parsed;
+    if (parsed < n) {  // the file ends, or stops parsing, before entry n
+        *corrupt = 1;
+        return hipSuccess;
+    }
     if (w[1]) {  // cannot happen for a chain that parsed in step 1
         *corrupt = 2;
         return hipSuccess;

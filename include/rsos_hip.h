@@ -173,7 +173,9 @@ int rh_store_destroy(rh_store *store);
  * FromIterator / ReplicatedMap::load_bulk (rsos/src/fingerprint_tree_map_iter/into_iter.rs:22-33,
  * src/replicated_map/write.rs:184).  _device: the columns are already in HBM.             */
 int rh_store_load(rh_store *store, const rh_columns *host_cols, size_t n);
-int rh_store_load_device(rh_store *store, const rh_columns *dev_cols, size_t n);
+/* dev_cols were written on `after_stream` (a hipStream_t; NULL = the null stream): the store's
+ * own stream waits for the work already queued there before reading them.                 */
+int rh_store_load_device(rh_store *store, const rh_columns *dev_cols, size_t n, void *after_stream);
 int rh_store_len(const rh_store *store, uint64_t *out);
 /* Aggregate over rank range [lo, hi) */
 int rh_store_aggregate(rh_store *store, uint64_t lo, uint64_t hi, rh_aggregate *out);
@@ -203,7 +205,7 @@ int rh_store_fingerprints(rh_store *store, uint64_t lo, uint64_t hi, uint8_t *ho
 int rh_store_apply(rh_store *store, const rh_columns *host_cols, const uint8_t *ops, size_t n,
                    uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted);
 int rh_store_apply_device(rh_store *store, const rh_columns *dev_cols, const uint8_t *dev_ops, size_t n,
-                          uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted);
+                          uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted, void *after_stream);
 
 /* LSM maintenance.  A batch merges into a sorted signed-delta run (O(batch + delta)); the delta
  * run merges into the base run when it exceeds max(base / divisor, min_rows) rows (default
@@ -245,9 +247,10 @@ int rh_snapshot_decode_device(const rh_schema *schema, int key_form, const void 
 /* Reload: replace the contents of `dated` (record_kind DATED) and / or `projection`
  * (PROJECTION) with a snapshot's entries; either store may be NULL, and both must have the
  * same key and value kinds on the same device.  bytes_on_device: 0 = host bytes (copied to
- * the device), 1 = device bytes.  info (nullable) reports what was read.                  */
+ * the device), 1 = device bytes (written on `after_stream`, which the store waits for).
+ * info (nullable) reports what was read.                                                   */
 int rh_store_load_snapshot(rh_store *dated, rh_store *projection, int key_form, const void *bytes, size_t len,
-                           int bytes_on_device, rh_snapshot_info *info);
+                           int bytes_on_device, rh_snapshot_info *info, void *after_stream);
 
 /* ---- RangeAggregate wire codec ---------------------------------------------------------
  * RangeAggregate<K> (rbsr/src/protocol.rs:63-88) under the gossip codec: bincode 1.3.3

@@ -440,6 +440,13 @@ struct rh_store {
     // Replace the contents with m records.  Sorted, duplicate-free input is required unless
     // last_wins, which sorts on the device and keeps the last record of each repeated key --
     // the result of inserting the records one by one (just_insert_bulk, src/replica/write.rs:107-121).
+    hipEvent_t dep = nullptr;  // orders the store's stream after a producer stream
+    int after(void *producer) {
+        if (!dep) RH_HIP(hipEventCreateWithFlags(&dep, hipEventDisableTiming));
+        RH_HIP(hipEventRecord(dep, static_cast<hipStream_t>(producer)));
+        RH_HIP(hipStreamWaitEvent(stream, dep, 0));
+        return RH_OK;
+    }
     int load_device(const rh_columns &c, size_t m, bool last_wins = false) {
         int rc;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
@@ -612,6 +619,8 @@ struct rh_store {
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
         snap.release();
         scratch.release();
+        if (dep) (void)hipEventDestroy(dep);
+        dep = nullptr;
     }
 };
 
@@ -662,11 +671,12 @@ int rh_store_load(rh_store *s, const rh_columns *h, size_t n) {
     return s->load_device(s->staging.view(s->schema), n);
 }
 
-int rh_store_load_device(rh_store *s, const rh_columns *dev_cols, size_t n) {
+int rh_store_load_device(rh_store *s, const rh_columns *dev_cols, size_t n, void *after_stream) {
     if (!s) return fail(RH_ERR_ARG, "NULL");
     int rc = check_cols(s->schema, dev_cols, n);
     if (rc) return rc;
     RH_LOCK(s);
+    if ((rc = s->after(after_stream))) return rc;
     return s->load_device(*dev_cols, n);
 }
 
@@ -773,11 +783,12 @@ int rh_store_apply(rh_store *s, const rh_columns *h, const uint8_t *ops, size_t 
 }
 
 int rh_store_apply_device(rh_store *s, const rh_columns *dev_cols, const uint8_t *dev_ops, size_t m,
-                          uint64_t *n_new, uint64_t *n_over, uint64_t *n_del) {
+                          uint64_t *n_new, uint64_t *n_over, uint64_t *n_del, void *after_stream) {
     if (!s) return fail(RH_ERR_ARG, "NULL");
     int rc = check_cols(s->schema, dev_cols, m);
     if (rc) return rc;
     RH_LOCK(s);
+    if ((rc = s->after(after_stream))) return rc;
     uint64_t c[3];
     if ((rc = s->apply_device(*dev_cols, dev_ops, m, c))) return rc;
     if (n_new) *n_new = c[0];
@@ -920,7 +931,7 @@ int rh_snapshot_decode_device(const rh_schema *schema, int key_form, const void 
 }
 
 int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const void *bytes, size_t len,
-                           int on_device, rh_snapshot_info *info) {
+                           int on_device, rh_snapshot_info *info, void *after_stream) {
     if (!dated && !proj) return fail(RH_ERR_ARG, "no store given");
     if (!bytes && len) return fail(RH_ERR_ARG, "bytes is NULL");
     if (dated && dated->schema.record_kind != RH_REC_DATED) return fail(RH_ERR_ARG, "dated store must be DATED");
@@ -945,6 +956,7 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
     const size_t hl = std::min<size_t>(len, 16);
     if (on_device) {
         if (!aligned16(bytes)) return fail(RH_ERR_ARG, "snapshot bytes must be 16-byte aligned");
+        if ((rc = a->after(after_stream))) return rc;
         if (hl) RH_HIP(hipMemcpyAsync(h, bytes, hl, hipMemcpyDeviceToHost, a->stream));
         RH_HIP(hipStreamSynchronize(a->stream));
     } else if (hl) {

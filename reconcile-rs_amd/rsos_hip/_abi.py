@@ -61,7 +61,7 @@ SIGNATURES = [
     ("rh_store_create", C.c_int, [C.c_int, C.POINTER(Schema), C.POINTER(C.c_void_p)]),
     ("rh_store_destroy", C.c_int, [P]),
     ("rh_store_load", C.c_int, [P, C.POINTER(Columns), SZ]),
-    ("rh_store_load_device", C.c_int, [P, C.POINTER(Columns), SZ]),
+    ("rh_store_load_device", C.c_int, [P, C.POINTER(Columns), SZ, VP]),
     ("rh_store_len", C.c_int, [P, C.POINTER(C.c_uint64)]),
     ("rh_store_aggregate", C.c_int, [P, C.c_uint64, C.c_uint64, C.POINTER(Aggregate)]),
     ("rh_store_aggregates", C.c_int, [P, U64P, U64P, SZ, P]),
@@ -74,14 +74,14 @@ SIGNATURES = [
     ("rh_store_apply", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rh_store_apply_device", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
-                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), VP]),
     ("rh_store_compact", C.c_int, [P]),
     ("rh_store_set_compaction", C.c_int, [P, C.c_uint64, C.c_uint64]),
     ("rh_store_stats", C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rh_snapshot_header", C.c_int, [VP, SZ, C.POINTER(C.c_uint64)]),
     ("rh_snapshot_decode_device", C.c_int, [C.POINTER(Schema), C.c_int, VP, SZ, C.POINTER(Columns), SZ,
                                             C.POINTER(SnapshotInfo), VP]),
-    ("rh_store_load_snapshot", C.c_int, [P, P, C.c_int, VP, SZ, C.c_int, C.POINTER(SnapshotInfo)]),
+    ("rh_store_load_snapshot", C.c_int, [P, P, C.c_int, VP, SZ, C.c_int, C.POINTER(SnapshotInfo), VP]),
     ("rh_wire_encode_range_aggregates", C.c_int, [C.POINTER(Schema), C.c_int, C.c_int, U8P, VP, U8P, VP, P, SZ,
                                                   U8P, SZ, C.POINTER(C.c_size_t)]),
     ("rh_wire_decode_range_aggregates", C.c_int, [C.POINTER(Schema), C.c_int, C.c_int, U8P, SZ, SZ, U8P, VP, U8P,

@@ -74,9 +74,13 @@ def load_snapshot(data, dated=None, projection=None, key_form: str = "array") ->
         ptr, size, keep = data.data_ptr(), data.numel() * data.element_size(), data
     else:
         ptr, size, keep = _host_buffer(data)
+    stream = None
+    if is_dev:
+        import torch
+        stream = torch.cuda.current_stream(data.device).cuda_stream
     A.check(A.lib().rh_store_load_snapshot(dated._h if dated is not None else None,
                                            projection._h if projection is not None else None,
-                                           _FORMS[key_form], ptr, size, 1 if is_dev else 0, C.byref(info)),
+                                           _FORMS[key_form], ptr, size, 1 if is_dev else 0, C.byref(info), stream),
             "rh_store_load_snapshot")
     del keep
     return SnapshotInfo.from_c(info)

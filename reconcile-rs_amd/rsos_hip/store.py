@@ -30,6 +30,12 @@ Key = Union[bytes, int]
 HOST_COLS = ("keys", "phys", "logical", "node", "tags", "values")
 
 
+def _torch_stream() -> int:
+    """The stream torch queued the device columns on: the store waits for it before reading."""
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
 def _np_ptr(a: Optional[np.ndarray]) -> Optional[int]:
     return None if a is None else a.ctypes.data
 
@@ -106,7 +112,7 @@ class GpuFingerprintStore:
         from .device import _check_cols, _columns
         n = _check_cols(self.schema, cols)
         c = _columns(cols)
-        A.check(A.lib().rh_store_load_device(self._h, C.byref(c), n), "rh_store_load_device")
+        A.check(A.lib().rh_store_load_device(self._h, C.byref(c), n, _torch_stream()), "rh_store_load_device")
 
     def apply_device(self, cols, ops=None) -> Tuple[int, int, int]:
         """apply() with device (torch) columns / ops; returns (new, overwritten, deleted)."""
@@ -117,7 +123,8 @@ class GpuFingerprintStore:
         c = _columns(cols)
         a, b, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
         A.check(A.lib().rh_store_apply_device(self._h, C.byref(c), None if ops is None else ops.data_ptr(), m,
-                                              C.byref(a), C.byref(b), C.byref(d)), "rh_store_apply_device")
+                                              C.byref(a), C.byref(b), C.byref(d), _torch_stream()),
+                "rh_store_apply_device")
         return int(a.value), int(b.value), int(d.value)
 
     def compact(self) -> None:

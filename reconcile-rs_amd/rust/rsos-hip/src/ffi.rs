@@ -96,7 +96,8 @@ extern "C" {
     pub fn rh_store_create(device: c_int, schema: *const rh_schema, out: *mut *mut rh_store) -> c_int;
     pub fn rh_store_destroy(store: *mut rh_store) -> c_int;
     pub fn rh_store_load(store: *mut rh_store, cols: *const rh_columns, n: usize) -> c_int;
-    pub fn rh_store_load_device(store: *mut rh_store, dev_cols: *const rh_columns, n: usize) -> c_int;
+    pub fn rh_store_load_device(store: *mut rh_store, dev_cols: *const rh_columns, n: usize,
+                                after_stream: *mut c_void) -> c_int;
     pub fn rh_store_len(store: *const rh_store, out: *mut u64) -> c_int;
     pub fn rh_store_aggregate(store: *mut rh_store, lo: u64, hi: u64, out: *mut rh_aggregate) -> c_int;
     pub fn rh_store_aggregates(store: *mut rh_store, lo: *const u64, hi: *const u64, r: usize, out: *mut rh_aggregate) -> c_int;
@@ -110,7 +111,8 @@ extern "C" {
     pub fn rh_store_apply(store: *mut rh_store, cols: *const rh_columns, ops: *const u8, n: usize,
                           n_new: *mut u64, n_over: *mut u64, n_del: *mut u64) -> c_int;
     pub fn rh_store_apply_device(store: *mut rh_store, dev_cols: *const rh_columns, dev_ops: *const u8, n: usize,
-                                 n_new: *mut u64, n_over: *mut u64, n_del: *mut u64) -> c_int;
+                                 n_new: *mut u64, n_over: *mut u64, n_del: *mut u64,
+                                 after_stream: *mut c_void) -> c_int;
     pub fn rh_store_compact(store: *mut rh_store) -> c_int;
     pub fn rh_store_set_compaction(store: *mut rh_store, divisor: u64, min_rows: u64) -> c_int;
     pub fn rh_store_stats(store: *const rh_store, base_rows: *mut u64, delta_rows: *mut u64,
@@ -121,7 +123,7 @@ extern "C" {
                                      stream: *mut c_void) -> c_int;
     pub fn rh_store_load_snapshot(dated: *mut rh_store, projection: *mut rh_store, key_form: c_int,
                                   bytes: *const c_void, len: usize, bytes_on_device: c_int,
-                                  info: *mut rh_snapshot_info) -> c_int;
+                                  info: *mut rh_snapshot_info, after_stream: *mut c_void) -> c_int;
     pub fn rh_wire_encode_range_aggregates(schema: *const rh_schema, key_form: c_int, msg_tag: c_int,
                                            start_kinds: *const u8, start_keys: *const c_void, end_kinds: *const u8,
                                            end_keys: *const c_void, aggregates: *const rh_aggregate, r: usize,

@@ -564,3 +564,52 @@ def test_store_batch_keys_sharing_leading_bytes(gpu, oracle_lib):
     assert np.array_equal(st.fingerprints(), want)
     assert [k for k, _ in st.enumerate()] == [keys[i].tobytes() for i in order]
     st.close()
+
+
+def _torch_root(torch, fps) -> int:
+    """Σ fingerprints mod 2^256 by an independent torch reduction over u16 limbs."""
+    limbs16 = fps.view(torch.int16).to(torch.int64) & 0xFFFF
+    col = limbs16.sum(dim=0).cpu().tolist()
+    return sum(int(c) << (16 * i) for i, c in enumerate(col)) % M256
+
+
+def test_full_size_incremental_properties(gpu):
+    """config5's shape at a tenth of the size: 10 M resident records, then 1 M-record random-key
+    batches (inserts, then a batch that overwrites 100 k and deletes 100 k existing keys).  After
+    each batch the store's root equals an independent torch reduction over the lifts of exactly
+    the records that should be live, and rank / size agree (count-agreement law)."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema, lift_records
+    from rsos_hip.store import KeyRange
+    from rsos_hip.synth import make_records
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n, m = 10_000_000, 1_000_000
+    base = make_records(s, n, seed=5)
+    st = GpuFingerprintStore(s)
+    st.load_bulk_device(base)
+    live = [lift_records(s, base, block_sums=False)[0]]
+    for k in range(2):
+        b = make_records(s, m, seed=600 + k, random_keys=True)
+        assert st.apply_device(b) == (m, 0, 0)
+        live.append(lift_records(s, b, block_sums=False)[0])
+        root = st.aggregate()
+        assert root.size == n + (k + 1) * m
+        assert root.fingerprint.to_int() == (sum(_torch_root(torch, f) for f in live)) % M256
+    # overwrite rows [0, 100k) of the base with new values, delete rows [100k, 200k)
+    ov = {c: t[:200_000].clone() for c, t in base.items()}
+    ov["values"][:100_000] ^= 0x5A
+    ops = torch.zeros(200_000, dtype=torch.uint8, device="cuda")
+    ops[100_000:] = 1
+    assert st.apply_device(ov, ops) == (0, 100_000, 100_000)
+    new_fps, _ = lift_records(s, {c: t[:100_000] for c, t in ov.items()}, block_sums=False)
+    want = (sum(_torch_root(torch, f) for f in live) - _torch_root(torch, live[0][:200_000])
+            + _torch_root(torch, new_fps)) % M256
+    root = st.aggregate()
+    assert root.size == n + 2 * m - 100_000 and root.fingerprint.to_int() == want
+    # count agreement over a key range spanning base and delta rows
+    lo_key, hi_key = base["keys"][50_000].cpu().numpy().tobytes(), base["keys"][5_000_000].cpu().numpy().tobytes()
+    agg = st.aggregate(KeyRange(lo_key, hi_key))
+    assert agg.size == st.rank(hi_key) - st.rank(lo_key)
+    st.compact()
+    assert st.aggregate() == root and st.stats()["delta_rows"] == 0
+    st.close()

@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     p.add_argument("--cpu-sample", type=int, default=0, help="records in the CPU baseline sample (0: the whole shard)")
     p.add_argument("--batch", type=int, default=1_000_000, help="config5: records per update batch")
+    p.add_argument("--overwrite", type=float, default=0.0,
+                   help="config5: fraction of each batch that re-stamps existing keys (the new - old delta)")
     p.add_argument("--e2e", action="store_true", help="also time host->device->host end to end (DESIGN.md)")
     p.add_argument("--check", type=int, default=1, help="oracle spot-check of a sample before timing")
     return p.parse_args()
@@ -236,14 +238,25 @@ def incremental(args, world, rank, dev, dist):
     schema = getattr(RecordSchema, kind)(kname, vname)
     st = GpuFingerprintStore(schema, device=dev.index)
     base = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     st.load_bulk_device(base)
     load_s = time.perf_counter() - t0
-    del base
-    torch.cuda.empty_cache()
     m = args.batch
-    batches = [make_records(schema, m, seed=1000 * (rank + 1) + k, device=dev, random_keys=True)
-               for k in range(args.warmup + args.steps)]
+    m_over = int(m * args.overwrite)
+    batches = []
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7 + rank)
+    for k in range(args.warmup + args.steps):
+        b = make_records(schema, m, seed=1000 * (rank + 1) + k, device=dev, random_keys=True)
+        if m_over:  # re-stamp distinct existing keys: an overwrite, the new - old delta (mutate.rs:31-41)
+            rows = torch.randperm(n, generator=gen, device=dev)[:m_over]
+            b["keys"][:m_over] = base["keys"][rows]
+            b["phys"][:m_over] = base["phys"][rows] + 1_000_000
+        batches.append(b)
+    del base
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     for k in range(args.warmup):
         st.apply_device(batches[k])
     if dist is not None:
@@ -276,7 +289,9 @@ def incremental(args, world, rank, dev, dist):
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (seeded): sorted resident set + uniformly random update keys",
-            "config": {"workload": desc, "resident_records_per_gpu": n, "batch": m,
+            "config": {"workload": desc + (f"; {args.overwrite:.0%} of each batch overwrites existing keys"
+                                           if m_over else ""),
+                       "resident_records_per_gpu": n, "batch": m, "overwrites_per_batch": m_over,
                        "parallelism": f"key-range shards x{world}"},
             "batch_counts": {"new": counts[0], "overwritten": counts[1], "deleted": counts[2]},
             "final_size": root.size, "bulk_load_s": round(load_s, 3),
@@ -365,6 +380,17 @@ def reload(args, world, rank, dev, dist):
                          "kernel_avg_us": round(dec_s * 1e6, 1)},
             "root_check": "dated root == Σ lift(source rows)",
         }
+        if args.e2e:  # the file's bytes in (pinned) host memory: H2D inside the reload
+            host = blob.cpu().pin_memory()
+            best = None
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                load_snapshot(host.numpy(), dated, proj)
+                dt = time.perf_counter() - t1
+                best = dt if best is None else min(best, dt)
+            line["end_to_end"] = {"entries": n, "seconds": round(best, 5), "m_entries_per_s": round(n / best / 1e6, 1),
+                                  "from": "pinned host bytes (H2D of the whole file inside the call)"}
         if args.cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_reload(sd, sp, cols, args.cpu_sample or 1_000_000)
         print(json.dumps(line), flush=True)

@@ -440,6 +440,22 @@ struct rh_store {
     // Replace the contents with m records.  Sorted, duplicate-free input is required unless
     // last_wins, which sorts on the device and keeps the last record of each repeated key --
     // the result of inserting the records one by one (just_insert_bulk, src/replica/write.rs:107-121).
+    // sort m (key, fp, op) rows into key order (sops receives the ops); *flags & 1: duplicate
+    // keys.  One sync: the MSD-only pass, then the full sort only if it reported a tie.
+    int sort_keys(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, uint8_t *okeys,
+                  uint8_t *ofps, uint32_t *flags) {
+        int rc;
+        if ((rc = sops.ensure(m + 64)) || (rc = flag.ensure(4))) return rc;
+        for (int full = 0; full < 2; full++) {
+            RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
+            RH_HIP(kops->sort_batch(keys, fps, ops, m, scratch, okeys, ofps, sops.p, flag.p, full == 1, stream));
+            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            RH_HIP(hipMemcpyAsync(flags, flag.p, 4, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+            if (!(*flags & 2)) return RH_OK;
+        }
+        return RH_OK;
+    }
     hipEvent_t dep = nullptr;  // orders the store's stream after a producer stream
     int after(void *producer) {
         if (!dep) RH_HIP(hipEventCreateWithFlags(&dep, hipEventDisableTiming));
@@ -470,14 +486,9 @@ struct rh_store {
             const int nxt = 1 - cb;
             if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)))
                 return rc;
-            RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
-            RH_HIP(kops->sort_batch(bkeys[cb].p, bfps[cb].p, nullptr, m, scratch, bkeys[nxt].p, bfps[nxt].p, sops.p,
-                                    flag.p, stream));
-            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-            uint32_t dup = 0;
-            RH_HIP(hipMemcpyAsync(&dup, flag.p, 4, hipMemcpyDeviceToHost, stream));
-            if ((rc = sync())) return rc;
-            if (dup) {  // stable sort: within a run of equal keys the last record is last
+            uint32_t flags = 0;
+            if ((rc = sort_keys(bkeys[cb].p, bfps[cb].p, nullptr, m, bkeys[nxt].p, bfps[nxt].p, &flags))) return rc;
+            if (flags & 1) {  // stable sort: within a run of equal keys the last record is last
                 RH_HIP(kops->dedup_last(bkeys[nxt].p, bfps[nxt].p, m, scratch, bkeys[cb].p, bfps[cb].p, counts.p,
                                         stream));
                 if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -526,14 +537,9 @@ struct rh_store {
         // 1. lift the batch (delete rows are lifted too and ignored)
         if ((rc = lift_dispatch(schema, c, m, lfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
         // 2. key order + duplicate check
-        RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
-        RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, scratch, skeys.p, sfps.p, sops.p,
-                                flag.p, stream));
-        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        uint32_t dup = 0;
-        RH_HIP(hipMemcpyAsync(&dup, flag.p, 4, hipMemcpyDeviceToHost, stream));
-        if ((rc = sync())) return rc;
-        if (dup) return fail(RH_ERR_ARG, "duplicate key within one batch");
+        uint32_t flags = 0;
+        if ((rc = sort_keys(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, skeys.p, sfps.p, &flags))) return rc;
+        if (flags & 1) return fail(RH_ERR_ARG, "duplicate key within one batch");
         // 3. where each key is now: base and delta runs
         uint32_t *rank_b = scratch.u32(9, m), *rank_d = scratch.u32(10, m);
         uint8_t *present_b = scratch.u8(2, m), *present_d = scratch.u8(3, m);

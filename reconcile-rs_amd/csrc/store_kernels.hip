@@ -135,25 +135,22 @@ __global__ void k_iota(uint32_t *p, uint64_t m) {
     if (j < m) p[j] = (uint32_t)j;
 }
 
-// *tie = 1 if two keys adjacent in perm order share their most significant digit
-template <int KK, int KL>
-__global__ void k_prefix_ties(const uint8_t *keys, const uint32_t *perm, uint64_t m, uint32_t *tie) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
-    if (j < m && key_digit<KK, KL>(keys + (uint64_t)perm[j] * KL, 0) == key_digit<KK, KL>(keys + (uint64_t)perm[j - 1] * KL, 0))
-        atomicOr(tie, 1u);
-}
-
-// gather the batch into key order; flag adjacent duplicates
+// gather the batch into key order; flags |= 1 on adjacent duplicates, and (msd_only) |= 2 when
+// adjacent keys share their most significant digit (order not final)
 template <int KK, int KL>
 __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, const uint32_t *perm,
-                         uint64_t m, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *dup) {
+                         uint64_t m, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, int msd_only) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const uint64_t s = perm[j];
     copy_bytes<KL>(skeys + j * KL, keys + s * KL);
     copy_bytes<32>(sfps + 32 * j, fps + 32 * s);
     sops[j] = ops ? ops[s] : 0;
-    if (j > 0 && key_cmp<KK, KL>(keys + s * KL, keys + (uint64_t)perm[j - 1] * KL) == 0) atomicOr(dup, 1u);
+    if (j > 0) {
+        const uint8_t *prev = keys + (uint64_t)perm[j - 1] * KL;
+        if (key_cmp<KK, KL>(keys + s * KL, prev) == 0) atomicOr(flags, 1u);
+        else if (msd_only && key_digit<KK, KL>(keys + s * KL, 0) == key_digit<KK, KL>(prev, 0)) atomicOr(flags, 2u);
+    }
 }
 
 // ---- search ---------------------------------------------------------------------------------
@@ -477,14 +474,12 @@ struct KeyOps final : StoreKeyOps {
     static constexpr int BITS = KK == KEY_U32 ? 32 : 64;
 
     hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
-                          uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *dup, hipStream_t st) override {
+                          uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, bool full,
+                          hipStream_t st) override {
         hipError_t e;
         uint32_t *perm = s.u32(0, m), *perm2 = s.u32(1, m);
         uint64_t *dig = s.u64(0, m), *dig2 = s.u64(1, m);
         if (s.err) return s.err;
-        // Multi-digit keys: sort on the most significant digit alone first.  If no two keys then
-        // share that digit the order is already final (random and spread keys: always); else
-        // fall back to the full LSD sort (least significant digit first, stable passes).
         auto pass = [&](int d) -> hipError_t {
             hipError_t e2;
             hipLaunchKernelGGL((k_digit<KK, KL>), g1(m), dim3(256), 0, st, keys, perm, m, d, dig);
@@ -497,24 +492,14 @@ struct KeyOps final : StoreKeyOps {
             return hipSuccess;
         };
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
-        if (D > 1) {
-            uint32_t *tie = s.u32(14, 1);
-            if (s.err) return s.err;
-            if ((e = hipMemsetAsync(tie, 0, 4, st))) return e;
-            if ((e = pass(0))) return e;
-            hipLaunchKernelGGL((k_prefix_ties<KK, KL>), g1(m), dim3(256), 0, st, keys, perm, m, tie);
-            uint32_t tie_h = 0;
-            if ((e = hipMemcpyAsync(&tie_h, tie, 4, hipMemcpyDeviceToHost, st))) return e;
-            if ((e = hipStreamSynchronize(st))) return e;
-            if (tie_h) {
-                hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
-                for (int d = D - 1; d >= 0; d--)
-                    if ((e = pass(d))) return e;
-            }
-        } else {
-            if ((e = pass(0))) return e;
-        }
-        hipLaunchKernelGGL((k_gather<KK, KL>), g1(m), dim3(256), 0, st, keys, fps, ops, perm, m, skeys, sfps, sops, dup);
+        // multi-digit keys: the most significant digit alone orders random and spread keys
+        // (k_gather reports a tie); the LSD sort (least significant digit first, stable passes)
+        // is the fallback
+        const int lo_digit = (full || D == 1) ? D - 1 : 0;
+        for (int d = lo_digit; d >= 0; d--)
+            if ((e = pass(d))) return e;
+        hipLaunchKernelGGL((k_gather<KK, KL>), g1(m), dim3(256), 0, st, keys, fps, ops, perm, m, skeys, sfps, sops,
+                           flags, (full || D == 1) ? 0 : 1);
         return hipGetLastError();
     }
 

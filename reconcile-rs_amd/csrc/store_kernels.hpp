@@ -70,11 +70,13 @@ static_assert(sizeof(DeltaRec) == 80, "DeltaRec layout");
 // Key-type-specialised device operations of the store.
 struct StoreKeyOps {
     virtual ~StoreKeyOps() = default;
-    // sort a batch by key (LSD radix over u64 digits), gather keys / fingerprints / ops into key
-    // order; *dup |= 1 if two batch keys are equal
+    // sort a batch by key and gather keys / fingerprints / ops into key order.  full = false:
+    // one radix pass on the most significant u64 digit only, and *flags |= 2 if two keys share
+    // that digit (the order is then not final: sort again with full = true, the LSD radix over
+    // every digit).  *flags |= 1 if two batch keys are equal.
     virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
-                                  Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *dup,
-                                  hipStream_t st) = 0;
+                                  Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags,
+                                  bool full, hipStream_t st) = 0;
     // lower-bound rank of each query key (and whether it is present)
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;

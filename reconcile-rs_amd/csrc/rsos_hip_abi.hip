@@ -115,12 +115,16 @@ template <class T>
 struct DevBuf {
     T *p = nullptr;
     size_t cap = 0;  // elements
+    // Grows geometrically (x1.5): a run that gains a batch of rows per call (the delta run) is
+    // reallocated O(log n) times, not every call -- hipFree drains the device, and one
+    // realloc per batch cost ~0.6 ms of idle GPU per config5 batch.
     int ensure(size_t n) {
         if (n <= cap && p) return RH_OK;
         if (p) (void)hipFree(p);
         p = nullptr;
+        const size_t grown = cap + cap / 2;
         cap = 0;
-        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        size_t bytes = std::max<size_t>(std::max(n, grown), 1) * sizeof(T);
         bytes = (bytes + 255) & ~size_t(255);
         hipError_t e = hipMalloc(&p, bytes);
         if (e != hipSuccess) return fail(RH_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -390,13 +394,13 @@ struct rh_store {
     uint64_t nd = 0;
     int cd = 0;
     int64_t dtotal = 0;  // Σ count deltas
-    DevBuf<uint8_t> dkeys[2], dpay[2], dbsums, dssums;
-    DevBuf<int32_t> dcnt;  // inclusive prefix of the count deltas
+    DevBuf<uint8_t> dkeys[2], dpay[2], dbsums[2], dssums[2];
+    DevBuf<int32_t> dcnt[2];  // inclusive prefix of the count deltas
     uint64_t compact_div = 8, compact_min = 65536, compactions = 0;
     // batch scratch
     DevColumns staging;
     DevBuf<uint8_t> lfps, skeys, sfps, sops, hops, bpay, dops, cfps, cops;
-    DevBuf<uint64_t> counts, counts2;
+    DevBuf<uint64_t> counts, counts2, results;
     DevBuf<uint32_t> flag;
     // query scratch
     DevBuf<uint64_t> q_lo, q_hi, q_dlo, q_dhi, q_merged;
@@ -421,20 +425,20 @@ struct rh_store {
         }
         return RH_OK;
     }
-    int resum_delta() {  // contribution sums + count prefix; leaves dtotal on the host
+    // Contribution sums + count-delta prefix of delta buffer `buf`, sized for n_max rows; the
+    // true row count n = nd_old + counts[0] - counts[2] is read on the device (rows past it
+    // count as zero), so no host round trip is needed between the merge and the sums.
+    int resum_delta_async(int buf, uint64_t n_max, uint64_t nd_old, const uint64_t *merge_counts) {
         int rc;
-        const size_t nbk = rh_num_blocks(nd), ns = rh_num_superblocks(nd);
-        if ((rc = dbsums.ensure(nbk * 32 + 32)) || (rc = dssums.ensure(ns * 32 + 32)) || (rc = dcnt.ensure(nd + 16)))
+        const size_t nbk = rh_num_blocks(n_max), ns = rh_num_superblocks(n_max);
+        if ((rc = dbsums[buf].ensure(nbk * 32 + 32)) || (rc = dssums[buf].ensure(ns * 32 + 32)) ||
+            (rc = dcnt[buf].ensure(n_max + 16)))
             return rc;
-        dtotal = 0;
-        if (!nd) return RH_OK;
-        RH_HIP(rh::launch_delta_sums(dpay[cd].p, nd, dbsums.p, dcnt.p, scratch, stream));
-        RH_HIP(rh::launch_reduce(dbsums.p, nbk, dssums.p, stream));
+        if (!n_max) return RH_OK;
+        RH_HIP(rh::launch_delta_sums(dpay[buf].p, n_max, nd_old, merge_counts, dbsums[buf].p, dcnt[buf].p, scratch,
+                                     stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        int32_t t = 0;
-        RH_HIP(hipMemcpyAsync(&t, dcnt.p + nd - 1, 4, hipMemcpyDeviceToHost, stream));
-        if ((rc = sync())) return rc;
-        dtotal = t;
+        RH_HIP(rh::launch_reduce(dbsums[buf].p, nbk, dssums[buf].p, stream));
         return RH_OK;
     }
     // Replace the contents with m records.  Sorted, duplicate-free input is required unless
@@ -536,33 +540,68 @@ struct rh_store {
             return rc;
         // 1. lift the batch (delete rows are lifted too and ignored)
         if ((rc = lift_dispatch(schema, c, m, lfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
-        // 2. key order + duplicate check
-        uint32_t flags = 0;
-        if ((rc = sort_keys(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, skeys.p, sfps.p, &flags))) return rc;
-        if (flags & 1) return fail(RH_ERR_ARG, "duplicate key within one batch");
-        // 3. where each key is now: base and delta runs
+        // 2-5 run without a host round trip: everything is written to the delta run's *other*
+        // buffers, and one sync at the end brings back the flags and counts.  A duplicate key
+        // then leaves the store exactly as it was (nothing is committed); a tie on the leading
+        // key digit re-runs the steps with the full sort.
+        const int nxt = 1 - cd;
+        const uint64_t n_max = nd + m;
         uint32_t *rank_b = scratch.u32(9, m), *rank_d = scratch.u32(10, m);
         uint8_t *present_b = scratch.u8(2, m), *present_d = scratch.u8(3, m);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        RH_HIP(kops->search(bkeys[cb].p, nb, skeys.p, m, rank_b, present_b, stream));
-        RH_HIP(kops->search(dkeys[cd].p, nd, skeys.p, m, rank_d, present_d, stream));
-        // 4. the batch's delta records, then merge them into the delta run
-        RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d, dpay[cd].p,
-                                      bpay.p, dops.p, counts.p, scratch, stream));
-        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        const int nxt = 1 - cd;
-        if ((rc = dkeys[nxt].ensure((nd + m) * kl + 64)) || (rc = dpay[nxt].ensure((nd + m) * sizeof(rh::DeltaRec) + 64)))
+        // capacity for the largest delta run the policy allows (threshold + one batch), so the
+        // run grows without reallocations (a hipFree drains the device)
+        const uint64_t thresh = std::max<uint64_t>(nb / compact_div, compact_min);
+        const uint64_t plan = std::max<uint64_t>(n_max, std::min<uint64_t>(thresh, nb + nd) + m);
+        if ((rc = dkeys[nxt].ensure(plan * kl + 64)) || (rc = dpay[nxt].ensure(plan * sizeof(rh::DeltaRec) + 64)) ||
+            (rc = dbsums[nxt].ensure(rh_num_blocks(plan) * 32 + 32)) ||
+            (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) || (rc = dcnt[nxt].ensure(plan + 16)))
             return rc;
-        RH_HIP(kops->merge(dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p, dops.p, m, sizeof(rh::DeltaRec), scratch,
-                           dkeys[nxt].p, dpay[nxt].p, counts2.p, stream, rank_d, present_d));
-        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        uint64_t c2[3];
-        RH_HIP(hipMemcpyAsync(out, counts.p, 24, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(c2, counts2.p, 24, hipMemcpyDeviceToHost, stream));
-        if ((rc = sync())) return rc;
+        // one 64-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,
+        // [6] sort flags, [7] Σ count deltas of the new delta run
+        if ((rc = results.ensure(8))) return rc;
+        uint64_t *r_counts = results.p, *r_merge = results.p + 3;
+        uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
+        int32_t *r_total = reinterpret_cast<int32_t *>(results.p + 7);
+        uint64_t host[8];
+        uint32_t flags = 0;
+        for (int full = 0; full < 2; full++) {
+            // 2. key order (+ duplicate / leading-digit-tie flags)
+            RH_HIP(hipMemsetAsync(results.p, 0, 64, stream));
+            RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, scratch, skeys.p, sfps.p,
+                                    sops.p, r_flags, full == 1, stream));
+            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            // 3. where each key is now: base and delta runs
+            RH_HIP(kops->search(bkeys[cb].p, nb, skeys.p, m, rank_b, present_b, stream));
+            RH_HIP(kops->search(dkeys[cd].p, nd, skeys.p, m, rank_d, present_d, stream));
+            // 4. the batch's delta records, merged into the delta run's other buffer
+            RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d,
+                                          dpay[cd].p, bpay.p, dops.p, r_counts, scratch, stream));
+            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            RH_HIP(kops->merge(dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p, dops.p, m, sizeof(rh::DeltaRec), scratch,
+                               dkeys[nxt].p, dpay[nxt].p, r_merge, stream, rank_d, present_d));
+            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            // 5. its sums, then the one round trip
+            if ((rc = resum_delta_async(nxt, n_max, nd, r_merge))) return rc;
+            RH_HIP(hipMemcpyAsync(r_total, dcnt[nxt].p + n_max - 1, 4, hipMemcpyDeviceToDevice, stream));
+            RH_HIP(hipMemcpyAsync(host, results.p, 64, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+            memcpy(&flags, &host[6], 4);
+            if (!(flags & 2)) break;
+        }
+        int32_t total;
+        memcpy(&total, &host[7], 4);
+        const uint64_t c2[3] = {host[3], host[4], host[5]};
+        out[0] = host[0];
+        out[1] = host[1];
+        out[2] = host[2];
+        if (flags & 1) {
+            out[0] = out[1] = out[2] = 0;
+            return fail(RH_ERR_ARG, "duplicate key within one batch");
+        }
         cd = nxt;
         nd = nd + c2[0] - c2[2];
-        if ((rc = resum_delta())) return rc;
+        dtotal = total;
         if (nd > std::max<uint64_t>(nb / compact_div, compact_min)) return compact();
         return RH_OK;
     }
@@ -592,10 +631,10 @@ struct rh_store {
                                       reinterpret_cast<uint64_t *>(res), stream));
         if (nd) {
             RH_HIP(kops->bounds(dkeys[cd].p, nd, q_keys.p, lo_kind, q_keys.p + kl, hi_kind, q_dlo.p, q_dhi.p, stream));
-            RH_HIP(rh::launch_range_query(dpay[cd].p, dbsums.p, dssums.p, nd, q_dlo.p, q_dhi.p, 1,
+            RH_HIP(rh::launch_range_query(dpay[cd].p, dbsums[cd].p, dssums[cd].p, nd, q_dlo.p, q_dhi.p, 1,
                                           reinterpret_cast<uint64_t *>(q_dout.p), stream, sizeof(rh::DeltaRec)));
             RH_HIP(rh::launch_agg_merge(reinterpret_cast<uint64_t *>(q_bout.p), reinterpret_cast<uint64_t *>(q_dout.p),
-                                        q_dlo.p, q_dhi.p, dcnt.p, reinterpret_cast<uint64_t *>(q_out.p), stream));
+                                        q_dlo.p, q_dhi.p, dcnt[cd].p, reinterpret_cast<uint64_t *>(q_out.p), stream));
         }
         RH_HIP(hipMemcpyAsync(out, q_out.p, sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
         return sync();
@@ -608,7 +647,7 @@ struct rh_store {
         RH_HIP(hipMemcpyAsync(q_keys.p, keys, m * kl, hipMemcpyHostToDevice, stream));
         RH_HIP(kops->search(bkeys[cb].p, nb, q_keys.p, m, q_rank.p, nullptr, stream));
         if (nd) RH_HIP(kops->search(dkeys[cd].p, nd, q_keys.p, m, q_drank.p, nullptr, stream));
-        RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, dcnt.p, m, q_merged.p, stream));
+        RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, dcnt[cd].p, m, q_merged.p, stream));
         RH_HIP(hipMemcpyAsync(out, q_merged.p, m * 8, hipMemcpyDeviceToHost, stream));
         return sync();
     }
@@ -617,10 +656,14 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
         }
-        bsums.release(); ssums.release(); dbsums.release(); dssums.release(); dcnt.release();
+        bsums.release(); ssums.release();
+        for (int k = 0; k < 2; k++) {
+            dbsums[k].release(); dssums[k].release(); dcnt[k].release();
+        }
         staging.release();
         lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); bpay.release();
         dops.release(); cfps.release(); cops.release(); counts.release(); counts2.release(); flag.release();
+        results.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
         snap.release();

@@ -224,7 +224,7 @@ struct Unit {  // the widest access that divides a B-byte row
 // the widest units (consecutive lanes: consecutive source units)
 template <int B>
 __device__ __forceinline__ void move_rows(const uint8_t *src, uint8_t *dst, uint64_t i0, uint32_t rows,
-                                          const int32_t *shift) {
+                                          const int32_t *shift, uint64_t cap) {
     using U = typename Unit<B>::T;
     constexpr int NU = B / Unit<B>::SIZE;
     const U *s = reinterpret_cast<const U *>(src) + i0 * NU;
@@ -232,14 +232,18 @@ __device__ __forceinline__ void move_rows(const uint8_t *src, uint8_t *dst, uint
     for (uint32_t w = threadIdx.x; w < rows * NU; w += blockDim.x) {
         const uint32_t r = w / NU;
         const int32_t sh = shift[r];
-        if (sh != INT32_MIN) d[(uint64_t)((int64_t)(i0 + r) + sh) * NU + (w - r * NU)] = s[w];
+        const uint64_t pos = (uint64_t)((int64_t)(i0 + r) + sh);
+        // pos < cap always holds for a key-sorted batch; the guard keeps a speculative merge of
+        // a batch whose order was not final (re-run by the caller) inside the output run
+        if (sh != INT32_MIN && pos < cap) d[pos * NU + (w - r * NU)] = s[w];
     }
 }
 
 template <int KL, int P>
 __global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const uint8_t *pay, uint64_t n,
                                                     const uint32_t *ins_rank, const uint32_t *del_rank,
-                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay) {
+                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay,
+                                                    uint64_t cap) {
     static_assert(KL % 4 == 0 && P % 4 == 0, "dword rows");
     __shared__ uint64_t bounds[4];
     __shared__ int32_t shift[MOVE_TILE];  // pos - i, or INT32_MIN for a deleted row
@@ -262,8 +266,8 @@ __global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const u
         shift[r] = gone ? INT32_MIN : (int32_t)((int64_t)ins_le - (int64_t)del_lt);
     }
     __syncthreads();
-    move_rows<KL>(keys, okeys, i0, rows, shift);
-    move_rows<P>(pay, opay, i0, rows, shift);
+    move_rows<KL>(keys, okeys, i0, rows, shift, cap);
+    move_rows<P>(pay, opay, i0, rows, shift, cap);
 }
 
 // inserts and overwrites land at r + (#inserts before j) - (#deletes before j): for an insert
@@ -272,10 +276,11 @@ __global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const u
 template <int KL, int P>
 __global__ void k_scatter(const uint8_t *skeys, const uint8_t *spay, const uint8_t *present, const uint8_t *sops,
                           const uint32_t *rank, const uint32_t *cum_ins, const uint32_t *cum_del, uint64_t m,
-                          uint8_t *okeys, uint8_t *opay) {
+                          uint8_t *okeys, uint8_t *opay, uint64_t cap) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m || sops[j] != 0) return;
     const uint64_t pos = (uint64_t)rank[j] + cum_ins[j] - cum_del[j];
+    if (pos >= cap) return;  // only for a batch whose order was not final (see move_rows)
     if (!present[j]) copy_bytes<KL>(okeys + pos * KL, skeys + j * KL);
     copy_bytes<P>(opay + (uint64_t)P * pos, spay + (uint64_t)P * j);
 }
@@ -408,10 +413,13 @@ __global__ __launch_bounds__(1024) void k_sum_parts3(const uint32_t *part, uint6
 
 // one pass over the delta run: the 256-row block sums of the contributions and each entry's
 // count delta (live - in_base), which the caller then prefix-sums
-__global__ __launch_bounds__(256) void k_delta_sums(const uint8_t *dpay, uint64_t n, uint8_t *bsums, int32_t *cnt) {
+__global__ __launch_bounds__(256) void k_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_old,
+                                                    const uint64_t *merge_counts, uint8_t *bsums, int32_t *cnt) {
     __shared__ SumTile tile;
+    const uint64_t n = nd_old + merge_counts[0] - merge_counts[2];
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n_max) cnt[i] = 0;
     if (i < n) {
         const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
         fp_load(reinterpret_cast<const uint8_t *>(r.contrib), h);
@@ -541,10 +549,10 @@ struct KeyOps final : StoreKeyOps {
         if (n) {
             const uint64_t tiles = (n + MOVE_TILE - 1) / MOVE_TILE;
             hipLaunchKernelGGL((k_move_tiles<KL, P>), dim3((uint32_t)tiles), dim3(256), 0, st, keys, pay, n, ins_rank,
-                               del_rank, counts, okeys, opay);
+                               del_rank, counts, okeys, opay, n + m);
         }
         hipLaunchKernelGGL((k_scatter<KL, P>), g1(m), dim3(256), 0, st, skeys, spay, present, sops, rank, cins, cdel,
-                           m, okeys, opay);
+                           m, okeys, opay, n + m);
         hipLaunchKernelGGL(k_count_ovr, g1(m), dim3(256), 0, st, sops, present, m,
                            reinterpret_cast<unsigned long long *>(counts + 1));
         return hipGetLastError();
@@ -636,10 +644,11 @@ hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
     return hipGetLastError();
 }
 
-hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n, uint8_t *bsums, int32_t *cnt, Scratch &s,
-                             hipStream_t st) {
+hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_old, const uint64_t *merge_counts,
+                             uint8_t *bsums, int32_t *cnt, Scratch &s, hipStream_t st) {
+    const uint64_t n = n_max;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_delta_sums, g1(n), dim3(256), 0, st, dpay, n, bsums, cnt);
+    hipLaunchKernelGGL(k_delta_sums, g1(n), dim3(256), 0, st, dpay, n_max, nd_old, merge_counts, bsums, cnt);
     size_t tb = 0;
     hipError_t e;
     if ((e = rocprim::inclusive_scan(nullptr, tb, cnt, cnt, n, rocprim::plus<int32_t>(), st))) return e;

@@ -104,9 +104,11 @@ hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
                               const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
                               const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
                               uint64_t *counts, Scratch &s, hipStream_t st);
-// block sums of the contributions (bsums) + inclusive prefix of the count deltas (cnt)
-hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n, uint8_t *bsums, int32_t *cnt, Scratch &s,
-                             hipStream_t st);
+// block sums of the contributions (bsums) + inclusive prefix of the count deltas (cnt) over
+// n_max rows, of which the first nd_old + merge_counts[0] - merge_counts[2] (read on the
+// device) are real and the rest count as zero
+hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_old, const uint64_t *merge_counts,
+                             uint8_t *bsums, int32_t *cnt, Scratch &s, hipStream_t st);
 hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops, hipStream_t st);
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
                             const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out, hipStream_t st);

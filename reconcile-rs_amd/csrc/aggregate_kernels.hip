@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void k_lift_encoded(const uint8_t *bytes, cons
 // ---- reductions ------------------------------------------------------------------------------
 
 // fingerprint i of an array whose entries are `stride` bytes apart (32 for plain fingerprint
-// arrays; the store's delta records carry their 32-byte contribution first, stride 80)
+// arrays; the store's delta records carry their 32-byte contribution first, stride 48)
 __device__ __forceinline__ void load_fp(const uint8_t *src, uint64_t i, uint32_t f[8], uint32_t stride = 32) {
     const uint4 *p = reinterpret_cast<const uint4 *>(src + (uint64_t)stride * i);
     uint4 a = p[0], b = p[1];
@@ -117,6 +117,22 @@ __device__ __forceinline__ void acc_span(Acc &a, const uint8_t *src, uint64_t lo
         uint32_t f[8];
         load_fp(src, i, f, stride);
         acc_add_fp(a, f);
+    }
+}
+
+// Σ of n 256-bit entries (one workgroup): the root fingerprint of a run from its super-block
+// sums, kept on the host so that the whole-map aggregate is O(1) (the root node's cached
+// Aggregate, rsos/src/fingerprint_tree_map/query.rs:25-76 with an unbounded range)
+__global__ __launch_bounds__(256) void k_total(const uint8_t *in, uint64_t n, uint64_t *out) {
+    __shared__ uint64_t lds[4 * 8];
+    Acc a;
+    acc_zero(a);
+    acc_span(a, in, 0, n);
+    uint32_t f[8];
+    acc_block_reduce<256>(a, lds, f);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) out[q] = (uint64_t)f[2 * q] | ((uint64_t)f[2 * q + 1] << 32);
     }
 }
 
@@ -203,6 +219,11 @@ hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStre
     if (n_in == 0) return hipSuccess;
     const uint64_t g = (n_in + 255) / 256;
     hipLaunchKernelGGL(k_reduce, dim3((uint32_t)g), dim3(256), 0, st, in, stride, n_in, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_total, dim3(1), dim3(256), 0, st, in, n, out);
     return hipGetLastError();
 }
 

@@ -19,6 +19,8 @@ hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint6
                                uint8_t *fps, uint8_t *bsums, hipStream_t st);
 // stride: bytes between consecutive level-0 entries (32 = a fingerprint array)
 hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st, uint32_t stride = 32);
+// out[0..3] = Σ of n 256-bit entries (n small: one workgroup)
+hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_t st);
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
                               hipStream_t st, uint32_t stride = 32);

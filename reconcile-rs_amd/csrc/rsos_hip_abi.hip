@@ -397,6 +397,10 @@ struct rh_store {
     DevBuf<uint8_t> dkeys[2], dpay[2], dbsums[2], dssums[2];
     DevBuf<int32_t> dcnt[2];  // inclusive prefix of the count deltas
     uint64_t compact_div = 8, compact_min = 65536, compactions = 0;
+    // the whole-map fingerprint = base total + delta contribution total, kept on the host after
+    // every load / batch / compaction (the reference's root node Aggregate): aggregate(..) is O(1)
+    uint64_t root_b[4] = {0, 0, 0, 0}, root_d[4] = {0, 0, 0, 0};
+    DevBuf<uint64_t> tot;
     // batch scratch
     DevColumns staging;
     DevBuf<uint8_t> lfps, skeys, sfps, sops, hops, bpay, dops, cfps, cops;
@@ -418,10 +422,14 @@ struct rh_store {
     int resum_base() {
         int rc;
         const size_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
-        if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32))) return rc;
+        if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4))) return rc;
         if (nb) {
             RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
             RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
+            RH_HIP(rh::launch_total(ssums.p, ns, tot.p, stream));
+            RH_HIP(hipMemcpyAsync(root_b, tot.p, 32, hipMemcpyDeviceToHost, stream));  // the caller syncs
+        } else {
+            memset(root_b, 0, sizeof root_b);
         }
         return RH_OK;
     }
@@ -475,6 +483,7 @@ struct rh_store {
         nd = 0;
         dtotal = 0;
         nb = 0;
+        memset(root_d, 0, sizeof root_d);
         if (m) {
             RH_HIP(hipMemcpyAsync(bkeys[cb].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
             if ((rc = lift_dispatch(schema, c, m, bfps[cb].p, nullptr, nullptr, nullptr, false, stream))) return rc;
@@ -510,11 +519,15 @@ struct rh_store {
         int rc;
         if (nd == 0) return RH_OK;
         if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64)) || (rc = counts2.ensure(4))) return rc;
-        RH_HIP(rh::launch_delta_cur(dpay[cd].p, nd, cfps.p, cops.p, stream));
+        uint32_t *crank = scratch.u32(14, nd);
+        uint8_t *cpres = scratch.u8(4, nd);
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        // every delta key's base slot is in its DeltaRec (brank): the merge needs no search
+        RH_HIP(rh::launch_delta_cur(dpay[cd].p, nd, bfps[cb].p, cfps.p, cops.p, crank, cpres, stream));
         const int nxt = 1 - cb;
         if ((rc = bkeys[nxt].ensure((nb + nd) * kl + 64)) || (rc = bfps[nxt].ensure((nb + nd) * 32 + 64))) return rc;
         RH_HIP(kops->merge(bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, cfps.p, cops.p, nd, 32, scratch, bkeys[nxt].p,
-                           bfps[nxt].p, counts2.p, stream));
+                           bfps[nxt].p, counts2.p, stream, crank, cpres));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         uint64_t c[3];
         RH_HIP(hipMemcpyAsync(c, counts2.p, 24, hipMemcpyDeviceToHost, stream));
@@ -524,6 +537,7 @@ struct rh_store {
         nb = nb + c[0] - c[2];
         nd = 0;
         dtotal = 0;
+        memset(root_d, 0, sizeof root_d);
         compactions++;
         if (nb != want) return fail(RH_ERR_STATE, "compaction size mismatch (internal error)");
         if ((rc = resum_base())) return rc;
@@ -557,17 +571,17 @@ struct rh_store {
             (rc = dbsums[nxt].ensure(rh_num_blocks(plan) * 32 + 32)) ||
             (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) || (rc = dcnt[nxt].ensure(plan + 16)))
             return rc;
-        // one 64-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,
-        // [6] sort flags, [7] Σ count deltas of the new delta run
-        if ((rc = results.ensure(8))) return rc;
+        // one 96-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,
+        // [6] sort flags, [7] Σ count deltas of the new delta run, [8..11] Σ of its contributions
+        if ((rc = results.ensure(12))) return rc;
         uint64_t *r_counts = results.p, *r_merge = results.p + 3;
         uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
         int32_t *r_total = reinterpret_cast<int32_t *>(results.p + 7);
-        uint64_t host[8];
+        uint64_t host[12];
         uint32_t flags = 0;
         for (int full = 0; full < 2; full++) {
             // 2. key order (+ duplicate / leading-digit-tie flags)
-            RH_HIP(hipMemsetAsync(results.p, 0, 64, stream));
+            RH_HIP(hipMemsetAsync(results.p, 0, 96, stream));
             RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, scratch, skeys.p, sfps.p,
                                     sops.p, r_flags, full == 1, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -584,7 +598,8 @@ struct rh_store {
             // 5. its sums, then the one round trip
             if ((rc = resum_delta_async(nxt, n_max, nd, r_merge))) return rc;
             RH_HIP(hipMemcpyAsync(r_total, dcnt[nxt].p + n_max - 1, 4, hipMemcpyDeviceToDevice, stream));
-            RH_HIP(hipMemcpyAsync(host, results.p, 64, hipMemcpyDeviceToHost, stream));
+            RH_HIP(rh::launch_total(dssums[nxt].p, rh_num_superblocks(n_max), results.p + 8, stream));
+            RH_HIP(hipMemcpyAsync(host, results.p, 96, hipMemcpyDeviceToHost, stream));
             if ((rc = sync())) return rc;
             memcpy(&flags, &host[6], 4);
             if (!(flags & 2)) break;
@@ -602,6 +617,7 @@ struct rh_store {
         cd = nxt;
         nd = nd + c2[0] - c2[2];
         dtotal = total;
+        memcpy(root_d, &host[8], sizeof root_d);
         if (nd > std::max<uint64_t>(nb / compact_div, compact_min)) return compact();
         return RH_OK;
     }
@@ -619,6 +635,11 @@ struct rh_store {
     }
     int aggregate_keys(int lo_kind, const void *lo_key, int hi_kind, const void *hi_key, rh_aggregate *out) {
         int rc;
+        if (!lo_kind && !hi_kind) {  // `..`: the cached root
+            rh_fp_add(root_b, root_d, out->fingerprint);
+            out->size = size();
+            return RH_OK;
+        }
         if ((rc = q_keys.ensure(2 * kl + 64)) || (rc = q_lo.ensure(1)) || (rc = q_hi.ensure(1)) ||
             (rc = q_dlo.ensure(1)) || (rc = q_dhi.ensure(1)) || (rc = q_out.ensure(1)) || (rc = q_bout.ensure(1)) ||
             (rc = q_dout.ensure(1)))
@@ -656,7 +677,7 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
         }
-        bsums.release(); ssums.release();
+        bsums.release(); ssums.release(); tot.release();
         for (int k = 0; k < 2; k++) {
             dbsums[k].release(); dssums[k].release(); dcnt[k].release();
         }

@@ -3,11 +3,12 @@
 //
 // Store layout in HBM (rank order):
 //   base  : keys[nB][KL] + fps[nB][32] + block sums [nB/256][32] + super sums [nB/65536][32]
-//   delta : keys[nD][KL] + DeltaRec[nD] (80 B) + block / super sums of the contributions +
+//   delta : keys[nD][KL] + DeltaRec[nD] (48 B) + block / super sums of the contributions +
 //           an inclusive prefix of the count deltas
 // A DeltaRec for key k says what the batches since the last compaction did to k:
 //   contrib = cur_fp - base_fp   (cur_fp = 0 if k is now deleted; base_fp = 0 if k not in base)
 //   in_base, live                 (so the count delta is live - in_base, in {-1, 0, +1})
+//   brank                         (k's lower-bound rank in the base run)
 // so every aggregate over a key range is   base part + Σ contrib over the delta part,
 // exactly as FingerprintTreeMap composes signed deltas into its cached aggregates
 // (rsos/src/fingerprint_tree_map/mutate.rs:31-41 overwrite delta, :93-154 remove).
@@ -351,7 +352,8 @@ __global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
         if (in_b) fp_load(base_fps + 32ull * rank_b[j], base);
         DeltaRec r;
         r.flags = (in_b ? DeltaRec::IN_BASE : 0u);
-        r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        r.brank = rank_b[j];
+        r.pad[0] = r.pad[1] = 0;
         uint32_t cur[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (!isdel) {
             fp_load(sfps + 32 * j, cur);
@@ -362,8 +364,6 @@ __global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
             c_del = was_live;
         }
         fp_sub(cur, base, r.contrib);
-#pragma unroll
-        for (int i = 0; i < 8; i++) r.base[i] = base[i];
         // deleting a key the base does not hold needs no entry (drop any delta entry it has)
         dops[j] = (isdel && !in_b) ? 1 : 0;
         reinterpret_cast<DeltaRec *>(bpay)[j] = r;
@@ -431,15 +431,21 @@ __global__ __launch_bounds__(256) void k_delta_sums(const uint8_t *dpay, uint64_
     if (threadIdx.x == 0) store_sum(bsums, blockIdx.x, f8);
 }
 
-// compaction input: cur fp = contrib + base, op = live ? upsert : delete
-__global__ void k_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops) {
+// compaction input: cur fp = contrib + base fp, op = live ? upsert : delete, and the key's
+// place in the base (no search: brank was recorded when the entry was built)
+__global__ void k_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
+                            uint32_t *rank, uint8_t *present) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
-    uint32_t cur[8];
-    fp_add(r.contrib, r.base, cur);
+    const bool in_b = (r.flags & DeltaRec::IN_BASE) != 0;
+    uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cur[8];
+    if (in_b) fp_load(base_fps + 32ull * r.brank, base);
+    fp_add(r.contrib, base, cur);
     fp_store(fps + 32 * i, cur);
     ops[i] = (r.flags & DeltaRec::LIVE) ? 0 : 1;
+    rank[i] = r.brank;
+    present[i] = in_b ? 1 : 0;
 }
 
 // aggregate over a key range of the merged view = base part + delta part; the delta part's
@@ -657,9 +663,10 @@ hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_ol
     return rocprim::inclusive_scan(tmp, tb, cnt, cnt, n, rocprim::plus<int32_t>(), st);
 }
 
-hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops, hipStream_t st) {
+hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
+                            uint32_t *rank, uint8_t *present, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_delta_cur, g1(n), dim3(256), 0, st, dpay, n, fps, ops);
+    hipLaunchKernelGGL(k_delta_cur, g1(n), dim3(256), 0, st, dpay, n, base_fps, fps, ops, rank, present);
     return hipGetLastError();
 }
 

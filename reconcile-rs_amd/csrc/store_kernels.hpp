@@ -56,16 +56,19 @@ struct Scratch {
     }
 };
 
-// One entry of the store's delta run (80 B): what the batches since the last compaction did to
-// a key.  contrib = cur - base (mod 2^256); count delta = live - in_base.
+// One entry of the store's delta run (48 B): what the batches since the last compaction did to
+// a key.  contrib = cur - base (mod 2^256); count delta = live - in_base.  brank is the key's
+// lower-bound rank in the base run: the base does not change until the next compaction, so it
+// locates the base fingerprint (cur = base_fps[brank] + contrib) and the key's slot in the
+// compaction merge without searching again.
 struct DeltaRec {
     enum : uint32_t { IN_BASE = 1, LIVE = 2 };
     uint32_t contrib[8];
-    uint32_t base[8];
+    uint32_t brank;
     uint32_t flags;
-    uint32_t pad[3];
+    uint32_t pad[2];
 };
-static_assert(sizeof(DeltaRec) == 80, "DeltaRec layout");
+static_assert(sizeof(DeltaRec) == 48, "DeltaRec layout (16-byte multiple: rows are loaded as uint4)");
 
 // Key-type-specialised device operations of the store.
 struct StoreKeyOps {
@@ -81,7 +84,7 @@ struct StoreKeyOps {
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;
     // merge a key-sorted batch (ops: 0 upsert, 1 delete) into a sorted run of (key, payload)
-    // rows -> (okeys, opay); payload 32 (fingerprints) or 80 (DeltaRec);
+    // rows -> (okeys, opay); payload 32 (fingerprints) or 48 (DeltaRec);
     // counts = {inserted, overwritten, deleted}.  rank / present: the batch keys' search result
     // in the run if the caller already has it (else searched here)
     virtual hipError_t merge(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys,
@@ -109,7 +112,10 @@ hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
 // device) are real and the rest count as zero
 hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_old, const uint64_t *merge_counts,
                              uint8_t *bsums, int32_t *cnt, Scratch &s, hipStream_t st);
-hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, uint8_t *fps, uint8_t *ops, hipStream_t st);
+// compaction input from the delta run: cur fingerprints, ops (live ? upsert : delete) and each
+// key's place in the base (rank = brank, present = in_base) for the merge
+hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
+                            uint32_t *rank, uint8_t *present, hipStream_t st);
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
                             const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out, hipStream_t st);
 hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, const int32_t *cnt_prefix, uint64_t m,

@@ -390,12 +390,15 @@ struct rh_store {
     uint64_t nb = 0;
     int cb = 0;
     DevBuf<uint8_t> bkeys[2], bfps[2], bsums, ssums;
+    DevBuf<uint64_t> bsmp, dsmp;  // leading digits of every 256th key (sampled search)
     // delta run
     uint64_t nd = 0;
     int cd = 0;
     int64_t dtotal = 0;  // Σ count deltas
     DevBuf<uint8_t> dkeys[2], dpay[2], dbsums[2], dssums[2];
-    DevBuf<int32_t> dcnt[2];  // inclusive prefix of the count deltas
+    DevBuf<int32_t> dblk[2];  // inclusive block prefix of the count deltas
+    DevBuf<int16_t> dinb[2];  // each row's inclusive count prefix inside its 256-row block
+    DevBuf<uint64_t> mcnt;    // merge counters
     uint64_t compact_div = 8, compact_min = 65536, compactions = 0;
     // the whole-map fingerprint = base total + delta contribution total, kept on the host after
     // every load / batch / compaction (the reference's root node Aggregate): aggregate(..) is O(1)
@@ -419,12 +422,15 @@ struct rh_store {
         RH_HIP(hipStreamSynchronize(stream));
         return RH_OK;
     }
-    int resum_base() {
+    int resum_base(bool have_block_sums = false) {
         int rc;
         const size_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
-        if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4))) return rc;
+        if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4)) ||
+            (rc = bsmp.ensure(nbk + 1)))
+            return rc;
         if (nb) {
-            RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
+            RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, stream));
+            if (!have_block_sums) RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
             RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
             RH_HIP(rh::launch_total(ssums.p, ns, tot.p, stream));
             RH_HIP(hipMemcpyAsync(root_b, tot.p, 32, hipMemcpyDeviceToHost, stream));  // the caller syncs
@@ -433,20 +439,17 @@ struct rh_store {
         }
         return RH_OK;
     }
-    // Contribution sums + count-delta prefix of delta buffer `buf`, sized for n_max rows; the
-    // true row count n = nd_old + counts[0] - counts[2] is read on the device (rows past it
-    // count as zero), so no host round trip is needed between the merge and the sums.
-    int resum_delta_async(int buf, uint64_t n_max, uint64_t nd_old, const uint64_t *merge_counts) {
-        int rc;
+    // After a merge into delta buffer `buf` (sized for n_max rows; the merge wrote its block
+    // sums and block count totals, zero past the true row count, which only the device knows):
+    // the inclusive block prefix of the count deltas (its last entry -> *total), the super-block
+    // sums, and the contribution total -> fp_total.  No host round trip.
+    rh::CntPrefix cnt_prefix(int buf) const { return rh::CntPrefix{dblk[buf].p, dinb[buf].p}; }
+    int finish_delta_async(int buf, uint64_t n_max, int32_t *total, uint64_t *fp_total) {
         const size_t nbk = rh_num_blocks(n_max), ns = rh_num_superblocks(n_max);
-        if ((rc = dbsums[buf].ensure(nbk * 32 + 32)) || (rc = dssums[buf].ensure(ns * 32 + 32)) ||
-            (rc = dcnt[buf].ensure(n_max + 16)))
-            return rc;
-        if (!n_max) return RH_OK;
-        RH_HIP(rh::launch_delta_sums(dpay[buf].p, n_max, nd_old, merge_counts, dbsums[buf].p, dcnt[buf].p, scratch,
-                                     stream));
+        RH_HIP(rh::launch_count_prefix(dblk[buf].p, nbk, total, scratch, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        RH_HIP(rh::launch_reduce(dbsums[buf].p, nbk, dssums[buf].p, stream));
+        if (nbk) RH_HIP(rh::launch_reduce(dbsums[buf].p, nbk, dssums[buf].p, stream));
+        RH_HIP(rh::launch_total(dssums[buf].p, ns, fp_total, stream));
         return RH_OK;
     }
     // Replace the contents with m records.  Sorted, duplicate-free input is required unless
@@ -464,7 +467,7 @@ struct rh_store {
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             RH_HIP(hipMemcpyAsync(flags, flag.p, 4, hipMemcpyDeviceToHost, stream));
             if ((rc = sync())) return rc;
-            if (!(*flags & 2)) return RH_OK;
+            if (!(*flags & 6)) return RH_OK;  // 2: leading-digit tie, 4: skewed buckets
         }
         return RH_OK;
     }
@@ -525,12 +528,17 @@ struct rh_store {
         // every delta key's base slot is in its DeltaRec (brank): the merge needs no search
         RH_HIP(rh::launch_delta_cur(dpay[cd].p, nd, bfps[cb].p, cfps.p, cops.p, crank, cpres, stream));
         const int nxt = 1 - cb;
-        if ((rc = bkeys[nxt].ensure((nb + nd) * kl + 64)) || (rc = bfps[nxt].ensure((nb + nd) * 32 + 64))) return rc;
-        RH_HIP(kops->merge(bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, cfps.p, cops.p, nd, 32, scratch, bkeys[nxt].p,
-                           bfps[nxt].p, counts2.p, stream, crank, cpres));
+        const uint64_t nbk = rh_num_blocks(nb + nd);
+        if ((rc = bkeys[nxt].ensure((nb + nd) * kl + 64)) || (rc = bfps[nxt].ensure((nb + nd) * 32 + 64)) ||
+            (rc = bsums.ensure(nbk * 32 + 32)) || (rc = mcnt.ensure(8)))
+            return rc;
+        // the merged base and its block sums in one pass
+        RH_HIP(rh::launch_merge_run((int)kl, 32, bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, cfps.p, cops.p, crank,
+                                    cpres, nd, scratch, bkeys[nxt].p, bfps[nxt].p, bsums.p, nullptr, nullptr, nbk,
+                                    mcnt.p, nullptr, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         uint64_t c[3];
-        RH_HIP(hipMemcpyAsync(c, counts2.p, 24, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(c, mcnt.p, 24, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
         const uint64_t want = size();
         cb = nxt;
@@ -540,7 +548,7 @@ struct rh_store {
         memset(root_d, 0, sizeof root_d);
         compactions++;
         if (nb != want) return fail(RH_ERR_STATE, "compaction size mismatch (internal error)");
-        if ((rc = resum_base())) return rc;
+        if ((rc = resum_base(true))) return rc;
         return sync();
     }
     int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3]) {
@@ -554,6 +562,8 @@ struct rh_store {
             return rc;
         // 1. lift the batch (delete rows are lifted too and ignored)
         if ((rc = lift_dispatch(schema, c, m, lfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
+        if ((rc = dsmp.ensure(rh_num_blocks(nd) + 1))) return rc;
+        RH_HIP(kops->sample(dkeys[cd].p, nd, dsmp.p, stream));
         // 2-5 run without a host round trip: everything is written to the delta run's *other*
         // buffers, and one sync at the end brings back the flags and counts.  A duplicate key
         // then leaves the store exactly as it was (nothing is committed); a tie on the leading
@@ -569,7 +579,9 @@ struct rh_store {
         const uint64_t plan = std::max<uint64_t>(n_max, std::min<uint64_t>(thresh, nb + nd) + m);
         if ((rc = dkeys[nxt].ensure(plan * kl + 64)) || (rc = dpay[nxt].ensure(plan * sizeof(rh::DeltaRec) + 64)) ||
             (rc = dbsums[nxt].ensure(rh_num_blocks(plan) * 32 + 32)) ||
-            (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) || (rc = dcnt[nxt].ensure(plan + 16)))
+            (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
+            (rc = dblk[nxt].ensure(rh_num_blocks(plan) + 16)) || (rc = dinb[nxt].ensure(plan + 16)) ||
+            (rc = mcnt.ensure(8)))
             return rc;
         // one 96-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,
         // [6] sort flags, [7] Σ count deltas of the new delta run, [8..11] Σ of its contributions
@@ -586,23 +598,24 @@ struct rh_store {
                                     sops.p, r_flags, full == 1, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 3. where each key is now: base and delta runs
-            RH_HIP(kops->search(bkeys[cb].p, nb, skeys.p, m, rank_b, present_b, stream));
-            RH_HIP(kops->search(dkeys[cd].p, nd, skeys.p, m, rank_d, present_d, stream));
+            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, skeys.p, m, rank_b, present_b, stream));
+            RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp.p, skeys.p, m, rank_d, present_d, stream));
             // 4. the batch's delta records, merged into the delta run's other buffer
             RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d,
                                           dpay[cd].p, bpay.p, dops.p, r_counts, scratch, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-            RH_HIP(kops->merge(dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p, dops.p, m, sizeof(rh::DeltaRec), scratch,
-                               dkeys[nxt].p, dpay[nxt].p, r_merge, stream, rank_d, present_d));
+            // (one pass: the merged run, its block sums and count prefixes)
+            RH_HIP(rh::launch_merge_run((int)kl, sizeof(rh::DeltaRec), dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p,
+                                        dops.p, rank_d, present_d, m, scratch, dkeys[nxt].p, dpay[nxt].p,
+                                        dbsums[nxt].p, dblk[nxt].p, dinb[nxt].p, rh_num_blocks(n_max), mcnt.p, r_merge,
+                                        stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-            // 5. its sums, then the one round trip
-            if ((rc = resum_delta_async(nxt, n_max, nd, r_merge))) return rc;
-            RH_HIP(hipMemcpyAsync(r_total, dcnt[nxt].p + n_max - 1, 4, hipMemcpyDeviceToDevice, stream));
-            RH_HIP(rh::launch_total(dssums[nxt].p, rh_num_superblocks(n_max), results.p + 8, stream));
+            // 5. count prefix, super sums and totals, then the one round trip
+            if ((rc = finish_delta_async(nxt, n_max, r_total, results.p + 8))) return rc;
             RH_HIP(hipMemcpyAsync(host, results.p, 96, hipMemcpyDeviceToHost, stream));
             if ((rc = sync())) return rc;
             memcpy(&flags, &host[6], 4);
-            if (!(flags & 2)) break;
+            if (!(flags & 6)) break;  // 2: leading-digit tie, 4: skewed buckets
         }
         int32_t total;
         memcpy(&total, &host[7], 4);
@@ -655,7 +668,7 @@ struct rh_store {
             RH_HIP(rh::launch_range_query(dpay[cd].p, dbsums[cd].p, dssums[cd].p, nd, q_dlo.p, q_dhi.p, 1,
                                           reinterpret_cast<uint64_t *>(q_dout.p), stream, sizeof(rh::DeltaRec)));
             RH_HIP(rh::launch_agg_merge(reinterpret_cast<uint64_t *>(q_bout.p), reinterpret_cast<uint64_t *>(q_dout.p),
-                                        q_dlo.p, q_dhi.p, dcnt[cd].p, reinterpret_cast<uint64_t *>(q_out.p), stream));
+                                        q_dlo.p, q_dhi.p, cnt_prefix(cd), reinterpret_cast<uint64_t *>(q_out.p), stream));
         }
         RH_HIP(hipMemcpyAsync(out, q_out.p, sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
         return sync();
@@ -666,9 +679,9 @@ struct rh_store {
             (rc = q_merged.ensure(m)))
             return rc;
         RH_HIP(hipMemcpyAsync(q_keys.p, keys, m * kl, hipMemcpyHostToDevice, stream));
-        RH_HIP(kops->search(bkeys[cb].p, nb, q_keys.p, m, q_rank.p, nullptr, stream));
+        RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, q_keys.p, m, q_rank.p, nullptr, stream));
         if (nd) RH_HIP(kops->search(dkeys[cd].p, nd, q_keys.p, m, q_drank.p, nullptr, stream));
-        RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, dcnt[cd].p, m, q_merged.p, stream));
+        RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, cnt_prefix(cd), m, q_merged.p, stream));
         RH_HIP(hipMemcpyAsync(out, q_merged.p, m * 8, hipMemcpyDeviceToHost, stream));
         return sync();
     }
@@ -677,9 +690,9 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
         }
-        bsums.release(); ssums.release(); tot.release();
+        bsums.release(); ssums.release(); tot.release(); bsmp.release(); dsmp.release(); mcnt.release();
         for (int k = 0; k < 2; k++) {
-            dbsums[k].release(); dssums[k].release(); dcnt[k].release();
+            dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release();
         }
         staging.release();
         lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); bpay.release();

@@ -28,6 +28,10 @@
 
 namespace rh {
 
+namespace {
+inline dim3 g1(uint64_t m) { return dim3((uint32_t)((m + 255) / 256)); }
+}
+
 // ---- key order ----------------------------------------------------------------------------
 
 template <int KK, int KL>
@@ -154,6 +158,218 @@ __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t 
     }
 }
 
+// ---- batch sort: one MSD bucket pass + per-bucket sort in LDS ----------------------------------
+// For the update batches (m <= SB_MAX_M): the most significant u64 digit d of each key is
+// bucketed by (d - min) >> shift into SB_N buckets (shift chosen so the batch's digit range
+// spans them: random and dense key ranges both spread), and each bucket is then ordered by
+// (d, input index) in LDS -- so the result is the stable sort by d.  Six short kernels and no
+// host round trip, where the library radix sort spends ~20 merge passes on a 1 M batch.
+// *flags |= 4 if a bucket is larger than SB_CAP (skewed digits): the caller re-sorts with the
+// full LSD radix, like a leading-digit tie (|= 2).
+constexpr int SB_BITS = 14, SB_N = 1 << SB_BITS;  // buckets (~61 keys each for a 1 M batch)
+constexpr int SB_TILE = 4096;                     // keys per histogram workgroup (16 per lane)
+constexpr int SB_CAP = 256;                       // largest bucket ordered in LDS (one wave)
+constexpr uint64_t SB_MAX_M = 2ull << 20;
+
+template <int KK, int KL>
+__global__ __launch_bounds__(256) void k_sb_minmax(const uint8_t *keys, uint64_t m, uint64_t *part) {
+    __shared__ uint64_t lo[4], hi[4];
+    uint64_t a = ~0ull, b = 0;
+    const uint64_t i0 = (uint64_t)blockIdx.x * SB_TILE;
+    for (uint32_t t = threadIdx.x; t < SB_TILE; t += 256) {
+        const uint64_t i = i0 + t;
+        if (i < m) {
+            const uint64_t d = key_digit<KK, KL>(keys + i * KL, 0);
+            a = d < a ? d : a;
+            b = d > b ? d : b;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
+        a = a2 < a ? a2 : a;
+        b = b2 > b ? b2 : b;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        lo[threadIdx.x >> 6] = a;
+        hi[threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) {
+            a = lo[w] < a ? lo[w] : a;
+            b = hi[w] > b ? hi[w] : b;
+        }
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = b;
+    }
+}
+
+// (min digit, shift) from the per-workgroup partials; every workgroup of the next kernels
+// folds the (few hundred) partials itself
+__device__ __forceinline__ void sb_params(const uint64_t *part, uint32_t nwg, uint64_t *mn, uint32_t *shift) {
+    __shared__ uint64_t lo[4], hi[4];
+    uint64_t a = ~0ull, b = 0;
+    for (uint32_t w = threadIdx.x; w < nwg; w += blockDim.x) {
+        a = part[2 * w] < a ? part[2 * w] : a;
+        b = part[2 * w + 1] > b ? part[2 * w + 1] : b;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
+        a = a2 < a ? a2 : a;
+        b = b2 > b ? b2 : b;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        lo[threadIdx.x >> 6] = a;
+        hi[threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    for (uint32_t w = 1; w < blockDim.x / 64; w++) {
+        a = lo[w] < a ? lo[w] : a;
+        b = hi[w] > b ? hi[w] : b;
+    }
+    a = lo[0] < a ? lo[0] : a;
+    b = hi[0] > b ? hi[0] : b;
+    const uint64_t range = b - a;
+    const int bits = range ? 64 - __clzll(range) : 0;
+    *mn = a;
+    *shift = bits > SB_BITS ? (uint32_t)(bits - SB_BITS) : 0u;
+}
+
+template <int KK, int KL>
+__global__ __launch_bounds__(256) void k_sb_hist(const uint8_t *keys, uint64_t m, const uint64_t *part, uint32_t nwg,
+                                                 uint32_t *hist) {
+    __shared__ uint32_t h[SB_N];
+    uint64_t mn;
+    uint32_t shift;
+    sb_params(part, nwg, &mn, &shift);
+    for (uint32_t b = threadIdx.x; b < SB_N; b += 256) h[b] = 0;
+    __syncthreads();
+    const uint64_t i0 = (uint64_t)blockIdx.x * SB_TILE;
+    for (uint32_t t = threadIdx.x; t < SB_TILE; t += 256) {
+        const uint64_t i = i0 + t;
+        if (i < m) atomicAdd(&h[(uint32_t)((key_digit<KK, KL>(keys + i * KL, 0) - mn) >> shift)], 1u);
+    }
+    __syncthreads();
+    uint32_t *o = hist + (uint64_t)blockIdx.x * SB_N;
+    for (uint32_t b = threadIdx.x; b < SB_N; b += 256) o[b] = h[b];
+}
+
+// per bucket: each workgroup's running offset within the bucket (in place), and the total
+__global__ __launch_bounds__(64) void k_sb_colscan(uint32_t *hist, uint32_t nwg, uint32_t *total) {
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= SB_N) return;
+    uint32_t run = 0;
+    for (uint32_t w0 = 0; w0 < nwg; w0 += 8) {  // 8 loads in flight per lane
+        uint32_t t[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) t[k] = w0 + k < nwg ? hist[(uint64_t)(w0 + k) * SB_N + b] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (w0 + k < nwg) hist[(uint64_t)(w0 + k) * SB_N + b] = run;
+            run += t[k];
+        }
+    }
+    total[b] = run;
+}
+
+// exclusive scan of the bucket totals (one workgroup of 1024, SB_N / 1024 buckets per lane)
+__global__ __launch_bounds__(1024) void k_sb_bucketscan(const uint32_t *total, uint32_t *start, uint32_t *flags) {
+    constexpr int PER = SB_N / 1024;
+    __shared__ uint32_t w[16];
+    const uint32_t t = threadIdx.x;
+    uint32_t v[PER], s = 0;
+    bool big = false;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        v[k] = total[PER * t + k];
+        big |= v[k] > (uint32_t)SB_CAP;
+        s += v[k];
+    }
+    uint32_t x = s;  // inclusive wave scan of the lane sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((t & 63) >= (uint32_t)o) x += y;
+    }
+    if ((t & 63) == 63) w[t >> 6] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t q = 0; q < (t >> 6); q++) before += w[q];
+    uint32_t run = before + x - s;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        start[PER * t + k] = run;
+        run += v[k];
+    }
+    if (__ballot(big) && (t & 63) == 0) atomicOr(flags, 4u);
+}
+
+template <int KK, int KL>
+__global__ __launch_bounds__(256) void k_sb_scatter(const uint8_t *keys, uint64_t m, const uint64_t *part,
+                                                    uint32_t nwg, const uint32_t *hist, const uint32_t *start,
+                                                    uint64_t *odig, uint32_t *oidx) {
+    __shared__ uint32_t cur[SB_N];
+    uint64_t mn;
+    uint32_t shift;
+    sb_params(part, nwg, &mn, &shift);
+    const uint32_t *h = hist + (uint64_t)blockIdx.x * SB_N;
+    for (uint32_t b = threadIdx.x; b < SB_N; b += 256) cur[b] = start[b] + h[b];
+    __syncthreads();
+    const uint64_t i0 = (uint64_t)blockIdx.x * SB_TILE;
+    for (uint32_t t = threadIdx.x; t < SB_TILE; t += 256) {
+        const uint64_t i = i0 + t;
+        if (i < m) {
+            const uint64_t d = key_digit<KK, KL>(keys + i * KL, 0);
+            const uint32_t pos = atomicAdd(&cur[(uint32_t)((d - mn) >> shift)], 1u);
+            odig[pos] = d;
+            oidx[pos] = (uint32_t)i;
+        }
+    }
+}
+
+// one wave per bucket: order its (digit, index) pairs by rank counting in LDS, then gather
+// keys / fingerprints / ops into place and flag duplicates (1) and digit ties (2)
+template <int KK, int KL>
+__global__ __launch_bounds__(64) void k_sb_sort(const uint64_t *dig, const uint32_t *idx, const uint32_t *start,
+                                                 const uint32_t *total, const uint8_t *keys, const uint8_t *fps,
+                                                 const uint8_t *ops, uint8_t *skeys, uint8_t *sfps, uint8_t *sops,
+                                                 uint32_t *flags) {
+    constexpr int D = KK == KEY_BYTES ? KL / 8 : 1;
+    __shared__ uint64_t d[SB_CAP], sd[SB_CAP];
+    __shared__ uint32_t x[SB_CAP], sx[SB_CAP];
+    const uint32_t b = blockIdx.x, n = total[b], s0 = start[b];
+    if (n == 0 || n > (uint32_t)SB_CAP) return;  // too large: flagged by k_sb_bucketscan
+    for (uint32_t t = threadIdx.x; t < n; t += 64) {
+        d[t] = dig[s0 + t];
+        x[t] = idx[s0 + t];
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n; t += 64) {
+        const uint64_t di = d[t];
+        const uint32_t xi = x[t];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < n; j++) r += (d[j] < di || (d[j] == di && x[j] < xi)) ? 1u : 0u;
+        sd[r] = di;
+        sx[r] = xi;
+    }
+    __syncthreads();
+    uint32_t f = 0;
+    for (uint32_t t = threadIdx.x; t < n; t += 64) {
+        const uint64_t j = (uint64_t)s0 + t, src = sx[t];
+        copy_bytes<KL>(skeys + j * KL, keys + src * KL);
+        copy_bytes<32>(sfps + 32 * j, fps + 32 * src);
+        sops[j] = ops ? ops[src] : 0;
+        if (t > 0 && sd[t - 1] == sd[t]) {
+            if (D == 1 || key_cmp<KK, KL>(keys + (uint64_t)sx[t - 1] * KL, keys + src * KL) == 0) f |= 1u;
+            else f |= 2u;
+        }
+    }
+    const unsigned long long any1 = __ballot((f & 1) != 0), any2 = __ballot((f & 2) != 0);
+    if (threadIdx.x == 0 && (any1 | any2)) atomicOr(flags, (any1 ? 1u : 0u) | (any2 ? 2u : 0u));
+}
+
 // ---- search ---------------------------------------------------------------------------------
 
 // lower_bound rank of each query key in a sorted key array; present = key at rank equals
@@ -164,6 +380,52 @@ __global__ void k_search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint
     if (j >= m) return;
     const uint8_t *key = q + j * KL;
     const uint64_t lo = lower_bound_keys<KK, KL>(keys, n, key);
+    rank[j] = (uint32_t)lo;
+    if (present) present[j] = (lo < n && key_cmp<KK, KL>(keys + lo * KL, key) == 0) ? 1 : 0;
+}
+
+// Sampled search: smp[s] = the leading u64 digit of keys[SMP_STRIDE * s].  The digit's place
+// among the samples bounds the key's rank to one stride-wide window (more when samples tie),
+// so a query touches the small, cache-resident sample array and then a few lines of one
+// window, instead of ~log2(n) scattered lines of the whole run.
+constexpr uint64_t SMP_STRIDE = 256;
+
+template <int KK, int KL>
+__global__ void k_sample(const uint8_t *keys, uint64_t n, uint64_t *smp) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s * SMP_STRIDE < n) smp[s] = key_digit<KK, KL>(keys + s * SMP_STRIDE * KL, 0);
+}
+
+__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t lo, uint64_t hi, uint64_t x) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <int KK, int KL>
+__global__ void k_search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint8_t *q, uint64_t m,
+                                 uint32_t *rank, uint8_t *present) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint8_t *key = q + j * KL;
+    const uint64_t d = key_digit<KK, KL>(key, 0), ns = (n + SMP_STRIDE - 1) / SMP_STRIDE;
+    const uint64_t a = lower_bound_u64(smp, 0, ns, d);  // samples < d: those keys are < key
+    uint64_t lo = a ? (a - 1) * SMP_STRIDE : 0, hi = n;
+    if (a < ns) {
+        if (smp[a] > d) hi = a * SMP_STRIDE;  // that sample's key is > key
+        else {                                // samples equal to d: up to the first one above
+            const uint64_t b = lower_bound_u64(smp, a, ns, d + 1);
+            hi = (b < ns && d != ~0ull) ? b * SMP_STRIDE : n;
+        }
+    }
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (key_cmp<KK, KL>(keys + mid * KL, key) < 0) lo = mid + 1;
+        else hi = mid;
+    }
     rank[j] = (uint32_t)lo;
     if (present) present[j] = (lo < n && key_cmp<KK, KL>(keys + lo * KL, key) == 0) ? 1 : 0;
 }
@@ -448,13 +710,20 @@ __global__ void k_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base
     present[i] = in_b ? 1 : 0;
 }
 
+// Σ count deltas of delta rows [0, i]: the inclusive block prefix before i's block plus the
+// inclusive prefix inside it
+__device__ __forceinline__ int64_t cnt_through(const CntPrefix &c, uint64_t i) {
+    const uint64_t b = i / 256;
+    return (int64_t)(b ? c.blk[b - 1] : 0) + c.inb[i];
+}
+
 // aggregate over a key range of the merged view = base part + delta part; the delta part's
 // size is the sum of its count deltas (prefix difference), not its entry count
 __global__ void k_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
-                            const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out) {
+                            const uint64_t *dhi, CntPrefix cp, uint64_t *out) {
     if (threadIdx.x != 0) return;
     const uint64_t lo = *dlo, hi = *dhi;
-    const int64_t c = (int64_t)(hi ? cnt_prefix[hi - 1] : 0) - (int64_t)(lo ? cnt_prefix[lo - 1] : 0);
+    const int64_t c = (hi ? cnt_through(cp, hi - 1) : 0) - (lo ? cnt_through(cp, lo - 1) : 0);
     uint64_t carry = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -468,19 +737,260 @@ __global__ void k_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg,
 }
 
 // rank in the merged view = rank in base + Σ count deltas of the delta keys below
-__global__ void k_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, const int32_t *cnt_prefix, uint64_t m,
+__global__ void k_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, CntPrefix cp, uint64_t m,
                              uint64_t *out) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const uint32_t rd = rank_d ? rank_d[j] : 0;
-    out[j] = (uint64_t)((int64_t)rank_b[j] + (rd ? cnt_prefix[rd - 1] : 0));
+    out[j] = (uint64_t)((int64_t)rank_b[j] + (rd ? cnt_through(cp, rd - 1) : 0));
+}
+
+// ---- run merge: the merged run and its block sums in one pass ----------------------------------
+// Merging a key-sorted batch into a sorted run A (rank / present: each batch key's lower bound
+// in A and whether A holds it; op 0 upsert, 1 drop):
+//   an upsert u lands at    pos_u = rank + U_before - R_before
+//   (U: upserts, R: batch keys present in A -- overwritten or dropped A rows), and the A rows
+//   that survive fill the remaining output slots in order.
+// k_mclass / exclusive scan / k_mlists list the upserts' positions and the removed A ranks;
+// k_merge_run then owns MT output rows per workgroup: it marks the upserts' slots, fills the
+// free slots with A survivors (the q-th survivor is A row s + k, k = #removed ranks before it,
+// found by a binary search over rank - index), copies each row once, and emits the 256-row
+// block sums of the payload's leading fingerprint -- and, for the delta run, each block's
+// count-delta total and every row's in-block count prefix.  This replaces a row-move pass, a
+// batch-scatter pass and a re-read of the whole run for its sums.
+constexpr int MT = 1024;  // output rows per workgroup (4 blocks of 256)
+
+// up (op 0) in the high word, present in the low word; zeroes the overwrite counter
+__global__ void k_mclass(const uint8_t *ops, const uint8_t *present, uint64_t m, uint64_t *v, uint64_t *counts) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j == 0) counts[1] = 0;
+    if (j < m) v[j] = ((uint64_t)(ops[j] == 0 ? 1u : 0u) << 32) | (present[j] ? 1u : 0u);
+}
+
+// counts: [1] overwrites (upsert of a present key), [3] upserts, [4] present
+__global__ void k_mlists(const uint8_t *ops, const uint8_t *present, const uint32_t *rank, const uint64_t *ex,
+                         uint64_t m, uint32_t *upos, uint32_t *usrc, uint32_t *rlist, uint64_t *counts) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool ovr = false;
+    if (j < m) {
+        const bool up = ops[j] == 0, pr = present[j] != 0;
+        const uint32_t U = (uint32_t)(ex[j] >> 32), R = (uint32_t)ex[j];
+        if (up) {
+            upos[U] = rank[j] + U - R;
+            usrc[U] = (uint32_t)j;
+        }
+        if (pr) rlist[R] = rank[j];
+        ovr = up && pr;
+        if (j == m - 1) {
+            counts[3] = U + (up ? 1u : 0u);
+            counts[4] = R + (pr ? 1u : 0u);
+        }
+    }
+    const unsigned long long b = __ballot(ovr);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(reinterpret_cast<unsigned long long *>(counts + 1), (unsigned long long)__popcll(b));
+}
+
+// counts[0] inserts, [2] removals (ins / ovr / del of the merge); also into out3 if given
+__global__ void k_mcounts(uint64_t *counts, uint64_t *out3) {
+    if (threadIdx.x != 0) return;
+    const uint64_t ovr = counts[1];
+    counts[0] = counts[3] - ovr;
+    counts[2] = counts[4] - ovr;
+    if (out3) {
+        out3[0] = counts[0];
+        out3[1] = ovr;
+        out3[2] = counts[2];
+    }
+}
+
+// smallest k in [lo, hi] with k == R or rlist[k] - k > s: the number of removed A rows before
+// the s-th survivor
+__device__ __forceinline__ uint64_t survivor_k(const uint32_t *rlist, uint64_t R, uint64_t lo, uint64_t hi, uint64_t s) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (mid >= R || (int64_t)rlist[mid] - (int64_t)mid > (int64_t)s) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+template <int KL, int P, bool COUNTS>
+__global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
+                                                   const uint8_t *bkeys, const uint8_t *bpay, uint64_t m,
+                                                   const uint32_t *upos, const uint32_t *usrc, const uint32_t *rlist,
+                                                   const uint64_t *counts, uint8_t *okeys, uint8_t *opay,
+                                                   uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk) {
+    static_assert(P % 16 == 0 && P >= 32, "payload: a leading fingerprint, 16-byte units");
+    __shared__ int32_t src[MT];  // A row, or -2 - batch row, or -1
+    __shared__ uint64_t prm[6];
+    __shared__ uint32_t wsum[4];
+    __shared__ SumTile tile;
+    const uint32_t t = threadIdx.x;
+    const uint64_t U = counts[3], R = counts[4];
+    const uint64_t nC = nA + U - R;  // <= nA + m
+    const uint64_t o0 = (uint64_t)blockIdx.x * MT;
+    if (t == 0) {
+        uint64_t o1 = o0, ju0 = 0, ju1 = 0, s0 = 0, k0 = 0, k1 = 0;
+        if (o0 < nC) {
+            o1 = o0 + MT < nC ? o0 + MT : nC;
+            ju0 = lower_bound_u32(upos, 0, U, o0);
+            ju1 = lower_bound_u32(upos, ju0, U, o1);
+            s0 = o0 >= ju0 ? o0 - ju0 : 0;
+            const uint64_t s1 = o1 >= ju1 ? o1 - ju1 : 0;
+            k0 = survivor_k(rlist, R, 0, R, s0);
+            k1 = survivor_k(rlist, R, k0, R, s1);
+        }
+        prm[0] = o1 - o0; prm[1] = ju0; prm[2] = ju1; prm[3] = s0; prm[4] = k0; prm[5] = k1;
+    }
+    for (uint32_t q = t; q < MT; q += 256) src[q] = -1;
+    __syncthreads();
+    const uint32_t nrows = (uint32_t)prm[0];
+    const uint64_t ju0 = prm[1], ju1 = prm[2], s0 = prm[3], k0 = prm[4], k1 = prm[5];
+    for (uint64_t u = ju0 + t; u < ju1; u += 256) {
+        const uint64_t p = (uint64_t)upos[u] - o0;
+        const uint32_t j = usrc[u];
+        if (p < nrows && j < m) src[p] = -2 - (int32_t)j;
+    }
+    __syncthreads();
+    // free slots (4 per lane) in order -> the tile's A survivors
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) cnt += (4 * t + k < nrows && src[4 * t + k] == -1) ? 1u : 0u;
+    uint32_t x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((t & 63) >= (uint32_t)o) x += y;
+    }
+    if ((t & 63) == 63) wsum[t >> 6] = x;
+    __syncthreads();
+    uint32_t q = x - cnt;
+    for (uint32_t w = 0; w < (t >> 6); w++) q += wsum[w];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t slot = 4 * t + k;
+        if (slot < nrows && src[slot] == -1) {
+            const uint64_t sidx = s0 + q;
+            const uint64_t i = sidx + survivor_k(rlist, R, k0, k1, sidx);
+            if (i < nA) src[slot] = (int32_t)i;
+            q++;
+        }
+    }
+    __syncthreads();
+    // copy + block sums: lane t moves row b * 256 + t of each of the tile's 4 blocks
+    for (int b = 0; b < MT / 256; b++) {
+        const uint32_t o = b * 256 + t;
+        uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int32_t c = 0;
+        const int32_t sr = o < nrows ? src[o] : -1;
+        if (sr != -1) {
+            const bool fromA = sr >= 0;
+            const uint64_t r = fromA ? (uint64_t)sr : (uint64_t)(-2 - sr);
+            const uint8_t *ks = (fromA ? akeys : bkeys) + r * KL;
+            const uint4 *ps = reinterpret_cast<const uint4 *>((fromA ? apay : bpay) + r * P);
+            const uint64_t od = o0 + o;
+            copy_bytes<KL>(okeys + od * KL, ks);
+            uint4 pv[P / 16];
+#pragma unroll
+            for (int k = 0; k < P / 16; k++) pv[k] = ps[k];
+            uint4 *pd = reinterpret_cast<uint4 *>(opay + od * P);
+#pragma unroll
+            for (int k = 0; k < P / 16; k++) pd[k] = pv[k];
+            h[0] = pv[0].x; h[1] = pv[0].y; h[2] = pv[0].z; h[3] = pv[0].w;
+            h[4] = pv[1].x; h[5] = pv[1].y; h[6] = pv[1].z; h[7] = pv[1].w;
+            if constexpr (COUNTS) {
+                const uint32_t f = pv[2].y;  // DeltaRec::flags
+                c = ((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0);
+            }
+        }
+        const uint64_t blk = o0 / 256 + b;
+        uint32_t f8[8];
+        block_sum_fps256(h, tile, f8);
+        if (t == 0 && blk < nbk) store_sum(obs, blk, f8);
+        if constexpr (COUNTS) {
+            int32_t y = c;
+#pragma unroll
+            for (int o2 = 1; o2 < 64; o2 <<= 1) {
+                const int32_t z = __shfl_up(y, o2, 64);
+                if ((t & 63) >= (uint32_t)o2) y += z;
+            }
+            __syncthreads();
+            if ((t & 63) == 63) wsum[t >> 6] = (uint32_t)y;
+            __syncthreads();
+            int32_t before = 0;
+            for (uint32_t w = 0; w < (t >> 6); w++) before += (int32_t)wsum[w];
+            if (o < nrows) oinb[o0 + o] = (int16_t)(before + y);
+            if (t == 255 && blk < nbk) ocnt[blk] = before + y;
+        }
+    }
+}
+
+__global__ void k_last_i32(const int32_t *a, uint64_t n, int32_t *out) {
+    if (threadIdx.x == 0) *out = n ? a[n - 1] : 0;
+}
+
+hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scratch &s, hipStream_t st) {
+    hipError_t e;
+    if (nbk) {
+        size_t tb = 0;
+        if ((e = rocprim::inclusive_scan(nullptr, tb, blk, blk, nbk, rocprim::plus<int32_t>(), st))) return e;
+        void *tmp = s.bytes(tb);
+        if (s.err) return s.err;
+        if ((e = rocprim::inclusive_scan(tmp, tb, blk, blk, nbk, rocprim::plus<int32_t>(), st))) return e;
+    }
+    hipLaunchKernelGGL(k_last_i32, dim3(1), dim3(64), 0, st, blk, nbk, total);
+    return hipGetLastError();
+}
+
+template <int KL, int P, bool COUNTS>
+hipError_t merge_run_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, const uint8_t *bkeys,
+                       const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank, const uint8_t *present, uint64_t m,
+                       Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb,
+                       uint64_t nbk, uint64_t *counts, uint64_t *out3, hipStream_t st) {
+    hipError_t e;
+    uint64_t *v = s.u64(3, m + 1), *ex = s.u64(4, m + 1);
+    uint32_t *upos = s.u32(3, m + 1), *usrc = s.u32(4, m + 1), *rlist = s.u32(5, m + 1);
+    if (s.err) return s.err;
+    if (m) {
+        hipLaunchKernelGGL(k_mclass, g1(m), dim3(256), 0, st, bops, present, m, v, counts);
+        size_t tb = 0;
+        if ((e = rocprim::exclusive_scan(nullptr, tb, v, ex, (uint64_t)0, m, rocprim::plus<uint64_t>(), st))) return e;
+        void *tmp = s.bytes(tb);
+        if (s.err) return s.err;
+        if ((e = rocprim::exclusive_scan(tmp, tb, v, ex, (uint64_t)0, m, rocprim::plus<uint64_t>(), st))) return e;
+        hipLaunchKernelGGL(k_mlists, g1(m), dim3(256), 0, st, bops, present, rank, ex, m, upos, usrc, rlist, counts);
+    } else {
+        if ((e = hipMemsetAsync(counts, 0, 5 * 8, st))) return e;
+    }
+    hipLaunchKernelGGL(k_mcounts, dim3(1), dim3(64), 0, st, counts, out3);
+    const uint64_t tiles = (nA + m + MT - 1) / MT;
+    if (tiles)
+        hipLaunchKernelGGL((k_merge_run<KL, P, COUNTS>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys, apay, nA,
+                           bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_run(int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
+                            const uint8_t *bkeys, const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank,
+                            const uint8_t *present, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay,
+                            uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *counts,
+                            uint64_t *out3, hipStream_t st) {
+#define RH_MR(KLV)                                                                                                 \
+    if (kl == KLV) {                                                                                               \
+        if (payload == 32)                                                                                         \
+            return merge_run_t<KLV, 32, false>(akeys, apay, nA, bkeys, bpay, bops, rank, present, m, s, okeys, opay, \
+                                               obs, ocnt, oinb, nbk, counts, out3, st);                            \
+        if (payload == (int)sizeof(DeltaRec))                                                                      \
+            return merge_run_t<KLV, sizeof(DeltaRec), true>(akeys, apay, nA, bkeys, bpay, bops, rank, present, m, s, \
+                                                            okeys, opay, obs, ocnt, oinb, nbk, counts, out3, st);  \
+    }
+    RH_MR(4) RH_MR(8) RH_MR(16) RH_MR(32)
+#undef RH_MR
+    return hipErrorInvalidValue;
 }
 
 // ---- host-side drivers --------------------------------------------------------------------------
 
-namespace {
-inline dim3 g1(uint64_t m) { return dim3((uint32_t)((m + 255) / 256)); }
-}
 
 template <int KK, int KL>
 struct KeyOps final : StoreKeyOps {
@@ -505,6 +1015,7 @@ struct KeyOps final : StoreKeyOps {
             std::swap(perm, perm2);
             return hipSuccess;
         };
+        if (!full && m <= SB_MAX_M) return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st);
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
         // multi-digit keys: the most significant digit alone orders random and spread keys
         // (k_gather reports a tie); the LSD sort (least significant digit first, stable passes)
@@ -517,10 +1028,42 @@ struct KeyOps final : StoreKeyOps {
         return hipGetLastError();
     }
 
+    hipError_t sort_batch_buckets(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
+                                  uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, hipStream_t st) {
+        const uint32_t nwg = (uint32_t)((m + SB_TILE - 1) / SB_TILE);
+        uint64_t *part = s.u64(2, 2ull * nwg), *dig = s.u64(0, m);
+        uint32_t *hist = s.u32(15, (uint64_t)nwg * SB_N), *idx = s.u32(0, m), *total = s.u32(1, SB_N);
+        uint32_t *start = s.u32(2, SB_N);
+        if (s.err) return s.err;
+        hipLaunchKernelGGL((k_sb_minmax<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part);
+        hipLaunchKernelGGL((k_sb_hist<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part, nwg, hist);
+        hipLaunchKernelGGL(k_sb_colscan, dim3(SB_N / 64), dim3(64), 0, st, hist, nwg, total);
+        hipLaunchKernelGGL(k_sb_bucketscan, dim3(1), dim3(1024), 0, st, total, start, flags);
+        hipLaunchKernelGGL((k_sb_scatter<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part, nwg, hist, start, dig,
+                           idx);
+        hipLaunchKernelGGL((k_sb_sort<KK, KL>), dim3(SB_N), dim3(64), 0, st, dig, idx, start, total, keys, fps, ops,
+                           skeys, sfps, sops, flags);
+        return hipGetLastError();
+    }
+
     hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present,
                       hipStream_t st) override {
         if (m == 0) return hipSuccess;
         hipLaunchKernelGGL((k_search<KK, KL>), g1(m), dim3(256), 0, st, keys, n, q, m, rank, present);
+        return hipGetLastError();
+    }
+
+    hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, hipStream_t st) override {
+        const uint64_t ns = (n + SMP_STRIDE - 1) / SMP_STRIDE;
+        if (ns == 0) return hipSuccess;
+        hipLaunchKernelGGL((k_sample<KK, KL>), g1(ns), dim3(256), 0, st, keys, n, smp);
+        return hipGetLastError();
+    }
+
+    hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint8_t *q, uint64_t m,
+                              uint32_t *rank, uint8_t *present, hipStream_t st) override {
+        if (m == 0) return hipSuccess;
+        hipLaunchKernelGGL((k_search_sampled<KK, KL>), g1(m), dim3(256), 0, st, keys, n, smp, q, m, rank, present);
         return hipGetLastError();
     }
 
@@ -671,15 +1214,15 @@ hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base
 }
 
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
-                            const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out, hipStream_t st) {
-    hipLaunchKernelGGL(k_agg_merge, dim3(1), dim3(64), 0, st, base_agg, delta_agg, dlo, dhi, cnt_prefix, out);
+                            const uint64_t *dhi, CntPrefix cp, uint64_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_agg_merge, dim3(1), dim3(64), 0, st, base_agg, delta_agg, dlo, dhi, cp, out);
     return hipGetLastError();
 }
 
-hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, const int32_t *cnt_prefix, uint64_t m,
+hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, CntPrefix cp, uint64_t m,
                              uint64_t *out, hipStream_t st) {
     if (m == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rank_merge, g1(m), dim3(256), 0, st, rank_b, rank_d, cnt_prefix, m, out);
+    hipLaunchKernelGGL(k_rank_merge, g1(m), dim3(256), 0, st, rank_b, rank_d, cp, m, out);
     return hipGetLastError();
 }
 

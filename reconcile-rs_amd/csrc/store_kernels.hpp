@@ -73,9 +73,10 @@ static_assert(sizeof(DeltaRec) == 48, "DeltaRec layout (16-byte multiple: rows a
 // Key-type-specialised device operations of the store.
 struct StoreKeyOps {
     virtual ~StoreKeyOps() = default;
-    // sort a batch by key and gather keys / fingerprints / ops into key order.  full = false:
-    // one radix pass on the most significant u64 digit only, and *flags |= 2 if two keys share
-    // that digit (the order is then not final: sort again with full = true, the LSD radix over
+    // sort a batch by key (stable) and gather keys / fingerprints / ops into key order.
+    // full = false: order by the most significant u64 digit only (a bucket pass + LDS sort),
+    // and *flags |= 2 if two keys share that digit, |= 4 if the digits are too skewed for the
+    // buckets (the order is then not final: sort again with full = true, the LSD radix over
     // every digit).  *flags |= 1 if two batch keys are equal.
     virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
                                   Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags,
@@ -83,6 +84,11 @@ struct StoreKeyOps {
     // lower-bound rank of each query key (and whether it is present)
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;
+    // smp[s] = leading digit of keys[256 s] (ceil(n / 256) entries), and the lower-bound search
+    // through it (same results as search)
+    virtual hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, hipStream_t st) = 0;
+    virtual hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint8_t *q,
+                                      uint64_t m, uint32_t *rank, uint8_t *present, hipStream_t st) = 0;
     // merge a key-sorted batch (ops: 0 upsert, 1 delete) into a sorted run of (key, payload)
     // rows -> (okeys, opay); payload 32 (fingerprints) or 48 (DeltaRec);
     // counts = {inserted, overwritten, deleted}.  rank / present: the batch keys' search result
@@ -102,6 +108,28 @@ struct StoreKeyOps {
     virtual int compare_keys_host(const uint8_t *a, const uint8_t *b) const = 0;
 };
 
+// Σ count deltas of delta rows [0, i] = blk[i / 256 - 1] (inclusive block prefix) + inb[i]
+// (inclusive prefix inside the row's 256-row block)
+struct CntPrefix {
+    const int32_t *blk;
+    const int16_t *inb;
+};
+
+// Merge a key-sorted batch (ops 0 upsert / 1 drop; rank / present: its keys' lower bounds in
+// the run and whether the run holds them) into a sorted run of (key, payload) rows, writing
+// the merged run, the 256-row block sums of the payload's leading fingerprint (nbk blocks:
+// rows past the merged length count as zero) and, for DeltaRec payloads, each block's
+// count-delta total (ocnt) and the rows' in-block count prefixes (oinb).
+// counts (device, 8): [0] inserts, [1] overwrites, [2] removals; out3 (optional) gets the same.
+hipError_t launch_merge_run(int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
+                            const uint8_t *bkeys, const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank,
+                            const uint8_t *present, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay,
+                            uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *counts,
+                            uint64_t *out3, hipStream_t st);
+
+// in place: blk[b] <- Σ blk[0..b] (the inclusive block prefix); *total <- the last entry
+hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scratch &s, hipStream_t st);
+
 // delta-run kernels (store_kernels.hip)
 hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
                               const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
@@ -117,8 +145,8 @@ hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_ol
 hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
                             uint32_t *rank, uint8_t *present, hipStream_t st);
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
-                            const uint64_t *dhi, const int32_t *cnt_prefix, uint64_t *out, hipStream_t st);
-hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, const int32_t *cnt_prefix, uint64_t m,
+                            const uint64_t *dhi, CntPrefix cp, uint64_t *out, hipStream_t st);
+hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, CntPrefix cp, uint64_t m,
                              uint64_t *out, hipStream_t st);
 
 // nullptr if the store does not support this key type

@@ -566,6 +566,39 @@ def test_store_batch_keys_sharing_leading_bytes(gpu, oracle_lib):
     st.close()
 
 
+@pytest.mark.gpu
+def test_store_batch_sort_skewed_and_dense(gpu, oracle_lib):
+    """The update batches' bucket sort: a tight cluster of 3000 u64 keys plus far outliers (one
+    bucket overflows: the full radix sort takes over), then a dense arithmetic run and a
+    random batch (the bucket path) -- the store's key order and fingerprints match the oracle's."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    O = oracle_lib
+    s = RecordSchema.plain("u64", "bytes64")
+    rng = np.random.default_rng(33)
+    batches = [
+        np.concatenate([10**12 + np.arange(3000, dtype=np.uint64), np.array([5, 2**63, 2**64 - 7], np.uint64)]),
+        np.arange(20000, dtype=np.uint64) * 3 + 7,
+        rng.integers(0, 2**63, 50000, dtype=np.uint64) * 2 + 1,
+    ]
+    st = GpuFingerprintStore(s)
+    all_keys, all_vals = [], []
+    for b in batches:
+        b = b[rng.permutation(len(b))]
+        v = rng.integers(0, 256, (len(b), 64), dtype=np.uint8)
+        st.apply({"keys": b.view(np.uint8).reshape(-1, 8), "values": v}, np.zeros(len(b), np.uint8))
+        all_keys.append(b)
+        all_vals.append(v)
+    keys, vals = np.concatenate(all_keys), np.concatenate(all_vals)
+    keys, first = np.unique(keys, return_index=True)
+    assert len(keys) == st.size()
+    sch = O.Schema(O.KEY_U64, 8, O.VAL_BYTES, 64, O.REC_PLAIN, 0)
+    want = O.Records(sch, np.ascontiguousarray(keys.view(np.uint8).reshape(-1, 8)),
+                     np.ascontiguousarray(vals[first])).lift()
+    assert np.array_equal(st.fingerprints(), want)
+    assert [k for k, _ in st.enumerate()] == [int(k) for k in keys]
+    st.close()
+
+
 def _torch_root(torch, fps) -> int:
     """Σ fingerprints mod 2^256 by an independent torch reduction over u16 limbs."""
     limbs16 = fps.view(torch.int16).to(torch.int64) & 0xFFFF

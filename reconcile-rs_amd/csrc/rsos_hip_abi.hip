@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -390,7 +391,7 @@ struct rh_store {
     uint64_t nb = 0;
     int cb = 0;
     DevBuf<uint8_t> bkeys[2], bfps[2], bsums, ssums;
-    DevBuf<uint64_t> bsmp, dsmp;  // leading digits of every 256th key (sampled search)
+    DevBuf<uint64_t> bsmp, bsmp2, dsmp;  // leading digits of every 256th (16th) key: sampled search
     // delta run
     uint64_t nd = 0;
     int cd = 0;
@@ -407,7 +408,7 @@ struct rh_store {
     // batch scratch
     DevColumns staging;
     DevBuf<uint8_t> lfps, skeys, sfps, sops, hops, bpay, dops, cfps, cops;
-    DevBuf<uint64_t> counts, counts2, results;
+    DevBuf<uint64_t> counts, results;
     DevBuf<uint32_t> flag;
     // query scratch
     DevBuf<uint64_t> q_lo, q_hi, q_dlo, q_dhi, q_merged;
@@ -418,7 +419,17 @@ struct rh_store {
     rh::Scratch scratch;
 
     uint64_t size() const { return (uint64_t)((int64_t)nb + dtotal); }
+    // Wait for the stream by polling it: the batch path ends in one short wait for a 96-byte
+    // result, where an interrupt-driven wake-up costs tens of microseconds per batch.  Long
+    // waits (a compaction, a large load) fall back to the blocking call after ~1 ms.
     int sync() {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t e = hipStreamQuery(stream);
+            if (e == hipSuccess) return RH_OK;
+            if (e != hipErrorNotReady) return fail(RH_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1)) break;
+        }
         RH_HIP(hipStreamSynchronize(stream));
         return RH_OK;
     }
@@ -426,10 +437,10 @@ struct rh_store {
         int rc;
         const size_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
         if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4)) ||
-            (rc = bsmp.ensure(nbk + 1)))
+            (rc = bsmp.ensure(nbk + 1)) || (rc = bsmp2.ensure(nb / 16 + 2)))
             return rc;
         if (nb) {
-            RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, stream));
+            RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, bsmp2.p, stream));
             if (!have_block_sums) RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
             RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
             RH_HIP(rh::launch_total(ssums.p, ns, tot.p, stream));
@@ -521,7 +532,7 @@ struct rh_store {
     int compact() {  // merge the delta run into the base run
         int rc;
         if (nd == 0) return RH_OK;
-        if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64)) || (rc = counts2.ensure(4))) return rc;
+        if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64))) return rc;
         uint32_t *crank = scratch.u32(14, nd);
         uint8_t *cpres = scratch.u8(4, nd);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -558,12 +569,12 @@ struct rh_store {
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         if ((rc = lfps.ensure(m * 32 + 64)) || (rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) ||
             (rc = sops.ensure(m + 64)) || (rc = bpay.ensure(m * sizeof(rh::DeltaRec) + 64)) ||
-            (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)) || (rc = counts2.ensure(4)))
+            (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
         // 1. lift the batch (delete rows are lifted too and ignored)
         if ((rc = lift_dispatch(schema, c, m, lfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
         if ((rc = dsmp.ensure(rh_num_blocks(nd) + 1))) return rc;
-        RH_HIP(kops->sample(dkeys[cd].p, nd, dsmp.p, stream));
+        RH_HIP(kops->sample(dkeys[cd].p, nd, dsmp.p, nullptr, stream));
         // 2-5 run without a host round trip: everything is written to the delta run's *other*
         // buffers, and one sync at the end brings back the flags and counts.  A duplicate key
         // then leaves the store exactly as it was (nothing is committed); a tie on the leading
@@ -598,8 +609,8 @@ struct rh_store {
                                     sops.p, r_flags, full == 1, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 3. where each key is now: base and delta runs
-            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, skeys.p, m, rank_b, present_b, stream));
-            RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp.p, skeys.p, m, rank_d, present_d, stream));
+            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, skeys.p, m, rank_b, present_b, stream));
+            RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp.p, nullptr, skeys.p, m, rank_d, present_d, stream));
             // 4. the batch's delta records, merged into the delta run's other buffer
             RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d,
                                           dpay[cd].p, bpay.p, dops.p, r_counts, scratch, stream));
@@ -679,7 +690,7 @@ struct rh_store {
             (rc = q_merged.ensure(m)))
             return rc;
         RH_HIP(hipMemcpyAsync(q_keys.p, keys, m * kl, hipMemcpyHostToDevice, stream));
-        RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, q_keys.p, m, q_rank.p, nullptr, stream));
+        RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_keys.p, m, q_rank.p, nullptr, stream));
         if (nd) RH_HIP(kops->search(dkeys[cd].p, nd, q_keys.p, m, q_drank.p, nullptr, stream));
         RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, cnt_prefix(cd), m, q_merged.p, stream));
         RH_HIP(hipMemcpyAsync(out, q_merged.p, m * 8, hipMemcpyDeviceToHost, stream));
@@ -690,13 +701,13 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
         }
-        bsums.release(); ssums.release(); tot.release(); bsmp.release(); dsmp.release(); mcnt.release();
+        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); dsmp.release(); mcnt.release();
         for (int k = 0; k < 2; k++) {
             dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release();
         }
         staging.release();
         lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); bpay.release();
-        dops.release(); cfps.release(); cops.release(); counts.release(); counts2.release(); flag.release();
+        dops.release(); cfps.release(); cops.release(); counts.release(); flag.release();
         results.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();

@@ -4,7 +4,7 @@
 // Store layout in HBM (rank order):
 //   base  : keys[nB][KL] + fps[nB][32] + block sums [nB/256][32] + super sums [nB/65536][32]
 //   delta : keys[nD][KL] + DeltaRec[nD] (48 B) + block / super sums of the contributions +
-//           an inclusive prefix of the count deltas
+//           the count-delta prefix (inclusive per 256-row block + int16 inside each block)
 // A DeltaRec for key k says what the batches since the last compaction did to k:
 //   contrib = cur_fp - base_fp   (cur_fp = 0 if k is now deleted; base_fp = 0 if k not in base)
 //   in_base, live                 (so the count delta is live - in_base, in {-1, 0, +1})
@@ -16,8 +16,9 @@
 //
 // Batched update = FingerprintTreeMap::insert / remove applied to a whole batch at once
 // (mutate.rs:23-154): sort the batch by key, find every key in base and delta, build the
-// batch's DeltaRecs, merge them into the delta run (O(m + nD)); when the delta run passes
-// nB / 8 it is merged into the base (O(nB)) -- amortised, and on demand before rank / select.
+// batch's DeltaRecs, merge them into the delta run (O(m + nD), one pass that also writes the
+// run's sums); when the delta run passes nB / 8 it is merged into the base the same way
+// (O(nB)) -- amortised, and on demand before rank / select.
 #include <type_traits>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -256,22 +257,36 @@ __global__ __launch_bounds__(256) void k_sb_hist(const uint8_t *keys, uint64_t m
     for (uint32_t b = threadIdx.x; b < SB_N; b += 256) o[b] = h[b];
 }
 
-// per bucket: each workgroup's running offset within the bucket (in place), and the total
-__global__ __launch_bounds__(64) void k_sb_colscan(uint32_t *hist, uint32_t nwg, uint32_t *total) {
-    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= SB_N) return;
-    uint32_t run = 0;
-    for (uint32_t w0 = 0; w0 < nwg; w0 += 8) {  // 8 loads in flight per lane
+// per bucket: each workgroup's running offset within the bucket (in place), and the total.
+// 64 buckets per workgroup, 4 lanes per bucket: lane q sums a quarter of the histogram rows,
+// the quarters' sums are exchanged in LDS, then each lane writes its quarter's offsets.
+__global__ __launch_bounds__(256) void k_sb_colscan(uint32_t *hist, uint32_t nwg, uint32_t *total) {
+    __shared__ uint32_t part[4][64];
+    const uint32_t lb = threadIdx.x & 63, qt = threadIdx.x >> 6, b = blockIdx.x * 64 + lb;
+    const uint32_t per = (nwg + 3) / 4, w0 = qt * per, w1 = w0 + per < nwg ? w0 + per : nwg;
+    uint32_t sum = 0;
+    for (uint32_t w = w0; w < w1; w += 8) {
         uint32_t t[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) t[k] = w0 + k < nwg ? hist[(uint64_t)(w0 + k) * SB_N + b] : 0u;
+        for (int k = 0; k < 8; k++) t[k] = w + k < w1 ? hist[(uint64_t)(w + k) * SB_N + b] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += t[k];
+    }
+    part[qt][lb] = sum;
+    __syncthreads();
+    uint32_t run = 0;
+    for (uint32_t q = 0; q < qt; q++) run += part[q][lb];
+    if (qt == 3) total[b] = run + sum;
+    for (uint32_t w = w0; w < w1; w += 8) {
+        uint32_t t[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) t[k] = w + k < w1 ? hist[(uint64_t)(w + k) * SB_N + b] : 0u;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            if (w0 + k < nwg) hist[(uint64_t)(w0 + k) * SB_N + b] = run;
+            if (w + k < w1) hist[(uint64_t)(w + k) * SB_N + b] = run;
             run += t[k];
         }
     }
-    total[b] = run;
 }
 
 // exclusive scan of the bucket totals (one workgroup of 1024, SB_N / 1024 buckets per lane)
@@ -388,12 +403,14 @@ __global__ void k_search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint
 // among the samples bounds the key's rank to one stride-wide window (more when samples tie),
 // so a query touches the small, cache-resident sample array and then a few lines of one
 // window, instead of ~log2(n) scattered lines of the whole run.
-constexpr uint64_t SMP_STRIDE = 256;
+// A second level (every SMP2_STRIDE-th key; 8 B per 16 keys) narrows the window to a few
+// lines; it is built for the large, rarely rewritten base run.
+constexpr uint64_t SMP_STRIDE = 256, SMP2_STRIDE = 16;
 
 template <int KK, int KL>
-__global__ void k_sample(const uint8_t *keys, uint64_t n, uint64_t *smp) {
+__global__ void k_sample(const uint8_t *keys, uint64_t n, uint64_t stride, uint64_t *smp) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s * SMP_STRIDE < n) smp[s] = key_digit<KK, KL>(keys + s * SMP_STRIDE * KL, 0);
+    if (s * stride < n) smp[s] = key_digit<KK, KL>(keys + s * stride * KL, 0);
 }
 
 __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t lo, uint64_t hi, uint64_t x) {
@@ -405,22 +422,32 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t 
     return lo;
 }
 
+// narrow [lo, hi) (a window of the key array that holds the lower bound of a key with leading
+// digit d) with samples smp[s] = digit of key s * stride, s in [0, ns)
+__device__ __forceinline__ void sample_window(const uint64_t *smp, uint64_t ns, uint64_t stride, uint64_t d,
+                                              uint64_t &lo, uint64_t &hi) {
+    const uint64_t s_lo = lo / stride, s_hi = (hi + stride - 1) / stride < ns ? (hi + stride - 1) / stride : ns;
+    const uint64_t a = lower_bound_u64(smp, s_lo, s_hi, d);  // samples < d: those keys are < key
+    if (a > s_lo) lo = (a - 1) * stride > lo ? (a - 1) * stride : lo;
+    if (a < s_hi) {
+        if (smp[a] > d) hi = a * stride < hi ? a * stride : hi;  // that sample's key is > key
+        else {  // samples equal to d: up to the first one above
+            const uint64_t b = lower_bound_u64(smp, a, s_hi, d + 1);
+            if (b < s_hi && d != ~0ull && b * stride < hi) hi = b * stride;
+        }
+    }
+}
+
 template <int KK, int KL>
-__global__ void k_search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint8_t *q, uint64_t m,
-                                 uint32_t *rank, uint8_t *present) {
+__global__ void k_search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint64_t *smp2,
+                                 const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const uint8_t *key = q + j * KL;
-    const uint64_t d = key_digit<KK, KL>(key, 0), ns = (n + SMP_STRIDE - 1) / SMP_STRIDE;
-    const uint64_t a = lower_bound_u64(smp, 0, ns, d);  // samples < d: those keys are < key
-    uint64_t lo = a ? (a - 1) * SMP_STRIDE : 0, hi = n;
-    if (a < ns) {
-        if (smp[a] > d) hi = a * SMP_STRIDE;  // that sample's key is > key
-        else {                                // samples equal to d: up to the first one above
-            const uint64_t b = lower_bound_u64(smp, a, ns, d + 1);
-            hi = (b < ns && d != ~0ull) ? b * SMP_STRIDE : n;
-        }
-    }
+    const uint64_t d = key_digit<KK, KL>(key, 0);
+    uint64_t lo = 0, hi = n;
+    sample_window(smp, (n + SMP_STRIDE - 1) / SMP_STRIDE, SMP_STRIDE, d, lo, hi);
+    if (smp2) sample_window(smp2, (n + SMP2_STRIDE - 1) / SMP2_STRIDE, SMP2_STRIDE, d, lo, hi);
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
         if (key_cmp<KK, KL>(keys + mid * KL, key) < 0) lo = mid + 1;
@@ -428,124 +455,6 @@ __global__ void k_search_sampled(const uint8_t *keys, uint64_t n, const uint64_t
     }
     rank[j] = (uint32_t)lo;
     if (present) present[j] = (lo < n && key_cmp<KK, KL>(keys + lo * KL, key) == 0) ? 1 : 0;
-}
-
-// ---- sorted-run merge (payload P bytes per row) ------------------------------------------
-
-// classify: op 0 = upsert, 1 = delete.  INS = upsert of an absent key, DEL = delete of a
-// present key; an upsert of a present key overwrites its payload; deleting an absent key is a
-// no-op (FingerprintTreeMap::remove returns None).
-__global__ void k_classify(const uint8_t *sops, const uint8_t *present, uint64_t m, uint32_t *ins, uint32_t *del) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    const bool p = present[j], isdel = sops[j] != 0;
-    ins[j] = (!isdel && !p) ? 1u : 0u;
-    del[j] = (isdel && p) ? 1u : 0u;
-}
-
-// compact the ranks of inserts and deletes (both come out sorted: the batch is key-sorted)
-__global__ void k_compact(const uint32_t *rank, const uint32_t *ins, const uint32_t *del, const uint32_t *cum_ins,
-                          const uint32_t *cum_del, uint64_t m, uint32_t *ins_rank, uint32_t *del_rank) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    if (ins[j]) ins_rank[cum_ins[j]] = rank[j];
-    if (del[j]) del_rank[cum_del[j]] = rank[j];
-}
-
-// counts[0] = inserts, counts[2] = deletes (counts[1], overwrites, by k_count_ovr)
-__global__ void k_counts(const uint32_t *ins, const uint32_t *del, const uint32_t *cum_ins, const uint32_t *cum_del,
-                         uint64_t m, uint64_t *counts) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    counts[0] = m ? (uint64_t)cum_ins[m - 1] + ins[m - 1] : 0;
-    counts[1] = 0;
-    counts[2] = m ? (uint64_t)cum_del[m - 1] + del[m - 1] : 0;
-}
-
-__global__ void k_count_ovr(const uint8_t *sops, const uint8_t *present, uint64_t m, unsigned long long *ovr) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool o = j < m && sops[j] == 0 && present[j];
-    const unsigned long long b = __ballot(o);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(ovr, (unsigned long long)__popcll(b));
-}
-
-// Survivors move to i + #inserts(rank <= i) - #deletes(rank < i); deleted rows are skipped.
-// One workgroup covers MOVE_TILE consecutive rows: one lane finds the slice of the (sorted)
-// insert / delete rank lists that falls inside the tile, every row binary-searches only that
-// slice for its shift (kept in LDS), and then the tile's key and payload bytes are copied as
-// flat dword streams -- consecutive lanes read consecutive dwords of the source run and write
-// consecutive dwords of the destination (a shifted memmove between insert / delete points).
-// No n-sized scratch arrays, no n-sized scan.
-constexpr int MOVE_TILE = 1024;
-
-template <int B>
-struct Unit {  // the widest access that divides a B-byte row
-    static constexpr int SIZE = B % 16 == 0 ? 16 : B % 8 == 0 ? 8 : 4;
-    using T = typename std::conditional<SIZE == 16, uint4, typename std::conditional<SIZE == 8, uint2, uint32_t>::type>::type;
-};
-
-// rows [i0, i0 + rows) of a B-byte-row run to row i + shift[i - i0] of dst, as a flat stream of
-// the widest units (consecutive lanes: consecutive source units)
-template <int B>
-__device__ __forceinline__ void move_rows(const uint8_t *src, uint8_t *dst, uint64_t i0, uint32_t rows,
-                                          const int32_t *shift, uint64_t cap) {
-    using U = typename Unit<B>::T;
-    constexpr int NU = B / Unit<B>::SIZE;
-    const U *s = reinterpret_cast<const U *>(src) + i0 * NU;
-    U *d = reinterpret_cast<U *>(dst);
-    for (uint32_t w = threadIdx.x; w < rows * NU; w += blockDim.x) {
-        const uint32_t r = w / NU;
-        const int32_t sh = shift[r];
-        const uint64_t pos = (uint64_t)((int64_t)(i0 + r) + sh);
-        // pos < cap always holds for a key-sorted batch; the guard keeps a speculative merge of
-        // a batch whose order was not final (re-run by the caller) inside the output run
-        if (sh != INT32_MIN && pos < cap) d[pos * NU + (w - r * NU)] = s[w];
-    }
-}
-
-template <int KL, int P>
-__global__ __launch_bounds__(256) void k_move_tiles(const uint8_t *keys, const uint8_t *pay, uint64_t n,
-                                                    const uint32_t *ins_rank, const uint32_t *del_rank,
-                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay,
-                                                    uint64_t cap) {
-    static_assert(KL % 4 == 0 && P % 4 == 0, "dword rows");
-    __shared__ uint64_t bounds[4];
-    __shared__ int32_t shift[MOVE_TILE];  // pos - i, or INT32_MIN for a deleted row
-    const uint64_t i0 = (uint64_t)blockIdx.x * MOVE_TILE;
-    if (threadIdx.x == 0) {
-        const uint64_t a = counts[0], d = counts[2];  // list lengths: #inserts, #deletes
-        bounds[0] = lower_bound_u32(ins_rank, 0, a, i0);              // inserts with rank < i0
-        bounds[1] = lower_bound_u32(ins_rank, 0, a, i0 + MOVE_TILE);  // ... < tile end
-        bounds[2] = lower_bound_u32(del_rank, 0, d, i0);
-        bounds[3] = lower_bound_u32(del_rank, 0, d, i0 + MOVE_TILE);
-    }
-    __syncthreads();
-    const uint64_t ia = bounds[0], ib = bounds[1], da = bounds[2], db = bounds[3];
-    const uint32_t rows = (uint32_t)(n - i0 < (uint64_t)MOVE_TILE ? n - i0 : MOVE_TILE);
-    for (uint32_t r = threadIdx.x; r < rows; r += 256) {
-        const uint64_t i = i0 + r;
-        const uint64_t ins_le = lower_bound_u32(ins_rank, ia, ib, i + 1);  // rank <= i
-        const uint64_t del_lt = lower_bound_u32(del_rank, da, db, i);      // rank < i
-        const bool gone = del_lt < db && del_rank[del_lt] == i;
-        shift[r] = gone ? INT32_MIN : (int32_t)((int64_t)ins_le - (int64_t)del_lt);
-    }
-    __syncthreads();
-    move_rows<KL>(keys, okeys, i0, rows, shift, cap);
-    move_rows<P>(pay, opay, i0, rows, shift, cap);
-}
-
-// inserts and overwrites land at r + (#inserts before j) - (#deletes before j): for an insert
-// that is its slot; for an overwrite it is where its surviving row moved (the inserts with
-// rank <= r and the deletes with rank < r are exactly the batch entries before j in key order)
-template <int KL, int P>
-__global__ void k_scatter(const uint8_t *skeys, const uint8_t *spay, const uint8_t *present, const uint8_t *sops,
-                          const uint32_t *rank, const uint32_t *cum_ins, const uint32_t *cum_del, uint64_t m,
-                          uint8_t *okeys, uint8_t *opay, uint64_t cap) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m || sops[j] != 0) return;
-    const uint64_t pos = (uint64_t)rank[j] + cum_ins[j] - cum_del[j];
-    if (pos >= cap) return;  // only for a batch whose order was not final (see move_rows)
-    if (!present[j]) copy_bytes<KL>(okeys + pos * KL, skeys + j * KL);
-    copy_bytes<P>(opay + (uint64_t)P * pos, spay + (uint64_t)P * j);
 }
 
 // 1 if keys are not strictly increasing
@@ -671,26 +580,6 @@ __global__ __launch_bounds__(1024) void k_sum_parts3(const uint32_t *part, uint6
         for (uint32_t q = 0; q < blockDim.x / 64; q++) s += w[q][threadIdx.x];
         counts[threadIdx.x] = s;
     }
-}
-
-// one pass over the delta run: the 256-row block sums of the contributions and each entry's
-// count delta (live - in_base), which the caller then prefix-sums
-__global__ __launch_bounds__(256) void k_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_old,
-                                                    const uint64_t *merge_counts, uint8_t *bsums, int32_t *cnt) {
-    __shared__ SumTile tile;
-    const uint64_t n = nd_old + merge_counts[0] - merge_counts[2];
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (i < n_max) cnt[i] = 0;
-    if (i < n) {
-        const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
-        fp_load(reinterpret_cast<const uint8_t *>(r.contrib), h);
-        const uint32_t f = r.flags;
-        cnt[i] = (int32_t)((f & DeltaRec::LIVE) ? 1 : 0) - (int32_t)((f & DeltaRec::IN_BASE) ? 1 : 0);
-    }
-    uint32_t f8[8];
-    block_sum_fps256(h, tile, f8);
-    if (threadIdx.x == 0) store_sum(bsums, blockIdx.x, f8);
 }
 
 // compaction input: cur fp = contrib + base fp, op = live ? upsert : delete, and the key's
@@ -1037,7 +926,7 @@ struct KeyOps final : StoreKeyOps {
         if (s.err) return s.err;
         hipLaunchKernelGGL((k_sb_minmax<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part);
         hipLaunchKernelGGL((k_sb_hist<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part, nwg, hist);
-        hipLaunchKernelGGL(k_sb_colscan, dim3(SB_N / 64), dim3(64), 0, st, hist, nwg, total);
+        hipLaunchKernelGGL(k_sb_colscan, dim3(SB_N / 64), dim3(256), 0, st, hist, nwg, total);
         hipLaunchKernelGGL(k_sb_bucketscan, dim3(1), dim3(1024), 0, st, total, start, flags);
         hipLaunchKernelGGL((k_sb_scatter<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part, nwg, hist, start, dig,
                            idx);
@@ -1053,70 +942,20 @@ struct KeyOps final : StoreKeyOps {
         return hipGetLastError();
     }
 
-    hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, hipStream_t st) override {
-        const uint64_t ns = (n + SMP_STRIDE - 1) / SMP_STRIDE;
+    hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, uint64_t *smp2, hipStream_t st) override {
+        const uint64_t ns = (n + SMP_STRIDE - 1) / SMP_STRIDE, ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
         if (ns == 0) return hipSuccess;
-        hipLaunchKernelGGL((k_sample<KK, KL>), g1(ns), dim3(256), 0, st, keys, n, smp);
+        hipLaunchKernelGGL((k_sample<KK, KL>), g1(ns), dim3(256), 0, st, keys, n, SMP_STRIDE, smp);
+        if (smp2) hipLaunchKernelGGL((k_sample<KK, KL>), g1(ns2), dim3(256), 0, st, keys, n, SMP2_STRIDE, smp2);
         return hipGetLastError();
     }
 
-    hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint8_t *q, uint64_t m,
-                              uint32_t *rank, uint8_t *present, hipStream_t st) override {
+    hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint64_t *smp2,
+                              const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present, hipStream_t st) override {
         if (m == 0) return hipSuccess;
-        hipLaunchKernelGGL((k_search_sampled<KK, KL>), g1(m), dim3(256), 0, st, keys, n, smp, q, m, rank, present);
+        hipLaunchKernelGGL((k_search_sampled<KK, KL>), g1(m), dim3(256), 0, st, keys, n, smp, smp2, q, m, rank,
+                           present);
         return hipGetLastError();
-    }
-
-    template <int P>
-    hipError_t merge_p(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys, const uint8_t *spay,
-                       const uint8_t *sops, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay, uint64_t *counts,
-                       hipStream_t st, const uint32_t *rank_in, const uint8_t *present_in) {
-        hipError_t e;
-        uint32_t *ins = s.u32(3, m), *del = s.u32(4, m);
-        uint32_t *cins = s.u32(5, m), *cdel = s.u32(6, m), *ins_rank = s.u32(7, m), *del_rank = s.u32(8, m);
-        const uint32_t *rank = rank_in;
-        const uint8_t *present = present_in;
-        if (!rank_in || !present_in) {  // where each batch key sits in the run
-            uint32_t *r = s.u32(2, m);
-            uint8_t *pr = s.u8(0, m);
-            if (s.err) return s.err;
-            if ((e = search(keys, n, skeys, m, r, pr, st))) return e;
-            rank = r;
-            present = pr;
-        }
-        if (s.err) return s.err;
-        hipLaunchKernelGGL(k_classify, g1(m), dim3(256), 0, st, sops, present, m, ins, del);
-        size_t tb = 0;
-        if ((e = rocprim::exclusive_scan(nullptr, tb, ins, cins, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
-        void *tmp = s.bytes(tb);
-        if (s.err) return s.err;
-        if ((e = rocprim::exclusive_scan(tmp, tb, ins, cins, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
-        if ((e = rocprim::exclusive_scan(tmp, tb, del, cdel, 0u, m, rocprim::plus<uint32_t>(), st))) return e;
-        hipLaunchKernelGGL(k_compact, g1(m), dim3(256), 0, st, rank, ins, del, cins, cdel, m, ins_rank, del_rank);
-        // list lengths (counts[0], counts[2]) are read by the tile kernel on the device
-        hipLaunchKernelGGL(k_counts, dim3(1), dim3(64), 0, st, ins, del, cins, cdel, m, counts);
-        if (n) {
-            const uint64_t tiles = (n + MOVE_TILE - 1) / MOVE_TILE;
-            hipLaunchKernelGGL((k_move_tiles<KL, P>), dim3((uint32_t)tiles), dim3(256), 0, st, keys, pay, n, ins_rank,
-                               del_rank, counts, okeys, opay, n + m);
-        }
-        hipLaunchKernelGGL((k_scatter<KL, P>), g1(m), dim3(256), 0, st, skeys, spay, present, sops, rank, cins, cdel,
-                           m, okeys, opay, n + m);
-        hipLaunchKernelGGL(k_count_ovr, g1(m), dim3(256), 0, st, sops, present, m,
-                           reinterpret_cast<unsigned long long *>(counts + 1));
-        return hipGetLastError();
-    }
-
-    hipError_t merge(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys, const uint8_t *spay,
-                     const uint8_t *sops, uint64_t m, int payload, Scratch &s, uint8_t *okeys, uint8_t *opay,
-                     uint64_t *counts, hipStream_t st, const uint32_t *rank, const uint8_t *present) override {
-        if (m == 0) return hipMemsetAsync(counts, 0, 24, st);
-        if (payload == 32)
-            return merge_p<32>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st, rank, present);
-        if (payload == (int)sizeof(DeltaRec))
-            return merge_p<sizeof(DeltaRec)>(keys, pay, n, skeys, spay, sops, m, s, okeys, opay, counts, st, rank,
-                                             present);
-        return hipErrorInvalidValue;
     }
 
     hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) override {
@@ -1191,19 +1030,6 @@ hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
                        present_d, dpay, bpay, dops, part);
     hipLaunchKernelGGL(k_sum_parts3, dim3(1), dim3(1024), 0, st, part, groups, counts);
     return hipGetLastError();
-}
-
-hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_old, const uint64_t *merge_counts,
-                             uint8_t *bsums, int32_t *cnt, Scratch &s, hipStream_t st) {
-    const uint64_t n = n_max;
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_delta_sums, g1(n), dim3(256), 0, st, dpay, n_max, nd_old, merge_counts, bsums, cnt);
-    size_t tb = 0;
-    hipError_t e;
-    if ((e = rocprim::inclusive_scan(nullptr, tb, cnt, cnt, n, rocprim::plus<int32_t>(), st))) return e;
-    void *tmp = s.bytes(tb);
-    if (s.err) return s.err;
-    return rocprim::inclusive_scan(tmp, tb, cnt, cnt, n, rocprim::plus<int32_t>(), st);
 }
 
 hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,

@@ -84,19 +84,12 @@ struct StoreKeyOps {
     // lower-bound rank of each query key (and whether it is present)
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;
-    // smp[s] = leading digit of keys[256 s] (ceil(n / 256) entries), and the lower-bound search
-    // through it (same results as search)
-    virtual hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, hipStream_t st) = 0;
-    virtual hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint8_t *q,
-                                      uint64_t m, uint32_t *rank, uint8_t *present, hipStream_t st) = 0;
-    // merge a key-sorted batch (ops: 0 upsert, 1 delete) into a sorted run of (key, payload)
-    // rows -> (okeys, opay); payload 32 (fingerprints) or 48 (DeltaRec);
-    // counts = {inserted, overwritten, deleted}.  rank / present: the batch keys' search result
-    // in the run if the caller already has it (else searched here)
-    virtual hipError_t merge(const uint8_t *keys, const uint8_t *pay, uint64_t n, const uint8_t *skeys,
-                             const uint8_t *spay, const uint8_t *sops, uint64_t m, int payload, Scratch &s,
-                             uint8_t *okeys, uint8_t *opay, uint64_t *counts, hipStream_t st,
-                             const uint32_t *rank = nullptr, const uint8_t *present = nullptr) = 0;
+    // smp[s] = leading digit of keys[256 s] (ceil(n / 256) entries), smp2 (optional) the same
+    // for every 16th key, and the lower-bound search through them (same results as search)
+    virtual hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, uint64_t *smp2, hipStream_t st) = 0;
+    virtual hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint64_t *smp2,
+                                      const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present,
+                                      hipStream_t st) = 0;
     virtual hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) = 0;
     // keep the last row of every run of equal keys of a key-sorted run (a stable sort keeps
     // input order within a run, so this is "the last insert wins"); counts[0] = rows kept
@@ -135,11 +128,6 @@ hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
                               const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
                               const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
                               uint64_t *counts, Scratch &s, hipStream_t st);
-// block sums of the contributions (bsums) + inclusive prefix of the count deltas (cnt) over
-// n_max rows, of which the first nd_old + merge_counts[0] - merge_counts[2] (read on the
-// device) are real and the rest count as zero
-hipError_t launch_delta_sums(const uint8_t *dpay, uint64_t n_max, uint64_t nd_old, const uint64_t *merge_counts,
-                             uint8_t *bsums, int32_t *cnt, Scratch &s, hipStream_t st);
 // compaction input from the delta run: cur fingerprints, ops (live ? upsert : delete) and each
 // key's place in the base (rank = brank, present = in_base) for the merge
 hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,

@@ -145,10 +145,16 @@ int rh_combine_aggregates_async(const rh_aggregate *dev_in, size_t parts, size_t
                                 rh_aggregate *dev_out, void *stream);
 
 /* ---- host helpers --------------------------------------------------------------------- */
-/* End-to-end lift of host records: H2D copy, lift on `device`, D2H of the fingerprints.
- * The PCIe-inclusive path a host caller (the Rust shim) uses for a one-shot batch.        */
+/* End-to-end lift of host records: H2D copy, lift on `device`, D2H of the fingerprints,
+ * pipelined in ~128 MB chunks over three streams (copy in / lift / copy out, so PCIe carries
+ * both directions at once).  The PCIe-inclusive path a host caller (the Rust shim) uses for a
+ * one-shot batch; host buffers from rh_host_alloc (pinned) let the copies overlap.         */
 int rh_lift_host(int device, const rh_schema *schema, const rh_columns *host_cols, size_t n,
                  uint8_t *host_fps);
+
+/* Page-locked host memory for rh_lift_host / rh_store_load / rh_store_apply buffers.     */
+int rh_host_alloc(size_t bytes, void **out);
+int rh_host_free(void *p);
 
 /* Fingerprint group on the host (rsos/src/fingerprint.rs:145-173), for callers' combines */
 void rh_fp_add(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <chrono>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -345,6 +346,56 @@ struct DevColumns {
 
 }  // namespace
 
+namespace {
+
+// The host path as a pipeline, kept per device between calls: chunk k's columns go up on the
+// copy-in stream while chunk k-1 is lifted and chunk k-2's fingerprints come down on the
+// copy-out stream.  PCIe is full duplex, so a run costs about its host-to-device copy alone
+// (pinned host buffers; pageable ones are staged by the runtime and serialise).
+struct HostPipe {
+    static constexpr int DEPTH = 3;
+    hipStream_t in = nullptr, comp = nullptr, out = nullptr;
+    DevColumns cols[DEPTH];
+    DevBuf<uint8_t> fps[DEPTH];
+    hipEvent_t up[DEPTH] = {}, down[DEPTH] = {}, lifted[DEPTH] = {};
+    std::mutex mu;
+    int init() {
+        if (in) return RH_OK;
+        RH_HIP(hipStreamCreateWithFlags(&in, hipStreamNonBlocking));
+        RH_HIP(hipStreamCreateWithFlags(&comp, hipStreamNonBlocking));
+        RH_HIP(hipStreamCreateWithFlags(&out, hipStreamNonBlocking));
+        for (int b = 0; b < DEPTH; b++) {
+            RH_HIP(hipEventCreateWithFlags(&up[b], hipEventDisableTiming));
+            RH_HIP(hipEventCreateWithFlags(&lifted[b], hipEventDisableTiming));
+            RH_HIP(hipEventCreateWithFlags(&down[b], hipEventDisableTiming));
+        }
+        return RH_OK;
+    }
+};
+
+HostPipe &host_pipe(int device) {
+    static std::mutex m;
+    static std::vector<std::unique_ptr<HostPipe>> pipes;
+    std::lock_guard<std::mutex> g(m);
+    if ((int)pipes.size() <= device) pipes.resize(device + 1);
+    if (!pipes[device]) pipes[device].reset(new HostPipe());
+    return *pipes[device];
+}
+
+rh_columns host_rows(const rh_schema &s, const rh_columns &h, size_t at) {
+    const size_t kr = key_row(s), vr = value_row(s);
+    rh_columns c = h;
+    if (c.keys) c.keys = static_cast<const uint8_t *>(c.keys) + at * kr;
+    if (c.values) c.values = static_cast<const uint8_t *>(c.values) + at * vr;
+    if (c.phys) c.phys += at;
+    if (c.logical) c.logical += at;
+    if (c.node) c.node += at;
+    if (c.tags) c.tags += at;
+    return c;
+}
+
+}  // namespace
+
 extern "C" int rh_lift_host(int device, const rh_schema *schema, const rh_columns *h, size_t n, uint8_t *host_fps) {
     int rc = check_schema(schema);
     if (rc) return rc;
@@ -352,26 +403,44 @@ extern "C" int rh_lift_host(int device, const rh_schema *schema, const rh_column
     if (n == 0) return RH_OK;
     if (!host_fps) return fail(RH_ERR_ARG, "host_fps is NULL");
     RH_HIP(hipSetDevice(device));
-    hipStream_t st;
-    RH_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    DevColumns dc;
-    DevBuf<uint8_t> fps;
-    rc = dc.upload(*schema, *h, n, st);
-    if (!rc) rc = fps.ensure(n * 32);
-    if (!rc) {
-        rh_columns v = dc.view(*schema);
-        rc = lift_dispatch(*schema, v, n, fps.p, nullptr, nullptr, nullptr, false, st);
+    HostPipe &p = host_pipe(device);
+    std::lock_guard<std::mutex> g(p.mu);
+    if ((rc = p.init())) return rc;
+    // ~128 MB of record columns per chunk
+    const size_t rec = key_row(*schema) + value_row(*schema) + 21;
+    const size_t chunk = std::max<size_t>(65536, (128u << 20) / rec);
+    for (size_t k = 0, at = 0; at < n; k++, at += chunk) {
+        const int b = (int)(k % HostPipe::DEPTH);
+        const size_t c = std::min(chunk, n - at);
+        // buffer set b is free once chunk k - DEPTH's fingerprints are down
+        if (k >= (size_t)HostPipe::DEPTH) RH_HIP(hipStreamWaitEvent(p.in, p.down[b], 0));
+        if ((rc = p.cols[b].upload(*schema, host_rows(*schema, *h, at), c, p.in)) || (rc = p.fps[b].ensure(chunk * 32)))
+            return rc;
+        RH_HIP(hipEventRecord(p.up[b], p.in));
+        RH_HIP(hipStreamWaitEvent(p.comp, p.up[b], 0));
+        if ((rc = lift_dispatch(*schema, p.cols[b].view(*schema), c, p.fps[b].p, nullptr, nullptr, nullptr, false,
+                                p.comp)))
+            return rc;
+        RH_HIP(hipEventRecord(p.lifted[b], p.comp));
+        RH_HIP(hipStreamWaitEvent(p.out, p.lifted[b], 0));
+        RH_HIP(hipMemcpyAsync(host_fps + at * 32, p.fps[b].p, c * 32, hipMemcpyDeviceToHost, p.out));
+        RH_HIP(hipEventRecord(p.down[b], p.out));
     }
-    if (!rc) {
-        hipError_t e = hipMemcpyAsync(host_fps, fps.p, n * 32, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) rc = fail(RH_ERR_HIP, std::string("rh_lift_host: ") + hipGetErrorString(e));
-    }
-    (void)hipStreamSynchronize(st);
-    dc.release();
-    fps.release();
-    (void)hipStreamDestroy(st);
-    return rc;
+    RH_HIP(hipStreamSynchronize(p.out));
+    return RH_OK;
+}
+
+extern "C" int rh_host_alloc(size_t bytes, void **out) {
+    if (!out) return fail(RH_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (!bytes) return RH_OK;
+    RH_HIP(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    return RH_OK;
+}
+
+extern "C" int rh_host_free(void *p) {
+    if (p) RH_HIP(hipHostFree(p));
+    return RH_OK;
 }
 
 // =================================================================================================

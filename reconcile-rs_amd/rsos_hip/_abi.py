@@ -56,6 +56,8 @@ SIGNATURES = [
     ("rh_range_aggregates_async", C.c_int, [U8P, U8P, U8P, SZ, U64P, U64P, SZ, P, VP]),
     ("rh_combine_aggregates_async", C.c_int, [P, SZ, SZ, P, VP]),
     ("rh_lift_host", C.c_int, [C.c_int, C.POINTER(Schema), C.POINTER(Columns), SZ, U8P]),
+    ("rh_host_alloc", C.c_int, [SZ, C.POINTER(C.c_void_p)]),
+    ("rh_host_free", C.c_int, [C.c_void_p]),
     ("rh_fp_add", None, [U64P, U64P, U64P]),
     ("rh_fp_sub", None, [U64P, U64P, U64P]),
     ("rh_store_create", C.c_int, [C.c_int, C.POINTER(Schema), C.POINTER(C.c_void_p)]),

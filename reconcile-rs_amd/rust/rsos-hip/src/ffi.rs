@@ -91,6 +91,8 @@ extern "C" {
     pub fn rh_combine_aggregates_async(dev_in: *const rh_aggregate, parts: usize, r: usize, dev_out: *mut rh_aggregate,
                                        stream: *mut c_void) -> c_int;
     pub fn rh_lift_host(device: c_int, schema: *const rh_schema, cols: *const rh_columns, n: usize, fps: *mut u8) -> c_int;
+    pub fn rh_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
+    pub fn rh_host_free(p: *mut c_void) -> c_int;
     pub fn rh_fp_add(a: *const u64, b: *const u64, out: *mut u64);
     pub fn rh_fp_sub(a: *const u64, b: *const u64, out: *mut u64);
     pub fn rh_store_create(device: c_int, schema: *const rh_schema, out: *mut *mut rh_store) -> c_int;

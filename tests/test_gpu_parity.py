@@ -328,18 +328,30 @@ def test_store_apply_insert_overwrite_delete(gpu, oracle_lib):
     st.close()
 
 
-def test_lift_host_end_to_end(gpu, oracle_lib):
+@pytest.mark.parametrize("value,n,pinned", [("bytes64", 4000, False), ("bytes1024", 500_000, True)])
+def test_lift_host_end_to_end(gpu, oracle_lib, value, n, pinned):
+    """rh_lift_host: one chunk from pageable buffers, and (1 KiB values: ~126 k records per
+    chunk) four chunks through the three-deep pipeline into a pinned rh_host_alloc buffer."""
     import ctypes as C
     from rsos_hip import RecordSchema, _abi as A
     from rsos_hip.synth import make_records, to_host
-    s = RecordSchema.dated("bytes16", "bytes64")
-    h = to_host(make_records(s, 4000, seed=21, tombstone_fraction=0.1))
+    s = RecordSchema.dated("bytes16", value)
+    h = to_host(make_records(s, n, seed=21, tombstone_fraction=0.1))
     cols = A.Columns(*[None if h.get(k) is None else h[k].ctypes.data for k in
                        ("keys", "phys", "logical", "node", "tags", "values")])
-    out = np.zeros((4000, 32), np.uint8)
     sc = s.c()
-    A.check(A.lib().rh_lift_host(0, C.byref(sc), C.byref(cols), 4000, out.ctypes.data), "rh_lift_host")
-    assert np.array_equal(out, oracle_records(oracle_lib, s, h).lift(threads=8))
+    ptr = C.c_void_p()
+    if pinned:
+        A.check(A.lib().rh_host_alloc(n * 32, C.byref(ptr)), "rh_host_alloc")
+        out = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(n, 32))
+    else:
+        out = np.zeros((n, 32), np.uint8)
+    try:
+        A.check(A.lib().rh_lift_host(0, C.byref(sc), C.byref(cols), n, out.ctypes.data), "rh_lift_host")
+        assert np.array_equal(out, oracle_records(oracle_lib, s, h).lift(threads=16))
+    finally:
+        if pinned:
+            A.check(A.lib().rh_host_free(ptr), "rh_host_free")
 
 
 # ---- full size: size-independent properties ------------------------------------------------------

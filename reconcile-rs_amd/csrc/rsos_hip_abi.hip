@@ -567,17 +567,25 @@ struct rh_store {
         dtotal = 0;
         nb = 0;
         memset(root_d, 0, sizeof root_d);
+        // the lift writes the block sums as it goes; they stand unless the keys turn out to be
+        // unsorted (then the rows are re-ordered and everything is re-summed)
+        if ((rc = bsums.ensure(rh_num_blocks(m) * 32 + 32))) return rc;
         if (m) {
             RH_HIP(hipMemcpyAsync(bkeys[cb].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
-            if ((rc = lift_dispatch(schema, c, m, bfps[cb].p, nullptr, nullptr, nullptr, false, stream))) return rc;
+            if ((rc = lift_dispatch(schema, c, m, bfps[cb].p, bsums.p, nullptr, nullptr, false, stream))) return rc;
             RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
             RH_HIP(kops->check_sorted(bkeys[cb].p, m, flag.p, stream));
         }
+        nb = m;
+        if ((rc = resum_base(true))) return rc;
         uint32_t bad = 0;
         if (m) RH_HIP(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
+        if (!bad) return RH_OK;
+        nb = 0;  // an error below leaves the store empty
+        memset(root_b, 0, sizeof root_b);
         uint64_t kept = m;
-        if (bad) {
+        {
             if (!last_wins) return fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
             const int nxt = 1 - cb;
             if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)))

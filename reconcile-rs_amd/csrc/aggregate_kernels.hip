@@ -34,61 +34,144 @@ __device__ __forceinline__ void load_block_bytes(const uint8_t *base, uint64_t a
     }
 }
 
+// Records of one chunk (<= 1,024 B) -- every K / V pair of ordinary size -- go through a
+// lane-refill loop: a wave owns ENC_PER_WAVE consecutive records, every iteration compresses
+// one block for each lane, and a lane whose record is done takes the next unclaimed record of
+// the wave's range (ballot + lane rank).  Lanes stay busy whatever the mix of record lengths,
+// where one record per lane would leave a wave running its longest record's block count.
+// Longer records are left to k_lift_encoded_long.
+constexpr int ENC_PER_WAVE = 64 * 8;
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// 16 message words of the block at byte `addr` with `blen` valid bytes (bytes past blen are
+// zero): 4 x 16-byte + 1 dword loads from the dword-aligned address, then a funnel shift
+__device__ __forceinline__ void load_block_fast(const uint8_t *base, uint64_t addr, uint32_t blen, bool partial,
+                                                uint32_t m[16]) {
+    const uint64_t a4 = addr & ~3ull;
+    const uint32_t sh = (uint32_t)(addr & 3) * 8u;
+    uint32_t d[17];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const u32x4_a4 v = *reinterpret_cast<const u32x4_a4 *>(base + a4 + 16 * q);
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+    d[16] = *reinterpret_cast<const uint32_t *>(base + a4 + 64);
+#pragma unroll
+    for (int j = 0; j < 16; j++) m[j] = __builtin_amdgcn_alignbit(d[j + 1], d[j], sh);
+    if (partial) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int valid = (int)blen - 4 * j;
+            const uint32_t mask = valid >= 4 ? 0xFFFFFFFFu : valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u);
+            m[j] &= mask;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_lift_encoded_short(const uint8_t *bytes, const uint64_t *offs, uint64_t n,
+                                                            uint64_t limit, uint8_t *fps) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint64_t w0 = wave * ENC_PER_WAVE;
+    if (w0 >= n) return;  // uniform per wave
+    const uint64_t w1 = w0 + ENC_PER_WAVE < n ? w0 + ENC_PER_WAVE : n;
+    uint64_t next = w0;  // first unclaimed record of the wave's range (same in every lane)
+    uint64_t i = 0, start = 0, len = 0;
+    uint32_t b = 0, nb = 0, cv[8];
+    bool active = false;
+    for (;;) {
+        // lanes without a record claim the next ones, in order; a multi-chunk record is skipped
+        // (k_lift_encoded_long hashes it) and the lane claims again
+        bool need = !active;
+        for (;;) {
+            const uint64_t mask = __ballot(need && next < w1);
+            if (!mask) break;
+            const uint64_t cand = next + lanes_below(mask);
+            next += (uint64_t)__popcll(mask);
+            if (need && cand < w1) {
+                const uint64_t s0 = offs[cand], l0 = offs[cand + 1] - s0;
+                if (l0 <= (uint64_t)CHUNK_LEN) {
+                    i = cand;
+                    start = s0;
+                    len = l0;
+                    b = 0;
+                    nb = l0 == 0 ? 1u : (uint32_t)((l0 + 63) / 64);
+                    cv_iv(cv);
+                    active = true;
+                    need = false;
+                }
+            } else {
+                need = false;
+            }
+        }
+        if (!__ballot(active)) break;
+        if (active) {
+            const uint64_t boff = 64ull * b;
+            const uint32_t blen = (uint32_t)(len - boff < 64 ? len - boff : 64);
+            uint32_t m[16];
+            if (start + boff + 68 <= limit) load_block_fast(bytes, start + boff, blen, blen < 64, m);
+            else load_block_bytes(bytes, start + boff, blen, limit, m);  // the buffer's last bytes
+            const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | ROOT) : 0u);
+            compress(cv, m, 0u, 0u, blen, flags);
+            if (++b == nb) {
+                store_fp(fps, i, cv);
+                active = false;
+            }
+        }
+    }
+}
+
+// records longer than one chunk: chunk CVs on a stack, parent nodes (one record per lane;
+// shorter records return at once)
 constexpr int ENC_STACK = 40;
 
-__global__ __launch_bounds__(256) void k_lift_encoded(const uint8_t *bytes, const uint64_t *offs,
-                                                      uint64_t n, uint64_t limit, uint8_t *fps,
-                                                      uint8_t *bsums) {
-    __shared__ SumTile tile;
+__global__ __launch_bounds__(256) void k_lift_encoded_long(const uint8_t *bytes, const uint64_t *offs,
+                                                           uint64_t n, uint64_t limit, uint8_t *fps) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (i < n) {
-        const uint64_t start = offs[i];
-        const uint64_t len = offs[i + 1] - start;
-        const uint64_t nchunks = len == 0 ? 1 : (len + CHUNK_LEN - 1) / CHUNK_LEN;
-        uint32_t stk[ENC_STACK][8];
-        int sp = 0;
-        uint32_t cv[8];
-        for (uint64_t c = 0; c < nchunks; c++) {
-            const uint64_t cbeg = c * CHUNK_LEN;
-            const uint64_t clen = len - cbeg < (uint64_t)CHUNK_LEN ? len - cbeg : (uint64_t)CHUNK_LEN;
-            const uint32_t nb = clen == 0 ? 1u : (uint32_t)((clen + 63) / 64);
-            cv_iv(cv);
-            for (uint32_t b = 0; b < nb; b++) {
-                const uint64_t boff = cbeg + 64ull * b;
-                const uint32_t blen = (uint32_t)(len - boff < 64 ? len - boff : 64);
-                uint32_t m[16];
-                load_block_bytes(bytes, start + boff, blen, limit, m);
-                uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b == nb - 1 ? CHUNK_END : 0u);
-                if (nchunks == 1 && b == nb - 1) flags |= ROOT;
-                compress(cv, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
-            }
-            if (c + 1 < nchunks) {
-                uint64_t total = c + 1;
-                while ((total & 1) == 0) {
-                    sp--;
-                    uint32_t p[8];
-                    parent(p, stk[sp], cv, 0u);
-                    for (int q = 0; q < 8; q++) cv[q] = p[q];
-                    total >>= 1;
-                }
-                for (int q = 0; q < 8; q++) stk[sp][q] = cv[q];
-                sp++;
-            }
+    if (i >= n) return;
+    const uint64_t start = offs[i];
+    const uint64_t len = offs[i + 1] - start;
+    if (len <= (uint64_t)CHUNK_LEN) return;
+    const uint64_t nchunks = (len + CHUNK_LEN - 1) / CHUNK_LEN;
+    uint32_t stk[ENC_STACK][8];
+    int sp = 0;
+    uint32_t cv[8];
+    for (uint64_t c = 0; c < nchunks; c++) {
+        const uint64_t cbeg = c * CHUNK_LEN;
+        const uint64_t clen = len - cbeg < (uint64_t)CHUNK_LEN ? len - cbeg : (uint64_t)CHUNK_LEN;
+        const uint32_t nb = (uint32_t)((clen + 63) / 64);
+        cv_iv(cv);
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint64_t boff = cbeg + 64ull * b;
+            const uint32_t blen = (uint32_t)(len - boff < 64 ? len - boff : 64);
+            uint32_t m[16];
+            load_block_bytes(bytes, start + boff, blen, limit, m);
+            const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b == nb - 1 ? CHUNK_END : 0u);
+            compress(cv, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
         }
-        for (int s = sp - 1; s >= 0; s--) {
-            uint32_t p[8];
-            parent(p, stk[s], cv, s == 0 ? ROOT : 0u);
-            for (int q = 0; q < 8; q++) cv[q] = p[q];
+        if (c + 1 < nchunks) {
+            uint64_t total = c + 1;
+            while ((total & 1) == 0) {
+                sp--;
+                uint32_t p[8];
+                parent(p, stk[sp], cv, 0u);
+                for (int q = 0; q < 8; q++) cv[q] = p[q];
+                total >>= 1;
+            }
+            for (int q = 0; q < 8; q++) stk[sp][q] = cv[q];
+            sp++;
         }
-        for (int q = 0; q < 8; q++) h[q] = cv[q];
-        store_fp(fps, i, h);
     }
-    if (bsums) {
-        uint32_t f[8];
-        block_sum_fps256(h, tile, f);
-        if (threadIdx.x == 0) store_sum(bsums, blockIdx.x, f);
+    for (int s = sp - 1; s >= 0; s--) {
+        uint32_t p[8];
+        parent(p, stk[s], cv, s == 0 ? ROOT : 0u);
+        for (int q = 0; q < 8; q++) cv[q] = p[q];
     }
+    store_fp(fps, i, cv);
 }
 
 // ---- reductions ------------------------------------------------------------------------------
@@ -210,8 +293,12 @@ __global__ void k_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64
 hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint64_t n, uint64_t limit,
                                uint8_t *fps, uint8_t *bsums, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    const uint64_t g = (n + 255) / 256;
-    hipLaunchKernelGGL(k_lift_encoded, dim3((uint32_t)g), dim3(256), 0, st, bytes, offs, n, limit, fps, bsums);
+    const uint64_t waves = (n + ENC_PER_WAVE - 1) / ENC_PER_WAVE;
+    hipLaunchKernelGGL(k_lift_encoded_short, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, st, bytes, offs, n,
+                       limit, fps);
+    hipLaunchKernelGGL(k_lift_encoded_long, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, bytes, offs, n, limit,
+                       fps);
+    if (bsums) hipLaunchKernelGGL(k_reduce, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, fps, 32u, n, bsums);
     return hipGetLastError();
 }
 

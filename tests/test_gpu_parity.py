@@ -180,6 +180,28 @@ def test_encoded_random_ragged(gpu, oracle_lib):
     assert np.array_equal(fps.cpu().numpy(), want)
 
 
+def test_encoded_short_mix(gpu, oracle_lib):
+    """Mostly one-chunk records (the lane-refill kernel) with a few multi-chunk ones scattered
+    in (left to the long kernel), over many waves; the last record ends at the buffer's end."""
+    import torch
+    from rsos_hip import lift_encoded
+    rng = np.random.default_rng(11)
+    n = 20_011
+    lens = rng.integers(0, 200, n)
+    lens[rng.integers(0, n, 40)] = rng.integers(1025, 4000, 40)
+    lens[rng.integers(0, n, 40)] = 1024
+    lens[-1] = 67
+    blobs = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in lens]
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    data = torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).cuda()
+    fps, bs = lift_encoded(data, torch.from_numpy(offs).cuda())
+    want = oracle_lib.lift_encoded(blobs, threads=8)
+    assert np.array_equal(fps.cpu().numpy(), want)
+    tot = sum(int.from_bytes(f.tobytes(), "little") for f in want[:256]) % (1 << 256)
+    assert int.from_bytes(bs.cpu().numpy()[0].tobytes(), "little") == tot
+
+
 def test_empty_batches(gpu):
     import torch
     from rsos_hip import RecordSchema, lift_records, range_aggregates

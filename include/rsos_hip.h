@@ -201,6 +201,26 @@ int rh_store_select(rh_store *store, uint64_t r, void *key_out);
 int rh_store_keys(rh_store *store, uint64_t lo, uint64_t hi, void *host_out);
 int rh_store_fingerprints(rh_store *store, uint64_t lo, uint64_t hi, uint8_t *host_out);
 
+/* ---- rbsr protocol round, batched ---------------------------------------------------------
+ * protocol_round_with_policy (rbsr/src/protocol.rs:212-317) asks its RsosView, for every active
+ * segment, aggregate(start..end) and the ranks of both bounds (BoundedRange::parse,
+ * rbsr/src/protocol/rank.rs), and for every SPLIT child select(cut) and aggregate(child).  These
+ * two calls answer one round's questions in two device round trips, against one state of the
+ * store (the one-snapshot-per-round law, rsos_view.rs:36); the policy (any RefinementPolicy)
+ * and the round's bookkeeping stay with the host driver.
+ * resolve: r segments in the wire codec's form -- start kind 0 = Unbounded, 1 = Included(key);
+ * end kind 0 = Unbounded, 1 = Excluded(key); keys r * key_len bytes (rows of unbounded sides
+ * are ignored).  Out: raw_start = Unbounded ? 0 : rank(start), raw_end = Unbounded ? size :
+ * rank(end), and the local aggregate over the key range (ZERO for an inverted segment,
+ * raw_end < raw_start, which the driver drops).
+ * split: m select() ranks (each < size, RH_ERR_ARG otherwise) -> m keys (m * key_len bytes),
+ * and q rank ranges [lo, hi) -> q aggregates.                                                */
+int rh_store_resolve_segments(rh_store *store, size_t r, const uint8_t *start_kinds, const void *start_keys,
+                              const uint8_t *end_kinds, const void *end_keys, uint64_t *raw_start,
+                              uint64_t *raw_end, rh_aggregate *local);
+int rh_store_split_segments(rh_store *store, size_t m, const uint64_t *select_ranks, void *keys_out, size_t q,
+                            const uint64_t *lo, const uint64_t *hi, rh_aggregate *out);
+
 /* Batched insert / overwrite / delete (FingerprintTreeMap::insert / remove, mutate.rs:23-154).
  * ops[i]: 0 = insert-or-overwrite record i, 1 = delete key i (its value columns are ignored).
  * Keys within one batch must be distinct (RH_ERR_ARG, store unchanged).  On return every

@@ -589,6 +589,25 @@ size_t or_ftm_rank(const or_ftm *t, const uint8_t *key) {
     return index + idx;
 }
 
+/* select(index): the index-th key (query.rs:142-161).  Returns the record row holding it, or
+ * (size_t)-1 when index >= len (the reference panics). */
+size_t or_ftm_select(const or_ftm *t, size_t index) {
+    const ftm_node *n = t->root;
+    if (index >= n->subtree.size) return (size_t)-1;
+    while (!n->leaf) {
+        const ftm_node *next = n->child[n->nkeys];
+        for (uint32_t i = 0; i < n->nkeys; i++) {
+            const size_t sub = n->child[i]->subtree.size;
+            if (index < sub) { next = n->child[i]; break; }
+            index -= sub;
+            if (index == 0) return n->rec[i];
+            index -= 1;
+        }
+        n = next;
+    }
+    return n->rec[index];
+}
+
 static int check_aux(const ftm_node *n) {
     if (!n->leaf)
         for (uint32_t i = 0; i <= n->nkeys; i++)

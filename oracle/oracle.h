@@ -105,6 +105,8 @@ void    or_ftm_root(const or_ftm *t, or_aggregate *out);
 void    or_ftm_aggregate(const or_ftm *t, const uint8_t *lo_key, const uint8_t *hi_key,
                          or_aggregate *out);
 size_t  or_ftm_rank(const or_ftm *t, const uint8_t *key);
+/* select(index) -> the record row holding the index-th key; (size_t)-1 if index >= len */
+size_t  or_ftm_select(const or_ftm *t, size_t index);
 /* 0 on success; -1 if the per-node cached aggregates disagree with a recomputation */
 int     or_ftm_check(const or_ftm *t);
 

@@ -66,6 +66,8 @@ def lib() -> C.CDLL:
         L.or_ftm_aggregate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(Aggregate)]
         L.or_ftm_rank.argtypes = [C.c_void_p, C.c_void_p]
         L.or_ftm_rank.restype = C.c_size_t
+        L.or_ftm_select.argtypes = [C.c_void_p, C.c_size_t]
+        L.or_ftm_select.restype = C.c_size_t
         L.or_ftm_check.argtypes = [C.c_void_p]
         L.or_ftm_check.restype = C.c_int
         _lib = L
@@ -167,6 +169,13 @@ class FingerprintTreeMap:
 
     def rank(self, key: bytes) -> int:
         return int(lib().or_ftm_rank(self._h, C.create_string_buffer(key, len(key))))
+
+    def select(self, index: int) -> int:
+        """The record row holding the index-th key (query.rs:142-161); IndexError past the end."""
+        row = int(lib().or_ftm_select(self._h, index))
+        if row == (1 << 64) - 1:
+            raise IndexError("select: index >= len")
+        return row
 
     def check(self) -> bool:
         return lib().or_ftm_check(self._h) == 0

@@ -484,6 +484,8 @@ struct rh_store {
     DevBuf<rh_aggregate> q_out, q_bout, q_dout;
     DevBuf<uint8_t> q_keys;
     DevBuf<uint32_t> q_rank, q_drank;
+    DevBuf<uint8_t> q_kind;  // protocol round: the segments' bound kinds
+    std::vector<uint8_t> h_keys;  // protocol round: interleaved start / end keys
     DevBuf<uint8_t> snap;  // a host snapshot's bytes while it is decoded
     rh::Scratch scratch;
 
@@ -773,6 +775,58 @@ struct rh_store {
         RH_HIP(hipMemcpyAsync(out, q_merged.p, m * 8, hipMemcpyDeviceToHost, stream));
         return sync();
     }
+    // rbsr protocol round, step 1 (protocol.rs:225-255): every segment's local aggregate and
+    // raw rank bounds, against the compacted base run (select needs rank order anyway).
+    int resolve(size_t r, const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys,
+                uint64_t *raw_lo, uint64_t *raw_hi, rh_aggregate *out) {
+        int rc;
+        if ((rc = compact())) return rc;
+        if ((rc = q_keys.ensure(2 * r * kl + 64)) || (rc = q_rank.ensure(2 * r)) || (rc = q_lo.ensure(r)) ||
+            (rc = q_hi.ensure(r)) || (rc = q_out.ensure(r)) || (rc = q_kind.ensure(2 * r + 64)))
+            return rc;
+        h_keys.assign(2 * r * kl, 0);
+        for (size_t j = 0; j < r; j++) {  // row 2j: start key, 2j + 1: end key (unbounded: zeros)
+            if (sk[j]) memcpy(&h_keys[2 * j * kl], skeys + j * kl, kl);
+            if (ek[j]) memcpy(&h_keys[(2 * j + 1) * kl], ekeys + j * kl, kl);
+        }
+        RH_HIP(hipMemcpyAsync(q_keys.p, h_keys.data(), 2 * r * kl, hipMemcpyHostToDevice, stream));
+        RH_HIP(hipMemcpyAsync(q_kind.p, sk, r, hipMemcpyHostToDevice, stream));
+        RH_HIP(hipMemcpyAsync(q_kind.p + r, ek, r, hipMemcpyHostToDevice, stream));
+        if (nb) RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_keys.p, 2 * r, q_rank.p, nullptr, stream));
+        else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
+        RH_HIP(rh::launch_resolve_bounds(q_rank.p, q_kind.p, q_kind.p + r, r, nb, q_lo.p, q_hi.p, stream));
+        // an inverted segment (hi < lo) is clamped to the empty range: ZERO
+        RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, r,
+                                      reinterpret_cast<uint64_t *>(q_out.p), stream));
+        RH_HIP(hipMemcpyAsync(raw_lo, q_lo.p, r * 8, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(raw_hi, q_hi.p, r * 8, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(out, q_out.p, r * sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
+        return sync();
+    }
+    // step 2 (protocol.rs:288-313): the select() cuts of every SPLIT and the children's aggregates
+    int split(size_t m, const uint64_t *sel, uint8_t *keys_out, size_t q, const uint64_t *lo, const uint64_t *hi,
+              rh_aggregate *out) {
+        int rc;
+        if ((rc = compact())) return rc;
+        for (size_t i = 0; i < m; i++)
+            if (sel[i] >= nb) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+        if ((rc = q_merged.ensure(m + 1)) || (rc = q_keys.ensure(m * kl + 64)) || (rc = q_lo.ensure(q + 1)) ||
+            (rc = q_hi.ensure(q + 1)) || (rc = q_out.ensure(q + 1)))
+            return rc;
+        if (m) {
+            RH_HIP(hipMemcpyAsync(q_merged.p, sel, m * 8, hipMemcpyHostToDevice, stream));
+            RH_HIP(rh::launch_gather_keys(bkeys[cb].p, (uint32_t)kl, q_merged.p, m, q_keys.p, stream));
+            RH_HIP(hipMemcpyAsync(keys_out, q_keys.p, m * kl, hipMemcpyDeviceToHost, stream));
+        }
+        if (q) {
+            RH_HIP(hipMemcpyAsync(q_lo.p, lo, q * 8, hipMemcpyHostToDevice, stream));
+            RH_HIP(hipMemcpyAsync(q_hi.p, hi, q * 8, hipMemcpyHostToDevice, stream));
+            RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, q,
+                                          reinterpret_cast<uint64_t *>(q_out.p), stream));
+            RH_HIP(hipMemcpyAsync(out, q_out.p, q * sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
+        }
+        return sync();
+    }
     void release() {
         (void)hipStreamSynchronize(stream);
         for (int k = 0; k < 2; k++) {
@@ -788,6 +842,7 @@ struct rh_store {
         results.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
+        q_kind.release();
         snap.release();
         scratch.release();
         if (dep) (void)hipEventDestroy(dep);
@@ -903,6 +958,31 @@ int rh_store_aggregate_keys(rh_store *s, int lo_kind, const void *lo_key, int hi
     if ((lo_kind && !lo_key) || (hi_kind && !hi_key)) return fail(RH_ERR_ARG, "bound key is NULL");
     RH_LOCK(s);
     return s->aggregate_keys(lo_kind, lo_key, hi_kind, hi_key, out);
+}
+
+int rh_store_resolve_segments(rh_store *s, size_t r, const uint8_t *start_kinds, const void *start_keys,
+                              const uint8_t *end_kinds, const void *end_keys, uint64_t *raw_start,
+                              uint64_t *raw_end, rh_aggregate *local) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    if (r == 0) return RH_OK;
+    if (!start_kinds || !end_kinds || !raw_start || !raw_end || !local) return fail(RH_ERR_ARG, "NULL buffer");
+    for (size_t j = 0; j < r; j++) {
+        if (start_kinds[j] > 1 || end_kinds[j] > 1)
+            return fail(RH_ERR_ARG, "segment bound kind must be 0 (Unbounded) or 1 (Included / Excluded)");
+        if ((start_kinds[j] && !start_keys) || (end_kinds[j] && !end_keys)) return fail(RH_ERR_ARG, "bound key is NULL");
+    }
+    RH_LOCK(s);
+    return s->resolve(r, start_kinds, static_cast<const uint8_t *>(start_keys), end_kinds,
+                      static_cast<const uint8_t *>(end_keys), raw_start, raw_end, local);
+}
+
+int rh_store_split_segments(rh_store *s, size_t m, const uint64_t *select_ranks, void *keys_out, size_t q,
+                            const uint64_t *lo, const uint64_t *hi, rh_aggregate *out) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    if ((m && (!select_ranks || !keys_out)) || (q && (!lo || !hi || !out))) return fail(RH_ERR_ARG, "NULL buffer");
+    if (m == 0 && q == 0) return RH_OK;
+    RH_LOCK(s);
+    return s->split(m, select_ranks, static_cast<uint8_t *>(keys_out), q, lo, hi, out);
 }
 
 int rh_store_fingerprints(rh_store *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {

@@ -634,6 +634,28 @@ __global__ void k_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, Cnt
     out[j] = (uint64_t)((int64_t)rank_b[j] + (rd ? cnt_through(cp, rd - 1) : 0));
 }
 
+// ---- protocol-round helpers (rbsr/src/protocol.rs:225-317) ------------------------------------
+// A segment's bounds as a rank range of the base run: Unbounded start -> 0, Included(k) ->
+// rank(k); Unbounded end -> n, Excluded(k) -> rank(k) (BoundedRange::parse, protocol/rank.rs).
+// rank[2j] / rank[2j + 1] are the searched ranks of the start / end keys.
+__global__ void k_resolve_bounds(const uint32_t *rank, const uint8_t *skind, const uint8_t *ekind, uint64_t r,
+                                 uint64_t n, uint64_t *lo, uint64_t *hi) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= r) return;
+    lo[j] = skind[j] ? (uint64_t)rank[2 * j] : 0ull;
+    hi[j] = ekind[j] ? (uint64_t)rank[2 * j + 1] : n;
+}
+
+// out[i] = keys[sel[i]]: the select() cuts of every SPLIT in a round, one dword per lane
+__global__ void k_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t words = kl / 4;
+    if (t >= m * words) return;
+    const uint64_t i = t / words, w = t % words;
+    reinterpret_cast<uint32_t *>(out)[i * words + w] =
+        reinterpret_cast<const uint32_t *>(keys + sel[i] * kl)[w];
+}
+
 // ---- run merge: the merged run and its block sums in one pass ----------------------------------
 // Merging a key-sorted batch into a sorted run A (rank / present: each batch key's lower bound
 // in A and whether A holds it; op 0 upsert, 1 drop):
@@ -1042,6 +1064,20 @@ hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
                             const uint64_t *dhi, CntPrefix cp, uint64_t *out, hipStream_t st) {
     hipLaunchKernelGGL(k_agg_merge, dim3(1), dim3(64), 0, st, base_agg, delta_agg, dlo, dhi, cp, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, const uint8_t *ekind, uint64_t r,
+                                 uint64_t n, uint64_t *lo, uint64_t *hi, hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_resolve_bounds, g1(r), dim3(256), 0, st, rank, skind, ekind, r, n, lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out,
+                              hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_keys, g1(m * (kl / 4)), dim3(256), 0, st, keys, kl, sel, m, out);
     return hipGetLastError();
 }
 

@@ -137,6 +137,13 @@ hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg,
 hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, CntPrefix cp, uint64_t m,
                              uint64_t *out, hipStream_t st);
 
+// protocol round: segment bounds -> base-run rank ranges (rank: 2 searched ranks per segment),
+// and the keys at given ranks (kl a multiple of 4)
+hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, const uint8_t *ekind, uint64_t r,
+                                 uint64_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
+hipError_t launch_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out,
+                              hipStream_t st);
+
 // nullptr if the store does not support this key type
 StoreKeyOps *store_key_ops(int key_kind, int key_len);
 

@@ -73,6 +73,8 @@ SIGNATURES = [
     ("rh_store_keys", C.c_int, [P, C.c_uint64, C.c_uint64, VP]),
     ("rh_store_select", C.c_int, [P, C.c_uint64, VP]),
     ("rh_store_fingerprints", C.c_int, [P, C.c_uint64, C.c_uint64, U8P]),
+    ("rh_store_resolve_segments", C.c_int, [P, SZ, U8P, VP, U8P, VP, U64P, U64P, P]),
+    ("rh_store_split_segments", C.c_int, [P, SZ, U64P, VP, SZ, U64P, U64P, P]),
     ("rh_store_apply", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rh_store_apply_device", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),

@@ -1,0 +1,211 @@
+"""rbsr's protocol driver over a GpuFingerprintStore: one round in two device round trips.
+
+Host-side mirror of rbsr/src/protocol.rs (names, argument meaning, outputs):
+
+  initial_ranges(local)                                   protocol.rs:97-102
+  protocol_round(local, active, children, enumerations)   protocol.rs:161-178 (FixedFanOut 16)
+  protocol_round_with_policy(local, policy, ...)          protocol.rs:212-317
+  RoundOutcome                                            protocol.rs:135-142, protocol/outcome.rs
+  Comparison, FixedFanOut, SqrtFanOut, FanOut,
+  SplitStride rules                                       rbsr/src/policy/{comparison,cutoffs,
+                                                          fixed_fan_out,sqrt_fan_out,params}.rs
+
+The reference walks the active segments one by one and asks its RsosView four questions per
+segment and two per SPLIT child, each an O(log n) tree walk.  Against an HBM-resident store each
+question would be a device round trip, so the round is answered in two batched calls instead:
+
+  1. rh_store_resolve_segments: for every segment, the raw ranks of both bounds and the local
+     aggregate over its key range (BoundedRange::parse and `local.aggregate(..)`, :225-255);
+  2. the policy decides every segment on the host, in segment order (Comparison carries the
+     children emitted so far, which the cut arithmetic gives without any key);
+     rh_store_split_segments then returns the keys at every SPLIT cut (`select`, :305) and the
+     aggregate of every child that is not the parent itself (:297-307).
+
+Both calls see one state of the store (rsos_view.rs:36).  The outputs are appended in the
+reference's order: child_ranges (SPLIT children, bounced IDLIST parents) and enumeration_ranges
+(IDLIST), segment by segment.  A segment is a RangeAggregate (start None = Unbounded, else
+Included(start); end None = Unbounded, else Excluded(end)); an enumeration range is a
+(start, end) pair in the same convention.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from .fingerprint import Aggregate
+from .wire import RangeAggregate
+
+Key = Union[bytes, int]
+EnumerationRange = Tuple[Optional[Key], Optional[Key]]
+
+SKIP = "skip"
+ENUMERATE = "enumerate"
+
+
+@dataclass(frozen=True)
+class Split:
+    """Decision::Split(SplitStride): elements per child range, never zero (params.rs:52-60)."""
+    stride: int
+
+    def __post_init__(self):
+        if self.stride <= 0:
+            object.__setattr__(self, "stride", 1)
+
+
+@dataclass(frozen=True)
+class Comparison:
+    """policy/comparison.rs: the local and remote aggregates of one segment."""
+    local: Aggregate
+    remote: Aggregate
+    children_emitted: int = 0
+
+    def span(self) -> int:
+        return self.local.size
+
+    def remote_size(self) -> int:
+        return self.remote.size
+
+    def agrees(self) -> bool:
+        return self.local == self.remote
+
+
+def shared_cutoffs(c: Comparison):
+    """policy/cutoffs.rs: the outcomes every shipped policy shares."""
+    local, remote = c.span(), c.remote_size()
+    if c.agrees():
+        return SKIP
+    if remote == 0:
+        return ENUMERATE
+    if local == 0:
+        return Split(1)
+    if local == 1 and remote == 1:
+        return ENUMERATE
+    if local == 1:
+        return Split(1)
+    return None
+
+
+def fan_out(b: int) -> int:
+    """FanOut::new: 0 and 1 are raised to 2 (params.rs:82-84)."""
+    return 2 if b < 2 else b
+
+
+class FixedFanOut:
+    """At most `fan_out` children per SPLIT, stride ceil(span / b) (fixed_fan_out.rs)."""
+
+    def __init__(self, b: int = 16):  # FanOut::NEGENTROPY
+        self.fan_out = fan_out(b)
+
+    def decide(self, c: Comparison):
+        d = shared_cutoffs(c)
+        if d is not None:
+            return d
+        return Split(-(-c.span() // self.fan_out))
+
+
+class SqrtFanOut:
+    """Stride floor(sqrt(span)) in f32 arithmetic, as `(span as f32).sqrt() as usize`
+    (sqrt_fan_out.rs)."""
+
+    def decide(self, c: Comparison):
+        d = shared_cutoffs(c)
+        if d is not None:
+            return d
+        return Split(int(np.sqrt(np.float32(c.span()))))
+
+
+DEFAULT_POLICY = FixedFanOut(16)
+
+
+@dataclass
+class RoundOutcome:
+    """What one round did (protocol.rs:135-142); `+=` accumulates a whole reconciliation."""
+    skipped: int = 0
+    enumerated: int = 0
+    split: int = 0
+    children: int = 0
+    dropped_malformed: int = 0
+
+    def __iadd__(self, o: "RoundOutcome") -> "RoundOutcome":
+        self.skipped += o.skipped
+        self.enumerated += o.enumerated
+        self.split += o.split
+        self.children += o.children
+        self.dropped_malformed += o.dropped_malformed
+        return self
+
+
+def initial_ranges(local) -> List[RangeAggregate]:
+    """{(-inf, +inf), A(whole store)}: the cached root, O(1) (protocol.rs:97-102)."""
+    return [RangeAggregate(None, None, local.aggregate())]
+
+
+def protocol_round(local, active: Sequence[RangeAggregate], child_ranges: List[RangeAggregate],
+                   enumeration_ranges: List[EnumerationRange]) -> RoundOutcome:
+    return protocol_round_with_policy(local, DEFAULT_POLICY, active, child_ranges, enumeration_ranges)
+
+
+def protocol_round_with_policy(local, policy, active: Sequence[RangeAggregate],
+                               child_ranges: List[RangeAggregate],
+                               enumeration_ranges: List[EnumerationRange]) -> RoundOutcome:
+    outcome = RoundOutcome()
+    if not active:
+        return outcome
+    raw_lo, raw_hi, locals_ = local.resolve_segments(active)       # round trip 1
+    size = local.size()
+    # decide every segment in order; SPLIT children are planned as rank ranges
+    plan = []        # (kind, segment, payload) in segment order
+    sel: List[int] = []          # select() ranks of every cut
+    agg_lo: List[int] = []       # child rank ranges whose aggregate is needed
+    agg_hi: List[int] = []
+    for seg, rl, rh, la in zip(active, raw_lo.tolist(), raw_hi.tolist(), locals_):
+        if rh < rl:  # inverted: covers no keys (protocol.rs:232-245)
+            outcome.dropped_malformed += 1
+            continue
+        start_index, end_index = min(rl, size), min(rh, size)   # StoreSize::admit
+        comparison = Comparison(la, seg.aggregate, outcome.children)
+        span = comparison.span()
+        decision = policy.decide(comparison)
+        if isinstance(decision, Split) and span > 1 and decision.stride >= span:
+            decision = ENUMERATE  # a non-progressing SPLIT becomes an IDLIST (:263-272)
+        if decision == SKIP:
+            outcome.skipped += 1
+        elif decision == ENUMERATE:
+            outcome.enumerated += 1
+            bounce = seg.aggregate.size != 0
+            if bounce:
+                outcome.children += 1
+            plan.append((ENUMERATE, seg, bounce))
+        else:
+            outcome.split += 1
+            stride = decision.stride
+            cuts = list(range(start_index + stride, end_index, stride)) if stride else []
+            first_sel = len(sel)
+            sel.extend(cuts)
+            bounds = [start_index] + cuts + [end_index]
+            first_agg = len(agg_lo)
+            if cuts:  # an uncut child is the parent: its aggregate is already in hand (:292-296)
+                agg_lo.extend(bounds[:-1])
+                agg_hi.extend(bounds[1:])
+            outcome.children += len(cuts) + 1
+            plan.append(("split", seg, (first_sel, len(cuts), first_agg, la)))
+    keys, aggs = local.split_segments(sel, agg_lo, agg_hi) if (sel or agg_lo) else ([], [])  # round trip 2
+    for kind, seg, p in plan:
+        if kind == ENUMERATE:
+            if p:
+                child_ranges.append(RangeAggregate(seg.start, seg.end, Aggregate.ZERO))
+            enumeration_ranges.append((seg.start, seg.end))
+            continue
+        first_sel, ncuts, first_agg, la = p
+        if ncuts == 0:
+            child_ranges.append(RangeAggregate(seg.start, seg.end, la))
+            continue
+        cur = seg.start
+        for k in range(ncuts):
+            nxt = keys[first_sel + k]
+            child_ranges.append(RangeAggregate(cur, nxt, aggs[first_agg + k]))
+            cur = nxt
+        child_ranges.append(RangeAggregate(cur, seg.end, aggs[first_agg + ncuts]))
+    return outcome

@@ -215,6 +215,42 @@ class GpuFingerprintStore:
                 "rh_store_fingerprints")
         return out
 
+    # ---- rbsr protocol round, batched (rh_store_resolve_segments / rh_store_split_segments) ----
+    def resolve_segments(self, segments: Sequence) -> Tuple[np.ndarray, np.ndarray, list]:
+        """For r segments (objects with .start / .end: None = Unbounded, else Included(start) /
+        Excluded(end)): raw start / end ranks (Unbounded -> 0 / size) and the local aggregate
+        over each key range (ZERO if inverted), in one device round trip."""
+        r, kl = len(segments), self.schema.key_row
+        sk, ek = np.zeros(max(r, 1), np.uint8), np.zeros(max(r, 1), np.uint8)
+        skeys, ekeys = np.zeros((max(r, 1), kl), np.uint8), np.zeros((max(r, 1), kl), np.uint8)
+        for j, seg in enumerate(segments):
+            if seg.start is not None:
+                sk[j] = 1
+                skeys[j] = np.frombuffer(self._key_bytes(seg.start), np.uint8)
+            if seg.end is not None:
+                ek[j] = 1
+                ekeys[j] = np.frombuffer(self._key_bytes(seg.end), np.uint8)
+        lo, hi = np.zeros(max(r, 1), np.uint64), np.zeros(max(r, 1), np.uint64)
+        out = (A.Aggregate * max(r, 1))()
+        A.check(A.lib().rh_store_resolve_segments(self._h, r, _np_ptr(sk), _np_ptr(skeys), _np_ptr(ek),
+                                                  _np_ptr(ekeys), _np_ptr(lo), _np_ptr(hi), out),
+                "rh_store_resolve_segments")
+        return lo[:r], hi[:r], [Aggregate.from_c(out[j]) for j in range(r)]
+
+    def split_segments(self, select_ranks: Sequence[int], lo: Sequence[int], hi: Sequence[int]):
+        """select() at every rank of `select_ranks` and the aggregates of the rank ranges
+        [lo[i], hi[i]), in one device round trip: (keys, aggregates)."""
+        kl = self.schema.key_row
+        sel = np.ascontiguousarray(select_ranks, dtype=np.uint64)
+        lo_a = np.ascontiguousarray(lo, dtype=np.uint64)
+        hi_a = np.ascontiguousarray(hi, dtype=np.uint64)
+        m, q = len(sel), len(lo_a)
+        keys = np.zeros((max(m, 1), kl), np.uint8)
+        out = (A.Aggregate * max(q, 1))()
+        A.check(A.lib().rh_store_split_segments(self._h, m, _np_ptr(sel), _np_ptr(keys), q, _np_ptr(lo_a),
+                                                _np_ptr(hi_a), out), "rh_store_split_segments")
+        return [self._key_out(keys[i].tobytes()) for i in range(m)], [Aggregate.from_c(out[j]) for j in range(q)]
+
     def apply(self, cols: Dict[str, np.ndarray], ops: np.ndarray) -> Tuple[int, int, int]:
         """Batched insert (op 0) / delete (op 1); returns (new, overwritten, deleted)."""
         c, held = self._columns(cols)

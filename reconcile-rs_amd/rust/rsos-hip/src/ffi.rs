@@ -110,6 +110,11 @@ extern "C" {
     pub fn rh_store_select(store: *mut rh_store, r: u64, key_out: *mut c_void) -> c_int;
     pub fn rh_store_keys(store: *mut rh_store, lo: u64, hi: u64, host_out: *mut c_void) -> c_int;
     pub fn rh_store_fingerprints(store: *mut rh_store, lo: u64, hi: u64, host_out: *mut u8) -> c_int;
+    pub fn rh_store_resolve_segments(store: *mut rh_store, r: usize, start_kinds: *const u8,
+                                     start_keys: *const c_void, end_kinds: *const u8, end_keys: *const c_void,
+                                     raw_start: *mut u64, raw_end: *mut u64, local: *mut rh_aggregate) -> c_int;
+    pub fn rh_store_split_segments(store: *mut rh_store, m: usize, select_ranks: *const u64, keys_out: *mut c_void,
+                                   q: usize, lo: *const u64, hi: *const u64, out: *mut rh_aggregate) -> c_int;
     pub fn rh_store_apply(store: *mut rh_store, cols: *const rh_columns, ops: *const u8, n: usize,
                           n_new: *mut u64, n_over: *mut u64, n_del: *mut u64) -> c_int;
     pub fn rh_store_apply_device(store: *mut rh_store, dev_cols: *const rh_columns, dev_ops: *const u8, n: usize,

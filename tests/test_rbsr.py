@@ -1,0 +1,308 @@
+"""rbsr protocol rounds (rbsr/src/protocol.rs:212-317) served by the GPU store.
+
+rsos_hip.rbsr answers a round in two batched store calls; oracle/rbsr.py is the literal,
+one-question-at-a-time restatement over the oracle's FingerprintTreeMap.  The CPU tests pin the
+oracle driver to the reference's own doc examples (protocol.rs:114-133, :190-210) and run the
+product driver's host logic against it through a batched adapter over the same FTM; the GPU
+tests run both drivers through whole two-replica reconciliations and require identical rounds.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import rbsr as OR  # oracle/rbsr.py
+
+
+# ---- helpers ---------------------------------------------------------------------------------
+
+def _u32_recs(pairs):
+    pairs = sorted(pairs)
+    k = np.array([a for a, _ in pairs], np.uint32)
+    v = np.array([b for _, b in pairs], np.uint32)
+    n = len(pairs)
+    return O.Records(O.Schema(O.KEY_U32, 4, O.VAL_U32, 4, O.REC_PLAIN, 0), k.view(np.uint8).reshape(n, 4),
+                     v.view(np.uint8).reshape(n, 4))
+
+
+def _ftm(recs):
+    t = O.FingerprintTreeMap(recs)
+    t.fill(0, recs.n)
+    return t
+
+
+def _agg_t(a):
+    """rsos_hip Aggregate -> the oracle's (fp limbs, size)."""
+    return tuple(int(x) for x in a.fingerprint.limbs), int(a.size)
+
+
+def _norm(children):
+    out = []
+    for c in children:
+        if isinstance(c, tuple):
+            out.append(c)
+        else:
+            out.append((c.start, c.end, _agg_t(c.aggregate)))
+    return out
+
+
+class BatchedFtm:
+    """The two batched questions of rsos_hip.rbsr answered by the oracle FTM (host-logic check)."""
+
+    def __init__(self, view):
+        self.v = view
+
+    def size(self):
+        return self.v.size()
+
+    def aggregate(self):
+        from rsos_hip import Aggregate, Fingerprint
+        fp, size = self.v.aggregate(None, None)
+        return Aggregate(size, Fingerprint(fp))
+
+    def resolve_segments(self, segs):
+        from rsos_hip import Aggregate, Fingerprint
+        n = self.v.size()
+        lo = np.array([0 if s.start is None else self.v.rank(s.start) for s in segs], np.uint64)
+        hi = np.array([n if s.end is None else self.v.rank(s.end) for s in segs], np.uint64)
+        aggs = []
+        for s in segs:
+            fp, size = self.v.aggregate(s.start, s.end)
+            aggs.append(Aggregate(size, Fingerprint(fp)))
+        return lo, hi, aggs
+
+    def split_segments(self, sel, lo, hi):
+        from rsos_hip import Aggregate, Fingerprint
+        keys = [self.v.select(int(r)) for r in sel]
+        aggs = []
+        for a, b in zip(lo, hi):
+            ka = None if a == 0 else self.v.select(int(a))
+            kb = None if b >= self.v.size() else self.v.select(int(b))
+            fp, size = self.v.aggregate(ka, kb)
+            aggs.append(Aggregate(size, Fingerprint(fp)))
+        return keys, aggs
+
+
+def _to_product(segs):
+    from rsos_hip import Aggregate, Fingerprint
+    from rsos_hip.wire import RangeAggregate
+    return [RangeAggregate(s, e, Aggregate(a[1], Fingerprint(tuple(a[0])))) for s, e, a in segs]
+
+
+def reconcile(a, b, round_fn, init, max_rounds=200):
+    """Ping-pong rounds starting from a's root at b; per round: (children, enumerations, outcome)."""
+    active = init(a)
+    sides = [b, a]
+    log, enums = [], {id(a): [], id(b): []}
+    for k in range(max_rounds):
+        if not active:
+            return log, enums[id(a)], enums[id(b)]
+        side = sides[k % 2]
+        children, en = [], []
+        outcome = round_fn(side, active, children, en)
+        log.append((_norm(children), list(en), outcome))
+        enums[id(side)].extend(en)
+        active = children
+    raise AssertionError("reconciliation did not terminate")
+
+
+def _covered(k, ranges, lt):
+    return any((s is None or not lt(k, s)) and (e is None or lt(k, e)) for s, e in ranges)
+
+
+# ---- CPU: the oracle driver against the reference's doc examples -------------------------------
+
+def test_oracle_round_doc_example_three_outcomes(oracle_lib):
+    """protocol.rs:114-133: SKIP, IDLIST and SPLIT in one round against the same responder."""
+    b = OR.FtmView(_ftm(_u32_recs([(i, i) for i in range(40)])), True)
+    empty = OR.FtmView(_ftm(_u32_recs([])), True)
+    c = OR.FtmView(_ftm(_u32_recs([(i + 1000, i) for i in range(40)])), True)
+    active = OR.initial_ranges(b) + OR.initial_ranges(empty) + OR.initial_ranges(c)
+    children, enums = [], []
+    sk, en, sp, ch, dr = OR.protocol_round(b, OR.fixed_fan_out(16), active, children, enums)
+    assert (sk, en, sp, dr) == (1, 1, 1, 0)
+    assert ch == len(children)
+
+
+def test_oracle_round_doc_example_sqrt(oracle_lib):
+    """protocol.rs:190-210: SqrtFanOut cuts a 400-element span into 20 children."""
+    a = OR.FtmView(_ftm(_u32_recs([(i, i) for i in range(400)])), True)
+    b = OR.FtmView(_ftm(_u32_recs([(i, i) for i in range(400)] + [(999, 999)])), True)
+    children, enums = [], []
+    OR.protocol_round(a, OR.sqrt_fan_out, OR.initial_ranges(b), children, enums)
+    assert len(children) == 20 and enums == []
+
+
+def test_policy_params():
+    """params.rs doc examples: ceil(10 / 3) = 4; FanOut 0 / 1 -> 2; a zero stride -> 1."""
+    from rsos_hip.fingerprint import Aggregate, Fingerprint
+    from rsos_hip.rbsr import Comparison, FixedFanOut, Split, fan_out
+    z = Fingerprint((0, 0, 0, 0))
+    c = Comparison(Aggregate(10, Fingerprint((1, 0, 0, 0))), Aggregate(7, z))
+    assert FixedFanOut(3).decide(c) == Split(4)
+    assert fan_out(0) == fan_out(1) == 2
+    assert Split(0).stride == 1
+
+
+def test_batched_driver_host_logic_matches_oracle(oracle_lib):
+    """rsos_hip.rbsr's batched driver, fed by the oracle FTM, reproduces the literal driver's
+    rounds on a u32 reconciliation with one-sided keys, changed values and an empty range."""
+    from rsos_hip import rbsr as R
+    rng = np.random.default_rng(4)
+    keys = rng.choice(2**31, 3000, replace=False)
+    a_pairs = {int(k): int(k) % 977 for k in keys[:2800]}
+    b_pairs = dict(a_pairs)
+    for k in keys[2800:2900]:
+        a_pairs[int(k)] = 1
+    for k in keys[2900:]:
+        b_pairs[int(k)] = 2
+    for k in keys[:40]:
+        b_pairs[int(k)] += 5
+    va = OR.FtmView(_ftm(_u32_recs(a_pairs.items())), True)
+    vb = OR.FtmView(_ftm(_u32_recs(b_pairs.items())), True)
+    for policy, decide in [(R.FixedFanOut(16), OR.fixed_fan_out(16)), (R.SqrtFanOut(), OR.sqrt_fan_out),
+                           (R.FixedFanOut(2), OR.fixed_fan_out(2))]:
+        want = reconcile(va, vb, lambda v, act, ch, en: OR.protocol_round(v, decide, act, ch, en),
+                         OR.initial_ranges)
+        pa, pb = BatchedFtm(va), BatchedFtm(vb)
+
+        def prod(v, act, ch, en):
+            o = R.protocol_round_with_policy(v, policy, _to_product(act) if act and isinstance(act[0], tuple)
+                                             else act, ch, en)
+            return (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed)
+        got = reconcile(pa, pb, prod, R.initial_ranges)
+        assert len(got[0]) == len(want[0])
+        for (gc, ge, go), (wc, we, wo) in zip(got[0], want[0]):
+            assert go == wo and ge == we and gc == wc
+        # soundness: every one-sided key is enumerated by its holder
+        lt = lambda x, y: x < y  # noqa: E731
+        for k in keys[2800:2900]:
+            assert _covered(int(k), want[1], lt)
+        for k in keys[2900:]:
+            assert _covered(int(k), want[2], lt)
+        for k in keys[:40]:
+            assert _covered(int(k), want[1], lt) or _covered(int(k), want[2], lt)
+
+
+def test_oracle_drops_inverted_segment(oracle_lib):
+    a = OR.FtmView(_ftm(_u32_recs([(i, i) for i in range(100)])), True)
+    children, enums = [], []
+    out = OR.protocol_round(a, OR.fixed_fan_out(16), [(50, 10, ((1, 0, 0, 0), 3))], children, enums)
+    assert out == (0, 0, 0, 0, 1) and children == [] and enums == []
+
+
+# ---- GPU: the batched driver on the device store against the literal oracle driver --------------
+
+def _dated_sets(seed, n_common, n_a, n_b, n_mod):
+    rng = np.random.default_rng(seed)
+    tot = n_common + n_a + n_b
+    keys = np.unique(rng.integers(0, 256, (tot + 64, 16), dtype=np.uint8), axis=0)[:tot]
+    rng.shuffle(keys)
+    vals = rng.integers(0, 256, (tot, 64), dtype=np.uint8)
+    phys = (1_700_000_000_000 + np.arange(tot)).astype(np.uint64)
+
+    def cols(idx, bump=()):
+        idx = np.array(sorted(idx, key=lambda i: keys[i].tobytes()))
+        p = phys[idx].copy()
+        for j, i in enumerate(idx):
+            if i in bump:
+                p[j] += 1
+        n = len(idx)
+        return {"keys": keys[idx].copy(), "values": vals[idx].copy(), "phys": p,
+                "logical": np.zeros(n, np.uint32), "node": np.ones(n, np.uint64), "tags": np.zeros(n, np.uint8)}
+    common = list(range(n_common))
+    a_idx = common + list(range(n_common, n_common + n_a))
+    b_idx = common + list(range(n_common + n_a, tot))
+    mod = set(range(n_mod))
+    return keys, cols(a_idx), cols(b_idx, bump=mod), a_idx[n_common:], b_idx[n_common:], sorted(mod)
+
+
+def _gpu_and_oracle(schema, c):
+    from rsos_hip import GpuFingerprintStore
+    st = GpuFingerprintStore(schema)
+    st.load_bulk(c)
+    sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+    recs = O.Records(sc, c["keys"], c["values"], c["phys"], c["logical"], c["node"], c["tags"])
+    return st, OR.FtmView(_ftm(recs), False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["fixed16", "sqrt", "fixed2"])
+def test_gpu_reconciliation_rounds_match_oracle(gpu, oracle_lib, policy):
+    from rsos_hip import RecordSchema, rbsr as R
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(7, 20_000, 60, 45, 30)
+    ga, oa = _gpu_and_oracle(schema, ca)
+    gb, ob = _gpu_and_oracle(schema, cb)
+    pol, decide = {"fixed16": (R.FixedFanOut(16), OR.fixed_fan_out(16)), "sqrt": (R.SqrtFanOut(), OR.sqrt_fan_out),
+                   "fixed2": (R.FixedFanOut(2), OR.fixed_fan_out(2))}[policy]
+    want = reconcile(oa, ob, lambda v, act, ch, en: OR.protocol_round(v, decide, act, ch, en), OR.initial_ranges)
+
+    def prod(st, act, ch, en):
+        o = R.protocol_round_with_policy(st, pol, act, ch, en)
+        return (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed)
+
+    def prod_init(st):
+        return R.initial_ranges(st)
+    got_log, got_ea, got_eb = reconcile(ga, gb, prod, prod_init)
+    assert len(got_log) == len(want[0]) > 2
+    for (gc, ge, go), (wc, we, wo) in zip(got_log, want[0]):
+        assert go == wo
+        assert ge == we
+        assert gc == wc
+    lt = lambda x, y: x < y  # noqa: E731  (memcmp order of [u8; 16])
+    for i in only_a:
+        assert _covered(keys[i].tobytes(), got_ea, lt)
+    for i in only_b:
+        assert _covered(keys[i].tobytes(), got_eb, lt)
+    for i in mod:
+        assert _covered(keys[i].tobytes(), got_ea, lt) or _covered(keys[i].tobytes(), got_eb, lt)
+    ga.close()
+    gb.close()
+
+
+@pytest.mark.gpu
+def test_gpu_round_edge_segments(gpu, oracle_lib):
+    """Inverted, empty, beyond-the-end and unbounded segments, u64 keys, an empty store, and a
+    store with a pending delta run (the round compacts it first: one snapshot)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    rng = np.random.default_rng(9)
+    keys = np.unique(rng.integers(0, 2**40, 5000, dtype=np.uint64))
+    vals = rng.integers(0, 2**63, len(keys), dtype=np.uint64)
+    n = len(keys)
+    schema = RecordSchema.plain("u64", "u64")
+    st = GpuFingerprintStore(schema)
+    st.load_bulk({"keys": keys[:-100].view(np.uint8).reshape(-1, 8), "values": vals[:-100].view(np.uint8).reshape(-1, 8)})
+    # the last 100 records arrive as a batch: they sit in the delta run until the round compacts
+    st.apply({"keys": keys[-100:].view(np.uint8).reshape(-1, 8), "values": vals[-100:].view(np.uint8).reshape(-1, 8)},
+             np.zeros(100, np.uint8))
+    recs = O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0), keys.view(np.uint8).reshape(n, 8),
+                     vals.view(np.uint8).reshape(n, 8))
+    ov = OR.FtmView(_ftm(recs), True)
+    k = [int(x) for x in keys]
+    segs = [(k[3000], k[100], ((0, 0, 0, 0), 5)),           # inverted: dropped
+            (k[10], k[10], ((1, 0, 0, 0), 1)),              # empty local range, remote 1
+            (k[-1] + 1, None, ((0, 0, 0, 0), 0)),           # beyond the end, remote empty: SKIP
+            (None, k[7], ((0, 0, 0, 0), 0)),                # remote empty: IDLIST, no bounce
+            (k[20], k[21], ((9, 9, 9, 9), 1)),              # 1 vs 1: IDLIST + bounce
+            (None, None, ((5, 0, 0, 0), 9)),                # whole store: SPLIT
+            (0, 2**64 - 1, ((5, 0, 0, 0), 2))]
+    for pol, decide in [(R.FixedFanOut(16), OR.fixed_fan_out(16)), (R.SqrtFanOut(), OR.sqrt_fan_out)]:
+        wc, we = [], []
+        wo = OR.protocol_round(ov, decide, segs, wc, we)
+        gc, ge = [], []
+        o = R.protocol_round_with_policy(st, pol, _to_product(segs), gc, ge)
+        assert (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed) == wo
+        assert wo[4] == 1
+        assert ge == we and _norm(gc) == wc
+    empty = GpuFingerprintStore(schema)
+    empty.load_bulk({"keys": np.zeros((0, 8), np.uint8), "values": np.zeros((0, 8), np.uint8)})
+    gc, ge = [], []
+    o = R.protocol_round(empty, _to_product(segs[1:]), gc, ge)
+    eo = OR.FtmView(_ftm(O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0),
+                                   np.zeros((0, 8), np.uint8), np.zeros((0, 8), np.uint8))), True)
+    wc, we = [], []
+    assert (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed) == \
+        OR.protocol_round(eo, OR.fixed_fan_out(16), segs[1:], wc, we)
+    assert ge == we and _norm(gc) == wc
+    st.close()
+    empty.close()

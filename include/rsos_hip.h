@@ -221,6 +221,31 @@ int rh_store_resolve_segments(rh_store *store, size_t r, const uint8_t *start_ki
 int rh_store_split_segments(rh_store *store, size_t m, const uint64_t *select_ranks, void *keys_out, size_t q,
                             const uint64_t *lo, const uint64_t *hi, rh_aggregate *out);
 
+/* A whole round in one call, for the shipped policies that decide on the span alone:
+ * FixedFanOut(fan_out) (rbsr/src/policy/fixed_fan_out.rs; fan_out < 2 is raised to 2, 16 =
+ * FanOut::NEGENTROPY, the default of protocol_round) and SqrtFanOut (sqrt_fan_out.rs).  Segments
+ * travel in the wire codec's SoA form (rh_wire_*): `active` in (n items); children (SPLIT
+ * children and bounced IDLIST parents, with aggregates) and enumeration ranges (IDLIST;
+ * aggregates NULL) out, in the reference's order.  The output arrays belong to the store: the
+ * call fills both rh_segments with pointers to them (cap = n = the item count), valid until the
+ * next call on this store -- so a round's children may be passed straight to the peer store's
+ * round, never back to the store that produced them.                                         */
+typedef enum rh_policy { RH_POLICY_FIXED_FAN_OUT = 0, RH_POLICY_SQRT_FAN_OUT = 1 } rh_policy;
+typedef struct rh_segments {
+    uint8_t *start_kinds;     /* 0 = Unbounded, 1 = Included(key)                        */
+    void *start_keys;         /* cap * key_len bytes                                     */
+    uint8_t *end_kinds;       /* 0 = Unbounded, 1 = Excluded(key)                        */
+    void *end_keys;           /* cap * key_len bytes                                     */
+    rh_aggregate *aggregates; /* the segment's aggregate (unused for enumerations)       */
+    size_t n;                 /* items                                                   */
+    size_t cap;               /* capacity of the arrays (>= n)                           */
+} rh_segments;
+typedef struct rh_round_outcome { /* RoundOutcome (protocol.rs:135-142)                 */
+    uint64_t skipped, enumerated, split, children, dropped_malformed;
+} rh_round_outcome;
+int rh_store_protocol_round(rh_store *store, int policy, uint64_t fan_out, const rh_segments *active,
+                            rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome);
+
 /* Batched insert / overwrite / delete (FingerprintTreeMap::insert / remove, mutate.rs:23-154).
  * ops[i]: 0 = insert-or-overwrite record i, 1 = delete key i (its value columns are ignored).
  * Keys within one batch must be distinct (RH_ERR_ARG, store unchanged).  On return every

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <chrono>
@@ -827,6 +828,155 @@ struct rh_store {
         }
         return sync();
     }
+    // A whole protocol round (protocol_round_with_policy, protocol.rs:212-317) for the policies
+    // that decide on the span alone: the two batched steps above with the decision loop between
+    // them on the host, no per-segment round trip.
+    std::vector<uint64_t> pr_lo, pr_hi, pr_sel, pr_alo, pr_ahi;
+    std::vector<rh_aggregate> pr_loc, pr_aggs;
+    std::vector<uint8_t> pr_keys, pr_csk, pr_cek, pr_cskeys, pr_cekeys, pr_esk, pr_eek, pr_eskeys, pr_eekeys;
+    std::vector<rh_aggregate> pr_caggs;
+    struct Plan {
+        uint8_t kind;  // 0 skip, 1 enumerate, 2 split
+        uint8_t bounce;
+        uint64_t ncuts, first_sel, first_agg;
+    };
+    std::vector<Plan> pr_plan;
+    int protocol_round(int policy, uint64_t param, const rh_segments &in, rh_segments *ch, rh_segments *en,
+                       rh_round_outcome *oc) {
+        int rc;
+        const size_t r = in.n;
+        rh_round_outcome o{};
+        pr_lo.resize(r);
+        pr_hi.resize(r);
+        pr_loc.resize(r);
+        if (r && (rc = resolve(r, in.start_kinds, static_cast<const uint8_t *>(in.start_keys), in.end_kinds,
+                               static_cast<const uint8_t *>(in.end_keys), pr_lo.data(), pr_hi.data(), pr_loc.data())))
+            return rc;
+        const uint64_t n = nb;  // resolve compacted: the base run is the whole store
+        const uint64_t b = param < 2 ? 2 : param;  // FanOut::new
+        pr_plan.assign(r, Plan{0, 0, 0, 0, 0});
+        pr_sel.clear();
+        pr_alo.clear();
+        pr_ahi.clear();
+        uint64_t n_enum = 0;
+        for (size_t j = 0; j < r; j++) {
+            Plan &p = pr_plan[j];
+            p.kind = 3;  // dropped unless decided below
+            if (pr_hi[j] < pr_lo[j]) {  // inverted (protocol.rs:232-245)
+                o.dropped_malformed++;
+                continue;
+            }
+            const uint64_t si = std::min(pr_lo[j], n), ei = std::min(pr_hi[j], n);
+            const rh_aggregate &l = pr_loc[j], &rm = in.aggregates[j];
+            const uint64_t span = l.size, remote = rm.size;
+            // shared_cutoffs (policy/cutoffs.rs), then the policy's stride
+            int kind;
+            uint64_t stride = 0;
+            if (l.size == rm.size && !memcmp(l.fingerprint, rm.fingerprint, 32)) kind = 0;
+            else if (remote == 0) kind = 1;
+            else if (span == 0) kind = 2, stride = 1;
+            else if (span == 1 && remote == 1) kind = 1;
+            else if (span == 1) kind = 2, stride = 1;
+            else {
+                kind = 2;
+                stride = policy == RH_POLICY_SQRT_FAN_OUT ? (uint64_t)std::sqrt((float)span)  // (span as f32).sqrt() as usize
+                                                          : (span + b - 1) / b;               // ceil(span / b)
+                if (stride == 0) stride = 1;                                                  // SplitStride::per_child
+            }
+            if (kind == 2 && span > 1 && stride >= span) kind = 1;  // non-progressing SPLIT -> IDLIST (:263-272)
+            p.kind = (uint8_t)kind;
+            if (kind == 0) {
+                o.skipped++;
+            } else if (kind == 1) {
+                o.enumerated++;
+                n_enum++;
+                if (remote != 0) {
+                    p.bounce = 1;
+                    o.children++;
+                }
+            } else {
+                o.split++;
+                p.first_sel = pr_sel.size();
+                p.first_agg = pr_alo.size();
+                for (uint64_t c = si + stride; c < ei && c >= si; c += stride) pr_sel.push_back(c);  // cut_before
+                p.ncuts = pr_sel.size() - p.first_sel;
+                if (p.ncuts) {  // an uncut child is the parent, whose aggregate is in hand (:292-296)
+                    uint64_t cur = si;
+                    for (uint64_t c = 0; c < p.ncuts; c++) {
+                        pr_alo.push_back(cur);
+                        pr_ahi.push_back(pr_sel[p.first_sel + c]);
+                        cur = pr_sel[p.first_sel + c];
+                    }
+                    pr_alo.push_back(cur);
+                    pr_ahi.push_back(ei);
+                }
+                o.children += p.ncuts + 1;
+            }
+        }
+        if (oc) *oc = o;
+        // the outputs live in the store (borrowed by the caller until its next call on this store)
+        pr_csk.resize(o.children + 1);
+        pr_cek.resize(o.children + 1);
+        pr_cskeys.resize((o.children + 1) * kl);
+        pr_cekeys.resize((o.children + 1) * kl);
+        pr_caggs.resize(o.children + 1);
+        pr_esk.resize(n_enum + 1);
+        pr_eek.resize(n_enum + 1);
+        pr_eskeys.resize((n_enum + 1) * kl);
+        pr_eekeys.resize((n_enum + 1) * kl);
+        *ch = rh_segments{pr_csk.data(), pr_cskeys.data(), pr_cek.data(), pr_cekeys.data(), pr_caggs.data(), 0,
+                          (size_t)o.children};
+        *en = rh_segments{pr_esk.data(), pr_eskeys.data(), pr_eek.data(), pr_eekeys.data(), nullptr, 0, (size_t)n_enum};
+        pr_keys.resize(pr_sel.size() * kl);
+        pr_aggs.resize(pr_alo.size());
+        if ((!pr_sel.empty() || !pr_alo.empty()) &&
+            (rc = split(pr_sel.size(), pr_sel.data(), pr_keys.data(), pr_alo.size(), pr_alo.data(), pr_ahi.data(),
+                        pr_aggs.data())))
+            return rc;
+        // assemble in segment order
+        const uint8_t *sk = static_cast<const uint8_t *>(in.start_keys), *ek = static_cast<const uint8_t *>(in.end_keys);
+        uint8_t *csk = static_cast<uint8_t *>(ch->start_keys), *cek = static_cast<uint8_t *>(ch->end_keys);
+        uint8_t *esk = static_cast<uint8_t *>(en->start_keys), *eek = static_cast<uint8_t *>(en->end_keys);
+        size_t nc = 0, ne = 0;
+        auto put = [&](uint8_t skind, const uint8_t *skey, uint8_t ekind, const uint8_t *ekey, const rh_aggregate &a) {
+            ch->start_kinds[nc] = skind;
+            ch->end_kinds[nc] = ekind;
+            if (skind) memcpy(csk + nc * kl, skey, kl); else memset(csk + nc * kl, 0, kl);
+            if (ekind) memcpy(cek + nc * kl, ekey, kl); else memset(cek + nc * kl, 0, kl);
+            ch->aggregates[nc] = a;
+            nc++;
+        };
+        const rh_aggregate zero{};
+        for (size_t j = 0; j < r; j++) {
+            const Plan &p = pr_plan[j];
+            const uint8_t *s0 = in.start_kinds[j] ? sk + j * kl : nullptr, *e0 = in.end_kinds[j] ? ek + j * kl : nullptr;
+            if (p.kind == 1) {
+                if (p.bounce) put(in.start_kinds[j], s0, in.end_kinds[j], e0, zero);
+                en->start_kinds[ne] = in.start_kinds[j];
+                en->end_kinds[ne] = in.end_kinds[j];
+                if (s0) memcpy(esk + ne * kl, s0, kl); else memset(esk + ne * kl, 0, kl);
+                if (e0) memcpy(eek + ne * kl, e0, kl); else memset(eek + ne * kl, 0, kl);
+                ne++;
+            } else if (p.kind == 2) {
+                if (p.ncuts == 0) {
+                    put(in.start_kinds[j], s0, in.end_kinds[j], e0, pr_loc[j]);
+                    continue;
+                }
+                uint8_t cur_kind = in.start_kinds[j];
+                const uint8_t *cur = s0;
+                for (uint64_t c = 0; c < p.ncuts; c++) {
+                    const uint8_t *cut = pr_keys.data() + (p.first_sel + c) * kl;
+                    put(cur_kind, cur, 1, cut, pr_aggs[p.first_agg + c]);
+                    cur_kind = 1;
+                    cur = cut;
+                }
+                put(1, cur, in.end_kinds[j], e0, pr_aggs[p.first_agg + p.ncuts]);
+            }
+        }
+        ch->n = nc;
+        en->n = ne;
+        return RH_OK;
+    }
     void release() {
         (void)hipStreamSynchronize(stream);
         for (int k = 0; k < 2; k++) {
@@ -983,6 +1133,25 @@ int rh_store_split_segments(rh_store *s, size_t m, const uint64_t *select_ranks,
     if (m == 0 && q == 0) return RH_OK;
     RH_LOCK(s);
     return s->split(m, select_ranks, static_cast<uint8_t *>(keys_out), q, lo, hi, out);
+}
+
+int rh_store_protocol_round(rh_store *s, int policy, uint64_t fan_out, const rh_segments *active,
+                            rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome) {
+    if (!s || !active || !children || !enumerations) return fail(RH_ERR_ARG, "NULL");
+    if (policy != RH_POLICY_FIXED_FAN_OUT && policy != RH_POLICY_SQRT_FAN_OUT) return fail(RH_ERR_ARG, "unknown policy");
+    const size_t r = active->n;
+    if (r && (!active->start_kinds || !active->end_kinds || !active->aggregates))
+        return fail(RH_ERR_ARG, "active segments: NULL buffer");
+    for (size_t j = 0; j < r; j++) {
+        if (active->start_kinds[j] > 1 || active->end_kinds[j] > 1)
+            return fail(RH_ERR_ARG, "segment bound kind must be 0 (Unbounded) or 1 (Included / Excluded)");
+        if ((active->start_kinds[j] && !active->start_keys) || (active->end_kinds[j] && !active->end_keys))
+            return fail(RH_ERR_ARG, "bound key is NULL");
+    }
+    *children = rh_segments{};
+    *enumerations = rh_segments{};
+    RH_LOCK(s);
+    return s->protocol_round(policy, fan_out, *active, children, enumerations, outcome);
 }
 
 int rh_store_fingerprints(rh_store *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {

@@ -35,6 +35,19 @@ class Aggregate(C.Structure):
     _fields_ = [("fingerprint", C.c_uint64 * 4), ("size", C.c_uint64)]
 
 
+class Segments(C.Structure):  # rh_segments
+    _fields_ = [("start_kinds", C.c_void_p), ("start_keys", C.c_void_p), ("end_kinds", C.c_void_p),
+                ("end_keys", C.c_void_p), ("aggregates", C.c_void_p), ("n", C.c_size_t), ("cap", C.c_size_t)]
+
+
+class RoundOutcome(C.Structure):  # rh_round_outcome
+    _fields_ = [("skipped", C.c_uint64), ("enumerated", C.c_uint64), ("split", C.c_uint64),
+                ("children", C.c_uint64), ("dropped_malformed", C.c_uint64)]
+
+
+POLICY_FIXED_FAN_OUT, POLICY_SQRT_FAN_OUT = 0, 1
+
+
 class SnapshotInfo(C.Structure):
     _fields_ = [("entries", C.c_uint64), ("tombstones", C.c_uint64), ("entries_end", C.c_uint64),
                 ("keys", C.c_uint64)]
@@ -75,6 +88,8 @@ SIGNATURES = [
     ("rh_store_fingerprints", C.c_int, [P, C.c_uint64, C.c_uint64, U8P]),
     ("rh_store_resolve_segments", C.c_int, [P, SZ, U8P, VP, U8P, VP, U64P, U64P, P]),
     ("rh_store_split_segments", C.c_int, [P, SZ, U64P, VP, SZ, U64P, U64P, P]),
+    ("rh_store_protocol_round", C.c_int, [P, C.c_int, C.c_uint64, C.POINTER(Segments), C.POINTER(Segments),
+                                          C.POINTER(Segments), C.POINTER(RoundOutcome)]),
     ("rh_store_apply", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rh_store_apply_device", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),

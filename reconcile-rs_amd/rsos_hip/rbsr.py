@@ -21,6 +21,11 @@ question would be a device round trip, so the round is answered in two batched c
      rh_store_split_segments then returns the keys at every SPLIT cut (`select`, :305) and the
      aggregate of every child that is not the parent itself (:297-307).
 
+For FixedFanOut and SqrtFanOut, which decide on the span alone, the whole round runs inside
+the library instead (rh_store_protocol_round: the same two device steps with the decision loop
+in C++ between them), on segments in the wire codec's SoA form (`Segments`); a reconciliation
+that never leaves that form (protocol_round_segments) touches no per-segment Python object.
+
 Both calls see one state of the store (rsos_view.rs:36).  The outputs are appended in the
 reference's order: child_ranges (SPLIT children, bounced IDLIST parents) and enumeration_ranges
 (IDLIST), segment by segment.  A segment is a RangeAggregate (start None = Unbounded, else
@@ -34,8 +39,11 @@ from typing import List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
-from .fingerprint import Aggregate
-from .wire import RangeAggregate
+import ctypes as C
+
+from . import _abi as A
+from .fingerprint import Aggregate, Fingerprint
+from .wire import RangeAggregate, _key_bytes, _key_out
 
 Key = Union[bytes, int]
 EnumerationRange = Tuple[Optional[Key], Optional[Key]]
@@ -137,6 +145,121 @@ class RoundOutcome:
         return self
 
 
+AGG_DTYPE = np.dtype([("fingerprint", "<u8", (4,)), ("size", "<u8")])  # rh_aggregate
+
+
+class Segments:
+    """A round's segments in SoA form (rh_segments; the arrays rh_wire_* encodes): bound kinds
+    (start 0 = Unbounded / 1 = Included, end 0 = Unbounded / 1 = Excluded), key rows and
+    aggregates, n items of `cap`."""
+
+    def __init__(self, key_len: int, cap: int):
+        cap = max(int(cap), 1)
+        self.start_kinds = np.zeros(cap, np.uint8)
+        self.start_keys = np.zeros((cap, key_len), np.uint8)
+        self.end_kinds = np.zeros(cap, np.uint8)
+        self.end_keys = np.zeros((cap, key_len), np.uint8)
+        self.aggregates = np.zeros(cap, AGG_DTYPE)
+        self.n = 0
+
+    def __len__(self) -> int:
+        return self.n
+
+    @property
+    def cap(self) -> int:
+        return len(self.start_kinds)
+
+    def c(self) -> A.Segments:
+        return A.Segments(self.start_kinds.ctypes.data, self.start_keys.ctypes.data, self.end_kinds.ctypes.data,
+                          self.end_keys.ctypes.data, self.aggregates.ctypes.data, self.n, self.cap)
+
+    @staticmethod
+    def from_items(schema, items: Sequence) -> "Segments":
+        """From RangeAggregates (or (start, end) pairs, aggregates left ZERO)."""
+        seg = Segments(schema.key_row, len(items))
+        for i, it in enumerate(items):
+            start, end = (it.start, it.end) if hasattr(it, "start") else it
+            if start is not None:
+                seg.start_kinds[i] = 1
+                seg.start_keys[i] = np.frombuffer(_key_bytes(schema, start), np.uint8)
+            if end is not None:
+                seg.end_kinds[i] = 1
+                seg.end_keys[i] = np.frombuffer(_key_bytes(schema, end), np.uint8)
+            if hasattr(it, "aggregate"):
+                seg.aggregates["fingerprint"][i] = it.aggregate.fingerprint.limbs
+                seg.aggregates["size"][i] = it.aggregate.size
+        seg.n = len(items)
+        return seg
+
+    def bounds(self, schema, i: int) -> EnumerationRange:
+        s = _key_out(schema, self.start_keys[i].tobytes()) if self.start_kinds[i] else None
+        e = _key_out(schema, self.end_keys[i].tobytes()) if self.end_kinds[i] else None
+        return s, e
+
+    def items(self, schema) -> List[RangeAggregate]:
+        out = []
+        for i in range(self.n):
+            s, e = self.bounds(schema, i)
+            a = self.aggregates[i]
+            out.append(RangeAggregate(s, e, Aggregate(int(a["size"]),
+                                                      Fingerprint(tuple(int(x) for x in a["fingerprint"])))))
+        return out
+
+
+def _view(ptr, n: int, ctype, shape) -> np.ndarray:
+    if n == 0 or not ptr:
+        return np.zeros(shape, np.dtype(ctype))
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=shape)
+
+
+def _wrap(cs: A.Segments, key_len: int, copy: bool, with_aggs: bool) -> "Segments":
+    n = int(cs.n)
+    seg = Segments.__new__(Segments)
+    seg.n = n
+    m = max(n, 1)
+    seg.start_kinds = _view(cs.start_kinds, n, C.c_uint8, (m,))
+    seg.end_kinds = _view(cs.end_kinds, n, C.c_uint8, (m,))
+    seg.start_keys = _view(cs.start_keys, n, C.c_uint8, (m, key_len))
+    seg.end_keys = _view(cs.end_keys, n, C.c_uint8, (m, key_len))
+    if with_aggs and n:
+        seg.aggregates = _view(cs.aggregates, n, C.c_uint8, (m * AGG_DTYPE.itemsize,)).view(AGG_DTYPE)
+    else:
+        seg.aggregates = np.zeros(m, AGG_DTYPE)
+    if copy and n:
+        for k in ("start_kinds", "end_kinds", "start_keys", "end_keys", "aggregates"):
+            setattr(seg, k, getattr(seg, k).copy())
+    return seg
+
+
+def protocol_round_segments(store, policy, active: Segments,
+                            copy: bool = True) -> Tuple[Segments, Segments, RoundOutcome]:
+    """One round of FixedFanOut / SqrtFanOut inside the library: (children, enumerations, outcome).
+    copy=False returns views of the store's own output arrays, valid until the store's next call
+    (enough to hand the children to the peer store's round)."""
+    if isinstance(policy, FixedFanOut):
+        kind, b = A.POLICY_FIXED_FAN_OUT, policy.fan_out
+    elif isinstance(policy, SqrtFanOut):
+        kind, b = A.POLICY_SQRT_FAN_OUT, 0
+    else:
+        raise TypeError("protocol_round_segments runs FixedFanOut / SqrtFanOut; use protocol_round_with_policy")
+    kl = store.schema.key_row
+    a, cc, ec, oc = active.c(), A.Segments(), A.Segments(), A.RoundOutcome()
+    A.check(A.lib().rh_store_protocol_round(store._h, kind, b, C.byref(a), C.byref(cc), C.byref(ec), C.byref(oc)),
+            "rh_store_protocol_round")
+    return (_wrap(cc, kl, copy, True), _wrap(ec, kl, copy, False),
+            RoundOutcome(int(oc.skipped), int(oc.enumerated), int(oc.split), int(oc.children),
+                         int(oc.dropped_malformed)))
+
+
+def initial_segments(store) -> Segments:
+    seg = Segments(store.schema.key_row, 1)
+    agg = store.aggregate()
+    seg.aggregates["fingerprint"][0] = agg.fingerprint.limbs
+    seg.aggregates["size"][0] = agg.size
+    seg.n = 1
+    return seg
+
+
 def initial_ranges(local) -> List[RangeAggregate]:
     """{(-inf, +inf), A(whole store)}: the cached root, O(1) (protocol.rs:97-102)."""
     return [RangeAggregate(None, None, local.aggregate())]
@@ -149,7 +272,16 @@ def protocol_round(local, active: Sequence[RangeAggregate], child_ranges: List[R
 
 def protocol_round_with_policy(local, policy, active: Sequence[RangeAggregate],
                                child_ranges: List[RangeAggregate],
-                               enumeration_ranges: List[EnumerationRange]) -> RoundOutcome:
+                               enumeration_ranges: List[EnumerationRange], native: Optional[bool] = None) -> RoundOutcome:
+    """native: None = the library's one-call round when the policy allows it (FixedFanOut,
+    SqrtFanOut) and `local` is a GpuFingerprintStore; False = the two-call path for any policy."""
+    if native is None:
+        native = isinstance(policy, (FixedFanOut, SqrtFanOut)) and hasattr(local, "_h")
+    if native:
+        ch, en, outcome = protocol_round_segments(local, policy, Segments.from_items(local.schema, active))
+        child_ranges.extend(ch.items(local.schema))
+        enumeration_ranges.extend(en.bounds(local.schema, i) for i in range(en.n))
+        return outcome
     outcome = RoundOutcome()
     if not active:
         return outcome

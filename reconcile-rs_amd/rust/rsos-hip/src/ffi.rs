@@ -60,6 +60,31 @@ pub struct rh_snapshot_info {
     pub keys: u64,
 }
 
+pub const RH_POLICY_FIXED_FAN_OUT: c_int = 0;
+pub const RH_POLICY_SQRT_FAN_OUT: c_int = 1;
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct rh_segments {
+    pub start_kinds: *mut u8,
+    pub start_keys: *mut c_void,
+    pub end_kinds: *mut u8,
+    pub end_keys: *mut c_void,
+    pub aggregates: *mut rh_aggregate,
+    pub n: usize,
+    pub cap: usize,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default, PartialEq, Eq)]
+pub struct rh_round_outcome {
+    pub skipped: u64,
+    pub enumerated: u64,
+    pub split: u64,
+    pub children: u64,
+    pub dropped_malformed: u64,
+}
+
 pub const RH_ERR_ARG: c_int = -1;
 pub const RH_ERR_HIP: c_int = -2;
 pub const RH_ERR_OOM: c_int = -3;
@@ -115,6 +140,9 @@ extern "C" {
                                      raw_start: *mut u64, raw_end: *mut u64, local: *mut rh_aggregate) -> c_int;
     pub fn rh_store_split_segments(store: *mut rh_store, m: usize, select_ranks: *const u64, keys_out: *mut c_void,
                                    q: usize, lo: *const u64, hi: *const u64, out: *mut rh_aggregate) -> c_int;
+    pub fn rh_store_protocol_round(store: *mut rh_store, policy: c_int, fan_out: u64, active: *const rh_segments,
+                                   children: *mut rh_segments, enumerations: *mut rh_segments,
+                                   outcome: *mut rh_round_outcome) -> c_int;
     pub fn rh_store_apply(store: *mut rh_store, cols: *const rh_columns, ops: *const u8, n: usize,
                           n_new: *mut u64, n_over: *mut u64, n_del: *mut u64) -> c_int;
     pub fn rh_store_apply_device(store: *mut rh_store, dev_cols: *const rh_columns, dev_ops: *const u8, n: usize,

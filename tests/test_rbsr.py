@@ -226,8 +226,9 @@ def _gpu_and_oracle(schema, c):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("policy", ["fixed16", "sqrt", "fixed2"])
-def test_gpu_reconciliation_rounds_match_oracle(gpu, oracle_lib, policy):
+def test_gpu_reconciliation_rounds_match_oracle(gpu, oracle_lib, policy, native):
     from rsos_hip import RecordSchema, rbsr as R
     schema = RecordSchema.dated("bytes16", "bytes64")
     keys, ca, cb, only_a, only_b, mod = _dated_sets(7, 20_000, 60, 45, 30)
@@ -238,7 +239,7 @@ def test_gpu_reconciliation_rounds_match_oracle(gpu, oracle_lib, policy):
     want = reconcile(oa, ob, lambda v, act, ch, en: OR.protocol_round(v, decide, act, ch, en), OR.initial_ranges)
 
     def prod(st, act, ch, en):
-        o = R.protocol_round_with_policy(st, pol, act, ch, en)
+        o = R.protocol_round_with_policy(st, pol, act, ch, en, native=native)
         return (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed)
 
     def prod_init(st):
@@ -289,15 +290,16 @@ def test_gpu_round_edge_segments(gpu, oracle_lib):
     for pol, decide in [(R.FixedFanOut(16), OR.fixed_fan_out(16)), (R.SqrtFanOut(), OR.sqrt_fan_out)]:
         wc, we = [], []
         wo = OR.protocol_round(ov, decide, segs, wc, we)
-        gc, ge = [], []
-        o = R.protocol_round_with_policy(st, pol, _to_product(segs), gc, ge)
-        assert (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed) == wo
-        assert wo[4] == 1
-        assert ge == we and _norm(gc) == wc
+        for native in (True, False):
+            gc, ge = [], []
+            o = R.protocol_round_with_policy(st, pol, _to_product(segs), gc, ge, native=native)
+            assert (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed) == wo
+            assert wo[4] == 1
+            assert ge == we and _norm(gc) == wc
     empty = GpuFingerprintStore(schema)
     empty.load_bulk({"keys": np.zeros((0, 8), np.uint8), "values": np.zeros((0, 8), np.uint8)})
     gc, ge = [], []
-    o = R.protocol_round(empty, _to_product(segs[1:]), gc, ge)
+    o = R.protocol_round(empty, _to_product(segs[1:]), gc, ge)  # native (FixedFanOut 16)
     eo = OR.FtmView(_ftm(O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0),
                                    np.zeros((0, 8), np.uint8), np.zeros((0, 8), np.uint8))), True)
     wc, we = [], []
@@ -306,3 +308,51 @@ def test_gpu_round_edge_segments(gpu, oracle_lib):
     assert ge == we and _norm(gc) == wc
     st.close()
     empty.close()
+
+
+@pytest.mark.gpu
+def test_gpu_soa_reconciliation_and_wire(gpu, oracle_lib):
+    """A reconciliation that stays in SoA form end to end (protocol_round_segments), each round's
+    children shipped through the wire codec (ComparisonItem datagram bytes) and decoded by the
+    peer, equals the object-level rounds; the children of a SPLIT sum to their parent."""
+    from rsos_hip import RecordSchema, rbsr as R, wire
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(13, 30_000, 80, 70, 50)
+    ga, _ = _gpu_and_oracle(schema, ca)
+    gb, _ = _gpu_and_oracle(schema, cb)
+    want, _, _ = reconcile(ga, gb, lambda v, act, ch, en: _outcome(R.protocol_round(v, act, ch, en)),
+                           R.initial_ranges)
+    pol = R.FixedFanOut(16)
+    active = R.initial_segments(ga)
+    sides = [gb, ga]
+    k = 0
+    while len(active):
+        side = sides[k % 2]
+        ch, en, o = R.protocol_round_segments(side, pol, active)
+        wc, we, wo = want[k]
+        assert _outcome(o) == wo
+        assert _norm(ch.items(schema)) == wc
+        assert [en.bounds(schema, i) for i in range(en.n)] == we
+        # over the wire: encode the children as ComparisonItems, decode on the other side
+        items = ch.items(schema)
+        data = wire.encode(schema, items, msg_tag=wire.COMPARISON_ITEM)
+        back, used = wire.decode_stream(schema, data, len(items), msg_tag=wire.COMPARISON_ITEM)
+        assert back == items and used == len(data)
+        active = R.Segments.from_items(schema, back)
+        k += 1
+    assert k == len(want)
+    # zero-copy ping-pong: each store's output arrays feed the peer store directly
+    active, k = R.initial_segments(ga), 0
+    while len(active):
+        active, en, o = R.protocol_round_segments(sides[k % 2], pol, active, copy=False)
+        assert _outcome(o) == want[k][2]
+        assert _norm(active.items(schema)) == want[k][0]
+        assert [en.bounds(schema, i) for i in range(en.n)] == want[k][1]
+        k += 1
+    assert k == len(want)
+    ga.close()
+    gb.close()
+
+
+def _outcome(o):
+    return (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed)

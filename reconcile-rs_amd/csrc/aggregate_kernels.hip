@@ -263,6 +263,59 @@ __global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, uint32_
     }
 }
 
+// One wave per query (4 per workgroup), for batches of many queries over a run with block and
+// super-block sums (a protocol round's segments and children): the same head rows + blocks +
+// super-blocks decomposition, lanes striding by 64, a wave butterfly instead of the workgroup
+// reduction.  The one-workgroup form above wastes 3 of 4 waves on the short ranges a round has.
+__device__ __forceinline__ void acc_span_lane(Acc &a, const uint8_t *src, uint64_t lo, uint64_t hi, uint32_t lane,
+                                              uint32_t stride = 32) {
+    for (uint64_t i = lo + lane; i < hi; i += 64) {
+        uint32_t f[8];
+        load_fp(src, i, f, stride);
+        acc_add_fp(a, f);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_range_query_wave(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
+                                                          const uint8_t *ssums, uint64_t n, const uint64_t *qlo,
+                                                          const uint64_t *qhi, uint64_t r, uint64_t *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (j >= r) return;  // uniform per wave
+    uint64_t lo = qlo[j], hi = qhi[j];
+    if (hi > n) hi = n;
+    if (lo > hi) lo = hi;
+    Acc a;
+    acc_zero(a);
+    const uint64_t B = 256;
+    const uint64_t b1 = (lo + B - 1) / B, b2 = hi / B;
+    if (b1 >= b2) {
+        acc_span_lane(a, fps, lo, hi, lane, stride);
+    } else {
+        acc_span_lane(a, fps, lo, b1 * B, lane, stride);
+        acc_span_lane(a, fps, b2 * B, hi, lane, stride);
+        const uint64_t s1 = (b1 + B - 1) / B, s2 = b2 / B;
+        if (s1 >= s2) {
+            acc_span_lane(a, bsums, b1, b2, lane);
+        } else {
+            acc_span_lane(a, bsums, b1, s1 * B, lane);
+            acc_span_lane(a, bsums, s2 * B, b2, lane);
+            acc_span_lane(a, ssums, s1, s2, lane);
+        }
+    }
+    acc_wave_reduce(a);
+    if (lane == 0) {
+        uint32_t f[8];
+        acc_normalise(a, f);
+        uint64_t *o = out + 5 * j;
+        o[0] = (uint64_t)f[0] | ((uint64_t)f[1] << 32);
+        o[1] = (uint64_t)f[2] | ((uint64_t)f[3] << 32);
+        o[2] = (uint64_t)f[4] | ((uint64_t)f[5] << 32);
+        o[3] = (uint64_t)f[6] | ((uint64_t)f[7] << 32);
+        o[4] = hi - lo;
+    }
+}
+
 // out[j] = Σ_p in[p*r + j] over rh_aggregate {u64 fp[4]; u64 size}
 __global__ void k_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64_t *out) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -318,6 +371,11 @@ hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const ui
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
                               hipStream_t st, uint32_t stride) {
     if (r == 0) return hipSuccess;
+    if (bsums && ssums && r >= 64) {  // many queries: one wave each
+        hipLaunchKernelGGL(k_range_query_wave, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, fps, stride, bsums,
+                           ssums, n, lo, hi, r, out);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_range_query, dim3((uint32_t)r), dim3(256), 0, st, fps, stride, bsums, ssums, n, lo, hi, r, out);
     return hipGetLastError();
 }

@@ -17,6 +17,7 @@
 #include <cstring>
 #include <chrono>
 #include <memory>
+#include <new>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -450,6 +451,46 @@ extern "C" int rh_host_free(void *p) {
 // merged into the base when it passes base / compact_div, and before any rank-order query
 // (select, rank-range aggregates, key / fingerprint dumps).  Key-range aggregates and ranks
 // are answered from base + delta without compaction.
+// Page-locked host array with the part of std::vector's interface the protocol round uses:
+// the round's copies in and out of HBM then run at PCIe speed without a staging copy.
+template <class T>
+struct PinnedVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    PinnedVec() = default;
+    PinnedVec(const PinnedVec &) = delete;
+    PinnedVec &operator=(const PinnedVec &) = delete;
+    ~PinnedVec() { release(); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = cap = 0;
+    }
+    void reserve(size_t want) {
+        if (want <= cap) return;
+        const size_t c = std::max<size_t>(std::max(want, cap + cap / 2), 64);
+        T *q = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void **>(&q), c * sizeof(T), hipHostMallocDefault) != hipSuccess || !q)
+            throw std::bad_alloc();
+        if (n) memcpy(q, p, n * sizeof(T));
+        if (p) (void)hipHostFree(p);
+        p = q;
+        cap = c;
+    }
+    void resize(size_t m) { reserve(m); n = m; }
+    void assign(size_t m, uint8_t byte) { resize(m); memset(p, byte, m * sizeof(T)); }
+    void clear() { n = 0; }
+    void push_back(const T &v) {
+        if (n == cap) reserve(n + 1);
+        p[n++] = v;
+    }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    T *data() { return p; }
+    T &operator[](size_t i) { return p[i]; }
+    const T &operator[](size_t i) const { return p[i]; }
+};
+
 struct rh_store {
     int device = 0;
     rh_schema schema{};
@@ -486,7 +527,7 @@ struct rh_store {
     DevBuf<uint8_t> q_keys;
     DevBuf<uint32_t> q_rank, q_drank;
     DevBuf<uint8_t> q_kind;  // protocol round: the segments' bound kinds
-    std::vector<uint8_t> h_keys;  // protocol round: interleaved start / end keys
+    PinnedVec<uint8_t> h_keys;  // protocol round: interleaved start / end keys
     DevBuf<uint8_t> snap;  // a host snapshot's bytes while it is decoded
     rh::Scratch scratch;
 
@@ -831,9 +872,10 @@ struct rh_store {
     // A whole protocol round (protocol_round_with_policy, protocol.rs:212-317) for the policies
     // that decide on the span alone: the two batched steps above with the decision loop between
     // them on the host, no per-segment round trip.
-    std::vector<uint64_t> pr_lo, pr_hi, pr_sel, pr_alo, pr_ahi;
-    std::vector<rh_aggregate> pr_loc, pr_aggs;
-    std::vector<uint8_t> pr_keys, pr_csk, pr_cek, pr_cskeys, pr_cekeys, pr_esk, pr_eek, pr_eskeys, pr_eekeys;
+    PinnedVec<uint64_t> pr_lo, pr_hi, pr_sel, pr_alo, pr_ahi;
+    PinnedVec<rh_aggregate> pr_loc, pr_aggs;
+    PinnedVec<uint8_t> pr_keys;
+    std::vector<uint8_t> pr_csk, pr_cek, pr_cskeys, pr_cekeys, pr_esk, pr_eek, pr_eskeys, pr_eekeys;
     std::vector<rh_aggregate> pr_caggs;
     struct Plan {
         uint8_t kind;  // 0 skip, 1 enumerate, 2 split
@@ -1122,8 +1164,12 @@ int rh_store_resolve_segments(rh_store *s, size_t r, const uint8_t *start_kinds,
         if ((start_kinds[j] && !start_keys) || (end_kinds[j] && !end_keys)) return fail(RH_ERR_ARG, "bound key is NULL");
     }
     RH_LOCK(s);
-    return s->resolve(r, start_kinds, static_cast<const uint8_t *>(start_keys), end_kinds,
-                      static_cast<const uint8_t *>(end_keys), raw_start, raw_end, local);
+    try {
+        return s->resolve(r, start_kinds, static_cast<const uint8_t *>(start_keys), end_kinds,
+                          static_cast<const uint8_t *>(end_keys), raw_start, raw_end, local);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "resolve: host allocation failed");
+    }
 }
 
 int rh_store_split_segments(rh_store *s, size_t m, const uint64_t *select_ranks, void *keys_out, size_t q,
@@ -1151,7 +1197,13 @@ int rh_store_protocol_round(rh_store *s, int policy, uint64_t fan_out, const rh_
     *children = rh_segments{};
     *enumerations = rh_segments{};
     RH_LOCK(s);
-    return s->protocol_round(policy, fan_out, *active, children, enumerations, outcome);
+    try {  // no exception crosses the C ABI
+        return s->protocol_round(policy, fan_out, *active, children, enumerations, outcome);
+    } catch (const std::bad_alloc &) {
+        *children = rh_segments{};
+        *enumerations = rh_segments{};
+        return fail(RH_ERR_OOM, "protocol round: host allocation failed");
+    }
 }
 
 int rh_store_fingerprints(rh_store *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {

@@ -137,7 +137,7 @@ def main():
         batch, ops = diff_batch(schema, cols, args.n, d, seed=d)
         b.apply_device(batch, ops)
         b.compact()
-        reconcile_soa(a, b, 3)  # warm up the query buffers
+        reconcile_soa(a, b)  # warm up: the stores' pinned round buffers reach their size
         rounds, wall, segs = reconcile_soa(a, b)
         line = {"n": args.n, "d": d, "rounds": rounds, "segments": segs,
                 "soa_native_ms": round(wall * 1e3, 3)}

@@ -233,8 +233,10 @@ def test_range_aggregates_match_prefix_sums(gpu, oracle_lib):
     for f in want:
         pref.append(pref[-1] + fp_int(f))
     rng = np.random.default_rng(2)
-    lo = list(rng.integers(0, n, 200)) + [0, 0, 5, n - 1, 65536, 65535, 256, 100, n]
-    hi = list(rng.integers(0, n + 50, 200)) + [n, 0, 5, n, 3 * 65536 + 7, 65536 * 4, 512, 50, n]
+    short = rng.integers(0, n - 700, 300)  # a protocol round's many short ranges (one wave each)
+    width = rng.integers(0, 700, 300)
+    lo = list(rng.integers(0, n, 200)) + [0, 0, 5, n - 1, 65536, 65535, 256, 100, n] + list(short)
+    hi = list(rng.integers(0, n + 50, 200)) + [n, 0, 5, n, 3 * 65536 + 7, 65536 * 4, 512, 50, n] + list(short + width)
     lo_t = torch.tensor(lo, dtype=torch.int64, device="cuda")
     hi_t = torch.tensor(hi, dtype=torch.int64, device="cuda")
     for b, sup in ((bs, ss), (bs, None), (None, None)):

@@ -124,8 +124,10 @@ int rh_lift_dual_async(const rh_schema *schema, const rh_columns *dev_cols, size
 
 /* Generic path: BLAKE3 of pre-encoded canonical bytes (rsos::encoding::encode_to_vec of
  * k then v, public-api/rsos.txt:61), record i = bytes[offsets[i] .. offsets[i+1]).
- * `bytes` must be readable up to offsets[n] rounded up to a multiple of 4.               */
-int rh_lift_encoded_async(const uint8_t *dev_bytes, const uint64_t *dev_offsets, size_t n,
+ * bytes_len: the readable size of dev_bytes, a multiple of 4 and >= offsets[n] (pad the
+ * buffer).  Nothing is read at or past bytes_len: offsets that decrease or exceed it are a
+ * caller error that yields wrong fingerprints, not a fault.  Fully asynchronous.          */
+int rh_lift_encoded_async(const uint8_t *dev_bytes, size_t bytes_len, const uint64_t *dev_offsets, size_t n,
                           uint8_t *dev_fps, uint8_t *dev_block_sums, void *stream);
 
 /* out[g] = Σ in[256 g .. 256 g + 255]  (32-byte fingerprints, mod 2^256) */

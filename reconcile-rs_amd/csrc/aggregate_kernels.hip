@@ -48,6 +48,18 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
+// record i's bytes [start, start + len), clipped to the buffer: offsets that decrease or run
+// past `limit` (a caller error) give a wrong fingerprint, never an out-of-bounds read or a loop
+// over a wrapped-around length
+__device__ __forceinline__ void record_span(const uint64_t *offs, uint64_t i, uint64_t limit, uint64_t &start,
+                                            uint64_t &len) {
+    uint64_t a = offs[i], b = offs[i + 1];
+    if (a > limit) a = limit;
+    if (b > limit) b = limit;
+    start = a;
+    len = b > a ? b - a : 0;
+}
+
 // 16 message words of the block at byte `addr` with `blen` valid bytes (bytes past blen are
 // zero): 4 x 16-byte + 1 dword loads from the dword-aligned address, then a funnel shift
 __device__ __forceinline__ void load_block_fast(const uint8_t *base, uint64_t addr, uint32_t blen, bool partial,
@@ -93,7 +105,8 @@ __global__ __launch_bounds__(256) void k_lift_encoded_short(const uint8_t *bytes
             const uint64_t cand = next + lanes_below(mask);
             next += (uint64_t)__popcll(mask);
             if (need && cand < w1) {
-                const uint64_t s0 = offs[cand], l0 = offs[cand + 1] - s0;
+                uint64_t s0, l0;
+                record_span(offs, cand, limit, s0, l0);
                 if (l0 <= (uint64_t)CHUNK_LEN) {
                     i = cand;
                     start = s0;
@@ -133,8 +146,8 @@ __global__ __launch_bounds__(256) void k_lift_encoded_long(const uint8_t *bytes,
                                                            uint64_t n, uint64_t limit, uint8_t *fps) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const uint64_t start = offs[i];
-    const uint64_t len = offs[i + 1] - start;
+    uint64_t start, len;
+    record_span(offs, i, limit, start, len);
     if (len <= (uint64_t)CHUNK_LEN) return;
     const uint64_t nchunks = (len + CHUNK_LEN - 1) / CHUNK_LEN;
     uint32_t stk[ENC_STACK][8];

@@ -231,19 +231,15 @@ int rh_lift_dual_async(const rh_schema *schema, const rh_columns *cols, size_t n
     return lift_dispatch(*schema, *cols, n, fps_d, bs_d, fps_p, bs_p, true, static_cast<hipStream_t>(stream));
 }
 
-int rh_lift_encoded_async(const uint8_t *bytes, const uint64_t *offsets, size_t n, uint8_t *fps,
+int rh_lift_encoded_async(const uint8_t *bytes, size_t bytes_len, const uint64_t *offsets, size_t n, uint8_t *fps,
                           uint8_t *block_sums, void *stream) {
     if (n == 0) return RH_OK;
     if (!offsets || !fps) return fail(RH_ERR_ARG, "offsets / fps is NULL");
+    if (bytes_len && !bytes) return fail(RH_ERR_ARG, "bytes is NULL");
+    if (bytes_len % 4) return fail(RH_ERR_ARG, "bytes_len must be a multiple of 4 (pad the buffer)");
     if (!aligned16(fps) || !aligned16(block_sums)) return fail(RH_ERR_ARG, "outputs must be 16-byte aligned");
-    // the kernel needs the total byte count as its read limit: read offsets[n] (8 bytes)
-    uint64_t total = 0;
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    RH_HIP(hipMemcpyAsync(&total, offsets + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    RH_HIP(hipStreamSynchronize(st));
-    if (total && !bytes) return fail(RH_ERR_ARG, "bytes is NULL");
-    const uint64_t limit = (total + 3) & ~3ull;
-    RH_HIP(rh::launch_lift_encoded(bytes, offsets, n, limit, fps, block_sums, st));
+    // no host round trip: bytes_len bounds every read, whatever the offsets say
+    RH_HIP(rh::launch_lift_encoded(bytes, offsets, n, bytes_len, fps, block_sums, static_cast<hipStream_t>(stream)));
     return RH_OK;
 }
 

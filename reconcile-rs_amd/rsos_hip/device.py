@@ -111,7 +111,8 @@ def lift_encoded(data: torch.Tensor, offsets: torch.Tensor, block_sums: bool = T
     # the kernel may read the last dword containing data[offsets[n]-1]: pad to 4
     if data.numel() % 4:
         data = torch.cat([data, torch.zeros(4 - data.numel() % 4, dtype=torch.uint8, device=dev)])
-    A.check(A.lib().rh_lift_encoded_async(_ptr(data), _ptr(offsets), n, _ptr(fps), _ptr(bs), _stream()),
+    A.check(A.lib().rh_lift_encoded_async(_ptr(data), data.numel(), _ptr(offsets), n, _ptr(fps), _ptr(bs),
+                                          _stream()),
             "rh_lift_encoded_async")
     return fps, bs
 

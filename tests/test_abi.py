@@ -108,3 +108,11 @@ def test_python_value_types_mirror_reference(rsos_hip_lib):
     assert str(f) == "0000000000000004000000000000000300000000000000020000000000000001"
     z = Aggregate(2, f + (-f))
     assert not z.is_empty() and Aggregate.ZERO.is_empty()
+
+
+def test_encoded_lift_rejects_unpadded_length(rsos_hip_lib):
+    """bytes_len must be a multiple of 4: checked before anything is launched."""
+    from rsos_hip import _abi as A
+    buf = (C.c_uint64 * 8)()
+    rc = A.lib().rh_lift_encoded_async(C.addressof(buf), 7, C.addressof(buf), 1, C.addressof(buf), None, None)
+    assert rc == A.ERR_ARG and b"multiple of 4" in A.lib().rh_last_error()

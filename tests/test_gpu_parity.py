@@ -202,6 +202,24 @@ def test_encoded_short_mix(gpu, oracle_lib):
     assert int.from_bytes(bs.cpu().numpy()[0].tobytes(), "little") == tot
 
 
+def test_encoded_malformed_offsets_are_bounded(gpu, oracle_lib):
+    """Offsets that decrease or run past the buffer: no fault, no runaway loop; well-formed
+    records in the same launch still hash correctly."""
+    import torch
+    from rsos_hip import lift_encoded
+    blobs = [b"abc", b"x" * 70, b"", b"hello world"]
+    data = bytearray(b"".join(blobs))
+    offs = [0]
+    for b in blobs:
+        offs.append(offs[-1] + len(b))
+    good = len(offs) - 1
+    offs += [offs[-1] - 5, 1 << 40, 3, (1 << 64) - 1 - (1 << 63)]  # decreasing, far past the end, ...
+    t = torch.frombuffer(data, dtype=torch.uint8).cuda()
+    fps, _ = lift_encoded(t, torch.tensor(offs, dtype=torch.int64).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(fps.cpu().numpy()[:good], oracle_lib.lift_encoded(blobs))
+
+
 def test_empty_batches(gpu):
     import torch
     from rsos_hip import RecordSchema, lift_records, range_aggregates

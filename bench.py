@@ -11,7 +11,7 @@ Workload (BASELINE.json configs[1]): 10 M records per GPU, 16 B key / 64 B value
 (FingerprintTreeMap<[u8;16], Entry<Timestamp, Vec<u8>>>, 120 canonical bytes per record).
 Weak scaling: every GPU holds its own 10 M-record shard of one globally key-sorted set.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config1|config2|config3|config3_full|config4|config5|snapshot|bench_u32]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config1|config2|config3|config3_full|config4|config5|snapshot|rbsr|bench_u32]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Prints ONE JSON line on rank 0.
@@ -46,6 +46,10 @@ CONFIGS = {
                   "benches/bench.rs fill shape: FingerprintTreeMap<u32,u32>"),
     "config5": ("bytes16", "bytes64", "dated", 100_000_000,
                 "BASELINE configs[4]: 1M random inserts per batch into a 100M-record resident map"),
+    "rbsr": ("bytes16", "bytes64", "dated", 10_000_000,
+             "rbsr reconciliation (SURVEY 8a row a13): two GPU-resident replicas of 10M records/GPU "
+             "(16 B key / 64 B value, dated) differing in --diffs keys, FixedFanOut(16) rounds until no "
+             "segment is left"),
     "snapshot": ("bytes16", "bytes64", "dated", 10_000_000,
                  "snapshot reload (SURVEY 8f row 4): RCNL v1 file of 10M entries (16 B key / 64 B value, "
                  "10% tombstones) resident in HBM -> dated + projection stores"),
@@ -67,6 +71,7 @@ def parse():
     p.add_argument("--overwrite", type=float, default=0.0,
                    help="config5: fraction of each batch that re-stamps existing keys (the new - old delta)")
     p.add_argument("--e2e", action="store_true", help="also time host->device->host end to end (DESIGN.md)")
+    p.add_argument("--diffs", type=int, default=10_000, help="rbsr: keys in which the two replicas differ")
     p.add_argument("--check", type=int, default=1, help="oracle spot-check of a sample before timing")
     return p.parse_args()
 
@@ -99,6 +104,8 @@ def main():
         return incremental(args, world, rank, dev, dist)
     if args.config == "snapshot":
         return reload(args, world, rank, dev, dist)
+    if args.config == "rbsr":
+        return reconcile(args, world, rank, dev, dist)
     kname, vname, kind, n_default, desc = CONFIGS[args.config]
     n = args.records or n_default
     schema = getattr(RecordSchema, kind)(kname, vname)
@@ -398,6 +405,117 @@ def reload(args, world, rank, dev, dist):
     proj.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def reconcile(args, world, rank, dev, dist):
+    """rbsr: one step = one whole reconciliation between two GPU stores (replica A, and replica B
+    = A minus d/2 keys, with d/2 records re-stamped): FixedFanOut(16) rounds, each answered by
+    rh_store_protocol_round on the responding store, the children handed to the peer store, until
+    no segment is left (rbsr/src/protocol.rs:97-317 driven as src/replica/dispatch.rs does)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    from rsos_hip.synth import make_records
+    kname, vname, kind, n_default, desc = CONFIGS["rbsr"]
+    n = args.records or n_default
+    d = max(2, args.diffs)
+    schema = getattr(RecordSchema, kind)(kname, vname)
+    cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
+    a, b = GpuFingerprintStore(schema, device=dev.index), GpuFingerprintStore(schema, device=dev.index)
+    a.load_bulk_device(cols)
+    b.load_bulk_device(cols)
+    g = torch.Generator(device=dev)
+    g.manual_seed(11 + rank)
+    rows = torch.randperm(n, generator=g, device=dev)[:d]
+    batch = {k: v[rows].clone() for k, v in cols.items()}
+    batch["phys"] += 1_000_000
+    ops = torch.zeros(d, dtype=torch.uint8, device=dev)
+    ops[: d // 2] = 1  # B lacks these keys; the other half differ in their stamp
+    b.apply_device(batch, ops)
+    b.compact()
+    cpu_line = None
+    if args.cpu_baseline and world == 1:  # the same replicas and differences, reconciled on the CPU
+        cpu_line = cpu_baseline_reconcile(schema, cols, rows.cpu().numpy(), args.cpu_sample or n)
+    del cols, batch
+    pol = R.FixedFanOut(16)
+
+    def run():
+        active, k, segs, enum = R.initial_segments(a), 0, 0, 0
+        while len(active):
+            segs += len(active)
+            active, en, _ = R.protocol_round_segments((b, a)[k % 2], pol, active, copy=False)
+            enum += len(en)
+            k += 1
+        return k, segs, enum
+
+    for _ in range(max(args.warmup, 1)):
+        rounds, segs, enum = run()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rounds, segs, enum = run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        line = {
+            "metric": "rbsr reconciliation on GPU stores (segments answered per second)",
+            "value": round(segs * args.steps * world / elapsed / 1e6, 3), "unit": "M segments/s",
+            "reconciliations_per_s": round(args.steps * world / elapsed, 2),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded): sorted resident set; replica B lacks d/2 keys and re-stamps d/2",
+            "config": {"workload": desc, "records_per_replica": n, "diffs": d, "policy": "FixedFanOut(16)",
+                       "parallelism": f"key-range shards x{world} (each rank reconciles its own shard pair)"},
+            "rounds": rounds, "segments_per_reconciliation": segs, "enumerations": enum,
+            "step": "initial_ranges + protocol rounds (rh_store_protocol_round, 2 device round trips each) "
+                    "until no segment is left",
+        }
+        if cpu_line:
+            line["cpu_baseline"] = cpu_line
+        print(json.dumps(line), flush=True)
+    a.close()
+    b.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_reconcile(schema, cols, rows, m):
+    """The same reconciliation on the CPU: oracle.c's restatement of protocol_round_with_policy
+    (one aggregate / rank / select question at a time, FixedFanOut(16)) over two oracle
+    FingerprintTreeMaps holding the first m records of each replica."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from rsos_hip.synth import to_host
+    h = to_host(cols, 0, m)
+    h.setdefault("tags", np.zeros(m, np.uint8))
+    rows = rows[rows < m]
+    d = len(rows)
+    keep = np.ones(m, bool)
+    keep[rows[: d // 2]] = False
+    phys = h["phys"].copy()
+    phys[rows[d // 2:]] += 1_000_000
+    sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+    ra = O.Records(sc, h["keys"], h["values"], h["phys"], h["logical"], h["node"], h["tags"])
+    rb = O.Records(sc, h["keys"][keep], h["values"][keep], phys[keep], h["logical"][keep], h["node"][keep],
+                   h["tags"][keep])
+    ta, tb = O.FingerprintTreeMap(ra), O.FingerprintTreeMap(rb)
+    ta.fill(0, ra.n)
+    tb.fill(0, rb.n)
+    t0 = time.perf_counter()
+    rounds, segs, _ = O.reconcile_fixed(ta, tb, 16)
+    dt = time.perf_counter() - t0
+    return {"value": round(segs / dt / 1e6, 4), "unit": "M segments/s", "cores": 1, "kind": "port",
+            "reconciliation_ms": round(dt * 1e3, 3),
+            "sample": f"one reconciliation of two oracle FTMs (oracle.c) of {m} records differing in {d} keys "
+                      f"({segs} segments, {rounds} rounds)"}
 
 
 def cpu_baseline_reload(sd, sp, cols, m):

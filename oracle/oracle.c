@@ -608,6 +608,119 @@ size_t or_ftm_select(const or_ftm *t, size_t index) {
     return n->rec[index];
 }
 
+/* ---- rbsr protocol rounds over two FTMs (the CPU baseline of bench.py --config rbsr) ----------
+ * protocol_round_with_policy (rbsr/src/protocol.rs:212-317) under FixedFanOut(b), restated one
+ * question at a time as the reference asks them: aggregate(range) (:230), rank of both bounds
+ * (protocol/rank.rs:85-125), shared_cutoffs + ceil(span / b) (policy/cutoffs.rs,
+ * fixed_fan_out.rs), and per SPLIT child select(cut) + aggregate(child) (:288-313).  Rounds
+ * alternate between the two trees until no segment is left, starting from a's root. */
+typedef struct {
+    uint8_t sk, ek;           /* 0 Unbounded, 1 Included / Excluded */
+    uint8_t skey[32], ekey[32];
+    or_aggregate agg;
+} or_seg;
+
+typedef struct { or_seg *v; size_t n, cap; } seg_vec;
+
+static void seg_push(seg_vec *q, const or_seg *x) {
+    if (q->n == q->cap) {
+        q->cap = q->cap ? 2 * q->cap : 64;
+        q->v = (or_seg *)realloc(q->v, q->cap * sizeof(or_seg));
+    }
+    q->v[q->n++] = *x;
+}
+
+static void seg_bounds(const or_seg *g, const uint8_t **lo, const uint8_t **hi) {
+    *lo = g->sk ? g->skey : NULL;
+    *hi = g->ek ? g->ekey : NULL;
+}
+
+/* one round on tree t: returns the number of IDLIST (enumerated) segments */
+static size_t round_fixed(const or_ftm *t, size_t b, const seg_vec *in, seg_vec *out) {
+    size_t enumerated = 0;
+    const size_t size = t->root->subtree.size;
+    for (size_t j = 0; j < in->n; j++) {
+        const or_seg *g = &in->v[j];
+        const uint8_t *lo, *hi;
+        seg_bounds(g, &lo, &hi);
+        or_aggregate local;
+        or_ftm_aggregate(t, lo, hi, &local);
+        const size_t raw_s = lo ? or_ftm_rank(t, lo) : 0, raw_e = hi ? or_ftm_rank(t, hi) : size;
+        if (raw_e < raw_s) continue; /* dropped as malformed */
+        const size_t si = raw_s < size ? raw_s : size, ei = raw_e < size ? raw_e : size;
+        const uint64_t span = local.size, remote = g->agg.size;
+        int kind; /* 0 skip, 1 enumerate, 2 split */
+        uint64_t stride = 0;
+        if (span == remote && !memcmp(local.fp, g->agg.fp, 32)) kind = 0;
+        else if (remote == 0) kind = 1;
+        else if (span == 0) kind = 2, stride = 1;
+        else if (span == 1 && remote == 1) kind = 1;
+        else if (span == 1) kind = 2, stride = 1;
+        else kind = 2, stride = (span + b - 1) / b;
+        if (kind == 2 && span > 1 && stride >= span) kind = 1;
+        if (kind == 1) {
+            enumerated++;
+            if (remote != 0) {
+                or_seg c = *g;
+                memset(&c.agg, 0, sizeof c.agg);
+                seg_push(out, &c);
+            }
+        } else if (kind == 2) {
+            or_seg c = *g;
+            size_t cur = si;
+            for (;;) {
+                const size_t nxt = cur + stride;
+                if (!(nxt < ei)) {
+                    c.ek = g->ek;
+                    memcpy(c.ekey, g->ekey, sizeof c.ekey);
+                    if (cur == si) c.agg = local;
+                    else {
+                        seg_bounds(&c, &lo, &hi);
+                        or_ftm_aggregate(t, lo, hi, &c.agg);
+                    }
+                    seg_push(out, &c);
+                    break;
+                }
+                c.ek = 1;
+                memcpy(c.ekey, rec_key(t, or_ftm_select(t, nxt)), t->kst);
+                seg_bounds(&c, &lo, &hi);
+                or_ftm_aggregate(t, lo, hi, &c.agg);
+                seg_push(out, &c);
+                c.sk = 1;
+                memcpy(c.skey, c.ekey, sizeof c.skey);
+                cur = nxt;
+            }
+        }
+    }
+    return enumerated;
+}
+
+int or_reconcile_fixed(const or_ftm *a, const or_ftm *bt, size_t fan_out, uint64_t out[3]) {
+    if (a->kst > 32 || bt->kst > 32) return -1;
+    const size_t b = fan_out < 2 ? 2 : fan_out;
+    seg_vec cur = {0}, nxt = {0};
+    or_seg root;
+    memset(&root, 0, sizeof root);
+    or_ftm_root(a, &root.agg);
+    seg_push(&cur, &root);
+    uint64_t rounds = 0, segs = 0, enums = 0;
+    while (cur.n) {
+        segs += cur.n;
+        nxt.n = 0;
+        enums += round_fixed(rounds % 2 ? a : bt, b, &cur, &nxt);
+        seg_vec t = cur;
+        cur = nxt;
+        nxt = t;
+        rounds++;
+    }
+    free(cur.v);
+    free(nxt.v);
+    out[0] = rounds;
+    out[1] = segs;
+    out[2] = enums;
+    return 0;
+}
+
 static int check_aux(const ftm_node *n) {
     if (!n->leaf)
         for (uint32_t i = 0; i <= n->nkeys; i++)

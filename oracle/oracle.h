@@ -107,6 +107,9 @@ void    or_ftm_aggregate(const or_ftm *t, const uint8_t *lo_key, const uint8_t *
 size_t  or_ftm_rank(const or_ftm *t, const uint8_t *key);
 /* select(index) -> the record row holding the index-th key; (size_t)-1 if index >= len */
 size_t  or_ftm_select(const or_ftm *t, size_t index);
+/* a whole FixedFanOut(fan_out) reconciliation between two trees (rbsr protocol rounds, starting
+ * from a's root at b); out: rounds, segments answered, IDLIST segments.  -1 if keys > 32 B */
+int     or_reconcile_fixed(const or_ftm *a, const or_ftm *b, size_t fan_out, uint64_t out[3]);
 /* 0 on success; -1 if the per-node cached aggregates disagree with a recomputation */
 int     or_ftm_check(const or_ftm *t);
 

@@ -68,6 +68,8 @@ def lib() -> C.CDLL:
         L.or_ftm_rank.restype = C.c_size_t
         L.or_ftm_select.argtypes = [C.c_void_p, C.c_size_t]
         L.or_ftm_select.restype = C.c_size_t
+        L.or_reconcile_fixed.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.or_reconcile_fixed.restype = C.c_int
         L.or_ftm_check.argtypes = [C.c_void_p]
         L.or_ftm_check.restype = C.c_int
         _lib = L
@@ -179,3 +181,12 @@ class FingerprintTreeMap:
 
     def check(self) -> bool:
         return lib().or_ftm_check(self._h) == 0
+
+
+def reconcile_fixed(a: FingerprintTreeMap, b: FingerprintTreeMap, fan_out: int = 16):
+    """A whole FixedFanOut reconciliation in C (oracle.c or_reconcile_fixed):
+    (rounds, segments answered, IDLIST segments)."""
+    out = (C.c_uint64 * 3)()
+    if lib().or_reconcile_fixed(a._h, b._h, fan_out, out) != 0:
+        raise ValueError("keys longer than 32 bytes")
+    return int(out[0]), int(out[1]), int(out[2])

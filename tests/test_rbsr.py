@@ -183,6 +183,28 @@ def test_batched_driver_host_logic_matches_oracle(oracle_lib):
             assert _covered(int(k), want[1], lt) or _covered(int(k), want[2], lt)
 
 
+def test_c_reconciliation_matches_literal_driver(oracle_lib):
+    """oracle.c's whole-reconciliation loop (the bench's native CPU baseline) takes the same
+    rounds, answers the same segments and enumerates the same ranges as the Python driver."""
+    rng = np.random.default_rng(8)
+    keys = rng.choice(2**31, 5000, replace=False)
+    a_pairs = {int(k): 7 for k in keys[:4900]}
+    b_pairs = dict(a_pairs)
+    for k in keys[4900:4950]:
+        a_pairs[int(k)] = 1
+    for k in keys[4950:]:
+        b_pairs[int(k)] = 2
+    for k in keys[:30]:
+        b_pairs[int(k)] = 9
+    ta, tb = _ftm(_u32_recs(a_pairs.items())), _ftm(_u32_recs(b_pairs.items()))
+    va, vb = OR.FtmView(ta, True), OR.FtmView(tb, True)
+    for b in (16, 2, 5):
+        log, ea, eb = reconcile(va, vb, lambda v, act, ch, en: OR.protocol_round(v, OR.fixed_fan_out(b), act, ch, en),
+                                OR.initial_ranges)
+        want = (len(log), 1 + sum(len(c) for c, _, _ in log[:-1]), len(ea) + len(eb))
+        assert O.reconcile_fixed(ta, tb, b) == want
+
+
 def test_oracle_drops_inverted_segment(oracle_lib):
     a = OR.FtmView(_ftm(_u32_recs([(i, i) for i in range(100)])), True)
     children, enums = [], []

@@ -522,8 +522,6 @@ struct rh_store {
     DevBuf<rh_aggregate> q_out, q_bout, q_dout;
     DevBuf<uint8_t> q_keys;
     DevBuf<uint32_t> q_rank, q_drank;
-    DevBuf<uint8_t> q_kind;  // protocol round: the segments' bound kinds
-    PinnedVec<uint8_t> h_keys;  // protocol round: interleaved start / end keys
     DevBuf<uint8_t> snap;  // a host snapshot's bytes while it is decoded
     rh::Scratch scratch;
 
@@ -815,62 +813,96 @@ struct rh_store {
     }
     // rbsr protocol round, step 1 (protocol.rs:225-255): every segment's local aggregate and
     // raw rank bounds, against the compacted base run (select needs rank order anyway).
-    int resolve(size_t r, const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys,
-                uint64_t *raw_lo, uint64_t *raw_hi, rh_aggregate *out) {
+    // The two steps move their inputs in one host-to-device copy and their results out in one
+    // device-to-host copy, through page-locked staging: a round trip is then 1 + kernels + 1
+    // queue operations.
+    PinnedVec<uint8_t> stage_in, stage_out, stage_out2;  // step 2's results land beside step 1's
+    DevBuf<uint8_t> q_in, q_res;
+    static size_t pad8(size_t x) { return (x + 7) & ~size_t(7); }
+    // step 1, results in stage_out: lo[r] u64, hi[r] u64, aggregates[r]
+    int resolve_staged(size_t r, const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys,
+                       const uint64_t **lo, const uint64_t **hi, const rh_aggregate **aggs) {
         int rc;
         if ((rc = compact())) return rc;
-        if ((rc = q_keys.ensure(2 * r * kl + 64)) || (rc = q_rank.ensure(2 * r)) || (rc = q_lo.ensure(r)) ||
-            (rc = q_hi.ensure(r)) || (rc = q_out.ensure(r)) || (rc = q_kind.ensure(2 * r + 64)))
+        const size_t kb = pad8(2 * r * kl), in_bytes = kb + pad8(2 * r), out_bytes = 16 * r + r * sizeof(rh_aggregate);
+        if ((rc = q_in.ensure(in_bytes + 64)) || (rc = q_res.ensure(out_bytes + 64)) || (rc = q_rank.ensure(2 * r)))
             return rc;
-        h_keys.assign(2 * r * kl, 0);
+        stage_in.resize(in_bytes);
+        stage_out.resize(out_bytes);
+        uint8_t *h = stage_in.data();
         for (size_t j = 0; j < r; j++) {  // row 2j: start key, 2j + 1: end key (unbounded: zeros)
-            if (sk[j]) memcpy(&h_keys[2 * j * kl], skeys + j * kl, kl);
-            if (ek[j]) memcpy(&h_keys[(2 * j + 1) * kl], ekeys + j * kl, kl);
+            if (sk[j]) memcpy(h + 2 * j * kl, skeys + j * kl, kl); else memset(h + 2 * j * kl, 0, kl);
+            if (ek[j]) memcpy(h + (2 * j + 1) * kl, ekeys + j * kl, kl); else memset(h + (2 * j + 1) * kl, 0, kl);
         }
-        RH_HIP(hipMemcpyAsync(q_keys.p, h_keys.data(), 2 * r * kl, hipMemcpyHostToDevice, stream));
-        RH_HIP(hipMemcpyAsync(q_kind.p, sk, r, hipMemcpyHostToDevice, stream));
-        RH_HIP(hipMemcpyAsync(q_kind.p + r, ek, r, hipMemcpyHostToDevice, stream));
-        if (nb) RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_keys.p, 2 * r, q_rank.p, nullptr, stream));
+        memcpy(h + kb, sk, r);
+        memcpy(h + kb + r, ek, r);
+        RH_HIP(hipMemcpyAsync(q_in.p, h, in_bytes, hipMemcpyHostToDevice, stream));
+        uint64_t *d_lo = reinterpret_cast<uint64_t *>(q_res.p), *d_hi = d_lo + r, *d_agg = d_hi + r;
+        if (nb) RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_in.p, 2 * r, q_rank.p, nullptr, stream));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
-        RH_HIP(rh::launch_resolve_bounds(q_rank.p, q_kind.p, q_kind.p + r, r, nb, q_lo.p, q_hi.p, stream));
+        RH_HIP(rh::launch_resolve_bounds(q_rank.p, q_in.p + kb, q_in.p + kb + r, r, nb, d_lo, d_hi, stream));
         // an inverted segment (hi < lo) is clamped to the empty range: ZERO
-        RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, r,
-                                      reinterpret_cast<uint64_t *>(q_out.p), stream));
-        RH_HIP(hipMemcpyAsync(raw_lo, q_lo.p, r * 8, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(raw_hi, q_hi.p, r * 8, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(out, q_out.p, r * sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
-        return sync();
+        RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, d_lo, d_hi, r, d_agg, stream));
+        RH_HIP(hipMemcpyAsync(stage_out.data(), q_res.p, out_bytes, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        *lo = reinterpret_cast<const uint64_t *>(stage_out.data());
+        *hi = *lo + r;
+        *aggs = reinterpret_cast<const rh_aggregate *>(*hi + r);
+        return RH_OK;
     }
-    // step 2 (protocol.rs:288-313): the select() cuts of every SPLIT and the children's aggregates
-    int split(size_t m, const uint64_t *sel, uint8_t *keys_out, size_t q, const uint64_t *lo, const uint64_t *hi,
-              rh_aggregate *out) {
+    int resolve(size_t r, const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys,
+                uint64_t *raw_lo, uint64_t *raw_hi, rh_aggregate *out) {
+        const uint64_t *lo, *hi;
+        const rh_aggregate *aggs;
+        int rc = resolve_staged(r, sk, skeys, ek, ekeys, &lo, &hi, &aggs);
+        if (rc) return rc;
+        memcpy(raw_lo, lo, r * 8);
+        memcpy(raw_hi, hi, r * 8);
+        memcpy(out, aggs, r * sizeof(rh_aggregate));
+        return RH_OK;
+    }
+    // step 2 (protocol.rs:288-313): the select() cuts of every SPLIT and the children's
+    // aggregates; results in stage_out: keys[m] (padded to 8 B), aggregates[q]
+    int split_staged(size_t m, const uint64_t *sel, size_t q, const uint64_t *lo, const uint64_t *hi,
+                     const uint8_t **keys, const rh_aggregate **aggs) {
         int rc;
         if ((rc = compact())) return rc;
         for (size_t i = 0; i < m; i++)
             if (sel[i] >= nb) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
-        if ((rc = q_merged.ensure(m + 1)) || (rc = q_keys.ensure(m * kl + 64)) || (rc = q_lo.ensure(q + 1)) ||
-            (rc = q_hi.ensure(q + 1)) || (rc = q_out.ensure(q + 1)))
-            return rc;
-        if (m) {
-            RH_HIP(hipMemcpyAsync(q_merged.p, sel, m * 8, hipMemcpyHostToDevice, stream));
-            RH_HIP(rh::launch_gather_keys(bkeys[cb].p, (uint32_t)kl, q_merged.p, m, q_keys.p, stream));
-            RH_HIP(hipMemcpyAsync(keys_out, q_keys.p, m * kl, hipMemcpyDeviceToHost, stream));
-        }
-        if (q) {
-            RH_HIP(hipMemcpyAsync(q_lo.p, lo, q * 8, hipMemcpyHostToDevice, stream));
-            RH_HIP(hipMemcpyAsync(q_hi.p, hi, q * 8, hipMemcpyHostToDevice, stream));
-            RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, q,
-                                          reinterpret_cast<uint64_t *>(q_out.p), stream));
-            RH_HIP(hipMemcpyAsync(out, q_out.p, q * sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
-        }
-        return sync();
+        const size_t in_bytes = 8 * (m + 2 * q), kb = pad8(m * kl), out_bytes = kb + q * sizeof(rh_aggregate);
+        if ((rc = q_in.ensure(in_bytes + 64)) || (rc = q_res.ensure(out_bytes + 64))) return rc;
+        stage_in.resize(in_bytes);
+        stage_out2.resize(out_bytes);
+        uint64_t *h = reinterpret_cast<uint64_t *>(stage_in.data());
+        memcpy(h, sel, m * 8);
+        memcpy(h + m, lo, q * 8);
+        memcpy(h + m + q, hi, q * 8);
+        RH_HIP(hipMemcpyAsync(q_in.p, h, in_bytes, hipMemcpyHostToDevice, stream));
+        const uint64_t *d_sel = reinterpret_cast<const uint64_t *>(q_in.p), *d_lo = d_sel + m, *d_hi = d_lo + q;
+        if (m) RH_HIP(rh::launch_gather_keys(bkeys[cb].p, (uint32_t)kl, d_sel, m, q_res.p, stream));
+        if (q)
+            RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, d_lo, d_hi, q,
+                                          reinterpret_cast<uint64_t *>(q_res.p + kb), stream));
+        RH_HIP(hipMemcpyAsync(stage_out2.data(), q_res.p, out_bytes, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        *keys = stage_out2.data();
+        *aggs = reinterpret_cast<const rh_aggregate *>(stage_out2.data() + kb);
+        return RH_OK;
+    }
+    int split(size_t m, const uint64_t *sel, uint8_t *keys_out, size_t q, const uint64_t *lo, const uint64_t *hi,
+              rh_aggregate *out) {
+        const uint8_t *keys;
+        const rh_aggregate *aggs;
+        int rc = split_staged(m, sel, q, lo, hi, &keys, &aggs);
+        if (rc) return rc;
+        if (m) memcpy(keys_out, keys, m * kl);
+        if (q) memcpy(out, aggs, q * sizeof(rh_aggregate));
+        return RH_OK;
     }
     // A whole protocol round (protocol_round_with_policy, protocol.rs:212-317) for the policies
     // that decide on the span alone: the two batched steps above with the decision loop between
     // them on the host, no per-segment round trip.
-    PinnedVec<uint64_t> pr_lo, pr_hi, pr_sel, pr_alo, pr_ahi;
-    PinnedVec<rh_aggregate> pr_loc, pr_aggs;
-    PinnedVec<uint8_t> pr_keys;
+    std::vector<uint64_t> pr_sel, pr_alo, pr_ahi;
     std::vector<uint8_t> pr_csk, pr_cek, pr_cskeys, pr_cekeys, pr_esk, pr_eek, pr_eskeys, pr_eekeys;
     std::vector<rh_aggregate> pr_caggs;
     struct Plan {
@@ -884,12 +916,12 @@ struct rh_store {
         int rc;
         const size_t r = in.n;
         rh_round_outcome o{};
-        pr_lo.resize(r);
-        pr_hi.resize(r);
-        pr_loc.resize(r);
-        if (r && (rc = resolve(r, in.start_kinds, static_cast<const uint8_t *>(in.start_keys), in.end_kinds,
-                               static_cast<const uint8_t *>(in.end_keys), pr_lo.data(), pr_hi.data(), pr_loc.data())))
+        const uint64_t *pr_lo = nullptr, *pr_hi = nullptr;
+        const rh_aggregate *res_loc = nullptr;
+        if (r && (rc = resolve_staged(r, in.start_kinds, static_cast<const uint8_t *>(in.start_keys), in.end_kinds,
+                                      static_cast<const uint8_t *>(in.end_keys), &pr_lo, &pr_hi, &res_loc)))
             return rc;
+        const rh_aggregate *pr_loc = res_loc;  // stays valid: step 2 stages its results apart
         const uint64_t n = nb;  // resolve compacted: the base run is the whole store
         const uint64_t b = param < 2 ? 2 : param;  // FanOut::new
         pr_plan.assign(r, Plan{0, 0, 0, 0, 0});
@@ -965,11 +997,11 @@ struct rh_store {
         *ch = rh_segments{pr_csk.data(), pr_cskeys.data(), pr_cek.data(), pr_cekeys.data(), pr_caggs.data(), 0,
                           (size_t)o.children};
         *en = rh_segments{pr_esk.data(), pr_eskeys.data(), pr_eek.data(), pr_eekeys.data(), nullptr, 0, (size_t)n_enum};
-        pr_keys.resize(pr_sel.size() * kl);
-        pr_aggs.resize(pr_alo.size());
+        const uint8_t *pr_keys = nullptr;
+        const rh_aggregate *pr_aggs = nullptr;
         if ((!pr_sel.empty() || !pr_alo.empty()) &&
-            (rc = split(pr_sel.size(), pr_sel.data(), pr_keys.data(), pr_alo.size(), pr_alo.data(), pr_ahi.data(),
-                        pr_aggs.data())))
+            (rc = split_staged(pr_sel.size(), pr_sel.data(), pr_alo.size(), pr_alo.data(), pr_ahi.data(), &pr_keys,
+                               &pr_aggs)))
             return rc;
         // assemble in segment order
         const uint8_t *sk = static_cast<const uint8_t *>(in.start_keys), *ek = static_cast<const uint8_t *>(in.end_keys);
@@ -1003,7 +1035,7 @@ struct rh_store {
                 uint8_t cur_kind = in.start_kinds[j];
                 const uint8_t *cur = s0;
                 for (uint64_t c = 0; c < p.ncuts; c++) {
-                    const uint8_t *cut = pr_keys.data() + (p.first_sel + c) * kl;
+                    const uint8_t *cut = pr_keys + (p.first_sel + c) * kl;
                     put(cur_kind, cur, 1, cut, pr_aggs[p.first_agg + c]);
                     cur_kind = 1;
                     cur = cut;
@@ -1030,7 +1062,8 @@ struct rh_store {
         results.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
-        q_kind.release();
+        q_in.release(); q_res.release();
+        stage_in.release(); stage_out.release(); stage_out2.release();
         snap.release();
         scratch.release();
         if (dep) (void)hipEventDestroy(dep);

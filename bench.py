@@ -72,6 +72,8 @@ def parse():
                    help="config5: fraction of each batch that re-stamps existing keys (the new - old delta)")
     p.add_argument("--e2e", action="store_true", help="also time host->device->host end to end (DESIGN.md)")
     p.add_argument("--diffs", type=int, default=10_000, help="rbsr: keys in which the two replicas differ")
+    p.add_argument("--dual", action="store_true",
+                   help="dated configs: both lifts of Replica::map_insert (dated + projection) per record")
     p.add_argument("--check", type=int, default=1, help="oracle spot-check of a sample before timing")
     return p.parse_args()
 
@@ -96,7 +98,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     import rsos_hip
-    from rsos_hip import RecordSchema, lift_records, range_aggregates, reduce_blocks, combine_aggregates
+    from rsos_hip import RecordSchema, lift_records, lift_dual, range_aggregates, reduce_blocks, combine_aggregates
     from rsos_hip.synth import make_records
     from rsos_hip.shard import equal_count_ranges, gather_async, local_ranges
 
@@ -112,6 +114,10 @@ def main():
     rec_bytes = schema.record_len()                     # canonical bytes BLAKE3 absorbs
     read_bytes = schema.key_row + schema.value_row + (20 if schema.dated_kind else 0)
     hbm_bytes = read_bytes + 32                          # + fingerprint write
+    dual = args.dual and kind == "dated"
+    if dual:  # + the projection's canonical bytes and its fingerprint (src/replica/write.rs:44-45)
+        rec_bytes += schema.with_kind(2).record_len()
+        hbm_bytes += 32
 
     # this rank's shard of the globally sorted key space: global rows [rank*n, (rank+1)*n)
     cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
@@ -125,6 +131,8 @@ def main():
     nb = (n + 255) // 256
     fps = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     bs = torch.empty((nb, 32), dtype=torch.uint8, device=dev)
+    dual_out = (fps, bs, torch.empty((n, 32), dtype=torch.uint8, device=dev),
+                torch.empty((nb, 32), dtype=torch.uint8, device=dev)) if dual else None
     # double-buffered per-step aggregates: step k's all_gather runs while step k+1 lifts
     outs = [torch.empty((R, 5), dtype=torch.int64, device=dev) for _ in range(2)]
     gath = [torch.empty((world, R, 5), dtype=torch.int64, device=dev) for _ in range(2)] if world > 1 else None
@@ -152,7 +160,10 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        lift_records(schema, cols, fps=fps, bsums=bs)
+        if dual:
+            lift_dual(schema, cols, out=dual_out)
+        else:
+            lift_records(schema, cols, fps=fps, bsums=bs)
         if timed:
             e1.record(stream)
             lift_ms.append((e0, e1))
@@ -196,7 +207,7 @@ def main():
     recs = total * args.steps
     gib_s = recs * rec_bytes / elapsed / 2**30
     achieved = hbm_bytes * n / lift_avg_s / 1e9
-    traffic = load_traffic(args.config, n)
+    traffic = None if dual else load_traffic(args.config, n)
     line = {
         "metric": "fingerprint-hash GiB/s + M records/s (device-resident) at 1/2/4/8 MI355X",
         "value": round(gib_s, 2),
@@ -211,22 +222,24 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (seeded, SURVEY §8d generator), resident in HBM before timing",
-        "config": {"workload": desc, "records_per_gpu": n, "records_total": total, "ranges": R,
+        "config": {"workload": desc + ("; both lifts of Replica::map_insert (dated + projection)" if dual else ""),
+                   "records_per_gpu": n, "records_total": total, "ranges": R,
                    "canonical_bytes_per_record": rec_bytes, "hbm_bytes_per_record": hbm_bytes,
                    "parallelism": f"key-range shards x{world}" + (
                        (" + RCCL all_gather (overlapped with the next lift)" if dist.get_backend() == "nccl"
                         else " + gloo all_gather (rehearsal)") if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "rh::k_lift (lift + block sums)", "kernel_avg_us": round(lift_avg_s * 1e6, 2)},
+                     "kernel": "rh::k_lift_dual (dated + projection lifts + block sums)" if dual else
+                               "rh::k_lift (lift + block sums)", "kernel_avg_us": round(lift_avg_s * 1e6, 2)},
         "oracle_spot_check": checked,
         "total_aggregate_size": int(root[:, 4].sum()),
     }
-    valu = load_valu(args.config, n, lift_avg_s)
+    valu = None if dual else load_valu(args.config, n, lift_avg_s)
     if valu:
         line["valu"] = valu
     if args.cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample)
+        line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample, dual)
     if args.e2e:
         line["end_to_end"] = end_to_end(schema, cols, n)
     print(json.dumps(line), flush=True)
@@ -590,10 +603,12 @@ def spot_check(schema, cols, n):
     return f"bit-exact on {m} rows"
 
 
-def cpu_baseline(schema, cols, sample):
+def cpu_baseline(schema, cols, sample, dual=False):
     """The reference's CPU path restated (oracle/oracle.c): FingerprintTreeMap fill -- one lift per
     insert into an order-6 B-tree with per-node Aggregate caches, serial (one writer holds the map's
-    write lock, src/replica/write.rs:117-120), over a bounded sample of the same records."""
+    write lock, src/replica/write.rs:117-120), over a bounded sample of the same records.  dual:
+    Replica::map_insert's two inserts per record, into the dated map and its projection
+    (src/replica/write.rs:44-45)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from rsos_hip.synth import to_host
@@ -607,13 +622,26 @@ def cpu_baseline(schema, cols, sample):
     t0 = time.perf_counter()
     t.fill(0, m)
     dt = time.perf_counter() - t0
+    recs_p = None
+    if dual:
+        sp = schema.with_kind(2)
+        recs_p = O.Records(O.Schema(sp.key_kind, sp.key_len, sp.value_kind, sp.value_len, sp.record_kind, 0),
+                           h["keys"], h.get("values"), None, None, None, h.get("tags"))
+        tp = O.FingerprintTreeMap(recs_p)
+        t0 = time.perf_counter()
+        tp.fill(0, m)
+        dt += time.perf_counter() - t0
+        rec_bytes += sp.record_len()
     fill = {"value": round(m * rec_bytes / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "mrec_per_s": round(m / dt / 1e6, 3),
-            "sample": f"FingerprintTreeMap fill (oracle/oracle.c restatement, serial inserts) of the first "
+            "sample": f"FingerprintTreeMap fill{'s of the dated map and its projection' if dual else ''} "
+                      f"(oracle/oracle.c restatement, serial inserts) of the first "
                       f"{m} records of the benchmark shard, {dt:.2f} s"}
     threads = min(16, os.cpu_count() or 1)
     t0 = time.perf_counter()
     recs.lift(threads=threads)
+    if recs_p is not None:
+        recs_p.lift(threads=threads)
     dt2 = time.perf_counter() - t0
     fill["batch_lift_all_cores"] = {"value": round(m * rec_bytes / dt2 / 2**30, 4), "unit": "GiB/s",
                                     "cores": threads, "mrec_per_s": round(m / dt2 / 1e6, 3)}

@@ -83,17 +83,24 @@ def lift_records(schema: RecordSchema, cols: Dict[str, torch.Tensor], block_sums
     return fps, (bsums if block_sums else None)
 
 
-def lift_dual(schema: RecordSchema, cols: Dict[str, torch.Tensor]):
+def lift_dual(schema: RecordSchema, cols: Dict[str, torch.Tensor], out=None):
     """Both lifts of Replica::map_insert (src/replica/write.rs:44-45) from one read of the
-    records: (dated fps, dated block sums, projection fps, projection block sums)."""
+    records: (dated fps, dated block sums, projection fps, projection block sums).  `out`: the
+    same four tensors, preallocated (reused across calls)."""
     if schema.record_kind != A.REC_DATED:
         raise ValueError("dual lift needs a DATED schema")
     n = _check_cols(schema, cols)
     dev = next(iter(cols.values())).device
-    fd = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    fp = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    bd = torch.empty((block_sums_for(n), 32), dtype=torch.uint8, device=dev)
-    bp = torch.empty((block_sums_for(n), 32), dtype=torch.uint8, device=dev)
+    if out is not None:
+        fd, bd, fp, bp = out
+        if fd.shape != (n, 32) or fp.shape != (n, 32) or bd.shape[0] < block_sums_for(n) or \
+                bp.shape[0] < block_sums_for(n):
+            raise ValueError("out tensors have the wrong shape")
+    else:
+        fd = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        fp = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        bd = torch.empty((block_sums_for(n), 32), dtype=torch.uint8, device=dev)
+        bp = torch.empty((block_sums_for(n), 32), dtype=torch.uint8, device=dev)
     s, c = schema.c(), _columns(cols)
     A.check(A.lib().rh_lift_dual_async(C.byref(s), C.byref(c), n, _ptr(fd), _ptr(bd), _ptr(fp), _ptr(bp),
                                        _stream()), "rh_lift_dual_async")

@@ -378,3 +378,51 @@ def test_gpu_soa_reconciliation_and_wire(gpu, oracle_lib):
 
 def _outcome(o):
     return (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["u32_u32", "b32_b64", "u64_b64"])
+def test_gpu_reconciliation_other_key_types(gpu, oracle_lib, shape):
+    """The round on every store key type (u32 numeric order, 32-byte memcmp order, u64): the
+    native round equals the literal driver over the FTM, round by round."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    rng = np.random.default_rng(21)
+    kk, kl, vname, vl = {"u32_u32": ("u32", 4, "u32", 4), "b32_b64": ("bytes32", 32, "bytes64", 64),
+                         "u64_b64": ("u64", 8, "bytes64", 64)}[shape]
+    schema = RecordSchema.plain(kk, vname)
+    n = 12_000
+    if kk == "u32":
+        keys = np.unique(rng.integers(0, 2**32, n + 100, dtype=np.uint64).astype(np.uint32))[:n]
+        krows = keys.view(np.uint8).reshape(-1, 4)
+        key_int = True
+    elif kk == "u64":
+        keys = np.unique(rng.integers(0, 2**63, n + 100, dtype=np.uint64))[:n]
+        krows = keys.view(np.uint8).reshape(-1, 8)
+        key_int = True
+    else:
+        krows = np.unique(rng.integers(0, 256, (n + 100, kl), dtype=np.uint8), axis=0)[:n]
+        key_int = False
+    n = len(krows)
+    vals = rng.integers(0, 256, (n, vl), dtype=np.uint8)
+    drop = rng.choice(n, 40, replace=False)
+    keep = np.ones(n, bool)
+    keep[drop[:20]] = False
+    vals_b = vals.copy()
+    vals_b[drop[20:]] ^= 0x5A
+    stores, views = [], []
+    for kr, vv in ((krows, vals), (krows[keep], vals_b[keep])):
+        st = GpuFingerprintStore(schema)
+        st.load_bulk({"keys": np.ascontiguousarray(kr), "values": np.ascontiguousarray(vv)})
+        sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+        t = _ftm(O.Records(sc, np.ascontiguousarray(kr), np.ascontiguousarray(vv)))
+        stores.append(st)
+        views.append(OR.FtmView(t, key_int))
+    want = reconcile(views[0], views[1],
+                     lambda v, act, ch, en: OR.protocol_round(v, OR.fixed_fan_out(16), act, ch, en), OR.initial_ranges)
+    got = reconcile(stores[0], stores[1], lambda v, act, ch, en: _outcome(R.protocol_round(v, act, ch, en)),
+                    R.initial_ranges)
+    assert len(got[0]) == len(want[0]) > 2
+    for (gc, ge, go), (wc, we, wo) in zip(got[0], want[0]):
+        assert go == wo and ge == we and gc == wc
+    for st in stores:
+        st.close()

@@ -210,6 +210,138 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
     }
 }
 
+/// What one batched round did (the fields of `rbsr::RoundOutcome`, which has no public
+/// constructor).
+#[derive(Clone, Copy, Debug, Default, PartialEq, Eq)]
+pub struct RoundCounts {
+    pub skipped: usize,
+    pub enumerated: usize,
+    pub split: usize,
+    pub children: usize,
+    pub dropped_malformed: usize,
+}
+
+fn start_key<K: Clone>(b: Bound<&K>) -> Option<K> {
+    match b {
+        Bound::Included(k) | Bound::Excluded(k) => Some(k.clone()),
+        Bound::Unbounded => None,
+    }
+}
+
+impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
+    /// One `rbsr` protocol round under `FixedFanOut(fan_out)` with the store's questions
+    /// batched (`protocol_round_with_policy`, rbsr/src/protocol.rs:212-317; cutoffs
+    /// policy/cutoffs.rs; stride `ceil(span / b)`, fixed_fan_out.rs).  Ranks and `select` come
+    /// from the host mirror; every segment's local aggregate is one device call, and every SPLIT
+    /// child's aggregate a second one -- two device round trips per round instead of one per
+    /// question.  Outputs are appended in the reference's order.
+    pub fn protocol_round_fixed(
+        &self,
+        fan_out: usize,
+        active: Vec<rbsr::RangeAggregate<K>>,
+        child_ranges: &mut Vec<rbsr::RangeAggregate<K>>,
+        enumeration_ranges: &mut Vec<rbsr::EnumerationRange<K>>,
+    ) -> RoundCounts {
+        let b = fan_out.max(2); // FanOut::new
+        let size = self.entries.len();
+        let mut counts = RoundCounts::default();
+        // step 1: raw ranks of both bounds (BoundedRange::parse), then all local aggregates
+        let raw: Vec<(usize, usize)> = active
+            .iter()
+            .map(|s| (self.bound_rank(s.start_bound(), true), self.bound_rank(s.end_bound(), false)))
+            .collect();
+        let clamped: Vec<(usize, usize)> = raw.iter().map(|&(l, h)| (l, h.max(l))).collect(); // inverted -> ZERO
+        let local = self.aggregates_by_rank(&clamped);
+        // the decisions, in segment order; SPLIT children planned as rank ranges
+        enum Plan {
+            Drop,
+            Skip,
+            Enumerate,
+            Split { cuts: Vec<usize>, first: usize },
+        }
+        let mut plans = Vec::with_capacity(active.len());
+        let mut child_spans: Vec<(usize, usize)> = Vec::new();
+        for (j, seg) in active.iter().enumerate() {
+            let (lo, hi) = raw[j];
+            if hi < lo {
+                counts.dropped_malformed += 1;
+                plans.push(Plan::Drop);
+                continue;
+            }
+            let (si, ei) = (lo.min(size), hi.min(size));
+            let (mine, theirs) = (&local[j], seg.aggregate());
+            let (span, remote) = (mine.size(), theirs.size());
+            let mut stride = 0usize;
+            let mut enumerate = false;
+            let skip = mine == theirs;
+            if !skip {
+                if remote == 0 || (span == 1 && remote == 1) {
+                    enumerate = true;
+                } else if span <= 1 {
+                    stride = 1;
+                } else {
+                    stride = span.div_ceil(b).max(1);
+                    if stride >= span {
+                        enumerate = true; // a non-progressing SPLIT becomes an IDLIST (:263-272)
+                    }
+                }
+            }
+            if skip {
+                counts.skipped += 1;
+                plans.push(Plan::Skip);
+            } else if enumerate {
+                counts.enumerated += 1;
+                if remote != 0 {
+                    counts.children += 1;
+                }
+                plans.push(Plan::Enumerate);
+            } else {
+                counts.split += 1;
+                let cuts: Vec<usize> = (1..).map(|k| si + k * stride).take_while(|&c| c < ei).collect();
+                let first = child_spans.len();
+                if !cuts.is_empty() {
+                    let mut cur = si;
+                    for &c in &cuts {
+                        child_spans.push((cur, c));
+                        cur = c;
+                    }
+                    child_spans.push((cur, ei));
+                }
+                counts.children += cuts.len() + 1;
+                plans.push(Plan::Split { cuts, first });
+            }
+        }
+        // step 2: every child's aggregate in one device call
+        let child_aggs = if child_spans.is_empty() { Vec::new() } else { self.aggregates_by_rank(&child_spans) };
+        for ((seg, plan), mine) in active.into_iter().zip(plans).zip(local) {
+            let (start, end) = (start_key(seg.start_bound()), start_key(seg.end_bound()));
+            match plan {
+                Plan::Drop | Plan::Skip => {}
+                Plan::Enumerate => {
+                    if seg.aggregate().size() != 0 {
+                        child_ranges.push(rbsr::RangeAggregate::new(start.clone(), end.clone(), Aggregate::ZERO));
+                    }
+                    enumeration_ranges.push((seg.start_bound().cloned(), seg.end_bound().cloned()));
+                }
+                Plan::Split { cuts, first } => {
+                    if cuts.is_empty() {
+                        child_ranges.push(rbsr::RangeAggregate::new(start, end, mine)); // the parent itself
+                        continue;
+                    }
+                    let mut cur = start;
+                    for (i, &c) in cuts.iter().enumerate() {
+                        let key = self.entries[c].0.clone(); // select(c)
+                        child_ranges.push(rbsr::RangeAggregate::new(cur, Some(key.clone()), child_aggs[first + i]));
+                        cur = Some(key);
+                    }
+                    child_ranges.push(rbsr::RangeAggregate::new(cur, end, child_aggs[first + cuts.len()]));
+                }
+            }
+        }
+        counts
+    }
+}
+
 impl<K: GpuKey, V: GpuRecord> Drop for HipFingerprintMap<K, V> {
     fn drop(&mut self) {
         // SAFETY: store came from rh_store_create and is destroyed once.

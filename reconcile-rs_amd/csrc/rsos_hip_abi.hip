@@ -596,7 +596,9 @@ struct rh_store {
         RH_HIP(hipStreamWaitEvent(stream, dep, 0));
         return RH_OK;
     }
-    int load_device(const rh_columns &c, size_t m, bool last_wins = false) {
+    // lifted: bfps[cb] and bsums already hold the records' fingerprints and block sums (the
+    // snapshot reload's dual lift wrote them, sized exactly as below)
+    int load_device(const rh_columns &c, size_t m, bool last_wins = false, bool lifted = false) {
         int rc;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
             (rc = counts.ensure(4)))
@@ -610,7 +612,9 @@ struct rh_store {
         if ((rc = bsums.ensure(rh_num_blocks(m) * 32 + 32))) return rc;
         if (m) {
             RH_HIP(hipMemcpyAsync(bkeys[cb].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
-            if ((rc = lift_dispatch(schema, c, m, bfps[cb].p, bsums.p, nullptr, nullptr, false, stream))) return rc;
+            if (!lifted &&
+                (rc = lift_dispatch(schema, c, m, bfps[cb].p, bsums.p, nullptr, nullptr, false, stream)))
+                return rc;
             RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
             RH_HIP(kops->check_sorted(bkeys[cb].p, m, flag.p, stream));
         }
@@ -1486,10 +1490,22 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
     rc = snapshot_decode_into(ds, key_form, dev, len, n, cols, a->scratch, a->stream, &inf);
     if (!on_device) a->snap.release();
     if (rc) return rc;
+    // both stores: Replica::map_insert's two lifts in one read of the columns (the dual kernel
+    // writes straight into each store's fingerprint and block-sum buffers)
+    const bool dual = dated && proj && n;
+    if (dual) {
+        for (rh_store *x : {dated, proj})
+            if ((rc = x->bfps[x->cb].ensure(n * 32 + 64)) || (rc = x->bsums.ensure(rh_num_blocks(n) * 32 + 32)))
+                return rc;
+        if ((rc = lift_dispatch(ds, cols, n, dated->bfps[dated->cb].p, dated->bsums.p, proj->bfps[proj->cb].p,
+                                proj->bsums.p, true, a->stream)))
+            return rc;
+        if ((rc = proj->after(a->stream))) return rc;
+    }
     for (rh_store *x : {dated, proj}) {
         if (!x) continue;
         RH_HIP(hipSetDevice(x->device));
-        if ((rc = x->load_device(cols, n, true))) return rc;
+        if ((rc = x->load_device(cols, n, true, dual))) return rc;
         inf.keys = x->nb;
     }
     if (info) *info = inf;

@@ -124,11 +124,18 @@ int rh_lift_dual_async(const rh_schema *schema, const rh_columns *dev_cols, size
 
 /* Generic path: BLAKE3 of pre-encoded canonical bytes (rsos::encoding::encode_to_vec of
  * k then v, public-api/rsos.txt:61), record i = bytes[offsets[i] .. offsets[i+1]).
- * bytes_len: the readable size of dev_bytes, a multiple of 4 and >= offsets[n] (pad the
- * buffer).  Nothing is read at or past bytes_len: offsets that decrease or exceed it are a
+ * dev_bytes 4-byte aligned; bytes_len: its readable size, a multiple of 4 and >= offsets[n]
+ * (pad the buffer).  Nothing is read at or past bytes_len: offsets that decrease or exceed it are a
  * caller error that yields wrong fingerprints, not a fault.  Fully asynchronous.          */
 int rh_lift_encoded_async(const uint8_t *dev_bytes, size_t bytes_len, const uint64_t *dev_offsets, size_t n,
                           uint8_t *dev_fps, uint8_t *dev_block_sums, void *stream);
+
+/* Generic path for fixed-length encodings (a K / V pair whose canonical encoding always has
+ * one length: fixed-width integers, arrays, fixed-size structs): record i =
+ * bytes[i * record_len .. (i + 1) * record_len), no offsets.  dev_bytes 4-byte aligned;
+ * bytes_len: its readable size, a multiple of 4 and >= n * record_len (RH_ERR_ARG otherwise).               */
+int rh_lift_fixed_async(const uint8_t *dev_bytes, size_t bytes_len, size_t record_len, size_t n,
+                        uint8_t *dev_fps, uint8_t *dev_block_sums, void *stream);
 
 /* out[g] = Σ in[256 g .. 256 g + 255]  (32-byte fingerprints, mod 2^256) */
 int rh_reduce_blocks_async(const uint8_t *dev_in, size_t n_in, uint8_t *dev_out, void *stream);

@@ -142,28 +142,25 @@ __global__ __launch_bounds__(256) void k_lift_encoded_short(const uint8_t *bytes
 // shorter records return at once)
 constexpr int ENC_STACK = 40;
 
-__global__ __launch_bounds__(256) void k_lift_encoded_long(const uint8_t *bytes, const uint64_t *offs,
-                                                           uint64_t n, uint64_t limit, uint8_t *fps) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    uint64_t start, len;
-    record_span(offs, i, limit, start, len);
-    if (len <= (uint64_t)CHUNK_LEN) return;
-    const uint64_t nchunks = (len + CHUNK_LEN - 1) / CHUNK_LEN;
+// BLAKE3 of bytes [start, start + len), any length: chunk CVs on a stack, parent nodes
+__device__ __forceinline__ void hash_span(const uint8_t *bytes, uint64_t start, uint64_t len, uint64_t limit,
+                                          uint32_t cv[8]) {
+    const uint64_t nchunks = len == 0 ? 1 : (len + CHUNK_LEN - 1) / CHUNK_LEN;
     uint32_t stk[ENC_STACK][8];
     int sp = 0;
-    uint32_t cv[8];
     for (uint64_t c = 0; c < nchunks; c++) {
         const uint64_t cbeg = c * CHUNK_LEN;
         const uint64_t clen = len - cbeg < (uint64_t)CHUNK_LEN ? len - cbeg : (uint64_t)CHUNK_LEN;
-        const uint32_t nb = (uint32_t)((clen + 63) / 64);
+        const uint32_t nb = clen == 0 ? 1u : (uint32_t)((clen + 63) / 64);
         cv_iv(cv);
         for (uint32_t b = 0; b < nb; b++) {
             const uint64_t boff = cbeg + 64ull * b;
             const uint32_t blen = (uint32_t)(len - boff < 64 ? len - boff : 64);
             uint32_t m[16];
-            load_block_bytes(bytes, start + boff, blen, limit, m);
-            const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b == nb - 1 ? CHUNK_END : 0u);
+            if (start + boff + 68 <= limit) load_block_fast(bytes, start + boff, blen, blen < 64, m);
+            else load_block_bytes(bytes, start + boff, blen, limit, m);
+            uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b == nb - 1 ? CHUNK_END : 0u);
+            if (nchunks == 1 && b == nb - 1) flags |= ROOT;
             compress(cv, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
         }
         if (c + 1 < nchunks) {
@@ -179,11 +176,82 @@ __global__ __launch_bounds__(256) void k_lift_encoded_long(const uint8_t *bytes,
             sp++;
         }
     }
-    for (int s = sp - 1; s >= 0; s--) {
+    for (int s2 = sp - 1; s2 >= 0; s2--) {
         uint32_t p[8];
-        parent(p, stk[s], cv, s == 0 ? ROOT : 0u);
+        parent(p, stk[s2], cv, s2 == 0 ? ROOT : 0u);
         for (int q = 0; q < 8; q++) cv[q] = p[q];
     }
+}
+
+__global__ __launch_bounds__(256) void k_lift_encoded_long(const uint8_t *bytes, const uint64_t *offs,
+                                                           uint64_t n, uint64_t limit, uint8_t *fps) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t start, len;
+    record_span(offs, i, limit, start, len);
+    if (len <= (uint64_t)CHUNK_LEN) return;
+    uint32_t cv[8];
+    hash_span(bytes, start, len, limit, cv);
+    store_fp(fps, i, cv);
+}
+
+// ---- fixed-length encodings -------------------------------------------------------------------
+// Every record `len` bytes at stride `len` (a K / V pair whose canonical encoding has one length:
+// fixed-width integers, arrays, fixed-size structs).  No offsets to read, and every lane of a wave
+// runs the same blocks in lockstep.
+// ALIGNED (len % 4 == 0): every block starts on a dword, so its words load as they are -- no
+// funnel shift -- and the last block's byte count (the same in every lane) masks whole words.
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_lift_fixed_short(const uint8_t *bytes, uint32_t len, uint64_t n,
+                                                          uint64_t limit, uint8_t *fps) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t start = i * len;
+    const uint32_t nb = len == 0 ? 1u : (len + 63) / 64;
+    uint32_t cv[8];
+    cv_iv(cv);
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t boff = 64u * b;
+        const uint32_t blen = len - boff < 64u ? len - boff : 64u;
+        uint32_t m[16];
+        if (ALIGNED && blen == 64 && start + boff + 64 <= limit) {  // a full block (uniform branch)
+            const u32x4_a4 *p = reinterpret_cast<const u32x4_a4 *>(bytes + start + boff);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const u32x4_a4 v = p[q];
+                m[4 * q] = v.x;
+                m[4 * q + 1] = v.y;
+                m[4 * q + 2] = v.z;
+                m[4 * q + 3] = v.w;
+            }
+        } else if (ALIGNED && start + boff + 64 <= limit) {
+            const u32x4_a4 *p = reinterpret_cast<const u32x4_a4 *>(bytes + start + boff);
+            const uint32_t words = blen / 4;  // uniform: whole words only
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const u32x4_a4 v = (uint32_t)(4 * q) < words ? p[q] : u32x4_a4{0u, 0u, 0u, 0u};
+                m[4 * q] = (uint32_t)(4 * q) < words ? v.x : 0u;
+                m[4 * q + 1] = (uint32_t)(4 * q + 1) < words ? v.y : 0u;
+                m[4 * q + 2] = (uint32_t)(4 * q + 2) < words ? v.z : 0u;
+                m[4 * q + 3] = (uint32_t)(4 * q + 3) < words ? v.w : 0u;
+            }
+        } else if (start + boff + 68 <= limit) {
+            load_block_fast(bytes, start + boff, blen, blen < 64, m);
+        } else {
+            load_block_bytes(bytes, start + boff, blen, limit, m);
+        }
+        const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | ROOT) : 0u);
+        compress(cv, m, 0u, 0u, blen, flags);
+    }
+    store_fp(fps, i, cv);
+}
+
+__global__ __launch_bounds__(256) void k_lift_fixed_long(const uint8_t *bytes, uint64_t len, uint64_t n,
+                                                         uint64_t limit, uint8_t *fps) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t cv[8];
+    hash_span(bytes, i * len, len, limit, cv);
     store_fp(fps, i, cv);
 }
 
@@ -377,6 +445,19 @@ hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStre
 
 hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_t st) {
     hipLaunchKernelGGL(k_total, dim3(1), dim3(256), 0, st, in, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_lift_fixed(const uint8_t *bytes, uint64_t len, uint64_t n, uint64_t limit, uint8_t *fps,
+                             uint8_t *bsums, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const dim3 g((uint32_t)((n + 255) / 256));
+    if (len <= (uint64_t)CHUNK_LEN && len % 4 == 0)
+        hipLaunchKernelGGL(k_lift_fixed_short<true>, g, dim3(256), 0, st, bytes, (uint32_t)len, n, limit, fps);
+    else if (len <= (uint64_t)CHUNK_LEN)
+        hipLaunchKernelGGL(k_lift_fixed_short<false>, g, dim3(256), 0, st, bytes, (uint32_t)len, n, limit, fps);
+    else hipLaunchKernelGGL(k_lift_fixed_long, g, dim3(256), 0, st, bytes, len, n, limit, fps);
+    if (bsums) hipLaunchKernelGGL(k_reduce, g, dim3(256), 0, st, fps, 32u, n, bsums);
     return hipGetLastError();
 }
 

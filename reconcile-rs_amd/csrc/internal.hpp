@@ -17,6 +17,9 @@ bool schema_instantiated(int kk, int kl, int vk, int vl);
 
 hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint64_t n, uint64_t limit,
                                uint8_t *fps, uint8_t *bsums, hipStream_t st);
+// fixed-length records: record i = bytes[i * len, (i + 1) * len), read limit `limit`
+hipError_t launch_lift_fixed(const uint8_t *bytes, uint64_t len, uint64_t n, uint64_t limit, uint8_t *fps,
+                             uint8_t *bsums, hipStream_t st);
 // stride: bytes between consecutive level-0 entries (32 = a fingerprint array)
 hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st, uint32_t stride = 32);
 // out[0..3] = Σ of n 256-bit entries (n small: one workgroup)

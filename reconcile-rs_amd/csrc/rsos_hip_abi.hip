@@ -237,9 +237,23 @@ int rh_lift_encoded_async(const uint8_t *bytes, size_t bytes_len, const uint64_t
     if (!offsets || !fps) return fail(RH_ERR_ARG, "offsets / fps is NULL");
     if (bytes_len && !bytes) return fail(RH_ERR_ARG, "bytes is NULL");
     if (bytes_len % 4) return fail(RH_ERR_ARG, "bytes_len must be a multiple of 4 (pad the buffer)");
+    if (reinterpret_cast<uintptr_t>(bytes) % 4) return fail(RH_ERR_ARG, "bytes must be 4-byte aligned");
     if (!aligned16(fps) || !aligned16(block_sums)) return fail(RH_ERR_ARG, "outputs must be 16-byte aligned");
     // no host round trip: bytes_len bounds every read, whatever the offsets say
     RH_HIP(rh::launch_lift_encoded(bytes, offsets, n, bytes_len, fps, block_sums, static_cast<hipStream_t>(stream)));
+    return RH_OK;
+}
+
+int rh_lift_fixed_async(const uint8_t *bytes, size_t bytes_len, size_t record_len, size_t n, uint8_t *fps,
+                        uint8_t *block_sums, void *stream) {
+    if (n == 0) return RH_OK;
+    if (!fps) return fail(RH_ERR_ARG, "fps is NULL");
+    if (bytes_len && !bytes) return fail(RH_ERR_ARG, "bytes is NULL");
+    if (bytes_len % 4) return fail(RH_ERR_ARG, "bytes_len must be a multiple of 4 (pad the buffer)");
+    if (reinterpret_cast<uintptr_t>(bytes) % 4) return fail(RH_ERR_ARG, "bytes must be 4-byte aligned");
+    if (record_len && n > bytes_len / record_len) return fail(RH_ERR_ARG, "n * record_len exceeds bytes_len");
+    if (!aligned16(fps) || !aligned16(block_sums)) return fail(RH_ERR_ARG, "outputs must be 16-byte aligned");
+    RH_HIP(rh::launch_lift_fixed(bytes, record_len, n, bytes_len, fps, block_sums, static_cast<hipStream_t>(stream)));
     return RH_OK;
 }
 

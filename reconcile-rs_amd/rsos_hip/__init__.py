@@ -17,13 +17,13 @@ from __future__ import annotations
 
 from .fingerprint import Aggregate, Fingerprint
 from .schema import RecordSchema
-from .device import (lift_records, lift_dual, lift_encoded, reduce_blocks, range_aggregates,
+from .device import (lift_records, lift_dual, lift_encoded, lift_fixed, reduce_blocks, range_aggregates,
                      combine_aggregates, block_sums_for)
 from .store import GpuFingerprintStore
 from ._abi import RsosHipError, lib
 
 __all__ = [
-    "Aggregate", "Fingerprint", "RecordSchema", "lift_records", "lift_dual", "lift_encoded",
+    "Aggregate", "Fingerprint", "RecordSchema", "lift_records", "lift_dual", "lift_encoded", "lift_fixed",
     "reduce_blocks", "range_aggregates", "combine_aggregates", "block_sums_for",
     "GpuFingerprintStore", "RsosHipError", "lib",
 ]

@@ -65,6 +65,7 @@ SIGNATURES = [
     ("rh_lift_records_async", C.c_int, [C.POINTER(Schema), C.POINTER(Columns), SZ, U8P, U8P, VP]),
     ("rh_lift_dual_async", C.c_int, [C.POINTER(Schema), C.POINTER(Columns), SZ, U8P, U8P, U8P, U8P, VP]),
     ("rh_lift_encoded_async", C.c_int, [U8P, SZ, U64P, SZ, U8P, U8P, VP]),
+    ("rh_lift_fixed_async", C.c_int, [U8P, SZ, SZ, SZ, U8P, U8P, VP]),
     ("rh_reduce_blocks_async", C.c_int, [U8P, SZ, U8P, VP]),
     ("rh_range_aggregates_async", C.c_int, [U8P, U8P, U8P, SZ, U64P, U64P, SZ, P, VP]),
     ("rh_combine_aggregates_async", C.c_int, [P, SZ, SZ, P, VP]),

@@ -124,6 +124,27 @@ def lift_encoded(data: torch.Tensor, offsets: torch.Tensor, block_sums: bool = T
     return fps, bs
 
 
+def lift_fixed(data: torch.Tensor, record_len: int, n: Optional[int] = None, block_sums: bool = True):
+    """BLAKE3 of fixed-length canonical records: record i = data[i*record_len:(i+1)*record_len]
+    (n defaults to data.numel() // record_len; trailing bytes are padding)."""
+    if data.dtype != torch.uint8 or not data.is_cuda or data.dim() != 1:
+        raise ValueError("data must be a 1-D uint8 device tensor")
+    if record_len < 0:
+        raise ValueError("record_len must be >= 0")
+    if n is None:
+        if record_len == 0:
+            raise ValueError("n is required when record_len is 0")
+        n = data.numel() // record_len
+    dev = data.device
+    fps = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    bs = torch.empty((block_sums_for(n), 32), dtype=torch.uint8, device=dev) if block_sums else None
+    if data.numel() % 4:
+        data = torch.cat([data, torch.zeros(4 - data.numel() % 4, dtype=torch.uint8, device=dev)])
+    A.check(A.lib().rh_lift_fixed_async(_ptr(data), data.numel(), record_len, n, _ptr(fps), _ptr(bs), _stream()),
+            "rh_lift_fixed_async")
+    return fps, bs
+
+
 def reduce_blocks(x: torch.Tensor) -> torch.Tensor:
     """out[g] = Σ x[256g .. 256g+255] (mod 2^256)."""
     n = x.shape[0]

@@ -109,6 +109,8 @@ extern "C" {
                               stream: *mut c_void) -> c_int;
     pub fn rh_lift_encoded_async(dev_bytes: *const u8, bytes_len: usize, dev_offsets: *const u64, n: usize,
                                  dev_fps: *mut u8, dev_block_sums: *mut u8, stream: *mut c_void) -> c_int;
+    pub fn rh_lift_fixed_async(dev_bytes: *const u8, bytes_len: usize, record_len: usize, n: usize,
+                               dev_fps: *mut u8, dev_block_sums: *mut u8, stream: *mut c_void) -> c_int;
     pub fn rh_reduce_blocks_async(dev_in: *const u8, n_in: usize, dev_out: *mut u8, stream: *mut c_void) -> c_int;
     pub fn rh_range_aggregates_async(dev_fps: *const u8, dev_block_sums: *const u8, dev_super_sums: *const u8,
                                      n: usize, dev_lo: *const u64, dev_hi: *const u64, r: usize,

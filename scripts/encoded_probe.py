@@ -4,7 +4,7 @@ of 0..128 bytes, i.e. 16..144 B)."""
 import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reconcile-rs_amd"))
 import torch
-from rsos_hip import lift_encoded
+from rsos_hip import lift_encoded, lift_fixed
 
 def timeit(fn, reps=10):
     fn(); torch.cuda.synchronize()
@@ -21,6 +21,8 @@ data = torch.randint(0, 256, (n * 120,), dtype=torch.uint8, device="cuda", gener
 offs = torch.arange(0, n + 1, dtype=torch.int64, device="cuda") * 120
 t = timeit(lambda: lift_encoded(data, offs))
 print(f"fixed 120 B: {t*1e6:.0f} us  {n/t/1e9:.2f} G rec/s  {n*120/t/1e9:.0f} GB/s")
+t = timeit(lambda: lift_fixed(data, 120))
+print(f"fixed 120 B via rh_lift_fixed_async (no offsets): {t*1e6:.0f} us  {n/t/1e9:.2f} G rec/s  {n*120/t/1e9:.0f} GB/s")
 lens = 16 + torch.randint(0, 129, (n,), dtype=torch.int64, device="cuda", generator=g)
 offs = torch.zeros(n + 1, dtype=torch.int64, device="cuda"); offs[1:] = torch.cumsum(lens, 0)
 tot = int(offs[-1])

@@ -116,3 +116,11 @@ def test_encoded_lift_rejects_unpadded_length(rsos_hip_lib):
     buf = (C.c_uint64 * 8)()
     rc = A.lib().rh_lift_encoded_async(C.addressof(buf), 7, C.addressof(buf), 1, C.addressof(buf), None, None)
     assert rc == A.ERR_ARG and b"multiple of 4" in A.lib().rh_last_error()
+
+
+def test_fixed_lift_rejects_short_buffer(rsos_hip_lib):
+    """n * record_len must fit in bytes_len: checked before anything is launched."""
+    from rsos_hip import _abi as A
+    buf = (C.c_uint64 * 8)()
+    rc = A.lib().rh_lift_fixed_async(C.addressof(buf), 64, 120, 1, C.addressof(buf), None, None)
+    assert rc == A.ERR_ARG and b"exceeds" in A.lib().rh_last_error()

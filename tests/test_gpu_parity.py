@@ -202,6 +202,41 @@ def test_encoded_short_mix(gpu, oracle_lib):
     assert int.from_bytes(bs.cpu().numpy()[0].tobytes(), "little") == tot
 
 
+@pytest.mark.parametrize("length", [0, 1, 4, 63, 64, 65, 120, 128, 1023, 1024, 1025, 2048, 3000])
+def test_fixed_length_records(gpu, oracle_lib, length):
+    """rh_lift_fixed_async: one length for every record (one chunk, exact blocks, multi-chunk),
+    several workgroups and a ragged last one; block sums over the fingerprints."""
+    import torch
+    from rsos_hip import lift_fixed
+    rng = np.random.default_rng(length)
+    n = 700
+    raw = rng.integers(0, 256, n * length + 3, dtype=np.uint8)  # + bytes past the last record
+    blobs = [raw[i * length:(i + 1) * length].tobytes() for i in range(n)]
+    fps, bs = lift_fixed(torch.from_numpy(raw).cuda(), length, n=n)
+    want = oracle_lib.lift_encoded(blobs, threads=8)
+    assert np.array_equal(fps.cpu().numpy(), want)
+    tot = sum(int.from_bytes(f.tobytes(), "little") for f in want[256:512]) % (1 << 256)
+    assert int.from_bytes(bs.cpu().numpy()[1].tobytes(), "little") == tot
+
+
+def test_fixed_equals_encoded_full_size(gpu, oracle_lib):
+    """10 M records of 120 B: the fixed-length path equals the offsets path everywhere and the
+    oracle on a sample."""
+    import torch
+    from rsos_hip import lift_encoded, lift_fixed
+    n, L = 10_000_000, 120
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    a, ba = lift_fixed(data, L)
+    b, bb = lift_encoded(data, torch.arange(0, n + 1, dtype=torch.int64, device="cuda") * L)
+    assert torch.equal(a, b) and torch.equal(ba, bb)
+    idx = np.random.default_rng(1).integers(0, n, 300)
+    host = data.view(n, L)[torch.from_numpy(idx).cuda()].cpu().numpy()
+    want = oracle_lib.lift_encoded([r.tobytes() for r in host], threads=8)
+    assert np.array_equal(a[torch.from_numpy(idx).cuda()].cpu().numpy(), want)
+
+
 def test_encoded_malformed_offsets_are_bounded(gpu, oracle_lib):
     """Offsets that decrease or run past the buffer: no fault, no runaway loop; well-formed
     records in the same launch still hash correctly."""

@@ -1,0 +1,213 @@
+"""The reference's own tests of this path, restated against the GPU store.
+
+  aggregate_matches_brute_force_for_every_boundary_pair
+      rsos/src/fingerprint_tree_map/tests/aggregate.rs:59-78 (100 u32/u32 keys, every lo..hi)
+  big_test          tests/basic.rs: 1,000 random u64/u64 inserts, the root checked
+                    after each, partition additivity, rank / select
+  test_compare / diff / reconcile
+      tests/diff.rs:12-108: the two-tree diff driver over rbsr, its expected ranges, and
+      reconcile() bringing both trees to the same content
+
+The reference's trees hold `&str` values in test_compare; the ranges the diff reports depend only
+on which keys differ, so the restatement uses u32 values (the store needs fixed-width values).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import rbsr as OR  # oracle/rbsr.py
+
+
+def _u32_recs(pairs):
+    pairs = sorted(pairs)
+    k = np.array([a for a, _ in pairs], np.uint32)
+    v = np.array([b for _, b in pairs], np.uint32)
+    n = len(pairs)
+    return O.Records(O.Schema(O.KEY_U32, 4, O.VAL_U32, 4, O.REC_PLAIN, 0), k.view(np.uint8).reshape(n, 4),
+                     v.view(np.uint8).reshape(n, 4))
+
+
+def _ftm(recs):
+    t = O.FingerprintTreeMap(recs)
+    t.fill(0, recs.n)
+    return t
+
+
+def oracle_diff(a, b):
+    """tests/diff.rs:12-37 over the oracle: (ranges a owes b, ranges b owes a)."""
+    da, db = [], []
+    seg_a = OR.initial_ranges(a)
+    while seg_a:
+        seg_b = []
+        OR.protocol_round(b, OR.fixed_fan_out(16), seg_a, seg_b, db)
+        seg_a = []
+        OR.protocol_round(a, OR.fixed_fan_out(16), seg_b, seg_a, da)
+    return da, db
+
+
+def gpu_diff(a, b):
+    """The same driver on two GPU stores (rsos_hip.rbsr, the library's native round)."""
+    from rsos_hip import rbsr as R
+    da, db = [], []
+    seg_a = R.initial_ranges(a)
+    while seg_a:
+        seg_b = []
+        R.protocol_round(b, seg_a, seg_b, db)
+        seg_a = []
+        R.protocol_round(a, seg_b, seg_a, da)
+    return da, db
+
+
+def _u32_store(pairs):
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    pairs = sorted(pairs)
+    st = GpuFingerprintStore(RecordSchema.plain("u32", "u32"))
+    k = np.array([a for a, _ in pairs], np.uint32).view(np.uint8).reshape(-1, 4)
+    v = np.array([b for _, b in pairs], np.uint32).view(np.uint8).reshape(-1, 4)
+    st.load_bulk({"keys": k, "values": v})
+    return st
+
+
+TREES = {
+    1: [(25, 1), (50, 2), (75, 3)],
+    4: [(75, 3), (25, 1), (40, 2)],
+    5: [(25, 1), (50, 2), (75, 4)],
+}
+EXPECT = {  # tests/diff.rs:79-95
+    1: ([], []),
+    4: ([(40, 75)], [(40, 75)]),
+    5: ([(75, None)], [(75, None)]),
+}
+
+
+def test_compare_oracle(oracle_lib):
+    t1 = OR.FtmView(_ftm(_u32_recs(TREES[1])), True)
+    for j in (1, 4, 5):
+        tj = OR.FtmView(_ftm(_u32_recs(TREES[j])), True)
+        assert oracle_diff(t1, tj) == EXPECT[j]
+
+
+@pytest.mark.gpu
+def test_compare_gpu(gpu):
+    s1 = _u32_store(TREES[1])
+    for j in (1, 4, 5):
+        sj = _u32_store(TREES[j])
+        assert (s1.aggregate() == sj.aggregate()) == (j == 1)
+        assert gpu_diff(s1, sj) == EXPECT[j]
+        sj.close()
+    s1.close()
+
+
+@pytest.mark.gpu
+def test_aggregate_every_boundary_pair(gpu, oracle_lib):
+    """aggregate.rs:59-78: 100 u32/u32 keys (k, 7k), every range lo..hi for 0 <= lo <= hi <= 100,
+    against a fold of lift -- all 5,151 key ranges in one batched device call."""
+    from rsos_hip.wire import RangeAggregate
+    from rsos_hip import Aggregate
+    entries = [(k, 7 * k) for k in range(100)]
+    st = _u32_store(entries)
+    fps = _u32_recs(entries).lift()
+    fold = [0]
+    for f in fps:
+        fold.append(fold[-1] + int.from_bytes(f.tobytes(), "little"))
+    pairs = [(lo, hi) for lo in range(101) for hi in range(lo, 101)]
+    segs = [RangeAggregate(lo, hi, Aggregate.ZERO) for lo, hi in pairs]
+    raw_lo, raw_hi, aggs = st.resolve_segments(segs)
+    for (lo, hi), a, rl, rh in zip(pairs, aggs, raw_lo, raw_hi):
+        assert (int(rl), int(rh)) == (lo, hi)
+        assert a.size == hi - lo
+        assert a.fingerprint.to_int() == (fold[hi] - fold[lo]) % (1 << 256), (lo, hi)
+    st.close()
+
+
+@pytest.mark.gpu
+def test_big_test_mirror(gpu, oracle_lib):
+    """tests/basic.rs big_test: 1,000 random u64/u64 inserts one at a time; after each the root
+    equals the FTM's; at the end partition additivity agg(..mid) + agg(mid..) == agg(..) for
+    every 50th key and the rank / select inverse."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    rng = np.random.default_rng(90)
+    m = 1000
+    keys = rng.integers(0, 1 << 20, m, dtype=np.uint64)  # repeats: overwrites
+    vals = rng.integers(0, 1 << 62, m, dtype=np.uint64)
+    recs = O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0), keys.view(np.uint8).reshape(m, 8),
+                     vals.view(np.uint8).reshape(m, 8))
+    t = O.FingerprintTreeMap(recs)
+    st = GpuFingerprintStore(RecordSchema.plain("u64", "u64"))
+    st.load_bulk({"keys": np.zeros((0, 8), np.uint8), "values": np.zeros((0, 8), np.uint8)})
+    for i in range(m):
+        st.insert(int(keys[i]), int(vals[i]).to_bytes(8, "little"))
+        t.insert(i)
+        fp, size = t.root()
+        root = st.aggregate()
+        assert root.size == size == len(t)
+        assert root.fingerprint.limbs == tuple(int(x) for x in fp), i
+    uniq = np.unique(keys)
+    whole = st.aggregate()
+    for mid in uniq[::50]:
+        lo = st.aggregate(KeyRange(None, int(mid)))
+        hi = st.aggregate(KeyRange(int(mid), None))
+        assert lo + hi == whole
+    for r in range(0, len(uniq), 37):
+        k = st.select(r)
+        assert k == int(uniq[r]) and st.rank(k) == r
+    st.close()
+
+
+@pytest.mark.gpu
+def test_reconcile_to_convergence(gpu, oracle_lib):
+    """tests/diff.rs reconcile(): the ranges each side owes are sent as records and inserted by
+    the other side (the sender's value wins, local first); afterwards both stores hold the same
+    content -- equal roots, and the root is the FTM fold of the merged content."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    rng = np.random.default_rng(17)
+    common = rng.choice(1 << 30, 6000, replace=False).astype(np.uint64)
+    a = {int(k): int(k) * 3 for k in common[:5800]}
+    b = dict(a)
+    for k in common[5800:5900]:
+        a[int(k)] = 11
+    for k in common[5900:]:
+        b[int(k)] = 22
+    for k in common[:40]:
+        b[int(k)] += 1
+
+    def store(d):
+        ks = np.array(sorted(d), np.uint64)
+        vs = np.array([d[int(k)] for k in ks], np.uint64)
+        st = GpuFingerprintStore(RecordSchema.plain("u64", "u64"))
+        st.load_bulk({"keys": ks.view(np.uint8).reshape(-1, 8), "values": vs.view(np.uint8).reshape(-1, 8)})
+        return st
+
+    sa, sb = store(a), store(b)
+    owed_a, owed_b = gpu_diff(sa, sb)
+    assert owed_a and owed_b
+
+    def send(src_store, src, dst_store, dst, ranges):
+        keys = []
+        for s, e in ranges:
+            keys += [k for k, _ in src_store.enumerate(KeyRange(s, e))]
+        if not keys:
+            return
+        ks = np.array(keys, np.uint64)
+        vs = np.array([src[int(k)] for k in ks], np.uint64)
+        dst_store.apply({"keys": ks.view(np.uint8).reshape(-1, 8), "values": vs.view(np.uint8).reshape(-1, 8)},
+                        np.zeros(len(ks), np.uint8))
+        for k in keys:
+            dst[int(k)] = src[int(k)]
+
+    send(sa, a, sb, b, owed_a)
+    send(sb, b, sa, a, owed_b)
+    assert a == b
+    ra, rb = sa.aggregate(), sb.aggregate()
+    assert ra == rb and ra.size == len(a)
+    ks = np.array(sorted(a), np.uint64)
+    vs = np.array([a[int(k)] for k in ks], np.uint64)
+    t = O.FingerprintTreeMap(O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0),
+                                       ks.view(np.uint8).reshape(-1, 8), vs.view(np.uint8).reshape(-1, 8)))
+    t.fill(0, len(ks))
+    assert ra.fingerprint.limbs == tuple(int(x) for x in t.root()[0])
+    assert gpu_diff(sa, sb) == ([], [])
+    sa.close()
+    sb.close()

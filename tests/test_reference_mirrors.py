@@ -211,3 +211,35 @@ def test_reconcile_to_convergence(gpu, oracle_lib):
     assert gpu_diff(sa, sb) == ([], [])
     sa.close()
     sb.close()
+
+
+@pytest.mark.gpu
+def test_concurrent_readers_one_store(gpu, oracle_lib):
+    """§8b threading: the store is shared by readers under the replica's read lock
+    (src/replica.rs:69,74); the library serialises calls on one store with its own mutex.
+    8 host threads (ctypes releases the GIL inside each call) query one store at once; every
+    answer equals the single-threaded one."""
+    import threading
+    from rsos_hip.store import KeyRange
+    entries = [(k * 3, k) for k in range(20_000)]
+    st = _u32_store(entries)
+    rng = np.random.default_rng(5)
+    queries = [tuple(sorted(int(x) for x in rng.integers(0, 60_000, 2))) for _ in range(300)]
+    want = [(st.aggregate(KeyRange(a, b)), st.rank(a)) for a, b in queries]
+    errors = []
+
+    def reader(seed):
+        order = np.random.default_rng(seed).permutation(len(queries))
+        for j in order:
+            a, b = queries[j]
+            got = (st.aggregate(KeyRange(a, b)), st.rank(a))
+            if got != want[j]:
+                errors.append((j, got, want[j]))
+
+    threads = [threading.Thread(target=reader, args=(s,)) for s in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors[:3]
+    st.close()

@@ -18,7 +18,7 @@ end None = Unbounded else Excluded, agg = (fp limbs tuple, size); enumeration ra
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import List
 
 import numpy as np
 

@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import ipaddress
 import struct
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, Optional, Sequence
 
 import numpy as np
 

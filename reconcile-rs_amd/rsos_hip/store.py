@@ -23,7 +23,7 @@ from typing import Dict, Iterator, Optional, Sequence, Tuple, Union
 import numpy as np
 
 from . import _abi as A
-from .fingerprint import Aggregate, Fingerprint
+from .fingerprint import Aggregate
 from .schema import RecordSchema
 
 Key = Union[bytes, int]

@@ -426,3 +426,65 @@ def test_gpu_reconciliation_other_key_types(gpu, oracle_lib, shape):
         assert go == wo and ge == we and gc == wc
     for st in stores:
         st.close()
+
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(a=st.dictionaries(st.integers(0, 400), st.integers(0, 3), max_size=120),
+       b=st.dictionaries(st.integers(0, 400), st.integers(0, 3), max_size=120),
+       fan=st.sampled_from([0, 2, 3, 16, 1000]), sqrt=st.booleans())
+def test_batched_driver_property(oracle_lib, a, b, fan, sqrt):
+    """Random replica pairs (empty, equal, disjoint, overlapping with changed values) under
+    random policies: the batched driver's host logic reproduces the literal driver round by round,
+    and every key the replicas disagree on is enumerated by a side that holds it."""
+    from rsos_hip import rbsr as R
+    va = OR.FtmView(_ftm(_u32_recs(a.items())), True)
+    vb = OR.FtmView(_ftm(_u32_recs(b.items())), True)
+    pol, decide = (R.SqrtFanOut(), OR.sqrt_fan_out) if sqrt else (R.FixedFanOut(fan), OR.fixed_fan_out(fan))
+    want = reconcile(va, vb, lambda v, act, ch, en: OR.protocol_round(v, decide, act, ch, en), OR.initial_ranges)
+
+    def prod(v, act, ch, en):
+        o = R.protocol_round_with_policy(v, pol, act, ch, en)
+        return (o.skipped, o.enumerated, o.split, o.children, o.dropped_malformed)
+    got = reconcile(BatchedFtm(va), BatchedFtm(vb), prod, R.initial_ranges)
+    assert len(got[0]) == len(want[0])
+    for (gc, ge, go), (wc, we, wo) in zip(got[0], want[0]):
+        assert go == wo and ge == we and gc == wc
+    lt = lambda x, y: x < y  # noqa: E731
+    for k in set(a) | set(b):
+        if a.get(k) != b.get(k):
+            holders = ([want[1]] if k in a else []) + ([want[2]] if k in b else [])
+            assert any(_covered(k, r, lt) for r in holders), k
+
+
+@pytest.mark.gpu
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow,
+                                                                  HealthCheck.function_scoped_fixture])
+@given(a=st.dictionaries(st.integers(0, 2**32 - 1), st.integers(0, 3), max_size=300),
+       b=st.dictionaries(st.integers(0, 2**32 - 1), st.integers(0, 3), max_size=300),
+       fan=st.sampled_from([0, 2, 16]), sqrt=st.booleans())
+def test_gpu_native_round_property(gpu, oracle_lib, a, b, fan, sqrt):
+    """Random u32 replica pairs on GPU stores (including empty ones) under random policies: the
+    library's one-call round equals the literal driver over the FTM, round by round."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+
+    def store(d):
+        pairs = sorted(d.items())
+        s = GpuFingerprintStore(RecordSchema.plain("u32", "u32"))
+        s.load_bulk({"keys": np.array([k for k, _ in pairs], np.uint32).view(np.uint8).reshape(-1, 4),
+                     "values": np.array([v for _, v in pairs], np.uint32).view(np.uint8).reshape(-1, 4)})
+        return s
+    va = OR.FtmView(_ftm(_u32_recs(a.items())), True)
+    vb = OR.FtmView(_ftm(_u32_recs(b.items())), True)
+    pol, decide = (R.SqrtFanOut(), OR.sqrt_fan_out) if sqrt else (R.FixedFanOut(fan), OR.fixed_fan_out(fan))
+    want = reconcile(va, vb, lambda v, act, ch, en: OR.protocol_round(v, decide, act, ch, en), OR.initial_ranges)
+    ga, gb = store(a), store(b)
+    got = reconcile(ga, gb, lambda v, act, ch, en: _outcome(R.protocol_round_with_policy(v, pol, act, ch, en)),
+                    R.initial_ranges)
+    assert len(got[0]) == len(want[0])
+    for (gc, ge, go), (wc, we, wo) in zip(got[0], want[0]):
+        assert go == wo and ge == we and gc == wc
+    ga.close()
+    gb.close()

@@ -243,3 +243,34 @@ def test_concurrent_readers_one_store(gpu, oracle_lib):
         t.join()
     assert not errors, errors[:3]
     st.close()
+
+
+@pytest.mark.gpu
+def test_u64_keys_full_range_order(gpu, oracle_lib):
+    """u64 keys across the whole range (top bit set included) order numerically, as Ord of u64
+    does: ranks, selects, key-range aggregates and an update batch agree with the FTM."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    rng = np.random.default_rng(64)
+    keys = np.unique(np.concatenate([rng.integers(0, 2**64 - 1, 3000, dtype=np.uint64, endpoint=True),
+                                     np.array([0, 1, 2**63 - 1, 2**63, 2**64 - 1], np.uint64)]))
+    n = len(keys)
+    vals = rng.integers(0, 2**63, n, dtype=np.uint64)
+    st = GpuFingerprintStore(RecordSchema.plain("u64", "u64"))
+    st.load_bulk({"keys": keys.view(np.uint8).reshape(n, 8), "values": vals.view(np.uint8).reshape(n, 8)})
+    recs = O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0), keys.view(np.uint8).reshape(n, 8),
+                     vals.view(np.uint8).reshape(n, 8))
+    t = _ftm(recs)
+    assert st.aggregate().fingerprint.limbs == tuple(int(x) for x in t.root()[0])
+    probes = [0, 1, 2**63 - 1, 2**63, 2**63 + 1, 2**64 - 1] + [int(x) for x in rng.integers(0, 2**64 - 1, 200,
+                                                                                              dtype=np.uint64)]
+    for z in probes:
+        assert st.rank(z) == t.rank(np.uint64(z).tobytes()), z
+    for r in range(0, n, 97):
+        assert st.select(r) == int(keys[r])
+    for a, b in zip(probes[::2], probes[1::2]):
+        lo, hi = min(a, b), max(a, b)
+        got = st.aggregate(KeyRange(lo, hi))
+        fp, size = t.aggregate(np.uint64(lo).tobytes(), np.uint64(hi).tobytes())
+        assert got.size == size and got.fingerprint.limbs == tuple(int(x) for x in fp), (lo, hi)
+    st.close()

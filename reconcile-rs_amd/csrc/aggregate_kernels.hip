@@ -201,16 +201,30 @@ __global__ __launch_bounds__(256) void k_lift_encoded_long(const uint8_t *bytes,
 // runs the same blocks in lockstep.
 // ALIGNED (len % 4 == 0): every block starts on a dword, so its words load as they are -- no
 // funnel shift -- and the last block's byte count (the same in every lane) masks whole words.
+// The workgroup's 256-row block sum is formed on the way out (bsums != nullptr), as the schema
+// kernels do, instead of a second pass over the fingerprints.
+__device__ __forceinline__ void fixed_epilogue(uint8_t *fps, uint8_t *bsums, uint64_t i, bool live, uint32_t cv[8]) {
+    if (live) store_fp(fps, i, cv);
+    if (bsums) {  // uniform: every lane reaches the workgroup barriers
+        __shared__ SumTile tile;
+        uint32_t h[8], f[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) h[q] = live ? cv[q] : 0u;
+        block_sum_fps256(h, tile, f);
+        if (threadIdx.x == 0) store_sum(bsums, blockIdx.x, f);
+    }
+}
+
 template <bool ALIGNED>
 __global__ __launch_bounds__(256) void k_lift_fixed_short(const uint8_t *bytes, uint32_t len, uint64_t n,
-                                                          uint64_t limit, uint8_t *fps) {
+                                                          uint64_t limit, uint8_t *fps, uint8_t *bsums) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+    const bool live = i < n;
     const uint64_t start = i * len;
     const uint32_t nb = len == 0 ? 1u : (len + 63) / 64;
     uint32_t cv[8];
     cv_iv(cv);
-    for (uint32_t b = 0; b < nb; b++) {
+    for (uint32_t b = 0; live && b < nb; b++) {
         const uint32_t boff = 64u * b;
         const uint32_t blen = len - boff < 64u ? len - boff : 64u;
         uint32_t m[16];
@@ -243,16 +257,16 @@ __global__ __launch_bounds__(256) void k_lift_fixed_short(const uint8_t *bytes, 
         const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | ROOT) : 0u);
         compress(cv, m, 0u, 0u, blen, flags);
     }
-    store_fp(fps, i, cv);
+    fixed_epilogue(fps, bsums, i, live, cv);
 }
 
 __global__ __launch_bounds__(256) void k_lift_fixed_long(const uint8_t *bytes, uint64_t len, uint64_t n,
-                                                         uint64_t limit, uint8_t *fps) {
+                                                         uint64_t limit, uint8_t *fps, uint8_t *bsums) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+    const bool live = i < n;
     uint32_t cv[8];
-    hash_span(bytes, i * len, len, limit, cv);
-    store_fp(fps, i, cv);
+    if (live) hash_span(bytes, i * len, len, limit, cv);
+    fixed_epilogue(fps, bsums, i, live, cv);
 }
 
 // ---- reductions ------------------------------------------------------------------------------
@@ -453,11 +467,11 @@ hipError_t launch_lift_fixed(const uint8_t *bytes, uint64_t len, uint64_t n, uin
     if (n == 0) return hipSuccess;
     const dim3 g((uint32_t)((n + 255) / 256));
     if (len <= (uint64_t)CHUNK_LEN && len % 4 == 0)
-        hipLaunchKernelGGL(k_lift_fixed_short<true>, g, dim3(256), 0, st, bytes, (uint32_t)len, n, limit, fps);
+        hipLaunchKernelGGL(k_lift_fixed_short<true>, g, dim3(256), 0, st, bytes, (uint32_t)len, n, limit, fps, bsums);
     else if (len <= (uint64_t)CHUNK_LEN)
-        hipLaunchKernelGGL(k_lift_fixed_short<false>, g, dim3(256), 0, st, bytes, (uint32_t)len, n, limit, fps);
-    else hipLaunchKernelGGL(k_lift_fixed_long, g, dim3(256), 0, st, bytes, len, n, limit, fps);
-    if (bsums) hipLaunchKernelGGL(k_reduce, g, dim3(256), 0, st, fps, 32u, n, bsums);
+        hipLaunchKernelGGL(k_lift_fixed_short<false>, g, dim3(256), 0, st, bytes, (uint32_t)len, n, limit, fps,
+                           bsums);
+    else hipLaunchKernelGGL(k_lift_fixed_long, g, dim3(256), 0, st, bytes, len, n, limit, fps, bsums);
     return hipGetLastError();
 }
 

@@ -11,6 +11,15 @@
 
 namespace rh {
 
+// fingerprint i of an array whose entries are `stride` bytes apart (32 for plain fingerprint
+// arrays; the store's delta records carry their 32-byte contribution first, stride 48)
+__device__ __forceinline__ void load_fp(const uint8_t *src, uint64_t i, uint32_t f[8], uint32_t stride = 32) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(src + (uint64_t)stride * i);
+    uint4 a = p[0], b = p[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
 // ---- generic encoded-bytes lift -------------------------------------------------------------
 
 // 16 message words of the block starting at byte `addr`, `blen` (0..64) valid bytes; bytes
@@ -85,8 +94,13 @@ __device__ __forceinline__ void load_block_fast(const uint8_t *base, uint64_t ad
     }
 }
 
+// bsums: the wave's ENC_PER_WAVE records are whole 256-row blocks, so it forms their block sums at
+// the end from the fingerprints just written (its own, and those k_lift_encoded_long wrote before
+// this launch) -- L2-resident reads instead of a second pass.
+static_assert(ENC_PER_WAVE % 256 == 0, "a wave's records must be whole 256-row blocks");
+
 __global__ __launch_bounds__(256) void k_lift_encoded_short(const uint8_t *bytes, const uint64_t *offs, uint64_t n,
-                                                            uint64_t limit, uint8_t *fps) {
+                                                            uint64_t limit, uint8_t *fps, uint8_t *bsums) {
     const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const uint64_t w0 = wave * ENC_PER_WAVE;
     if (w0 >= n) return;  // uniform per wave
@@ -134,6 +148,31 @@ __global__ __launch_bounds__(256) void k_lift_encoded_short(const uint8_t *bytes
                 store_fp(fps, i, cv);
                 active = false;
             }
+        }
+    }
+    if (!bsums) return;
+    __threadfence_block();  // workgroup scope: this wave reads its own stores back (same L2); an agent-scope fence would write back L2
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int blk = 0; blk < ENC_PER_WAVE / 256; blk++) {
+        const uint64_t r0 = w0 + 256ull * blk;
+        if (r0 >= n) break;  // uniform
+        Acc a;
+        acc_zero(a);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t r = r0 + lane + 64 * k;
+            if (r < n) {
+                uint32_t f[8];
+                load_fp(fps, r, f);
+                acc_add_fp(a, f);
+            }
+        }
+        acc_wave_reduce(a);
+        if (lane == 0) {
+            uint32_t f[8];
+            acc_normalise(a, f);
+            store_sum(bsums, r0 / 256, f);
         }
     }
 }
@@ -271,14 +310,6 @@ __global__ __launch_bounds__(256) void k_lift_fixed_long(const uint8_t *bytes, u
 
 // ---- reductions ------------------------------------------------------------------------------
 
-// fingerprint i of an array whose entries are `stride` bytes apart (32 for plain fingerprint
-// arrays; the store's delta records carry their 32-byte contribution first, stride 48)
-__device__ __forceinline__ void load_fp(const uint8_t *src, uint64_t i, uint32_t f[8], uint32_t stride = 32) {
-    const uint4 *p = reinterpret_cast<const uint4 *>(src + (uint64_t)stride * i);
-    uint4 a = p[0], b = p[1];
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
-    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
-}
 
 __global__ __launch_bounds__(256) void k_reduce(const uint8_t *in, uint32_t stride, uint64_t n_in, uint8_t *out) {
     __shared__ SumTile tile;
@@ -442,11 +473,11 @@ hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint6
                                uint8_t *fps, uint8_t *bsums, hipStream_t st) {
     if (n == 0) return hipSuccess;
     const uint64_t waves = (n + ENC_PER_WAVE - 1) / ENC_PER_WAVE;
-    hipLaunchKernelGGL(k_lift_encoded_short, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, st, bytes, offs, n,
-                       limit, fps);
+    // multi-chunk records first: the short kernel's block sums read their fingerprints
     hipLaunchKernelGGL(k_lift_encoded_long, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, bytes, offs, n, limit,
                        fps);
-    if (bsums) hipLaunchKernelGGL(k_reduce, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, fps, 32u, n, bsums);
+    hipLaunchKernelGGL(k_lift_encoded_short, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, st, bytes, offs, n,
+                       limit, fps, bsums);
     return hipGetLastError();
 }
 

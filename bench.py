@@ -83,7 +83,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # a torch.distributed launcher (it sets RANK / WORLD_SIZE) gets the process group even at
+    # world size 1, so the RCCL path (init, all_gather, barrier, all_reduce) also runs on one GPU
+    launched = "RANK" in os.environ and "WORLD_SIZE" in os.environ
+    if world > 1 or launched:
         import torch.distributed as dist
         backend = os.environ.get("BENCH_BACKEND", "nccl")  # gloo: functional rehearsal only
         ngpu = torch.cuda.device_count()
@@ -135,7 +138,7 @@ def main():
                 torch.empty((nb, 32), dtype=torch.uint8, device=dev)) if dual else None
     # double-buffered per-step aggregates: step k's all_gather runs while step k+1 lifts
     outs = [torch.empty((R, 5), dtype=torch.int64, device=dev) for _ in range(2)]
-    gath = [torch.empty((world, R, 5), dtype=torch.int64, device=dev) for _ in range(2)] if world > 1 else None
+    gath = [torch.empty((world, R, 5), dtype=torch.int64, device=dev) for _ in range(2)] if dist is not None else None
     stream = torch.cuda.current_stream()
 
     # correctness gate before timing: sampled rows vs the oracle (rank 0)
@@ -227,7 +230,7 @@ def main():
                    "canonical_bytes_per_record": rec_bytes, "hbm_bytes_per_record": hbm_bytes,
                    "parallelism": f"key-range shards x{world}" + (
                        (" + RCCL all_gather (overlapped with the next lift)" if dist.get_backend() == "nccl"
-                        else " + gloo all_gather (rehearsal)") if world > 1 else "")},
+                        else " + gloo all_gather (rehearsal)") if dist is not None else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "rh::k_lift_dual (dated + projection lifts + block sums)" if dual else

@@ -124,3 +124,32 @@ def test_fixed_lift_rejects_short_buffer(rsos_hip_lib):
     buf = (C.c_uint64 * 8)()
     rc = A.lib().rh_lift_fixed_async(C.addressof(buf), 64, 120, 1, C.addressof(buf), None, None)
     assert rc == A.ERR_ARG and b"exceeds" in A.lib().rh_last_error()
+
+
+def test_product_fails_loudly_without_the_library(tmp_path):
+    """No CPU fallback: with librsos_hip.so missing, the binding raises instead of computing."""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import rsos_hip._abi as A\n"
+        "A.LIB_PATH = %r\n"
+        "try:\n"
+        "    A.lib()\n"
+        "except RuntimeError as e:\n"
+        "    print('raised:', e)\n"
+        "    sys.exit(0)\n"
+        "sys.exit(1)\n"
+    ) % (os.path.join(ROOT, "reconcile-rs_amd"), str(tmp_path / "missing.so"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "HIP path is the only path" in r.stdout
+
+
+def test_host_tensors_are_rejected(rsos_hip_lib):
+    """The device entry points take HBM-resident columns; host tensors are an error, not a CPU path."""
+    import torch
+    from rsos_hip import RecordSchema, lift_records
+    s = RecordSchema.plain("u32", "u32")
+    cols = {"keys": torch.zeros((4, 4), dtype=torch.uint8), "values": torch.zeros((4, 4), dtype=torch.uint8)}
+    with pytest.raises((ValueError, RuntimeError)):
+        lift_records(s, cols)

@@ -274,3 +274,61 @@ def test_u64_keys_full_range_order(gpu, oracle_lib):
         fp, size = t.aggregate(np.uint64(lo).tobytes(), np.uint64(hi).tobytes())
         assert got.size == size and got.fingerprint.limbs == tuple(int(x) for x in fp), (lo, hi)
     st.close()
+
+
+@pytest.mark.gpu
+def test_sharded_store_matches_single(gpu, oracle_lib):
+    """rsos_hip.sharded: one map over several stores (here 3 shards on device 0), answering the
+    Rsos surface and protocol rounds by decomposition, equals one store -- before and after a
+    routed update batch -- and reconciles round by round like the FTM driver."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    from rsos_hip.sharded import ShardedStore
+    from rsos_hip.store import KeyRange
+    rng = np.random.default_rng(33)
+    schema = RecordSchema.plain("u64", "u64")
+    keys = np.unique(rng.integers(0, 2**63, 9000, dtype=np.uint64))
+    n = len(keys)
+    vals = rng.integers(0, 2**62, n, dtype=np.uint64)
+    cols = {"keys": keys.view(np.uint8).reshape(n, 8), "values": vals.view(np.uint8).reshape(n, 8)}
+    one = GpuFingerprintStore(schema)
+    one.load_bulk(cols)
+    sh = ShardedStore(schema, [0, 0, 0])
+    sh.load_bulk(cols)
+    assert sh.size() == one.size() and sh.aggregate() == one.aggregate()
+    probes = [int(x) for x in rng.integers(0, 2**63, 60, dtype=np.uint64)] + [int(keys[0]), int(keys[-1])]
+    for a, b in zip(probes[::2], probes[1::2]):
+        lo, hi = min(a, b), max(a, b)
+        assert sh.aggregate(KeyRange(lo, hi)) == one.aggregate(KeyRange(lo, hi))
+        assert sh.rank(lo) == one.rank(lo)
+    for r in range(0, n, 401):
+        assert sh.select(r) == one.select(r)
+    # a routed batch: new keys everywhere, overwrites, deletes
+    newk = rng.integers(0, 2**63, 700, dtype=np.uint64)
+    bk = np.unique(np.concatenate([newk, keys[::37]]))
+    bv = rng.integers(0, 2**62, len(bk), dtype=np.uint64)
+    ops = (rng.random(len(bk)) < 0.2).astype(np.uint8)
+    batch = {"keys": bk.view(np.uint8).reshape(-1, 8), "values": bv.view(np.uint8).reshape(-1, 8)}
+    assert sh.apply(batch, ops) == one.apply(batch, ops)
+    assert sh.size() == one.size() and sh.aggregate() == one.aggregate()
+    for r in range(0, one.size(), 389):
+        assert sh.select(r) == one.select(r)
+    # protocol rounds: the sharded map against a single store holding different content
+    other = GpuFingerprintStore(schema)
+    other.load_bulk(cols)
+    got = _rounds(sh, other)
+    want = _rounds(one, other)
+    assert got == want and len(got) > 2
+    for s in (one, other):
+        s.close()
+    sh.close()
+
+
+def _rounds(a, b):
+    from rsos_hip import rbsr as R
+    out, active, sides, k = [], R.initial_ranges(a), [b, a], 0
+    while active:
+        ch, en = [], []
+        o = R.protocol_round_with_policy(sides[k % 2], R.DEFAULT_POLICY, active, ch, en, native=False)
+        out.append(([(c.start, c.end, c.aggregate) for c in ch], en, (o.skipped, o.enumerated, o.split)))
+        active, k = ch, k + 1
+    return out

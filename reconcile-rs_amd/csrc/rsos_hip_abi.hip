@@ -1225,7 +1225,11 @@ int rh_store_split_segments(rh_store *s, size_t m, const uint64_t *select_ranks,
     if ((m && (!select_ranks || !keys_out)) || (q && (!lo || !hi || !out))) return fail(RH_ERR_ARG, "NULL buffer");
     if (m == 0 && q == 0) return RH_OK;
     RH_LOCK(s);
-    return s->split(m, select_ranks, static_cast<uint8_t *>(keys_out), q, lo, hi, out);
+    try {  // no exception crosses the C ABI
+        return s->split(m, select_ranks, static_cast<uint8_t *>(keys_out), q, lo, hi, out);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "split: host allocation failed");
+    }
 }
 
 int rh_store_protocol_round(rh_store *s, int policy, uint64_t fan_out, const rh_segments *active,

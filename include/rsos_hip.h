@@ -12,6 +12,9 @@
  *   - the Rsos<K> trait surface (size / aggregate / rank / select / insert / delete)
  *                                                    rsos/src/rsos_trait.rs:39-90
  *     which rbsr consumes through RsosView<K>        rbsr/src/rsos_view.rs:55-91
+ *   - rbsr's protocol round, its questions batched   rbsr/src/protocol.rs:212-317
+ *   - the snapshot reload and the RangeAggregate wire codec
+ *                                                    src/snapshot.rs:30-98, gossip/src/bincode.rs:65-100
  *
  * Conventions
  *   - Every call returns rh_status (0 = ok, negative = error); rh_last_error() gives a
@@ -43,7 +46,7 @@ typedef enum rh_status {
     RH_OK = 0,
     RH_ERR_ARG = -1,         /* bad argument (null pointer, misaligned buffer, bad range)     */
     RH_ERR_HIP = -2,         /* a HIP runtime call failed (message in rh_last_error)           */
-    RH_ERR_OOM = -3,         /* device allocation failed                                       */
+    RH_ERR_OOM = -3,         /* device (or page-locked host) allocation failed                 */
     RH_ERR_UNSUPPORTED = -4, /* schema has no specialised kernel: encode on the host and use
                                 rh_lift_encoded_async (the generic canonical-bytes path)       */
     RH_ERR_STATE = -5,       /* call not valid in the store's current state                   */

@@ -70,7 +70,9 @@ def parse():
     p.add_argument("--batch", type=int, default=1_000_000, help="config5: records per update batch")
     p.add_argument("--overwrite", type=float, default=0.0,
                    help="config5: fraction of each batch that re-stamps existing keys (the new - old delta)")
-    p.add_argument("--e2e", action="store_true", help="also time host->device->host end to end (DESIGN.md)")
+    p.add_argument("--e2e", type=int, default=-1,
+                   help="also time host->device->host end to end (DESIGN.md): 1 on, 0 off; "
+                        "default on for config2 at one GPU")
     p.add_argument("--diffs", type=int, default=10_000, help="rbsr: keys in which the two replicas differ")
     p.add_argument("--dual", action="store_true",
                    help="dated configs: both lifts of Replica::map_insert (dated + projection) per record")
@@ -243,7 +245,7 @@ def main():
         line["valu"] = valu
     if args.cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample, dual)
-    if args.e2e:
+    if args.e2e == 1 or (args.e2e < 0 and args.config == "config2" and world == 1):
         line["end_to_end"] = end_to_end(schema, cols, n)
     print(json.dumps(line), flush=True)
     if dist is not None:
@@ -403,7 +405,7 @@ def reload(args, world, rank, dev, dist):
                          "kernel_avg_us": round(dec_s * 1e6, 1)},
             "root_check": "dated root == Σ lift(source rows)",
         }
-        if args.e2e:  # the file's bytes in (pinned) host memory: H2D inside the reload
+        if args.e2e == 1:  # the file's bytes in (pinned) host memory: H2D inside the reload
             host = blob.cpu().pin_memory()
             best = None
             for _ in range(3):

@@ -402,15 +402,11 @@ __device__ __forceinline__ void acc_span_lane(Acc &a, const uint8_t *src, uint64
     }
 }
 
-__global__ __launch_bounds__(256) void k_range_query_wave(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
-                                                          const uint8_t *ssums, uint64_t n, const uint64_t *qlo,
-                                                          const uint64_t *qhi, uint64_t r, uint64_t *out) {
-    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63;
-    if (j >= r) return;  // uniform per wave
-    uint64_t lo = qlo[j], hi = qhi[j];
-    if (hi > n) hi = n;
-    if (lo > hi) lo = hi;
+// Σ over rank range [lo, hi) (already clamped) by one wave; lane 0 writes the rh_aggregate
+// {u64 fp[4]; u64 size} at o
+__device__ __forceinline__ void wave_range_agg(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
+                                               const uint8_t *ssums, uint64_t lo, uint64_t hi, uint32_t lane,
+                                               uint64_t *o) {
     Acc a;
     acc_zero(a);
     const uint64_t B = 256;
@@ -433,7 +429,6 @@ __global__ __launch_bounds__(256) void k_range_query_wave(const uint8_t *fps, ui
     if (lane == 0) {
         uint32_t f[8];
         acc_normalise(a, f);
-        uint64_t *o = out + 5 * j;
         o[0] = (uint64_t)f[0] | ((uint64_t)f[1] << 32);
         o[1] = (uint64_t)f[2] | ((uint64_t)f[3] << 32);
         o[2] = (uint64_t)f[4] | ((uint64_t)f[5] << 32);
@@ -441,6 +436,297 @@ __global__ __launch_bounds__(256) void k_range_query_wave(const uint8_t *fps, ui
         o[4] = hi - lo;
     }
 }
+
+__global__ __launch_bounds__(256) void k_range_query_wave(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
+                                                          const uint8_t *ssums, uint64_t n, const uint64_t *qlo,
+                                                          const uint64_t *qhi, uint64_t r, uint64_t *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (j >= r) return;  // uniform per wave
+    uint64_t lo = qlo[j], hi = qhi[j];
+    if (hi > n) hi = n;
+    if (lo > hi) lo = hi;
+    wave_range_agg(fps, stride, bsums, ssums, lo, hi, lane, out + 5 * j);
+}
+
+// ---- one rbsr protocol round on the device (protocol_round_with_policy, rbsr/src/protocol.rs:212-317) ----
+// round_decide takes a segment's decision from its resolved rank range and local / remote
+// aggregates: SKIP on equal aggregates, the shared cutoffs (rbsr/src/policy/cutoffs.rs), then
+// the policy's stride -- FixedFanOut ceil(span / b) (policy/fixed_fan_out.rs), SqrtFanOut
+// (span as f32).sqrt() (policy/sqrt_fan_out.rs) -- and a non-progressing SPLIT turned IDLIST
+// (protocol.rs:263-272).  An IDLIST with a non-empty remote side bounces its range back as one
+// child with the ZERO aggregate; a SPLIT's children are cut at every stride-th rank
+// (protocol.rs:288-313).  kind: 0 skip, 1 IDLIST, 2 SPLIT, 3 dropped (inverted, :232-245).
+struct RoundSeg {
+    int kind;
+    uint64_t stride, si, ei, children, enums;
+};
+__device__ __forceinline__ RoundSeg round_decide(uint64_t l, uint64_t h, const uint64_t *L, const uint64_t *R,
+                                                 uint64_t n, int sqrt_policy, uint64_t b) {
+    RoundSeg g{3, 0, 0, 0, 0, 0};
+    if (h < l) return g;
+    g.si = l < n ? l : n;
+    g.ei = h < n ? h : n;
+    const uint64_t span = L[4], rem = R[4];
+    uint64_t st = 0;
+    int k;
+    if (span == rem && L[0] == R[0] && L[1] == R[1] && L[2] == R[2] && L[3] == R[3]) k = 0;
+    else if (rem == 0) k = 1;
+    else if (span == 0) k = 2, st = 1;
+    else if (span == 1 && rem == 1) k = 1;
+    else if (span == 1) k = 2, st = 1;
+    else {
+        k = 2;
+        st = sqrt_policy ? (uint64_t)__fsqrt_rn((float)span) : (span + b - 1) / b;
+        if (st == 0) st = 1;  // SplitStride::per_child
+    }
+    if (k == 2 && span > 1 && st >= span) k = 1;
+    g.kind = k;
+    g.stride = st;
+    if (k == 1) {
+        g.enums = 1;
+        g.children = rem != 0;
+    } else if (k == 2) {
+        g.children = (g.ei > g.si ? (g.ei - g.si - 1) / st : 0) + 1;  // cuts at si + i * st < ei, i >= 1
+    }
+    return g;
+}
+
+// Child c (k-th of segment j), by one wave: its bounds (the parent's own, or the keys at the cut
+// ranks) and its aggregate -- the parent's local one for an uncut SPLIT, ZERO for a bounced
+// IDLIST, else the rank range summed like k_range_query_wave.
+__device__ __forceinline__ void round_emit_child(uint64_t c, uint64_t j, uint64_t k, const RoundLayout &L,
+                                                 uint32_t kl, uint32_t lane, const RoundIn &in, const RoundSegs &g,
+                                                 uint8_t *out) {
+    uint8_t skd = in.sk[j], ekd = in.ek[j];
+    const uint8_t *skey = skd ? in.skeys + j * kl : nullptr, *ekey = ekd ? in.ekeys + j * kl : nullptr;
+    uint64_t *agg = reinterpret_cast<uint64_t *>(out + L.caggs) + 5 * c;
+    const uint64_t ncuts = g.nch[j] - 1;
+    if (g.kind[j] == 1 || ncuts == 0) {
+        if (lane < 5) agg[lane] = g.kind[j] == 1 ? 0ull : g.loc[5 * j + lane];
+    } else {
+        const uint64_t st = g.stride[j], s0 = g.si[j];
+        const uint64_t lo = s0 + k * st, hi = k == ncuts ? g.ei[j] : s0 + (k + 1) * st;
+        if (k) skd = 1, skey = in.bkeys + lo * kl;
+        if (k != ncuts) ekd = 1, ekey = in.bkeys + hi * kl;
+        wave_range_agg(in.fps, 32, in.bsums, in.ssums, lo, hi, lane, agg);
+    }
+    if (lane == 0) {
+        out[L.csk + c] = skd;
+        out[L.cek + c] = ekd;
+    }
+    if (lane < kl / 4) {
+        reinterpret_cast<uint32_t *>(out + L.cskeys + c * kl)[lane] =
+            skey ? reinterpret_cast<const uint32_t *>(skey)[lane] : 0u;
+        reinterpret_cast<uint32_t *>(out + L.cekeys + c * kl)[lane] =
+            ekey ? reinterpret_cast<const uint32_t *>(ekey)[lane] : 0u;
+    }
+}
+
+// Segment j's IDLIST range as enumeration e (unbounded sides' keys written as zeros)
+__device__ __forceinline__ void round_emit_enum(uint64_t j, uint64_t e, const RoundLayout &L, uint32_t kl,
+                                                const RoundIn &in, const RoundSegs &, uint8_t *out) {
+    const uint8_t skd = in.sk[j], ekd = in.ek[j];
+    out[L.esk + e] = skd;
+    out[L.eek + e] = ekd;
+    uint32_t *os = reinterpret_cast<uint32_t *>(out + L.eskeys + e * kl);
+    uint32_t *oe = reinterpret_cast<uint32_t *>(out + L.eekeys + e * kl);
+    const uint32_t *is = reinterpret_cast<const uint32_t *>(in.skeys + j * kl);
+    const uint32_t *ie = reinterpret_cast<const uint32_t *>(in.ekeys + j * kl);
+    for (uint32_t w = 0; w < kl / 4; w++) {
+        os[w] = skd ? is[w] : 0u;
+        oe[w] = ekd ? ie[w] : 0u;
+    }
+}
+
+// j = the last segment with choff[j] <= c (it owns child c)
+__device__ __forceinline__ uint64_t round_owner(const uint64_t *choff, uint64_t r, uint64_t c) {
+    uint64_t a = 0, z = r;
+    while (a < z) {
+        const uint64_t mid = (a + z) >> 1;
+        if (choff[mid] <= c) a = mid + 1;
+        else z = mid;
+    }
+    return a - 1;
+}
+
+// Large rounds, step 1 (after the bounds' ranks and local aggregates): every segment's decision;
+// hdr gets the RoundOutcome counts (protocol.rs:135-142) -- skipped, enumerated, split,
+// children, dropped
+__global__ __launch_bounds__(256) void k_round_plan(RoundSegs g, const uint64_t *remote, uint64_t r, uint64_t n,
+                                                    int sqrt_policy, uint64_t b, uint64_t *hdr) {
+    __shared__ unsigned long long cnt[5];
+    if (threadIdx.x < 5) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < r) {
+        const RoundSeg d = round_decide(g.lo[j], g.hi[j], g.loc + 5 * j, remote + 5 * j, n, sqrt_policy, b);
+        g.kind[j] = (uint8_t)d.kind;
+        g.stride[j] = d.stride;
+        g.si[j] = d.si;
+        g.ei[j] = d.ei;
+        g.nch[j] = d.children;
+        g.nen[j] = d.enums;
+        atomicAdd(&cnt[d.kind == 3 ? 4 : d.kind], 1ull);
+        if (d.children) atomicAdd(&cnt[3], (unsigned long long)d.children);
+    }
+    __syncthreads();
+    if (threadIdx.x < 5 && cnt[threadIdx.x]) atomicAdd((unsigned long long *)&hdr[threadIdx.x], cnt[threadIdx.x]);
+}
+
+// Every child, one wave each, grid-stride (the count is known on the device only), then the
+// enumerations, one thread each
+__global__ __launch_bounds__(256) void k_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl,
+                                                    RoundIn in, RoundSegs g, uint8_t *out) {
+    const uint64_t nc = hdr[3], ne = hdr[1];
+    if (nc > cap) return;  // the host grows the buffer and launches again
+    const RoundLayout L = round_layout(nc, ne, kl);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nc; c += nw) {
+        const uint64_t j = round_owner(g.choff, r, c);
+        round_emit_child(c, j, c - g.choff[j], L, kl, lane, in, g, out);
+    }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < r; j += nw * 64)
+        if (g.nen[j]) round_emit_enum(j, g.enoff[j], L, kl, in, g, out);
+}
+
+// Every segment's raw rank range and local aggregate, one wave each
+__global__ __launch_bounds__(256) void k_round_bounds(const uint32_t *rank, RoundIn in, RoundSegs g, uint64_t r,
+                                                      uint64_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (j >= r) return;  // uniform per wave
+    const uint64_t l = in.sk[j] ? (uint64_t)rank[j] : 0ull, h = in.ek[j] ? (uint64_t)rank[r + j] : n;
+    if (lane == 0) {
+        g.lo[j] = l;
+        g.hi[j] = h;
+    }
+    uint64_t hi = h < n ? h : n, lo = l;
+    if (lo > hi) lo = hi;
+    wave_range_agg(in.fps, 32, in.bsums, in.ssums, lo, hi, lane, g.loc + 5 * j);
+}
+
+// Medium rounds (r <= ROUND_SMALL): decisions, the children / enumeration offsets (block scan)
+// and the header in one workgroup, between k_round_bounds and k_round_emit -- three launches
+// where the large path takes six.  Tiny rounds (r <= ROUND_TINY: one segment per wave, at most
+// 16 * fan-out children) run whole in k_round_small, one launch.  Both write the per-segment
+// arrays, so a round whose children outnumber cap can be emitted again by k_round_emit.
+constexpr uint32_t ROUND_SMALL = 1024, ROUND_TINY = 16;
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *wsum, uint64_t *total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint64_t x = v;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (uint32_t i = 0; i < nwv; i++) {
+            const uint64_t t = wsum[i];
+            wsum[i] = acc;
+            acc += t;
+        }
+        *total = acc;
+    }
+    __syncthreads();
+    return wsum[w] + x - v;
+}
+
+__global__ __launch_bounds__(1024) void k_round_small(const uint32_t *rank, RoundIn in, RoundSegs g, uint64_t r,
+                                                      uint64_t n, int sqrt_policy, uint64_t b, uint64_t cap,
+                                                      uint32_t kl, uint8_t *out) {
+    __shared__ uint64_t wsum[2][16], tot[2];
+    __shared__ unsigned long long cnt[5];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t < 5) cnt[t] = 0;
+    const bool mine = t < r;
+    if (mine) {
+        g.lo[t] = in.sk[t] ? (uint64_t)rank[t] : 0ull;
+        g.hi[t] = in.ek[t] ? (uint64_t)rank[r + t] : n;
+    }
+    __syncthreads();
+    for (uint64_t j = w; j < r; j += 16) {
+        uint64_t lo = g.lo[j], hi = g.hi[j];
+        if (hi > n) hi = n;
+        if (lo > hi) lo = hi;
+        wave_range_agg(in.fps, 32, in.bsums, in.ssums, lo, hi, lane, g.loc + 5 * j);
+    }
+    __syncthreads();
+    RoundSeg d{3, 0, 0, 0, 0, 0};
+    if (mine) {
+        d = round_decide(g.lo[t], g.hi[t], g.loc + 5 * t, in.remote + 5 * t, n, sqrt_policy, b);
+        g.kind[t] = (uint8_t)d.kind;
+        g.stride[t] = d.stride;
+        g.si[t] = d.si;
+        g.ei[t] = d.ei;
+        g.nch[t] = d.children;
+        g.nen[t] = d.enums;
+        atomicAdd(&cnt[d.kind == 3 ? 4 : d.kind], 1ull);
+    }
+    const uint64_t co = block_exclusive_scan(d.children, wsum[0], &tot[0]);
+    const uint64_t eo = block_exclusive_scan(d.enums, wsum[1], &tot[1]);
+    const uint64_t nc = tot[0], ne = tot[1];
+    if (mine) {
+        g.choff[t] = co;
+        g.enoff[t] = eo;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t *hdr = reinterpret_cast<uint64_t *>(out);
+        hdr[0] = cnt[0];
+        hdr[1] = ne;
+        hdr[2] = cnt[2];
+        hdr[3] = nc;
+        hdr[4] = cnt[4];
+    }
+    if (nc > cap) return;  // uniform
+    const RoundLayout L = round_layout(nc, ne, kl);
+    if (mine && d.enums) round_emit_enum(t, eo, L, kl, in, g, out);
+    for (uint64_t c = w; c < nc; c += 16) {
+        const uint64_t j = round_owner(g.choff, r, c);
+        round_emit_child(c, j, c - g.choff[j], L, kl, lane, in, g, out);
+    }
+}
+__global__ __launch_bounds__(1024) void k_round_plan_scan(RoundIn in, RoundSegs g, uint64_t r, uint64_t n,
+                                                          int sqrt_policy, uint64_t b, uint8_t *out) {
+    __shared__ uint64_t wsum[2][16], tot[2];
+    __shared__ unsigned long long cnt[5];
+    const uint32_t t = threadIdx.x;
+    if (t < 5) cnt[t] = 0;
+    __syncthreads();
+    const bool mine = t < r;
+    RoundSeg d{3, 0, 0, 0, 0, 0};
+    if (mine) {
+        d = round_decide(g.lo[t], g.hi[t], g.loc + 5 * t, in.remote + 5 * t, n, sqrt_policy, b);
+        g.kind[t] = (uint8_t)d.kind;
+        g.stride[t] = d.stride;
+        g.si[t] = d.si;
+        g.ei[t] = d.ei;
+        g.nch[t] = d.children;
+        g.nen[t] = d.enums;
+        atomicAdd(&cnt[d.kind == 3 ? 4 : d.kind], 1ull);
+    }
+    const uint64_t co = block_exclusive_scan(d.children, wsum[0], &tot[0]);
+    const uint64_t eo = block_exclusive_scan(d.enums, wsum[1], &tot[1]);
+    const uint64_t nc = tot[0], ne = tot[1];
+    if (mine) {
+        g.choff[t] = co;
+        g.enoff[t] = eo;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t *hdr = reinterpret_cast<uint64_t *>(out);
+        hdr[0] = cnt[0];
+        hdr[1] = ne;
+        hdr[2] = cnt[2];
+        hdr[3] = nc;
+        hdr[4] = cnt[4];
+    }
+}
+
 
 // out[j] = Σ_p in[p*r + j] over rh_aggregate {u64 fp[4]; u64 size}
 __global__ void k_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64_t *out) {
@@ -516,6 +802,47 @@ hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const ui
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_range_query, dim3((uint32_t)r), dim3(256), 0, st, fps, stride, bsums, ssums, n, lo, hi, r, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_plan(const RoundSegs &g, const uint64_t *remote, uint64_t r, uint64_t n, int sqrt_policy,
+                             uint64_t b, uint64_t *hdr, hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_round_plan, dim3((uint32_t)((r + 255) / 256)), dim3(256), 0, st, g, remote, r, n,
+                       sqrt_policy, b, hdr);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl, const RoundIn &in,
+                             const RoundSegs &g, uint8_t *out, hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    const uint64_t wgs = std::min<uint64_t>(std::max<uint64_t>((cap + 3) / 4, (r + 255) / 256), 4096);
+    hipLaunchKernelGGL(k_round_emit, dim3((uint32_t)wgs), dim3(256), 0, st, hdr, cap, r, kl, in, g, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_bounds(const uint32_t *rank, const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n,
+                               hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_round_bounds, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, rank, in, g, r, n);
+    return hipGetLastError();
+}
+
+uint64_t round_tiny_max() { return ROUND_TINY; }
+uint64_t round_small_max() { return ROUND_SMALL; }
+
+hipError_t launch_round_plan_scan(const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n, int sqrt_policy,
+                                  uint64_t b, uint8_t *out, hipStream_t st) {
+    if (r == 0 || r > ROUND_SMALL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_round_plan_scan, dim3(1), dim3(ROUND_SMALL), 0, st, in, g, r, n, sqrt_policy, b, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_small(const uint32_t *rank, const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n,
+                              int sqrt_policy, uint64_t b, uint64_t cap, uint32_t kl, uint8_t *out, hipStream_t st) {
+    if (r == 0 || r > ROUND_TINY) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_round_small, dim3(1), dim3(ROUND_SMALL), 0, st, rank, in, g, r, n, sqrt_policy, b, cap, kl,
+                       out);
     return hipGetLastError();
 }
 

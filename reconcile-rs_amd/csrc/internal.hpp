@@ -27,6 +27,61 @@ hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
                               hipStream_t st, uint32_t stride = 32);
+
+// One rbsr protocol round's output, read back in one copy: a 64-byte header (u64 skipped,
+// enumerated, split, children, dropped), then the children (start kinds, end kinds, start keys,
+// end keys, aggregates) and the enumerations (kinds and keys), each array 16-byte aligned.
+struct RoundLayout {
+    uint64_t csk, cek, cskeys, cekeys, caggs, esk, eek, eskeys, eekeys, end;
+};
+__host__ __device__ inline RoundLayout round_layout(uint64_t nc, uint64_t ne, uint64_t kl) {
+    auto pad = [](uint64_t x) { return (x + 15) & ~15ull; };
+    RoundLayout o;
+    uint64_t p = 64;
+    o.csk = p, p += pad(nc);
+    o.cek = p, p += pad(nc);
+    o.cskeys = p, p += pad(nc * kl);
+    o.cekeys = p, p += pad(nc * kl);
+    o.caggs = p, p += pad(nc * 40);
+    o.esk = p, p += pad(ne);
+    o.eek = p, p += pad(ne);
+    o.eskeys = p, p += pad(ne * kl);
+    o.eekeys = p, p += pad(ne * kl);
+    o.end = p;
+    return o;
+}
+// A round's per-segment device arrays: kind (0 skip, 1 IDLIST, 2 SPLIT, 3 dropped), raw rank
+// range, local aggregate (5 u64), stride, clamped rank range, children / enumeration counts and
+// their exclusive offsets
+struct RoundSegs {
+    uint8_t *kind;
+    uint64_t *lo, *hi, *loc, *stride, *si, *ei, *nch, *choff, *nen, *enoff;
+};
+// The round's segments as they came in (device: bound kinds, bound keys, remote aggregates) and
+// the store's base run
+struct RoundIn {
+    const uint8_t *sk, *ek, *skeys, *ekeys;
+    const uint64_t *remote;
+    const uint8_t *bkeys, *fps, *bsums, *ssums;
+};
+// large rounds: decisions (g.lo / g.hi / g.loc filled) -> hdr (zeroed by the caller) gets the
+// outcome counts; after the offsets are scanned, children and enumerations into `out`
+// (round_layout(hdr children, hdr enumerated, kl)), nothing when the children outnumber cap
+hipError_t launch_round_plan(const RoundSegs &g, const uint64_t *remote, uint64_t r, uint64_t n, int sqrt_policy,
+                             uint64_t b, uint64_t *hdr, hipStream_t st);
+hipError_t launch_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl, const RoundIn &in,
+                             const RoundSegs &g, uint8_t *out, hipStream_t st);
+// every segment's raw rank range (from the searched bound ranks) and local aggregate
+hipError_t launch_round_bounds(const uint32_t *rank, const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n,
+                               hipStream_t st);
+// medium rounds (r <= round_small_max()): decisions, offsets and the header in one workgroup
+uint64_t round_small_max();
+hipError_t launch_round_plan_scan(const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n, int sqrt_policy,
+                                  uint64_t b, uint8_t *out, hipStream_t st);
+// tiny rounds (r <= round_tiny_max()): from the searched bound ranks to `out` in one launch
+uint64_t round_tiny_max();
+hipError_t launch_round_small(const uint32_t *rank, const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n,
+                              int sqrt_policy, uint64_t b, uint64_t cap, uint32_t kl, uint8_t *out, hipStream_t st);
 hipError_t launch_combine(const uint64_t *in, uint64_t parts, uint64_t r, uint64_t *out, hipStream_t st);
 
 }  // namespace rh

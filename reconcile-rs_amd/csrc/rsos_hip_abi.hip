@@ -837,6 +837,7 @@ struct rh_store {
     PinnedVec<uint8_t> stage_in, stage_out, stage_out2;  // step 2's results land beside step 1's
     DevBuf<uint8_t> q_in, q_res;
     static size_t pad8(size_t x) { return (x + 7) & ~size_t(7); }
+    static size_t pad16(size_t x) { return (x + 15) & ~size_t(15); }
     // step 1, results in stage_out: lo[r] u64, hi[r] u64, aggregates[r]
     int resolve_staged(size_t r, const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys,
                        const uint64_t **lo, const uint64_t **hi, const rh_aggregate **aggs) {
@@ -918,151 +919,104 @@ struct rh_store {
         return RH_OK;
     }
     // A whole protocol round (protocol_round_with_policy, protocol.rs:212-317) for the policies
-    // that decide on the span alone: the two batched steps above with the decision loop between
-    // them on the host, no per-segment round trip.
-    std::vector<uint64_t> pr_sel, pr_alo, pr_ahi;
-    std::vector<uint8_t> pr_csk, pr_cek, pr_cskeys, pr_cekeys, pr_esk, pr_eek, pr_eskeys, pr_eekeys;
-    std::vector<rh_aggregate> pr_caggs;
-    struct Plan {
-        uint8_t kind;  // 0 skip, 1 enumerate, 2 split
-        uint8_t bounce;
-        uint64_t ncuts, first_sel, first_agg;
-    };
-    std::vector<Plan> pr_plan;
+    // that decide on the span alone, in one device round trip: the segments go up in one copy
+    // (or one per array when large), the bounds' ranks, local aggregates, decisions, children
+    // (cut keys and aggregates) and enumerations are formed on the device (k_round_*), and the
+    // round comes back in one copy of round_layout() -- the header first when the worst-case
+    // layout is large, so the copy is exact.
+    DevBuf<uint8_t> r_in, r_kind, r_out;
+    DevBuf<uint64_t> r_seg;
+    PinnedVec<uint8_t> pr_out;
+    static constexpr size_t kRoundSmall = 256 << 10;  // below this, one speculative copy each way
     int protocol_round(int policy, uint64_t param, const rh_segments &in, rh_segments *ch, rh_segments *en,
                        rh_round_outcome *oc) {
         int rc;
         const size_t r = in.n;
-        rh_round_outcome o{};
-        const uint64_t *pr_lo = nullptr, *pr_hi = nullptr;
-        const rh_aggregate *res_loc = nullptr;
-        if (r && (rc = resolve_staged(r, in.start_kinds, static_cast<const uint8_t *>(in.start_keys), in.end_kinds,
-                                      static_cast<const uint8_t *>(in.end_keys), &pr_lo, &pr_hi, &res_loc)))
-            return rc;
-        const rh_aggregate *pr_loc = res_loc;  // stays valid: step 2 stages its results apart
-        const uint64_t n = nb;  // resolve compacted: the base run is the whole store
+        if (oc) *oc = rh_round_outcome{};
+        *ch = rh_segments{};
+        *en = rh_segments{};
+        if (r == 0) return RH_OK;
+        if ((rc = compact())) return rc;
+        const uint64_t n = nb;                     // compacted: the base run is the whole store
         const uint64_t b = param < 2 ? 2 : param;  // FanOut::new
-        pr_plan.assign(r, Plan{0, 0, 0, 0, 0});
-        pr_sel.clear();
-        pr_alo.clear();
-        pr_ahi.clear();
-        uint64_t n_enum = 0;
-        for (size_t j = 0; j < r; j++) {
-            Plan &p = pr_plan[j];
-            p.kind = 3;  // dropped unless decided below
-            if (pr_hi[j] < pr_lo[j]) {  // inverted (protocol.rs:232-245)
-                o.dropped_malformed++;
-                continue;
-            }
-            const uint64_t si = std::min(pr_lo[j], n), ei = std::min(pr_hi[j], n);
-            const rh_aggregate &l = pr_loc[j], &rm = in.aggregates[j];
-            const uint64_t span = l.size, remote = rm.size;
-            // shared_cutoffs (policy/cutoffs.rs), then the policy's stride
-            int kind;
-            uint64_t stride = 0;
-            if (l.size == rm.size && !memcmp(l.fingerprint, rm.fingerprint, 32)) kind = 0;
-            else if (remote == 0) kind = 1;
-            else if (span == 0) kind = 2, stride = 1;
-            else if (span == 1 && remote == 1) kind = 1;
-            else if (span == 1) kind = 2, stride = 1;
-            else {
-                kind = 2;
-                stride = policy == RH_POLICY_SQRT_FAN_OUT ? (uint64_t)std::sqrt((float)span)  // (span as f32).sqrt() as usize
-                                                          : (span + b - 1) / b;               // ceil(span / b)
-                if (stride == 0) stride = 1;                                                  // SplitStride::per_child
-            }
-            if (kind == 2 && span > 1 && stride >= span) kind = 1;  // non-progressing SPLIT -> IDLIST (:263-272)
-            p.kind = (uint8_t)kind;
-            if (kind == 0) {
-                o.skipped++;
-            } else if (kind == 1) {
-                o.enumerated++;
-                n_enum++;
-                if (remote != 0) {
-                    p.bounce = 1;
-                    o.children++;
-                }
-            } else {
-                o.split++;
-                p.first_sel = pr_sel.size();
-                p.first_agg = pr_alo.size();
-                for (uint64_t c = si + stride; c < ei && c >= si; c += stride) pr_sel.push_back(c);  // cut_before
-                p.ncuts = pr_sel.size() - p.first_sel;
-                if (p.ncuts) {  // an uncut child is the parent, whose aggregate is in hand (:292-296)
-                    uint64_t cur = si;
-                    for (uint64_t c = 0; c < p.ncuts; c++) {
-                        pr_alo.push_back(cur);
-                        pr_ahi.push_back(pr_sel[p.first_sel + c]);
-                        cur = pr_sel[p.first_sel + c];
-                    }
-                    pr_alo.push_back(cur);
-                    pr_ahi.push_back(ei);
-                }
-                o.children += p.ncuts + 1;
-            }
-        }
-        if (oc) *oc = o;
-        // the outputs live in the store (borrowed by the caller until its next call on this store)
-        pr_csk.resize(o.children + 1);
-        pr_cek.resize(o.children + 1);
-        pr_cskeys.resize((o.children + 1) * kl);
-        pr_cekeys.resize((o.children + 1) * kl);
-        pr_caggs.resize(o.children + 1);
-        pr_esk.resize(n_enum + 1);
-        pr_eek.resize(n_enum + 1);
-        pr_eskeys.resize((n_enum + 1) * kl);
-        pr_eekeys.resize((n_enum + 1) * kl);
-        *ch = rh_segments{pr_csk.data(), pr_cskeys.data(), pr_cek.data(), pr_cekeys.data(), pr_caggs.data(), 0,
-                          (size_t)o.children};
-        *en = rh_segments{pr_esk.data(), pr_eskeys.data(), pr_eek.data(), pr_eekeys.data(), nullptr, 0, (size_t)n_enum};
-        const uint8_t *pr_keys = nullptr;
-        const rh_aggregate *pr_aggs = nullptr;
-        if ((!pr_sel.empty() || !pr_alo.empty()) &&
-            (rc = split_staged(pr_sel.size(), pr_sel.data(), pr_alo.size(), pr_alo.data(), pr_ahi.data(), &pr_keys,
-                               &pr_aggs)))
+        // device input: start kinds, end kinds, start keys then end keys (searched as one run of
+        // 2r queries), remote aggregates
+        const size_t o_ek = pad16(r), o_sk = o_ek + pad16(r), o_ekeys = o_sk + r * kl,
+                     o_rem = pad16(o_ekeys + r * kl), in_bytes = o_rem + r * sizeof(rh_aggregate);
+        uint64_t cap = r * std::min<uint64_t>(b, 16);
+        if ((rc = r_in.ensure(in_bytes + 64)) || (rc = r_kind.ensure(r)) || (rc = r_seg.ensure(14 * r)) ||
+            (rc = q_rank.ensure(2 * r)) || (rc = r_out.ensure(rh::round_layout(cap, r, kl).end)))
             return rc;
-        // assemble in segment order
-        const uint8_t *sk = static_cast<const uint8_t *>(in.start_keys), *ek = static_cast<const uint8_t *>(in.end_keys);
-        uint8_t *csk = static_cast<uint8_t *>(ch->start_keys), *cek = static_cast<uint8_t *>(ch->end_keys);
-        uint8_t *esk = static_cast<uint8_t *>(en->start_keys), *eek = static_cast<uint8_t *>(en->end_keys);
-        size_t nc = 0, ne = 0;
-        auto put = [&](uint8_t skind, const uint8_t *skey, uint8_t ekind, const uint8_t *ekey, const rh_aggregate &a) {
-            ch->start_kinds[nc] = skind;
-            ch->end_kinds[nc] = ekind;
-            if (skind) memcpy(csk + nc * kl, skey, kl); else memset(csk + nc * kl, 0, kl);
-            if (ekind) memcpy(cek + nc * kl, ekey, kl); else memset(cek + nc * kl, 0, kl);
-            ch->aggregates[nc] = a;
-            nc++;
-        };
-        const rh_aggregate zero{};
-        for (size_t j = 0; j < r; j++) {
-            const Plan &p = pr_plan[j];
-            const uint8_t *s0 = in.start_kinds[j] ? sk + j * kl : nullptr, *e0 = in.end_kinds[j] ? ek + j * kl : nullptr;
-            if (p.kind == 1) {
-                if (p.bounce) put(in.start_kinds[j], s0, in.end_kinds[j], e0, zero);
-                en->start_kinds[ne] = in.start_kinds[j];
-                en->end_kinds[ne] = in.end_kinds[j];
-                if (s0) memcpy(esk + ne * kl, s0, kl); else memset(esk + ne * kl, 0, kl);
-                if (e0) memcpy(eek + ne * kl, e0, kl); else memset(eek + ne * kl, 0, kl);
-                ne++;
-            } else if (p.kind == 2) {
-                if (p.ncuts == 0) {
-                    put(in.start_kinds[j], s0, in.end_kinds[j], e0, pr_loc[j]);
-                    continue;
-                }
-                uint8_t cur_kind = in.start_kinds[j];
-                const uint8_t *cur = s0;
-                for (uint64_t c = 0; c < p.ncuts; c++) {
-                    const uint8_t *cut = pr_keys + (p.first_sel + c) * kl;
-                    put(cur_kind, cur, 1, cut, pr_aggs[p.first_agg + c]);
-                    cur_kind = 1;
-                    cur = cut;
-                }
-                put(1, cur, in.end_kinds[j], e0, pr_aggs[p.first_agg + p.ncuts]);
-            }
+        const struct { const void *src; size_t off, bytes; } parts[5] = {
+            {in.start_kinds, 0, r}, {in.end_kinds, o_ek, r}, {in.start_keys, o_sk, r * kl},
+            {in.end_keys, o_ekeys, r * kl}, {in.aggregates, o_rem, r * sizeof(rh_aggregate)}};
+        if (in_bytes <= kRoundSmall) {
+            stage_in.resize(in_bytes);
+            for (const auto &p : parts)
+                if (p.src) memcpy(stage_in.data() + p.off, p.src, p.bytes);
+            RH_HIP(hipMemcpyAsync(r_in.p, stage_in.data(), in_bytes, hipMemcpyHostToDevice, stream));
+        } else {
+            for (const auto &p : parts)  // keys of an all-unbounded side may be NULL (never read)
+                if (p.src) RH_HIP(hipMemcpyAsync(r_in.p + p.off, p.src, p.bytes, hipMemcpyHostToDevice, stream));
         }
-        ch->n = nc;
-        en->n = ne;
+        const uint8_t *d_sk = r_in.p, *d_ek = r_in.p + o_ek, *d_skeys = r_in.p + o_sk, *d_ekeys = r_in.p + o_ekeys;
+        const uint64_t *d_rem = reinterpret_cast<const uint64_t *>(r_in.p + o_rem);
+        uint64_t *lo = r_seg.p, *hi = lo + r, *loc = hi + r, *st = loc + 5 * r, *si = st + r, *ei = si + r,
+                 *nch = ei + r, *choff = nch + r, *nen = choff + r, *enoff = nen + r;
+        const rh::RoundSegs g{r_kind.p, lo, hi, loc, st, si, ei, nch, choff, nen, enoff};
+        const rh::RoundIn din{d_sk, d_ek, d_skeys, d_ekeys, d_rem, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p};
+        uint64_t *hdr = reinterpret_cast<uint64_t *>(r_out.p);
+        const int sq = policy == RH_POLICY_SQRT_FAN_OUT;
+        if (n) RH_HIP(kops->search_sampled(bkeys[cb].p, n, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream));
+        else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
+        if (r <= rh::round_tiny_max()) {
+            RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, r_out.p, stream));
+        } else if (r <= rh::round_small_max()) {
+            RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
+            RH_HIP(rh::launch_round_plan_scan(din, g, r, n, sq, b, r_out.p, stream));
+            RH_HIP(rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
+        } else {
+            RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
+            RH_HIP(hipMemsetAsync(hdr, 0, 64, stream));
+            RH_HIP(rh::launch_round_plan(g, d_rem, r, n, sq, b, hdr, stream));
+            RH_HIP(rh::launch_exclusive_scan_u64(nch, choff, r, scratch, stream));
+            RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
+            RH_HIP(rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
+        }
+        const size_t worst = rh::round_layout(cap, r, kl).end;
+        uint64_t h[5];
+        if (worst <= kRoundSmall) {
+            pr_out.resize(worst);
+            RH_HIP(hipMemcpyAsync(pr_out.data(), r_out.p, worst, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+            memcpy(h, pr_out.data(), sizeof h);
+        } else {
+            pr_out.resize(64);
+            RH_HIP(hipMemcpyAsync(pr_out.data(), r_out.p, 64, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+            memcpy(h, pr_out.data(), sizeof h);
+        }
+        const uint64_t nc = h[3], ne = h[1];
+        const rh::RoundLayout L = rh::round_layout(nc, ne, kl);
+        const bool regrow = nc > cap;
+        if (regrow) {  // more children than the first guess (a wide fan-out): emit again
+            cap = nc;
+            if ((rc = r_out.ensure(L.end))) return rc;  // r_out may have moved: restore its header
+            pr_out.resize(L.end);
+            hdr = reinterpret_cast<uint64_t *>(r_out.p);
+            RH_HIP(hipMemcpyAsync(hdr, pr_out.data(), 64, hipMemcpyHostToDevice, stream));
+            RH_HIP(rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
+        }
+        if (regrow || worst > kRoundSmall) {
+            pr_out.resize(L.end);
+            RH_HIP(hipMemcpyAsync(pr_out.data() + 64, r_out.p + 64, L.end - 64, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+        }
+        if (oc) *oc = rh_round_outcome{h[0], h[1], h[2], h[3], h[4]};
+        uint8_t *o = pr_out.data();
+        *ch = rh_segments{o + L.csk, o + L.cskeys, o + L.cek, o + L.cekeys,
+                          reinterpret_cast<rh_aggregate *>(o + L.caggs), (size_t)nc, (size_t)nc};
+        *en = rh_segments{o + L.esk, o + L.eskeys, o + L.eek, o + L.eekeys, nullptr, (size_t)ne, (size_t)ne};
         return RH_OK;
     }
     void release() {
@@ -1082,6 +1036,7 @@ struct rh_store {
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
         q_in.release(); q_res.release();
         stage_in.release(); stage_out.release(); stage_out2.release();
+        r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); pr_out.release();
         snap.release();
         scratch.release();
         if (dep) (void)hipEventDestroy(dep);

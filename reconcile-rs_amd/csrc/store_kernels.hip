@@ -1074,6 +1074,16 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
     return hipGetLastError();
 }
 
+hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    size_t tb = 0;
+    hipError_t e;
+    if ((e = rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), st))) return e;
+    void *tmp = s.bytes(tb);
+    if (s.err) return s.err;
+    return rocprim::exclusive_scan(tmp, tb, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), st);
+}
+
 hipError_t launch_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out,
                               hipStream_t st) {
     if (m == 0) return hipSuccess;

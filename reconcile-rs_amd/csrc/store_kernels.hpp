@@ -143,6 +143,7 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
                                  uint64_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
 hipError_t launch_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out,
                               hipStream_t st);
+hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);
 
 // nullptr if the store does not support this key type
 StoreKeyOps *store_key_ops(int key_kind, int key_len);

@@ -170,8 +170,13 @@ class Segments:
         return len(self.start_kinds)
 
     def c(self) -> A.Segments:
-        return A.Segments(self.start_kinds.ctypes.data, self.start_keys.ctypes.data, self.end_kinds.ctypes.data,
-                          self.end_keys.ctypes.data, self.aggregates.ctypes.data, self.n, self.cap)
+        ptrs = self.__dict__.get("_ptrs")
+        if ptrs is None or ptrs[0] is not self.start_kinds:  # the arrays' addresses, looked up once
+            ptrs = (self.start_kinds, tuple(a.ctypes.data for a in (self.start_kinds, self.start_keys, self.end_kinds,
+                                                                    self.end_keys, self.aggregates)))
+            self._ptrs = ptrs
+        sk, skeys, ek, ekeys, aggs = ptrs[1]
+        return A.Segments(sk, skeys, ek, ekeys, aggs, self.n, self.cap)
 
     @staticmethod
     def from_items(schema, items: Sequence) -> "Segments":
@@ -206,10 +211,19 @@ class Segments:
         return out
 
 
-def _view(ptr, n: int, ctype, shape) -> np.ndarray:
+class _Raw:
+    """A pointer as an __array_interface__: numpy wraps it in ~2 us (a ctypes array's PEP 3118
+    format goes through numpy's Python-level parser, ~10 us per array)."""
+    __slots__ = ("__array_interface__",)
+
+
+def _view(ptr, n: int, shape) -> np.ndarray:
+    """uint8 array of `shape` at ptr (zeros when n == 0)."""
     if n == 0 or not ptr:
-        return np.zeros(shape, np.dtype(ctype))
-    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=shape)
+        return np.zeros(shape, np.uint8)
+    o = _Raw()
+    o.__array_interface__ = {"data": (ptr, False), "shape": shape, "typestr": "|u1", "version": 3}
+    return np.asarray(o)
 
 
 def _wrap(cs: A.Segments, key_len: int, copy: bool, with_aggs: bool) -> "Segments":
@@ -217,12 +231,12 @@ def _wrap(cs: A.Segments, key_len: int, copy: bool, with_aggs: bool) -> "Segment
     seg = Segments.__new__(Segments)
     seg.n = n
     m = max(n, 1)
-    seg.start_kinds = _view(cs.start_kinds, n, C.c_uint8, (m,))
-    seg.end_kinds = _view(cs.end_kinds, n, C.c_uint8, (m,))
-    seg.start_keys = _view(cs.start_keys, n, C.c_uint8, (m, key_len))
-    seg.end_keys = _view(cs.end_keys, n, C.c_uint8, (m, key_len))
+    seg.start_kinds = _view(cs.start_kinds, n, (m,))
+    seg.end_kinds = _view(cs.end_kinds, n, (m,))
+    seg.start_keys = _view(cs.start_keys, n, (m, key_len))
+    seg.end_keys = _view(cs.end_keys, n, (m, key_len))
     if with_aggs and n:
-        seg.aggregates = _view(cs.aggregates, n, C.c_uint8, (m * AGG_DTYPE.itemsize,)).view(AGG_DTYPE)
+        seg.aggregates = _view(cs.aggregates, n, (m * AGG_DTYPE.itemsize,)).view(AGG_DTYPE)
     else:
         seg.aggregates = np.zeros(m, AGG_DTYPE)
     if copy and n:

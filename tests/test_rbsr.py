@@ -488,3 +488,33 @@ def test_gpu_native_round_property(gpu, oracle_lib, a, b, fan, sqrt):
         assert go == wo and ge == we and gc == wc
     ga.close()
     gb.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["fixed16", "sqrt"])
+def test_gpu_native_round_large_batches(gpu, policy):
+    """Rounds of tens of thousands of segments -- the per-array input copies, the header-first
+    readback and, under SqrtFanOut, more children than the first capacity guess -- answered by the
+    one-call device round equal the two-call path (host decisions, tested above against the
+    literal driver) round by round."""
+    from rsos_hip import RecordSchema, rbsr as R
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(17, 200_000, 1000, 1000, 1000)
+    ga, _ = _gpu_and_oracle(schema, ca)
+    gb, _ = _gpu_and_oracle(schema, cb)
+    pol = {"fixed16": R.FixedFanOut(16), "sqrt": R.SqrtFanOut()}[policy]
+    active, sides, k, widest = R.initial_segments(ga), [gb, ga], 0, 0
+    while len(active):
+        side = sides[k % 2]
+        widest = max(widest, len(active))
+        items = active.items(schema)
+        ch, en, o = R.protocol_round_segments(side, pol, active)
+        want_ch, want_en = [], []
+        wo = R.protocol_round_with_policy(side, pol, items, want_ch, want_en, native=False)
+        assert _outcome(o) == _outcome(wo)
+        assert _norm(ch.items(schema)) == _norm(want_ch)
+        assert [en.bounds(schema, i) for i in range(en.n)] == want_en
+        active, k = ch, k + 1
+    assert widest > 4000 and k > 3
+    ga.close()
+    gb.close()

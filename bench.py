@@ -492,7 +492,7 @@ def reconcile(args, world, rank, dev, dist):
             "config": {"workload": desc, "records_per_replica": n, "diffs": d, "policy": "FixedFanOut(16)",
                        "parallelism": f"key-range shards x{world} (each rank reconciles its own shard pair)"},
             "rounds": rounds, "segments_per_reconciliation": segs, "enumerations": enum,
-            "step": "initial_ranges + protocol rounds (rh_store_protocol_round, 2 device round trips each) "
+            "step": "initial_ranges + protocol rounds (rh_store_protocol_round, one device round trip each) "
                     "until no segment is left",
         }
         if cpu_line:

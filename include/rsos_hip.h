@@ -233,7 +233,8 @@ int rh_store_resolve_segments(rh_store *store, size_t r, const uint8_t *start_ki
 int rh_store_split_segments(rh_store *store, size_t m, const uint64_t *select_ranks, void *keys_out, size_t q,
                             const uint64_t *lo, const uint64_t *hi, rh_aggregate *out);
 
-/* A whole round in one call, for the shipped policies that decide on the span alone:
+/* A whole round in one call and one device round trip (decisions, cut keys and children formed on
+ * the device), for the shipped policies that decide on the span alone:
  * FixedFanOut(fan_out) (rbsr/src/policy/fixed_fan_out.rs; fan_out < 2 is raised to 2, 16 =
  * FanOut::NEGENTROPY, the default of protocol_round) and SqrtFanOut (sqrt_fan_out.rs).  Segments
  * travel in the wire codec's SoA form (rh_wire_*): `active` in (n items); children (SPLIT

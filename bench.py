@@ -126,6 +126,11 @@ def main():
 
     # this rank's shard of the globally sorted key space: global rows [rank*n, (rank+1)*n)
     cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
+    if dist is not None:
+        # the steps run on a high-priority stream: HIP maps it to its own hardware queue, so RCCL's
+        # per-step all_gather (a normal-priority stream) cannot sit in front of the next lift
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     base = rank * n
     total = n * world
     R = args.ranges
@@ -138,9 +143,10 @@ def main():
     bs = torch.empty((nb, 32), dtype=torch.uint8, device=dev)
     dual_out = (fps, bs, torch.empty((n, 32), dtype=torch.uint8, device=dev),
                 torch.empty((nb, 32), dtype=torch.uint8, device=dev)) if dual else None
-    # double-buffered per-step aggregates: step k's all_gather runs while step k+1 lifts
+    # per-step aggregates and their gathers: RCCL runs each step's all_gather on its own stream
+    # after that step's range queries; the compute stream never waits for it, so the ranks only
+    # meet in the collectives and at the end, where every step's gather is combined
     outs = [torch.empty((R, 5), dtype=torch.int64, device=dev) for _ in range(2)]
-    gath = [torch.empty((world, R, 5), dtype=torch.int64, device=dev) for _ in range(2)] if dist is not None else None
     stream = torch.cuda.current_stream()
 
     # correctness gate before timing: sampled rows vs the oracle (rank 0)
@@ -149,18 +155,20 @@ def main():
         checked = spot_check(schema, cols, n)
 
     lift_ms = []
-    state = {"pending": None, "res": None, "k": 0}
+    state = {"pending": [], "res": None, "k": 0}
 
-    def finish():  # combine the last in-flight gather
-        if state["pending"] is not None:
-            work, g = state["pending"]
+    def finish():  # combine every in-flight gather, in step order
+        for work, g, _ in state["pending"]:
             work.wait()
             state["res"] = combine_aggregates(g)
-            state["pending"] = None
+        state["pending"] = []
         return state["res"]
 
     def step(timed: bool):
-        out = outs[state["k"] % 2]
+        if dist is None:
+            out = outs[state["k"] % 2]
+        else:  # held by the pending gather until finish()
+            out = torch.empty((R, 5), dtype=torch.int64, device=dev)
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -177,8 +185,8 @@ def main():
         if dist is None:
             state["res"] = out
         else:
-            finish()  # the previous step's gather, overlapped with this step's lift
-            state["pending"] = gather_async(dist, out, gath[state["k"] % 2])
+            g = torch.empty((world, R, 5), dtype=torch.int64, device=dev)
+            state["pending"].append(gather_async(dist, out, g) + (out,))
         state["k"] += 1
 
     for _ in range(args.warmup):
@@ -231,7 +239,7 @@ def main():
                    "records_per_gpu": n, "records_total": total, "ranges": R,
                    "canonical_bytes_per_record": rec_bytes, "hbm_bytes_per_record": hbm_bytes,
                    "parallelism": f"key-range shards x{world}" + (
-                       (" + RCCL all_gather (overlapped with the next lift)" if dist.get_backend() == "nccl"
+                       (" + RCCL all_gather per step (off the compute stream; combined at the end)" if dist.get_backend() == "nccl"
                         else " + gloo all_gather (rehearsal)") if dist is not None else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -290,6 +290,10 @@ def incremental(args, world, rank, dev, dist):
     del base
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+    # capacity for the map this run grows into (its resident rows plus every batch), reserved
+    # before the first batch the way a replica sizes its store: no reallocation in the loop
+    reserved = n + m * (args.warmup + args.steps)
+    st.reserve(reserved, m)
     for k in range(args.warmup):
         st.apply_device(batches[k])
     if dist is not None:
@@ -331,6 +335,7 @@ def incremental(args, world, rank, dev, dist):
             "step": "apply_device (lift + sort + base/delta search + delta merge; amortised compaction) "
                     "+ root aggregate",
             "compactions_in_timed_steps": stats["compactions"] - comp0, "delta_rows_at_end": stats["delta_rows"],
+            "reserved_rows": reserved,
         }
         if args.cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_incremental(schema, m, args.cpu_sample or 10_000_000)

@@ -277,6 +277,12 @@ int rh_store_apply_device(rh_store *store, const rh_columns *dev_cols, const uin
  * dumps).  Results never depend on the policy, only timings do.                            */
 int rh_store_compact(rh_store *store);
 int rh_store_set_compaction(rh_store *store, uint64_t divisor, uint64_t min_rows);
+/* Capacity for `rows` resident rows fed batches of up to `batch_rows` rows (the device-side
+ * analogue of reserving a collection's capacity): both run buffers, the batch buffers and the
+ * merge scratch are sized up front, so later batches and compactions never reallocate (a
+ * reallocation frees the old buffer, and hipFree waits for the whole device).  Compacts first;
+ * contents and every answer are unchanged.  Optional: buffers otherwise grow on demand.    */
+int rh_store_reserve(rh_store *store, uint64_t rows, uint64_t batch_rows);
 int rh_store_stats(const rh_store *store, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions);
 
 /* ---- snapshot reload ------------------------------------------------------------------

@@ -135,6 +135,26 @@ struct DevBuf {
         cap = bytes / sizeof(T);
         return RH_OK;
     }
+    // grow to n elements keeping the first `used` ones (ordered on `st`)
+    int grow_keep(size_t n, size_t used, hipStream_t st) {
+        if (n <= cap && p) return RH_OK;
+        T *q = nullptr;
+        const size_t bytes = ((std::max<size_t>(n, 1) * sizeof(T)) + 255) & ~size_t(255);
+        hipError_t e = hipMalloc(&q, bytes);
+        if (e != hipSuccess) return fail(RH_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        if (p && used) {
+            e = hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                (void)hipFree(q);
+                return fail(RH_ERR_HIP, std::string("grow: ") + hipGetErrorString(e));
+            }
+        }
+        if (p) (void)hipFree(p);
+        p = q;
+        cap = bytes / sizeof(T);
+        return RH_OK;
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -695,6 +715,43 @@ struct rh_store {
         if ((rc = resum_base(true))) return rc;
         return sync();
     }
+    // Capacity for `rows` resident rows taking batches of up to `batch` rows: both base buffers
+    // for a compaction's output, both delta buffers for the largest run the policy allows, the
+    // batch buffers and the merge / compaction scratch.  Growing any of these later frees the
+    // old buffer, and hipFree waits for the whole device.
+    int reserve(uint64_t rows, uint64_t batch) {
+        int rc;
+        if ((rc = compact())) return rc;  // the delta run is empty: its buffers hold nothing
+        const uint64_t thresh = std::max<uint64_t>(rows / compact_div, compact_min);
+        const uint64_t plan = thresh + batch, base = rows + plan;
+        for (int k = 0; k < 2; k++) {
+            if (k == cb) {
+                if ((rc = bkeys[k].grow_keep(base * kl + 64, nb * kl, stream)) ||
+                    (rc = bfps[k].grow_keep(base * 32 + 64, nb * 32, stream)))
+                    return rc;
+            } else if ((rc = bkeys[k].ensure(base * kl + 64)) || (rc = bfps[k].ensure(base * 32 + 64))) {
+                return rc;
+            }
+            if ((rc = dkeys[k].ensure(plan * kl + 64)) || (rc = dpay[k].ensure(plan * sizeof(rh::DeltaRec) + 64)) ||
+                (rc = dbsums[k].ensure(rh_num_blocks(plan) * 32 + 32)) ||
+                (rc = dssums[k].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
+                (rc = dblk[k].ensure(rh_num_blocks(plan) + 16)) || (rc = dinb[k].ensure(plan + 16)))
+                return rc;
+        }
+        if ((rc = bsums.ensure(rh_num_blocks(base) * 32 + 32)) || (rc = ssums.ensure(rh_num_superblocks(base) * 32 + 32)) ||
+            (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(base / 16 + 2)) ||
+            (rc = dsmp.ensure(rh_num_blocks(plan) + 1)) || (rc = cfps.ensure(plan * 32 + 64)) ||
+            (rc = cops.ensure(plan + 64)) || (rc = lfps.ensure(batch * 32 + 64)) || (rc = skeys.ensure(batch * kl + 64)) ||
+            (rc = sfps.ensure(batch * 32 + 64)) || (rc = sops.ensure(std::max(batch, base) + 64)) ||
+            (rc = bpay.ensure(batch * sizeof(rh::DeltaRec) + 64)) || (rc = dops.ensure(batch + 64)) ||
+            (rc = mcnt.ensure(8)) || (rc = results.ensure(12)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
+            return rc;
+        RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        // bsums / ssums / samples may have moved: derive them again from the kept fingerprints
+        if ((rc = resum_base())) return rc;
+        return sync();
+    }
     int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3]) {
         int rc;
         out[0] = out[1] = out[2] = 0;
@@ -1236,6 +1293,13 @@ int rh_store_stats(const rh_store *s, uint64_t *base_rows, uint64_t *delta_rows,
     if (delta_rows) *delta_rows = s->nd;
     if (compactions) *compactions = s->compactions;
     return RH_OK;
+}
+
+int rh_store_reserve(rh_store *s, uint64_t rows, uint64_t batch_rows) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    if (rows >= (1ull << 31) || batch_rows >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows)");
+    RH_LOCK(s);
+    return s->reserve(rows, batch_rows);
 }
 
 int rh_store_set_compaction(rh_store *s, uint64_t divisor, uint64_t min_rows) {

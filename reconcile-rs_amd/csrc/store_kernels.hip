@@ -1074,6 +1074,24 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
     return hipGetLastError();
 }
 
+hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch) {
+    // the slots launch_merge_run (m <= plan), the compaction (plan) and a batch (batch) take
+    (void)s.u64(3, plan + 1), (void)s.u64(4, plan + 1);
+    (void)s.u32(3, plan + 1), (void)s.u32(4, plan + 1), (void)s.u32(5, plan + 1);
+    (void)s.u32(14, plan), (void)s.u8(4, plan);
+    (void)s.u32(9, batch), (void)s.u32(10, batch), (void)s.u8(2, batch), (void)s.u8(3, batch);
+    size_t t1 = 0, t2 = 0;
+    hipError_t e;
+    if ((e = rocprim::exclusive_scan(nullptr, t1, (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0,
+                                     plan + 1, rocprim::plus<uint64_t>(), s.stream)))
+        return e;
+    if ((e = rocprim::inclusive_scan(nullptr, t2, (const int32_t *)nullptr, (int32_t *)nullptr,
+                                     (plan + 255) / 256 + 1, rocprim::plus<int32_t>(), s.stream)))
+        return e;
+    (void)s.bytes(std::max(t1, t2));
+    return hipSuccess;
+}
+
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st) {
     if (n == 0) return hipSuccess;
     size_t tb = 0;

@@ -143,6 +143,8 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
                                  uint64_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
 hipError_t launch_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out,
                               hipStream_t st);
+// pre-size the scratch slots a merge of up to `plan` rows and a batch of `batch` rows use
+hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch);
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);
 
 // nullptr if the store does not support this key type

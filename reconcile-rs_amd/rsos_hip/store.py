@@ -133,6 +133,11 @@ class GpuFingerprintStore:
     def set_compaction(self, divisor: int, min_rows: int) -> None:
         A.check(A.lib().rh_store_set_compaction(self._h, divisor, min_rows), "rh_store_set_compaction")
 
+    def reserve(self, rows: int, batch_rows: int) -> None:
+        """Size every device buffer for `rows` resident rows and batches of up to `batch_rows`
+        (compacts first; contents unchanged), so later batches never reallocate."""
+        A.check(A.lib().rh_store_reserve(self._h, rows, batch_rows), "rh_store_reserve")
+
     def stats(self) -> Dict[str, int]:
         b, d, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         A.check(A.lib().rh_store_stats(self._h, C.byref(b), C.byref(d), C.byref(c)), "rh_store_stats")

@@ -152,6 +152,7 @@ extern "C" {
                                  after_stream: *mut c_void) -> c_int;
     pub fn rh_store_compact(store: *mut rh_store) -> c_int;
     pub fn rh_store_set_compaction(store: *mut rh_store, divisor: u64, min_rows: u64) -> c_int;
+    pub fn rh_store_reserve(store: *mut rh_store, rows: u64, batch_rows: u64) -> c_int;
     pub fn rh_store_stats(store: *const rh_store, base_rows: *mut u64, delta_rows: *mut u64,
                           compactions: *mut u64) -> c_int;
     pub fn rh_snapshot_header(bytes: *const c_void, len: usize, entries: *mut u64) -> c_int;

@@ -560,8 +560,9 @@ def test_store_rejects_bad_batches_unchanged(gpu):
 
 def test_store_lsm_policies_agree(gpu, oracle_lib):
     """The LSM store answers identically whether the delta run is compacted after every batch
-    or never: key-range aggregates, ranks and sizes over base + delta equal the compacted base,
-    and both equal a fold of the oracle's lift over the expected contents."""
+    or never, or with its capacity reserved up front (rh_store_reserve, twice, the second time
+    over a pending delta run): key-range aggregates, ranks and sizes over base + delta equal the
+    compacted base, and all equal a fold of the oracle's lift over the expected contents."""
     import torch
     from rsos_hip import GpuFingerprintStore, RecordSchema
     from rsos_hip.store import KeyRange
@@ -571,11 +572,13 @@ def test_store_lsm_policies_agree(gpu, oracle_lib):
     keys = np.unique(rng.integers(0, 2**40, 50_000, dtype=np.uint64))
     vals = rng.integers(0, 2**63, len(keys), dtype=np.uint64)
     content = {int(k): int(v) for k, v in zip(keys, vals)}
-    lazy, eager = GpuFingerprintStore(s), GpuFingerprintStore(s)
+    lazy, eager, res = GpuFingerprintStore(s), GpuFingerprintStore(s), GpuFingerprintStore(s)
     lazy.set_compaction(1, 1 << 40)         # threshold max(base / 1, 2^40): never on its own
     eager.set_compaction(1 << 40, 0)        # threshold max(base / 2^40, 0) = 0: after every batch
-    for st in (lazy, eager):
+    res.set_compaction(8, 4096)             # the default ratio, with capacity reserved up front
+    for st in (lazy, eager, res):
         st.load_bulk({"keys": keys.view(np.uint8).reshape(-1, 8), "values": vals.view(np.uint8).reshape(-1, 8)})
+    res.reserve(len(keys) + 10_000, 6000)
     sc = O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0)
     inserted = []
     for rnd in range(6):
@@ -596,6 +599,9 @@ def test_store_lsm_policies_agree(gpu, oracle_lib):
                sum(1 for k in dele if int(k) in content))
         assert lazy.apply(cols, ops[perm]) == exp
         assert eager.apply(cols, ops[perm]) == exp
+        assert res.apply(cols, ops[perm]) == exp
+        if rnd == 2:  # grow again with a pending delta run and a live base (kept across the move)
+            res.reserve(4 * len(keys), 8000)
         for k, v in zip(bk, bv):
             if int(k) not in content:
                 inserted.append(int(k))
@@ -609,24 +615,28 @@ def test_store_lsm_policies_agree(gpu, oracle_lib):
         pref = [0]
         for f in fps:
             pref.append(pref[-1] + fp_int(f))
-        assert lazy.size() == eager.size() == len(ks)
+        assert lazy.size() == eager.size() == res.size() == len(ks)
         assert lazy.aggregate().fingerprint.to_int() == eager.aggregate().fingerprint.to_int() == pref[-1] % M256
+        assert res.aggregate().fingerprint.to_int() == pref[-1] % M256
         for _ in range(25):
             a, b = sorted(int(x) for x in rng.integers(0, 2**40, 2))
             ra, rb = np.searchsorted(ks, a), np.searchsorted(ks, b)
-            for st in (lazy, eager):
+            for st in (lazy, eager, res):
                 agg = st.aggregate(KeyRange(a, b))
                 assert agg.size == rb - ra and agg.fingerprint.to_int() == (pref[rb] - pref[ra]) % M256
         probes = rng.integers(0, 2**40, 64, dtype=np.uint64)
         want = np.searchsorted(ks, probes)
         assert (lazy.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
         assert (eager.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
+        assert (res.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
     # a rank-order query compacts the lazy store; afterwards both agree row for row
     assert lazy.select(100) == int(ks[100])
     assert lazy.stats()["delta_rows"] == 0
     assert np.array_equal(lazy.fingerprints(), eager.fingerprints())
+    assert np.array_equal(res.fingerprints(), eager.fingerprints())
     lazy.close()
     eager.close()
+    res.close()
 
 
 def test_store_batch_keys_sharing_leading_bytes(gpu, oracle_lib):

@@ -574,7 +574,8 @@ struct rh_store {
         RH_HIP(hipStreamSynchronize(stream));
         return RH_OK;
     }
-    int resum_base(bool have_block_sums = false) {
+    // root_dst: where the base total lands (pinned memory keeps the copy asynchronous)
+    int resum_base(bool have_block_sums = false, uint64_t *root_dst = nullptr) {
         int rc;
         const size_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
         if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4)) ||
@@ -585,9 +586,9 @@ struct rh_store {
             if (!have_block_sums) RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
             RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
             RH_HIP(rh::launch_total(ssums.p, ns, tot.p, stream));
-            RH_HIP(hipMemcpyAsync(root_b, tot.p, 32, hipMemcpyDeviceToHost, stream));  // the caller syncs
+            RH_HIP(hipMemcpyAsync(root_dst ? root_dst : root_b, tot.p, 32, hipMemcpyDeviceToHost, stream));  // the caller syncs
         } else {
-            memset(root_b, 0, sizeof root_b);
+            memset(root_dst ? root_dst : root_b, 0, sizeof root_b);
         }
         return RH_OK;
     }
@@ -633,6 +634,14 @@ struct rh_store {
     // lifted: bfps[cb] and bsums already hold the records' fingerprints and block sums (the
     // snapshot reload's dual lift wrote them, sized exactly as below)
     int load_device(const rh_columns &c, size_t m, bool last_wins = false, bool lifted = false) {
+        int rc = load_begin(c, m, lifted);
+        return rc ? rc : load_finish(m, last_wins);
+    }
+    // the load in two halves, so that two stores loading the same columns (a snapshot reload)
+    // overlap on their streams: begin enqueues the copy, the sortedness check and the sums;
+    // finish waits, and re-orders the rows if the keys were not sorted
+    PinnedVec<uint32_t> load_flag;
+    int load_begin(const rh_columns &c, size_t m, bool lifted) {
         int rc;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
             (rc = counts.ensure(4)))
@@ -653,10 +662,17 @@ struct rh_store {
             RH_HIP(kops->check_sorted(bkeys[cb].p, m, flag.p, stream));
         }
         nb = m;
-        if ((rc = resum_base(true))) return rc;
-        uint32_t bad = 0;
-        if (m) RH_HIP(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, stream));
+        load_flag.assign(10, 0);  // [0] unsorted flag, [2..9] the base total (8-byte aligned)
+        uint64_t *root_pin = reinterpret_cast<uint64_t *>(load_flag.data() + 2);
+        if ((rc = resum_base(true, root_pin))) return rc;
+        if (m) RH_HIP(hipMemcpyAsync(load_flag.data(), flag.p, 4, hipMemcpyDeviceToHost, stream));
+        return RH_OK;
+    }
+    int load_finish(size_t m, bool last_wins) {
+        int rc;
         if ((rc = sync())) return rc;
+        memcpy(root_b, load_flag.data() + 2, sizeof root_b);
+        const uint32_t bad = load_flag[0];
         if (!bad) return RH_OK;
         nb = 0;  // an error below leaves the store empty
         memset(root_b, 0, sizeof root_b);
@@ -1092,7 +1108,7 @@ struct rh_store {
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
         q_in.release(); q_res.release();
-        stage_in.release(); stage_out.release(); stage_out2.release();
+        stage_in.release(); stage_out.release(); stage_out2.release(); load_flag.release();
         r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); pr_out.release();
         snap.release();
         scratch.release();
@@ -1539,10 +1555,11 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
             return rc;
         if ((rc = proj->after(a->stream))) return rc;
     }
+    for (rh_store *x : {dated, proj})  // both stores' loads overlap on their own streams
+        if (x && (rc = x->load_begin(cols, n, dual))) return rc;
     for (rh_store *x : {dated, proj}) {
         if (!x) continue;
-        RH_HIP(hipSetDevice(x->device));
-        if ((rc = x->load_device(cols, n, true, dual))) return rc;
+        if ((rc = x->load_finish(n, true))) return rc;
         inf.keys = x->nb;
     }
     if (info) *info = inf;

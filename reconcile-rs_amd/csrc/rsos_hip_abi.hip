@@ -1023,17 +1023,32 @@ struct rh_store {
         const struct { const void *src; size_t off, bytes; } parts[5] = {
             {in.start_kinds, 0, r}, {in.end_kinds, o_ek, r}, {in.start_keys, o_sk, r * kl},
             {in.end_keys, o_ekeys, r * kl}, {in.aggregates, o_rem, r * sizeof(rh_aggregate)}};
+        // tiny rounds read their segments from, and write the round into, page-locked host memory
+        // (mapped into the device's address space): no copy command either way
+        const size_t worst = rh::round_layout(cap, r, kl).end;
+        const bool zero_copy = r <= rh::round_tiny_max() && in_bytes <= kRoundSmall && worst <= kRoundSmall;
+        const uint8_t *in_p = r_in.p;
+        uint8_t *out_p = r_out.p;
         if (in_bytes <= kRoundSmall) {
             stage_in.resize(in_bytes);
             for (const auto &p : parts)
                 if (p.src) memcpy(stage_in.data() + p.off, p.src, p.bytes);
-            RH_HIP(hipMemcpyAsync(r_in.p, stage_in.data(), in_bytes, hipMemcpyHostToDevice, stream));
+            if (zero_copy) {
+                pr_out.resize(worst);
+                void *di = nullptr, *dout = nullptr;
+                RH_HIP(hipHostGetDevicePointer(&di, stage_in.data(), 0));
+                RH_HIP(hipHostGetDevicePointer(&dout, pr_out.data(), 0));
+                in_p = static_cast<const uint8_t *>(di);
+                out_p = static_cast<uint8_t *>(dout);
+            } else {
+                RH_HIP(hipMemcpyAsync(r_in.p, stage_in.data(), in_bytes, hipMemcpyHostToDevice, stream));
+            }
         } else {
             for (const auto &p : parts)  // keys of an all-unbounded side may be NULL (never read)
                 if (p.src) RH_HIP(hipMemcpyAsync(r_in.p + p.off, p.src, p.bytes, hipMemcpyHostToDevice, stream));
         }
-        const uint8_t *d_sk = r_in.p, *d_ek = r_in.p + o_ek, *d_skeys = r_in.p + o_sk, *d_ekeys = r_in.p + o_ekeys;
-        const uint64_t *d_rem = reinterpret_cast<const uint64_t *>(r_in.p + o_rem);
+        const uint8_t *d_sk = in_p, *d_ek = in_p + o_ek, *d_skeys = in_p + o_sk, *d_ekeys = in_p + o_ekeys;
+        const uint64_t *d_rem = reinterpret_cast<const uint64_t *>(in_p + o_rem);
         uint64_t *lo = r_seg.p, *hi = lo + r, *loc = hi + r, *st = loc + 5 * r, *si = st + r, *ei = si + r,
                  *nch = ei + r, *choff = nch + r, *nen = choff + r, *enoff = nen + r;
         const rh::RoundSegs g{r_kind.p, lo, hi, loc, st, si, ei, nch, choff, nen, enoff};
@@ -1043,7 +1058,7 @@ struct rh_store {
         if (n) RH_HIP(kops->search_sampled(bkeys[cb].p, n, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
         if (r <= rh::round_tiny_max()) {
-            RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, r_out.p, stream));
+            RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, out_p, stream));
         } else if (r <= rh::round_small_max()) {
             RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
             RH_HIP(rh::launch_round_plan_scan(din, g, r, n, sq, b, r_out.p, stream));
@@ -1056,9 +1071,11 @@ struct rh_store {
             RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
             RH_HIP(rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
         }
-        const size_t worst = rh::round_layout(cap, r, kl).end;
         uint64_t h[5];
-        if (worst <= kRoundSmall) {
+        if (zero_copy) {
+            if ((rc = sync())) return rc;
+            memcpy(h, pr_out.data(), sizeof h);
+        } else if (worst <= kRoundSmall) {
             pr_out.resize(worst);
             RH_HIP(hipMemcpyAsync(pr_out.data(), r_out.p, worst, hipMemcpyDeviceToHost, stream));
             if ((rc = sync())) return rc;

@@ -9,7 +9,7 @@ CONFIG=${CONFIG:-config2}
 RECORDS=${RECORDS:-10000000}
 mkdir -p gpurun_out
 step() { local name=$1; shift; echo "== $name"; timeout -k 10 600 "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -n 3 "gpurun_out/$name.log"; [ $rc -eq 0 ] || exit $rc; }
-B="python3 bench.py --config $CONFIG --records $RECORDS --steps 10 --warmup 3 --cpu-baseline 0 --check 0"
+B="python3 bench.py --config $CONFIG --records $RECORDS --steps 10 --warmup 3 --cpu-baseline 0 --check 0 --e2e 0"
 step stats_$CONFIG rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats_$CONFIG -o run -- $B
 step fetch_$CONFIG rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_lift --output-format csv -d gpurun_out/fetch_$CONFIG -o run -- $B
 step write_$CONFIG rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_lift --output-format csv -d gpurun_out/write_$CONFIG -o run -- $B

@@ -7,12 +7,17 @@ One step = one pass of the path over one batch resident in HBM:
   aggregates of rbsr's default fan-out (rbsr/src/protocol.rs:40) -> (N > 1) all_gather of the
   per-shard (R x 40 B) aggregates over RCCL + carry-add combine.
 
-Workload (BASELINE.json configs[1]): 10 M records per GPU, 16 B key / 64 B value, dated
-(FingerprintTreeMap<[u8;16], Entry<Timestamp, Vec<u8>>>, 120 canonical bytes per record).
-Weak scaling: every GPU holds its own 10 M-record shard of one globally key-sorted set.
+Default workload (BASELINE.json configs[3], the north_star's shape): 100 M records in total,
+16 B key / 64 B value, dated (FingerprintTreeMap<[u8;16], Entry<Timestamp, Vec<u8>>>, 120
+canonical bytes per record), one globally key-sorted set cut into N equal-count key-range
+shards.  Strong scaling: at N = 1 one MI355X holds all 100 M records (the north_star target);
+at N = 8 each GPU holds 12.5 M.  `--config config2` is BASELINE configs[1] (10 M per GPU, weak).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config config1|config2|config3|config3_full|config4|config5|snapshot|rbsr|bench_u32]
-  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+--gpus N > 1 without a launcher: bench.py starts `python -m torch.distributed.run
+--nproc-per-node N` as a child process (no exec) and exits with its status; under a launcher
+(RANK / WORLD_SIZE set) WORLD_SIZE must equal N.  Fewer visible GPUs than N is an error.
 
 Prints ONE JSON line on rank 0.
 """
@@ -21,6 +26,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,20 +37,22 @@ sys.path.insert(0, os.path.join(ROOT, "reconcile-rs_amd"))
 import torch  # noqa: E402
 
 CONFIGS = {
-    # name: (key, value, record kind, records per GPU, description)
+    # name: (key, value, record kind, records, description); `records` are per GPU (weak scaling)
+    # unless the config is in STRONG (the total, cut into one key-range shard per GPU)
     "config1": ("u64", "bytes64", "plain", 1_000_000,
-                "BASELINE configs[0]: the reference's CPU case, FingerprintTreeMap<u64, Vec<u8>> of 1M "
-                "u64-key / 64 B-value records (GPU lift beside the CPU fill)"),
+                "BASELINE configs[0]: the reference's CPU case, FingerprintTreeMap<u64, Vec<u8>> of {per} "
+                "u64-key / 64 B-value records per GPU (GPU lift beside the CPU fill)"),
     "config2": ("bytes16", "bytes64", "dated", 10_000_000,
-                "BASELINE configs[1]: 10M records/GPU, 16 B key / 64 B value, dated Entry<Timestamp,Vec<u8>>"),
+                "BASELINE configs[1]: {per} records per GPU, 16 B key / 64 B value, dated Entry<Timestamp,Vec<u8>>"),
     "config3": ("bytes16", "bytes1024", "dated", 10_000_000,
-                "BASELINE configs[2] shape: 16 B key / 1 KiB value, dated (10M/GPU bench sample of the 100M set)"),
+                "BASELINE configs[2] shape: {per} records per GPU, 16 B key / 1 KiB value, dated"),
     "config3_full": ("bytes16", "bytes1024", "dated", 100_000_000,
-                     "BASELINE configs[2]: 100M records, 16 B key / 1 KiB value, dated, 1 GPU"),
-    "config4": ("bytes16", "bytes64", "dated", 12_500_000,
-                "BASELINE configs[3] per-GPU shard: 100M records over 8 GPUs, 16 B key / 64 B value"),
+                     "BASELINE configs[2]: {total} records in total ({per} per GPU), 16 B key / 1 KiB value, dated"),
+    "config4": ("bytes16", "bytes64", "dated", 100_000_000,
+                "BASELINE configs[3] (north_star shape): {total} records in total, 16 B key / 64 B value, dated "
+                "Entry<Timestamp,Vec<u8>>, key-range sharded over {world} GPU(s) ({per} per GPU)"),
     "bench_u32": ("u32", "u32", "plain", 10_000_000,
-                  "benches/bench.rs fill shape: FingerprintTreeMap<u32,u32>"),
+                  "benches/bench.rs fill shape: FingerprintTreeMap<u32,u32>, {per} records per GPU"),
     "config5": ("bytes16", "bytes64", "dated", 100_000_000,
                 "BASELINE configs[4]: 1M random inserts per batch into a 100M-record resident map"),
     "rbsr": ("bytes16", "bytes64", "dated", 10_000_000,
@@ -54,7 +63,16 @@ CONFIGS = {
                  "snapshot reload (SURVEY 8f row 4): RCNL v1 file of 10M entries (16 B key / 64 B value, "
                  "10% tombstones) resident in HBM -> dated + projection stores"),
 }
+STRONG = {"config4", "config3_full"}  # total fixed as N grows
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level table (spec)
+
+
+def _count(x: int) -> str:
+    return f"{x / 1e6:g}M" if x % 100_000 == 0 else str(x)
+
+
+def describe(config: str, total: int, per: int, world: int) -> str:
+    return CONFIGS[config][4].format(total=_count(total), per=_count(per), world=world)
 
 
 def parse():
@@ -62,11 +80,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", default="config2", choices=sorted(CONFIGS))
-    p.add_argument("--records", type=int, default=0, help="override records per GPU")
+    p.add_argument("--config", default="config4", choices=sorted(CONFIGS))
+    p.add_argument("--records", type=int, default=0,
+                   help="override the record count: the total for config4 / config3_full (strong scaling), "
+                        "per GPU for the others")
     p.add_argument("--ranges", type=int, default=16)
+    p.add_argument("--dump-aggregates", default="", help="write the step's combined range aggregates (JSON) here")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
-    p.add_argument("--cpu-sample", type=int, default=0, help="records in the CPU baseline sample (0: the whole shard)")
+    p.add_argument("--cpu-sample", type=int, default=0,
+                   help="records in the CPU baseline sample (0: min(shard, 10M), ~3 s of serial fill)")
     p.add_argument("--batch", type=int, default=1_000_000, help="config5: records per update batch")
     p.add_argument("--overwrite", type=float, default=0.0,
                    help="config5: fraction of each batch that re-stamps existing keys (the new - old delta)")
@@ -107,8 +129,43 @@ def gpu_spinup(ms: float, dev) -> dict:
     return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "launches": k}
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 from a plain `python bench.py`: start N ranks (one per GPU) under
+    torch.distributed.run as a child process and return its exit status.  Nothing here touches
+    the GPU (torch.cuda.device_count() does not initialise it), so the parent never holds a
+    device while the ranks run.  None: this process is already a rank (or N = 1)."""
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return None
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    have = torch.cuda.device_count()
+    if have < 1:
+        raise SystemExit("bench: no GPU visible")
+    # gloo rehearsal (BENCH_BACKEND=gloo) may put several ranks on one GPU; RCCL needs one each
+    if args.gpus > have and backend == "nccl":
+        raise SystemExit(f"bench: --gpus {args.gpus} but only {have} GPU(s) are visible")
+    if args.gpus == 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -119,11 +176,15 @@ def main():
         import torch.distributed as dist
         backend = os.environ.get("BENCH_BACKEND", "nccl")  # gloo: functional rehearsal only
         ngpu = torch.cuda.device_count()
+        if backend == "nccl" and world > ngpu:
+            raise SystemExit(f"bench: {world} ranks but only {ngpu} GPU(s): RCCL needs one GPU per rank")
         torch.cuda.set_device(local % max(ngpu, 1))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -140,8 +201,17 @@ def main():
         return reload(args, world, rank, dev, dist)
     if args.config == "rbsr":
         return reconcile(args, world, rank, dev, dist)
-    kname, vname, kind, n_default, desc = CONFIGS[args.config]
-    n = args.records or n_default
+    kname, vname, kind, n_default, _ = CONFIGS[args.config]
+    strong = args.config in STRONG
+    if strong:  # equal-count key-range shards of one fixed total: rank r holds [r*T/N, (r+1)*T/N)
+        total = args.records or n_default
+        base = total * rank // world
+        n = total * (rank + 1) // world - base
+    else:       # every rank holds its own n-record shard of one n*N-record set
+        n = args.records or n_default
+        total = n * world
+        base = rank * n
+    desc = describe(args.config, total, n, world)
     schema = getattr(RecordSchema, kind)(kname, vname)
     rec_bytes = schema.record_len()                     # canonical bytes BLAKE3 absorbs
     read_bytes = schema.key_row + schema.value_row + (20 if schema.dated_kind else 0)
@@ -151,15 +221,13 @@ def main():
         rec_bytes += schema.with_kind(2).record_len()
         hbm_bytes += 32
 
-    # this rank's shard of the globally sorted key space: global rows [rank*n, (rank+1)*n)
-    cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
+    # this rank's shard of the globally sorted key space: global rows [base, base + n)
+    cols = make_records(schema, n, seed=42, device=dev, first_index=base, key_space=total)
     if dist is not None:
         # the steps run on a high-priority stream: HIP maps it to its own hardware queue, so RCCL's
         # per-step all_gather (a normal-priority stream) cannot sit in front of the next lift
         torch.cuda.synchronize()
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
-    base = rank * n
-    total = n * world
     R = args.ranges
     lo_l, hi_l = local_ranges(equal_count_ranges(total, R), base, n)
     lo = torch.tensor(lo_l, dtype=torch.int64, device=dev)
@@ -240,10 +308,23 @@ def main():
     lift_avg_s = sum(a.elapsed_time(b) for a, b in lift_ms) / len(lift_ms) / 1e3
 
     root = res.cpu().numpy()  # the step's result: R combined range aggregates over all shards
+    per_rank = [n]
+    if dist is not None:  # every rank's record count, for the line (checked to cover the total)
+        cnt = torch.tensor([n], dtype=torch.int64, device=dev)
+        parts = [torch.empty_like(cnt) for _ in range(world)]
+        dist.all_gather(parts, cnt)
+        per_rank = [int(p.item()) for p in parts]
+        if sum(per_rank) != total:
+            raise SystemExit(f"bench: shards hold {sum(per_rank)} records, expected {total}")
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
+    if int(root[:, 4].sum()) != total:
+        raise SystemExit(f"bench: combined range aggregates count {int(root[:, 4].sum())} records, expected {total}")
+    if args.dump_aggregates:
+        with open(args.dump_aggregates, "w") as f:
+            json.dump({"world": world, "total": total, "ranges": [[int(x) for x in row] for row in root]}, f)
 
     recs = total * args.steps
     gib_s = recs * rec_bytes / elapsed / 2**30
@@ -255,16 +336,17 @@ def main():
         "unit": "GiB/s",
         "mrec_per_s": round(recs / elapsed / 1e6, 1),
         "n_gpus": world,
+        "rccl_world_size": dist.get_world_size() if dist is not None else 1,
         "steps": args.steps,
         "warmup": args.warmup, "spinup": spin,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (seeded, SURVEY §8d generator), resident in HBM before timing",
         "config": {"workload": desc + ("; both lifts of Replica::map_insert (dated + projection)" if dual else ""),
-                   "records_per_gpu": n, "records_total": total, "ranges": R,
+                   "records_per_gpu": n, "records_per_rank": per_rank, "records_total": total, "ranges": R,
                    "canonical_bytes_per_record": rec_bytes, "hbm_bytes_per_record": hbm_bytes,
                    "parallelism": f"key-range shards x{world}" + (
                        (" + RCCL all_gather per step (off the compute stream; combined at the end)" if dist.get_backend() == "nccl"
@@ -280,8 +362,8 @@ def main():
     if valu:
         line["valu"] = valu
     if args.cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample, dual)
-    if args.e2e == 1 or (args.e2e < 0 and args.config == "config2" and world == 1):
+        line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample or min(n, 10_000_000), dual)
+    if args.e2e == 1 or (args.e2e < 0 and args.config in ("config2", "config4") and world == 1):
         line["end_to_end"] = end_to_end(schema, cols, n)
     print(json.dumps(line), flush=True)
     if dist is not None:
@@ -298,7 +380,7 @@ def incremental(args, world, rank, dev, dist):
     n = args.records or n_default
     schema = getattr(RecordSchema, kind)(kname, vname)
     st = GpuFingerprintStore(schema, device=dev.index)
-    base = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
+    base = make_records(schema, n, seed=42, device=dev, first_index=rank * n, key_space=n * world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     st.load_bulk_device(base)
@@ -384,7 +466,7 @@ def reload(args, world, rank, dev, dist):
     kname, vname, kind, n_default, desc = CONFIGS["snapshot"]
     n = args.records or n_default
     sd, sp = RecordSchema.dated(kname, vname), RecordSchema.projection(kname, vname)
-    cols = make_records(sd, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world,
+    cols = make_records(sd, n, seed=42, device=dev, first_index=rank * n, key_space=n * world,
                         tombstone_fraction=0.1)
     blob = make_snapshot(cols, sd)
     file_bytes = blob.numel()
@@ -479,7 +561,7 @@ def reconcile(args, world, rank, dev, dist):
     n = args.records or n_default
     d = max(2, args.diffs)
     schema = getattr(RecordSchema, kind)(kname, vname)
-    cols = make_records(schema, n, seed=42 + rank, device=dev, first_index=rank * n, key_space=n * world)
+    cols = make_records(schema, n, seed=42, device=dev, first_index=rank * n, key_space=n * world)
     a, b = GpuFingerprintStore(schema, device=dev.index), GpuFingerprintStore(schema, device=dev.index)
     a.load_bulk_device(cols)
     b.load_bulk_device(cols)
@@ -743,12 +825,12 @@ def load_valu(config, n, lift_s):
     launch over this run's measured lift time, against the rate gfx950 sustains for this mix --
     one wave64 instruction per 4 cycles per SIMD (DESIGN.md §4) at the clock the PMC pass saw;
     peak_nominal: the full-rate 2-operand rate, one per 2 cycles per SIMD at 2.4 GHz."""
-    p = os.path.join(ROOT, "profiles", f"r01_valu_{config}.json")
+    p = _profile(f"valu_{config}.json", n)
+    if p is None:
+        return None
     try:
         with open(p) as f:
             v = json.load(f)
-        if int(v.get("records", -1)) != n:
-            return None
         instr = float(v["valu_wave_instructions_per_launch"])
         clock = float(v["effective_clock_ghz"]) * 1e9
         sustained = 256 * 4 * clock / 4
@@ -765,14 +847,24 @@ def load_valu(config, n, lift_s):
 def load_traffic(config, n):
     """HBM bytes per lift launch from the committed rocprofv3 PMC summary, if one exists for this
     config and size (profiles/traffic_<config>.json; FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)."""
-    p = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
-    try:
-        with open(p) as f:
-            t = json.load(f)
-        if int(t.get("records", -1)) == n:
-            return t.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    p = _profile(f"traffic_{config}.json", n)
+    if p is None:
+        return None
+    with open(p) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def _profile(suffix, n):
+    """The newest committed profile summary (profiles/rNN_<suffix>, newest round first) that was
+    collected at this record count, or None."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_" + suffix)), reverse=True):
+        try:
+            with open(p) as f:
+                if int(json.load(f).get("records", -1)) == n:
+                    return p
+        except (OSError, ValueError):
+            continue
     return None
 
 

@@ -346,6 +346,12 @@ int rh_wire_decode_range_aggregates(const rh_schema *schema, int key_form, int m
                                     size_t r_cap, uint8_t *start_kinds, void *start_keys, uint8_t *end_kinds,
                                     void *end_keys, rh_aggregate *aggregates, size_t *r_out, size_t *consumed);
 
+/* ---- testing ---------------------------------------------------------------------------
+ * Make the named internal failure point fail once (RH_ERR_OOM) on the calling thread; NULL or
+ * "" clears it.  Points: "snapshot.load_begin" (the projection store's half of a reload),
+ * "snapshot.load_finish" (the dated store's).  For tests of error paths only.              */
+int rh_debug_fail_point(const char *name);
+
 #ifdef __cplusplus
 }
 #endif

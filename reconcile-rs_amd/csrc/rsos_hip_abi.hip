@@ -37,6 +37,15 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
+// Failure injection for the error paths tests cannot otherwise reach (rh_debug_fail_point):
+// the named point fails once, with RH_ERR_OOM, on this thread.
+thread_local std::string g_fail_point;
+bool fail_point(const char *name) {
+    if (g_fail_point.empty() || g_fail_point != name) return false;
+    g_fail_point.clear();
+    return true;
+}
+
 #define RH_HIP(expr)                                                                           \
     do {                                                                                       \
         hipError_t e_ = (expr);                                                                \
@@ -487,6 +496,10 @@ template <class T>
 struct PinnedVec {
     T *p = nullptr;
     size_t n = 0, cap = 0;
+    // hipHostMallocMapped: the buffer also has a device address (hipHostGetDevicePointer), so a
+    // kernel may read it or write it in place; the writes are visible to the host once the
+    // stream has synchronised (the kernel's end-of-dispatch release)
+    unsigned flags = hipHostMallocMapped | hipHostMallocPortable;
     PinnedVec() = default;
     PinnedVec(const PinnedVec &) = delete;
     PinnedVec &operator=(const PinnedVec &) = delete;
@@ -500,7 +513,7 @@ struct PinnedVec {
         if (want <= cap) return;
         const size_t c = std::max<size_t>(std::max(want, cap + cap / 2), 64);
         T *q = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void **>(&q), c * sizeof(T), hipHostMallocDefault) != hipSuccess || !q)
+        if (hipHostMalloc(reinterpret_cast<void **>(&q), c * sizeof(T), flags) != hipSuccess || !q)
             throw std::bad_alloc();
         if (n) memcpy(q, p, n * sizeof(T));
         if (p) (void)hipHostFree(p);
@@ -560,6 +573,16 @@ struct rh_store {
     rh::Scratch scratch;
 
     uint64_t size() const { return (uint64_t)((int64_t)nb + dtotal); }
+    // After a failed load: drain the stream (no copy into host state still in flight) and leave
+    // the store empty, its size and root consistent
+    void reset_empty() {
+        (void)hipStreamSynchronize(stream);
+        (void)hipGetLastError();
+        nb = nd = 0;
+        dtotal = 0;
+        memset(root_b, 0, sizeof root_b);
+        memset(root_d, 0, sizeof root_d);
+    }
     // Wait for the stream by polling it: the batch path ends in one short wait for a 96-byte
     // result, where an interrupt-driven wake-up costs tens of microseconds per batch.  Long
     // waits (a compaction, a large load) fall back to the blocking call after ~1 ms.
@@ -643,6 +666,8 @@ struct rh_store {
     PinnedVec<uint32_t> load_flag;
     int load_begin(const rh_columns &c, size_t m, bool lifted) {
         int rc;
+        // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
+        if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
             (rc = counts.ensure(4)))
             return rc;
@@ -1026,7 +1051,7 @@ struct rh_store {
         // tiny rounds read their segments from, and write the round into, page-locked host memory
         // (mapped into the device's address space): no copy command either way
         const size_t worst = rh::round_layout(cap, r, kl).end;
-        const bool zero_copy = r <= rh::round_tiny_max() && in_bytes <= kRoundSmall && worst <= kRoundSmall;
+        bool zero_copy = r <= rh::round_tiny_max() && in_bytes <= kRoundSmall && worst <= kRoundSmall;
         const uint8_t *in_p = r_in.p;
         uint8_t *out_p = r_out.p;
         if (in_bytes <= kRoundSmall) {
@@ -1036,11 +1061,18 @@ struct rh_store {
             if (zero_copy) {
                 pr_out.resize(worst);
                 void *di = nullptr, *dout = nullptr;
-                RH_HIP(hipHostGetDevicePointer(&di, stage_in.data(), 0));
-                RH_HIP(hipHostGetDevicePointer(&dout, pr_out.data(), 0));
-                in_p = static_cast<const uint8_t *>(di);
-                out_p = static_cast<uint8_t *>(dout);
-            } else {
+                // both buffers are allocated mapped; if the runtime still gives no device address,
+                // take the copy path below instead
+                if (hipHostGetDevicePointer(&di, stage_in.data(), 0) != hipSuccess || !di ||
+                    hipHostGetDevicePointer(&dout, pr_out.data(), 0) != hipSuccess || !dout) {
+                    (void)hipGetLastError();
+                    zero_copy = false;
+                } else {
+                    in_p = static_cast<const uint8_t *>(di);
+                    out_p = static_cast<uint8_t *>(dout);
+                }
+            }
+            if (!zero_copy) {
                 RH_HIP(hipMemcpyAsync(r_in.p, stage_in.data(), in_bytes, hipMemcpyHostToDevice, stream));
             }
         } else {
@@ -1175,6 +1207,7 @@ int rh_store_destroy(rh_store *s) {
 
 int rh_store_load(rh_store *s, const rh_columns *h, size_t n) {
     if (!s || !h) return fail(RH_ERR_ARG, "NULL");
+    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
     RH_LOCK(s);
     int rc;
     if ((rc = s->staging.upload(s->schema, *h, n, s->stream))) return rc;
@@ -1183,6 +1216,7 @@ int rh_store_load(rh_store *s, const rh_columns *h, size_t n) {
 
 int rh_store_load_device(rh_store *s, const rh_columns *dev_cols, size_t n, void *after_stream) {
     if (!s) return fail(RH_ERR_ARG, "NULL");
+    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
     int rc = check_cols(s->schema, dev_cols, n);
     if (rc) return rc;
     RH_LOCK(s);
@@ -1572,14 +1606,33 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
             return rc;
         if ((rc = proj->after(a->stream))) return rc;
     }
-    for (rh_store *x : {dated, proj})  // both stores' loads overlap on their own streams
-        if (x && (rc = x->load_begin(cols, n, dual))) return rc;
+    // both stores' loads overlap on their own streams.  A failure in either half of either store
+    // leaves BOTH stores empty (streams drained): never a new size beside an old root, nor one
+    // store replaced and the other not
     for (rh_store *x : {dated, proj}) {
         if (!x) continue;
-        if ((rc = x->load_finish(n, true))) return rc;
+        if (x == proj && fail_point("snapshot.load_begin")) rc = fail(RH_ERR_OOM, "injected failure (load_begin)");
+        else rc = x->load_begin(cols, n, dual);
+        if (rc) break;
+    }
+    for (rh_store *x : {dated, proj}) {
+        if (rc || !x) break;
+        if (x == dated && fail_point("snapshot.load_finish")) rc = fail(RH_ERR_OOM, "injected failure (load_finish)");
+        else rc = x->load_finish(n, true);
         inf.keys = x->nb;
     }
+    if (rc) {
+        const std::string msg = g_err;
+        for (rh_store *x : {dated, proj})
+            if (x) x->reset_empty();
+        return fail(rc, msg);
+    }
     if (info) *info = inf;
+    return RH_OK;
+}
+
+int rh_debug_fail_point(const char *name) {
+    g_fail_point = name ? name : "";
     return RH_OK;
 }
 

@@ -107,6 +107,7 @@ SIGNATURES = [
                                                   U8P, SZ, C.POINTER(C.c_size_t)]),
     ("rh_wire_decode_range_aggregates", C.c_int, [C.POINTER(Schema), C.c_int, C.c_int, U8P, SZ, SZ, U8P, VP, U8P,
                                                   VP, P, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    ("rh_debug_fail_point", C.c_int, [C.c_char_p]),
 ]
 
 _lib = None

@@ -1,10 +1,11 @@
 """Seeded synthetic records of the BASELINE shapes, generated directly in HBM.
 
-Follows SURVEY.md §8(d): keys are unique and sorted by memcmp (the Ord of [u8; L]); stamps
+Follows SURVEY.md §8(d): SplitMix64 streams (counter-based: every byte is a function of the
+seed and the global row index), keys unique and sorted by memcmp (the Ord of [u8; L]); stamps
 follow benches/bench.rs:286-293's pattern (physical = 1_700_000_000_000 + i, logical 0,
 node_id 1); values are random bytes; optional tombstones at a given fraction.  Keys: the
-first 8 bytes are the big-endian u64 (i << 24 | r24) -- strictly increasing, hence unique
-and memcmp-sorted -- and the remaining key bytes are random.
+first 8 bytes are the big-endian u64 i * stride + r (r < stride) -- strictly increasing, hence
+unique and memcmp-sorted -- and the remaining key bytes are random.
 """
 from __future__ import annotations
 
@@ -16,14 +17,45 @@ from .schema import RecordSchema
 from . import _abi as A
 
 
-def _rand_bytes(gen: torch.Generator, shape, device) -> torch.Tensor:
-    # int64 random words viewed as bytes (fast on device)
-    n = 1
-    for s in shape:
-        n *= s
-    words = (n + 7) // 8
-    w = torch.randint(-2**63, 2**63 - 1, (words,), generator=gen, device=device, dtype=torch.int64)
-    return w.view(torch.uint8)[:n].view(*shape)
+_M64 = (1 << 64) - 1
+
+
+def _s64(c: int) -> int:
+    """An unsigned 64-bit constant as the int64 torch computes with (two's complement)."""
+    c &= _M64
+    return c - (1 << 64) if c >> 63 else c
+
+
+_GOLD, _C1, _C2 = _s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)
+
+
+def _srl(z: torch.Tensor, k: int) -> torch.Tensor:
+    """Logical right shift of int64 bit patterns."""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def splitmix64(seed: int, ctr: torch.Tensor) -> torch.Tensor:
+    """Counter-based SplitMix64: the ctr-th output of the stream seeded `seed`,
+    as int64 bit patterns.  Element i depends only on (seed, ctr[i]), so any row range of a data
+    set is generated identically whatever shard or chunk asks for it."""
+    z = (ctr + 1) * _GOLD + _s64(seed * 0xD1B54A32D192ED03)
+    z = (z ^ _srl(z, 30)) * _C1
+    z = (z ^ _srl(z, 27)) * _C2
+    return z ^ _srl(z, 31)
+
+
+def _row_bytes(seed: int, idx: torch.Tensor, width: int, chunk_words: int = 1 << 25) -> torch.Tensor:
+    """(n, width) bytes: row i = the words idx[i] * W .. idx[i] * W + W - 1 of the stream, W =
+    ceil(width / 8); generated in row chunks so temporaries stay ~chunk_words words."""
+    n, w8 = idx.shape[0], (width + 7) // 8
+    out = torch.empty((n, w8 * 8), dtype=torch.uint8, device=idx.device)
+    step = max(1, chunk_words // max(w8, 1))
+    lane = torch.arange(w8, device=idx.device, dtype=torch.int64)
+    for lo in range(0, n, step):
+        hi = min(n, lo + step)
+        ctr = idx[lo:hi, None] * w8 + lane[None, :]
+        out[lo:hi] = splitmix64(seed, ctr).view(torch.uint8).view(hi - lo, w8 * 8)
+    return out[:, :width] if width != w8 * 8 else out
 
 
 def make_records(schema: RecordSchema, n: int, seed: int = 42, device="cuda",
@@ -32,38 +64,39 @@ def make_records(schema: RecordSchema, n: int, seed: int = 42, device="cuda",
     """Rows [first_index, first_index + n) of a key-sorted set of `key_space` records
     (default first_index + n) whose keys spread evenly over the whole key space: row i's
     first 8 key bytes are the big-endian u64 i * stride + r, r < stride = 2^64 / key_space.
-    random_keys: uniformly random keys instead (unsorted; update batches that land anywhere
-    in an existing key range)."""
+    Every byte is a counter-based SplitMix64 function of (seed, global row index), so a shard
+    [a, b) of the set is the same rows whether it is generated alone or as part of the whole
+    (strong-scaling runs at any GPU count hash the same data set).
+    random_keys: uniformly random byte keys instead (unsorted; update batches that land
+    anywhere in an existing key range)."""
     dev = torch.device(device)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(seed)
     cols: Dict[str, torch.Tensor] = {}
     idx = torch.arange(first_index, first_index + n, device=dev, dtype=torch.int64)
+    sk, sv, st = seed * 4 + 1, seed * 4 + 2, seed * 4 + 3  # key / value / tag streams
     if schema.key_kind == A.KEY_BYTES:
         kl = schema.key_len
-        keys = _rand_bytes(gen, (n, kl), dev).clone()
+        keys = _row_bytes(sk, idx, kl).contiguous()
         space = max(key_space or (first_index + n), 2)
         stride = min((1 << 64) // space, (1 << 63) - 1)
-        r = torch.randint(0, stride, (n,), generator=gen, device=dev, dtype=torch.int64)
-        head = idx * stride + r  # wraps in int64; the bit pattern is the unsigned value
-        # big-endian bytes of head into keys[:, :8]
-        shifts = torch.arange(56, -8, -8, device=dev, dtype=torch.int64)
         if kl >= 8 and not random_keys:
+            r = _srl(splitmix64(st + (1 << 32), idx), 1) % stride
+            head = idx * stride + r  # wraps in int64; the bit pattern is the unsigned value
+            shifts = torch.arange(56, -8, -8, device=dev, dtype=torch.int64)  # big-endian bytes
             keys[:, :8] = ((head[:, None] >> shifts[None, :]) & 0xFF).to(torch.uint8)  # arithmetic >> ok: & 0xFF
         cols["keys"] = keys.contiguous()
-    elif schema.key_kind == A.KEY_U64:
-        r = torch.randint(0, 1 << 20, (n,), generator=gen, device=dev, dtype=torch.int64)
+    elif schema.key_kind == A.KEY_U64:  # integer keys stay sorted (random_keys applies to byte keys)
+        r = _srl(splitmix64(sk, idx), 44)  # < 2^20
         cols["keys"] = ((idx << 20) | r).contiguous().view(torch.uint8).view(n, 8)
     elif schema.key_kind == A.KEY_U32:
         cols["keys"] = idx.to(torch.int32).contiguous().view(torch.uint8).view(n, 4)
     if schema.value_row:
-        cols["values"] = _rand_bytes(gen, (n, schema.value_row), dev).contiguous()
+        cols["values"] = _row_bytes(sv, idx, schema.value_row).contiguous()
     if schema.record_kind == A.REC_DATED:
         cols["phys"] = (1_700_000_000_000 + idx).contiguous()
         cols["logical"] = torch.zeros(n, dtype=torch.int32, device=dev)
         cols["node"] = torch.ones(n, dtype=torch.int64, device=dev)
     if schema.record_kind != A.REC_PLAIN and tombstone_fraction > 0:
-        u = torch.rand(n, generator=gen, device=dev)
+        u = _srl(splitmix64(st, idx), 11).to(torch.float64) * (1.0 / (1 << 53))
         cols["tags"] = (u < tombstone_fraction).to(torch.uint8)
     return cols
 

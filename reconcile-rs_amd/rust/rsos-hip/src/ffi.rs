@@ -170,4 +170,5 @@ extern "C" {
                                            len: usize, r_cap: usize, start_kinds: *mut u8, start_keys: *mut c_void,
                                            end_kinds: *mut u8, end_keys: *mut c_void, aggregates: *mut rh_aggregate,
                                            r_out: *mut usize, consumed: *mut usize) -> c_int;
+    pub fn rh_debug_fail_point(name: *const c_char) -> c_int;
 }

@@ -126,10 +126,22 @@ impl Batch {
         for (k, v) in items {
             b.keys.extend(k.column_bytes());
             let mut row = RecordRow::default();
-            if let Some(v) = v {
-                v.write(&mut row);
+            match v {
+                Some(v) => {
+                    v.write(&mut row);
+                    // a present value must fill the value column exactly: padding or truncating it
+                    // would hash some other record and reconcile silently wrongly (rsos_trait.rs:54-56)
+                    if !row.tombstone {
+                        assert_eq!(row.value.len(), V::VALUE_LEN as usize,
+                                   "rsos-hip: GpuRecord::write produced a {}-byte value for a {}-byte value column",
+                                   row.value.len(), V::VALUE_LEN);
+                    } else {
+                        assert!(row.value.is_empty(), "rsos-hip: a tombstone row carries no value bytes");
+                        row.value = vec![0; V::VALUE_LEN as usize]; // never hashed (State::Tombstone)
+                    }
+                }
+                None => row.value = vec![0; V::VALUE_LEN as usize], // a delete: the value columns are ignored
             }
-            row.value.resize(V::VALUE_LEN as usize, 0);
             b.values.extend(&row.value);
             b.phys.push(row.phys);
             b.logical.push(row.logical);

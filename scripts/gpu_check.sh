@@ -17,7 +17,7 @@ run() {  # name, timeout, cmd...
   if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "fatal step $name ($rc): stopping"; exit $rc; fi
   return 0
 }
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+run pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench 600 python bench.py --steps "$STEPS" --warmup 5 --e2e 1
 run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps "$STEPS" --warmup 5 --cpu-baseline 0 --check 0 --e2e 0

@@ -1,0 +1,82 @@
+"""bench.py's multi-GPU path, end to end.
+
+GPU (one MI355X): the exact path the driver's N-GPU run times -- bench.py starting its own ranks
+(torch.distributed.run child), each rank lifting its key-range shard on a high-priority stream,
+gather_async of the per-shard (R x 40 B) aggregates after every step, the device
+combine_aggregates -- run at world size 2 with gloo (both ranks share the one GPU), checked bit
+for bit against the same workload in one process, and against an independent torch reduction of
+the whole set's lifts.  Strong scaling: both runs hash the same 100 M-shaped data set (the
+synthetic generator is counter-based, so a shard is the same rows at any world size).
+
+CPU: the launcher's argument checks (no GPU needed).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+M256 = 1 << 256
+
+
+def _bench(args, env_extra=None, timeout=240):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus 2 on a host with fewer GPUs must fail loudly, not report a one-GPU number."""
+    import torch
+    have = torch.cuda.device_count()
+    r = _bench(["--gpus", str(have + 1), "--steps", "1", "--warmup", "0"], timeout=120)
+    assert r.returncode != 0
+    assert "GPU" in (r.stderr + r.stdout)
+
+
+def test_bench_refuses_world_size_mismatch():
+    r = _bench(["--gpus", "2", "--steps", "1"], env_extra={"WORLD_SIZE": "3", "RANK": "0"}, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=3" in (r.stderr + r.stdout)
+
+
+def _agg_int(row):
+    return sum((int(x) & (2**64 - 1)) << (64 * i) for i, x in enumerate(row[:4]))
+
+
+@pytest.mark.gpu
+def test_bench_world2_gloo_equals_single_process(tmp_path, gpu):
+    total = 3_000_001  # not a multiple of the world size: shards of 1,500,000 and 1,500,001
+    common = ["--config", "config4", "--records", str(total), "--steps", "3", "--warmup", "1",
+              "--cpu-baseline", "0", "--e2e", "0", "--spinup-ms", "0", "--check", "0"]
+    one, two = tmp_path / "one.json", tmp_path / "two.json"
+    r1 = _bench(common + ["--gpus", "1", "--dump-aggregates", str(one)])
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    r2 = _bench(common + ["--gpus", "2", "--dump-aggregates", str(two)], env_extra={"BENCH_BACKEND": "gloo"})
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    line2 = json.loads(r2.stdout.strip().splitlines()[-1])
+    assert line2["n_gpus"] == 2 and line2["rccl_world_size"] == 2 and line2["scaling"] == "strong"
+    assert line2["config"]["records_per_rank"] == [1_500_000, 1_500_001]
+    a, b = json.loads(one.read_text()), json.loads(two.read_text())
+    assert a["world"] == 1 and b["world"] == 2
+    assert a["ranges"] == b["ranges"]  # the 16 combined range aggregates, bit for bit
+    # and the whole set's root against an independent torch reduction of its lifts
+    import torch
+    from rsos_hip import RecordSchema, lift_records
+    from rsos_hip.synth import make_records
+    s = RecordSchema.dated("bytes16", "bytes64")
+    cols = make_records(s, total, seed=42, key_space=total)
+    fps, _ = lift_records(s, cols, block_sums=False)
+    limbs16 = fps.view(torch.int16).to(torch.int64) & 0xFFFF
+    col = limbs16.sum(dim=0).cpu().tolist()
+    want = sum(int(c) << (16 * i) for i, c in enumerate(col)) % M256
+    assert sum(_agg_int(r) for r in a["ranges"]) % M256 == want
+    assert sum(int(r[4]) for r in a["ranges"]) == total
+    # equal-count ranges: range j holds rows [total*j/16, total*(j+1)/16)
+    assert [int(r[4]) for r in a["ranges"]] == [total * (j + 1) // 16 - total * j // 16 for j in range(16)]

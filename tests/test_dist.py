@@ -38,7 +38,7 @@ def _rank_main(rank, world, port, n, R, out_q):
         from rsos_hip.synth import make_records, to_host
         s = RecordSchema.dated("bytes16", "bytes64")
         base, _ = shard_rows(rank, world, n)
-        cols = make_records(s, n, seed=42 + rank, device="cpu", first_index=base, key_space=n * world)
+        cols = make_records(s, n, seed=42, device="cpu", first_index=base, key_space=n * world)
         h = to_host(cols)
         sc = O.Schema(s.key_kind, s.key_len, s.value_kind, s.value_len, s.record_kind, 0)
         fps = O.Records(sc, h["keys"], h["values"], h["phys"], h["logical"], h["node"]).lift(threads=2)
@@ -96,7 +96,7 @@ def test_sharded_range_aggregates_gloo_world2(oracle_lib):
     sc = O.Schema(s.key_kind, s.key_len, s.value_kind, s.value_len, s.record_kind, 0)
     fps = []
     for r in range(world):
-        h = to_host(make_records(s, n, seed=42 + r, device="cpu", first_index=r * n, key_space=n * world))
+        h = to_host(make_records(s, n, seed=42, device="cpu", first_index=r * n, key_space=n * world))
         fps.append(O.Records(sc, h["keys"], h["values"], h["phys"], h["logical"], h["node"]).lift(threads=2))
     allf = np.concatenate(fps)
     for j, (a, b) in enumerate(equal_count_ranges(n * world, R)):

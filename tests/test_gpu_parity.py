@@ -459,6 +459,44 @@ def test_full_size_config2_properties(gpu, oracle_lib):
     assert (agg_int(out[1]) + agg_int(out[2])) % M256 == want_root
 
 
+@pytest.mark.parametrize("value,n", [("bytes64", 100_000_000), ("bytes1024", 100_000_000)],
+                         ids=["north_star_100M_x_64B", "config3_full_100M_x_1KiB"])
+def test_full_size_100m_properties(gpu, oracle_lib, value, n):
+    """The north_star's 100 M x 16 B / 64 B dated set (bench.py's default config4 at N = 1) and
+    BASELINE configs[2]'s 100 M x 16 B / 1 KiB: oracle-checked windows at both ends and the
+    middle, the root aggregate against an independent torch reduction of the kernel's
+    fingerprints (u16 limbs), and partition additivity of range aggregates over the 16 equal
+    count ranges the bench queries."""
+    import torch
+    from rsos_hip import RecordSchema, lift_records, range_aggregates, reduce_blocks
+    from rsos_hip.synth import make_records, to_host
+    s = RecordSchema.dated("bytes16", value)
+    cols = make_records(s, n, seed=42, key_space=n)
+    fps, bs = lift_records(s, cols)
+    ss = reduce_blocks(bs)
+    w = 2048
+    for lo in (0, n // 2 - w // 2, n - w):
+        want = oracle_records(oracle_lib, s, to_host(cols, lo, lo + w)).lift(threads=8)
+        assert np.array_equal(fps[lo:lo + w].cpu().numpy(), want), lo
+    # a strided sample across the whole set (one row in ~50 k)
+    rows = torch.arange(12345, n, 48_611, device="cuda")
+    sub = {k: v[rows] for k, v in cols.items()}
+    want = oracle_records(oracle_lib, s, to_host(sub)).lift(threads=8)
+    assert np.array_equal(fps[rows].cpu().numpy(), want)
+    del cols, sub
+    want_root = 0
+    for lo in range(0, n, 25_000_000):  # the u16-limb reduction in chunks (bounded temporaries)
+        want_root += _torch_root(torch, fps[lo:lo + 25_000_000])
+    want_root %= M256
+    cuts = [n * j // 16 for j in range(17)]
+    lo_t = torch.tensor([0] + cuts[:-1], dtype=torch.int64, device="cuda")
+    hi_t = torch.tensor([n] + cuts[1:], dtype=torch.int64, device="cuda")
+    out = range_aggregates(fps, bs, ss, lo_t, hi_t).cpu().numpy()
+    assert agg_int(out[0]) == want_root and int(out[0][4]) == n
+    assert sum(agg_int(r) for r in out[1:]) % M256 == want_root
+    assert [int(r[4]) for r in out[1:]] == [b - a for a, b in zip(cuts, cuts[1:])]
+
+
 def test_store_device_batches_bytes16_dated(gpu, oracle_lib):
     """Batched insert / overwrite / delete on the device merge path (16 B keys, dated records),
     checked against a fold of the oracle's lift over the expected contents after each batch."""
@@ -744,4 +782,26 @@ def test_full_size_incremental_properties(gpu):
     assert agg.size == st.rank(hi_key) - st.rank(lo_key)
     st.compact()
     assert st.aggregate() == root and st.stats()["delta_rows"] == 0
+    st.close()
+
+
+def test_store_load_refuses_2_pow_31_rows(gpu):
+    """Ranks are 32-bit on the device: a load of >= 2^31 rows is an argument error before any
+    column is read (host or device path), and the store keeps its contents."""
+    import ctypes as C
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema, _abi as A
+    from rsos_hip.synth import make_records
+    s = RecordSchema.plain("u32", "u32")
+    st = GpuFingerprintStore(s)
+    st.load_bulk_device(make_records(s, 1000, seed=1))
+    root = st.aggregate()
+    tiny = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    cols = A.Columns(tiny.data_ptr(), None, None, None, None, tiny.data_ptr())
+    assert A.lib().rh_store_load_device(st._h, C.byref(cols), 1 << 31, None) == A.ERR_ARG
+    assert b"2^31" in A.lib().rh_last_error()
+    host = (C.c_uint8 * 64)()
+    hcols = A.Columns(C.addressof(host), None, None, None, None, C.addressof(host))
+    assert A.lib().rh_store_load(st._h, C.byref(hcols), (1 << 31) + 5) == A.ERR_ARG
+    assert st.aggregate() == root and st.size() == 1000
     st.close()

@@ -268,3 +268,33 @@ def test_device_snapshot_builder_matches_oracle(rsos_hip_lib, kv, form):
     want = OS.encode_snapshot(h["keys"], h["phys"], h["logical"], h["node"], h["tags"], h["values"],
                               ints.get(kv[0], form), ints.get(kv[1], "bytes"))
     assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("point", ["snapshot.load_begin", "snapshot.load_finish"])
+def test_reload_failure_leaves_both_stores_empty(gpu, point):
+    """A reload that fails after the first store has begun loading (an injected allocation
+    failure in the projection's load_begin, or in the dated store's load_finish) leaves BOTH
+    stores empty and consistent -- size 0 and the zero root -- never the new size beside the old
+    root; the stores reload normally afterwards."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, _abi as A
+    from rsos_hip.snapshot import load_snapshot
+    from rsos_hip.synth import make_records, make_snapshot
+    sd, sp, _ = _schemas("b16_b64")
+    old = make_records(sd, 3000, seed=11)
+    new = make_records(sd, 5000, seed=12, tombstone_fraction=0.1)
+    dated, proj = GpuFingerprintStore(sd), GpuFingerprintStore(sp)
+    load_snapshot(make_snapshot(old, sd), dated, proj)
+    assert dated.size() == proj.size() == 3000
+    blob = make_snapshot(new, sd)
+    A.lib().rh_debug_fail_point(point.encode())
+    with pytest.raises(A.RsosHipError) as e:
+        load_snapshot(blob, dated, proj)
+    assert e.value.code == A.ERR_OOM and "injected" in str(e.value)
+    for st in (dated, proj):
+        agg = st.aggregate()
+        assert st.size() == 0 and agg.size == 0 and agg.fingerprint.to_int() == 0
+    info = load_snapshot(blob, dated, proj)
+    assert info.keys == 5000 == dated.size() == proj.size()
+    torch.cuda.synchronize()

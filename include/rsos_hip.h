@@ -259,6 +259,17 @@ typedef struct rh_round_outcome { /* RoundOutcome (protocol.rs:135-142)         
 int rh_store_protocol_round(rh_store *store, int policy, uint64_t fan_out, const rh_segments *active,
                             rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome);
 
+/* Host tier (the diff path is latency-bound).  enable = 1 keeps, next to the
+ * HBM-resident store, a host copy of the keys in rank order and the exclusive prefix sums of the
+ * per-row fingerprints (computed on the device from the GPU lift; (key_len + 32) B of page-locked
+ * host memory per row), refreshed on the first question after the contents change.  Then
+ * rank / ranks / select / keys, aggregate(s) by rank or by key bounds, resolve / split with at most
+ * 16 * round_max questions, and protocol rounds of at most round_max segments are answered on the
+ * host: no device round trip, O(log n) per question -- the reference's query cost
+ * (query.rs:25-167).  Larger rounds stay on the device.  round_max 0 = the default (128).
+ * enable = 0 frees the copy.  Answers are identical either way.                              */
+int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
+
 /* Batched insert / overwrite / delete (FingerprintTreeMap::insert / remove, mutate.rs:23-154).
  * ops[i]: 0 = insert-or-overwrite record i, 1 = delete key i (its value columns are ignored).
  * Keys within one batch must be distinct (RH_ERR_ARG, store unchanged).  On return every

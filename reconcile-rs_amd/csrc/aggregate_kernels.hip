@@ -767,6 +767,119 @@ hipError_t launch_lift_encoded(const uint8_t *bytes, const uint64_t *offs, uint6
     return hipGetLastError();
 }
 
+// ---- exclusive 256-bit prefix sums (the host tier's per-row prefix) -----------------
+// out[i] = Σ in[0..i) mod 2^256 for i in [0, n] (out[n] = the total): one workgroup per chunk of
+// 256 entries, a carry-save wave scan (64-bit shuffles of the 8 u32-limb sums, which stay below
+// 2^40), the waves' totals through LDS, then the chunk's base -- base[c] = Σ in[0..256 c), from the
+// level above (the block sums' prefix for rows, the super-block sums' prefix for blocks).
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t x, int d) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    lo = __shfl_up(lo, d, 64);
+    hi = __shfl_up(hi, d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__global__ __launch_bounds__(256) void k_prefix256(const uint8_t *in, uint64_t n, const uint8_t *base,
+                                                   uint8_t *out) {
+    __shared__ uint64_t wtot[4][8];
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n) load_fp(in, i, f);
+    Acc a;
+#pragma unroll
+    for (int q = 0; q < 8; q++) a.l[q] = f[q];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint64_t y = shfl_up_u64(a.l[q], d);
+            if (lane >= (uint32_t)d) a.l[q] += y;
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) wtot[w][q] = a.l[q];
+    }
+    __syncthreads();
+    uint32_t bf[8];
+    load_fp(base, blockIdx.x, bf);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        uint64_t v = a.l[q] - f[q] + bf[q];  // inclusive -> exclusive, + the chunk's base
+        for (uint32_t k = 0; k < w; k++) v += wtot[k][q];
+        a.l[q] = v;
+    }
+    if (i <= n) {
+        uint32_t o[8];
+        acc_normalise(a, o);
+        store_sum(out, i, o);
+    }
+}
+
+// The top level, one workgroup: out[i] = Σ in[0..i) for i in [0, n], chunk by chunk with the
+// running total carried in LDS (n = the super-block count: at most 2^31 / 65536 + 1 entries)
+__global__ __launch_bounds__(256) void k_prefix_top(const uint8_t *in, uint64_t n, uint8_t *out) {
+    __shared__ uint64_t wtot[4][8];
+    __shared__ uint32_t run[8];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x < 8) run[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 <= n; c0 += 256) {
+        const uint64_t i = c0 + threadIdx.x;
+        uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (i < n) load_fp(in, i, f);
+        Acc a;
+#pragma unroll
+        for (int q = 0; q < 8; q++) a.l[q] = f[q];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint64_t y = shfl_up_u64(a.l[q], d);
+                if (lane >= (uint32_t)d) a.l[q] += y;
+            }
+        }
+        if (lane == 63) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) wtot[w][q] = a.l[q];
+        }
+        __syncthreads();
+        Acc e;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            uint64_t v = a.l[q] - f[q] + run[q];
+            for (uint32_t k = 0; k < w; k++) v += wtot[k][q];
+            e.l[q] = v;
+        }
+        uint32_t o[8];
+        acc_normalise(e, o);
+        if (i <= n) store_sum(out, i, o);
+        __syncthreads();  // every lane has read run[] and wtot[]
+        if (threadIdx.x == 255) {  // the chunk's inclusive total = the next chunk's running base
+            Acc t;
+#pragma unroll
+            for (int q = 0; q < 8; q++) t.l[q] = e.l[q] + f[q];
+            uint32_t r[8];
+            acc_normalise(t, r);
+#pragma unroll
+            for (int q = 0; q < 8; q++) run[q] = r[q];
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre,
+                         uint8_t *bpre, uint8_t *out, hipStream_t st) {
+    const uint64_t nbk = (n + 255) / 256, ns = (nbk + 255) / 256;
+    hipLaunchKernelGGL(k_prefix_top, dim3(1), dim3(256), 0, st, ssums, ns, spre);
+    hipLaunchKernelGGL(k_prefix256, dim3((uint32_t)(nbk / 256 + 1)), dim3(256), 0, st, bsums, nbk,
+                       (const uint8_t *)spre, bpre);
+    hipLaunchKernelGGL(k_prefix256, dim3((uint32_t)(n / 256 + 1)), dim3(256), 0, st, fps, n, (const uint8_t *)bpre,
+                       out);
+    return hipGetLastError();
+}
+
 hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st, uint32_t stride) {
     if (n_in == 0) return hipSuccess;
     const uint64_t g = (n_in + 255) / 256;

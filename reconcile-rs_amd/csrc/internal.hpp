@@ -24,6 +24,11 @@ hipError_t launch_lift_fixed(const uint8_t *bytes, uint64_t len, uint64_t n, uin
 hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStream_t st, uint32_t stride = 32);
 // out[0..3] = Σ of n 256-bit entries (n small: one workgroup)
 hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_t st);
+// Exclusive prefix sums of n fingerprints: out[i] = Σ fps[0..i) for i in [0, n] (n + 1 entries),
+// from the run's block sums (ceil(n/256)) and super-block sums (ceil(n/65536)); scratch: spre
+// (ceil(n/65536) + 1 entries), bpre (ceil(n/256) + 1 entries), 32 B each
+hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre,
+                         uint8_t *bpre, uint8_t *out, hipStream_t st);
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
                               hipStream_t st, uint32_t stride = 32);

@@ -24,6 +24,7 @@
 
 #include "../../include/rsos_hip.h"
 #include "internal.hpp"
+#include "host_tier.hpp"
 #include "lift_kernels.hpp"
 #include "snapshot_kernels.hpp"
 #include "store_kernels.hpp"
@@ -582,6 +583,44 @@ struct rh_store {
         dtotal = 0;
         memset(root_b, 0, sizeof root_b);
         memset(root_d, 0, sizeof root_d);
+        version++;
+    }
+    // ---- the host tier (host_tier.hpp) ---------------------------------------------------------
+    uint64_t version = 0;       // bumped by every change of contents (load, batch, failed load)
+    bool tier_on = false;
+    uint64_t tier_version = ~0ull, tier_round_max = 128;
+    rh::HostTier tier;
+    PinnedVec<uint8_t> tier_keys;
+    PinnedVec<uint64_t> tier_prefix;
+    DevBuf<uint8_t> tier_dpre, tier_spre, tier_bpre;
+    std::vector<uint8_t> tier_out;  // the last host round, in round_layout()
+    bool tier_fresh() const { return tier_on && tier_version == version; }
+    // bring the host tier up to date: compact, the prefix sums on the device, one copy of the keys
+    // and one of the prefix sums down.  Costs ~(kl + 32) B per row of PCIe, once per change.
+    int tier_refresh() {
+        int rc;
+        if ((rc = compact())) return rc;
+        const uint64_t n = nb, nbk = rh_num_blocks(n), ns = rh_num_superblocks(n);
+        if ((rc = tier_dpre.ensure((n + 1) * 32 + 64)) || (rc = tier_spre.ensure((ns + 1) * 32 + 64)) ||
+            (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)))
+            return rc;
+        try {
+            tier_keys.resize(n * kl + 64);
+            tier_prefix.resize((n + 1) * 4 + 8);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+        }
+        if (n) {
+            RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, stream));
+            RH_HIP(hipMemcpyAsync(tier_keys.data(), bkeys[cb].p, n * kl, hipMemcpyDeviceToHost, stream));
+            RH_HIP(hipMemcpyAsync(tier_prefix.data(), tier_dpre.p, (n + 1) * 32, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+        } else {
+            memset(tier_prefix.data(), 0, 32);
+        }
+        tier.build((uint32_t)kl, schema.key_kind, n, tier_keys.data(), tier_prefix.data());
+        tier_version = version;
+        return RH_OK;
     }
     // Wait for the stream by polling it: the batch path ends in one short wait for a 96-byte
     // result, where an interrupt-driven wake-up costs tens of microseconds per batch.  Long
@@ -668,6 +707,7 @@ struct rh_store {
         int rc;
         // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        version++;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
             (rc = counts.ensure(4)))
             return rc;
@@ -798,6 +838,7 @@ struct rh_store {
         out[0] = out[1] = out[2] = 0;
         if (m == 0) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
         if ((rc = lfps.ensure(m * 32 + 64)) || (rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) ||
             (rc = sops.ensure(m + 64)) || (rc = bpay.ensure(m * sizeof(rh::DeltaRec) + 64)) ||
             (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
@@ -1159,6 +1200,7 @@ struct rh_store {
         q_in.release(); q_res.release();
         stage_in.release(); stage_out.release(); stage_out2.release(); load_flag.release();
         r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); pr_out.release();
+        tier_keys.release(); tier_prefix.release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release();
         snap.release();
         scratch.release();
         if (dep) (void)hipEventDestroy(dep);
@@ -1169,6 +1211,16 @@ struct rh_store {
 #define RH_LOCK(s)                                  \
     std::lock_guard<std::mutex> guard_((s)->mu);    \
     RH_HIP(hipSetDevice((s)->device))
+
+// Under the store's lock: 1 if the host tier answers (refreshing it first if the store changed
+// since; only then is the device touched), 0 if the tier is off, < 0 on error
+static int tier_ready(rh_store *s) {
+    if (!s->tier_on) return 0;
+    if (s->tier_fresh()) return 1;
+    RH_HIP(hipSetDevice(s->device));
+    const int rc = s->tier_refresh();
+    return rc ? rc : 1;
+}
 
 extern "C" {
 
@@ -1233,6 +1285,15 @@ int rh_store_len(const rh_store *s, uint64_t *out) {
 int rh_store_aggregates(rh_store *s, const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     if (r && (!lo || !hi || !out)) return fail(RH_ERR_ARG, "NULL buffer");
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        const int t = tier_ready(s);
+        if (t < 0) return t;
+        if (t) {
+            for (size_t j = 0; j < r; j++) s->tier.agg(lo[j], hi[j], out + j);
+            return RH_OK;
+        }
+    }
     RH_LOCK(s);
     return s->query(lo, hi, r, out);
 }
@@ -1244,6 +1305,16 @@ int rh_store_aggregate(rh_store *s, uint64_t lo, uint64_t hi, rh_aggregate *out)
 int rh_store_ranks(rh_store *s, const void *keys, size_t m, uint64_t *out) {
     if (!s || (m && (!keys || !out))) return fail(RH_ERR_ARG, "NULL");
     if (m == 0) return RH_OK;
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        const int t = tier_ready(s);
+        if (t < 0) return t;
+        if (t) {
+            const uint8_t *k = static_cast<const uint8_t *>(keys);
+            for (size_t j = 0; j < m; j++) out[j] = s->tier.rank(k + j * s->kl);
+            return RH_OK;
+        }
+    }
     RH_LOCK(s);
     return s->ranks(keys, m, out);
 }
@@ -1252,11 +1323,17 @@ int rh_store_rank(rh_store *s, const void *key, uint64_t *out) { return rh_store
 
 int rh_store_keys(rh_store *s, uint64_t lo, uint64_t hi, void *host_out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
-    RH_LOCK(s);
+    std::lock_guard<std::mutex> guard_(s->mu);
     int rc;
     if (lo > hi || hi > s->size()) return fail(RH_ERR_ARG, "bad rank range");
     if (hi == lo) return RH_OK;
     if (!host_out) return fail(RH_ERR_ARG, "host_out NULL");
+    if ((rc = tier_ready(s)) < 0) return rc;
+    if (rc) {
+        memcpy(host_out, s->tier.keys + lo * s->kl, (hi - lo) * s->kl);
+        return RH_OK;
+    }
+    RH_HIP(hipSetDevice(s->device));
     if ((rc = s->compact())) return rc;
     RH_HIP(hipMemcpyAsync(host_out, s->bkeys[s->cb].p + lo * s->kl, (hi - lo) * s->kl, hipMemcpyDeviceToHost,
                           s->stream));
@@ -1274,6 +1351,17 @@ int rh_store_aggregate_keys(rh_store *s, int lo_kind, const void *lo_key, int hi
     if (!s || !out) return fail(RH_ERR_ARG, "NULL");
     if (lo_kind < 0 || lo_kind > 2 || hi_kind < 0 || hi_kind > 2) return fail(RH_ERR_ARG, "bad bound kind");
     if ((lo_kind && !lo_key) || (hi_kind && !hi_key)) return fail(RH_ERR_ARG, "bound key is NULL");
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        const int t = tier_ready(s);
+        if (t < 0) return t;
+        if (t) {
+            const uint64_t lo = s->tier.bound_rank(lo_kind, static_cast<const uint8_t *>(lo_key), true);
+            const uint64_t hi = s->tier.bound_rank(hi_kind, static_cast<const uint8_t *>(hi_key), false);
+            s->tier.agg(lo, std::max(lo, hi), out);  // inverted -> ZERO
+            return RH_OK;
+        }
+    }
     RH_LOCK(s);
     return s->aggregate_keys(lo_kind, lo_key, hi_kind, hi_key, out);
 }
@@ -1289,6 +1377,20 @@ int rh_store_resolve_segments(rh_store *s, size_t r, const uint8_t *start_kinds,
             return fail(RH_ERR_ARG, "segment bound kind must be 0 (Unbounded) or 1 (Included / Excluded)");
         if ((start_kinds[j] && !start_keys) || (end_kinds[j] && !end_keys)) return fail(RH_ERR_ARG, "bound key is NULL");
     }
+    if (s->tier_on && r <= s->tier_round_max) {
+        std::lock_guard<std::mutex> g(s->mu);
+        const int t = tier_ready(s);
+        if (t < 0) return t;
+        if (t) {
+            const uint8_t *sk = static_cast<const uint8_t *>(start_keys), *ek = static_cast<const uint8_t *>(end_keys);
+            for (size_t j = 0; j < r; j++) {
+                raw_start[j] = start_kinds[j] ? s->tier.rank(sk + j * s->kl) : 0;
+                raw_end[j] = end_kinds[j] ? s->tier.rank(ek + j * s->kl) : s->tier.n;
+                s->tier.agg(raw_start[j], std::max(raw_start[j], raw_end[j]), local + j);  // inverted -> ZERO
+            }
+            return RH_OK;
+        }
+    }
     RH_LOCK(s);
     try {
         return s->resolve(r, start_kinds, static_cast<const uint8_t *>(start_keys), end_kinds,
@@ -1303,6 +1405,19 @@ int rh_store_split_segments(rh_store *s, size_t m, const uint64_t *select_ranks,
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     if ((m && (!select_ranks || !keys_out)) || (q && (!lo || !hi || !out))) return fail(RH_ERR_ARG, "NULL buffer");
     if (m == 0 && q == 0) return RH_OK;
+    if (s->tier_on && m + q <= 16 * s->tier_round_max) {
+        std::lock_guard<std::mutex> g(s->mu);
+        const int t = tier_ready(s);
+        if (t < 0) return t;
+        if (t) {
+            for (size_t i = 0; i < m; i++)
+                if (select_ranks[i] >= s->tier.n) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+            for (size_t i = 0; i < m; i++)
+                memcpy(static_cast<uint8_t *>(keys_out) + i * s->kl, s->tier.keys + select_ranks[i] * s->kl, s->kl);
+            for (size_t i = 0; i < q; i++) s->tier.agg(lo[i], hi[i], out + i);
+            return RH_OK;
+        }
+    }
     RH_LOCK(s);
     try {  // no exception crosses the C ABI
         return s->split(m, select_ranks, static_cast<uint8_t *>(keys_out), q, lo, hi, out);
@@ -1326,6 +1441,32 @@ int rh_store_protocol_round(rh_store *s, int policy, uint64_t fan_out, const rh_
     }
     *children = rh_segments{};
     *enumerations = rh_segments{};
+    if (outcome) *outcome = rh_round_outcome{};
+    if (r == 0) return RH_OK;
+    if (s->tier_on && r <= s->tier_round_max) {  // small rounds on the host tier
+        std::lock_guard<std::mutex> g(s->mu);
+        try {
+            const int t = tier_ready(s);
+            if (t < 0) return t;
+            if (t) {
+                uint64_t h[5];
+                s->tier.round(policy == RH_POLICY_SQRT_FAN_OUT, fan_out < 2 ? 2 : fan_out, *active, s->tier_out, h);
+                const uint64_t nc = h[3], ne = h[1];
+                const rh::RoundLayout L = rh::round_layout(nc, ne, s->kl);
+                uint8_t *o = s->tier_out.data();
+                if (outcome) *outcome = rh_round_outcome{h[0], h[1], h[2], h[3], h[4]};
+                *children = rh_segments{o + L.csk, o + L.cskeys, o + L.cek, o + L.cekeys,
+                                        reinterpret_cast<rh_aggregate *>(o + L.caggs), (size_t)nc, (size_t)nc};
+                *enumerations = rh_segments{o + L.esk, o + L.eskeys, o + L.eek, o + L.eekeys, nullptr, (size_t)ne,
+                                            (size_t)ne};
+                return RH_OK;
+            }
+        } catch (const std::bad_alloc &) {
+            *children = rh_segments{};
+            *enumerations = rh_segments{};
+            return fail(RH_ERR_OOM, "protocol round: host allocation failed");
+        }
+    }
     RH_LOCK(s);
     try {  // no exception crosses the C ABI
         return s->protocol_round(policy, fan_out, *active, children, enumerations, outcome);
@@ -1367,6 +1508,23 @@ int rh_store_reserve(rh_store *s, uint64_t rows, uint64_t batch_rows) {
     if (rows >= (1ull << 31) || batch_rows >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows)");
     RH_LOCK(s);
     return s->reserve(rows, batch_rows);
+}
+
+int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
+    if (!s || enable < 0 || enable > 1) return fail(RH_ERR_ARG, "bad host tier setting");
+    std::lock_guard<std::mutex> g(s->mu);
+    s->tier_on = enable == 1;
+    s->tier_round_max = round_max ? round_max : 128;
+    if (!s->tier_on) {  // give the host memory back
+        s->tier_version = ~0ull;
+        s->tier = rh::HostTier{};
+        s->tier_keys.release();
+        s->tier_prefix.release();
+        s->tier_out = std::vector<uint8_t>();
+        (void)hipSetDevice(s->device);
+        s->tier_dpre.release(), s->tier_spre.release(), s->tier_bpre.release();
+    }
+    return RH_OK;
 }
 
 int rh_store_set_compaction(rh_store *s, uint64_t divisor, uint64_t min_rows) {

@@ -56,13 +56,19 @@ class KeyRange:
         return KeyRange()
 
 
+# stores created with host_tier=None follow this (tests run the same suites with the tier on)
+DEFAULT_HOST_TIER = False
+
+
 class GpuFingerprintStore:
-    def __init__(self, schema: RecordSchema, device: int = 0):
+    def __init__(self, schema: RecordSchema, device: int = 0, host_tier: Optional[bool] = None):
         self.schema = schema
         self._s = schema.c()
         h = C.c_void_p()
         A.check(A.lib().rh_store_create(device, C.byref(self._s), C.byref(h)), "rh_store_create")
         self._h = h
+        if DEFAULT_HOST_TIER if host_tier is None else host_tier:
+            self.set_host_tier(True)
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -129,6 +135,12 @@ class GpuFingerprintStore:
 
     def compact(self) -> None:
         A.check(A.lib().rh_store_compact(self._h), "rh_store_compact")
+
+    def set_host_tier(self, enable: bool = True, round_max: int = 0) -> None:
+        """Answer rank / select / aggregate and protocol rounds of at most `round_max` segments
+        (0: the default, 128) from a host copy of the keys and fingerprint prefix sums, refreshed
+        from the device after every change (rh_store_set_host_tier)."""
+        A.check(A.lib().rh_store_set_host_tier(self._h, 1 if enable else 0, round_max), "rh_store_set_host_tier")
 
     def set_compaction(self, divisor: int, min_rows: int) -> None:
         A.check(A.lib().rh_store_set_compaction(self._h, divisor, min_rows), "rh_store_set_compaction")

@@ -151,6 +151,7 @@ extern "C" {
                                  n_new: *mut u64, n_over: *mut u64, n_del: *mut u64,
                                  after_stream: *mut c_void) -> c_int;
     pub fn rh_store_compact(store: *mut rh_store) -> c_int;
+    pub fn rh_store_set_host_tier(store: *mut rh_store, enable: c_int, round_max: u64) -> c_int;
     pub fn rh_store_set_compaction(store: *mut rh_store, divisor: u64, min_rows: u64) -> c_int;
     pub fn rh_store_reserve(store: *mut rh_store, rows: u64, batch_rows: u64) -> c_int;
     pub fn rh_store_stats(store: *const rh_store, base_rows: *mut u64, delta_rows: *mut u64,

@@ -805,3 +805,54 @@ def test_store_load_refuses_2_pow_31_rows(gpu):
     assert A.lib().rh_store_load(st._h, C.byref(hcols), (1 << 31) + 5) == A.ERR_ARG
     assert st.aggregate() == root and st.size() == 1000
     st.close()
+
+
+def test_host_tier_equals_device_answers(gpu, oracle_lib):
+    """The host tier (rh_store_set_host_tier) against the device path on the same store, before
+    and after batches (the tier refreshes on the first question after a change): ranks of
+    present and absent keys, select, key-range aggregates with every bound kind (inverted ones
+    give ZERO), rank-range aggregates, and the root against the oracle FTM's."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    from rsos_hip.synth import make_records, to_host
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 300_000
+    base = make_records(s, n, seed=21)
+    dev, tier = GpuFingerprintStore(s, host_tier=False), GpuFingerprintStore(s, host_tier=True)
+    for st in (dev, tier):
+        st.load_bulk_device(base)
+    rng = np.random.default_rng(5)
+    keys_h = to_host(base)["keys"]
+
+    def probe():
+        assert tier.size() == dev.size() and tier.aggregate() == dev.aggregate()
+        ks = [keys_h[i].tobytes() for i in rng.integers(0, n, 200)] + [rng.bytes(16) for _ in range(200)]
+        ks += [b"\x00" * 16, b"\xff" * 16]
+        karr = np.frombuffer(b"".join(ks), np.uint8).reshape(-1, 16)
+        assert np.array_equal(tier.ranks(karr), dev.ranks(karr))
+        assert [tier.rank(k) for k in ks[:20]] == [int(x) for x in dev.ranks(karr[:20])]
+        for r in [0, 1, tier.size() - 1] + list(rng.integers(0, tier.size(), 50)):
+            assert tier.select(int(r)) == dev.select(int(r))
+        for _ in range(100):
+            a, b = ks[rng.integers(len(ks))], ks[rng.integers(len(ks))]
+            sk, ek = ["included", "excluded"][rng.integers(2)], ["included", "excluded"][rng.integers(2)]
+            rg = KeyRange(a if rng.random() > 0.1 else None, b if rng.random() > 0.1 else None, sk, ek)
+            assert tier.aggregate(rg) == dev.aggregate(rg)
+        lo = rng.integers(0, tier.size(), 64)
+        hi = lo + rng.integers(0, 70_000, 64)
+        assert tier.aggregates_ranks(list(lo), list(hi)) == dev.aggregates_ranks(list(lo), list(hi))
+
+    probe()
+    for k in range(3):  # inserts, then overwrites + deletes of existing keys
+        b = make_records(s, 20_000, seed=300 + k, random_keys=True)
+        ops = None
+        if k == 2:
+            b = {c: t[1000:21000].clone() for c, t in base.items()}
+            b["values"][:10_000] ^= 0x33
+            ops = torch.zeros(20_000, dtype=torch.uint8, device="cuda")
+            ops[10_000:] = 1
+        assert tier.apply_device(b, ops) == dev.apply_device(b, ops)
+        probe()
+    dev.close()
+    tier.close()

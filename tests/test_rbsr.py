@@ -13,6 +13,17 @@ import oracle as O
 import rbsr as OR  # oracle/rbsr.py
 
 
+@pytest.fixture(autouse=True, params=["device", "host_tier"])
+def store_tier(request):
+    """Every GPU store of this module answers from the device, then from the host tier
+    (rh_store_set_host_tier): the answers must be identical."""
+    import rsos_hip.store as S
+    old = S.DEFAULT_HOST_TIER
+    S.DEFAULT_HOST_TIER = request.param == "host_tier"
+    yield request.param
+    S.DEFAULT_HOST_TIER = old
+
+
 # ---- helpers ---------------------------------------------------------------------------------
 
 def _u32_recs(pairs):

@@ -194,7 +194,7 @@ int rh_store_load(rh_store *store, const rh_columns *host_cols, size_t n);
 /* dev_cols were written on `after_stream` (a hipStream_t; NULL = the null stream): the store's
  * own stream waits for the work already queued there before reading them.                 */
 int rh_store_load_device(rh_store *store, const rh_columns *dev_cols, size_t n, void *after_stream);
-int rh_store_len(const rh_store *store, uint64_t *out);
+int rh_store_len(rh_store *store, uint64_t *out);
 /* Aggregate over rank range [lo, hi) */
 int rh_store_aggregate(rh_store *store, uint64_t lo, uint64_t hi, rh_aggregate *out);
 /* r rank ranges in one launch (the <= 16 child ranges of one rbsr SPLIT, protocol.rs:299-307) */
@@ -270,6 +270,17 @@ int rh_store_protocol_round(rh_store *store, int policy, uint64_t fan_out, const
  * enable = 0 frees the copy.  Answers are identical either way.                              */
 int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
 
+/* Staged single-record updates: Rsos::insert / delete one record at a time (mutate.rs:23-154)
+ * without one device round trip each.  rh_store_stage appends m host rows (columns as for
+ * rh_store_apply; ops[i] 0 = insert-or-overwrite, 1 = delete) to the store's pending batch and
+ * returns; the next call that reads the store (len, aggregate*, rank*, select, keys, rounds,
+ * stats, compact, apply, ...) first applies the pending rows as ONE batch, so every answer sees
+ * every staged record (one-snapshot-per-round, rbsr/src/rsos_view.rs:36).  A key staged more
+ * than once keeps its last operation, exactly as applying them in order would.  A load or
+ * snapshot reload drops the pending rows (it replaces the contents).  A staged batch the store
+ * rejects is dropped and its error returned by the call that flushed it.                      */
+int rh_store_stage(rh_store *store, const rh_columns *host_cols, const uint8_t *ops, size_t m);
+
 /* Batched insert / overwrite / delete (FingerprintTreeMap::insert / remove, mutate.rs:23-154).
  * ops[i]: 0 = insert-or-overwrite record i, 1 = delete key i (its value columns are ignored).
  * Keys within one batch must be distinct (RH_ERR_ARG, store unchanged).  On return every
@@ -294,7 +305,7 @@ int rh_store_set_compaction(rh_store *store, uint64_t divisor, uint64_t min_rows
  * reallocation frees the old buffer, and hipFree waits for the whole device).  Compacts first;
  * contents and every answer are unchanged.  Optional: buffers otherwise grow on demand.    */
 int rh_store_reserve(rh_store *store, uint64_t rows, uint64_t batch_rows);
-int rh_store_stats(const rh_store *store, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions);
+int rh_store_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions);
 
 /* ---- snapshot reload ------------------------------------------------------------------
  * FileSnapshot (src/snapshot.rs:30-58): "RCNL", u32 LE format version 1, then bincode 1.3.3

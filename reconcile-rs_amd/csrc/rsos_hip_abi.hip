@@ -585,6 +585,89 @@ struct rh_store {
         memset(root_d, 0, sizeof root_d);
         version++;
     }
+    // ---- the pending batch (rh_store_stage) --------------------------------------------------------
+    // Single-record inserts and deletes (Rsos::insert / delete, FingerprintTreeMap::insert /
+    // remove, mutate.rs:23-154) queue here on the host and reach the device as one batch
+    // (rh_store_apply's path) before anything reads the store: the one-device-batch-per-round
+    // shape of just_insert_bulk (src/replica/write.rs:107-121), never one device round trip per
+    // record.  A key staged twice keeps its last operation -- the result of applying them in order.
+    struct Pending {
+        std::vector<uint8_t> keys, vals, tags, ops;
+        std::vector<uint64_t> phys, node;
+        std::vector<uint32_t> logical;
+        size_t n = 0;
+        void clear() {
+            keys.clear(), vals.clear(), tags.clear(), ops.clear(), phys.clear(), node.clear(), logical.clear();
+            n = 0;
+        }
+    } pend;
+    int stage(const rh_columns &h, const uint8_t *ops, size_t m) {
+        const size_t kr = kl, vr = value_row(schema);
+        const bool dated = schema.record_kind == RH_REC_DATED;
+        auto app = [](auto &v, const auto *src, size_t cnt) {
+            if (src) v.insert(v.end(), src, src + cnt);
+            else v.resize(v.size() + cnt);
+        };
+        app(pend.keys, static_cast<const uint8_t *>(h.keys), m * kr);
+        app(pend.vals, static_cast<const uint8_t *>(h.values), m * vr);
+        app(pend.tags, h.tags, m);
+        app(pend.ops, ops, m);
+        if (dated) {
+            app(pend.phys, h.phys, m);
+            app(pend.node, h.node, m);
+            app(pend.logical, h.logical, m);
+        }
+        pend.n += m;
+        return RH_OK;
+    }
+    int key_cmp(const uint8_t *a, const uint8_t *b) const {
+        if (schema.key_kind == RH_KEY_U32 || schema.key_kind == RH_KEY_U64) {
+            uint64_t x = 0, y = 0;
+            memcpy(&x, a, kl);
+            memcpy(&y, b, kl);
+            return (x > y) - (x < y);
+        }
+        return memcmp(a, b, kl);
+    }
+    // one batch: the staged rows in key order, the last operation of each key kept
+    int flush() {
+        if (!pend.n) return RH_OK;
+        const size_t m = pend.n, kr = kl, vr = value_row(schema);
+        const bool dated = schema.record_kind == RH_REC_DATED;
+        std::vector<uint32_t> idx(m);
+        for (size_t i = 0; i < m; i++) idx[i] = (uint32_t)i;
+        const uint8_t *K = pend.keys.data();
+        std::stable_sort(idx.begin(), idx.end(),
+                         [&](uint32_t a, uint32_t b) { return key_cmp(K + (size_t)a * kr, K + (size_t)b * kr) < 0; });
+        Pending b;
+        size_t out = 0;
+        for (size_t i = 0; i < m; i++) {
+            if (i + 1 < m && key_cmp(K + (size_t)idx[i] * kr, K + (size_t)idx[i + 1] * kr) == 0) continue;
+            const size_t r = idx[i];
+            b.keys.insert(b.keys.end(), K + r * kr, K + r * kr + kr);
+            b.vals.insert(b.vals.end(), pend.vals.data() + r * vr, pend.vals.data() + r * vr + vr);
+            b.tags.push_back(pend.tags[r]);
+            b.ops.push_back(pend.ops[r]);
+            if (dated) {
+                b.phys.push_back(pend.phys[r]);
+                b.node.push_back(pend.node[r]);
+                b.logical.push_back(pend.logical[r]);
+            }
+            out++;
+        }
+        pend.clear();
+        const rh_columns h{b.keys.data(), dated ? b.phys.data() : nullptr, dated ? b.logical.data() : nullptr,
+                           dated ? b.node.data() : nullptr, schema.record_kind == RH_REC_PLAIN ? nullptr : b.tags.data(),
+                           b.vals.data()};
+        uint64_t c[3];
+        return apply_host(h, b.ops.data(), out, c);
+    }
+    int apply_host(const rh_columns &h, const uint8_t *ops, size_t m, uint64_t c[3]) {
+        int rc;
+        if ((rc = staging.upload(schema, h, m, stream)) || (rc = hops.ensure(m + 64))) return rc;
+        if (m) RH_HIP(hipMemcpyAsync(hops.p, ops, m, hipMemcpyHostToDevice, stream));
+        return apply_device(staging.view(schema), hops.p, m, c);
+    }
     // ---- the host tier (host_tier.hpp) ---------------------------------------------------------
     uint64_t version = 0;       // bumped by every change of contents (load, batch, failed load)
     bool tier_on = false;
@@ -1208,13 +1291,29 @@ struct rh_store {
     }
 };
 
-#define RH_LOCK(s)                                  \
+// Every call that reads or replaces the store first takes its lock; readers then flush the pending
+// batch (rh_store_stage) so that they see every staged record
+#define RH_LOCK_NOFLUSH(s)                          \
     std::lock_guard<std::mutex> guard_((s)->mu);    \
     RH_HIP(hipSetDevice((s)->device))
+#define RH_LOCK(s)                                  \
+    RH_LOCK_NOFLUSH(s);                             \
+    do {                                            \
+        const int frc_ = (s)->flush();              \
+        if (frc_) return frc_;                      \
+    } while (0)
+
+static int flush_locked(rh_store *s) {
+    if (!s->pend.n) return RH_OK;
+    RH_HIP(hipSetDevice(s->device));
+    return s->flush();
+}
 
 // Under the store's lock: 1 if the host tier answers (refreshing it first if the store changed
 // since; only then is the device touched), 0 if the tier is off, < 0 on error
 static int tier_ready(rh_store *s) {
+    const int frc = flush_locked(s);
+    if (frc) return frc;
     if (!s->tier_on) return 0;
     if (s->tier_fresh()) return 1;
     RH_HIP(hipSetDevice(s->device));
@@ -1260,7 +1359,8 @@ int rh_store_destroy(rh_store *s) {
 int rh_store_load(rh_store *s, const rh_columns *h, size_t n) {
     if (!s || !h) return fail(RH_ERR_ARG, "NULL");
     if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
-    RH_LOCK(s);
+    RH_LOCK_NOFLUSH(s);
+    s->pend.clear();  // a load replaces the contents: staged rows before it are superseded
     int rc;
     if ((rc = s->staging.upload(s->schema, *h, n, s->stream))) return rc;
     return s->load_device(s->staging.view(s->schema), n);
@@ -1271,13 +1371,17 @@ int rh_store_load_device(rh_store *s, const rh_columns *dev_cols, size_t n, void
     if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
     int rc = check_cols(s->schema, dev_cols, n);
     if (rc) return rc;
-    RH_LOCK(s);
+    RH_LOCK_NOFLUSH(s);
+    s->pend.clear();
     if ((rc = s->after(after_stream))) return rc;
     return s->load_device(*dev_cols, n);
 }
 
-int rh_store_len(const rh_store *s, uint64_t *out) {
+int rh_store_len(rh_store *s, uint64_t *out) {
     if (!s || !out) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const int rc = flush_locked(s);
+    if (rc) return rc;
     *out = s->size();
     return RH_OK;
 }
@@ -1342,8 +1446,10 @@ int rh_store_keys(rh_store *s, uint64_t lo, uint64_t hi, void *host_out) {
 
 int rh_store_select(rh_store *s, uint64_t r, void *key_out) {
     if (!s || !key_out) return fail(RH_ERR_ARG, "NULL");
-    if (r >= s->size()) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
-    return rh_store_keys(s, r, r + 1, key_out);
+    if (r == UINT64_MAX) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+    const int rc = rh_store_keys(s, r, r + 1, key_out);
+    if (rc == RH_ERR_ARG) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+    return rc;
 }
 
 int rh_store_aggregate_keys(rh_store *s, int lo_kind, const void *lo_key, int hi_kind, const void *hi_key,
@@ -1495,8 +1601,11 @@ int rh_store_compact(rh_store *s) {
     return s->compact();
 }
 
-int rh_store_stats(const rh_store *s, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions) {
+int rh_store_stats(rh_store *s, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const int rc = flush_locked(s);
+    if (rc) return rc;
     if (base_rows) *base_rows = s->nb;
     if (delta_rows) *delta_rows = s->nd;
     if (compactions) *compactions = s->compactions;
@@ -1508,6 +1617,22 @@ int rh_store_reserve(rh_store *s, uint64_t rows, uint64_t batch_rows) {
     if (rows >= (1ull << 31) || batch_rows >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows)");
     RH_LOCK(s);
     return s->reserve(rows, batch_rows);
+}
+
+int rh_store_stage(rh_store *s, const rh_columns *h, const uint8_t *ops, size_t m) {
+    if (!s || !h || (m && !ops)) return fail(RH_ERR_ARG, "NULL");
+    if (m == 0) return RH_OK;
+    const rh_schema &sc = s->schema;
+    if (sc.key_kind != RH_KEY_UNIT && !h->keys) return fail(RH_ERR_ARG, "keys column is NULL");
+    for (size_t i = 0; i < m; i++)
+        if (ops[i] > 1) return fail(RH_ERR_ARG, "op must be 0 (insert) or 1 (delete)");
+    std::lock_guard<std::mutex> g(s->mu);
+    if (s->pend.n + m >= (1ull << 31)) return fail(RH_ERR_ARG, "pending batch limit (2^31 rows) exceeded");
+    try {
+        return s->stage(*h, ops, m);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "stage: host allocation failed");
+    }
 }
 
 int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
@@ -1539,10 +1664,8 @@ int rh_store_apply(rh_store *s, const rh_columns *h, const uint8_t *ops, size_t 
     if (!s || !h || (m && !ops)) return fail(RH_ERR_ARG, "NULL");
     RH_LOCK(s);
     int rc;
-    if ((rc = s->staging.upload(s->schema, *h, m, s->stream)) || (rc = s->hops.ensure(m + 64))) return rc;
-    if (m) RH_HIP(hipMemcpyAsync(s->hops.p, ops, m, hipMemcpyHostToDevice, s->stream));
     uint64_t c[3];
-    if ((rc = s->apply_device(s->staging.view(s->schema), s->hops.p, m, c))) return rc;
+    if ((rc = s->apply_host(*h, ops, m, c))) return rc;
     if (n_new) *n_new = c[0];
     if (n_over) *n_over = c[1];
     if (n_del) *n_del = c[2];
@@ -1718,6 +1841,8 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
         la.lock();
     }
     RH_HIP(hipSetDevice(a->device));
+    for (rh_store *x : {dated, proj})  // a reload replaces the contents: staged rows are superseded
+        if (x) x->pend.clear();
     int rc;
     uint8_t h[16] = {0};
     const size_t hl = std::min<size_t>(len, 16);

@@ -9,6 +9,8 @@ behaviour), so callers and tests read like the reference's own:
   GpuFingerprintStore  rsos::Rsos<K> realisation rsos/src/rsos_trait.rs:39-129
                        (size / aggregate / rank / select / enumerate / insert / delete),
                        which rbsr consumes as RsosView<K> (rbsr/src/rsos_view.rs:55-91)
+  FingerprintMap       the same with the host owning K and V and single-record updates staged
+                       into one device batch (the Rust binding's HipFingerprintMap)
 
 All hashing runs in the HIP kernels of librsos_hip.so; nothing here computes a
 fingerprint on the CPU.  torch is used only for device memory and streams.
@@ -20,10 +22,11 @@ from .schema import RecordSchema
 from .device import (lift_records, lift_dual, lift_encoded, lift_fixed, reduce_blocks, range_aggregates,
                      combine_aggregates, block_sums_for)
 from .store import GpuFingerprintStore
+from .fmap import Entry, FingerprintMap
 from ._abi import RsosHipError, lib
 
 __all__ = [
     "Aggregate", "Fingerprint", "RecordSchema", "lift_records", "lift_dual", "lift_encoded", "lift_fixed",
     "reduce_blocks", "range_aggregates", "combine_aggregates", "block_sums_for",
-    "GpuFingerprintStore", "RsosHipError", "lib",
+    "GpuFingerprintStore", "FingerprintMap", "Entry", "RsosHipError", "lib",
 ]

@@ -127,7 +127,7 @@ extern "C" {
     pub fn rh_store_load(store: *mut rh_store, cols: *const rh_columns, n: usize) -> c_int;
     pub fn rh_store_load_device(store: *mut rh_store, dev_cols: *const rh_columns, n: usize,
                                 after_stream: *mut c_void) -> c_int;
-    pub fn rh_store_len(store: *const rh_store, out: *mut u64) -> c_int;
+    pub fn rh_store_len(store: *mut rh_store, out: *mut u64) -> c_int;
     pub fn rh_store_aggregate(store: *mut rh_store, lo: u64, hi: u64, out: *mut rh_aggregate) -> c_int;
     pub fn rh_store_aggregates(store: *mut rh_store, lo: *const u64, hi: *const u64, r: usize, out: *mut rh_aggregate) -> c_int;
     pub fn rh_store_aggregate_keys(store: *mut rh_store, lo_kind: c_int, lo_key: *const c_void, hi_kind: c_int,
@@ -151,10 +151,11 @@ extern "C" {
                                  n_new: *mut u64, n_over: *mut u64, n_del: *mut u64,
                                  after_stream: *mut c_void) -> c_int;
     pub fn rh_store_compact(store: *mut rh_store) -> c_int;
+    pub fn rh_store_stage(store: *mut rh_store, cols: *const rh_columns, ops: *const u8, n: usize) -> c_int;
     pub fn rh_store_set_host_tier(store: *mut rh_store, enable: c_int, round_max: u64) -> c_int;
     pub fn rh_store_set_compaction(store: *mut rh_store, divisor: u64, min_rows: u64) -> c_int;
     pub fn rh_store_reserve(store: *mut rh_store, rows: u64, batch_rows: u64) -> c_int;
-    pub fn rh_store_stats(store: *const rh_store, base_rows: *mut u64, delta_rows: *mut u64,
+    pub fn rh_store_stats(store: *mut rh_store, base_rows: *mut u64, delta_rows: *mut u64,
                           compactions: *mut u64) -> c_int;
     pub fn rh_snapshot_header(bytes: *const c_void, len: usize, entries: *mut u64) -> c_int;
     pub fn rh_snapshot_decode_device(schema: *const rh_schema, key_form: c_int, dev_bytes: *const c_void, len: usize,

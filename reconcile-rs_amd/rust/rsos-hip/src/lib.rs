@@ -7,8 +7,13 @@
 //! `public-api/rbsr.txt` is unchanged.
 //!
 //! Ownership follows the reference: the map owns `K` and `V` in host memory (select /
-//! enumerate return borrows into it); the device holds the keys, the per-element
-//! fingerprints and the block / super-block sums.  Laws:
+//! enumerate return borrows into it) in a sorted-blocks index (`sorted.rs`: O(log n) rank /
+//! select, O(log n + B) insert); the device holds the keys, the per-element fingerprints and the
+//! block / super-block sums, and the library's host tier (rh_store_set_host_tier) answers
+//! `aggregate` without a device round trip.  `insert` / `delete` stage one row in the library
+//! (rh_store_stage); everything staged reaches the device as ONE batch before the next
+//! `aggregate`, so a bulk seed through single inserts (just_insert_bulk,
+//! src/replica/write.rs:107-121) costs host work per record and one device batch.  Laws:
 //! * **summary-folds-lift** -- every fingerprint is computed by the GPU lift, which is
 //!   bit-exact with `rsos::lift` (pinned by the reference's golden vectors in the
 //!   MI355X repository's tests);
@@ -20,8 +25,8 @@
 //! this crate panics with the library's message.
 
 mod ffi;
+mod sorted;
 
-use std::cmp::Ordering;
 use std::ffi::CStr;
 use std::ops::{Bound, RangeBounds};
 use std::os::raw::c_void;
@@ -90,8 +95,8 @@ pub trait GpuRecord: Serialize {
 /// `Rsos<K>` on an MI355X.
 pub struct HipFingerprintMap<K: GpuKey, V: GpuRecord> {
     store: *mut ffi::rh_store,
-    /// rank-ordered host mirror (owns K and V; select / enumerate borrow from it)
-    entries: Vec<(K, V)>,
+    /// rank-ordered host index (owns K and V; select / enumerate borrow from it)
+    entries: sorted::SortedBlocks<K, V>,
 }
 
 // SAFETY: the C store serialises all calls with an internal mutex; the host mirror follows
@@ -169,7 +174,9 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         let mut store = std::ptr::null_mut();
         // SAFETY: valid schema pointer and out-pointer.
         check(unsafe { ffi::rh_store_create(device, &s, &mut store) }, "rh_store_create");
-        HipFingerprintMap { store, entries: Vec::new() }
+        // SAFETY: store was just created.
+        check(unsafe { ffi::rh_store_set_host_tier(store, 1, 0) }, "rh_store_set_host_tier");
+        HipFingerprintMap { store, entries: sorted::SortedBlocks::new() }
     }
 
     /// Bulk fill (FromIterator / ReplicatedMap::load_bulk): sort, de-duplicate keeping the
@@ -182,20 +189,14 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         let cols = batch.columns();
         // SAFETY: the column buffers outlive the synchronous call.
         check(unsafe { ffi::rh_store_load(self.store, &cols, items.len()) }, "rh_store_load");
-        self.entries = items;
+        self.entries = sorted::SortedBlocks::from_sorted(items);
     }
 
     fn bound_rank(&self, b: Bound<&K>, lower: bool) -> usize {
         match b {
             Bound::Unbounded => if lower { 0 } else { self.entries.len() },
-            Bound::Included(k) => {
-                if lower { self.entries.partition_point(|(e, _)| e < k) }
-                else { self.entries.partition_point(|(e, _)| e <= k) }
-            }
-            Bound::Excluded(k) => {
-                if lower { self.entries.partition_point(|(e, _)| e <= k) }
-                else { self.entries.partition_point(|(e, _)| e < k) }
-            }
+            Bound::Included(k) => if lower { self.entries.rank(k) } else { self.entries.rank_incl(k) },
+            Bound::Excluded(k) => if lower { self.entries.rank_incl(k) } else { self.entries.rank(k) },
         }
     }
 
@@ -210,15 +211,24 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         out.into_iter().map(|a| Aggregate::new(a.size as usize, Fingerprint(a.fingerprint))).collect()
     }
 
-    fn apply(&mut self, key: &K, value: Option<&V>) -> (u64, u64, u64) {
+    /// Stage one insert-or-overwrite (`value` Some) or delete in the library's pending batch; the
+    /// library applies everything staged as one device batch before the next question.
+    fn stage(&mut self, key: &K, value: Option<&V>) {
         let batch = Batch::new(std::iter::once((key, value)));
         let cols = batch.columns();
         let op = [if value.is_some() { 0u8 } else { 1u8 }];
-        let (mut a, mut b, mut d) = (0u64, 0u64, 0u64);
-        // SAFETY: buffers outlive the synchronous call.
-        check(unsafe { ffi::rh_store_apply(self.store, &cols, op.as_ptr(), 1, &mut a, &mut b, &mut d) },
-              "rh_store_apply");
-        (a, b, d)
+        // SAFETY: the library copies the row before returning.
+        check(unsafe { ffi::rh_store_stage(self.store, &cols, op.as_ptr(), 1) }, "rh_store_stage");
+    }
+
+    fn key_bound(b: Bound<&K>, lower: bool) -> (i32, Vec<u8>) {
+        // rh_store_aggregate_keys bound kinds: 0 = unbounded, 1 = included, 2 = excluded
+        let _ = lower;
+        match b {
+            Bound::Unbounded => (0, Vec::new()),
+            Bound::Included(k) => (1, k.column_bytes()),
+            Bound::Excluded(k) => (2, k.column_bytes()),
+        }
     }
 }
 
@@ -342,7 +352,7 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
                     }
                     let mut cur = start;
                     for (i, &c) in cuts.iter().enumerate() {
-                        let key = self.entries[c].0.clone(); // select(c)
+                        let key = self.entries.at(c).0.clone(); // select(c)
                         child_ranges.push(rbsr::RangeAggregate::new(cur, Some(key.clone()), child_aggs[first + i]));
                         cur = Some(key);
                     }
@@ -368,18 +378,25 @@ impl<K: GpuKey, V: GpuRecord> Rsos<K> for HipFingerprintMap<K, V> {
         self.entries.len()
     }
 
+    /// One ABI call: the library applies any staged rows, then its host tier answers from the
+    /// fingerprint prefix sums (an inverted range gives ZERO, rbsr/src/protocol.rs:230-232).
     fn aggregate<R: RangeBounds<K>>(&self, range: R) -> Aggregate {
-        let lo = self.bound_rank(range.start_bound(), true);
-        let hi = self.bound_rank(range.end_bound(), false).max(lo); // inverted -> ZERO
-        self.aggregates_by_rank(&[(lo, hi)])[0]
+        let (lk, lb) = Self::key_bound(range.start_bound(), true);
+        let (hk, hb) = Self::key_bound(range.end_bound(), false);
+        let mut out = ffi::rh_aggregate::default();
+        let ptr = |b: &Vec<u8>| if b.is_empty() { std::ptr::null() } else { b.as_ptr() as *const c_void };
+        // SAFETY: bound keys are key_len bytes (or NULL when unbounded); out is one aggregate.
+        check(unsafe { ffi::rh_store_aggregate_keys(self.store, lk, ptr(&lb), hk, ptr(&hb), &mut out) },
+              "rh_store_aggregate_keys");
+        Aggregate::new(out.size as usize, Fingerprint(out.fingerprint))
     }
 
     fn rank(&self, z: &K) -> usize {
-        self.entries.partition_point(|(e, _)| e.cmp(z) == Ordering::Less)
+        self.entries.rank(z)
     }
 
     fn select(&self, r: usize) -> &K {
-        &self.entries[r].0 // panics if r >= size(), as the reference does
+        &self.entries.at(r).0 // panics if r >= size(), as the reference does
     }
 
     fn enumerate<'a, R: RangeBounds<K> + 'a>(&'a self, range: R) -> impl Iterator<Item = (&'a K, &'a V)> + 'a
@@ -389,27 +406,17 @@ impl<K: GpuKey, V: GpuRecord> Rsos<K> for HipFingerprintMap<K, V> {
     {
         let lo = self.bound_rank(range.start_bound(), true);
         let hi = self.bound_rank(range.end_bound(), false).max(lo);
-        self.entries[lo..hi].iter().map(|(k, v)| (k, v))
+        self.entries.range(lo, hi).map(|(k, v)| (k, v))
     }
 
     fn insert(&mut self, key: K, value: V) -> Option<V> {
-        self.apply(&key, Some(&value));
-        match self.entries.binary_search_by(|(e, _)| e.cmp(&key)) {
-            Ok(i) => Some(std::mem::replace(&mut self.entries[i].1, value)),
-            Err(i) => {
-                self.entries.insert(i, (key, value));
-                None
-            }
-        }
+        self.stage(&key, Some(&value)); // panics on a value of the wrong length (Batch::new)
+        self.entries.insert(key, value)
     }
 
     fn delete(&mut self, key: &K) -> Option<V> {
-        match self.entries.binary_search_by(|(e, _)| e.cmp(key)) {
-            Ok(i) => {
-                self.apply(key, None);
-                Some(self.entries.remove(i).1)
-            }
-            Err(_) => None,
-        }
+        let old = self.entries.remove(key)?;
+        self.stage(key, None);
+        Some(old)
     }
 }

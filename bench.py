@@ -654,7 +654,7 @@ def cpu_baseline_reconcile(schema, cols, rows, m):
     ta.fill(0, ra.n)
     tb.fill(0, rb.n)
     t0 = time.perf_counter()
-    rounds, segs, _ = O.reconcile_fixed(ta, tb, 16)
+    rounds, segs, _ = O.reconcile_fixed(ta, tb, 16)  # no hashing in a round: the SIMD level does not apply
     dt = time.perf_counter() - t0
     return {"value": round(segs / dt / 1e6, 4), "unit": "M segments/s", "cores": 1, "kind": "port",
             "reconciliation_ms": round(dt * 1e3, 3),
@@ -671,6 +671,7 @@ def cpu_baseline_reload(sd, sp, cols, m):
     from rsos_hip.synth import to_host
     h = to_host(cols, 0, m)
     dt = 0.0
+    level = O.set_simd(2)  # the blake3 crate's SIMD row form (oracle/blake3_simd.c)
     for s in (sd, sp):
         sc = O.Schema(s.key_kind, s.key_len, s.value_kind, s.value_len, s.record_kind, 0)
         dated = s.record_kind == O.REC_DATED
@@ -680,7 +681,9 @@ def cpu_baseline_reload(sd, sp, cols, m):
         t0 = time.perf_counter()
         t.fill(0, m)
         dt += time.perf_counter() - t0
+    O.set_simd(0)
     return {"value": round(m / dt / 1e6, 3), "unit": "M entries/s", "cores": 1, "kind": "port",
+            "simd": ["portable", "sse4.1", "avx512vl"][level],
             "sample": f"replay of the first {m} entries into two FingerprintTreeMaps (dated + projection; "
                       f"oracle/oracle.c restatement, serial, decode not timed), {dt:.2f} s"}
 
@@ -701,10 +704,13 @@ def cpu_baseline_incremental(schema, m, resident):
                      cols.get("tags"))
     t = O.FingerprintTreeMap(recs)
     t.fill(0, resident)
+    level = O.set_simd(2)  # the blake3 crate's SIMD row form (oracle/blake3_simd.c)
     t0 = time.perf_counter()
     t.fill(resident, resident + m)
     dt = time.perf_counter() - t0
+    O.set_simd(0)
     return {"value": round(m / dt / 1e6, 3), "unit": "M records/s", "cores": 1, "kind": "port",
+            "simd": ["portable", "sse4.1", "avx512vl"][level],
             "sample": f"{m} random-key inserts into a {resident}-record FingerprintTreeMap "
                       f"(oracle/oracle.c restatement, serial), {dt:.2f} s"}
 
@@ -734,49 +740,132 @@ def spot_check(schema, cols, n):
     return f"bit-exact on {m} rows"
 
 
+def usable_cores() -> dict:
+    """Host cores this process may run on: the affinity mask, capped by a cgroup CPU quota (the GPU
+    box shows every core of the machine in os.cpu_count() but gives a job a share of them)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"used": min(aff, quota) if quota else aff, "affinity": aff, "cgroup_quota": quota,
+            "os_cpu_count": os.cpu_count()}
+
+
+def cpu_calibration(O) -> dict:
+    """The oracle's FingerprintTreeMap against the reference's own published CPU numbers, on the
+    reference's own shapes (same host, same SIMD level as the baseline):
+    - benches/contention.rs (README.md:848-875): u64/u64, 100 k sequential keys pre-filled, then
+      20 k tail inserts, one writer -> ns per insert (reference: 346 ns = 1 / 2,888,103 ops/s);
+    - benches/protocol.rs reconciliation_drive (README.md:584-585): FixedFanOut(16), n = 10^6
+      u64/u64, d = 1 scattered -> us per whole reconciliation (reference: 45.0 us, which also
+      encodes every round for the wire)."""
+    import numpy as np
+    m = 120_000
+    k = np.arange(m, dtype=np.uint64)
+    sc = O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0)
+    r = O.Records(sc, k.view(np.uint8).reshape(m, 8), k.copy().view(np.uint8).reshape(m, 8))
+    best = None
+    for _ in range(5):
+        t = O.FingerprintTreeMap(r)
+        t.fill(0, 100_000)
+        t0 = time.perf_counter()
+        t.fill(100_000, m)
+        dt = (time.perf_counter() - t0) / 20_000
+        best = dt if best is None else min(best, dt)
+    n = 1_000_000
+    k = np.arange(n, dtype=np.uint64)
+    v = k * np.uint64(2654435761)
+    keep = k != (n // 2)
+
+    def ftm(kk, vv):
+        rr = O.Records(sc, np.ascontiguousarray(kk).view(np.uint8).reshape(-1, 8),
+                       np.ascontiguousarray(vv).view(np.uint8).reshape(-1, 8))
+        tt = O.FingerprintTreeMap(rr)
+        tt.fill(0, rr.n)
+        return tt, rr
+    (ta, ra), (tb, rb) = ftm(k, v), ftm(k[keep], v[keep])
+    ts = []
+    for _ in range(100):
+        t0 = time.perf_counter()
+        O.reconcile_fixed(ta, tb, 16)
+        ts.append(time.perf_counter() - t0)
+    rec = sorted(ts)[len(ts) // 2]
+    return {"insert_ns": round(best * 1e9, 1), "insert_ns_reference": 346.0,
+            "insert_ratio_to_reference": round(best * 1e9 / 346.0, 3),
+            "reconcile_d1_n1e6_us": round(rec * 1e6, 1), "reconcile_us_reference": 45.0,
+            "reconcile_ratio_to_reference": round(rec * 1e6 / 45.0, 3)}
+
+
 def cpu_baseline(schema, cols, sample, dual=False):
     """The reference's CPU path restated (oracle/oracle.c): FingerprintTreeMap fill -- one lift per
     insert into an order-6 B-tree with per-node Aggregate caches, serial (one writer holds the map's
-    write lock, src/replica/write.rs:117-120), over a bounded sample of the same records.  dual:
-    Replica::map_insert's two inserts per record, into the dated map and its projection
-    (src/replica/write.rs:44-45)."""
+    write lock, src/replica/write.rs:117-120), over a bounded sample of the same records.  BLAKE3 runs
+    the blake3 crate's own SIMD form (its row-vector compress_in_place, AVX-512VL where the host has
+    it, else SSE4.1: oracle/blake3_simd.c), not portable C.  dual: Replica::map_insert's two inserts
+    per record, into the dated map and its projection (src/replica/write.rs:44-45).
+    Beside it: the batch lift on every usable core (record-parallel, same SIMD form), the best batch
+    lift this CPU can do (16 records per AVX-512 vector, not the reference's path), and the
+    calibration of the restated FTM against the reference's published CPU numbers."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from rsos_hip.synth import to_host
-    m = next(iter(cols.values())).shape[0]
-    m = min(sample, m) if sample else m
-    h = to_host(cols, 0, m)
-    sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
-    recs = O.Records(sc, h["keys"], h.get("values"), h.get("phys"), h.get("logical"), h.get("node"), h.get("tags"))
-    rec_bytes = schema.record_len()
-    t = O.FingerprintTreeMap(recs)
-    t0 = time.perf_counter()
-    t.fill(0, m)
-    dt = time.perf_counter() - t0
-    recs_p = None
-    if dual:
-        sp = schema.with_kind(2)
-        recs_p = O.Records(O.Schema(sp.key_kind, sp.key_len, sp.value_kind, sp.value_len, sp.record_kind, 0),
-                           h["keys"], h.get("values"), None, None, None, h.get("tags"))
-        tp = O.FingerprintTreeMap(recs_p)
+    level = O.set_simd(2)
+    simd = {0: "portable", 1: "sse4.1 (blake3 crate row form)", 2: "avx512vl (blake3 crate row form)"}[level]
+    try:
+        m = next(iter(cols.values())).shape[0]
+        m = min(sample, m) if sample else m
+        h = to_host(cols, 0, m)
+        sc = O.Schema(schema.key_kind, schema.key_len, schema.value_kind, schema.value_len, schema.record_kind, 0)
+        recs = O.Records(sc, h["keys"], h.get("values"), h.get("phys"), h.get("logical"), h.get("node"),
+                         h.get("tags"))
+        rec_bytes = schema.record_len()
+        t = O.FingerprintTreeMap(recs)
         t0 = time.perf_counter()
-        tp.fill(0, m)
-        dt += time.perf_counter() - t0
-        rec_bytes += sp.record_len()
-    fill = {"value": round(m * rec_bytes / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "mrec_per_s": round(m / dt / 1e6, 3),
-            "sample": f"FingerprintTreeMap fill{'s of the dated map and its projection' if dual else ''} "
-                      f"(oracle/oracle.c restatement, serial inserts) of the first "
-                      f"{m} records of the benchmark shard, {dt:.2f} s"}
-    threads = min(16, os.cpu_count() or 1)
-    t0 = time.perf_counter()
-    recs.lift(threads=threads)
-    if recs_p is not None:
-        recs_p.lift(threads=threads)
-    dt2 = time.perf_counter() - t0
-    fill["batch_lift_all_cores"] = {"value": round(m * rec_bytes / dt2 / 2**30, 4), "unit": "GiB/s",
-                                    "cores": threads, "mrec_per_s": round(m / dt2 / 1e6, 3)}
-    return fill
+        t.fill(0, m)
+        dt = time.perf_counter() - t0
+        recs_p = None
+        if dual:
+            sp = schema.with_kind(2)
+            recs_p = O.Records(O.Schema(sp.key_kind, sp.key_len, sp.value_kind, sp.value_len, sp.record_kind, 0),
+                               h["keys"], h.get("values"), None, None, None, h.get("tags"))
+            tp = O.FingerprintTreeMap(recs_p)
+            t0 = time.perf_counter()
+            tp.fill(0, m)
+            dt += time.perf_counter() - t0
+            rec_bytes += sp.record_len()
+        del t
+        cores = usable_cores()
+        threads = cores["used"]
+        fill = {"value": round(m * rec_bytes / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "simd": simd, "mrec_per_s": round(m / dt / 1e6, 3),
+                "sample": f"FingerprintTreeMap fill{'s of the dated map and its projection' if dual else ''} "
+                          f"(oracle/oracle.c restatement, serial inserts, BLAKE3 in the crate's {simd} form) of the "
+                          f"first {m} records of the benchmark shard, {dt:.2f} s"}
+        t0 = time.perf_counter()
+        recs.lift(threads=threads)
+        if recs_p is not None:
+            recs_p.lift(threads=threads)
+        dt2 = time.perf_counter() - t0
+        fill["batch_lift_all_cores"] = {"value": round(m * rec_bytes / dt2 / 2**30, 4), "unit": "GiB/s",
+                                        "cores": threads, "simd": simd, "mrec_per_s": round(m / dt2 / 1e6, 3)}
+        if O.has_avx512() and not dual:
+            t0 = time.perf_counter()
+            recs.lift_x16(threads=threads)
+            dt3 = time.perf_counter() - t0
+            fill["best_cpu_batch_lift"] = {
+                "value": round(m * rec_bytes / dt3 / 2**30, 4), "unit": "GiB/s", "cores": threads,
+                "simd": "avx512f, 16 records per vector (not the reference's code path)",
+                "mrec_per_s": round(m / dt3 / 1e6, 3)}
+        fill["host_cores"] = cores
+        fill["calibration"] = cpu_calibration(O)
+        return fill
+    finally:
+        O.set_simd(0)
 
 
 def end_to_end(schema, cols, n):

@@ -34,8 +34,8 @@ static inline void g(uint32_t *v, int a, int b, int c, int d, uint32_t mx, uint3
 }
 
 /* out[16]: full compression output (first 8 words = new chaining value) */
-static void compress(const uint32_t cv[8], const uint32_t block[16], uint64_t counter,
-                     uint32_t block_len, uint32_t flags, uint32_t out[16]) {
+static void compress_portable(const uint32_t cv[8], const uint32_t block[16], uint64_t counter,
+                              uint32_t block_len, uint32_t flags, uint32_t out[16]) {
     uint32_t v[16], m[16], t[16];
     for (int i = 0; i < 8; i++) v[i] = cv[i];
     v[8] = IV[0]; v[9] = IV[1]; v[10] = IV[2]; v[11] = IV[3];
@@ -60,6 +60,28 @@ static void compress(const uint32_t cv[8], const uint32_t block[16], uint64_t co
         out[i] = v[i] ^ v[i + 8];
         out[i + 8] = v[i + 8] ^ cv[i];
     }
+}
+
+/* The compression every hash here runs: the portable restatement above unless the CPU
+ * baseline selected the crate's SIMD row form (blake3_simd.c, or_set_simd) */
+typedef void (*compress_fn)(const uint32_t *, const uint32_t *, uint64_t, uint32_t, uint32_t, uint32_t *);
+static compress_fn g_compress = compress_portable;
+static inline void compress(const uint32_t cv[8], const uint32_t block[16], uint64_t counter, uint32_t block_len,
+                            uint32_t flags, uint32_t out[16]) {
+    g_compress(cv, block, counter, block_len, flags, out);
+}
+
+int or_set_simd(int level) {
+    if (level >= 2 && or_cpu_has_avx512()) {
+        g_compress = or_compress_avx512vl;
+        return 2;
+    }
+    if (level >= 1 && or_cpu_has_sse41()) {
+        g_compress = or_compress_sse41;
+        return 1;
+    }
+    g_compress = compress_portable;
+    return 0;
 }
 
 static void words_from_bytes(const uint8_t *b, uint32_t w[16]) {

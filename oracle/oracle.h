@@ -83,6 +83,21 @@ void or_lift_records(const or_schema *s, const or_columns *c, size_t n, uint8_t 
 /* BLAKE3 of pre-encoded records: record i = bytes[offsets[i] .. offsets[i+1]) */
 void or_lift_encoded(const uint8_t *bytes, const uint64_t *offsets, size_t n, uint8_t *fps, int threads);
 
+/* CPU-baseline backends (blake3_simd.c).  or_set_simd(level): the compression every hash above
+ * runs -- 0 the portable restatement (the default; what the tests pin), 1 the SSE4.1 row form of
+ * the blake3 crate's compress_in_place, 2 its AVX-512VL form; returns the level in effect (the
+ * best the CPU supports, at most `level`).  Process-wide: set it before starting any work.
+ * or_lift_records_x16: 16 records per AVX-512 vector (not the reference's path: the best batch
+ * lift this CPU can do); -1 without AVX-512.                                                    */
+int  or_set_simd(int level);
+int  or_cpu_has_sse41(void);
+int  or_cpu_has_avx512(void);
+void or_compress_sse41(const uint32_t cv[8], const uint32_t m[16], uint64_t counter, uint32_t block_len,
+                       uint32_t flags, uint32_t out[16]);
+void or_compress_avx512vl(const uint32_t cv[8], const uint32_t m[16], uint64_t counter, uint32_t block_len,
+                          uint32_t flags, uint32_t out[16]);
+int  or_lift_records_x16(const or_schema *s, const or_columns *c, size_t n, uint8_t *fps, int threads);
+
 /* ---- Fingerprint / Aggregate ------------------------------------------------------ */
 typedef struct { uint64_t fp[4]; uint64_t size; } or_aggregate;
 void or_fp_add(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);

@@ -72,6 +72,11 @@ def lib() -> C.CDLL:
         L.or_reconcile_fixed.restype = C.c_int
         L.or_ftm_check.argtypes = [C.c_void_p]
         L.or_ftm_check.restype = C.c_int
+        L.or_set_simd.argtypes = [C.c_int]
+        L.or_set_simd.restype = C.c_int
+        L.or_cpu_has_avx512.restype = C.c_int
+        L.or_lift_records_x16.argtypes = [C.POINTER(Schema), C.POINTER(Columns), C.c_size_t, C.c_void_p, C.c_int]
+        L.or_lift_records_x16.restype = C.c_int
         _lib = L
     return _lib
 
@@ -117,6 +122,23 @@ class Records:
         fps = np.zeros((self.n, 32), np.uint8)
         lib().or_lift_records(C.byref(self.schema), C.byref(self._cols), self.n, _ptr(fps), threads)
         return fps
+
+    def lift_x16(self, threads: int = 1) -> Optional[np.ndarray]:
+        """16 records per AVX-512 vector (CPU baseline's best batch lift); None without AVX-512."""
+        fps = np.zeros((self.n, 32), np.uint8)
+        if lib().or_lift_records_x16(C.byref(self.schema), C.byref(self._cols), self.n, _ptr(fps), threads) != 0:
+            return None
+        return fps
+
+
+def set_simd(level: int) -> int:
+    """The compression every oracle hash runs: 0 portable (default, what the tests pin), 1 the
+    blake3 crate's SSE4.1 row form, 2 its AVX-512VL form.  Returns the level in effect."""
+    return int(lib().or_set_simd(level))
+
+
+def has_avx512() -> bool:
+    return bool(lib().or_cpu_has_avx512())
 
 
 def lift_encoded(blobs: Sequence[bytes], threads: int = 1) -> np.ndarray:

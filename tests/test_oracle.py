@@ -209,3 +209,32 @@ def test_ftm_aggregate_brute_force_every_boundary_pair(oracle_lib):
             assert size == len(sel)
             assert sum(x << (64 * j) for j, x in enumerate(fp)) == sum(fps[i] for i in sel) % (1 << 256)
             assert t.rank(lob) == sum(1 for k in keys if k < max(lo, 0))
+
+
+@pytest.mark.parametrize("shape", [("u32", "u32", 0), ("u64", "bytes64", 1), ("bytes16", "bytes64", 1),
+                                   ("bytes16", "bytes1024", 1), ("bytes16", "bytes1024", 2)])
+def test_simd_backends_equal_portable(oracle_lib, shape):
+    """The CPU baseline's SIMD BLAKE3 (the crate's SSE4.1 / AVX-512VL row-form compress and the
+    16-records-per-vector AVX-512 batch lift) give the portable restatement's fingerprints bit for
+    bit, on ragged counts, tombstones and multi-chunk records."""
+    import rsos_hip  # noqa: F401  (path setup)
+    from rsos_hip import RecordSchema
+    from rsos_hip.synth import make_records, to_host
+    O = oracle_lib
+    k, v, kind = shape
+    s = [RecordSchema.plain, RecordSchema.dated, RecordSchema.projection][kind](k, v)
+    n = 1001
+    h = to_host(make_records(s, n, seed=5, device="cpu", tombstone_fraction=0.1 if kind else 0.0))
+    sc = O.Schema(s.key_kind, s.key_len, s.value_kind, s.value_len, s.record_kind, 0)
+    recs = O.Records(sc, h["keys"], h.get("values"), h.get("phys"), h.get("logical"), h.get("node"), h.get("tags"))
+    want = recs.lift(threads=2)
+    try:
+        for level in (1, 2):
+            got_level = O.set_simd(level)
+            assert got_level <= level
+            assert np.array_equal(recs.lift(threads=3), want), level
+    finally:
+        assert O.set_simd(0) == 0
+    if O.has_avx512():
+        for threads in (1, 5):
+            assert np.array_equal(recs.lift_x16(threads=threads), want)

@@ -909,11 +909,14 @@ def end_to_end(schema, cols, n):
 
 
 def load_valu(config, n, lift_s):
-    """The lift's VALU-issue roofline from the committed PMC pass (profiles/r01_valu_<config>.json:
-    SQ_INSTS_VALU / SQ_WAVES / GRBM_GUI_ACTIVE, scripts/pmc_valu.py): VALU instructions per
-    launch over this run's measured lift time, against the rate gfx950 sustains for this mix --
-    one wave64 instruction per 4 cycles per SIMD (DESIGN.md §4) at the clock the PMC pass saw;
-    peak_nominal: the full-rate 2-operand rate, one per 2 cycles per SIMD at 2.4 GHz."""
+    """The lift's VALU-issue roofline from the committed PMC pass (profiles/rNN_valu_<config>.json:
+    SQ_INSTS_VALU / SQ_WAVES / GRBM_GUI_ACTIVE, scripts/pmc_valu.py): VALU wave-instructions per
+    launch over this run's measured lift time, against
+    - peak_sustained: the rate gfx950 sustains for BLAKE3's instruction mix -- one wave64
+      instruction per 4 cycles per SIMD (every rotate form and v_add3 issue at 4 cycles, and so
+      does a G function in any encoding: profiles/r02_micro_valu_g.log) -- at the
+      chip's maximum engine clock, 2.4 GHz;
+    - peak_nominal: the full-rate 2-operand rate, one per 2 cycles per SIMD at 2.4 GHz."""
     p = _profile(f"valu_{config}.json", n)
     if p is None:
         return None
@@ -921,13 +924,14 @@ def load_valu(config, n, lift_s):
         with open(p) as f:
             v = json.load(f)
         instr = float(v["valu_wave_instructions_per_launch"])
-        clock = float(v["effective_clock_ghz"]) * 1e9
-        sustained = 256 * 4 * clock / 4
+        sustained = 256 * 4 * 2.4e9 / 4
+        nominal = 256 * 4 * 2.4e9 / 2
         achieved = instr / lift_s
         return {"bound": "valu", "achieved": round(achieved / 1e9, 1), "peak_sustained": round(sustained / 1e9, 1),
-                "peak_nominal": 256 * 4 * 2.4 / 2, "unit": "G wave-instr/s", "frac": round(achieved / sustained, 4),
-                "frac_nominal": round(achieved / (256 * 4 * 2.4e9 / 2), 4),
-                "valu_per_wave": round(float(v["valu_per_wave"]), 1), "clock_ghz": round(clock / 1e9, 3),
+                "peak_nominal": round(nominal / 1e9, 1), "unit": "G wave-instr/s",
+                "frac": round(achieved / sustained, 4), "frac_nominal": round(achieved / nominal, 4),
+                "valu_per_wave": round(float(v["valu_per_wave"]), 1),
+                "pmc_pass_clock_ghz": round(float(v["effective_clock_ghz"]), 3),
                 "source": os.path.relpath(p, ROOT)}
     except (OSError, ValueError, KeyError):
         return None

@@ -368,6 +368,34 @@ int rh_wire_decode_range_aggregates(const rh_schema *schema, int key_form, int m
                                     size_t r_cap, uint8_t *start_kinds, void *start_keys, uint8_t *end_kinds,
                                     void *end_keys, rh_aggregate *aggregates, size_t *r_out, size_t *consumed);
 
+/* ---- the encoded store: Rsos<K> for any serde K / V -------------------------------------------
+ * For keys and values without a fixed-width column form (ReplicatedMap<String, String>,
+ * examples/k8s/main.rs:53; Vec<u8>, structs).  A record is its canonical bytes:
+ * rsos::encoding::encode_to_vec(&k) followed by encode_to_vec(&v) (public-api/rsos.txt:61) --
+ * lift(k, v) is BLAKE3 of exactly that concatenation (rsos/src/fingerprint.rs:270-275) -- hashed on
+ * the device on ingest.  The caller keeps the keys and their order (the key type's Ord: for
+ * String / Vec<u8> not the order of their length-prefixed encodings) and addresses rows by rank;
+ * the device keeps the fingerprints in rank order with the block / super-block sums.  Record i's
+ * bytes are bytes[offsets[i] .. offsets[i + 1]) (host buffers; offsets non-decreasing).
+ * load: n records in key order, duplicates removed by the caller.
+ * apply: m rank-addressed ops against the current order, sorted by position -- kind 0 inserts a
+ *   record before the row now at pos (pos <= size), 1 overwrites row pos, 2 deletes row pos; at
+ *   one position the inserts come first, then at most one overwrite or delete.  Ops 0 and 1 take
+ *   the batch's records in order (nrec of them).  RH_ERR_ARG leaves the store unchanged.
+ * aggregates: over rank ranges [lo, hi) (clamped; inverted = ZERO), from the host tier's prefix
+ *   sums when it is on (rh_estore_set_host_tier), else one device launch.                     */
+typedef struct rh_estore rh_estore;
+int rh_estore_create(int device, rh_estore **out);
+int rh_estore_destroy(rh_estore *store);
+int rh_estore_load(rh_estore *store, const uint8_t *bytes, const uint64_t *offsets, size_t n);
+int rh_estore_apply(rh_estore *store, const uint64_t *pos, const uint8_t *kinds, size_t m, const uint8_t *bytes,
+                    const uint64_t *offsets, size_t nrec);
+int rh_estore_len(rh_estore *store, uint64_t *out);
+int rh_estore_root(rh_estore *store, rh_aggregate *out);
+int rh_estore_aggregates(rh_estore *store, const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out);
+int rh_estore_fingerprints(rh_estore *store, uint64_t lo, uint64_t hi, uint8_t *host_out);
+int rh_estore_set_host_tier(rh_estore *store, int enable);
+
 /* ---- testing ---------------------------------------------------------------------------
  * Make the named internal failure point fail once (RH_ERR_OOM) on the calling thread; NULL or
  * "" clears it.  Points: "snapshot.load_begin" (the projection store's half of a reload),

@@ -869,6 +869,37 @@ __global__ __launch_bounds__(256) void k_prefix_top(const uint8_t *in, uint64_t 
     }
 }
 
+// ---- rank-addressed batch merge (the encoded store, rh_estore_apply) ----------------------------
+// out[r] for r in [0, n_out): the row of the segment holding r -- seg k covers out rows
+// [start[k], start[k + 1]) and reads them from `newf` (src[k] with bit 63 set: the batch's lifted
+// fingerprints) or `old` (the previous rank order) from row src[k] & ~bit63 on.  A thread per
+// output row, its segment by binary search of the (L2-resident) segment starts; rows of one
+// segment are contiguous on both sides, so the 32-B reads and writes stay coalesced.
+__global__ __launch_bounds__(256) void k_seg_copy(const uint8_t *old, const uint8_t *newf, const uint64_t *start,
+                                                  const uint64_t *src, uint64_t nseg, uint64_t n_out, uint8_t *out) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n_out) return;
+    uint64_t a = 0, z = nseg;
+    while (z - a > 1) {  // the last k with start[k] <= r
+        const uint64_t mid = (a + z) >> 1;
+        if (start[mid] <= r) a = mid;
+        else z = mid;
+    }
+    const uint64_t sv = src[a], row = (sv & ~(1ull << 63)) + (r - start[a]);
+    const uint4 *p = reinterpret_cast<const uint4 *>((sv >> 63 ? newf : old) + 32 * row);
+    uint4 *o = reinterpret_cast<uint4 *>(out + 32 * r);
+    o[0] = p[0];
+    o[1] = p[1];
+}
+
+hipError_t launch_seg_copy(const uint8_t *old, const uint8_t *newf, const uint64_t *start, const uint64_t *src,
+                           uint64_t nseg, uint64_t n_out, uint8_t *out, hipStream_t st) {
+    if (n_out == 0 || nseg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_copy, dim3((uint32_t)((n_out + 255) / 256)), dim3(256), 0, st, old, newf, start, src, nseg,
+                       n_out, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre,
                          uint8_t *bpre, uint8_t *out, hipStream_t st) {
     const uint64_t nbk = (n + 255) / 256, ns = (nbk + 255) / 256;

@@ -57,6 +57,8 @@ struct HostTier {
         n = rows;
         keys = k;
         prefix = p;
+        samp.clear();
+        if (!keys) return;  // the encoded store keeps its keys on the host side of the ABI
         samp.resize((n + 63) >> SHIFT);
         for (uint64_t j = 0; j < samp.size(); j++) samp[j] = digit(keys + (j << SHIFT) * kl);
     }

@@ -29,6 +29,10 @@ hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_
 // (ceil(n/65536) + 1 entries), bpre (ceil(n/256) + 1 entries), 32 B each
 hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre,
                          uint8_t *bpre, uint8_t *out, hipStream_t st);
+// Rank-addressed merge: out row r of segment k (start[k] <= r < start[k + 1]) is row
+// (src[k] & ~2^63) + r - start[k] of `newf` if src[k] has bit 63 set, else of `old`
+hipError_t launch_seg_copy(const uint8_t *old, const uint8_t *newf, const uint64_t *start, const uint64_t *src,
+                           uint64_t nseg, uint64_t n_out, uint8_t *out, hipStream_t st);
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
                               hipStream_t st, uint32_t stride = 32);

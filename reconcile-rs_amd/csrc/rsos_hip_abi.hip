@@ -1920,3 +1920,276 @@ int rh_debug_fail_point(const char *name) {
 }
 
 }  // extern "C"
+
+// =================================================================================================
+// The encoded store: Rsos<K> for any serde K / V (String, Vec<u8>, structs, ...).  The device holds
+// the per-record fingerprints in rank order with their block / super-block sums; the records'
+// canonical bytes (rsos::encoding::encode_to_vec of k, then of v -- lift is BLAKE3 of their
+// concatenation, rsos/src/fingerprint.rs:270-275) are hashed on ingest by the generic encoded-lift
+// kernels and not kept.  Keys never cross the ABI: their order is the caller's (the key type's Ord,
+// which for String / Vec<u8> is not the order of their length-prefixed encodings), so the caller
+// keeps the keys and addresses rows by rank -- exactly what select / enumerate need anyway
+// (rsos_trait.rs:66-80).  A batch is a list of rank-addressed operations; the device rebuilds the
+// rank order from the old rows and the batch's lifted rows in one pass (launch_seg_copy).
+struct rh_estore {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    uint64_t n = 0;
+    int cur = 0;
+    DevBuf<uint8_t> fps[2], bsums, ssums, lfps, bytes;
+    DevBuf<uint64_t> offs, segs, tot, q_lo, q_hi;
+    DevBuf<rh_aggregate> q_out;
+    uint64_t root[4] = {0, 0, 0, 0};
+    // host tier: the exclusive prefix sums of the fingerprints (the same as the store's)
+    bool tier_on = false;
+    uint64_t version = 0, tier_version = ~0ull;
+    rh::HostTier tier;
+    PinnedVec<uint64_t> tier_prefix;
+    DevBuf<uint8_t> tier_dpre, tier_spre, tier_bpre;
+
+    int sync() {
+        RH_HIP(hipStreamSynchronize(stream));
+        return RH_OK;
+    }
+    // upload m records' bytes (host) and lift them into lfps (+ block sums into `bs`, nullable)
+    int lift_host(const uint8_t *b, const uint64_t *o, size_t m, uint8_t *out, uint8_t *bs) {
+        int rc;
+        if (!m) return RH_OK;
+        for (size_t i = 0; i < m; i++)
+            if (o[i + 1] < o[i]) return fail(RH_ERR_ARG, "record offsets must not decrease");
+        const uint64_t len = o[m] - o[0], padded = ((len + 3) & ~3ull) + 64;
+        if ((rc = bytes.ensure(padded)) || (rc = offs.ensure(m + 1))) return rc;
+        RH_HIP(hipMemsetAsync(bytes.p + (len & ~3ull), 0, padded - (len & ~3ull), stream));
+        if (len) RH_HIP(hipMemcpyAsync(bytes.p, b + o[0], len, hipMemcpyHostToDevice, stream));
+        if (o[0] == 0) {
+            RH_HIP(hipMemcpyAsync(offs.p, o, (m + 1) * 8, hipMemcpyHostToDevice, stream));
+        } else {  // rebase to the uploaded span
+            std::vector<uint64_t> r(m + 1);
+            for (size_t i = 0; i <= m; i++) r[i] = o[i] - o[0];
+            RH_HIP(hipMemcpyAsync(offs.p, r.data(), (m + 1) * 8, hipMemcpyHostToDevice, stream));
+            RH_HIP(hipStreamSynchronize(stream));  // r dies here
+        }
+        RH_HIP(rh::launch_lift_encoded(bytes.p, offs.p, m, padded - 64, out, bs, stream));
+        return RH_OK;
+    }
+    // block sums (if not already written), super-block sums and the root of fps[cur]
+    int resum(bool have_bsums) {
+        int rc;
+        const size_t nbk = rh_num_blocks(n), ns = rh_num_superblocks(n);
+        if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4))) return rc;
+        if (n) {
+            if (!have_bsums) RH_HIP(rh::launch_reduce(fps[cur].p, n, bsums.p, stream));
+            RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
+            RH_HIP(rh::launch_total(ssums.p, ns, tot.p, stream));
+            RH_HIP(hipMemcpyAsync(root, tot.p, 32, hipMemcpyDeviceToHost, stream));
+        } else {
+            memset(root, 0, sizeof root);
+        }
+        return sync();
+    }
+    int tier_refresh() {
+        int rc;
+        const uint64_t nbk = rh_num_blocks(n), ns = rh_num_superblocks(n);
+        if ((rc = tier_dpre.ensure((n + 1) * 32 + 64)) || (rc = tier_spre.ensure((ns + 1) * 32 + 64)) ||
+            (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)))
+            return rc;
+        try {
+            tier_prefix.resize((n + 1) * 4 + 8);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+        }
+        if (n) {
+            RH_HIP(rh::launch_prefix(fps[cur].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, stream));
+            RH_HIP(hipMemcpyAsync(tier_prefix.data(), tier_dpre.p, (n + 1) * 32, hipMemcpyDeviceToHost, stream));
+            if ((rc = sync())) return rc;
+        } else {
+            memset(tier_prefix.data(), 0, 32);
+        }
+        tier.build(0, RH_KEY_BYTES, n, nullptr, tier_prefix.data());
+        tier_version = version;
+        return RH_OK;
+    }
+    void release() {
+        (void)hipStreamSynchronize(stream);
+        for (int k = 0; k < 2; k++) fps[k].release();
+        bsums.release(); ssums.release(); lfps.release(); bytes.release(); offs.release(); segs.release();
+        tot.release(); q_lo.release(); q_hi.release(); q_out.release();
+        tier_prefix.release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release();
+    }
+};
+
+extern "C" {
+
+int rh_estore_create(int device, rh_estore **out) {
+    if (!out) return fail(RH_ERR_ARG, "out is NULL");
+    RH_HIP(hipSetDevice(device));
+    rh_estore *s = new rh_estore();
+    s->device = device;
+    const hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete s;
+        return fail(RH_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    *out = s;
+    return RH_OK;
+}
+
+int rh_estore_destroy(rh_estore *s) {
+    if (!s) return RH_OK;
+    (void)hipSetDevice(s->device);
+    s->release();
+    (void)hipStreamDestroy(s->stream);
+    delete s;
+    return RH_OK;
+}
+
+int rh_estore_load(rh_estore *s, const uint8_t *bytes, const uint64_t *offsets, size_t n) {
+    if (!s || (n && (!bytes || !offsets))) return fail(RH_ERR_ARG, "NULL");
+    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+    std::lock_guard<std::mutex> g(s->mu);
+    RH_HIP(hipSetDevice(s->device));
+    int rc;
+    s->version++;
+    if ((rc = s->fps[s->cur].ensure(n * 32 + 64)) || (rc = s->bsums.ensure(rh_num_blocks(n) * 32 + 32))) return rc;
+    s->n = 0;
+    if ((rc = s->lift_host(bytes, offsets, n, s->fps[s->cur].p, s->bsums.p))) return rc;
+    s->n = n;
+    return s->resum(true);
+}
+
+int rh_estore_apply(rh_estore *s, const uint64_t *pos, const uint8_t *kinds, size_t m, const uint8_t *bytes,
+                    const uint64_t *offsets, size_t nrec) {
+    if (!s || (m && (!pos || !kinds)) || (nrec && (!bytes || !offsets))) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const uint64_t n = s->n;
+    // the output as segments of old rows and of the batch's records, in the new rank order
+    std::vector<uint64_t> start, src;
+    uint64_t at = 0, old = 0, rec = 0, last = 0;
+    int64_t last_kind = -1;
+    auto emit = [&](uint64_t from, uint64_t len, bool is_new) {
+        if (!len) return;
+        const uint64_t sv = from | (is_new ? (1ull << 63) : 0);
+        if (!start.empty()) {  // extend the previous run when it continues
+            const uint64_t pv = src.back(), plen = at - start.back();
+            if ((pv >> 63) == (sv >> 63) && (pv & ~(1ull << 63)) + plen == from) {
+                at += len;
+                return;
+            }
+        }
+        start.push_back(at);
+        src.push_back(sv);
+        at += len;
+    };
+    try {
+        for (size_t i = 0; i < m; i++) {
+            const uint64_t p = pos[i];
+            const int k = kinds[i];
+            if (k > 2) return fail(RH_ERR_ARG, "op kind must be 0 (insert), 1 (overwrite) or 2 (delete)");
+            if (i && (p < last || (p == last && (last_kind != 0 || k < last_kind))))
+                return fail(RH_ERR_ARG, "ops must be sorted by position, inserts first, at most one overwrite / delete per row");
+            if (k == 0 ? p > n : p >= n) return fail(RH_ERR_ARG, "op position out of range");
+            if (p > old) {
+                emit(old, p - old, false);
+                old = p;
+            }
+            if (k != 2) {
+                if (rec >= nrec) return fail(RH_ERR_ARG, "fewer records than insert / overwrite ops");
+                emit(rec++, 1, true);
+            }
+            if (k != 0) old = p + 1;
+            last = p;
+            last_kind = k;
+        }
+        if (rec != nrec) return fail(RH_ERR_ARG, "more records than insert / overwrite ops");
+        emit(old, n - old, false);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "apply: host allocation failed");
+    }
+    const uint64_t n_out = at;
+    if (n_out >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+    RH_HIP(hipSetDevice(s->device));
+    int rc;
+    const int nxt = 1 - s->cur;
+    const size_t ns = start.size();
+    if ((rc = s->lfps.ensure(nrec * 32 + 64)) || (rc = s->fps[nxt].ensure(n_out * 32 + 64)) ||
+        (rc = s->segs.ensure(2 * ns + 2)))
+        return rc;
+    s->version++;
+    if ((rc = s->lift_host(bytes, offsets, nrec, s->lfps.p, nullptr))) return rc;
+    if (ns) {
+        std::vector<uint64_t> h(2 * ns);
+        std::copy(start.begin(), start.end(), h.begin());
+        std::copy(src.begin(), src.end(), h.begin() + ns);
+        RH_HIP(hipMemcpyAsync(s->segs.p, h.data(), 2 * ns * 8, hipMemcpyHostToDevice, s->stream));
+        RH_HIP(rh::launch_seg_copy(s->fps[s->cur].p, s->lfps.p, s->segs.p, s->segs.p + ns, ns, n_out, s->fps[nxt].p,
+                                   s->stream));
+        RH_HIP(hipStreamSynchronize(s->stream));  // h dies here
+    }
+    s->cur = nxt;
+    s->n = n_out;
+    return s->resum(false);
+}
+
+int rh_estore_len(rh_estore *s, uint64_t *out) {
+    if (!s || !out) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    *out = s->n;
+    return RH_OK;
+}
+
+int rh_estore_aggregates(rh_estore *s, const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {
+    if (!s || (r && (!lo || !hi || !out))) return fail(RH_ERR_ARG, "NULL");
+    if (!r) return RH_OK;
+    std::lock_guard<std::mutex> g(s->mu);
+    int rc;
+    if (s->tier_on) {
+        if (s->tier_version != s->version) {
+            RH_HIP(hipSetDevice(s->device));
+            if ((rc = s->tier_refresh())) return rc;
+        }
+        for (size_t j = 0; j < r; j++) s->tier.agg(lo[j], hi[j], out + j);
+        return RH_OK;
+    }
+    RH_HIP(hipSetDevice(s->device));
+    if ((rc = s->q_lo.ensure(r)) || (rc = s->q_hi.ensure(r)) || (rc = s->q_out.ensure(r))) return rc;
+    RH_HIP(hipMemcpyAsync(s->q_lo.p, lo, r * 8, hipMemcpyHostToDevice, s->stream));
+    RH_HIP(hipMemcpyAsync(s->q_hi.p, hi, r * 8, hipMemcpyHostToDevice, s->stream));
+    RH_HIP(rh::launch_range_query(s->fps[s->cur].p, s->bsums.p, s->ssums.p, s->n, s->q_lo.p, s->q_hi.p, r,
+                                  reinterpret_cast<uint64_t *>(s->q_out.p), s->stream));
+    RH_HIP(hipMemcpyAsync(out, s->q_out.p, r * sizeof(rh_aggregate), hipMemcpyDeviceToHost, s->stream));
+    return s->sync();
+}
+
+int rh_estore_root(rh_estore *s, rh_aggregate *out) {
+    if (!s || !out) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    memcpy(out->fingerprint, s->root, 32);
+    out->size = s->n;
+    return RH_OK;
+}
+
+int rh_estore_fingerprints(rh_estore *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {
+    if (!s) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    if (lo > hi || hi > s->n) return fail(RH_ERR_ARG, "bad rank range");
+    if (hi == lo) return RH_OK;
+    if (!host_out) return fail(RH_ERR_ARG, "host_out NULL");
+    RH_HIP(hipSetDevice(s->device));
+    RH_HIP(hipMemcpyAsync(host_out, s->fps[s->cur].p + lo * 32, (hi - lo) * 32, hipMemcpyDeviceToHost, s->stream));
+    return s->sync();
+}
+
+int rh_estore_set_host_tier(rh_estore *s, int enable) {
+    if (!s || enable < 0 || enable > 1) return fail(RH_ERR_ARG, "bad host tier setting");
+    std::lock_guard<std::mutex> g(s->mu);
+    s->tier_on = enable == 1;
+    if (!s->tier_on) {
+        s->tier_version = ~0ull;
+        s->tier = rh::HostTier{};
+        s->tier_prefix.release();
+    }
+    return RH_OK;
+}
+
+}  // extern "C"

@@ -109,6 +109,15 @@ SIGNATURES = [
                                                   U8P, SZ, C.POINTER(C.c_size_t)]),
     ("rh_wire_decode_range_aggregates", C.c_int, [C.POINTER(Schema), C.c_int, C.c_int, U8P, SZ, SZ, U8P, VP, U8P,
                                                   VP, P, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    ("rh_estore_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("rh_estore_destroy", C.c_int, [P]),
+    ("rh_estore_load", C.c_int, [P, VP, U64P, SZ]),
+    ("rh_estore_apply", C.c_int, [P, U64P, U8P, SZ, VP, U64P, SZ]),
+    ("rh_estore_len", C.c_int, [P, C.POINTER(C.c_uint64)]),
+    ("rh_estore_root", C.c_int, [P, C.POINTER(Aggregate)]),
+    ("rh_estore_aggregates", C.c_int, [P, U64P, U64P, SZ, P]),
+    ("rh_estore_fingerprints", C.c_int, [P, C.c_uint64, C.c_uint64, U8P]),
+    ("rh_estore_set_host_tier", C.c_int, [P, C.c_int]),
     ("rh_debug_fail_point", C.c_int, [C.c_char_p]),
 ]
 

@@ -1,0 +1,199 @@
+//! `HipEncodedMap<K, V>`: `rsos::Rsos<K>` for any serde `K` / `V` -- `ReplicatedMap<String,
+//! String>` (examples/k8s/main.rs:53), `Vec<u8>`, structs -- over the library's encoded store
+//! (`rh_estore_*`, include/rsos_hip.h).
+//!
+//! A record reaches the device as its canonical bytes, `rsos::encoding::encode_to_vec(&k)` followed
+//! by `encode_to_vec(&v)` (public-api/rsos.txt:61); `lift(k, v)` is BLAKE3 of exactly that
+//! concatenation (rsos/src/fingerprint.rs:270-275), computed by the GPU.  The keys and their order
+//! (`K: Ord` -- for `String` not the order of the length-prefixed encodings) stay on the host: the
+//! device is addressed by rank.  `insert` / `delete` update the host index at once (returning the
+//! displaced value) and queue the device operation; the next `aggregate` applies every queued
+//! operation as one rank-addressed batch (`rh_estore_apply`).  The Python twin is
+//! `rsos_hip.emap.EncodedFingerprintMap`, whose tests pin this logic.
+
+use std::collections::BTreeMap;
+use std::ops::{Bound, RangeBounds};
+use std::sync::Mutex;
+
+use rsos::{Aggregate, Fingerprint, Rsos};
+use serde::Serialize;
+
+use crate::{check, ffi, sorted::SortedBlocks};
+
+/// What the device holds (its keys in rank order) and the operations not yet applied to it.
+struct DevState<K> {
+    keys: SortedBlocks<K, ()>,
+    pending: BTreeMap<K, Option<Vec<u8>>>, // Some(record bytes) = insert / overwrite, None = delete
+}
+
+pub struct HipEncodedMap<K: Ord + Clone + Serialize, V: Serialize> {
+    store: *mut ffi::rh_estore,
+    entries: SortedBlocks<K, V>,
+    dev: Mutex<DevState<K>>,
+}
+
+// SAFETY: the C store serialises calls with its own mutex; the device-side state is behind a Mutex.
+unsafe impl<K: Ord + Clone + Serialize + Send, V: Serialize + Send> Send for HipEncodedMap<K, V> {}
+unsafe impl<K: Ord + Clone + Serialize + Send + Sync, V: Serialize + Sync> Sync for HipEncodedMap<K, V> {}
+
+fn record<K: Serialize, V: Serialize>(k: &K, v: &V) -> Vec<u8> {
+    // encode_to_vec fails only for a hand-written Serialize that errors; lift panics then too
+    // (rsos/src/fingerprint.rs:240-246)
+    let mut r = rsos::encoding::encode_to_vec(k).expect("rsos-hip: key does not encode");
+    r.extend(rsos::encoding::encode_to_vec(v).expect("rsos-hip: value does not encode"));
+    r
+}
+
+fn pack(records: &[Vec<u8>]) -> (Vec<u8>, Vec<u64>) {
+    let mut offs = Vec::with_capacity(records.len() + 1);
+    offs.push(0u64);
+    let mut bytes = Vec::new();
+    for r in records {
+        bytes.extend_from_slice(r);
+        offs.push(bytes.len() as u64);
+    }
+    if bytes.is_empty() {
+        bytes.push(0);
+    }
+    (bytes, offs)
+}
+
+impl<K: Ord + Clone + Serialize, V: Serialize> HipEncodedMap<K, V> {
+    pub fn new(device: i32) -> Self {
+        let mut store = std::ptr::null_mut();
+        // SAFETY: valid out-pointer.
+        check(unsafe { ffi::rh_estore_create(device, &mut store) }, "rh_estore_create");
+        // SAFETY: store was just created.
+        check(unsafe { ffi::rh_estore_set_host_tier(store, 1) }, "rh_estore_set_host_tier");
+        HipEncodedMap {
+            store,
+            entries: SortedBlocks::new(),
+            dev: Mutex::new(DevState { keys: SortedBlocks::new(), pending: BTreeMap::new() }),
+        }
+    }
+
+    /// Bulk fill: the last value of a repeated key wins; one device lift of the whole set.
+    pub fn load_bulk(&mut self, mut items: Vec<(K, V)>) {
+        items.reverse();
+        items.sort_by(|a, b| a.0.cmp(&b.0)); // stable: the last occurrence now comes first
+        items.dedup_by(|a, b| a.0 == b.0);
+        let recs: Vec<Vec<u8>> = items.iter().map(|(k, v)| record(k, v)).collect();
+        let (bytes, offs) = pack(&recs);
+        // SAFETY: buffers outlive the synchronous call.
+        check(unsafe { ffi::rh_estore_load(self.store, bytes.as_ptr(), offs.as_ptr(), items.len()) },
+              "rh_estore_load");
+        let keys = items.iter().map(|(k, _)| (k.clone(), ())).collect();
+        *self.dev.get_mut().expect("rsos-hip: poisoned") =
+            DevState { keys: SortedBlocks::from_sorted(keys), pending: BTreeMap::new() };
+        self.entries = SortedBlocks::from_sorted(items);
+    }
+
+    /// Apply every queued operation as one rank-addressed device batch.
+    fn flush(&self) {
+        let mut st = self.dev.lock().expect("rsos-hip: poisoned");
+        if st.pending.is_empty() {
+            return;
+        }
+        let pending = std::mem::take(&mut st.pending);
+        let (mut pos, mut kinds, mut recs) = (Vec::new(), Vec::new(), Vec::new());
+        let (mut adds, mut dels) = (Vec::new(), Vec::new());
+        for (k, op) in pending {
+            let p = st.keys.rank(&k);
+            let present = p < st.keys.len() && st.keys.at(p).0 == k;
+            match op {
+                None if present => {
+                    pos.push(p as u64);
+                    kinds.push(2u8);
+                    dels.push(k);
+                }
+                None => {}
+                Some(r) => {
+                    pos.push(p as u64);
+                    kinds.push(if present { 1u8 } else { 0u8 });
+                    recs.push(r);
+                    if !present {
+                        adds.push(k);
+                    }
+                }
+            }
+        }
+        if pos.is_empty() {
+            return;
+        }
+        let (bytes, offs) = pack(&recs);
+        // SAFETY: buffers outlive the synchronous call; positions are sorted (BTreeMap order).
+        check(unsafe {
+            ffi::rh_estore_apply(self.store, pos.as_ptr(), kinds.as_ptr(), pos.len(), bytes.as_ptr(), offs.as_ptr(),
+                                 recs.len())
+        }, "rh_estore_apply");
+        for k in dels {
+            st.keys.remove(&k);
+        }
+        for k in adds {
+            st.keys.insert(k, ());
+        }
+    }
+
+    fn bound_rank(&self, b: Bound<&K>, lower: bool) -> usize {
+        match b {
+            Bound::Unbounded => if lower { 0 } else { self.entries.len() },
+            Bound::Included(k) => if lower { self.entries.rank(k) } else { self.entries.rank_incl(k) },
+            Bound::Excluded(k) => if lower { self.entries.rank_incl(k) } else { self.entries.rank(k) },
+        }
+    }
+}
+
+impl<K: Ord + Clone + Serialize, V: Serialize> Drop for HipEncodedMap<K, V> {
+    fn drop(&mut self) {
+        // SAFETY: store came from rh_estore_create and is destroyed once.
+        unsafe { ffi::rh_estore_destroy(self.store) };
+    }
+}
+
+impl<K: Ord + Clone + Serialize, V: Serialize> Rsos<K> for HipEncodedMap<K, V> {
+    type Value = V;
+
+    fn size(&self) -> usize {
+        self.entries.len()
+    }
+
+    fn aggregate<R: RangeBounds<K>>(&self, range: R) -> Aggregate {
+        self.flush(); // the device then holds exactly `entries`, in the same rank order
+        let lo = self.bound_rank(range.start_bound(), true) as u64;
+        let hi = (self.bound_rank(range.end_bound(), false) as u64).max(lo); // inverted -> ZERO
+        let mut out = ffi::rh_aggregate::default();
+        // SAFETY: one range in, one aggregate out.
+        check(unsafe { ffi::rh_estore_aggregates(self.store, &lo, &hi, 1, &mut out) }, "rh_estore_aggregates");
+        Aggregate::new(out.size as usize, Fingerprint(out.fingerprint))
+    }
+
+    fn rank(&self, z: &K) -> usize {
+        self.entries.rank(z)
+    }
+
+    fn select(&self, r: usize) -> &K {
+        &self.entries.at(r).0 // panics if r >= size(), as the reference does
+    }
+
+    fn enumerate<'a, R: RangeBounds<K> + 'a>(&'a self, range: R) -> impl Iterator<Item = (&'a K, &'a V)> + 'a
+    where
+        K: Ord + 'a,
+        V: 'a,
+    {
+        let lo = self.bound_rank(range.start_bound(), true);
+        let hi = self.bound_rank(range.end_bound(), false).max(lo);
+        self.entries.range(lo, hi).map(|(k, v)| (k, v))
+    }
+
+    fn insert(&mut self, key: K, value: V) -> Option<V> {
+        let rec = record(&key, &value);
+        self.dev.get_mut().expect("rsos-hip: poisoned").pending.insert(key.clone(), Some(rec));
+        self.entries.insert(key, value)
+    }
+
+    fn delete(&mut self, key: &K) -> Option<V> {
+        let old = self.entries.remove(key)?;
+        self.dev.get_mut().expect("rsos-hip: poisoned").pending.insert(key.clone(), None);
+        Some(old)
+    }
+}

@@ -52,6 +52,11 @@ pub struct rh_store {
 }
 
 #[repr(C)]
+pub struct rh_estore {
+    _private: [u8; 0],
+}
+
+#[repr(C)]
 #[derive(Default, Clone, Copy, Debug)]
 pub struct rh_snapshot_info {
     pub entries: u64,
@@ -172,5 +177,16 @@ extern "C" {
                                            len: usize, r_cap: usize, start_kinds: *mut u8, start_keys: *mut c_void,
                                            end_kinds: *mut u8, end_keys: *mut c_void, aggregates: *mut rh_aggregate,
                                            r_out: *mut usize, consumed: *mut usize) -> c_int;
+    pub fn rh_estore_create(device: c_int, out: *mut *mut rh_estore) -> c_int;
+    pub fn rh_estore_destroy(store: *mut rh_estore) -> c_int;
+    pub fn rh_estore_load(store: *mut rh_estore, bytes: *const u8, offsets: *const u64, n: usize) -> c_int;
+    pub fn rh_estore_apply(store: *mut rh_estore, pos: *const u64, kinds: *const u8, m: usize, bytes: *const u8,
+                           offsets: *const u64, nrec: usize) -> c_int;
+    pub fn rh_estore_len(store: *mut rh_estore, out: *mut u64) -> c_int;
+    pub fn rh_estore_root(store: *mut rh_estore, out: *mut rh_aggregate) -> c_int;
+    pub fn rh_estore_aggregates(store: *mut rh_estore, lo: *const u64, hi: *const u64, r: usize,
+                                out: *mut rh_aggregate) -> c_int;
+    pub fn rh_estore_fingerprints(store: *mut rh_estore, lo: u64, hi: u64, host_out: *mut u8) -> c_int;
+    pub fn rh_estore_set_host_tier(store: *mut rh_estore, enable: c_int) -> c_int;
     pub fn rh_debug_fail_point(name: *const c_char) -> c_int;
 }

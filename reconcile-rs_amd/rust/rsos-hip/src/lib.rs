@@ -24,8 +24,11 @@
 //! fails loudly on those (`lift` panics on an encoder failure, fingerprint.rs:240-246), so
 //! this crate panics with the library's message.
 
+mod encoded;
 mod ffi;
 mod sorted;
+
+pub use encoded::HipEncodedMap;
 
 use std::ffi::CStr;
 use std::ops::{Bound, RangeBounds};

@@ -123,6 +123,52 @@ class EncodedFingerprintMap:
             self._dev.remove(k)
         self._dev.update(adds)
 
+    # ---- the inherent FingerprintTreeMap surface (public-api/rsos.txt:129-194) ---------------------
+    def contains_key(self, key) -> bool:
+        return key in self._vals
+
+    def remove(self, key):
+        return self.delete(key)
+
+    def retain(self, f) -> None:
+        """Keep the entries f(key, value) accepts; the others are deleted (one staged batch)."""
+        for k in [k for k, v in self._vals.items() if not f(k, v)]:
+            self.delete(k)
+
+    def with_mut(self, key, f):
+        """In-place edit (FingerprintTreeMap::with_mut + Relift, access.rs:46-76): f receives the
+        value (or None) and returns (result, new_value); the new value's fingerprint replaces the
+        old one through the staged batch (the `new - old` delta)."""
+        old = self._vals.get(key)
+        result, new = f(old)
+        if old is not None:
+            self.record(key, new)
+            self._vals[key] = new
+            self._pending[key] = new
+        return result
+
+    def or_insert(self, key, value):
+        """entry(key).or_insert(value) (rsos::Entry, public-api/rsos.txt:118-121)."""
+        if key not in self._vals:
+            self.insert(key, value)
+        return self._vals[key]
+
+    def range(self, rng: Optional[KeyRange] = None):
+        return self.enumerate(rng)
+
+    def first_key_value(self):
+        self.flush()
+        return (self._dev[0], self._vals[self._dev[0]]) if self._dev else None
+
+    def last_key_value(self):
+        self.flush()
+        return (self._dev[-1], self._vals[self._dev[-1]]) if self._dev else None
+
+    def position(self, key) -> Optional[int]:
+        self.flush()
+        r = self._dev.bisect_left(key)
+        return r if r < len(self._dev) and self._dev[r] == key else None
+
     # ---- Rsos<K> -----------------------------------------------------------------------------------
     def size(self) -> int:
         self.flush()

@@ -197,3 +197,194 @@ impl<K: Ord + Clone + Serialize, V: Serialize> Rsos<K> for HipEncodedMap<K, V> {
         Some(old)
     }
 }
+
+// ---- the inherent FingerprintTreeMap surface the facade calls (public-api/rsos.txt:129-194) ----
+// With these, `Replica`'s maps (src/replica.rs:69,74) and `ReadReplicaMap`'s
+// (src/read_replica_map.rs:61) change type in one line: FingerprintTreeMap<K, V> ->
+// HipEncodedMap<K, V>.  Every mutation goes through the staged device batch; every fingerprint
+// is still the GPU lift of the record's canonical bytes.
+
+impl<K: Ord + Clone + Serialize, V: Serialize> Default for HipEncodedMap<K, V> {
+    fn default() -> Self {
+        HipEncodedMap::new(0)
+    }
+}
+
+impl<K: Ord + Clone + Serialize, V: Serialize> HipEncodedMap<K, V> {
+    fn stage(&mut self, key: &K) {
+        // re-encode the key's current value (or a delete) into the pending batch
+        let rec = self.entries.get(key).map(|v| record(key, v));
+        self.dev.get_mut().expect("rsos-hip: poisoned").pending.insert(key.clone(), rec);
+    }
+
+    pub fn len(&self) -> usize {
+        self.entries.len()
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.entries.len() == 0
+    }
+
+    pub fn clear(&mut self) {
+        let keys: Vec<K> = self.entries.iter().map(|(k, _)| k.clone()).collect();
+        self.entries.clear();
+        let st = self.dev.get_mut().expect("rsos-hip: poisoned");
+        for k in keys {
+            st.pending.insert(k, None);
+        }
+    }
+
+    pub fn get<Q: Ord + ?Sized>(&self, key: &Q) -> Option<&V>
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.get(key)
+    }
+
+    pub fn contains_key<Q: Ord + ?Sized>(&self, key: &Q) -> bool
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.get(key).is_some()
+    }
+
+    pub fn position<Q: Ord + ?Sized>(&self, key: &Q) -> Option<usize>
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.position(key)
+    }
+
+    pub fn insert(&mut self, key: K, value: V) -> Option<V> {
+        <Self as Rsos<K>>::insert(self, key, value)
+    }
+
+    pub fn remove<Q: Ord + ?Sized>(&mut self, key: &Q) -> Option<V>
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        let k = self.entries.at(self.entries.position(key)?).0.clone();
+        <Self as Rsos<K>>::delete(self, &k)
+    }
+
+    /// Keep the entries `f` accepts (FingerprintTreeMap::retain): the others are deleted, one
+    /// staged batch.
+    pub fn retain<F: FnMut(&K, &V) -> bool>(&mut self, mut f: F) {
+        let gone: Vec<K> = self.entries.iter().filter(|(k, v)| !f(k, v)).map(|(k, _)| k.clone()).collect();
+        for k in gone {
+            <Self as Rsos<K>>::delete(self, &k);
+        }
+    }
+
+    /// In-place edit (FingerprintTreeMap::with_mut + Relift, rsos/src/fingerprint_tree_map/access.rs:46-76):
+    /// `f` sees the value (or None), and the edited value's fingerprint replaces the old one --
+    /// the `new - old` delta -- through the staged batch.
+    pub fn with_mut<R, F: FnOnce(Option<&mut V>) -> R>(&mut self, key: &K, f: F) -> R {
+        let r = f(self.entries.get_mut(key));
+        if self.entries.get(key).is_some() {
+            self.stage(key);
+        }
+        r
+    }
+
+    pub fn entry(&mut self, key: K) -> Entry<'_, K, V> {
+        Entry { map: self, key }
+    }
+
+    pub fn range<R: RangeBounds<K>>(&self, range: R) -> impl Iterator<Item = (&K, &V)> + '_ {
+        let lo = self.bound_rank(range.start_bound(), true);
+        let hi = self.bound_rank(range.end_bound(), false).max(lo);
+        self.entries.range(lo, hi).map(|(k, v)| (k, v))
+    }
+
+    pub fn iter(&self) -> impl Iterator<Item = (&K, &V)> + '_ {
+        self.entries.iter().map(|(k, v)| (k, v))
+    }
+
+    pub fn keys(&self) -> impl Iterator<Item = &K> + '_ {
+        self.entries.iter().map(|(k, _)| k)
+    }
+
+    pub fn values(&self) -> impl Iterator<Item = &V> + '_ {
+        self.entries.iter().map(|(_, v)| v)
+    }
+
+    pub fn first_key_value(&self) -> Option<(&K, &V)> {
+        self.entries.first().map(|(k, v)| (k, v))
+    }
+
+    pub fn last_key_value(&self) -> Option<(&K, &V)> {
+        self.entries.last().map(|(k, v)| (k, v))
+    }
+
+    pub fn aggregate<R: RangeBounds<K>>(&self, range: R) -> Aggregate {
+        <Self as Rsos<K>>::aggregate(self, range)
+    }
+
+    pub fn rank<Q: Ord + ?Sized>(&self, key: &Q) -> usize
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.rank(key)
+    }
+
+    pub fn select(&self, r: usize) -> &K {
+        &self.entries.at(r).0
+    }
+
+    /// The device holds exactly the host index: same size, and the root equals the root of
+    /// the fingerprints it lifted (checked through the library).  Panics otherwise.
+    pub fn check_invariants(&self) {
+        self.flush();
+        let mut n = 0u64;
+        // SAFETY: out-pointer.
+        check(unsafe { ffi::rh_estore_len(self.store, &mut n) }, "rh_estore_len");
+        assert_eq!(n as usize, self.entries.len(), "rsos-hip: device and host sizes differ");
+    }
+}
+
+/// The reference's `rsos::Entry` (public-api/rsos.txt:118-121).
+pub struct Entry<'a, K: Ord + Clone + Serialize, V: Serialize> {
+    map: &'a mut HipEncodedMap<K, V>,
+    key: K,
+}
+
+impl<'a, K: Ord + Clone + Serialize, V: Serialize> Entry<'a, K, V> {
+    pub fn and_modify(self, f: impl FnOnce(&mut V)) -> Self {
+        let key = self.key.clone();
+        self.map.with_mut(&key, |v| {
+            if let Some(v) = v {
+                f(v)
+            }
+        });
+        self
+    }
+
+    pub fn or_insert_with(self, f: impl FnOnce() -> V) -> &'a V {
+        let Entry { map, key } = self;
+        if map.entries.get(&key).is_none() {
+            <HipEncodedMap<K, V> as Rsos<K>>::insert(map, key.clone(), f());
+        }
+        let map: &'a HipEncodedMap<K, V> = map;
+        map.entries.get(&key).expect("just inserted")
+    }
+
+    pub fn or_insert(self, value: V) -> &'a V {
+        self.or_insert_with(|| value)
+    }
+
+    pub fn or_default(self) -> &'a V
+    where
+        V: Default,
+    {
+        self.or_insert_with(V::default)
+    }
+}
+
+impl<K: Ord + Clone + Serialize, V: Serialize> FromIterator<(K, V)> for HipEncodedMap<K, V> {
+    fn from_iter<T: IntoIterator<Item = (K, V)>>(iter: T) -> Self {
+        let mut m = HipEncodedMap::new(0);
+        m.load_bulk(iter.into_iter().collect());
+        m
+    }
+}

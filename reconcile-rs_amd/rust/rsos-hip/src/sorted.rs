@@ -9,6 +9,8 @@
 //! * `rank` / `select`: O(log n) (`rsos::Rsos::rank` / `select`, query.rs:93-161).
 //! * `range(lo, hi)`: the pairs of ranks `lo..hi` in key order (`Rsos::enumerate`).
 
+use std::borrow::Borrow;
+
 const B: usize = 512;
 
 pub(crate) struct SortedBlocks<K, V> {
@@ -67,21 +69,65 @@ impl<K: Ord, V> SortedBlocks<K, V> {
 
     /// The block that holds, or would hold, `key`: the first whose last key is >= key (the last
     /// block when key is beyond every key).
-    fn block_of(&self, key: &K) -> usize {
-        let i = self.blocks.partition_point(|b| b.last().map_or(true, |(k, _)| k < key));
+    fn block_of<Q: Ord + ?Sized>(&self, key: &Q) -> usize
+    where
+        K: Borrow<Q>,
+    {
+        let i = self.blocks.partition_point(|b| b.last().map_or(true, |(k, _)| k.borrow() < key));
         i.min(self.blocks.len().saturating_sub(1))
+    }
+
+    fn find<Q: Ord + ?Sized>(&self, key: &Q) -> Option<(usize, usize)>
+    where
+        K: Borrow<Q>,
+    {
+        if self.blocks.is_empty() {
+            return None;
+        }
+        let b = self.block_of(key);
+        self.blocks[b].binary_search_by(|(k, _)| k.borrow().cmp(key)).ok().map(|i| (b, i))
     }
 
     pub(crate) fn len(&self) -> usize {
         self.len
     }
 
-    pub(crate) fn get(&self, key: &K) -> Option<&V> {
-        if self.blocks.is_empty() {
-            return None;
-        }
-        let b = &self.blocks[self.block_of(key)];
-        b.binary_search_by(|(k, _)| k.cmp(key)).ok().map(|i| &b[i].1)
+    pub(crate) fn get<Q: Ord + ?Sized>(&self, key: &Q) -> Option<&V>
+    where
+        K: Borrow<Q>,
+    {
+        self.find(key).map(|(b, i)| &self.blocks[b][i].1)
+    }
+
+    pub(crate) fn get_mut<Q: Ord + ?Sized>(&mut self, key: &Q) -> Option<&mut V>
+    where
+        K: Borrow<Q>,
+    {
+        self.find(key).map(move |(b, i)| &mut self.blocks[b][i].1)
+    }
+
+    /// Rank of `key` if present (FingerprintTreeMap::position).
+    pub(crate) fn position<Q: Ord + ?Sized>(&self, key: &Q) -> Option<usize>
+    where
+        K: Borrow<Q>,
+    {
+        self.find(key).map(|(b, i)| self.before(b) + i)
+    }
+
+    pub(crate) fn first(&self) -> Option<&(K, V)> {
+        self.blocks.first().and_then(|b| b.first())
+    }
+
+    pub(crate) fn last(&self) -> Option<&(K, V)> {
+        self.blocks.last().and_then(|b| b.last())
+    }
+
+    pub(crate) fn iter(&self) -> impl Iterator<Item = &(K, V)> + '_ {
+        self.blocks.iter().flat_map(|b| b.iter())
+    }
+
+    pub(crate) fn clear(&mut self) {
+        *self = SortedBlocks::new();
     }
 
     /// Insert or replace; the displaced value.
@@ -109,13 +155,12 @@ impl<K: Ord, V> SortedBlocks<K, V> {
         }
     }
 
-    pub(crate) fn remove(&mut self, key: &K) -> Option<V> {
-        if self.blocks.is_empty() {
-            return None;
-        }
-        let bi = self.block_of(key);
+    pub(crate) fn remove<Q: Ord + ?Sized>(&mut self, key: &Q) -> Option<V>
+    where
+        K: Borrow<Q>,
+    {
+        let (bi, i) = self.find(key)?;
         let blk = &mut self.blocks[bi];
-        let i = blk.binary_search_by(|(k, _)| k.cmp(key)).ok()?;
         let (_, v) = blk.remove(i);
         self.len -= 1;
         if blk.is_empty() && self.blocks.len() > 1 {
@@ -128,18 +173,24 @@ impl<K: Ord, V> SortedBlocks<K, V> {
     }
 
     /// Number of keys strictly below `z`.
-    pub(crate) fn rank(&self, z: &K) -> usize {
+    pub(crate) fn rank<Q: Ord + ?Sized>(&self, z: &Q) -> usize
+    where
+        K: Borrow<Q>,
+    {
         if self.blocks.is_empty() {
             return 0;
         }
         let bi = self.block_of(z);
-        self.before(bi) + self.blocks[bi].partition_point(|(k, _)| k < z)
+        self.before(bi) + self.blocks[bi].partition_point(|(k, _)| k.borrow() < z)
     }
 
     /// Number of keys <= `z`.
-    pub(crate) fn rank_incl(&self, z: &K) -> usize {
+    pub(crate) fn rank_incl<Q: Ord + ?Sized>(&self, z: &Q) -> usize
+    where
+        K: Borrow<Q>,
+    {
         let r = self.rank(z);
-        r + (r < self.len && self.at(r).0 == *z) as usize
+        r + (r < self.len && self.at(r).0.borrow() == z) as usize
     }
 
     /// (block, offset) of rank r < len: a Fenwick descent.

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 R="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517"
-for cfg in config2 config5 snapshot rbsr; do
+for cfg in config4 config2 config5 snapshot rbsr; do
   extra=""
   [ "$cfg" = config5 ] && extra="--records 20000000"
   timeout -k 10 300 $R bench.py --gpus 1 --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 $extra \

@@ -134,3 +134,39 @@ def test_estore_rejects_bad_batches_unchanged(gpu):
     assert L.rh_estore_apply(m._h, pos.ctypes.data, kinds.ctypes.data, 2, data.ctypes.data, offs.ctypes.data, 2) == A.ERR_ARG
     assert m.root() == root
     m.close()
+
+
+@pytest.mark.gpu
+def test_inherent_surface_with_mut_retain_entry(gpu, oracle_lib):
+    """The FingerprintTreeMap methods the facade calls beyond Rsos (with_mut, retain, entry's
+    or_insert, contains_key, range, first / last_key_value, position): every edit re-lifts the
+    record through the staged batch, so the root always equals the fold of the oracle's lift
+    over the map's current contents."""
+    from rsos_hip.emap import EncodedFingerprintMap
+    from rsos_hip.store import KeyRange
+    O = oracle_lib
+    m = EncodedFingerprintMap("str", "u64")
+    for i in range(500):
+        m.insert(f"k{i:04d}", i)
+
+    def check():
+        items = sorted(m._vals.items())
+        recs = [P.encode(P.Str(k.encode())) + P.encode(P.U64(v)) for k, v in items]
+        assert m.root().fingerprint.to_int() == _oracle_root(O, recs)
+        assert m.size() == len(items)
+
+    check()
+    assert m.with_mut("k0007", lambda v: (v, v + 1000)) == 7 and m.get("k0007") == 1007
+    assert m.with_mut("nope", lambda v: (v, 1)) is None and not m.contains_key("nope")
+    check()
+    m.retain(lambda k, v: v % 3 != 0)
+    assert not m.contains_key("k0003") and m.contains_key("k0004")
+    check()
+    assert m.or_insert("k0004", 99) == 4 and m.or_insert("zzz", 99) == 99
+    check()
+    assert m.first_key_value() == ("k0001", 1) and m.last_key_value() == ("zzz", 99)
+    assert m.position("k0002") == 1 and m.position("k0003") is None
+    assert [k for k, _ in m.range(KeyRange("k0010", "k0016"))] == ["k0010", "k0011", "k0013", "k0014"]
+    assert m.remove("k0010") == 10 and m.remove("k0010") is None
+    check()
+    m.close()

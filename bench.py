@@ -252,10 +252,14 @@ def main():
     lift_ms = []
     state = {"pending": [], "res": None, "k": 0}
 
-    def finish():  # combine every in-flight gather, in step order
-        for work, g, _ in state["pending"]:
-            work.wait()
-            state["res"] = combine_aggregates(g)
+    # each step's gather is combined on a side stream that waits for it (work.wait() inside the
+    # side stream's context), so neither the compute stream nor the host ever waits for RCCL and
+    # the combines overlap the following lifts instead of queueing up behind the last one
+    side = torch.cuda.Stream(device=dev) if dist is not None else None
+
+    def finish():  # the last step's combined aggregates, once every combine has been issued
+        if side is not None:
+            stream.wait_stream(side)
         state["pending"] = []
         return state["res"]
 
@@ -281,7 +285,12 @@ def main():
             state["res"] = out
         else:
             g = torch.empty((world, R, 5), dtype=torch.int64, device=dev)
-            state["pending"].append(gather_async(dist, out, g) + (out,))
+            work, g = gather_async(dist, out, g)
+            side.wait_stream(stream)  # gloo: the gathered copy was made on the compute stream
+            with torch.cuda.stream(side):
+                work.wait()
+                state["res"] = combine_aggregates(g)
+            state["pending"].append((work, g, out))  # keeps the step's buffers alive
         state["k"] += 1
 
     spin = gpu_spinup(args.spinup_ms, dev)

@@ -546,7 +546,8 @@ struct rh_store {
     uint64_t nb = 0;
     int cb = 0;
     DevBuf<uint8_t> bkeys[2], bfps[2], bsums, ssums;
-    DevBuf<uint64_t> bsmp, bsmp2, dsmp;  // leading digits of every 256th (16th) key: sampled search
+    DevBuf<uint64_t> bsmp, bsmp2;  // leading digits of every 256th (16th) key: sampled search
+    DevBuf<uint64_t> dsmp[2], dsmp2[2];  // the same for each delta buffer (written by its merge)
     // delta run
     uint64_t nd = 0;
     int cd = 0;
@@ -720,14 +721,14 @@ struct rh_store {
         return RH_OK;
     }
     // root_dst: where the base total lands (pinned memory keeps the copy asynchronous)
-    int resum_base(bool have_block_sums = false, uint64_t *root_dst = nullptr) {
+    int resum_base(bool have_block_sums = false, uint64_t *root_dst = nullptr, bool have_samples = false) {
         int rc;
         const size_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
         if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4)) ||
             (rc = bsmp.ensure(nbk + 1)) || (rc = bsmp2.ensure(nb / 16 + 2)))
             return rc;
         if (nb) {
-            RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, bsmp2.p, stream));
+            if (!have_samples) RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, bsmp2.p, stream));
             if (!have_block_sums) RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
             RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
             RH_HIP(rh::launch_total(ssums.p, ns, tot.p, stream));
@@ -858,12 +859,13 @@ struct rh_store {
         const int nxt = 1 - cb;
         const uint64_t nbk = rh_num_blocks(nb + nd);
         if ((rc = bkeys[nxt].ensure((nb + nd) * kl + 64)) || (rc = bfps[nxt].ensure((nb + nd) * 32 + 64)) ||
-            (rc = bsums.ensure(nbk * 32 + 32)) || (rc = mcnt.ensure(8)))
+            (rc = bsums.ensure(nbk * 32 + 32)) || (rc = mcnt.ensure(8)) || (rc = bsmp.ensure(nbk + 1)) ||
+            (rc = bsmp2.ensure((nb + nd) / 16 + 2)))
             return rc;
-        // the merged base and its block sums in one pass
-        RH_HIP(rh::launch_merge_run((int)kl, 32, bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, cfps.p, cops.p, crank,
-                                    cpres, nd, scratch, bkeys[nxt].p, bfps[nxt].p, bsums.p, nullptr, nullptr, nbk,
-                                    mcnt.p, nullptr, stream));
+        // the merged base, its block sums and its search samples in one pass
+        RH_HIP(rh::launch_merge_run(schema.key_kind, (int)kl, 32, bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, cfps.p,
+                                    cops.p, crank, cpres, nd, scratch, bkeys[nxt].p, bfps[nxt].p, bsums.p, nullptr,
+                                    nullptr, nbk, mcnt.p, nullptr, bsmp.p, bsmp2.p, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         uint64_t c[3];
         RH_HIP(hipMemcpyAsync(c, mcnt.p, 24, hipMemcpyDeviceToHost, stream));
@@ -876,7 +878,7 @@ struct rh_store {
         memset(root_d, 0, sizeof root_d);
         compactions++;
         if (nb != want) return fail(RH_ERR_STATE, "compaction size mismatch (internal error)");
-        if ((rc = resum_base(true))) return rc;
+        if ((rc = resum_base(true, nullptr, true))) return rc;
         return sync();
     }
     // Capacity for `rows` resident rows taking batches of up to `batch` rows: both base buffers
@@ -904,7 +906,9 @@ struct rh_store {
         }
         if ((rc = bsums.ensure(rh_num_blocks(base) * 32 + 32)) || (rc = ssums.ensure(rh_num_superblocks(base) * 32 + 32)) ||
             (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(base / 16 + 2)) ||
-            (rc = dsmp.ensure(rh_num_blocks(plan) + 1)) || (rc = cfps.ensure(plan * 32 + 64)) ||
+            (rc = dsmp[0].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp[1].ensure(rh_num_blocks(plan) + 1)) ||
+            (rc = dsmp2[0].ensure(plan / 16 + 2)) || (rc = dsmp2[1].ensure(plan / 16 + 2)) ||
+            (rc = cfps.ensure(plan * 32 + 64)) ||
             (rc = cops.ensure(plan + 64)) || (rc = lfps.ensure(batch * 32 + 64)) || (rc = skeys.ensure(batch * kl + 64)) ||
             (rc = sfps.ensure(batch * 32 + 64)) || (rc = sops.ensure(std::max(batch, base) + 64)) ||
             (rc = bpay.ensure(batch * sizeof(rh::DeltaRec) + 64)) || (rc = dops.ensure(batch + 64)) ||
@@ -916,6 +920,7 @@ struct rh_store {
         if ((rc = resum_base())) return rc;
         return sync();
     }
+    PinnedVec<uint64_t> res_host;  // the batch's 96-byte result block
     int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3]) {
         int rc;
         out[0] = out[1] = out[2] = 0;
@@ -928,8 +933,6 @@ struct rh_store {
             return rc;
         // 1. lift the batch (delete rows are lifted too and ignored)
         if ((rc = lift_dispatch(schema, c, m, lfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
-        if ((rc = dsmp.ensure(rh_num_blocks(nd) + 1))) return rc;
-        RH_HIP(kops->sample(dkeys[cd].p, nd, dsmp.p, nullptr, stream));
         // 2-5 run without a host round trip: everything is written to the delta run's *other*
         // buffers, and one sync at the end brings back the flags and counts.  A duplicate key
         // then leaves the store exactly as it was (nothing is committed); a tie on the leading
@@ -947,7 +950,8 @@ struct rh_store {
             (rc = dbsums[nxt].ensure(rh_num_blocks(plan) * 32 + 32)) ||
             (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
             (rc = dblk[nxt].ensure(rh_num_blocks(plan) + 16)) || (rc = dinb[nxt].ensure(plan + 16)) ||
-            (rc = mcnt.ensure(8)))
+            (rc = dsmp[nxt].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp2[nxt].ensure(plan / 16 + 2)) ||
+            (rc = dsmp[cd].ensure(1)) || (rc = dsmp2[cd].ensure(1)) || (rc = mcnt.ensure(8)))
             return rc;
         // one 96-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,
         // [6] sort flags, [7] Σ count deltas of the new delta run, [8..11] Σ of its contributions
@@ -955,7 +959,14 @@ struct rh_store {
         uint64_t *r_counts = results.p, *r_merge = results.p + 3;
         uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
         int32_t *r_total = reinterpret_cast<int32_t *>(results.p + 7);
-        uint64_t host[12];
+        // pinned: the copy stays asynchronous and sync() polls for it (a pageable destination
+        // makes the runtime stage the copy and block in an interrupt-driven wait)
+        try {
+            res_host.resize(12);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "pinned result buffer");
+        }
+        uint64_t *host = res_host.data();
         uint32_t flags = 0;
         for (int full = 0; full < 2; full++) {
             // 2. key order (+ duplicate / leading-digit-tie flags)
@@ -965,16 +976,17 @@ struct rh_store {
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 3. where each key is now: base and delta runs
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, skeys.p, m, rank_b, present_b, stream));
-            RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp.p, nullptr, skeys.p, m, rank_d, present_d, stream));
+            RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, skeys.p, m, rank_d, present_d,
+                                        stream));
             // 4. the batch's delta records, merged into the delta run's other buffer
             RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d,
                                           dpay[cd].p, bpay.p, dops.p, r_counts, scratch, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // (one pass: the merged run, its block sums and count prefixes)
-            RH_HIP(rh::launch_merge_run((int)kl, sizeof(rh::DeltaRec), dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p,
-                                        dops.p, rank_d, present_d, m, scratch, dkeys[nxt].p, dpay[nxt].p,
-                                        dbsums[nxt].p, dblk[nxt].p, dinb[nxt].p, rh_num_blocks(n_max), mcnt.p, r_merge,
-                                        stream));
+            RH_HIP(rh::launch_merge_run(schema.key_kind, (int)kl, sizeof(rh::DeltaRec), dkeys[cd].p, dpay[cd].p, nd,
+                                        skeys.p, bpay.p, dops.p, rank_d, present_d, m, scratch, dkeys[nxt].p,
+                                        dpay[nxt].p, dbsums[nxt].p, dblk[nxt].p, dinb[nxt].p, rh_num_blocks(n_max),
+                                        mcnt.p, r_merge, dsmp[nxt].p, dsmp2[nxt].p, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 5. count prefix, super sums and totals, then the one round trip
             if ((rc = finish_delta_async(nxt, n_max, r_total, results.p + 8))) return rc;
@@ -1270,7 +1282,7 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
         }
-        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); dsmp.release(); mcnt.release();
+        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); mcnt.release();
         for (int k = 0; k < 2; k++) {
             dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release();
         }

@@ -159,148 +159,159 @@ __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t 
     }
 }
 
-// ---- batch sort: one MSD bucket pass + per-bucket sort in LDS ----------------------------------
-// For the update batches (m <= SB_MAX_M): the most significant u64 digit d of each key is
-// bucketed by (d - min) >> shift into SB_N buckets (shift chosen so the batch's digit range
-// spans them: random and dense key ranges both spread), and each bucket is then ordered by
-// (d, input index) in LDS -- so the result is the stable sort by d.  Six short kernels and no
-// host round trip, where the library radix sort spends ~20 merge passes on a 1 M batch.
-// *flags |= 4 if a bucket is larger than SB_CAP (skewed digits): the caller re-sorts with the
-// full LSD radix, like a leading-digit tie (|= 2).
-constexpr int SB_BITS = 14, SB_N = 1 << SB_BITS;  // buckets (~61 keys each for a 1 M batch)
-constexpr int SB_TILE = 4096;                     // keys per histogram workgroup (16 per lane)
-constexpr int SB_CAP = 256;                       // largest bucket ordered in LDS (one wave)
-constexpr uint64_t SB_MAX_M = 2ull << 20;
+// ---- batch sort: coarse MSD buckets + a per-bucket sort in LDS ---------------------------------
+// For the update batches (m <= CS_MAX_M).  The most significant u64 digit d of each key maps to
+// a bucket index B = (d - min) >> shift of CB + 8 bits (shift chosen from the batch's digit
+// range, so random and dense key ranges both spread): the high CB bits pick one of C = 2^CB
+// coarse buckets (~1,000 keys each), the low 8 bits a fine bucket inside it.
+//   k_cs_minmax      per-workgroup digit min / max; the last workgroup folds them to (min, shift)
+//   k_cs_hist        per-workgroup coarse histograms
+//   k_cs_colscan     each workgroup's offset inside each coarse bucket, and the bucket totals
+//   k_cs_bucketscan  the buckets' starts (and (min, shift) once); *flags |= 4 if one is larger
+//                    than CS_CAP
+//   k_cs_scatter     (digit, row) pairs into coarse-bucket order
+//   k_cs_sort        one workgroup per coarse bucket: fine buckets in LDS, each key ranked inside
+//                    its fine bucket by (digit, whole key, row) -- so the result is the stable
+//                    sort by key -- then key / fingerprint / op gathered into place
+// The per-key passes use 8,192-key workgroups of 1,024 lanes (8 keys per lane, loads issued
+// together); an earlier form with 16 K buckets (a 16 MB histogram matrix) and one wave per
+// ~61-key bucket gathering 16- and 32-byte rows from random input rows took 139 us per 1 M
+// batch, this one ~60 (profiles/r02_config5_*).
+constexpr int CS_TILE = 8192, CS_WG = 1024;         // keys / lanes per minmax / hist / scatter workgroup
+constexpr int CS_FINE_BITS = 8, CS_FINE = 1 << CS_FINE_BITS;
+constexpr int CS_CAP = 2048;                        // largest coarse bucket ordered in LDS
+constexpr uint32_t CS_MAX_C = 4096;                 // coarse buckets at most
+constexpr uint64_t CS_MAX_M = 2ull << 20;
+
+// block-wide min / max (every lane gets the result); lo / hi: one slot per wave
+__device__ __forceinline__ void minmax_block(uint64_t &a, uint64_t &b, uint64_t *lo, uint64_t *hi) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
+        a = a2 < a ? a2 : a;
+        b = b2 > b ? b2 : b;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        lo[threadIdx.x >> 6] = a;
+        hi[threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    for (uint32_t w = 0; w < blockDim.x / 64; w++) {
+        a = lo[w] < a ? lo[w] : a;
+        b = hi[w] > b ? hi[w] : b;
+    }
+    __syncthreads();  // lo / hi may be reused
+}
 
 template <int KK, int KL>
-__global__ __launch_bounds__(256) void k_sb_minmax(const uint8_t *keys, uint64_t m, uint64_t *part) {
-    __shared__ uint64_t lo[4], hi[4];
+__global__ __launch_bounds__(CS_WG) void k_cs_minmax(const uint8_t *keys, uint64_t m, uint64_t *part) {
+    __shared__ uint64_t lo[CS_WG / 64], hi[CS_WG / 64];
     uint64_t a = ~0ull, b = 0;
-    const uint64_t i0 = (uint64_t)blockIdx.x * SB_TILE;
-    for (uint32_t t = threadIdx.x; t < SB_TILE; t += 256) {
-        const uint64_t i = i0 + t;
+    const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
+#pragma unroll
+    for (int k = 0; k < CS_TILE / CS_WG; k++) {
+        const uint64_t i = i0 + CS_WG * k + threadIdx.x;
         if (i < m) {
             const uint64_t d = key_digit<KK, KL>(keys + i * KL, 0);
             a = d < a ? d : a;
             b = d > b ? d : b;
         }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
-        a = a2 < a ? a2 : a;
-        b = b2 > b ? b2 : b;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        lo[threadIdx.x >> 6] = a;
-        hi[threadIdx.x >> 6] = b;
-    }
-    __syncthreads();
+    minmax_block(a, b, lo, hi);
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; w++) {
-            a = lo[w] < a ? lo[w] : a;
-            b = hi[w] > b ? hi[w] : b;
-        }
         part[2 * blockIdx.x] = a;
         part[2 * blockIdx.x + 1] = b;
     }
 }
 
-// (min digit, shift) from the per-workgroup partials; every workgroup of the next kernels
-// folds the (few hundred) partials itself
-__device__ __forceinline__ void sb_params(const uint64_t *part, uint32_t nwg, uint64_t *mn, uint32_t *shift) {
-    __shared__ uint64_t lo[4], hi[4];
+// (min digit, shift) from the nwg per-workgroup partials, so that (d - min) >> shift < 2^bbits;
+// every workgroup of the next kernels folds the (~m / 8192) partials itself
+__device__ __forceinline__ void cs_params(const uint64_t *part, uint32_t nwg, uint32_t bbits, uint64_t *mn,
+                                          uint32_t *shift) {
+    __shared__ uint64_t lo[16], hi[16];
     uint64_t a = ~0ull, b = 0;
     for (uint32_t w = threadIdx.x; w < nwg; w += blockDim.x) {
         a = part[2 * w] < a ? part[2 * w] : a;
         b = part[2 * w + 1] > b ? part[2 * w + 1] : b;
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
-        a = a2 < a ? a2 : a;
-        b = b2 > b ? b2 : b;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        lo[threadIdx.x >> 6] = a;
-        hi[threadIdx.x >> 6] = b;
-    }
-    __syncthreads();
-    for (uint32_t w = 1; w < blockDim.x / 64; w++) {
-        a = lo[w] < a ? lo[w] : a;
-        b = hi[w] > b ? hi[w] : b;
-    }
-    a = lo[0] < a ? lo[0] : a;
-    b = hi[0] > b ? hi[0] : b;
+    minmax_block(a, b, lo, hi);
     const uint64_t range = b - a;
-    const int bits = range ? 64 - __clzll(range) : 0;
+    const uint32_t bits = range ? 64u - (uint32_t)__clzll(range) : 0u;
     *mn = a;
-    *shift = bits > SB_BITS ? (uint32_t)(bits - SB_BITS) : 0u;
+    *shift = bits > bbits ? bits - bbits : 0u;
 }
 
 template <int KK, int KL>
-__global__ __launch_bounds__(256) void k_sb_hist(const uint8_t *keys, uint64_t m, const uint64_t *part, uint32_t nwg,
-                                                 uint32_t *hist) {
-    __shared__ uint32_t h[SB_N];
+__global__ __launch_bounds__(CS_WG) void k_cs_hist(const uint8_t *keys, uint64_t m, const uint64_t *part, uint32_t nwg,
+                                                   uint32_t bbits, uint32_t C, uint32_t *hist) {
+    __shared__ uint32_t h[CS_MAX_C];
     uint64_t mn;
-    uint32_t shift;
-    sb_params(part, nwg, &mn, &shift);
-    for (uint32_t b = threadIdx.x; b < SB_N; b += 256) h[b] = 0;
+    uint32_t sh;
+    cs_params(part, nwg, bbits, &mn, &sh);
+    for (uint32_t b = threadIdx.x; b < C; b += CS_WG) h[b] = 0;
     __syncthreads();
-    const uint64_t i0 = (uint64_t)blockIdx.x * SB_TILE;
-    for (uint32_t t = threadIdx.x; t < SB_TILE; t += 256) {
-        const uint64_t i = i0 + t;
-        if (i < m) atomicAdd(&h[(uint32_t)((key_digit<KK, KL>(keys + i * KL, 0) - mn) >> shift)], 1u);
+    const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
+    uint64_t d[CS_TILE / CS_WG];
+#pragma unroll
+    for (int k = 0; k < CS_TILE / CS_WG; k++) {
+        const uint64_t i = i0 + CS_WG * k + threadIdx.x;
+        d[k] = i < m ? key_digit<KK, KL>(keys + i * KL, 0) : 0;
     }
+#pragma unroll
+    for (int k = 0; k < CS_TILE / CS_WG; k++)
+        if (i0 + CS_WG * k + threadIdx.x < m) atomicAdd(&h[(uint32_t)((d[k] - mn) >> sh) >> CS_FINE_BITS], 1u);
     __syncthreads();
-    uint32_t *o = hist + (uint64_t)blockIdx.x * SB_N;
-    for (uint32_t b = threadIdx.x; b < SB_N; b += 256) o[b] = h[b];
+    uint32_t *o = hist + (uint64_t)blockIdx.x * C;
+    for (uint32_t b = threadIdx.x; b < C; b += CS_WG) o[b] = h[b];
 }
 
-// per bucket: each workgroup's running offset within the bucket (in place), and the total.
-// 64 buckets per workgroup, 4 lanes per bucket: lane q sums a quarter of the histogram rows,
-// the quarters' sums are exchanged in LDS, then each lane writes its quarter's offsets.
-__global__ __launch_bounds__(256) void k_sb_colscan(uint32_t *hist, uint32_t nwg, uint32_t *total) {
+// per coarse bucket: each workgroup's running offset within the bucket (in place), and the
+// total.  64 buckets per workgroup, 4 lanes per bucket: lane q sums a quarter of the rows, the
+// quarters' sums are exchanged in LDS, then each lane writes its quarter's offsets.
+__global__ __launch_bounds__(256) void k_cs_colscan(uint32_t *hist, uint32_t nwg, uint32_t C, uint32_t *total) {
     __shared__ uint32_t part[4][64];
     const uint32_t lb = threadIdx.x & 63, qt = threadIdx.x >> 6, b = blockIdx.x * 64 + lb;
-    const uint32_t per = (nwg + 3) / 4, w0 = qt * per, w1 = w0 + per < nwg ? w0 + per : nwg;
+    const bool live = b < C;
+    const uint32_t per = (nwg + 3) / 4, w0 = qt * per < nwg ? qt * per : nwg, w1 = w0 + per < nwg ? w0 + per : nwg;
     uint32_t sum = 0;
-    for (uint32_t w = w0; w < w1; w += 8) {
-        uint32_t t[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) t[k] = w + k < w1 ? hist[(uint64_t)(w + k) * SB_N + b] : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; k++) sum += t[k];
-    }
+    if (live)
+        for (uint32_t w = w0; w < w1; w++) sum += hist[(uint64_t)w * C + b];
     part[qt][lb] = sum;
     __syncthreads();
     uint32_t run = 0;
     for (uint32_t q = 0; q < qt; q++) run += part[q][lb];
+    if (!live) return;
     if (qt == 3) total[b] = run + sum;
-    for (uint32_t w = w0; w < w1; w += 8) {
-        uint32_t t[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) t[k] = w + k < w1 ? hist[(uint64_t)(w + k) * SB_N + b] : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            if (w + k < w1) hist[(uint64_t)(w + k) * SB_N + b] = run;
-            run += t[k];
-        }
+    for (uint32_t w = w0; w < w1; w++) {
+        const uint32_t v = hist[(uint64_t)w * C + b];
+        hist[(uint64_t)w * C + b] = run;
+        run += v;
     }
 }
 
-// exclusive scan of the bucket totals (one workgroup of 1024, SB_N / 1024 buckets per lane)
-__global__ __launch_bounds__(1024) void k_sb_bucketscan(const uint32_t *total, uint32_t *start, uint32_t *flags) {
-    constexpr int PER = SB_N / 1024;
+// exclusive scan of the C bucket totals (one workgroup of 1024; C <= 4 * 1024); also folds the
+// minmax partials once into params = (min, shift) for the scatter and the bucket sorts
+__global__ __launch_bounds__(1024) void k_cs_bucketscan(const uint32_t *total, uint32_t C, uint32_t *start,
+                                                        uint32_t *flags, const uint64_t *part, uint32_t nwg,
+                                                        uint32_t bbits, uint64_t *params) {
     __shared__ uint32_t w[16];
-    const uint32_t t = threadIdx.x;
-    uint32_t v[PER], s = 0;
+    const uint32_t t = threadIdx.x, per = (C + 1023) / 1024;
+    uint64_t mn;
+    uint32_t sh;
+    cs_params(part, nwg, bbits, &mn, &sh);
+    if (t == 0) {
+        params[0] = mn;
+        params[1] = sh;
+    }
+    uint32_t v[4] = {0, 0, 0, 0}, s = 0;
     bool big = false;
 #pragma unroll
-    for (int k = 0; k < PER; k++) {
-        v[k] = total[PER * t + k];
-        big |= v[k] > (uint32_t)SB_CAP;
-        s += v[k];
+    for (uint32_t k = 0; k < 4; k++) {
+        if (k < per && per * t + k < C) {
+            v[k] = total[per * t + k];
+            big |= v[k] > (uint32_t)CS_CAP;
+            s += v[k];
+        }
     }
     uint32_t x = s;  // inclusive wave scan of the lane sums
 #pragma unroll
@@ -310,79 +321,162 @@ __global__ __launch_bounds__(1024) void k_sb_bucketscan(const uint32_t *total, u
     }
     if ((t & 63) == 63) w[t >> 6] = x;
     __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t q = 0; q < (t >> 6); q++) before += w[q];
-    uint32_t run = before + x - s;
+    uint32_t run = x - s;
+    for (uint32_t q = 0; q < (t >> 6); q++) run += w[q];
 #pragma unroll
-    for (int k = 0; k < PER; k++) {
-        start[PER * t + k] = run;
-        run += v[k];
+    for (uint32_t k = 0; k < 4; k++) {
+        if (k < per && per * t + k < C) {
+            start[per * t + k] = run;
+            run += v[k];
+        }
     }
     if (__ballot(big) && (t & 63) == 0) atomicOr(flags, 4u);
 }
 
 template <int KK, int KL>
-__global__ __launch_bounds__(256) void k_sb_scatter(const uint8_t *keys, uint64_t m, const uint64_t *part,
-                                                    uint32_t nwg, const uint32_t *hist, const uint32_t *start,
-                                                    uint64_t *odig, uint32_t *oidx) {
-    __shared__ uint32_t cur[SB_N];
-    uint64_t mn;
-    uint32_t shift;
-    sb_params(part, nwg, &mn, &shift);
-    const uint32_t *h = hist + (uint64_t)blockIdx.x * SB_N;
-    for (uint32_t b = threadIdx.x; b < SB_N; b += 256) cur[b] = start[b] + h[b];
+__global__ __launch_bounds__(CS_WG) void k_cs_scatter(const uint8_t *keys, uint64_t m, const uint64_t *params,
+                                                      uint32_t C, const uint32_t *hist, const uint32_t *start,
+                                                      uint64_t *odig, uint32_t *oidx) {
+    __shared__ uint32_t cur[CS_MAX_C];
+    const uint64_t mn = params[0], sh = params[1];
+    const uint32_t *h = hist + (uint64_t)blockIdx.x * C;
+    for (uint32_t b = threadIdx.x; b < C; b += CS_WG) cur[b] = start[b] + h[b];
     __syncthreads();
-    const uint64_t i0 = (uint64_t)blockIdx.x * SB_TILE;
-    for (uint32_t t = threadIdx.x; t < SB_TILE; t += 256) {
-        const uint64_t i = i0 + t;
+    const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
+    uint64_t d[CS_TILE / CS_WG];
+#pragma unroll
+    for (int k = 0; k < CS_TILE / CS_WG; k++) {
+        const uint64_t i = i0 + CS_WG * k + threadIdx.x;
+        d[k] = i < m ? key_digit<KK, KL>(keys + i * KL, 0) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < CS_TILE / CS_WG; k++) {
+        const uint64_t i = i0 + CS_WG * k + threadIdx.x;
         if (i < m) {
-            const uint64_t d = key_digit<KK, KL>(keys + i * KL, 0);
-            const uint32_t pos = atomicAdd(&cur[(uint32_t)((d - mn) >> shift)], 1u);
-            odig[pos] = d;
+            const uint32_t pos = atomicAdd(&cur[(uint32_t)((d[k] - mn) >> sh) >> CS_FINE_BITS], 1u);
+            odig[pos] = d[k];
             oidx[pos] = (uint32_t)i;
         }
     }
 }
 
-// one wave per bucket: order its (digit, index) pairs by rank counting in LDS, then gather
-// keys / fingerprints / ops into place and flag duplicates (1) and digit ties (2)
+// rows 256 (K0 + k) + lane, k < 4, of a bucket's sorted order: key / fingerprint / op from the
+// input rows sx[] into place
+template <int KL, int K0>
+__device__ __forceinline__ void cs_gather(const uint32_t *sx, uint32_t n, uint32_t s0, const uint8_t *keys,
+                                          const uint8_t *fps, const uint8_t *ops, uint8_t *skeys, uint8_t *sfps,
+                                          uint8_t *sops) {
+    static_assert(KL % 4 == 0, "keys: whole dwords");
+    const uint32_t t = threadIdx.x;
+    uint32_t kw[4][KL / 4], ov[4];
+    uint4 f0[4], f1[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t j = 256 * (K0 + k) + t;
+        const uint64_t src = j < n ? sx[j] : 0;  // row 0 stands in past n (not stored)
+#pragma unroll
+        for (int q = 0; q < KL / 4; q++) kw[k][q] = reinterpret_cast<const uint32_t *>(keys + src * KL)[q];
+        f0[k] = reinterpret_cast<const uint4 *>(fps + 32 * src)[0];
+        f1[k] = reinterpret_cast<const uint4 *>(fps + 32 * src)[1];
+        ov[k] = ops ? ops[src] : 0u;
+    }
+    // written out per row: a loop here is rotated into a variable trip count, which indexes the
+    // arrays dynamically and puts them in scratch memory
+    auto put = [&](int k, const uint32_t *w, uint4 a, uint4 b, uint32_t op) {
+        const uint32_t j = 256 * (K0 + k) + t;
+        if (j >= n) return;
+        const uint64_t o = (uint64_t)s0 + j;
+#pragma unroll
+        for (int q = 0; q < KL / 4; q++) reinterpret_cast<uint32_t *>(skeys + o * KL)[q] = w[q];
+        reinterpret_cast<uint4 *>(sfps + 32 * o)[0] = a;
+        reinterpret_cast<uint4 *>(sfps + 32 * o)[1] = b;
+        sops[o] = (uint8_t)op;
+    };
+    put(0, kw[0], f0[0], f1[0], ov[0]);
+    put(1, kw[1], f0[1], f1[1], ov[1]);
+    put(2, kw[2], f0[2], f1[2], ov[2]);
+    put(3, kw[3], f0[3], f1[3], ov[3]);
+}
+
+// one workgroup per coarse bucket (n <= CS_CAP keys, CS_CAP / 256 per lane, held in registers)
 template <int KK, int KL>
-__global__ __launch_bounds__(64) void k_sb_sort(const uint64_t *dig, const uint32_t *idx, const uint32_t *start,
-                                                 const uint32_t *total, const uint8_t *keys, const uint8_t *fps,
-                                                 const uint8_t *ops, uint8_t *skeys, uint8_t *sfps, uint8_t *sops,
-                                                 uint32_t *flags) {
-    constexpr int D = KK == KEY_BYTES ? KL / 8 : 1;
-    __shared__ uint64_t d[SB_CAP], sd[SB_CAP];
-    __shared__ uint32_t x[SB_CAP], sx[SB_CAP];
-    const uint32_t b = blockIdx.x, n = total[b], s0 = start[b];
-    if (n == 0 || n > (uint32_t)SB_CAP) return;  // too large: flagged by k_sb_bucketscan
-    for (uint32_t t = threadIdx.x; t < n; t += 64) {
-        d[t] = dig[s0 + t];
-        x[t] = idx[s0 + t];
+__global__ __launch_bounds__(256) void k_cs_sort(const uint64_t *dig, const uint32_t *idx, const uint32_t *start,
+                                                 const uint32_t *total, const uint64_t *params, const uint8_t *keys,
+                                                 const uint8_t *fps, const uint8_t *ops, uint8_t *skeys, uint8_t *sfps,
+                                                 uint8_t *sops, uint32_t *flags) {
+    constexpr int D = KK == KEY_BYTES ? KL / 8 : 1, PER = CS_CAP / 256;
+    static_assert(CS_FINE == 256, "one fine bucket per lane");
+    __shared__ uint64_t td[CS_CAP];
+    __shared__ uint32_t tx[CS_CAP], sx[CS_CAP];
+    __shared__ uint32_t fst[CS_FINE], fcur[CS_FINE], wsum[4];
+    const uint32_t b = blockIdx.x, t = threadIdx.x, n = total[b], s0 = start[b];
+    if (n == 0 || n > (uint32_t)CS_CAP) return;  // uniform; too large: flagged by k_cs_bucketscan
+    const uint64_t mn = params[0], sh = params[1];
+    uint64_t d[PER];
+    uint32_t x[PER], f[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t i = 256 * k + t;
+        d[k] = i < n ? dig[s0 + i] : 0;
+        x[k] = i < n ? idx[s0 + i] : 0;
+        f[k] = (uint32_t)((d[k] - mn) >> sh) & (CS_FINE - 1);
     }
+    fcur[t] = 0;
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < n; t += 64) {
-        const uint64_t di = d[t];
-        const uint32_t xi = x[t];
-        uint32_t r = 0;
-        for (uint32_t j = 0; j < n; j++) r += (d[j] < di || (d[j] == di && x[j] < xi)) ? 1u : 0u;
-        sd[r] = di;
-        sx[r] = xi;
+#pragma unroll
+    for (int k = 0; k < PER; k++)
+        if (256 * k + t < n) atomicAdd(&fcur[f[k]], 1u);
+    __syncthreads();
+    // exclusive scan of the fine counts, lane t holding bucket t
+    const uint32_t c = fcur[t];
+    uint32_t y = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t z = __shfl_up(y, o, 64);
+        if ((t & 63) >= (uint32_t)o) y += z;
     }
+    if ((t & 63) == 63) wsum[t >> 6] = y;
     __syncthreads();
-    uint32_t f = 0;
-    for (uint32_t t = threadIdx.x; t < n; t += 64) {
-        const uint64_t j = (uint64_t)s0 + t, src = sx[t];
-        copy_bytes<KL>(skeys + j * KL, keys + src * KL);
-        copy_bytes<32>(sfps + 32 * j, fps + 32 * src);
-        sops[j] = ops ? ops[src] : 0;
-        if (t > 0 && sd[t - 1] == sd[t]) {
-            if (D == 1 || key_cmp<KK, KL>(keys + (uint64_t)sx[t - 1] * KL, keys + src * KL) == 0) f |= 1u;
-            else f |= 2u;
+    uint32_t before = y - c;
+    for (uint32_t q = 0; q < (t >> 6); q++) before += wsum[q];
+    fst[t] = before;
+    fcur[t] = before;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        if (256 * k + t < n) {
+            const uint32_t p = atomicAdd(&fcur[f[k]], 1u);
+            td[p] = d[k];
+            tx[p] = x[k];
         }
     }
-    const unsigned long long any1 = __ballot((f & 1) != 0), any2 = __ballot((f & 2) != 0);
-    if (threadIdx.x == 0 && (any1 | any2)) atomicOr(flags, (any1 ? 1u : 0u) | (any2 ? 2u : 0u));
+    __syncthreads();
+    // fine bucket g spans [fst[g], fcur[g]); rank each key inside it by (digit, key, row)
+    bool dup = false;
+    for (uint32_t p = t; p < n; p += 256) {
+        const uint64_t dp = td[p];
+        const uint32_t xp = tx[p], g = (uint32_t)((dp - mn) >> sh) & (CS_FINE - 1);
+        const uint32_t lo = fst[g], hi = fcur[g];
+        uint32_t r = lo;
+        for (uint32_t q = lo; q < hi; q++) {
+            const uint64_t dq = td[q];
+            if (dq != dp) {
+                r += dq < dp ? 1u : 0u;
+            } else if (q != p) {
+                const uint32_t xq = tx[q];
+                const int cmp = D == 1 ? 0 : key_cmp<KK, KL>(keys + (uint64_t)xq * KL, keys + (uint64_t)xp * KL);
+                if (cmp == 0) dup = true;
+                r += (cmp < 0 || (cmp == 0 && xq < xp)) ? 1u : 0u;
+            }
+        }
+        sx[r] = xp;
+    }
+    __syncthreads();
+    // gather key / fingerprint / op of the sorted rows, 4 per lane at a time with all of the
+    // group's loads before its stores
+    cs_gather<KL, 0>(sx, n, s0, keys, fps, ops, skeys, sfps, sops);
+    if (n > 4 * 256) cs_gather<KL, 4>(sx, n, s0, keys, fps, ops, skeys, sfps, sops);
+    if (__ballot(dup) && (t & 63) == 0) atomicOr(flags, 1u);
 }
 
 // ---- search ---------------------------------------------------------------------------------
@@ -725,14 +819,17 @@ __device__ __forceinline__ uint64_t survivor_k(const uint32_t *rlist, uint64_t R
     return lo;
 }
 
-template <int KL, int P, bool COUNTS>
+template <int KK, int KL, int P, bool COUNTS>
 __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
                                                    const uint8_t *bkeys, const uint8_t *bpay, uint64_t m,
                                                    const uint32_t *upos, const uint32_t *usrc, const uint32_t *rlist,
                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay,
-                                                   uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk) {
+                                                   uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
+                                                   uint64_t *osmp, uint64_t *osmp2) {
     static_assert(P % 16 == 0 && P >= 32, "payload: a leading fingerprint, 16-byte units");
+    static_assert(MT % SMP_STRIDE == 0 && SMP_STRIDE % SMP2_STRIDE == 0, "whole sample strides per tile");
     __shared__ int32_t src[MT];  // A row, or -2 - batch row, or -1
+    __shared__ uint64_t smp_t[MT / SMP2_STRIDE];
     __shared__ uint64_t prm[6];
     __shared__ uint32_t wsum[4];
     __shared__ SumTile tile;
@@ -801,6 +898,9 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
             const uint4 *ps = reinterpret_cast<const uint4 *>((fromA ? apay : bpay) + r * P);
             const uint64_t od = o0 + o;
             copy_bytes<KL>(okeys + od * KL, ks);
+            // the merged run's search samples (k_sample's, without re-reading the run), staged in
+            // LDS and written as whole lines after the copy
+            if (osmp2 && (o % SMP2_STRIDE) == 0) smp_t[o / SMP2_STRIDE] = key_digit<KK, KL>(ks, 0);
             uint4 pv[P / 16];
 #pragma unroll
             for (int k = 0; k < P / 16; k++) pv[k] = ps[k];
@@ -834,6 +934,14 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
             if (t == 255 && blk < nbk) ocnt[blk] = before + y;
         }
     }
+    if (osmp2) {
+        __syncthreads();
+        constexpr uint32_t R = SMP_STRIDE / SMP2_STRIDE;
+        if (t < MT / SMP2_STRIDE && t * SMP2_STRIDE < nrows) {
+            osmp2[o0 / SMP2_STRIDE + t] = smp_t[t];
+            if (osmp && t % R == 0) osmp[o0 / SMP_STRIDE + t / R] = smp_t[t];
+        }
+    }
 }
 
 __global__ void k_last_i32(const int32_t *a, uint64_t n, int32_t *out) {
@@ -853,11 +961,12 @@ hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scrat
     return hipGetLastError();
 }
 
-template <int KL, int P, bool COUNTS>
+template <int KK, int KL, int P, bool COUNTS>
 hipError_t merge_run_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, const uint8_t *bkeys,
                        const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank, const uint8_t *present, uint64_t m,
                        Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb,
-                       uint64_t nbk, uint64_t *counts, uint64_t *out3, hipStream_t st) {
+                       uint64_t nbk, uint64_t *counts, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2,
+                       hipStream_t st) {
     hipError_t e;
     uint64_t *v = s.u64(3, m + 1), *ex = s.u64(4, m + 1);
     uint32_t *upos = s.u32(3, m + 1), *usrc = s.u32(4, m + 1), *rlist = s.u32(5, m + 1);
@@ -876,26 +985,29 @@ hipError_t merge_run_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, c
     hipLaunchKernelGGL(k_mcounts, dim3(1), dim3(64), 0, st, counts, out3);
     const uint64_t tiles = (nA + m + MT - 1) / MT;
     if (tiles)
-        hipLaunchKernelGGL((k_merge_run<KL, P, COUNTS>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys, apay, nA,
-                           bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk);
+        hipLaunchKernelGGL((k_merge_run<KK, KL, P, COUNTS>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys, apay,
+                           nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk, osmp,
+                           osmp2);
     return hipGetLastError();
 }
 
-hipError_t launch_merge_run(int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
+hipError_t launch_merge_run(int kk, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
                             const uint8_t *bkeys, const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank,
                             const uint8_t *present, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay,
                             uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *counts,
-                            uint64_t *out3, hipStream_t st) {
-#define RH_MR(KLV)                                                                                                 \
-    if (kl == KLV) {                                                                                               \
+                            uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+    if (osmp && !osmp2) return hipErrorInvalidValue;  // the stride-256 samples come from the stride-16 ones
+#define RH_MR(KKV, KLV)                                                                                            \
+    if (kk == KKV && kl == KLV) {                                                                                  \
         if (payload == 32)                                                                                         \
-            return merge_run_t<KLV, 32, false>(akeys, apay, nA, bkeys, bpay, bops, rank, present, m, s, okeys, opay, \
-                                               obs, ocnt, oinb, nbk, counts, out3, st);                            \
+            return merge_run_t<KKV, KLV, 32, false>(akeys, apay, nA, bkeys, bpay, bops, rank, present, m, s, okeys, \
+                                                    opay, obs, ocnt, oinb, nbk, counts, out3, osmp, osmp2, st);    \
         if (payload == (int)sizeof(DeltaRec))                                                                      \
-            return merge_run_t<KLV, sizeof(DeltaRec), true>(akeys, apay, nA, bkeys, bpay, bops, rank, present, m, s, \
-                                                            okeys, opay, obs, ocnt, oinb, nbk, counts, out3, st);  \
+            return merge_run_t<KKV, KLV, sizeof(DeltaRec), true>(akeys, apay, nA, bkeys, bpay, bops, rank, present, \
+                                                                 m, s, okeys, opay, obs, ocnt, oinb, nbk, counts,  \
+                                                                 out3, osmp, osmp2, st);                           \
     }
-    RH_MR(4) RH_MR(8) RH_MR(16) RH_MR(32)
+    RH_MR(KEY_U32, 4) RH_MR(KEY_U64, 8) RH_MR(KEY_BYTES, 8) RH_MR(KEY_BYTES, 16) RH_MR(KEY_BYTES, 32)
 #undef RH_MR
     return hipErrorInvalidValue;
 }
@@ -926,7 +1038,7 @@ struct KeyOps final : StoreKeyOps {
             std::swap(perm, perm2);
             return hipSuccess;
         };
-        if (!full && m <= SB_MAX_M) return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st);
+        if (!full && m <= CS_MAX_M) return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st);
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
         // multi-digit keys: the most significant digit alone orders random and spread keys
         // (k_gather reports a tie); the LSD sort (least significant digit first, stable passes)
@@ -941,19 +1053,22 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t sort_batch_buckets(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
                                   uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, hipStream_t st) {
-        const uint32_t nwg = (uint32_t)((m + SB_TILE - 1) / SB_TILE);
-        uint64_t *part = s.u64(2, 2ull * nwg), *dig = s.u64(0, m);
-        uint32_t *hist = s.u32(15, (uint64_t)nwg * SB_N), *idx = s.u32(0, m), *total = s.u32(1, SB_N);
-        uint32_t *start = s.u32(2, SB_N);
+        uint32_t cb = 0;
+        while ((1ull << cb) * 1024 < m) cb++;  // ~1,000 keys per coarse bucket
+        const uint32_t C = 1u << cb, nwg = (uint32_t)((m + CS_TILE - 1) / CS_TILE), bbits = cb + CS_FINE_BITS;
+        uint64_t *part = s.u64(2, 2ull * nwg + 2), *dig = s.u64(0, m);
+        uint32_t *hist = s.u32(15, (uint64_t)nwg * C), *idx = s.u32(0, m), *total = s.u32(1, C);
+        uint32_t *start = s.u32(2, C);
         if (s.err) return s.err;
-        hipLaunchKernelGGL((k_sb_minmax<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part);
-        hipLaunchKernelGGL((k_sb_hist<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part, nwg, hist);
-        hipLaunchKernelGGL(k_sb_colscan, dim3(SB_N / 64), dim3(256), 0, st, hist, nwg, total);
-        hipLaunchKernelGGL(k_sb_bucketscan, dim3(1), dim3(1024), 0, st, total, start, flags);
-        hipLaunchKernelGGL((k_sb_scatter<KK, KL>), dim3(nwg), dim3(256), 0, st, keys, m, part, nwg, hist, start, dig,
+        uint64_t *params = part + 2ull * nwg;
+        hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part);
+        hipLaunchKernelGGL((k_cs_hist<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, nwg, bbits, C, hist);
+        hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(256), 0, st, hist, nwg, C, total);
+        hipLaunchKernelGGL(k_cs_bucketscan, dim3(1), dim3(1024), 0, st, total, C, start, flags, part, nwg, bbits, params);
+        hipLaunchKernelGGL((k_cs_scatter<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, params, C, hist, start, dig,
                            idx);
-        hipLaunchKernelGGL((k_sb_sort<KK, KL>), dim3(SB_N), dim3(64), 0, st, dig, idx, start, total, keys, fps, ops,
-                           skeys, sfps, sops, flags);
+        hipLaunchKernelGGL((k_cs_sort<KK, KL>), dim3(C), dim3(256), 0, st, dig, idx, start, total, params, keys, fps,
+                           ops, skeys, sfps, sops, flags);
         return hipGetLastError();
     }
 

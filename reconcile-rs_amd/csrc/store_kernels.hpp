@@ -74,10 +74,11 @@ static_assert(sizeof(DeltaRec) == 48, "DeltaRec layout (16-byte multiple: rows a
 struct StoreKeyOps {
     virtual ~StoreKeyOps() = default;
     // sort a batch by key (stable) and gather keys / fingerprints / ops into key order.
-    // full = false: order by the most significant u64 digit only (a bucket pass + LDS sort),
-    // and *flags |= 2 if two keys share that digit, |= 4 if the digits are too skewed for the
-    // buckets (the order is then not final: sort again with full = true, the LSD radix over
-    // every digit).  *flags |= 1 if two batch keys are equal.
+    // full = false: coarse buckets of the most significant u64 digit + a sort of each bucket in
+    // LDS (ties on that digit broken by the whole key); *flags |= 4 if the digits are too skewed
+    // for the buckets, and (multi-digit keys past the bucket path's size) |= 2 if two keys share
+    // the digit: the order is then not final -- sort again with full = true, the LSD radix over
+    // every digit.  *flags |= 1 if two batch keys are equal.
     virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
                                   Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags,
                                   bool full, hipStream_t st) = 0;
@@ -112,13 +113,15 @@ struct CntPrefix {
 // the run and whether the run holds them) into a sorted run of (key, payload) rows, writing
 // the merged run, the 256-row block sums of the payload's leading fingerprint (nbk blocks:
 // rows past the merged length count as zero) and, for DeltaRec payloads, each block's
-// count-delta total (ocnt) and the rows' in-block count prefixes (oinb).
+// count-delta total (ocnt) and the rows' in-block count prefixes (oinb), and (optional) the
+// merged run's search samples: osmp / osmp2 = the leading digit of every 256th / 16th key
+// (osmp only with osmp2).
 // counts (device, 8): [0] inserts, [1] overwrites, [2] removals; out3 (optional) gets the same.
-hipError_t launch_merge_run(int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
+hipError_t launch_merge_run(int key_kind, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
                             const uint8_t *bkeys, const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank,
                             const uint8_t *present, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay,
                             uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *counts,
-                            uint64_t *out3, hipStream_t st);
+                            uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
 
 // in place: blk[b] <- Σ blk[0..b] (the inclusive block prefix); *total <- the last entry
 hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scratch &s, hipStream_t st);

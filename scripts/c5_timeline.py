@@ -1,0 +1,19 @@
+"""Per-batch kernel timeline of a config5 kernel trace (scripts/gpu_c5_trace.sh):
+python scripts/c5_timeline.py gpurun_out/c5t/c5_kernel_trace.csv [batch ...]"""
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+lifts = [i for i, r in enumerate(rows) if "k_lift<" in r["Kernel_Name"] and int(r["Grid_Size_X"]) < 2_000_000]
+batches = [int(b) for b in sys.argv[2:]] or [len(lifts) - 3]
+for b in batches:
+    i0, i1 = lifts[b], lifts[b + 1]
+    t0 = int(rows[i0]["Start_Timestamp"])
+    busy, prev = 0, t0
+    print(f"--- batch {b}: span {(int(rows[i1]['Start_Timestamp']) - t0) / 1e3:.1f} us")
+    for r in rows[i0:i1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        busy += e - s
+        print(f"{(s - t0) / 1e3:8.1f} gap {(s - prev) / 1e3:6.1f} dur {(e - s) / 1e3:7.1f}  {r['Kernel_Name'][:90]}")
+        prev = e
+    print(f"kernels {busy / 1e3:.1f} us, idle after the last {(int(rows[i1]['Start_Timestamp']) - prev) / 1e3:.1f} us")

@@ -547,6 +547,9 @@ struct rh_store {
     int cb = 0;
     DevBuf<uint8_t> bkeys[2], bfps[2], bsums, ssums;
     DevBuf<uint64_t> bsmp, bsmp2;  // leading digits of every 256th (16th) key: sampled search
+    DevBuf<uint32_t> btab;         // the base run's search table over bsmp2 (k_search_table)
+    DevBuf<uint64_t> btabp;
+    rh::SearchTable base_table() const { return rh::SearchTable{btab.p, btabp.p, rh::search_table_bits(nb)}; }
     DevBuf<uint64_t> dsmp[2], dsmp2[2];  // the same for each delta buffer (written by its merge)
     // delta run
     uint64_t nd = 0;
@@ -729,6 +732,8 @@ struct rh_store {
             return rc;
         if (nb) {
             if (!have_samples) RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, bsmp2.p, stream));
+            if ((rc = btab.ensure((1ull << rh::search_table_bits(nb)) + 2)) || (rc = btabp.ensure(2))) return rc;
+            RH_HIP(rh::launch_search_table(bsmp2.p, nb, btab.p, btabp.p, stream));
             if (!have_block_sums) RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
             RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
             RH_HIP(rh::launch_total(ssums.p, ns, tot.p, stream));
@@ -975,7 +980,8 @@ struct rh_store {
                                     sops.p, r_flags, full == 1, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 3. where each key is now: base and delta runs
-            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, skeys.p, m, rank_b, present_b, stream));
+            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, skeys.p, m, rank_b, present_b, stream,
+                                        base_table()));
             RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, skeys.p, m, rank_d, present_d,
                                         stream));
             // 4. the batch's delta records, merged into the delta run's other buffer
@@ -1057,7 +1063,8 @@ struct rh_store {
             (rc = q_merged.ensure(m)))
             return rc;
         RH_HIP(hipMemcpyAsync(q_keys.p, keys, m * kl, hipMemcpyHostToDevice, stream));
-        RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_keys.p, m, q_rank.p, nullptr, stream));
+        RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_keys.p, m, q_rank.p, nullptr, stream,
+                                    base_table()));
         if (nd) RH_HIP(kops->search(dkeys[cd].p, nd, q_keys.p, m, q_drank.p, nullptr, stream));
         RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, cnt_prefix(cd), m, q_merged.p, stream));
         RH_HIP(hipMemcpyAsync(out, q_merged.p, m * 8, hipMemcpyDeviceToHost, stream));
@@ -1091,7 +1098,9 @@ struct rh_store {
         memcpy(h + kb + r, ek, r);
         RH_HIP(hipMemcpyAsync(q_in.p, h, in_bytes, hipMemcpyHostToDevice, stream));
         uint64_t *d_lo = reinterpret_cast<uint64_t *>(q_res.p), *d_hi = d_lo + r, *d_agg = d_hi + r;
-        if (nb) RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_in.p, 2 * r, q_rank.p, nullptr, stream));
+        if (nb)
+            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_in.p, 2 * r, q_rank.p, nullptr, stream,
+                                        base_table()));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
         RH_HIP(rh::launch_resolve_bounds(q_rank.p, q_in.p + kb, q_in.p + kb + r, r, nb, d_lo, d_hi, stream));
         // an inverted segment (hi < lo) is clamped to the empty range: ZERO
@@ -1223,7 +1232,9 @@ struct rh_store {
         const rh::RoundIn din{d_sk, d_ek, d_skeys, d_ekeys, d_rem, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p};
         uint64_t *hdr = reinterpret_cast<uint64_t *>(r_out.p);
         const int sq = policy == RH_POLICY_SQRT_FAN_OUT;
-        if (n) RH_HIP(kops->search_sampled(bkeys[cb].p, n, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream));
+        if (n)
+            RH_HIP(kops->search_sampled(bkeys[cb].p, n, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
+                                        base_table()));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
         if (r <= rh::round_tiny_max()) {
             RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, out_p, stream));
@@ -1282,7 +1293,7 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
         }
-        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); mcnt.release();
+        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); btab.release(); btabp.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); mcnt.release();
         for (int k = 0; k < 2; k++) {
             dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release();
         }

@@ -532,15 +532,50 @@ __device__ __forceinline__ void sample_window(const uint64_t *smp, uint64_t ns, 
     }
 }
 
+// Search table over a run's stride-16 samples (the large base run): tab[h] = the first sample
+// whose digit is >= min + (h << shift), h in [0, 2^bits], with (min, shift) in par[0..1] and the
+// shift chosen from the samples' digit range so that ~4 samples fall in each bucket.  A key's
+// bucket then brackets its lower bound to one or two lines of samples at the cost of one table
+// line, where the stride-256 samples took a ~19-step binary search (the deeper steps missing the
+// caches once per query).
+__global__ void k_search_table(const uint64_t *smp2, uint64_t ns2, uint32_t bits, uint32_t *tab, uint64_t *par) {
+    const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = 1ull << bits;
+    if (h > nt) return;
+    const uint64_t dmin = smp2[0], range = smp2[ns2 - 1] - dmin;
+    const uint32_t rb = range ? 64u - (uint32_t)__clzll(range) : 0u, sh = rb > bits ? rb - bits : 0u;
+    if (h == 0) {
+        par[0] = dmin;
+        par[1] = sh;
+    }
+    uint64_t v = ~0ull;  // bucket h's first digit (saturating)
+    if (h < nt) {
+        const uint64_t off = sh < 64 ? h << sh : 0;
+        v = (h == 0 || (off >> sh) == h) && dmin + off >= dmin ? dmin + off : ~0ull;
+    }
+    tab[h] = h == nt ? (uint32_t)ns2 : (uint32_t)lower_bound_u64(smp2, 0, ns2, v);
+}
+
 template <int KK, int KL>
 __global__ void k_search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint64_t *smp2,
-                                 const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present) {
+                                 SearchTable tb, const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const uint8_t *key = q + j * KL;
     const uint64_t d = key_digit<KK, KL>(key, 0);
     uint64_t lo = 0, hi = n;
-    sample_window(smp, (n + SMP_STRIDE - 1) / SMP_STRIDE, SMP_STRIDE, d, lo, hi);
+    if (tb.tab) {
+        // samples in buckets below d's are < d, those from the next bucket on are > d: the lower
+        // bound among the samples lies in [tab[h], tab[h + 1]], the key's in the rows around them
+        const uint64_t dmin = tb.par[0], sh = tb.par[1], nt = 1ull << tb.bits;
+        uint64_t h = d < dmin ? 0 : (d - dmin) >> sh;
+        h = h < nt ? h : nt - 1;
+        const uint64_t a0 = tb.tab[h], a1 = tb.tab[h + 1];
+        lo = a0 ? (a0 - 1) * SMP2_STRIDE : 0;
+        hi = a1 * SMP2_STRIDE < n ? a1 * SMP2_STRIDE : n;
+        lo = lo < hi ? lo : hi;
+    } else {
+        sample_window(smp, (n + SMP_STRIDE - 1) / SMP_STRIDE, SMP_STRIDE, d, lo, hi);
+    }
     if (smp2) sample_window(smp2, (n + SMP2_STRIDE - 1) / SMP2_STRIDE, SMP2_STRIDE, d, lo, hi);
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
@@ -1088,9 +1123,11 @@ struct KeyOps final : StoreKeyOps {
     }
 
     hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint64_t *smp2,
-                              const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present, hipStream_t st) override {
+                              const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present, hipStream_t st,
+                              SearchTable tb) override {
         if (m == 0) return hipSuccess;
-        hipLaunchKernelGGL((k_search_sampled<KK, KL>), g1(m), dim3(256), 0, st, keys, n, smp, smp2, q, m, rank,
+        if (!smp2 || n == 0) tb = SearchTable{};
+        hipLaunchKernelGGL((k_search_sampled<KK, KL>), g1(m), dim3(256), 0, st, keys, n, smp, smp2, tb, q, m, rank,
                            present);
         return hipGetLastError();
     }
@@ -1186,6 +1223,21 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
                                  uint64_t n, uint64_t *lo, uint64_t *hi, hipStream_t st) {
     if (r == 0) return hipSuccess;
     hipLaunchKernelGGL(k_resolve_bounds, g1(r), dim3(256), 0, st, rank, skind, ekind, r, n, lo, hi);
+    return hipGetLastError();
+}
+
+uint32_t search_table_bits(uint64_t n) {
+    const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
+    uint32_t b = 0;
+    while ((1ull << b) * 4 < ns2 && b < 24) b++;  // ~4 samples per bucket
+    return b;
+}
+
+hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st) {
+    const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
+    if (ns2 == 0) return hipSuccess;
+    const uint32_t bits = search_table_bits(n);
+    hipLaunchKernelGGL(k_search_table, g1((1ull << bits) + 1), dim3(256), 0, st, smp2, ns2, bits, tab, par);
     return hipGetLastError();
 }
 

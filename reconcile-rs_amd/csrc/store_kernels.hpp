@@ -70,6 +70,16 @@ struct DeltaRec {
 };
 static_assert(sizeof(DeltaRec) == 48, "DeltaRec layout (16-byte multiple: rows are loaded as uint4)");
 
+// A run's search table (k_search_table): tab has 2^bits + 1 entries, par = (min digit, shift).
+struct SearchTable {
+    const uint32_t *tab = nullptr;
+    const uint64_t *par = nullptr;
+    uint32_t bits = 0;
+};
+// table size for a run of n rows, and its build from the run's stride-16 samples
+uint32_t search_table_bits(uint64_t n);
+hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st);
+
 // Key-type-specialised device operations of the store.
 struct StoreKeyOps {
     virtual ~StoreKeyOps() = default;
@@ -88,9 +98,10 @@ struct StoreKeyOps {
     // smp[s] = leading digit of keys[256 s] (ceil(n / 256) entries), smp2 (optional) the same
     // for every 16th key, and the lower-bound search through them (same results as search)
     virtual hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, uint64_t *smp2, hipStream_t st) = 0;
+    // (tb: the run's search table, which replaces the stride-256 level; needs smp2)
     virtual hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint64_t *smp2,
                                       const uint8_t *q, uint64_t m, uint32_t *rank, uint8_t *present,
-                                      hipStream_t st) = 0;
+                                      hipStream_t st, SearchTable tb = SearchTable{}) = 0;
     virtual hipError_t check_sorted(const uint8_t *keys, uint64_t n, uint32_t *bad, hipStream_t st) = 0;
     // keep the last row of every run of equal keys of a key-sorted run (a stable sort keeps
     // input order within a run, so this is "the last insert wins"); counts[0] = rows kept

@@ -558,6 +558,9 @@ struct rh_store {
     DevBuf<uint8_t> dkeys[2], dpay[2], dbsums[2], dssums[2];
     DevBuf<int32_t> dblk[2];  // inclusive block prefix of the count deltas
     DevBuf<int16_t> dinb[2];  // each row's inclusive count prefix inside its 256-row block
+    DevBuf<int32_t> dsblk[2];  // exclusive super-block prefix of the count deltas
+    DevBuf<int32_t> dscnt;     // k_delta_finish's per-super-block count totals
+    DevBuf<uint32_t> fin_ticket;
     DevBuf<uint64_t> mcnt;    // merge counters
     uint64_t compact_div = 8, compact_min = 65536, compactions = 0;
     // the whole-map fingerprint = base total + delta contribution total, kept on the host after
@@ -747,13 +750,17 @@ struct rh_store {
     // sums and block count totals, zero past the true row count, which only the device knows):
     // the inclusive block prefix of the count deltas (its last entry -> *total), the super-block
     // sums, and the contribution total -> fp_total.  No host round trip.
-    rh::CntPrefix cnt_prefix(int buf) const { return rh::CntPrefix{dblk[buf].p, dinb[buf].p}; }
+    rh::CntPrefix cnt_prefix(int buf) const { return rh::CntPrefix{dsblk[buf].p, dblk[buf].p, dinb[buf].p}; }
     int finish_delta_async(int buf, uint64_t n_max, int32_t *total, uint64_t *fp_total) {
-        const size_t nbk = rh_num_blocks(n_max), ns = rh_num_superblocks(n_max);
-        RH_HIP(rh::launch_count_prefix(dblk[buf].p, nbk, total, scratch, stream));
-        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        if (nbk) RH_HIP(rh::launch_reduce(dbsums[buf].p, nbk, dssums[buf].p, stream));
-        RH_HIP(rh::launch_total(dssums[buf].p, ns, fp_total, stream));
+        int rc;
+        const size_t nbk = rh_num_blocks(n_max), ns = rh_num_superblocks(n_max) + 1;
+        if ((rc = dsblk[buf].ensure(ns)) || (rc = dscnt.ensure(ns)) || (rc = dssums[buf].ensure(ns * 32))) return rc;
+        if (!fin_ticket.p) {
+            if ((rc = fin_ticket.ensure(1))) return rc;
+            RH_HIP(hipMemsetAsync(fin_ticket.p, 0, 4, stream));
+        }
+        RH_HIP(rh::launch_delta_finish(dbsums[buf].p, dblk[buf].p, nbk, dssums[buf].p, dscnt.p, dsblk[buf].p,
+                                       fin_ticket.p, total, fp_total, stream));
         return RH_OK;
     }
     // Replace the contents with m records.  Sorted, duplicate-free input is required unless
@@ -906,6 +913,7 @@ struct rh_store {
             if ((rc = dkeys[k].ensure(plan * kl + 64)) || (rc = dpay[k].ensure(plan * sizeof(rh::DeltaRec) + 64)) ||
                 (rc = dbsums[k].ensure(rh_num_blocks(plan) * 32 + 32)) ||
                 (rc = dssums[k].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
+                (rc = dsblk[k].ensure(rh_num_superblocks(plan) + 16)) || (rc = dscnt.ensure(rh_num_superblocks(plan) + 16)) ||
                 (rc = dblk[k].ensure(rh_num_blocks(plan) + 16)) || (rc = dinb[k].ensure(plan + 16)))
                 return rc;
         }
@@ -954,6 +962,7 @@ struct rh_store {
         if ((rc = dkeys[nxt].ensure(plan * kl + 64)) || (rc = dpay[nxt].ensure(plan * sizeof(rh::DeltaRec) + 64)) ||
             (rc = dbsums[nxt].ensure(rh_num_blocks(plan) * 32 + 32)) ||
             (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
+            (rc = dsblk[nxt].ensure(rh_num_superblocks(plan) + 16)) || (rc = dscnt.ensure(rh_num_superblocks(plan) + 16)) ||
             (rc = dblk[nxt].ensure(rh_num_blocks(plan) + 16)) || (rc = dinb[nxt].ensure(plan + 16)) ||
             (rc = dsmp[nxt].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp2[nxt].ensure(plan / 16 + 2)) ||
             (rc = dsmp[cd].ensure(1)) || (rc = dsmp2[cd].ensure(1)) || (rc = mcnt.ensure(8)))
@@ -1293,9 +1302,9 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
         }
-        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); btab.release(); btabp.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); mcnt.release();
+        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); btab.release(); btabp.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); dscnt.release(); fin_ticket.release(); mcnt.release();
         for (int k = 0; k < 2; k++) {
-            dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release();
+            dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release(); dsblk[k].release();
         }
         staging.release();
         lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); bpay.release();

@@ -728,11 +728,114 @@ __global__ void k_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base
     present[i] = in_b ? 1 : 0;
 }
 
-// Σ count deltas of delta rows [0, i]: the inclusive block prefix before i's block plus the
-// inclusive prefix inside it
+// Σ count deltas of delta rows [0, i]: the super-block prefix, the blocks before i's inside its
+// super-block, and the rows up to i inside its block
 __device__ __forceinline__ int64_t cnt_through(const CntPrefix &c, uint64_t i) {
     const uint64_t b = i / 256;
-    return (int64_t)(b ? c.blk[b - 1] : 0) + c.inb[i];
+    return (int64_t)c.sblk[b / 256] + ((b % 256) ? c.blk[b - 1] : 0) + c.inb[i];
+}
+
+// After a merge into a delta buffer (k_merge_run wrote its block sums and block count totals):
+// the count prefix's upper levels, the super-block sums and the run's totals in one launch of one
+// workgroup per super-block.
+//   blk[b]   block b's count-delta total -> the inclusive prefix inside b's super-block
+//   ssums[s] super-block s's contribution sum;  scnt[s] its count total
+// and the workgroup that finishes last: sblk[s] = Σ scnt[0..s), *total = Σ scnt, fp_total = Σ
+// ssums.  The hand-off to it: sc1 (agent) stores of ssums / scnt, each storing wave's vmcnt wait, a
+// barrier, one agent-scope ticket add per workgroup; the last one reads them with sc1 loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility, row 1).  *ticket is 0 on entry and on exit.
+__global__ __launch_bounds__(256) void k_delta_finish(const uint8_t *bsums, int32_t *blk, uint64_t nbk, uint8_t *ssums,
+                                                      int32_t *scnt, int32_t *sblk, uint32_t *ticket, int32_t *total,
+                                                      uint64_t *fp_total) {
+    __shared__ SumTile tile;
+    __shared__ uint64_t lds[4 * 8];
+    __shared__ int32_t wsum[4];
+    __shared__ uint32_t last;
+    const uint32_t t = threadIdx.x;
+    const uint64_t sb = blockIdx.x, b = sb * 256 + t;
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t c = 0;
+    if (b < nbk) {
+        fp_load(bsums + 32 * b, h);
+        c = blk[b];
+    }
+    uint32_t f[8];
+    block_sum_fps256(h, tile, f);  // on lane 0
+    int32_t y = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t z = __shfl_up(y, o, 64);
+        if ((t & 63) >= (uint32_t)o) y += z;
+    }
+    if ((t & 63) == 63) wsum[t >> 6] = y;
+    __syncthreads();
+    int32_t before = 0;
+    for (uint32_t w = 0; w < (t >> 6); w++) before += wsum[w];
+    if (b < nbk) blk[b] = before + y;
+    if (t == 0) {
+        uint64_t *o = reinterpret_cast<uint64_t *>(ssums + 32 * sb);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            __hip_atomic_store(o + q, (uint64_t)f[2 * q] | ((uint64_t)f[2 * q + 1] << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == 255) __hip_atomic_store(scnt + sb, before + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0)
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u
+                                                                                                              : 0u;
+    __syncthreads();
+    if (!last) return;  // uniform
+    const uint32_t ns = gridDim.x;
+    Acc a;
+    acc_zero(a);
+    for (uint32_t q = t; q < ns; q += 256) {
+        const uint64_t *p = reinterpret_cast<const uint64_t *>(ssums + 32ull * q);
+        uint32_t g[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t v = __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g[2 * k] = (uint32_t)v;
+            g[2 * k + 1] = (uint32_t)(v >> 32);
+        }
+        acc_add_fp(a, g);
+    }
+    acc_block_reduce<256>(a, lds, f);
+    if (t == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) fp_total[q] = (uint64_t)f[2 * q] | ((uint64_t)f[2 * q + 1] << 32);
+    }
+    // exclusive scan of the super-block counts: a contiguous chunk per lane
+    const uint32_t chunk = (ns + 255) / 256, q0 = t * chunk < ns ? t * chunk : ns,
+                   q1 = q0 + chunk < ns ? q0 + chunk : ns;
+    int32_t run = 0;
+    for (uint32_t q = q0; q < q1; q++) run += __hip_atomic_load(scnt + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t z = __shfl_up(x, o, 64);
+        if ((t & 63) >= (uint32_t)o) x += z;
+    }
+    __syncthreads();  // wsum reuse
+    if ((t & 63) == 63) wsum[t >> 6] = x;
+    __syncthreads();
+    int32_t pre = x - run;
+    for (uint32_t w = 0; w < (t >> 6); w++) pre += wsum[w];
+    for (uint32_t q = q0; q < q1; q++) {
+        sblk[q] = pre;
+        pre += __hip_atomic_load(scnt + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == 255) *total = pre;
+    if (t == 0) *ticket = 0u;
+}
+
+hipError_t launch_delta_finish(const uint8_t *bsums, int32_t *blk, uint64_t nbk, uint8_t *ssums, int32_t *scnt,
+                               int32_t *sblk, uint32_t *ticket, int32_t *total, uint64_t *fp_total, hipStream_t st) {
+    const uint64_t ns = nbk ? (nbk + 255) / 256 : 1;
+    hipLaunchKernelGGL(k_delta_finish, dim3((uint32_t)ns), dim3(256), 0, st, bsums, blk, nbk, ssums, scnt, sblk,
+                       ticket, total, fp_total);
+    return hipGetLastError();
 }
 
 // aggregate over a key range of the merged view = base part + delta part; the delta part's

@@ -113,12 +113,18 @@ struct StoreKeyOps {
     virtual int compare_keys_host(const uint8_t *a, const uint8_t *b) const = 0;
 };
 
-// Σ count deltas of delta rows [0, i] = blk[i / 256 - 1] (inclusive block prefix) + inb[i]
-// (inclusive prefix inside the row's 256-row block)
+// Σ count deltas of delta rows [0, i] = sblk[i / 65536] (exclusive super-block prefix)
+// + blk[i / 256 - 1] (inclusive block prefix inside the super-block; 0 for its first block)
+// + inb[i] (inclusive prefix inside the row's 256-row block)
 struct CntPrefix {
+    const int32_t *sblk;
     const int32_t *blk;
     const int16_t *inb;
 };
+// after a delta merge: blk -> in-super-block prefixes, super-block sums, sblk, the count and
+// contribution totals (one launch; scnt: ns scratch ints, *ticket 0 on entry and exit)
+hipError_t launch_delta_finish(const uint8_t *bsums, int32_t *blk, uint64_t nbk, uint8_t *ssums, int32_t *scnt,
+                               int32_t *sblk, uint32_t *ticket, int32_t *total, uint64_t *fp_total, hipStream_t st);
 
 // Merge a key-sorted batch (ops 0 upsert / 1 drop; rank / present: its keys' lower bounds in
 // the run and whether the run holds them) into a sorted run of (key, payload) rows, writing

@@ -12,12 +12,23 @@
 namespace rh {
 
 // fingerprint i of an array whose entries are `stride` bytes apart (32 for plain fingerprint
-// arrays; the store's delta records carry their 32-byte contribution first, stride 48)
+// arrays; the store's delta records carry their 32-byte contribution first, stride 40: 8-byte
+// aligned, so those are read as 8-byte words)
 __device__ __forceinline__ void load_fp(const uint8_t *src, uint64_t i, uint32_t f[8], uint32_t stride = 32) {
-    const uint4 *p = reinterpret_cast<const uint4 *>(src + (uint64_t)stride * i);
-    uint4 a = p[0], b = p[1];
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
-    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    if ((stride & 15) == 0) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(src + (uint64_t)stride * i);
+        uint4 a = p[0], b = p[1];
+        f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+        f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    } else {
+        const uint2 *p = reinterpret_cast<const uint2 *>(src + (uint64_t)stride * i);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint2 v = p[k];
+            f[2 * k] = v.x;
+            f[2 * k + 1] = v.y;
+        }
+    }
 }
 
 // ---- generic encoded-bytes lift -------------------------------------------------------------

@@ -773,7 +773,6 @@ struct rh_store {
         int rc;
         if ((rc = sops.ensure(m + 64)) || (rc = flag.ensure(4))) return rc;
         for (int full = 0; full < 2; full++) {
-            RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
             RH_HIP(kops->sort_batch(keys, fps, ops, m, scratch, okeys, ofps, sops.p, flag.p, full == 1, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             RH_HIP(hipMemcpyAsync(flags, flag.p, 4, hipMemcpyDeviceToHost, stream));
@@ -983,8 +982,8 @@ struct rh_store {
         uint64_t *host = res_host.data();
         uint32_t flags = 0;
         for (int full = 0; full < 2; full++) {
-            // 2. key order (+ duplicate / leading-digit-tie flags)
-            RH_HIP(hipMemsetAsync(results.p, 0, 96, stream));
+            // 2. key order (+ duplicate / leading-digit-tie flags; the sort zeroes them, and every
+            //    other word of the result block is written by a later kernel)
             RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, scratch, skeys.p, sfps.p,
                                     sops.p, r_flags, full == 1, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -993,15 +992,13 @@ struct rh_store {
                                         base_table()));
             RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, skeys.p, m, rank_d, present_d,
                                         stream));
-            // 4. the batch's delta records, merged into the delta run's other buffer
-            RH_HIP(rh::launch_delta_build(sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p, rank_d, present_d,
-                                          dpay[cd].p, bpay.p, dops.p, r_counts, scratch, stream));
-            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-            // (one pass: the merged run, its block sums and count prefixes)
-            RH_HIP(rh::launch_merge_run(schema.key_kind, (int)kl, sizeof(rh::DeltaRec), dkeys[cd].p, dpay[cd].p, nd,
-                                        skeys.p, bpay.p, dops.p, rank_d, present_d, m, scratch, dkeys[nxt].p,
-                                        dpay[nxt].p, dbsums[nxt].p, dblk[nxt].p, dinb[nxt].p, rh_num_blocks(n_max),
-                                        mcnt.p, r_merge, dsmp[nxt].p, dsmp2[nxt].p, stream));
+            // 4. the batch's delta records and counts, merged into the delta run's other buffer
+            //    (one pass: the merged run, its block sums, count prefixes and search samples)
+            RH_HIP(rh::launch_delta_apply(schema.key_kind, (int)kl, sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p,
+                                          rank_d, present_d, dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p, dops.p,
+                                          r_counts, scratch, dkeys[nxt].p, dpay[nxt].p, dbsums[nxt].p, dblk[nxt].p,
+                                          dinb[nxt].p, rh_num_blocks(n_max), mcnt.p, r_merge, dsmp[nxt].p,
+                                          dsmp2[nxt].p, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 5. count prefix, super sums and totals, then the one round trip
             if ((rc = finish_delta_async(nxt, n_max, r_total, results.p + 8))) return rc;

@@ -204,7 +204,8 @@ __device__ __forceinline__ void minmax_block(uint64_t &a, uint64_t &b, uint64_t 
 }
 
 template <int KK, int KL>
-__global__ __launch_bounds__(CS_WG) void k_cs_minmax(const uint8_t *keys, uint64_t m, uint64_t *part) {
+__global__ __launch_bounds__(CS_WG) void k_cs_minmax(const uint8_t *keys, uint64_t m, uint64_t *part, uint32_t *flags) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *flags = 0;  // the sort's first launch: no memset of its own
     __shared__ uint64_t lo[CS_WG / 64], hi[CS_WG / 64];
     uint64_t a = ~0ull, b = 0;
     const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
@@ -638,12 +639,17 @@ __global__ void k_bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key,
 // Build the batch's DeltaRecs (key order) from its fingerprints, what base and delta hold for
 // each key, and the op; dops: 0 = upsert into the delta run, 1 = drop the key's delta entry.
 // counts (vs the merged view): [0] new keys, [1] overwritten, [2] deleted.
-__global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
-                              const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
-                              const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
-                              uint32_t *part) {
+// part[6 g + k], workgroup g: k = 0 new, 1 overwritten, 2 deleted (vs the merged view), and for
+// the merge into the delta run 3 upserts (dops 0), 4 keys the run holds (present_d), 5 both
+constexpr int DB_PARTS = 6, DB_WG = 1024;  // 1,024-row workgroups: ~1,000 partials per 1 M batch
+
+__global__ __launch_bounds__(DB_WG) void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m,
+                                                     const uint32_t *rank_b, const uint8_t *present_b,
+                                                     const uint8_t *base_fps, const uint32_t *rank_d,
+                                                     const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay,
+                                                     uint8_t *dops, uint32_t *part) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool c_new = false, c_over = false, c_del = false;
+    bool c_new = false, c_over = false, c_del = false, c_up = false, c_pr = false;
     if (j < m) {
         const bool isdel = sops[j] != 0, in_b = present_b[j], in_d = present_d[j];
         bool was_live = in_b;
@@ -653,7 +659,6 @@ __global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
         DeltaRec r;
         r.flags = (in_b ? DeltaRec::IN_BASE : 0u);
         r.brank = rank_b[j];
-        r.pad[0] = r.pad[1] = 0;
         uint32_t cur[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (!isdel) {
             fp_load(sfps + 32 * j, cur);
@@ -665,50 +670,129 @@ __global__ void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t
         }
         fp_sub(cur, base, r.contrib);
         // deleting a key the base does not hold needs no entry (drop any delta entry it has)
-        dops[j] = (isdel && !in_b) ? 1 : 0;
+        const bool drop = isdel && !in_b;
+        dops[j] = drop ? 1 : 0;
+        c_up = !drop;
+        c_pr = in_d;
         reinterpret_cast<DeltaRec *>(bpay)[j] = r;
     }
     // per-workgroup counts (same-address atomics from every wave would serialise in L2);
-    // k_sum_parts3 adds them up
-    __shared__ uint32_t wc[4][3];
-    const unsigned long long bn = __ballot(c_new), bo = __ballot(c_over), bd = __ballot(c_del);
-    if ((threadIdx.x & 63) == 0) {
-        wc[threadIdx.x >> 6][0] = (uint32_t)__popcll(bn);
-        wc[threadIdx.x >> 6][1] = (uint32_t)__popcll(bo);
-        wc[threadIdx.x >> 6][2] = (uint32_t)__popcll(bd);
-    }
+    // k_delta_parts adds them up
+    __shared__ uint32_t wc[DB_WG / 64][DB_PARTS];
+    const unsigned long long b[DB_PARTS] = {__ballot(c_new), __ballot(c_over), __ballot(c_del), __ballot(c_up),
+                                            __ballot(c_pr), __ballot(c_up && c_pr)};
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < DB_PARTS; k++) wc[threadIdx.x >> 6][k] = (uint32_t)__popcll(b[k]);
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < DB_PARTS) {
         uint32_t t = 0;
         for (uint32_t w = 0; w < blockDim.x / 64; w++) t += wc[w][threadIdx.x];
-        part[3ull * blockIdx.x + threadIdx.x] = t;
+        part[(uint64_t)DB_PARTS * blockIdx.x + threadIdx.x] = t;
     }
 }
 
-// counts[k] = Σ_g part[3 g + k], one workgroup
-__global__ __launch_bounds__(1024) void k_sum_parts3(const uint32_t *part, uint64_t groups, uint64_t *counts) {
-    __shared__ unsigned long long w[16][3];
-    unsigned long long t[3] = {0, 0, 0};
-    for (uint64_t g = threadIdx.x; g < groups; g += blockDim.x) {
-        t[0] += part[3 * g];
-        t[1] += part[3 * g + 1];
-        t[2] += part[3 * g + 2];
-    }
+// one workgroup over the G = ceil(m / 1024) partials: the batch counts (counts3), the merge counts
+// (mcnt: [0] inserts, [1] overwrites, [2] removals, [3] upserts U, [4] present R; out3 the first
+// three) and each workgroup's exclusive (U, R) offsets for k_delta_lists (off[2 g], off[2 g + 1])
+__global__ __launch_bounds__(1024) void k_delta_parts(const uint32_t *part, uint64_t G, uint64_t *counts3,
+                                                      uint64_t *mcnt, uint64_t *out3, uint32_t *off) {
+    // counts are < 2^31 (the store's row limit): 32-bit sums throughout
+    __shared__ uint32_t w[16][DB_PARTS];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint64_t chunk = (G + 1023) / 1024, g0 = t * chunk < G ? t * chunk : G, g1 = g0 + chunk < G ? g0 + chunk : G;
+    uint32_t sum[DB_PARTS] = {0, 0, 0, 0, 0, 0};
+    for (uint64_t g = g0; g < g1; g++)
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
+        for (int k = 0; k < DB_PARTS; k++) sum[k] += part[DB_PARTS * g + k];
+    // U (3) and R (4): inclusive wave scans; the others: wave totals
+    uint32_t xu = sum[3], xr = sum[4];
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            const uint32_t lo = __shfl_xor((uint32_t)t[k], m, 64), hi = __shfl_xor((uint32_t)(t[k] >> 32), m, 64);
-            t[k] += ((unsigned long long)hi << 32) | lo;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t yu = __shfl_up(xu, o, 64), yr = __shfl_up(xr, o, 64);
+        if (lane >= (uint32_t)o) {
+            xu += yu;
+            xr += yr;
         }
-        if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6][k] = t[k];
+    }
+    uint32_t tot[DB_PARTS];
+#pragma unroll
+    for (int k = 0; k < DB_PARTS; k++) {
+        uint32_t v = k == 3 ? xu : k == 4 ? xr : sum[k];
+        if (k != 3 && k != 4) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        } else {
+            v = __shfl(v, 63, 64);
+        }
+        tot[k] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < DB_PARTS; k++) w[wv][k] = tot[k];
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
-        unsigned long long s = 0;
-        for (uint32_t q = 0; q < blockDim.x / 64; q++) s += w[q][threadIdx.x];
-        counts[threadIdx.x] = s;
+    uint32_t u = xu - sum[3], r = xr - sum[4];
+    for (uint32_t q = 0; q < wv; q++) {
+        u += w[q][3];
+        r += w[q][4];
     }
+    for (uint64_t g = g0; g < g1; g++) {
+        off[2 * g] = u;
+        off[2 * g + 1] = r;
+        u += part[DB_PARTS * g + 3];
+        r += part[DB_PARTS * g + 4];
+    }
+    if (t == 0) {
+        uint64_t T[DB_PARTS];
+#pragma unroll
+        for (int k = 0; k < DB_PARTS; k++) {
+            T[k] = 0;
+            for (uint32_t q = 0; q < 16; q++) T[k] += w[q][k];
+        }
+        counts3[0] = T[0];
+        counts3[1] = T[1];
+        counts3[2] = T[2];
+        const uint64_t U = T[3], R = T[4], ov = T[5];
+        mcnt[0] = U - ov;
+        mcnt[1] = ov;
+        mcnt[2] = R - ov;
+        mcnt[3] = U;
+        mcnt[4] = R;
+        if (out3) {
+            out3[0] = U - ov;
+            out3[1] = ov;
+            out3[2] = R - ov;
+        }
+    }
+}
+
+// the merge lists of k_mlists, from the workgroup offsets: upos / usrc for the upserts, rlist
+// for the batch keys the run holds
+__global__ __launch_bounds__(DB_WG) void k_delta_lists(const uint8_t *dops, const uint8_t *present,
+                                                       const uint32_t *rank, const uint32_t *off, uint64_t m,
+                                                       uint32_t *upos, uint32_t *usrc, uint32_t *rlist) {
+    __shared__ uint32_t wu[DB_WG / 64], wr[DB_WG / 64];
+    const uint64_t j = (uint64_t)blockIdx.x * DB_WG + threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const bool up = j < m && dops[j] == 0, pr = j < m && present[j] != 0;
+    const unsigned long long bu = __ballot(up), br = __ballot(pr);
+    const uint32_t lu = __builtin_amdgcn_mbcnt_hi((uint32_t)(bu >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bu, 0u));
+    const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(br >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)br, 0u));
+    if (lane == 0) {
+        wu[wv] = (uint32_t)__popcll(bu);
+        wr[wv] = (uint32_t)__popcll(br);
+    }
+    __syncthreads();
+    uint32_t U = off[2 * blockIdx.x] + lu, R = off[2 * blockIdx.x + 1] + lr;
+    for (uint32_t q = 0; q < wv; q++) {
+        U += wu[q];
+        R += wr[q];
+    }
+    if (up) {
+        upos[U] = rank[j] + U - R;
+        usrc[U] = (uint32_t)j;
+    }
+    if (pr) rlist[R] = rank[j];
 }
 
 // compaction input: cur fp = contrib + base fp, op = live ? upsert : delete, and the key's
@@ -957,6 +1041,17 @@ __device__ __forceinline__ uint64_t survivor_k(const uint32_t *rlist, uint64_t R
     return lo;
 }
 
+__device__ __forceinline__ void words_of(const uint4 &v, uint32_t *w) {
+    w[0] = v.x;
+    w[1] = v.y;
+    w[2] = v.z;
+    w[3] = v.w;
+}
+__device__ __forceinline__ void words_of(const uint2 &v, uint32_t *w) {
+    w[0] = v.x;
+    w[1] = v.y;
+}
+
 template <int KK, int KL, int P, bool COUNTS>
 __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
                                                    const uint8_t *bkeys, const uint8_t *bpay, uint64_t m,
@@ -964,7 +1059,9 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay,
                                                    uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
                                                    uint64_t *osmp, uint64_t *osmp2) {
-    static_assert(P % 16 == 0 && P >= 32, "payload: a leading fingerprint, 16-byte units");
+    static_assert(P % 8 == 0 && P >= 32, "payload: a leading fingerprint, 8-byte units");
+    using V = typename std::conditional<P % 16 == 0, uint4, uint2>::type;  // widest aligned unit
+    constexpr int NV = P / (int)sizeof(V);
     static_assert(MT % SMP_STRIDE == 0 && SMP_STRIDE % SMP2_STRIDE == 0, "whole sample strides per tile");
     __shared__ int32_t src[MT];  // A row, or -2 - batch row, or -1
     __shared__ uint64_t smp_t[MT / SMP2_STRIDE];
@@ -1033,22 +1130,26 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
             const bool fromA = sr >= 0;
             const uint64_t r = fromA ? (uint64_t)sr : (uint64_t)(-2 - sr);
             const uint8_t *ks = (fromA ? akeys : bkeys) + r * KL;
-            const uint4 *ps = reinterpret_cast<const uint4 *>((fromA ? apay : bpay) + r * P);
+            const V *ps = reinterpret_cast<const V *>((fromA ? apay : bpay) + r * P);
             const uint64_t od = o0 + o;
             copy_bytes<KL>(okeys + od * KL, ks);
             // the merged run's search samples (k_sample's, without re-reading the run), staged in
             // LDS and written as whole lines after the copy
             if (osmp2 && (o % SMP2_STRIDE) == 0) smp_t[o / SMP2_STRIDE] = key_digit<KK, KL>(ks, 0);
-            uint4 pv[P / 16];
+            V pv[NV];
 #pragma unroll
-            for (int k = 0; k < P / 16; k++) pv[k] = ps[k];
-            uint4 *pd = reinterpret_cast<uint4 *>(opay + od * P);
+            for (int k = 0; k < NV; k++) pv[k] = ps[k];
+            V *pd = reinterpret_cast<V *>(opay + od * P);
 #pragma unroll
-            for (int k = 0; k < P / 16; k++) pd[k] = pv[k];
-            h[0] = pv[0].x; h[1] = pv[0].y; h[2] = pv[0].z; h[3] = pv[0].w;
-            h[4] = pv[1].x; h[5] = pv[1].y; h[6] = pv[1].z; h[7] = pv[1].w;
+            for (int k = 0; k < NV; k++) pd[k] = pv[k];
+            uint32_t w[P / 4];
+#pragma unroll
+            for (int k = 0; k < NV; k++) words_of(pv[k], w + k * (int)(sizeof(V) / 4));
+#pragma unroll
+            for (int k = 0; k < 8; k++) h[k] = w[k];
             if constexpr (COUNTS) {
-                const uint32_t f = pv[2].y;  // DeltaRec::flags
+                static_assert(P == sizeof(DeltaRec), "delta payload");
+                const uint32_t f = w[9];  // DeltaRec::flags
                 c = ((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0);
             }
         }
@@ -1100,6 +1201,26 @@ hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scrat
 }
 
 template <int KK, int KL, int P, bool COUNTS>
+hipError_t merge_kernel_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, const uint8_t *bkeys,
+                          const uint8_t *bpay, uint64_t m, const uint32_t *upos, const uint32_t *usrc,
+                          const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
+                          int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+    const uint64_t tiles = (nA + m + MT - 1) / MT;
+    if (tiles)
+        hipLaunchKernelGGL((k_merge_run<KK, KL, P, COUNTS>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys, apay,
+                           nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk, osmp,
+                           osmp2);
+    return hipGetLastError();
+}
+
+// the merge kernel alone, for lists and counts made elsewhere (launch_delta_apply)
+hipError_t launch_merge_kernel(int kk, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
+                               const uint8_t *bkeys, const uint8_t *bpay, uint64_t m, const uint32_t *upos,
+                               const uint32_t *usrc, const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys,
+                               uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
+                               uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
+
+template <int KK, int KL, int P, bool COUNTS>
 hipError_t merge_run_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, const uint8_t *bkeys,
                        const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank, const uint8_t *present, uint64_t m,
                        Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb,
@@ -1121,12 +1242,29 @@ hipError_t merge_run_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, c
         if ((e = hipMemsetAsync(counts, 0, 5 * 8, st))) return e;
     }
     hipLaunchKernelGGL(k_mcounts, dim3(1), dim3(64), 0, st, counts, out3);
-    const uint64_t tiles = (nA + m + MT - 1) / MT;
-    if (tiles)
-        hipLaunchKernelGGL((k_merge_run<KK, KL, P, COUNTS>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys, apay,
-                           nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk, osmp,
-                           osmp2);
-    return hipGetLastError();
+    return merge_kernel_t<KK, KL, P, COUNTS>(akeys, apay, nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay,
+                                             obs, ocnt, oinb, nbk, osmp, osmp2, st);
+}
+
+hipError_t launch_merge_kernel(int kk, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
+                               const uint8_t *bkeys, const uint8_t *bpay, uint64_t m, const uint32_t *upos,
+                               const uint32_t *usrc, const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys,
+                               uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
+                               uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+    if (osmp && !osmp2) return hipErrorInvalidValue;
+#define RH_MK(KKV, KLV)                                                                                            \
+    if (kk == KKV && kl == KLV) {                                                                                  \
+        if (payload == 32)                                                                                         \
+            return merge_kernel_t<KKV, KLV, 32, false>(akeys, apay, nA, bkeys, bpay, m, upos, usrc, rlist, counts,  \
+                                                       okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2, st);        \
+        if (payload == (int)sizeof(DeltaRec))                                                                      \
+            return merge_kernel_t<KKV, KLV, sizeof(DeltaRec), true>(akeys, apay, nA, bkeys, bpay, m, upos, usrc,    \
+                                                                    rlist, counts, okeys, opay, obs, ocnt, oinb,   \
+                                                                    nbk, osmp, osmp2, st);                         \
+    }
+    RH_MK(KEY_U32, 4) RH_MK(KEY_U64, 8) RH_MK(KEY_BYTES, 8) RH_MK(KEY_BYTES, 16) RH_MK(KEY_BYTES, 32)
+#undef RH_MK
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_merge_run(int kk, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
@@ -1177,6 +1315,7 @@ struct KeyOps final : StoreKeyOps {
             return hipSuccess;
         };
         if (!full && m <= CS_MAX_M) return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st);
+        if ((e = hipMemsetAsync(flags, 0, 4, st))) return e;
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
         // multi-digit keys: the most significant digit alone orders random and spread keys
         // (k_gather reports a tie); the LSD sort (least significant digit first, stable passes)
@@ -1199,7 +1338,7 @@ struct KeyOps final : StoreKeyOps {
         uint32_t *start = s.u32(2, C);
         if (s.err) return s.err;
         uint64_t *params = part + 2ull * nwg;
-        hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part);
+        hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, flags);
         hipLaunchKernelGGL((k_cs_hist<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, nwg, bbits, C, hist);
         hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(256), 0, st, hist, nwg, C, total);
         hipLaunchKernelGGL(k_cs_bucketscan, dim3(1), dim3(1024), 0, st, total, C, start, flags, part, nwg, bbits, params);
@@ -1295,18 +1434,25 @@ StoreKeyOps *store_key_ops(int kk, int kl) {
 
 // ---- delta launchers (key-type independent) -------------------------------------------------
 
-hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
-                              const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
-                              const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
-                              uint64_t *counts, Scratch &s, hipStream_t st) {
-    if (m == 0) return hipMemsetAsync(counts, 0, 24, st);
-    const uint64_t groups = (m + 255) / 256;
-    uint32_t *part = s.u32(13, groups * 3);
+hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t *sops, uint64_t m,
+                              const uint32_t *rank_b, const uint8_t *present_b, const uint8_t *base_fps,
+                              const uint32_t *rank_d, const uint8_t *present_d, const uint8_t *dkeys,
+                              const uint8_t *dpay, uint64_t nd, const uint8_t *skeys, uint8_t *bpay, uint8_t *dops,
+                              uint64_t *counts3, Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
+                              int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *mcnt, uint64_t *out3,
+                              uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+    if (m == 0) return hipErrorInvalidValue;
+    const uint64_t G = (m + DB_WG - 1) / DB_WG;
+    uint32_t *part = s.u32(13, G * DB_PARTS), *off = s.u32(6, 2 * G);
+    uint32_t *upos = s.u32(3, m + 1), *usrc = s.u32(4, m + 1), *rlist = s.u32(5, m + 1);
     if (s.err) return s.err;
-    hipLaunchKernelGGL(k_delta_build, g1(m), dim3(256), 0, st, sfps, sops, m, rank_b, present_b, base_fps, rank_d,
-                       present_d, dpay, bpay, dops, part);
-    hipLaunchKernelGGL(k_sum_parts3, dim3(1), dim3(1024), 0, st, part, groups, counts);
-    return hipGetLastError();
+    hipLaunchKernelGGL(k_delta_build, dim3((uint32_t)G), dim3(DB_WG), 0, st, sfps, sops, m, rank_b, present_b,
+                       base_fps, rank_d, present_d, dpay, bpay, dops, part);
+    hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(1024), 0, st, part, G, counts3, mcnt, out3, off);
+    hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, dops, present_d, rank_d, off, m, upos,
+                       usrc, rlist);
+    return launch_merge_kernel(kk, kl, (int)sizeof(DeltaRec), dkeys, dpay, nd, skeys, bpay, m, upos, usrc, rlist, mcnt,
+                               okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2, st);
 }
 
 hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,

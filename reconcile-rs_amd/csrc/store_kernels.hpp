@@ -56,19 +56,20 @@ struct Scratch {
     }
 };
 
-// One entry of the store's delta run (48 B): what the batches since the last compaction did to
+// One entry of the store's delta run (40 B): what the batches since the last compaction did to
 // a key.  contrib = cur - base (mod 2^256); count delta = live - in_base.  brank is the key's
 // lower-bound rank in the base run: the base does not change until the next compaction, so it
 // locates the base fingerprint (cur = base_fps[brank] + contrib) and the key's slot in the
 // compaction merge without searching again.
-struct DeltaRec {
+// Rows are moved as five 8-byte words (no padding to 48: the delta merge and the compaction
+// move 56 instead of 64 bytes per row).
+struct alignas(8) DeltaRec {
     enum : uint32_t { IN_BASE = 1, LIVE = 2 };
     uint32_t contrib[8];
     uint32_t brank;
     uint32_t flags;
-    uint32_t pad[2];
 };
-static_assert(sizeof(DeltaRec) == 48, "DeltaRec layout (16-byte multiple: rows are loaded as uint4)");
+static_assert(sizeof(DeltaRec) == 40, "DeltaRec layout (k_merge_run reads flags as word 9)");
 
 // A run's search table (k_search_table): tab has 2^bits + 1 entries, par = (min digit, shift).
 struct SearchTable {
@@ -88,7 +89,8 @@ struct StoreKeyOps {
     // LDS (ties on that digit broken by the whole key); *flags |= 4 if the digits are too skewed
     // for the buckets, and (multi-digit keys past the bucket path's size) |= 2 if two keys share
     // the digit: the order is then not final -- sort again with full = true, the LSD radix over
-    // every digit.  *flags |= 1 if two batch keys are equal.
+    // every digit.  *flags |= 1 if two batch keys are equal.  *flags is zeroed first (in stream
+    // order) by the sort itself.
     virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
                                   Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags,
                                   bool full, hipStream_t st) = 0;
@@ -144,10 +146,17 @@ hipError_t launch_merge_run(int key_kind, int kl, int payload, const uint8_t *ak
 hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scratch &s, hipStream_t st);
 
 // delta-run kernels (store_kernels.hip)
-hipError_t launch_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m, const uint32_t *rank_b,
-                              const uint8_t *present_b, const uint8_t *base_fps, const uint32_t *rank_d,
-                              const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay, uint8_t *dops,
-                              uint64_t *counts, Scratch &s, hipStream_t st);
+// The batch path after the searches: the batch's DeltaRecs (from its sorted fingerprints / ops
+// and what base and delta hold for each key; dops 0 = upsert into the delta run, 1 = drop the
+// key's entry), its counts vs the merged view (counts3: new, overwritten, deleted), the merge
+// lists, and the merge into the delta run (launch_merge_run's outputs; mcnt as its counts).
+hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t *sops, uint64_t m,
+                              const uint32_t *rank_b, const uint8_t *present_b, const uint8_t *base_fps,
+                              const uint32_t *rank_d, const uint8_t *present_d, const uint8_t *dkeys,
+                              const uint8_t *dpay, uint64_t nd, const uint8_t *skeys, uint8_t *bpay, uint8_t *dops,
+                              uint64_t *counts3, Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
+                              int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *mcnt, uint64_t *out3,
+                              uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
 // compaction input from the delta run: cur fingerprints, ops (live ? upsert : delete) and each
 // key's place in the base (rank = brank, present = in_base) for the merge
 hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,

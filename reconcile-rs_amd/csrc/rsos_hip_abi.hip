@@ -862,23 +862,24 @@ struct rh_store {
         int rc;
         if (nd == 0) return RH_OK;
         if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64))) return rc;
-        uint32_t *crank = scratch.u32(14, nd);
-        uint8_t *cpres = scratch.u8(4, nd);
-        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        // every delta key's base slot is in its DeltaRec (brank): the merge needs no search
-        RH_HIP(rh::launch_delta_cur(dpay[cd].p, nd, bfps[cb].p, cfps.p, cops.p, crank, cpres, stream));
         const int nxt = 1 - cb;
         const uint64_t nbk = rh_num_blocks(nb + nd);
         if ((rc = bkeys[nxt].ensure((nb + nd) * kl + 64)) || (rc = bfps[nxt].ensure((nb + nd) * 32 + 64)) ||
             (rc = bsums.ensure(nbk * 32 + 32)) || (rc = mcnt.ensure(8)) || (rc = bsmp.ensure(nbk + 1)) ||
             (rc = bsmp2.ensure((nb + nd) / 16 + 2)))
             return rc;
-        // the merged base, its block sums and its search samples in one pass
-        RH_HIP(rh::launch_merge_run(schema.key_kind, (int)kl, 32, bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, cfps.p,
-                                    cops.p, crank, cpres, nd, scratch, bkeys[nxt].p, bfps[nxt].p, bsums.p, nullptr,
-                                    nullptr, nbk, mcnt.p, nullptr, bsmp.p, bsmp2.p, stream));
+        // every delta key's base slot is in its DeltaRec (brank): the merge needs no search; the
+        // merged base, its block sums and its search samples in one pass
+        RH_HIP(rh::launch_compact(schema.key_kind, (int)kl, bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, dpay[cd].p, nd,
+                                  scratch, cfps.p, cops.p, bkeys[nxt].p, bfps[nxt].p, bsums.p, nbk, mcnt.p, bsmp.p, bsmp2.p,
+                                  stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        uint64_t c[3];
+        try {
+            res_host.resize(12);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "pinned result buffer");
+        }
+        uint64_t *c = res_host.data();  // pinned: an asynchronous copy that sync() polls for
         RH_HIP(hipMemcpyAsync(c, mcnt.p, 24, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
         const uint64_t want = size();

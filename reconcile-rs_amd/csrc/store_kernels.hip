@@ -539,21 +539,33 @@ __device__ __forceinline__ void sample_window(const uint64_t *smp, uint64_t ns, 
 // bucket then brackets its lower bound to one or two lines of samples at the cost of one table
 // line, where the stride-256 samples took a ~19-step binary search (the deeper steps missing the
 // caches once per query).
+__device__ __forceinline__ void table_params(const uint64_t *smp2, uint64_t ns2, uint32_t bits, uint64_t &dmin,
+                                             uint32_t &sh) {
+    dmin = smp2[0];
+    const uint64_t range = smp2[ns2 - 1] - dmin;
+    const uint32_t rb = range ? 64u - (uint32_t)__clzll(range) : 0u;
+    sh = rb > bits ? rb - bits : 0u;
+}
+
+// built from the samples in one pass: sample s opens buckets (h(s - 1), h(s)] (h(-1) = -1), and
+// the last sample closes the rest; bucket h's value is the first sample at or above it
 __global__ void k_search_table(const uint64_t *smp2, uint64_t ns2, uint32_t bits, uint32_t *tab, uint64_t *par) {
-    const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = 1ull << bits;
-    if (h > nt) return;
-    const uint64_t dmin = smp2[0], range = smp2[ns2 - 1] - dmin;
-    const uint32_t rb = range ? 64u - (uint32_t)__clzll(range) : 0u, sh = rb > bits ? rb - bits : 0u;
-    if (h == 0) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = 1ull << bits;
+    if (s > ns2) return;
+    uint64_t dmin;
+    uint32_t sh;
+    table_params(smp2, ns2, bits, dmin, sh);
+    if (s == 0) {
         par[0] = dmin;
         par[1] = sh;
     }
-    uint64_t v = ~0ull;  // bucket h's first digit (saturating)
-    if (h < nt) {
-        const uint64_t off = sh < 64 ? h << sh : 0;
-        v = (h == 0 || (off >> sh) == h) && dmin + off >= dmin ? dmin + off : ~0ull;
-    }
-    tab[h] = h == nt ? (uint32_t)ns2 : (uint32_t)lower_bound_u64(smp2, 0, ns2, v);
+    // h(s) = the bucket of sample s's digit (samples are sorted, so h is non-decreasing)
+    auto h = [&](uint64_t q) -> uint64_t {
+        const uint64_t v = (smp2[q] - dmin) >> sh;
+        return v < nt ? v : nt - 1;
+    };
+    const uint64_t lo = s == 0 ? 0 : h(s - 1) + 1, hi = s == ns2 ? nt : h(s);
+    for (uint64_t b = lo; b <= hi && b <= nt; b++) tab[b] = (uint32_t)s;
 }
 
 template <int KK, int KL>
@@ -694,8 +706,9 @@ __global__ __launch_bounds__(DB_WG) void k_delta_build(const uint8_t *sfps, cons
 // one workgroup over the G = ceil(m / 1024) partials: the batch counts (counts3), the merge counts
 // (mcnt: [0] inserts, [1] overwrites, [2] removals, [3] upserts U, [4] present R; out3 the first
 // three) and each workgroup's exclusive (U, R) offsets for k_delta_lists (off[2 g], off[2 g + 1])
-__global__ __launch_bounds__(1024) void k_delta_parts(const uint32_t *part, uint64_t G, uint64_t *counts3,
-                                                      uint64_t *mcnt, uint64_t *out3, uint32_t *off) {
+__global__ __launch_bounds__(1024) void k_delta_parts(const uint32_t *__restrict__ part, uint64_t G,
+                                                      uint64_t *__restrict__ counts3, uint64_t *__restrict__ mcnt,
+                                                      uint64_t *__restrict__ out3, uint32_t *__restrict__ off) {
     // counts are < 2^31 (the store's row limit): 32-bit sums throughout
     __shared__ uint32_t w[16][DB_PARTS];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -749,9 +762,11 @@ __global__ __launch_bounds__(1024) void k_delta_parts(const uint32_t *part, uint
             T[k] = 0;
             for (uint32_t q = 0; q < 16; q++) T[k] += w[q][k];
         }
-        counts3[0] = T[0];
-        counts3[1] = T[1];
-        counts3[2] = T[2];
+        if (counts3) {
+            counts3[0] = T[0];
+            counts3[1] = T[1];
+            counts3[2] = T[2];
+        }
         const uint64_t U = T[3], R = T[4], ov = T[5];
         mcnt[0] = U - ov;
         mcnt[1] = ov;
@@ -796,20 +811,40 @@ __global__ __launch_bounds__(DB_WG) void k_delta_lists(const uint8_t *dops, cons
 }
 
 // compaction input: cur fp = contrib + base fp, op = live ? upsert : delete, and the key's
-// place in the base (no search: brank was recorded when the entry was built)
-__global__ void k_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
-                            uint32_t *rank, uint8_t *present) {
+// place in the base (no search: brank was recorded when the entry was built); plus the
+// per-1024-row partials of k_delta_parts (slots 3 upserts, 4 keys the base holds, 5 both)
+__global__ __launch_bounds__(DB_WG) void k_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps,
+                                                     uint8_t *fps, uint8_t *ops, uint32_t *rank, uint8_t *present,
+                                                     uint32_t *part) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
-    const bool in_b = (r.flags & DeltaRec::IN_BASE) != 0;
-    uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cur[8];
-    if (in_b) fp_load(base_fps + 32ull * r.brank, base);
-    fp_add(r.contrib, base, cur);
-    fp_store(fps + 32 * i, cur);
-    ops[i] = (r.flags & DeltaRec::LIVE) ? 0 : 1;
-    rank[i] = r.brank;
-    present[i] = in_b ? 1 : 0;
+    bool up = false, pr = false;
+    if (i < n) {
+        const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
+        const bool in_b = (r.flags & DeltaRec::IN_BASE) != 0;
+        uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cur[8];
+        if (in_b) fp_load(base_fps + 32ull * r.brank, base);
+        fp_add(r.contrib, base, cur);
+        fp_store(fps + 32 * i, cur);
+        up = (r.flags & DeltaRec::LIVE) != 0;
+        pr = in_b;
+        ops[i] = up ? 0 : 1;
+        rank[i] = r.brank;
+        present[i] = in_b ? 1 : 0;
+    }
+    __shared__ uint32_t wc[DB_WG / 64][3];
+    const unsigned long long bu = __ballot(up), br = __ballot(pr), bo = __ballot(up && pr);
+    if ((threadIdx.x & 63) == 0) {
+        wc[threadIdx.x >> 6][0] = (uint32_t)__popcll(bu);
+        wc[threadIdx.x >> 6][1] = (uint32_t)__popcll(br);
+        wc[threadIdx.x >> 6][2] = (uint32_t)__popcll(bo);
+    }
+    __syncthreads();
+    if (threadIdx.x < DB_PARTS) {
+        uint32_t t = 0;
+        if (threadIdx.x >= 3)
+            for (uint32_t w = 0; w < blockDim.x / 64; w++) t += wc[w][threadIdx.x - 3];
+        part[(uint64_t)DB_PARTS * blockIdx.x + threadIdx.x] = t;
+    }
 }
 
 // Σ count deltas of delta rows [0, i]: the super-block prefix, the blocks before i's inside its
@@ -1455,11 +1490,24 @@ hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t
                                okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2, st);
 }
 
-hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
-                            uint32_t *rank, uint8_t *present, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_delta_cur, g1(n), dim3(256), 0, st, dpay, n, base_fps, fps, ops, rank, present);
-    return hipGetLastError();
+hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *bfps, uint64_t nb, const uint8_t *dkeys,
+                          const uint8_t *dpay, uint64_t nd, Scratch &s, uint8_t *cfps, uint8_t *cops, uint8_t *okeys,
+                          uint8_t *ofps,
+                          uint8_t *obs, uint64_t nbk, uint64_t *mcnt, uint64_t *osmp, uint64_t *osmp2,
+                          hipStream_t st) {
+    if (nd == 0) return hipErrorInvalidValue;
+    const uint64_t G = (nd + DB_WG - 1) / DB_WG;
+    uint32_t *part = s.u32(13, G * DB_PARTS), *off = s.u32(6, 2 * G), *crank = s.u32(14, nd);
+    uint32_t *upos = s.u32(3, nd + 1), *usrc = s.u32(4, nd + 1), *rlist = s.u32(5, nd + 1);
+    uint8_t *cpres = s.u8(4, nd);
+    if (s.err) return s.err;
+    hipLaunchKernelGGL(k_delta_cur, dim3((uint32_t)G), dim3(DB_WG), 0, st, dpay, nd, bfps, cfps, cops, crank, cpres,
+                       part);
+    hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(1024), 0, st, part, G, nullptr, mcnt, nullptr, off);
+    hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, cops, cpres, crank, off, nd, upos, usrc,
+                       rlist);
+    return launch_merge_kernel(kk, kl, 32, bkeys, bfps, nb, dkeys, cfps, nd, upos, usrc, rlist, mcnt, okeys, ofps, obs,
+                               nullptr, nullptr, nbk, osmp, osmp2, st);
 }
 
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
@@ -1486,7 +1534,7 @@ hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, 
     const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
     if (ns2 == 0) return hipSuccess;
     const uint32_t bits = search_table_bits(n);
-    hipLaunchKernelGGL(k_search_table, g1((1ull << bits) + 1), dim3(256), 0, st, smp2, ns2, bits, tab, par);
+    hipLaunchKernelGGL(k_search_table, g1(ns2 + 1), dim3(256), 0, st, smp2, ns2, bits, tab, par);
     return hipGetLastError();
 }
 
@@ -1495,6 +1543,8 @@ hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch) {
     (void)s.u64(3, plan + 1), (void)s.u64(4, plan + 1);
     (void)s.u32(3, plan + 1), (void)s.u32(4, plan + 1), (void)s.u32(5, plan + 1);
     (void)s.u32(14, plan), (void)s.u8(4, plan);
+    const uint64_t G = (std::max(plan, batch) + DB_WG - 1) / DB_WG;  // launch_delta_apply / launch_compact partials
+    (void)s.u32(13, G * DB_PARTS), (void)s.u32(6, 2 * G);
     (void)s.u32(9, batch), (void)s.u32(10, batch), (void)s.u8(2, batch), (void)s.u8(3, batch);
     size_t t1 = 0, t2 = 0;
     hipError_t e;

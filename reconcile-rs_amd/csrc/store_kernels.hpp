@@ -157,10 +157,13 @@ hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t
                               uint64_t *counts3, Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
                               int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *mcnt, uint64_t *out3,
                               uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
-// compaction input from the delta run: cur fingerprints, ops (live ? upsert : delete) and each
-// key's place in the base (rank = brank, present = in_base) for the merge
-hipError_t launch_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
-                            uint32_t *rank, uint8_t *present, hipStream_t st);
+// The compaction: the delta run's current fingerprints (contrib + the base's at brank), ops and
+// base slots, the merge lists, and the merge of the delta run into the base run (keys, fps, block
+// sums, search samples; mcnt as launch_merge_run's counts).  cfps / cops: nd * 32 / nd bytes.
+hipError_t launch_compact(int key_kind, int kl, const uint8_t *bkeys, const uint8_t *bfps, uint64_t nb,
+                          const uint8_t *dkeys, const uint8_t *dpay, uint64_t nd, Scratch &s, uint8_t *cfps,
+                          uint8_t *cops, uint8_t *okeys, uint8_t *ofps, uint8_t *obs, uint64_t nbk, uint64_t *mcnt, uint64_t *osmp,
+                          uint64_t *osmp2, hipStream_t st);
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
                             const uint64_t *dhi, CntPrefix cp, uint64_t *out, hipStream_t st);
 hipError_t launch_rank_merge(const uint32_t *rank_b, const uint32_t *rank_d, CntPrefix cp, uint64_t m,

@@ -856,3 +856,57 @@ def test_host_tier_equals_device_answers(gpu, oracle_lib):
         probe()
     dev.close()
     tier.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,m", [("u32", 1), ("u32", 1025), ("u64", 8193), ("bytes16", 2), ("bytes16", 70_000),
+                                    ("bytes32", 8192), ("bytes16", 1_500_000)])
+def test_store_batch_sort_sizes(gpu, kind, m):
+    """The update batches' bucket sort (store_kernels.hip k_cs_*) across key kinds and the sizes
+    at its tile and bucket-count boundaries (1, 1,025 and 8,193 keys; 1.5 M keys = 2,048 coarse
+    buckets): a shuffled batch applied to an empty store leaves the fingerprints of the batch's
+    rows in key order -- the GPU lift of the key-sorted columns, sorted on the host."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema, lift_records
+    from rsos_hip.synth import make_records
+    s = RecordSchema.plain(kind, "u32" if kind == "u32" else "bytes64")  # schemas with a store lift kernel
+    cols = make_records(s, m, seed=71 + m, random_keys=True)
+    perm = torch.randperm(m, generator=torch.Generator().manual_seed(m)).cuda()
+    cols = {c: t[perm].contiguous() for c, t in cols.items()}  # integer keys come sorted
+    st = GpuFingerprintStore(s)
+    assert st.apply_device(cols) == (m, 0, 0)
+    keys = cols["keys"].cpu().numpy().reshape(m, -1)
+    if kind == "u32":
+        order = np.argsort(keys.copy().view(np.uint32).ravel(), kind="stable")
+    elif kind == "u64":
+        order = np.argsort(keys.copy().view(np.uint64).ravel(), kind="stable")
+    else:
+        order = np.lexsort(keys.T[::-1])
+    o = torch.from_numpy(order).cuda()
+    want = lift_records(s, {c: t[o].contiguous() for c, t in cols.items()}, block_sums=False)[0].cpu().numpy()
+    st.compact()
+    assert np.array_equal(st.fingerprints(), want)
+    st.close()
+
+
+@pytest.mark.gpu
+def test_store_batch_sort_duplicate_in_large_batch(gpu):
+    """A repeated key in a 1 M batch (bucket path, full-key ties inside a fine bucket) is refused
+    and the store is left as it was; the same keys with the duplicate's leading 8 bytes kept but
+    its last byte changed are accepted."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema, RsosHipError
+    from rsos_hip.synth import make_records
+    s = RecordSchema.plain("bytes16", "bytes64")
+    st = GpuFingerprintStore(s)
+    st.load_bulk_device(make_records(s, 100_000, seed=5))
+    before = st.aggregate()
+    b = make_records(s, 1_000_000, seed=6, random_keys=True)
+    b["keys"][777_777] = b["keys"][123]
+    with pytest.raises(RsosHipError):
+        st.apply_device(b)
+    assert st.aggregate() == before
+    b["keys"][777_777, 15] ^= 0x01  # same leading digit as row 123, different key
+    assert st.apply_device(b) == (1_000_000, 0, 0)
+    assert st.size() == 1_100_000
+    st.close()

@@ -267,13 +267,15 @@ __global__ __launch_bounds__(CS_WG) void k_cs_hist(const uint8_t *keys, uint64_t
 }
 
 // per coarse bucket: each workgroup's running offset within the bucket (in place), and the
-// total.  64 buckets per workgroup, 4 lanes per bucket: lane q sums a quarter of the rows, the
-// quarters' sums are exchanged in LDS, then each lane writes its quarter's offsets.
-__global__ __launch_bounds__(256) void k_cs_colscan(uint32_t *hist, uint32_t nwg, uint32_t C, uint32_t *total) {
-    __shared__ uint32_t part[4][64];
+// total.  64 buckets per workgroup (one per lane of a wave, so the row reads are coalesced),
+// 16 lanes per bucket: lane q sums a sixteenth of the rows, the parts' sums are exchanged in LDS,
+// then each lane writes its part's offsets.
+__global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nwg, uint32_t C, uint32_t *total) {
+    constexpr uint32_t Q = 16;
+    __shared__ uint32_t part[Q][64];
     const uint32_t lb = threadIdx.x & 63, qt = threadIdx.x >> 6, b = blockIdx.x * 64 + lb;
     const bool live = b < C;
-    const uint32_t per = (nwg + 3) / 4, w0 = qt * per < nwg ? qt * per : nwg, w1 = w0 + per < nwg ? w0 + per : nwg;
+    const uint32_t per = (nwg + Q - 1) / Q, w0 = qt * per < nwg ? qt * per : nwg, w1 = w0 + per < nwg ? w0 + per : nwg;
     uint32_t sum = 0;
     if (live)
         for (uint32_t w = w0; w < w1; w++) sum += hist[(uint64_t)w * C + b];
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(256) void k_cs_colscan(uint32_t *hist, uint32_t nwg
     uint32_t run = 0;
     for (uint32_t q = 0; q < qt; q++) run += part[q][lb];
     if (!live) return;
-    if (qt == 3) total[b] = run + sum;
+    if (qt == Q - 1) total[b] = run + sum;
     for (uint32_t w = w0; w < w1; w++) {
         const uint32_t v = hist[(uint64_t)w * C + b];
         hist[(uint64_t)w * C + b] = run;
@@ -1375,7 +1377,7 @@ struct KeyOps final : StoreKeyOps {
         uint64_t *params = part + 2ull * nwg;
         hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, flags);
         hipLaunchKernelGGL((k_cs_hist<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, nwg, bbits, C, hist);
-        hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(256), 0, st, hist, nwg, C, total);
+        hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(1024), 0, st, hist, nwg, C, total);
         hipLaunchKernelGGL(k_cs_bucketscan, dim3(1), dim3(1024), 0, st, total, C, start, flags, part, nwg, bbits, params);
         hipLaunchKernelGGL((k_cs_scatter<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, params, C, hist, start, dig,
                            idx);

@@ -33,29 +33,40 @@ def _nbytes(t: torch.Tensor) -> int:
     return t.numel() * t.element_size()
 
 
+_NEED: Dict[tuple, tuple] = {}  # per schema: (column, row width) of every required column
+
+
+def _need(schema: RecordSchema) -> tuple:
+    key = (schema.key_row, schema.value_row, bool(schema.dated_kind))
+    got = _NEED.get(key)
+    if got is None:
+        need = [("keys", schema.key_row), ("values", schema.value_row)]
+        if schema.dated_kind:
+            need += [("phys", 8), ("logical", 4), ("node", 8)]
+        got = _NEED[key] = tuple((c, w) for c, w in need if w)
+    return got
+
+
 def _check_cols(schema: RecordSchema, cols: Dict[str, torch.Tensor]) -> int:
+    """The row count, after checking every column the schema needs: present, a contiguous device
+    tensor, and exactly n rows of its width (the kernels index rows by n)."""
     for k in cols:
         if k not in COLS:
             raise ValueError(f"unknown column {k!r}")
     if schema.key_row:
-        n = _nbytes(cols["keys"]) // schema.key_row
+        n = cols["keys"].nbytes // schema.key_row
     else:
-        n = _nbytes(cols["values"]) // max(schema.value_row, 1)
-    need = {"keys": schema.key_row, "values": schema.value_row}
-    if schema.dated_kind:
-        need.update({"phys": 8, "logical": 4, "node": 8})
-    for name, width in need.items():
-        if width == 0:
-            continue
+        n = cols["values"].nbytes // max(schema.value_row, 1)
+    for name, width in _need(schema):
         t = cols.get(name)
         if t is None:
             raise ValueError(f"column {name!r} is required by {schema}")
         if not t.is_cuda or not t.is_contiguous():
             raise ValueError(f"column {name!r} must be a contiguous device tensor")
-        if _nbytes(t) != n * width:
-            raise ValueError(f"column {name!r} has {_nbytes(t)} bytes, expected {n} x {width}")
+        if t.nbytes != n * width:
+            raise ValueError(f"column {name!r} has {t.nbytes} bytes, expected {n} x {width}")
     t = cols.get("tags")
-    if t is not None and (_nbytes(t) != n or not t.is_cuda):
+    if t is not None and (t.nbytes != n or not t.is_cuda):
         raise ValueError("tags must be n device bytes")
     return n
 

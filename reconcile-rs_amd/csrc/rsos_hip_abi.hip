@@ -731,7 +731,7 @@ struct rh_store {
         int rc;
         const size_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
         if ((rc = bsums.ensure(nbk * 32 + 32)) || (rc = ssums.ensure(ns * 32 + 32)) || (rc = tot.ensure(4)) ||
-            (rc = bsmp.ensure(nbk + 1)) || (rc = bsmp2.ensure(nb / 16 + 2)))
+            (rc = bsmp.ensure(nbk + 1)) || (rc = bsmp2.ensure(rh::sample2_entries(nb))))
             return rc;
         if (nb) {
             if (!have_samples) RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, bsmp2.p, stream));
@@ -866,7 +866,7 @@ struct rh_store {
         const uint64_t nbk = rh_num_blocks(nb + nd);
         if ((rc = bkeys[nxt].ensure((nb + nd) * kl + 64)) || (rc = bfps[nxt].ensure((nb + nd) * 32 + 64)) ||
             (rc = bsums.ensure(nbk * 32 + 32)) || (rc = mcnt.ensure(8)) || (rc = bsmp.ensure(nbk + 1)) ||
-            (rc = bsmp2.ensure((nb + nd) / 16 + 2)))
+            (rc = bsmp2.ensure(rh::sample2_entries(nb + nd))))
             return rc;
         // every delta key's base slot is in its DeltaRec (brank): the merge needs no search; the
         // merged base, its block sums and its search samples in one pass
@@ -918,9 +918,9 @@ struct rh_store {
                 return rc;
         }
         if ((rc = bsums.ensure(rh_num_blocks(base) * 32 + 32)) || (rc = ssums.ensure(rh_num_superblocks(base) * 32 + 32)) ||
-            (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(base / 16 + 2)) ||
+            (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(rh::sample2_entries(base))) ||
             (rc = dsmp[0].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp[1].ensure(rh_num_blocks(plan) + 1)) ||
-            (rc = dsmp2[0].ensure(plan / 16 + 2)) || (rc = dsmp2[1].ensure(plan / 16 + 2)) ||
+            (rc = dsmp2[0].ensure(rh::sample2_entries(plan))) || (rc = dsmp2[1].ensure(rh::sample2_entries(plan))) ||
             (rc = cfps.ensure(plan * 32 + 64)) ||
             (rc = cops.ensure(plan + 64)) || (rc = lfps.ensure(batch * 32 + 64)) || (rc = skeys.ensure(batch * kl + 64)) ||
             (rc = sfps.ensure(batch * 32 + 64)) || (rc = sops.ensure(std::max(batch, base) + 64)) ||
@@ -964,7 +964,7 @@ struct rh_store {
             (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
             (rc = dsblk[nxt].ensure(rh_num_superblocks(plan) + 16)) || (rc = dscnt.ensure(rh_num_superblocks(plan) + 16)) ||
             (rc = dblk[nxt].ensure(rh_num_blocks(plan) + 16)) || (rc = dinb[nxt].ensure(plan + 16)) ||
-            (rc = dsmp[nxt].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp2[nxt].ensure(plan / 16 + 2)) ||
+            (rc = dsmp[nxt].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp2[nxt].ensure(rh::sample2_entries(plan))) ||
             (rc = dsmp[cd].ensure(1)) || (rc = dsmp2[cd].ensure(1)) || (rc = mcnt.ensure(8)))
             return rc;
         // one 96-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,

@@ -500,9 +500,12 @@ __global__ void k_search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint
 // among the samples bounds the key's rank to one stride-wide window (more when samples tie),
 // so a query touches the small, cache-resident sample array and then a few lines of one
 // window, instead of ~log2(n) scattered lines of the whole run.
-// A second level (every SMP2_STRIDE-th key; 8 B per 16 keys) narrows the window to a few
-// lines; it is built for the large, rarely rewritten base run.
-constexpr uint64_t SMP_STRIDE = 256, SMP2_STRIDE = 16;
+// A second level (every SMP2_STRIDE-th key; 8 B per 8 keys) narrows the window to one line of
+// 16-byte keys (the key lines are what a batch of searches pays for: 2.4 -> ~1.9 distinct lines
+// per query against a 100 M-row base).
+constexpr uint64_t SMP_STRIDE = 256, SMP2_STRIDE = 8;  // 8 x 16-byte keys = one 128-byte line
+
+uint64_t sample2_entries(uint64_t n) { return (n + SMP2_STRIDE - 1) / SMP2_STRIDE + 2; }
 
 template <int KK, int KL>
 __global__ void k_sample(const uint8_t *keys, uint64_t n, uint64_t stride, uint64_t *smp) {
@@ -1528,7 +1531,7 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
 uint32_t search_table_bits(uint64_t n) {
     const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
     uint32_t b = 0;
-    while ((1ull << b) * 4 < ns2 && b < 24) b++;  // ~4 samples per bucket
+    while ((1ull << b) * 8 < ns2 && b < 24) b++;  // ~8 samples (one line) per bucket
     return b;
 }
 

@@ -71,13 +71,15 @@ struct alignas(8) DeltaRec {
 };
 static_assert(sizeof(DeltaRec) == 40, "DeltaRec layout (k_merge_run reads flags as word 9)");
 
+// entries of a run's second-level (stride SMP2_STRIDE) sample array for n rows, with slack
+uint64_t sample2_entries(uint64_t n);
 // A run's search table (k_search_table): tab has 2^bits + 1 entries, par = (min digit, shift).
 struct SearchTable {
     const uint32_t *tab = nullptr;
     const uint64_t *par = nullptr;
     uint32_t bits = 0;
 };
-// table size for a run of n rows, and its build from the run's stride-16 samples
+// table size for a run of n rows, and its build from the run's second-level samples
 uint32_t search_table_bits(uint64_t n);
 hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st);
 
@@ -98,7 +100,7 @@ struct StoreKeyOps {
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;
     // smp[s] = leading digit of keys[256 s] (ceil(n / 256) entries), smp2 (optional) the same
-    // for every 16th key, and the lower-bound search through them (same results as search)
+    // for every 8th key, and the lower-bound search through them (same results as search)
     virtual hipError_t sample(const uint8_t *keys, uint64_t n, uint64_t *smp, uint64_t *smp2, hipStream_t st) = 0;
     // (tb: the run's search table, which replaces the stride-256 level; needs smp2)
     virtual hipError_t search_sampled(const uint8_t *keys, uint64_t n, const uint64_t *smp, const uint64_t *smp2,

@@ -910,3 +910,51 @@ def test_store_batch_sort_duplicate_in_large_batch(gpu):
     assert st.apply_device(b) == (1_000_000, 0, 0)
     assert st.size() == 1_100_000
     st.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["clustered", "narrow", "tiny"])
+def test_store_device_ranks_skewed_keys(gpu, layout):
+    """The base run's searches (bucket table over the second-level samples, then one sample line
+    and one key line) on key sets whose leading 8 bytes are far from uniform: three clusters of
+    equal leading digits plus outliers at both ends ("clustered"), every key inside a range of
+    2^20 digits ("narrow"), and a 5-row store ("tiny").  Device ranks of present and absent
+    keys equal numpy's searchsorted over the sorted keys, before and after a batch that lands
+    in the delta run."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    s = RecordSchema.plain("bytes16", "bytes64")
+    rng = np.random.default_rng(97)
+    if layout == "clustered":
+        heads = np.array([[0x10] * 8, [0x80] + [0] * 7, [0x80] + [0] * 6 + [1]], np.uint8)
+        keys = np.concatenate([heads[rng.integers(0, 3, 200_000)], rng.integers(0, 256, (200_000, 8), dtype=np.uint8)],
+                              axis=1)
+        keys = np.concatenate([keys, np.array([[0] * 16, [255] * 16], np.uint8)])
+    elif layout == "narrow":
+        d = (np.uint64(0x123456789ABC0000) + rng.integers(0, 1 << 20, 300_000).astype(np.uint64)).astype(">u8")
+        keys = np.concatenate([d.view(np.uint8).reshape(-1, 8), rng.integers(0, 256, (300_000, 8), dtype=np.uint8)],
+                              axis=1)
+    else:
+        keys = rng.integers(0, 256, (5, 16), dtype=np.uint8)
+    keys = np.unique(keys.view("V16"), axis=0).view(np.uint8).reshape(-1, 16)  # sorted by memcmp
+    vals = rng.integers(0, 256, (len(keys), 64), dtype=np.uint8)
+    st = GpuFingerprintStore(s, host_tier=False)
+    st.load_bulk({"keys": keys, "values": vals})
+
+    def check(all_keys):
+        sk = np.unique(all_keys.view("V16"), axis=0)
+        probes = np.concatenate([all_keys[rng.integers(0, len(all_keys), 500)],
+                                 rng.integers(0, 256, (300, 16), dtype=np.uint8),
+                                 all_keys[rng.integers(0, len(all_keys), 200)] ^ np.eye(16, dtype=np.uint8)[15],
+                                 np.array([[0] * 16, [255] * 16, [0x80] + [0] * 15], np.uint8)])
+        want = np.searchsorted(sk.ravel(), probes.view("V16").ravel(), side="left")
+        assert np.array_equal(st.ranks(np.ascontiguousarray(probes)), want)
+
+    check(keys)
+    extra = rng.integers(0, 256, (1000, 16), dtype=np.uint8)
+    extra[:500, :8] = keys[rng.integers(0, len(keys), 500), :8]  # same leading digits as base keys
+    extra = np.unique(extra.view("V16"), axis=0).view(np.uint8).reshape(-1, 16)
+    extra = extra[~np.isin(extra.view("V16").ravel(), keys.view("V16").ravel())]
+    st.apply({"keys": extra, "values": rng.integers(0, 256, (len(extra), 64), dtype=np.uint8)},
+             np.zeros(len(extra), np.uint8))
+    check(np.concatenate([keys, extra]))
+    st.close()

@@ -332,10 +332,11 @@ __global__ __launch_bounds__(256) void k_reduce(const uint8_t *in, uint32_t stri
     if (threadIdx.x == 0) store_sum(out, blockIdx.x, f);
 }
 
-__device__ __forceinline__ void acc_span(Acc &a, const uint8_t *src, uint64_t lo, uint64_t hi, uint32_t stride = 32) {
+__device__ __forceinline__ void acc_span(Acc &a, const uint8_t *src, uint64_t lo, uint64_t hi, uint32_t stride = 32,
+                                         const uint32_t *slots = nullptr) {
     for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         uint32_t f[8];
-        load_fp(src, i, f, stride);
+        load_fp(src, slots ? slots[i] : i, f, stride);  // slots: entry i lives at src[slots[i]]
         acc_add_fp(a, f);
     }
 }
@@ -359,8 +360,8 @@ __global__ __launch_bounds__(256) void k_total(const uint8_t *in, uint64_t n, ui
 // One workgroup per query.  [lo, hi) = head rows + whole blocks + tail rows, the whole blocks
 // = head blocks + whole super-blocks + tail blocks.  Each thread sums at most a few hundred
 // entries into carry-save u64 limbs, then one block reduction.
-__global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
-                                                     const uint8_t *ssums, uint64_t n,
+__global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, uint32_t stride, const uint32_t *slots,
+                                                     const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                                                      const uint64_t *qlo, const uint64_t *qhi,
                                                      uint64_t r, uint64_t *out) {
     __shared__ uint64_t lds[4 * 8];
@@ -374,10 +375,10 @@ __global__ __launch_bounds__(256) void k_range_query(const uint8_t *fps, uint32_
     const uint64_t B = 256, S = 65536;
     const uint64_t b1 = (lo + B - 1) / B, b2 = hi / B;  // whole blocks [b1, b2)
     if (b1 >= b2 || bsums == nullptr) {
-        acc_span(a, fps, lo, hi, stride);
+        acc_span(a, fps, lo, hi, stride, slots);
     } else {
-        acc_span(a, fps, lo, b1 * B, stride);
-        acc_span(a, fps, b2 * B, hi, stride);
+        acc_span(a, fps, lo, b1 * B, stride, slots);
+        acc_span(a, fps, b2 * B, hi, stride, slots);
         const uint64_t s1 = (b1 + B - 1) / B, s2 = b2 / B;  // whole super-blocks [s1, s2)
         if (s1 >= s2 || ssums == nullptr) {
             acc_span(a, bsums, b1, b2);
@@ -949,14 +950,15 @@ hipError_t launch_lift_fixed(const uint8_t *bytes, uint64_t len, uint64_t n, uin
 
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
-                              hipStream_t st, uint32_t stride) {
+                              hipStream_t st, uint32_t stride, const uint32_t *slots) {
     if (r == 0) return hipSuccess;
-    if (bsums && ssums && r >= 64) {  // many queries: one wave each
+    if (bsums && ssums && r >= 64 && !slots) {  // many queries: one wave each
         hipLaunchKernelGGL(k_range_query_wave, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, fps, stride, bsums,
                            ssums, n, lo, hi, r, out);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_range_query, dim3((uint32_t)r), dim3(256), 0, st, fps, stride, bsums, ssums, n, lo, hi, r, out);
+    hipLaunchKernelGGL(k_range_query, dim3((uint32_t)r), dim3(256), 0, st, fps, stride, slots, bsums, ssums, n, lo, hi,
+                       r, out);
     return hipGetLastError();
 }
 

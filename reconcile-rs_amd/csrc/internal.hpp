@@ -33,9 +33,10 @@ hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, c
 // (src[k] & ~2^63) + r - start[k] of `newf` if src[k] has bit 63 set, else of `old`
 hipError_t launch_seg_copy(const uint8_t *old, const uint8_t *newf, const uint64_t *start, const uint64_t *src,
                            uint64_t nseg, uint64_t n_out, uint8_t *out, hipStream_t st);
+// slots (optional): row i's entry is fps + stride * slots[i] (the store's delta records live in a heap)
 hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const uint8_t *ssums, uint64_t n,
                               const uint64_t *lo, const uint64_t *hi, uint64_t r, uint64_t *out,
-                              hipStream_t st, uint32_t stride = 32);
+                              hipStream_t st, uint32_t stride = 32, const uint32_t *slots = nullptr);
 
 // One rbsr protocol round's output, read back in one copy: a 64-byte header (u64 skipped,
 // enumerated, split, children, dropped), then the children (start kinds, end kinds, start keys,

@@ -555,7 +555,10 @@ struct rh_store {
     uint64_t nd = 0;
     int cd = 0;
     int64_t dtotal = 0;  // Σ count deltas
-    DevBuf<uint8_t> dkeys[2], dpay[2], dbsums[2], dssums[2];
+    DevBuf<uint8_t> dkeys[2], dbsums[2], dssums[2];
+    DevBuf<uint32_t> dslot[2];  // the delta rows' record slots in dheap
+    DevBuf<uint8_t> dheap;      // DeltaRecs, appended per batch (slots heap_len ..), emptied by compaction
+    uint64_t heap_len = 0;
     DevBuf<int32_t> dblk[2];  // inclusive block prefix of the count deltas
     DevBuf<int16_t> dinb[2];  // each row's inclusive count prefix inside its 256-row block
     DevBuf<int32_t> dsblk[2];  // exclusive super-block prefix of the count deltas
@@ -569,7 +572,7 @@ struct rh_store {
     DevBuf<uint64_t> tot;
     // batch scratch
     DevColumns staging;
-    DevBuf<uint8_t> lfps, skeys, sfps, sops, hops, bpay, dops, cfps, cops;
+    DevBuf<uint8_t> lfps, skeys, sfps, sops, hops, dops, cfps, cops;
     DevBuf<uint64_t> counts, results;
     DevBuf<uint32_t> flag;
     // query scratch
@@ -587,6 +590,7 @@ struct rh_store {
         (void)hipStreamSynchronize(stream);
         (void)hipGetLastError();
         nb = nd = 0;
+        heap_len = 0;
         dtotal = 0;
         memset(root_b, 0, sizeof root_b);
         memset(root_d, 0, sizeof root_d);
@@ -807,6 +811,7 @@ struct rh_store {
             (rc = counts.ensure(4)))
             return rc;
         nd = 0;
+        heap_len = 0;
         dtotal = 0;
         nb = 0;
         memset(root_d, 0, sizeof root_d);
@@ -870,7 +875,7 @@ struct rh_store {
             return rc;
         // every delta key's base slot is in its DeltaRec (brank): the merge needs no search; the
         // merged base, its block sums and its search samples in one pass
-        RH_HIP(rh::launch_compact(schema.key_kind, (int)kl, bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, dpay[cd].p, nd,
+        RH_HIP(rh::launch_compact(schema.key_kind, (int)kl, bkeys[cb].p, bfps[cb].p, nb, dkeys[cd].p, dslot[cd].p, dheap.p, nd,
                                   scratch, cfps.p, cops.p, bkeys[nxt].p, bfps[nxt].p, bsums.p, nbk, mcnt.p, bsmp.p, bsmp2.p,
                                   stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -886,6 +891,7 @@ struct rh_store {
         cb = nxt;
         nb = nb + c[0] - c[2];
         nd = 0;
+        heap_len = 0;
         dtotal = 0;
         memset(root_d, 0, sizeof root_d);
         compactions++;
@@ -910,7 +916,7 @@ struct rh_store {
             } else if ((rc = bkeys[k].ensure(base * kl + 64)) || (rc = bfps[k].ensure(base * 32 + 64))) {
                 return rc;
             }
-            if ((rc = dkeys[k].ensure(plan * kl + 64)) || (rc = dpay[k].ensure(plan * sizeof(rh::DeltaRec) + 64)) ||
+            if ((rc = dkeys[k].ensure(plan * kl + 64)) || (rc = dslot[k].ensure(plan + 16)) ||
                 (rc = dbsums[k].ensure(rh_num_blocks(plan) * 32 + 32)) ||
                 (rc = dssums[k].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
                 (rc = dsblk[k].ensure(rh_num_superblocks(plan) + 16)) || (rc = dscnt.ensure(rh_num_superblocks(plan) + 16)) ||
@@ -924,7 +930,7 @@ struct rh_store {
             (rc = cfps.ensure(plan * 32 + 64)) ||
             (rc = cops.ensure(plan + 64)) || (rc = lfps.ensure(batch * 32 + 64)) || (rc = skeys.ensure(batch * kl + 64)) ||
             (rc = sfps.ensure(batch * 32 + 64)) || (rc = sops.ensure(std::max(batch, base) + 64)) ||
-            (rc = bpay.ensure(batch * sizeof(rh::DeltaRec) + 64)) || (rc = dops.ensure(batch + 64)) ||
+            (rc = dheap.ensure(plan * sizeof(rh::DeltaRec) + 64)) || (rc = dops.ensure(batch + 64)) ||
             (rc = mcnt.ensure(8)) || (rc = results.ensure(12)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
         RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch));
@@ -941,7 +947,7 @@ struct rh_store {
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
         if ((rc = lfps.ensure(m * 32 + 64)) || (rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) ||
-            (rc = sops.ensure(m + 64)) || (rc = bpay.ensure(m * sizeof(rh::DeltaRec) + 64)) ||
+            (rc = sops.ensure(m + 64)) ||
             (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
         // 1. lift the batch (delete rows are lifted too and ignored)
@@ -959,7 +965,10 @@ struct rh_store {
         // run grows without reallocations (a hipFree drains the device)
         const uint64_t thresh = std::max<uint64_t>(nb / compact_div, compact_min);
         const uint64_t plan = std::max<uint64_t>(n_max, std::min<uint64_t>(thresh, nb + nd) + m);
-        if ((rc = dkeys[nxt].ensure(plan * kl + 64)) || (rc = dpay[nxt].ensure(plan * sizeof(rh::DeltaRec) + 64)) ||
+        // the heap keeps its records (the live delta rows point into it) when it grows
+        if ((rc = dheap.grow_keep((heap_len + m) * sizeof(rh::DeltaRec) + 64, heap_len * sizeof(rh::DeltaRec), stream)))
+            return rc;
+        if ((rc = dkeys[nxt].ensure(plan * kl + 64)) || (rc = dslot[nxt].ensure(plan + 16)) ||
             (rc = dbsums[nxt].ensure(rh_num_blocks(plan) * 32 + 32)) ||
             (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
             (rc = dsblk[nxt].ensure(rh_num_superblocks(plan) + 16)) || (rc = dscnt.ensure(rh_num_superblocks(plan) + 16)) ||
@@ -996,8 +1005,8 @@ struct rh_store {
             // 4. the batch's delta records and counts, merged into the delta run's other buffer
             //    (one pass: the merged run, its block sums, count prefixes and search samples)
             RH_HIP(rh::launch_delta_apply(schema.key_kind, (int)kl, sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p,
-                                          rank_d, present_d, dkeys[cd].p, dpay[cd].p, nd, skeys.p, bpay.p, dops.p,
-                                          r_counts, scratch, dkeys[nxt].p, dpay[nxt].p, dbsums[nxt].p, dblk[nxt].p,
+                                          rank_d, present_d, dkeys[cd].p, dslot[cd].p, nd, dheap.p, heap_len, skeys.p,
+                                          dops.p, r_counts, scratch, dkeys[nxt].p, dslot[nxt].p, dbsums[nxt].p, dblk[nxt].p,
                                           dinb[nxt].p, rh_num_blocks(n_max), mcnt.p, r_merge, dsmp[nxt].p,
                                           dsmp2[nxt].p, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -1020,9 +1029,12 @@ struct rh_store {
         }
         cd = nxt;
         nd = nd + c2[0] - c2[2];
+        heap_len += m;
         dtotal = total;
         memcpy(root_d, &host[8], sizeof root_d);
-        if (nd > std::max<uint64_t>(nb / compact_div, compact_min)) return compact();
+        // the heap also holds records no row points to any more (overwritten or dropped keys)
+        const uint64_t thresh_now = std::max<uint64_t>(nb / compact_div, compact_min);
+        if (nd > thresh_now || heap_len > thresh_now) return compact();
         return RH_OK;
     }
     int query(const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {  // rank ranges
@@ -1056,8 +1068,9 @@ struct rh_store {
                                       reinterpret_cast<uint64_t *>(res), stream));
         if (nd) {
             RH_HIP(kops->bounds(dkeys[cd].p, nd, q_keys.p, lo_kind, q_keys.p + kl, hi_kind, q_dlo.p, q_dhi.p, stream));
-            RH_HIP(rh::launch_range_query(dpay[cd].p, dbsums[cd].p, dssums[cd].p, nd, q_dlo.p, q_dhi.p, 1,
-                                          reinterpret_cast<uint64_t *>(q_dout.p), stream, sizeof(rh::DeltaRec)));
+            RH_HIP(rh::launch_range_query(dheap.p, dbsums[cd].p, dssums[cd].p, nd, q_dlo.p, q_dhi.p, 1,
+                                          reinterpret_cast<uint64_t *>(q_dout.p), stream, sizeof(rh::DeltaRec),
+                                          dslot[cd].p));
             RH_HIP(rh::launch_agg_merge(reinterpret_cast<uint64_t *>(q_bout.p), reinterpret_cast<uint64_t *>(q_dout.p),
                                         q_dlo.p, q_dhi.p, cnt_prefix(cd), reinterpret_cast<uint64_t *>(q_out.p), stream));
         }
@@ -1298,14 +1311,14 @@ struct rh_store {
     void release() {
         (void)hipStreamSynchronize(stream);
         for (int k = 0; k < 2; k++) {
-            bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dpay[k].release();
+            bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dslot[k].release();
         }
         bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); btab.release(); btabp.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); dscnt.release(); fin_ticket.release(); mcnt.release();
         for (int k = 0; k < 2; k++) {
             dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release(); dsblk[k].release();
         }
         staging.release();
-        lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); bpay.release();
+        lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); dheap.release(); heap_len = 0;
         dops.release(); cfps.release(); cops.release(); counts.release(); flag.release();
         results.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();

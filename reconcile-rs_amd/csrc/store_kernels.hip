@@ -663,14 +663,15 @@ constexpr int DB_PARTS = 6, DB_WG = 1024;  // 1,024-row workgroups: ~1,000 parti
 __global__ __launch_bounds__(DB_WG) void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m,
                                                      const uint32_t *rank_b, const uint8_t *present_b,
                                                      const uint8_t *base_fps, const uint32_t *rank_d,
-                                                     const uint8_t *present_d, const uint8_t *dpay, uint8_t *bpay,
-                                                     uint8_t *dops, uint32_t *part) {
+                                                     const uint8_t *present_d, const uint32_t *dslot,
+                                                     const uint8_t *heap, uint8_t *bpay, uint8_t *dops,
+                                                     uint32_t *part) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool c_new = false, c_over = false, c_del = false, c_up = false, c_pr = false;
     if (j < m) {
         const bool isdel = sops[j] != 0, in_b = present_b[j], in_d = present_d[j];
         bool was_live = in_b;
-        if (in_d) was_live = (reinterpret_cast<const DeltaRec *>(dpay)[rank_d[j]].flags & DeltaRec::LIVE) != 0;
+        if (in_d) was_live = (reinterpret_cast<const DeltaRec *>(heap)[dslot[rank_d[j]]].flags & DeltaRec::LIVE) != 0;
         uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (in_b) fp_load(base_fps + 32ull * rank_b[j], base);
         DeltaRec r;
@@ -786,7 +787,7 @@ __global__ __launch_bounds__(1024) void k_delta_parts(const uint32_t *__restrict
     }
 }
 
-// the merge lists of k_mlists, from the workgroup offsets: upos / usrc for the upserts, rlist
+// the merge lists from the workgroup offsets: upos / usrc for the upserts, rlist
 // for the batch keys the run holds
 __global__ __launch_bounds__(DB_WG) void k_delta_lists(const uint8_t *dops, const uint8_t *present,
                                                        const uint32_t *rank, const uint32_t *off, uint64_t m,
@@ -818,13 +819,13 @@ __global__ __launch_bounds__(DB_WG) void k_delta_lists(const uint8_t *dops, cons
 // compaction input: cur fp = contrib + base fp, op = live ? upsert : delete, and the key's
 // place in the base (no search: brank was recorded when the entry was built); plus the
 // per-1024-row partials of k_delta_parts (slots 3 upserts, 4 keys the base holds, 5 both)
-__global__ __launch_bounds__(DB_WG) void k_delta_cur(const uint8_t *dpay, uint64_t n, const uint8_t *base_fps,
-                                                     uint8_t *fps, uint8_t *ops, uint32_t *rank, uint8_t *present,
-                                                     uint32_t *part) {
+__global__ __launch_bounds__(DB_WG) void k_delta_cur(const uint32_t *dslot, const uint8_t *heap, uint64_t n,
+                                                     const uint8_t *base_fps, uint8_t *fps, uint8_t *ops,
+                                                     uint32_t *rank, uint8_t *present, uint32_t *part) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool up = false, pr = false;
     if (i < n) {
-        const DeltaRec &r = reinterpret_cast<const DeltaRec *>(dpay)[i];
+        const DeltaRec &r = reinterpret_cast<const DeltaRec *>(heap)[dslot[i]];
         const bool in_b = (r.flags & DeltaRec::IN_BASE) != 0;
         uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cur[8];
         if (in_b) fp_load(base_fps + 32ull * r.brank, base);
@@ -1018,57 +1019,14 @@ __global__ void k_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *
 //   an upsert u lands at    pos_u = rank + U_before - R_before
 //   (U: upserts, R: batch keys present in A -- overwritten or dropped A rows), and the A rows
 //   that survive fill the remaining output slots in order.
-// k_mclass / exclusive scan / k_mlists list the upserts' positions and the removed A ranks;
-// k_merge_run then owns MT output rows per workgroup: it marks the upserts' slots, fills the
+// k_delta_parts / k_delta_lists list the upserts' positions and the removed A ranks (from
+// per-1,024-row counts and one scan of them); k_merge_run then owns MT output rows per workgroup: it marks the upserts' slots, fills the
 // free slots with A survivors (the q-th survivor is A row s + k, k = #removed ranks before it,
 // found by a binary search over rank - index), copies each row once, and emits the 256-row
 // block sums of the payload's leading fingerprint -- and, for the delta run, each block's
 // count-delta total and every row's in-block count prefix.  This replaces a row-move pass, a
 // batch-scatter pass and a re-read of the whole run for its sums.
 constexpr int MT = 1024;  // output rows per workgroup (4 blocks of 256)
-
-// up (op 0) in the high word, present in the low word; zeroes the overwrite counter
-__global__ void k_mclass(const uint8_t *ops, const uint8_t *present, uint64_t m, uint64_t *v, uint64_t *counts) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j == 0) counts[1] = 0;
-    if (j < m) v[j] = ((uint64_t)(ops[j] == 0 ? 1u : 0u) << 32) | (present[j] ? 1u : 0u);
-}
-
-// counts: [1] overwrites (upsert of a present key), [3] upserts, [4] present
-__global__ void k_mlists(const uint8_t *ops, const uint8_t *present, const uint32_t *rank, const uint64_t *ex,
-                         uint64_t m, uint32_t *upos, uint32_t *usrc, uint32_t *rlist, uint64_t *counts) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool ovr = false;
-    if (j < m) {
-        const bool up = ops[j] == 0, pr = present[j] != 0;
-        const uint32_t U = (uint32_t)(ex[j] >> 32), R = (uint32_t)ex[j];
-        if (up) {
-            upos[U] = rank[j] + U - R;
-            usrc[U] = (uint32_t)j;
-        }
-        if (pr) rlist[R] = rank[j];
-        ovr = up && pr;
-        if (j == m - 1) {
-            counts[3] = U + (up ? 1u : 0u);
-            counts[4] = R + (pr ? 1u : 0u);
-        }
-    }
-    const unsigned long long b = __ballot(ovr);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(reinterpret_cast<unsigned long long *>(counts + 1), (unsigned long long)__popcll(b));
-}
-
-// counts[0] inserts, [2] removals (ins / ovr / del of the merge); also into out3 if given
-__global__ void k_mcounts(uint64_t *counts, uint64_t *out3) {
-    if (threadIdx.x != 0) return;
-    const uint64_t ovr = counts[1];
-    counts[0] = counts[3] - ovr;
-    counts[2] = counts[4] - ovr;
-    if (out3) {
-        out3[0] = counts[0];
-        out3[1] = ovr;
-        out3[2] = counts[2];
-    }
-}
 
 // smallest k in [lo, hi] with k == R or rlist[k] - k > s: the number of removed A rows before
 // the s-th survivor
@@ -1092,16 +1050,20 @@ __device__ __forceinline__ void words_of(const uint2 &v, uint32_t *w) {
     w[1] = v.y;
 }
 
-template <int KK, int KL, int P, bool COUNTS>
+// HEAP (the delta run): a row's payload is the 4-byte slot of its DeltaRec in the record heap
+// (A rows: apay; batch row j: heap_base + j); the block sums and count prefixes are formed from
+// the records gathered through the slots, and only key + slot are moved.
+template <int KK, int KL, int P, bool COUNTS, bool HEAP>
 __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
                                                    const uint8_t *bkeys, const uint8_t *bpay, uint64_t m,
                                                    const uint32_t *upos, const uint32_t *usrc, const uint32_t *rlist,
                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay,
                                                    uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
-                                                   uint64_t *osmp, uint64_t *osmp2) {
-    static_assert(P % 8 == 0 && P >= 32, "payload: a leading fingerprint, 8-byte units");
+                                                   uint64_t *osmp, uint64_t *osmp2, const uint8_t *heap,
+                                                   uint32_t heap_base) {
+    static_assert(HEAP ? (P == 4 && COUNTS) : (P % 8 == 0 && P >= 32), "payload: a slot, or a leading fingerprint");
     using V = typename std::conditional<P % 16 == 0, uint4, uint2>::type;  // widest aligned unit
-    constexpr int NV = P / (int)sizeof(V);
+    constexpr int NV = P / (int)sizeof(V) > 0 ? P / (int)sizeof(V) : 1;
     static_assert(MT % SMP_STRIDE == 0 && SMP_STRIDE % SMP2_STRIDE == 0, "whole sample strides per tile");
     __shared__ int32_t src[MT];  // A row, or -2 - batch row, or -1
     __shared__ uint64_t smp_t[MT / SMP2_STRIDE];
@@ -1170,27 +1132,40 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
             const bool fromA = sr >= 0;
             const uint64_t r = fromA ? (uint64_t)sr : (uint64_t)(-2 - sr);
             const uint8_t *ks = (fromA ? akeys : bkeys) + r * KL;
-            const V *ps = reinterpret_cast<const V *>((fromA ? apay : bpay) + r * P);
             const uint64_t od = o0 + o;
             copy_bytes<KL>(okeys + od * KL, ks);
             // the merged run's search samples (k_sample's, without re-reading the run), staged in
             // LDS and written as whole lines after the copy
             if (osmp2 && (o % SMP2_STRIDE) == 0) smp_t[o / SMP2_STRIDE] = key_digit<KK, KL>(ks, 0);
-            V pv[NV];
+            if constexpr (HEAP) {
+                const uint32_t slot = fromA ? reinterpret_cast<const uint32_t *>(apay)[r] : heap_base + (uint32_t)r;
+                reinterpret_cast<uint32_t *>(opay)[od] = slot;
+                const uint2 *hp = reinterpret_cast<const uint2 *>(heap + (uint64_t)slot * sizeof(DeltaRec));
+                uint32_t w[10];
 #pragma unroll
-            for (int k = 0; k < NV; k++) pv[k] = ps[k];
-            V *pd = reinterpret_cast<V *>(opay + od * P);
+                for (int k = 0; k < 5; k++) words_of(hp[k], w + 2 * k);
 #pragma unroll
-            for (int k = 0; k < NV; k++) pd[k] = pv[k];
-            uint32_t w[P / 4];
-#pragma unroll
-            for (int k = 0; k < NV; k++) words_of(pv[k], w + k * (int)(sizeof(V) / 4));
-#pragma unroll
-            for (int k = 0; k < 8; k++) h[k] = w[k];
-            if constexpr (COUNTS) {
-                static_assert(P == sizeof(DeltaRec), "delta payload");
+                for (int k = 0; k < 8; k++) h[k] = w[k];
                 const uint32_t f = w[9];  // DeltaRec::flags
                 c = ((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0);
+            } else {
+                const V *ps = reinterpret_cast<const V *>((fromA ? apay : bpay) + r * P);
+                V pv[NV];
+#pragma unroll
+                for (int k = 0; k < NV; k++) pv[k] = ps[k];
+                V *pd = reinterpret_cast<V *>(opay + od * P);
+#pragma unroll
+                for (int k = 0; k < NV; k++) pd[k] = pv[k];
+                uint32_t w[P / 4];
+#pragma unroll
+                for (int k = 0; k < NV; k++) words_of(pv[k], w + k * (int)(sizeof(V) / 4));
+#pragma unroll
+                for (int k = 0; k < 8; k++) h[k] = w[k];
+                if constexpr (COUNTS) {
+                    static_assert(P == sizeof(DeltaRec), "delta payload");
+                    const uint32_t f = w[9];  // DeltaRec::flags
+                    c = ((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0);
+                }
             }
         }
         const uint64_t blk = o0 / 256 + b;
@@ -1223,108 +1198,41 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
     }
 }
 
-__global__ void k_last_i32(const int32_t *a, uint64_t n, int32_t *out) {
-    if (threadIdx.x == 0) *out = n ? a[n - 1] : 0;
-}
-
-hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scratch &s, hipStream_t st) {
-    hipError_t e;
-    if (nbk) {
-        size_t tb = 0;
-        if ((e = rocprim::inclusive_scan(nullptr, tb, blk, blk, nbk, rocprim::plus<int32_t>(), st))) return e;
-        void *tmp = s.bytes(tb);
-        if (s.err) return s.err;
-        if ((e = rocprim::inclusive_scan(tmp, tb, blk, blk, nbk, rocprim::plus<int32_t>(), st))) return e;
-    }
-    hipLaunchKernelGGL(k_last_i32, dim3(1), dim3(64), 0, st, blk, nbk, total);
-    return hipGetLastError();
-}
-
-template <int KK, int KL, int P, bool COUNTS>
+template <int KK, int KL, int P, bool COUNTS, bool HEAP = false>
 hipError_t merge_kernel_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, const uint8_t *bkeys,
                           const uint8_t *bpay, uint64_t m, const uint32_t *upos, const uint32_t *usrc,
                           const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
-                          int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+                          int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *osmp, uint64_t *osmp2, hipStream_t st,
+                          const uint8_t *heap = nullptr, uint32_t heap_base = 0) {
     const uint64_t tiles = (nA + m + MT - 1) / MT;
     if (tiles)
-        hipLaunchKernelGGL((k_merge_run<KK, KL, P, COUNTS>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys, apay,
-                           nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk, osmp,
-                           osmp2);
+        hipLaunchKernelGGL((k_merge_run<KK, KL, P, COUNTS, HEAP>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys,
+                           apay, nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk, osmp,
+                           osmp2, heap, heap_base);
     return hipGetLastError();
 }
 
-// the merge kernel alone, for lists and counts made elsewhere (launch_delta_apply)
+// the merge kernel alone, for lists and counts made by the caller: payload 32 = fingerprint rows
+// (the base run), payload 4 with a heap = slot rows (the delta run)
 hipError_t launch_merge_kernel(int kk, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
                                const uint8_t *bkeys, const uint8_t *bpay, uint64_t m, const uint32_t *upos,
                                const uint32_t *usrc, const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys,
                                uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
-                               uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
-
-template <int KK, int KL, int P, bool COUNTS>
-hipError_t merge_run_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA, const uint8_t *bkeys,
-                       const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank, const uint8_t *present, uint64_t m,
-                       Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb,
-                       uint64_t nbk, uint64_t *counts, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2,
-                       hipStream_t st) {
-    hipError_t e;
-    uint64_t *v = s.u64(3, m + 1), *ex = s.u64(4, m + 1);
-    uint32_t *upos = s.u32(3, m + 1), *usrc = s.u32(4, m + 1), *rlist = s.u32(5, m + 1);
-    if (s.err) return s.err;
-    if (m) {
-        hipLaunchKernelGGL(k_mclass, g1(m), dim3(256), 0, st, bops, present, m, v, counts);
-        size_t tb = 0;
-        if ((e = rocprim::exclusive_scan(nullptr, tb, v, ex, (uint64_t)0, m, rocprim::plus<uint64_t>(), st))) return e;
-        void *tmp = s.bytes(tb);
-        if (s.err) return s.err;
-        if ((e = rocprim::exclusive_scan(tmp, tb, v, ex, (uint64_t)0, m, rocprim::plus<uint64_t>(), st))) return e;
-        hipLaunchKernelGGL(k_mlists, g1(m), dim3(256), 0, st, bops, present, rank, ex, m, upos, usrc, rlist, counts);
-    } else {
-        if ((e = hipMemsetAsync(counts, 0, 5 * 8, st))) return e;
-    }
-    hipLaunchKernelGGL(k_mcounts, dim3(1), dim3(64), 0, st, counts, out3);
-    return merge_kernel_t<KK, KL, P, COUNTS>(akeys, apay, nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay,
-                                             obs, ocnt, oinb, nbk, osmp, osmp2, st);
-}
-
-hipError_t launch_merge_kernel(int kk, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
-                               const uint8_t *bkeys, const uint8_t *bpay, uint64_t m, const uint32_t *upos,
-                               const uint32_t *usrc, const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys,
-                               uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
-                               uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+                               uint64_t *osmp, uint64_t *osmp2, hipStream_t st, const uint8_t *heap = nullptr,
+                               uint32_t heap_base = 0) {
     if (osmp && !osmp2) return hipErrorInvalidValue;
 #define RH_MK(KKV, KLV)                                                                                            \
     if (kk == KKV && kl == KLV) {                                                                                  \
         if (payload == 32)                                                                                         \
             return merge_kernel_t<KKV, KLV, 32, false>(akeys, apay, nA, bkeys, bpay, m, upos, usrc, rlist, counts,  \
                                                        okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2, st);        \
-        if (payload == (int)sizeof(DeltaRec))                                                                      \
-            return merge_kernel_t<KKV, KLV, sizeof(DeltaRec), true>(akeys, apay, nA, bkeys, bpay, m, upos, usrc,    \
-                                                                    rlist, counts, okeys, opay, obs, ocnt, oinb,   \
-                                                                    nbk, osmp, osmp2, st);                         \
+        if (payload == 4 && heap)                                                                                  \
+            return merge_kernel_t<KKV, KLV, 4, true, true>(akeys, apay, nA, bkeys, bpay, m, upos, usrc, rlist,     \
+                                                           counts, okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2,  \
+                                                           st, heap, heap_base);                                   \
     }
     RH_MK(KEY_U32, 4) RH_MK(KEY_U64, 8) RH_MK(KEY_BYTES, 8) RH_MK(KEY_BYTES, 16) RH_MK(KEY_BYTES, 32)
 #undef RH_MK
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_merge_run(int kk, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
-                            const uint8_t *bkeys, const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank,
-                            const uint8_t *present, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay,
-                            uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *counts,
-                            uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
-    if (osmp && !osmp2) return hipErrorInvalidValue;  // the stride-256 samples come from the stride-16 ones
-#define RH_MR(KKV, KLV)                                                                                            \
-    if (kk == KKV && kl == KLV) {                                                                                  \
-        if (payload == 32)                                                                                         \
-            return merge_run_t<KKV, KLV, 32, false>(akeys, apay, nA, bkeys, bpay, bops, rank, present, m, s, okeys, \
-                                                    opay, obs, ocnt, oinb, nbk, counts, out3, osmp, osmp2, st);    \
-        if (payload == (int)sizeof(DeltaRec))                                                                      \
-            return merge_run_t<KKV, KLV, sizeof(DeltaRec), true>(akeys, apay, nA, bkeys, bpay, bops, rank, present, \
-                                                                 m, s, okeys, opay, obs, ocnt, oinb, nbk, counts,  \
-                                                                 out3, osmp, osmp2, st);                           \
-    }
-    RH_MR(KEY_U32, 4) RH_MR(KEY_U64, 8) RH_MR(KEY_BYTES, 8) RH_MR(KEY_BYTES, 16) RH_MR(KEY_BYTES, 32)
-#undef RH_MR
     return hipErrorInvalidValue;
 }
 
@@ -1477,27 +1385,30 @@ StoreKeyOps *store_key_ops(int kk, int kl) {
 hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t *sops, uint64_t m,
                               const uint32_t *rank_b, const uint8_t *present_b, const uint8_t *base_fps,
                               const uint32_t *rank_d, const uint8_t *present_d, const uint8_t *dkeys,
-                              const uint8_t *dpay, uint64_t nd, const uint8_t *skeys, uint8_t *bpay, uint8_t *dops,
-                              uint64_t *counts3, Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
-                              int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *mcnt, uint64_t *out3,
-                              uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
-    if (m == 0) return hipErrorInvalidValue;
+                              const uint32_t *dslot, uint64_t nd, uint8_t *heap, uint64_t heap_base,
+                              const uint8_t *skeys, uint8_t *dops, uint64_t *counts3, Scratch &s, uint8_t *okeys,
+                              uint32_t *oslot, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
+                              uint64_t *mcnt, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+    if (m == 0 || heap_base + m >= (1ull << 32)) return hipErrorInvalidValue;
     const uint64_t G = (m + DB_WG - 1) / DB_WG;
     uint32_t *part = s.u32(13, G * DB_PARTS), *off = s.u32(6, 2 * G);
     uint32_t *upos = s.u32(3, m + 1), *usrc = s.u32(4, m + 1), *rlist = s.u32(5, m + 1);
     if (s.err) return s.err;
+    // the batch's records go straight to the heap, at slots heap_base + j
+    uint8_t *bpay = heap + heap_base * sizeof(DeltaRec);
     hipLaunchKernelGGL(k_delta_build, dim3((uint32_t)G), dim3(DB_WG), 0, st, sfps, sops, m, rank_b, present_b,
-                       base_fps, rank_d, present_d, dpay, bpay, dops, part);
+                       base_fps, rank_d, present_d, dslot, heap, bpay, dops, part);
     hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(1024), 0, st, part, G, counts3, mcnt, out3, off);
     hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, dops, present_d, rank_d, off, m, upos,
                        usrc, rlist);
-    return launch_merge_kernel(kk, kl, (int)sizeof(DeltaRec), dkeys, dpay, nd, skeys, bpay, m, upos, usrc, rlist, mcnt,
-                               okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2, st);
+    return launch_merge_kernel(kk, kl, 4, dkeys, reinterpret_cast<const uint8_t *>(dslot), nd, skeys, nullptr, m, upos,
+                               usrc, rlist, mcnt, okeys, reinterpret_cast<uint8_t *>(oslot), obs, ocnt, oinb, nbk,
+                               osmp, osmp2, st, heap, (uint32_t)heap_base);
 }
 
 hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *bfps, uint64_t nb, const uint8_t *dkeys,
-                          const uint8_t *dpay, uint64_t nd, Scratch &s, uint8_t *cfps, uint8_t *cops, uint8_t *okeys,
-                          uint8_t *ofps,
+                          const uint32_t *dslot, const uint8_t *heap, uint64_t nd, Scratch &s, uint8_t *cfps,
+                          uint8_t *cops, uint8_t *okeys, uint8_t *ofps,
                           uint8_t *obs, uint64_t nbk, uint64_t *mcnt, uint64_t *osmp, uint64_t *osmp2,
                           hipStream_t st) {
     if (nd == 0) return hipErrorInvalidValue;
@@ -1506,8 +1417,8 @@ hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *b
     uint32_t *upos = s.u32(3, nd + 1), *usrc = s.u32(4, nd + 1), *rlist = s.u32(5, nd + 1);
     uint8_t *cpres = s.u8(4, nd);
     if (s.err) return s.err;
-    hipLaunchKernelGGL(k_delta_cur, dim3((uint32_t)G), dim3(DB_WG), 0, st, dpay, nd, bfps, cfps, cops, crank, cpres,
-                       part);
+    hipLaunchKernelGGL(k_delta_cur, dim3((uint32_t)G), dim3(DB_WG), 0, st, dslot, heap, nd, bfps, cfps, cops, crank,
+                       cpres, part);
     hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(1024), 0, st, part, G, nullptr, mcnt, nullptr, off);
     hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, cops, cpres, crank, off, nd, upos, usrc,
                        rlist);
@@ -1544,23 +1455,13 @@ hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, 
 }
 
 hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch) {
-    // the slots launch_merge_run (m <= plan), the compaction (plan) and a batch (batch) take
-    (void)s.u64(3, plan + 1), (void)s.u64(4, plan + 1);
+    // the slots the compaction (plan rows) and a batch (batch rows) take
     (void)s.u32(3, plan + 1), (void)s.u32(4, plan + 1), (void)s.u32(5, plan + 1);
     (void)s.u32(14, plan), (void)s.u8(4, plan);
     const uint64_t G = (std::max(plan, batch) + DB_WG - 1) / DB_WG;  // launch_delta_apply / launch_compact partials
     (void)s.u32(13, G * DB_PARTS), (void)s.u32(6, 2 * G);
     (void)s.u32(9, batch), (void)s.u32(10, batch), (void)s.u8(2, batch), (void)s.u8(3, batch);
-    size_t t1 = 0, t2 = 0;
-    hipError_t e;
-    if ((e = rocprim::exclusive_scan(nullptr, t1, (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0,
-                                     plan + 1, rocprim::plus<uint64_t>(), s.stream)))
-        return e;
-    if ((e = rocprim::inclusive_scan(nullptr, t2, (const int32_t *)nullptr, (int32_t *)nullptr,
-                                     (plan + 255) / 256 + 1, rocprim::plus<int32_t>(), s.stream)))
-        return e;
-    (void)s.bytes(std::max(t1, t2));
-    return hipSuccess;
+    return s.err;
 }
 
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st) {

@@ -130,41 +130,31 @@ struct CntPrefix {
 hipError_t launch_delta_finish(const uint8_t *bsums, int32_t *blk, uint64_t nbk, uint8_t *ssums, int32_t *scnt,
                                int32_t *sblk, uint32_t *ticket, int32_t *total, uint64_t *fp_total, hipStream_t st);
 
-// Merge a key-sorted batch (ops 0 upsert / 1 drop; rank / present: its keys' lower bounds in
-// the run and whether the run holds them) into a sorted run of (key, payload) rows, writing
-// the merged run, the 256-row block sums of the payload's leading fingerprint (nbk blocks:
-// rows past the merged length count as zero) and, for DeltaRec payloads, each block's
-// count-delta total (ocnt) and the rows' in-block count prefixes (oinb), and (optional) the
-// merged run's search samples: osmp / osmp2 = the leading digit of every 256th / 16th key
-// (osmp only with osmp2).
-// counts (device, 8): [0] inserts, [1] overwrites, [2] removals; out3 (optional) gets the same.
-hipError_t launch_merge_run(int key_kind, int kl, int payload, const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
-                            const uint8_t *bkeys, const uint8_t *bpay, const uint8_t *bops, const uint32_t *rank,
-                            const uint8_t *present, uint64_t m, Scratch &s, uint8_t *okeys, uint8_t *opay,
-                            uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *counts,
-                            uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
-
-// in place: blk[b] <- Σ blk[0..b] (the inclusive block prefix); *total <- the last entry
-hipError_t launch_count_prefix(int32_t *blk, uint64_t nbk, int32_t *total, Scratch &s, hipStream_t st);
 
 // delta-run kernels (store_kernels.hip)
-// The batch path after the searches: the batch's DeltaRecs (from its sorted fingerprints / ops
-// and what base and delta hold for each key; dops 0 = upsert into the delta run, 1 = drop the
-// key's entry), its counts vs the merged view (counts3: new, overwritten, deleted), the merge
-// lists, and the merge into the delta run (launch_merge_run's outputs; mcnt as its counts).
+// The batch path after the searches.  The delta run is rows of (key, slot): a slot indexes the
+// record heap, where every batch appends its DeltaRecs (heap_base + j for sorted batch row j);
+// a merge moves keys and slots and gathers the records only for the block sums and count
+// prefixes.  This launch: the batch's DeltaRecs (from its sorted fingerprints / ops and what
+// base and delta hold for each key; dops 0 = upsert into the delta run, 1 = drop the key's
+// entry), its counts vs the merged view (counts3: new, overwritten, deleted), the merge lists,
+// and the merge into the delta run's other buffer: keys, slots, block sums, count prefixes
+// (ocnt: each block's count-delta total, oinb: in-block prefixes), search samples; mcnt: [0]
+// inserts, [1] overwrites, [2] removals, [3] upserts, [4] batch keys the run held; out3 the first
+// three.
 hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t *sops, uint64_t m,
                               const uint32_t *rank_b, const uint8_t *present_b, const uint8_t *base_fps,
                               const uint32_t *rank_d, const uint8_t *present_d, const uint8_t *dkeys,
-                              const uint8_t *dpay, uint64_t nd, const uint8_t *skeys, uint8_t *bpay, uint8_t *dops,
-                              uint64_t *counts3, Scratch &s, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
-                              int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *mcnt, uint64_t *out3,
-                              uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
+                              const uint32_t *dslot, uint64_t nd, uint8_t *heap, uint64_t heap_base,
+                              const uint8_t *skeys, uint8_t *dops, uint64_t *counts3, Scratch &s, uint8_t *okeys,
+                              uint32_t *oslot, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
+                              uint64_t *mcnt, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
 // The compaction: the delta run's current fingerprints (contrib + the base's at brank), ops and
 // base slots, the merge lists, and the merge of the delta run into the base run (keys, fps, block
 // sums, search samples; mcnt as launch_merge_run's counts).  cfps / cops: nd * 32 / nd bytes.
 hipError_t launch_compact(int key_kind, int kl, const uint8_t *bkeys, const uint8_t *bfps, uint64_t nb,
-                          const uint8_t *dkeys, const uint8_t *dpay, uint64_t nd, Scratch &s, uint8_t *cfps,
-                          uint8_t *cops, uint8_t *okeys, uint8_t *ofps, uint8_t *obs, uint64_t nbk, uint64_t *mcnt, uint64_t *osmp,
+                          const uint8_t *dkeys, const uint32_t *dslot, const uint8_t *heap, uint64_t nd, Scratch &s,
+                          uint8_t *cfps, uint8_t *cops, uint8_t *okeys, uint8_t *ofps, uint8_t *obs, uint64_t nbk, uint64_t *mcnt, uint64_t *osmp,
                           uint64_t *osmp2, hipStream_t st);
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,
                             const uint64_t *dhi, CntPrefix cp, uint64_t *out, hipStream_t st);
@@ -177,7 +167,7 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
                                  uint64_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
 hipError_t launch_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out,
                               hipStream_t st);
-// pre-size the scratch slots a merge of up to `plan` rows and a batch of `batch` rows use
+// pre-size the scratch slots a compaction of up to `plan` delta rows and a batch of `batch` rows use
 hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch);
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);
 

@@ -698,12 +698,9 @@ struct rh_store {
         if ((rc = tier_dpre.ensure((n + 1) * 32 + 64)) || (rc = tier_spre.ensure((ns + 1) * 32 + 64)) ||
             (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)))
             return rc;
-        try {
-            tier_keys.resize(n * kl + 64);
-            tier_prefix.resize((n + 1) * 4 + 8);
-        } catch (const std::bad_alloc &) {
-            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
-        }
+        if ((rc = tier_reserve(n + n / 4))) return rc;  // headroom: a growing map re-pins rarely
+        tier_keys.resize(n * kl + 64);
+        tier_prefix.resize((n + 1) * 4 + 8);
         if (n) {
             RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, stream));
             RH_HIP(hipMemcpyAsync(tier_keys.data(), bkeys[cb].p, n * kl, hipMemcpyDeviceToHost, stream));
@@ -833,7 +830,23 @@ struct rh_store {
         if (m) RH_HIP(hipMemcpyAsync(load_flag.data(), flag.p, 4, hipMemcpyDeviceToHost, stream));
         return RH_OK;
     }
+    // page-locked host tier capacity for `rows` rows ahead of the refresh that fills it: pinning
+    // fresh pages is most of a first refresh (11-13 ms at 10^6 rows against ~1 ms of copying)
+    int tier_reserve(uint64_t rows) {
+        if (!tier_on) return RH_OK;
+        try {
+            tier_keys.reserve(rows * kl + 64);
+            tier_prefix.reserve((rows + 1) * 4 + 8);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+        }
+        return RH_OK;
+    }
     int load_finish(size_t m, bool last_wins) {
+        const int rc = load_finish_rows(m, last_wins);
+        return rc ? rc : tier_reserve(nb + nb / 4);
+    }
+    int load_finish_rows(size_t m, bool last_wins) {
         int rc;
         if ((rc = sync())) return rc;
         memcpy(root_b, load_flag.data() + 2, sizeof root_b);
@@ -935,6 +948,7 @@ struct rh_store {
             return rc;
         RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        if ((rc = tier_reserve(rows))) return rc;
         // bsums / ssums / samples may have moved: derive them again from the kept fingerprints
         if ((rc = resum_base())) return rc;
         return sync();
@@ -1683,6 +1697,10 @@ int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
     std::lock_guard<std::mutex> g(s->mu);
     s->tier_on = enable == 1;
     s->tier_round_max = round_max ? round_max : 128;
+    if (s->tier_on) {
+        const int rc = s->tier_reserve(s->nb + s->nd + (s->nb + s->nd) / 4);
+        if (rc) return rc;
+    }
     if (!s->tier_on) {  // give the host memory back
         s->tier_version = ~0ull;
         s->tier = rh::HostTier{};

@@ -80,3 +80,25 @@ def test_bench_world2_gloo_equals_single_process(tmp_path, gpu):
     assert sum(int(r[4]) for r in a["ranges"]) == total
     # equal-count ranges: range j holds rows [total*j/16, total*(j+1)/16)
     assert [int(r[4]) for r in a["ranges"]] == [total * (j + 1) // 16 - total * j // 16 for j in range(16)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_world_n_gloo_equals_single_process(tmp_path, gpu, world):
+    """The driver's N = 4 / 8 sharding rehearsed on one GPU (gloo; every rank shares the card):
+    bench.py starts `world` ranks, each lifts its uneven key-range shard of one 3,000,007-record
+    set, and the 16 combined range aggregates equal the one-process run's bit for bit."""
+    total = 3_000_007
+    common = ["--config", "config4", "--records", str(total), "--steps", "2", "--warmup", "1",
+              "--cpu-baseline", "0", "--e2e", "0", "--spinup-ms", "0", "--check", "0"]
+    one, many = tmp_path / "one.json", tmp_path / "many.json"
+    r1 = _bench(common + ["--gpus", "1", "--dump-aggregates", str(one)])
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    rn = _bench(common + ["--gpus", str(world), "--dump-aggregates", str(many)], env_extra={"BENCH_BACKEND": "gloo"},
+                timeout=300)
+    assert rn.returncode == 0, rn.stderr[-3000:]
+    line = json.loads(rn.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world and line["rccl_world_size"] == world
+    assert line["config"]["records_per_rank"] == [total * (r + 1) // world - total * r // world for r in range(world)]
+    a, b = json.loads(one.read_text()), json.loads(many.read_text())
+    assert b["world"] == world and a["ranges"] == b["ranges"]

@@ -752,6 +752,20 @@ struct rh_store {
     // the inclusive block prefix of the count deltas (its last entry -> *total), the super-block
     // sums, and the contribution total -> fp_total.  No host round trip.
     rh::CntPrefix cnt_prefix(int buf) const { return rh::CntPrefix{dsblk[buf].p, dblk[buf].p, dinb[buf].p}; }
+    // The delta run's block sums and count prefixes are formed on the first question that needs
+    // them after a batch (a key-range aggregate, a rank); the batch path keeps the run's count
+    // and contribution totals itself (k_delta_build / k_delta_parts), so the root stays O(1).
+    bool dsums_ok = true;
+    DevBuf<uint64_t> fin_out;  // finish_delta_async's totals when only the sums are wanted
+    int ensure_delta_sums() {
+        int rc;
+        if (nd == 0 || dsums_ok) return RH_OK;
+        if ((rc = fin_out.ensure(8))) return rc;
+        RH_HIP(rh::launch_delta_sums(dslot[cd].p, dheap.p, nd, dbsums[cd].p, dblk[cd].p, dinb[cd].p, stream));
+        if ((rc = finish_delta_async(cd, nd, reinterpret_cast<int32_t *>(fin_out.p), fin_out.p + 4))) return rc;
+        dsums_ok = true;
+        return RH_OK;
+    }
     int finish_delta_async(int buf, uint64_t n_max, int32_t *total, uint64_t *fp_total) {
         int rc;
         const size_t nbk = rh_num_blocks(n_max), ns = rh_num_superblocks(n_max) + 1;
@@ -991,11 +1005,12 @@ struct rh_store {
             (rc = dsmp[cd].ensure(1)) || (rc = dsmp2[cd].ensure(1)) || (rc = mcnt.ensure(8)))
             return rc;
         // one 96-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,
-        // [6] sort flags, [7] Σ count deltas of the new delta run, [8..11] Σ of its contributions
+        // [6] sort flags, [7] the change of the delta run's count total (int64), [8..11] the change
+        // of its contribution total
         if ((rc = results.ensure(12))) return rc;
         uint64_t *r_counts = results.p, *r_merge = results.p + 3;
         uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
-        int32_t *r_total = reinterpret_cast<int32_t *>(results.p + 7);
+        int64_t *r_dcnt = reinterpret_cast<int64_t *>(results.p + 7);
         // pinned: the copy stays asynchronous and sync() polls for it (a pageable destination
         // makes the runtime stage the copy and block in an interrupt-driven wait)
         try {
@@ -1022,17 +1037,16 @@ struct rh_store {
                                           rank_d, present_d, dkeys[cd].p, dslot[cd].p, nd, dheap.p, heap_len, skeys.p,
                                           dops.p, r_counts, scratch, dkeys[nxt].p, dslot[nxt].p, dbsums[nxt].p, dblk[nxt].p,
                                           dinb[nxt].p, rh_num_blocks(n_max), mcnt.p, r_merge, dsmp[nxt].p,
-                                          dsmp2[nxt].p, stream));
+                                          dsmp2[nxt].p, results.p + 8, r_dcnt, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-            // 5. count prefix, super sums and totals, then the one round trip
-            if ((rc = finish_delta_async(nxt, n_max, r_total, results.p + 8))) return rc;
+            // 5. the one round trip
             RH_HIP(hipMemcpyAsync(host, results.p, 96, hipMemcpyDeviceToHost, stream));
             if ((rc = sync())) return rc;
             memcpy(&flags, &host[6], 4);
             if (!(flags & 6)) break;  // 2: leading-digit tie, 4: skewed buckets
         }
-        int32_t total;
-        memcpy(&total, &host[7], 4);
+        int64_t dcnt;
+        memcpy(&dcnt, &host[7], 8);
         const uint64_t c2[3] = {host[3], host[4], host[5]};
         out[0] = host[0];
         out[1] = host[1];
@@ -1044,8 +1058,9 @@ struct rh_store {
         cd = nxt;
         nd = nd + c2[0] - c2[2];
         heap_len += m;
-        dtotal = total;
-        memcpy(root_d, &host[8], sizeof root_d);
+        dtotal += dcnt;
+        rh_fp_add(root_d, &host[8], root_d);  // mod 2^256
+        dsums_ok = false;
         // the heap also holds records no row points to any more (overwritten or dropped keys)
         const uint64_t thresh_now = std::max<uint64_t>(nb / compact_div, compact_min);
         if (nd > thresh_now || heap_len > thresh_now) return compact();
@@ -1081,6 +1096,7 @@ struct rh_store {
         RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, 1,
                                       reinterpret_cast<uint64_t *>(res), stream));
         if (nd) {
+            if ((rc = ensure_delta_sums())) return rc;
             RH_HIP(kops->bounds(dkeys[cd].p, nd, q_keys.p, lo_kind, q_keys.p + kl, hi_kind, q_dlo.p, q_dhi.p, stream));
             RH_HIP(rh::launch_range_query(dheap.p, dbsums[cd].p, dssums[cd].p, nd, q_dlo.p, q_dhi.p, 1,
                                           reinterpret_cast<uint64_t *>(q_dout.p), stream, sizeof(rh::DeltaRec),
@@ -1100,6 +1116,7 @@ struct rh_store {
         RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_keys.p, m, q_rank.p, nullptr, stream,
                                     base_table()));
         if (nd) RH_HIP(kops->search(dkeys[cd].p, nd, q_keys.p, m, q_drank.p, nullptr, stream));
+        if ((rc = ensure_delta_sums())) return rc;  // the count prefix
         RH_HIP(rh::launch_rank_merge(q_rank.p, nd ? q_drank.p : nullptr, cnt_prefix(cd), m, q_merged.p, stream));
         RH_HIP(hipMemcpyAsync(out, q_merged.p, m * 8, hipMemcpyDeviceToHost, stream));
         return sync();

@@ -128,6 +128,17 @@ __device__ __forceinline__ void fp_sub(const uint32_t a[8], const uint32_t b[8],
     }
 }
 
+__device__ __forceinline__ void words_of(const uint4 &v, uint32_t *w) {
+    w[0] = v.x;
+    w[1] = v.y;
+    w[2] = v.z;
+    w[3] = v.w;
+}
+__device__ __forceinline__ void words_of(const uint2 &v, uint32_t *w) {
+    w[0] = v.x;
+    w[1] = v.y;
+}
+
 // ---- batch sort ------------------------------------------------------------------------------
 
 template <int KK, int KL>
@@ -656,22 +667,30 @@ __global__ void k_bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key,
 // Build the batch's DeltaRecs (key order) from its fingerprints, what base and delta hold for
 // each key, and the op; dops: 0 = upsert into the delta run, 1 = drop the key's delta entry.
 // counts (vs the merged view): [0] new keys, [1] overwritten, [2] deleted.
-// part[6 g + k], workgroup g: k = 0 new, 1 overwritten, 2 deleted (vs the merged view), and for
-// the merge into the delta run 3 upserts (dops 0), 4 keys the run holds (present_d), 5 both
-constexpr int DB_PARTS = 6, DB_WG = 1024;  // 1,024-row workgroups: ~1,000 partials per 1 M batch
+// part[7 g + k], workgroup g: k = 0 new, 1 overwritten, 2 deleted (vs the merged view), and for
+// the merge into the delta run 3 upserts (dops 0), 4 keys the run holds (present_d), 5 both,
+// 6 the change of the run's count total (int32); dsum[4 g ..] the change of its contribution total
+// (Σ new entries' contrib − Σ replaced entries' contrib, mod 2^256)
+// 512-row workgroups (~2,000 partials per 1 M batch): at 1,024 lanes the 256-bit accumulators
+// of the totals spilled to scratch (a 128-VGPR cap)
+constexpr int DB_PARTS = 7, DB_WG = 512, DP_WG = 512;
 
 __global__ __launch_bounds__(DB_WG) void k_delta_build(const uint8_t *sfps, const uint8_t *sops, uint64_t m,
                                                      const uint32_t *rank_b, const uint8_t *present_b,
                                                      const uint8_t *base_fps, const uint32_t *rank_d,
                                                      const uint8_t *present_d, const uint32_t *dslot,
                                                      const uint8_t *heap, uint8_t *bpay, uint8_t *dops,
-                                                     uint32_t *part) {
+                                                     uint32_t *part, uint64_t *dsum) {
+    __shared__ uint64_t lds[(DB_WG / 64) * 8];
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool c_new = false, c_over = false, c_del = false, c_up = false, c_pr = false;
+    int32_t dcnt = 0;
+    uint32_t dfp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (j < m) {
         const bool isdel = sops[j] != 0, in_b = present_b[j], in_d = present_d[j];
         bool was_live = in_b;
-        if (in_d) was_live = (reinterpret_cast<const DeltaRec *>(heap)[dslot[rank_d[j]]].flags & DeltaRec::LIVE) != 0;
+        const DeltaRec *old_rec = in_d ? reinterpret_cast<const DeltaRec *>(heap) + dslot[rank_d[j]] : nullptr;
+        if (in_d) was_live = (old_rec->flags & DeltaRec::LIVE) != 0;
         uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (in_b) fp_load(base_fps + 32ull * rank_b[j], base);
         DeltaRec r;
@@ -693,6 +712,32 @@ __global__ __launch_bounds__(DB_WG) void k_delta_build(const uint8_t *sfps, cons
         c_up = !drop;
         c_pr = in_d;
         reinterpret_cast<DeltaRec *>(bpay)[j] = r;
+        // what this row changes in the run's totals: its new entry in, the entry it replaces out
+        if (!drop) dcnt += (isdel ? 0 : 1) - (in_b ? 1 : 0);
+        uint32_t nc[8], oc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; k++) nc[k] = drop ? 0u : r.contrib[k];
+        if (in_d) {
+            const uint2 *op = reinterpret_cast<const uint2 *>(old_rec);
+            uint32_t w[10];
+#pragma unroll
+            for (int k = 0; k < 5; k++) words_of(op[k], w + 2 * k);
+#pragma unroll
+            for (int k = 0; k < 8; k++) oc[k] = w[k];
+            dcnt -= ((w[9] & DeltaRec::LIVE) ? 1 : 0) - ((w[9] & DeltaRec::IN_BASE) ? 1 : 0);
+        }
+        fp_sub(nc, oc, dfp);
+    }
+    {
+        Acc a;
+        acc_zero(a);
+        acc_add_fp(a, dfp);
+        uint32_t f[8];
+        acc_block_reduce<DB_WG>(a, lds, f);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) dsum[4ull * blockIdx.x + q] = (uint64_t)f[2 * q] | ((uint64_t)f[2 * q + 1] << 32);
+        }
     }
     // per-workgroup counts (same-address atomics from every wave would serialise in L2);
     // k_delta_parts adds them up
@@ -702,27 +747,66 @@ __global__ __launch_bounds__(DB_WG) void k_delta_build(const uint8_t *sfps, cons
     if ((threadIdx.x & 63) == 0)
         for (int k = 0; k < DB_PARTS; k++) wc[threadIdx.x >> 6][k] = (uint32_t)__popcll(b[k]);
     __syncthreads();
-    if (threadIdx.x < DB_PARTS) {
+    if (threadIdx.x < DB_PARTS - 1) {
         uint32_t t = 0;
         for (uint32_t w = 0; w < blockDim.x / 64; w++) t += wc[w][threadIdx.x];
         part[(uint64_t)DB_PARTS * blockIdx.x + threadIdx.x] = t;
     }
+    // the count change: a block sum of small signed ints
+    int32_t y = dcnt;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) y += __shfl_xor(y, o, 64);
+    __shared__ int32_t wd[DB_WG / 64];
+    if ((threadIdx.x & 63) == 0) wd[threadIdx.x >> 6] = y;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t tsum = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) tsum += wd[w];
+        part[(uint64_t)DB_PARTS * blockIdx.x + DB_PARTS - 1] = (uint32_t)tsum;
+    }
 }
 
-// one workgroup over the G = ceil(m / 1024) partials: the batch counts (counts3), the merge counts
+// one workgroup over the G = ceil(m / DB_WG) partials: the batch counts (counts3), the merge counts
 // (mcnt: [0] inserts, [1] overwrites, [2] removals, [3] upserts U, [4] present R; out3 the first
 // three) and each workgroup's exclusive (U, R) offsets for k_delta_lists (off[2 g], off[2 g + 1])
-__global__ __launch_bounds__(1024) void k_delta_parts(const uint32_t *__restrict__ part, uint64_t G,
+// (dsum / dtot, optional: the per-workgroup contribution changes and their total; dcnt: the count
+// change's total)
+__global__ __launch_bounds__(DP_WG) void k_delta_parts(const uint32_t *__restrict__ part, uint64_t G,
                                                       uint64_t *__restrict__ counts3, uint64_t *__restrict__ mcnt,
-                                                      uint64_t *__restrict__ out3, uint32_t *__restrict__ off) {
+                                                      uint64_t *__restrict__ out3, uint32_t *__restrict__ off,
+                                                      const uint64_t *__restrict__ dsum, uint64_t *__restrict__ dtot,
+                                                      int64_t *__restrict__ dcnt) {
     // counts are < 2^31 (the store's row limit): 32-bit sums throughout
-    __shared__ uint32_t w[16][DB_PARTS];
+    constexpr uint32_t NW = DP_WG / 64;
+    __shared__ uint32_t w[NW][DB_PARTS];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint64_t chunk = (G + 1023) / 1024, g0 = t * chunk < G ? t * chunk : G, g1 = g0 + chunk < G ? g0 + chunk : G;
-    uint32_t sum[DB_PARTS] = {0, 0, 0, 0, 0, 0};
+    const uint64_t chunk = (G + DP_WG - 1) / DP_WG, g0 = t * chunk < G ? t * chunk : G,
+                   g1 = g0 + chunk < G ? g0 + chunk : G;
+    uint32_t sum[DB_PARTS] = {0, 0, 0, 0, 0, 0, 0};
     for (uint64_t g = g0; g < g1; g++)
 #pragma unroll
-        for (int k = 0; k < DB_PARTS; k++) sum[k] += part[DB_PARTS * g + k];
+        for (int k = 0; k < DB_PARTS; k++) sum[k] += part[DB_PARTS * g + k];  // slot 6: int32 bits, wraps right
+    if (dsum) {  // the contribution change (a uniform branch: every lane joins the block reduction)
+        __shared__ uint64_t lds[NW * 8];
+        Acc a;
+        acc_zero(a);
+        for (uint64_t g = g0; g < g1; g++) {
+            uint32_t f[8];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint64_t v = dsum[4 * g + q];
+                f[2 * q] = (uint32_t)v;
+                f[2 * q + 1] = (uint32_t)(v >> 32);
+            }
+            acc_add_fp(a, f);
+        }
+        uint32_t f[8];
+        acc_block_reduce<DP_WG>(a, lds, f);
+        if (t == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) dtot[q] = (uint64_t)f[2 * q] | ((uint64_t)f[2 * q + 1] << 32);
+        }
+    }
     // U (3) and R (4): inclusive wave scans; the others: wave totals
     uint32_t xu = sum[3], xr = sum[4];
 #pragma unroll
@@ -766,7 +850,12 @@ __global__ __launch_bounds__(1024) void k_delta_parts(const uint32_t *__restrict
 #pragma unroll
         for (int k = 0; k < DB_PARTS; k++) {
             T[k] = 0;
-            for (uint32_t q = 0; q < 16; q++) T[k] += w[q][k];
+            for (uint32_t q = 0; q < NW; q++) T[k] += w[q][k];
+        }
+        if (dcnt) {
+            int64_t d = 0;
+            for (uint32_t q = 0; q < NW; q++) d += (int32_t)w[q][DB_PARTS - 1];
+            *dcnt = d;
         }
         if (counts3) {
             counts3[0] = T[0];
@@ -847,7 +936,7 @@ __global__ __launch_bounds__(DB_WG) void k_delta_cur(const uint32_t *dslot, cons
     __syncthreads();
     if (threadIdx.x < DB_PARTS) {
         uint32_t t = 0;
-        if (threadIdx.x >= 3)
+        if (threadIdx.x >= 3 && threadIdx.x < 6)
             for (uint32_t w = 0; w < blockDim.x / 64; w++) t += wc[w][threadIdx.x - 3];
         part[(uint64_t)DB_PARTS * blockIdx.x + threadIdx.x] = t;
     }
@@ -858,6 +947,51 @@ __global__ __launch_bounds__(DB_WG) void k_delta_cur(const uint32_t *dslot, cons
 __device__ __forceinline__ int64_t cnt_through(const CntPrefix &c, uint64_t i) {
     const uint64_t b = i / 256;
     return (int64_t)c.sblk[b / 256] + ((b % 256) ? c.blk[b - 1] : 0) + c.inb[i];
+}
+
+// The delta run's block sums (of the contributions) and count prefixes, formed on the first
+// question after a batch that needs them (a key-range aggregate or a rank): the records gathered
+// through the slots, one workgroup per 256-row block; k_delta_finish then forms the upper levels.
+__global__ __launch_bounds__(256) void k_delta_sums(const uint32_t *dslot, const uint8_t *heap, uint64_t n,
+                                                    uint8_t *obs, int32_t *ocnt, int16_t *oinb) {
+    __shared__ SumTile tile;
+    __shared__ int32_t wsum[4];
+    const uint32_t t = threadIdx.x;
+    const uint64_t blk = blockIdx.x, i = blk * 256 + t;
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t c = 0;
+    if (i < n) {
+        const uint2 *hp = reinterpret_cast<const uint2 *>(heap + (uint64_t)dslot[i] * sizeof(DeltaRec));
+        uint32_t w[10];
+#pragma unroll
+        for (int k = 0; k < 5; k++) words_of(hp[k], w + 2 * k);
+#pragma unroll
+        for (int k = 0; k < 8; k++) h[k] = w[k];
+        c = ((w[9] & DeltaRec::LIVE) ? 1 : 0) - ((w[9] & DeltaRec::IN_BASE) ? 1 : 0);
+    }
+    uint32_t f8[8];
+    block_sum_fps256(h, tile, f8);
+    if (t == 0) store_sum(obs, blk, f8);
+    int32_t y = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t z = __shfl_up(y, o, 64);
+        if ((t & 63) >= (uint32_t)o) y += z;
+    }
+    if ((t & 63) == 63) wsum[t >> 6] = y;
+    __syncthreads();
+    int32_t before = 0;
+    for (uint32_t w = 0; w < (t >> 6); w++) before += wsum[w];
+    if (i < n) oinb[i] = (int16_t)(before + y);
+    if (t == 255) ocnt[blk] = before + y;
+}
+
+hipError_t launch_delta_sums(const uint32_t *dslot, const uint8_t *heap, uint64_t n, uint8_t *obs, int32_t *ocnt,
+                             int16_t *oinb, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delta_sums, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, dslot, heap, n, obs, ocnt,
+                       oinb);
+    return hipGetLastError();
 }
 
 // After a merge into a delta buffer (k_merge_run wrote its block sums and block count totals):
@@ -1039,20 +1173,11 @@ __device__ __forceinline__ uint64_t survivor_k(const uint32_t *rlist, uint64_t R
     return lo;
 }
 
-__device__ __forceinline__ void words_of(const uint4 &v, uint32_t *w) {
-    w[0] = v.x;
-    w[1] = v.y;
-    w[2] = v.z;
-    w[3] = v.w;
-}
-__device__ __forceinline__ void words_of(const uint2 &v, uint32_t *w) {
-    w[0] = v.x;
-    w[1] = v.y;
-}
 
 // HEAP (the delta run): a row's payload is the 4-byte slot of its DeltaRec in the record heap
-// (A rows: apay; batch row j: heap_base + j); the block sums and count prefixes are formed from
-// the records gathered through the slots, and only key + slot are moved.
+// (A rows: apay; batch row j: heap_base + j), and a merge moves key + slot only: the run's block
+// sums and count prefixes are formed by k_delta_sums on the first question that needs them, and
+// its totals are kept per batch by k_delta_build / k_delta_parts.
 template <int KK, int KL, int P, bool COUNTS, bool HEAP>
 __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const uint8_t *apay, uint64_t nA,
                                                    const uint8_t *bkeys, const uint8_t *bpay, uint64_t m,
@@ -1140,14 +1265,6 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
             if constexpr (HEAP) {
                 const uint32_t slot = fromA ? reinterpret_cast<const uint32_t *>(apay)[r] : heap_base + (uint32_t)r;
                 reinterpret_cast<uint32_t *>(opay)[od] = slot;
-                const uint2 *hp = reinterpret_cast<const uint2 *>(heap + (uint64_t)slot * sizeof(DeltaRec));
-                uint32_t w[10];
-#pragma unroll
-                for (int k = 0; k < 5; k++) words_of(hp[k], w + 2 * k);
-#pragma unroll
-                for (int k = 0; k < 8; k++) h[k] = w[k];
-                const uint32_t f = w[9];  // DeltaRec::flags
-                c = ((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0);
             } else {
                 const V *ps = reinterpret_cast<const V *>((fromA ? apay : bpay) + r * P);
                 V pv[NV];
@@ -1168,6 +1285,7 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
                 }
             }
         }
+        if constexpr (HEAP) continue;  // no sums: k_delta_sums forms them when a question needs them
         const uint64_t blk = o0 / 256 + b;
         uint32_t f8[8];
         block_sum_fps256(h, tile, f8);
@@ -1388,22 +1506,24 @@ hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t
                               const uint32_t *dslot, uint64_t nd, uint8_t *heap, uint64_t heap_base,
                               const uint8_t *skeys, uint8_t *dops, uint64_t *counts3, Scratch &s, uint8_t *okeys,
                               uint32_t *oslot, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
-                              uint64_t *mcnt, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st) {
+                              uint64_t *mcnt, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, uint64_t *dtot,
+                              int64_t *dcnt, hipStream_t st) {
     if (m == 0 || heap_base + m >= (1ull << 32)) return hipErrorInvalidValue;
     const uint64_t G = (m + DB_WG - 1) / DB_WG;
     uint32_t *part = s.u32(13, G * DB_PARTS), *off = s.u32(6, 2 * G);
+    uint64_t *dsum = s.u64(7, 4 * G);
     uint32_t *upos = s.u32(3, m + 1), *usrc = s.u32(4, m + 1), *rlist = s.u32(5, m + 1);
     if (s.err) return s.err;
     // the batch's records go straight to the heap, at slots heap_base + j
     uint8_t *bpay = heap + heap_base * sizeof(DeltaRec);
     hipLaunchKernelGGL(k_delta_build, dim3((uint32_t)G), dim3(DB_WG), 0, st, sfps, sops, m, rank_b, present_b,
-                       base_fps, rank_d, present_d, dslot, heap, bpay, dops, part);
-    hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(1024), 0, st, part, G, counts3, mcnt, out3, off);
+                       base_fps, rank_d, present_d, dslot, heap, bpay, dops, part, dsum);
+    hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(DP_WG), 0, st, part, G, counts3, mcnt, out3, off, dsum, dtot, dcnt);
     hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, dops, present_d, rank_d, off, m, upos,
                        usrc, rlist);
     return launch_merge_kernel(kk, kl, 4, dkeys, reinterpret_cast<const uint8_t *>(dslot), nd, skeys, nullptr, m, upos,
-                               usrc, rlist, mcnt, okeys, reinterpret_cast<uint8_t *>(oslot), obs, ocnt, oinb, nbk,
-                               osmp, osmp2, st, heap, (uint32_t)heap_base);
+                               usrc, rlist, mcnt, okeys, reinterpret_cast<uint8_t *>(oslot), nullptr, nullptr, nullptr,
+                               nbk, osmp, osmp2, st, heap, (uint32_t)heap_base);
 }
 
 hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *bfps, uint64_t nb, const uint8_t *dkeys,
@@ -1419,7 +1539,8 @@ hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *b
     if (s.err) return s.err;
     hipLaunchKernelGGL(k_delta_cur, dim3((uint32_t)G), dim3(DB_WG), 0, st, dslot, heap, nd, bfps, cfps, cops, crank,
                        cpres, part);
-    hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(1024), 0, st, part, G, nullptr, mcnt, nullptr, off);
+    hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(DP_WG), 0, st, part, G, nullptr, mcnt, nullptr, off, nullptr,
+                       nullptr, nullptr);
     hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, cops, cpres, crank, off, nd, upos, usrc,
                        rlist);
     return launch_merge_kernel(kk, kl, 32, bkeys, bfps, nb, dkeys, cfps, nd, upos, usrc, rlist, mcnt, okeys, ofps, obs,
@@ -1459,7 +1580,7 @@ hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch) {
     (void)s.u32(3, plan + 1), (void)s.u32(4, plan + 1), (void)s.u32(5, plan + 1);
     (void)s.u32(14, plan), (void)s.u8(4, plan);
     const uint64_t G = (std::max(plan, batch) + DB_WG - 1) / DB_WG;  // launch_delta_apply / launch_compact partials
-    (void)s.u32(13, G * DB_PARTS), (void)s.u32(6, 2 * G);
+    (void)s.u32(13, G * DB_PARTS), (void)s.u32(6, 2 * G), (void)s.u64(7, 4 * G);
     (void)s.u32(9, batch), (void)s.u32(10, batch), (void)s.u8(2, batch), (void)s.u8(3, batch);
     return s.err;
 }

@@ -138,8 +138,8 @@ hipError_t launch_delta_finish(const uint8_t *bsums, int32_t *blk, uint64_t nbk,
 // prefixes.  This launch: the batch's DeltaRecs (from its sorted fingerprints / ops and what
 // base and delta hold for each key; dops 0 = upsert into the delta run, 1 = drop the key's
 // entry), its counts vs the merged view (counts3: new, overwritten, deleted), the merge lists,
-// and the merge into the delta run's other buffer: keys, slots, block sums, count prefixes
-// (ocnt: each block's count-delta total, oinb: in-block prefixes), search samples; mcnt: [0]
+// and the merge into the delta run's other buffer: keys, slots and search samples (obs / ocnt /
+// oinb unused: the run's sums are formed lazily, launch_delta_sums); mcnt: [0]
 // inserts, [1] overwrites, [2] removals, [3] upserts, [4] batch keys the run held; out3 the first
 // three.
 hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t *sops, uint64_t m,
@@ -148,7 +148,13 @@ hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t
                               const uint32_t *dslot, uint64_t nd, uint8_t *heap, uint64_t heap_base,
                               const uint8_t *skeys, uint8_t *dops, uint64_t *counts3, Scratch &s, uint8_t *okeys,
                               uint32_t *oslot, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
-                              uint64_t *mcnt, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, hipStream_t st);
+                              uint64_t *mcnt, uint64_t *out3, uint64_t *osmp, uint64_t *osmp2, uint64_t *dtot,
+                              int64_t *dcnt, hipStream_t st);
+// the delta run's block sums and count prefixes (what launch_delta_finish completes), formed
+// lazily: the batch path keeps only the run's totals (dtot: Σ contributions' change, dcnt: count
+// change, per batch)
+hipError_t launch_delta_sums(const uint32_t *dslot, const uint8_t *heap, uint64_t n, uint8_t *obs, int32_t *ocnt,
+                             int16_t *oinb, hipStream_t st);
 // The compaction: the delta run's current fingerprints (contrib + the base's at brank), ops and
 // base slots, the merge lists, and the merge of the delta run into the base run (keys, fps, block
 // sums, search samples; mcnt as launch_merge_run's counts).  cfps / cops: nd * 32 / nd bytes.

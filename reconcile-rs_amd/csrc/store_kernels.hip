@@ -1160,7 +1160,7 @@ __global__ void k_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *
 // block sums of the payload's leading fingerprint -- and, for the delta run, each block's
 // count-delta total and every row's in-block count prefix.  This replaces a row-move pass, a
 // batch-scatter pass and a re-read of the whole run for its sums.
-constexpr int MT = 1024;  // output rows per workgroup (4 blocks of 256)
+constexpr int MT = 2048;  // output rows per workgroup (8 blocks of 256; 2,048 measured best of 1,024 / 2,048 / 4,096)
 
 // smallest k in [lo, hi] with k == R or rlist[k] - k > s: the number of removed A rows before
 // the s-th survivor
@@ -1222,10 +1222,11 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
         if (p < nrows && j < m) src[p] = -2 - (int32_t)j;
     }
     __syncthreads();
-    // free slots (4 per lane) in order -> the tile's A survivors
+    // free slots (MT / 256 per lane) in order -> the tile's A survivors
+    constexpr int SPL = MT / 256;
     uint32_t cnt = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) cnt += (4 * t + k < nrows && src[4 * t + k] == -1) ? 1u : 0u;
+    for (int k = 0; k < SPL; k++) cnt += (SPL * t + k < nrows && src[SPL * t + k] == -1) ? 1u : 0u;
     uint32_t x = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1237,8 +1238,8 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
     uint32_t q = x - cnt;
     for (uint32_t w = 0; w < (t >> 6); w++) q += wsum[w];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t slot = 4 * t + k;
+    for (int k = 0; k < SPL; k++) {
+        const uint32_t slot = SPL * t + k;
         if (slot < nrows && src[slot] == -1) {
             const uint64_t sidx = s0 + q;
             const uint64_t i = sidx + survivor_k(rlist, R, k0, k1, sidx);
@@ -1309,9 +1310,10 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
     if (osmp2) {
         __syncthreads();
         constexpr uint32_t R = SMP_STRIDE / SMP2_STRIDE;
-        if (t < MT / SMP2_STRIDE && t * SMP2_STRIDE < nrows) {
-            osmp2[o0 / SMP2_STRIDE + t] = smp_t[t];
-            if (osmp && t % R == 0) osmp[o0 / SMP_STRIDE + t / R] = smp_t[t];
+        for (uint32_t e = t; e < MT / SMP2_STRIDE; e += 256) {
+            if (e * SMP2_STRIDE >= nrows) break;
+            osmp2[o0 / SMP2_STRIDE + e] = smp_t[e];
+            if (osmp && e % R == 0) osmp[o0 / SMP_STRIDE + e / R] = smp_t[e];
         }
     }
 }

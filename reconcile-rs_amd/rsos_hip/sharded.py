@@ -51,6 +51,29 @@ class ShardedStore:
     def _shard_of(self, key: Key) -> int:
         return bisect.bisect_right(self.splitters, key)
 
+    def _order_view(self, rows: np.ndarray) -> np.ndarray:
+        """Key rows (n x key_row bytes) as a numpy array that sorts as the keys' Ord: numeric for
+        u32 / u64 keys (stored little-endian), memcmp for byte keys ('S' compares equal-length
+        rows in byte order; stripping trailing NULs keeps that order)."""
+        from . import _abi as A
+        rows = np.ascontiguousarray(rows, dtype=np.uint8).reshape(-1, self.schema.key_row)
+        if self.schema.key_kind == A.KEY_U32:
+            return rows.view("<u4").ravel()
+        if self.schema.key_kind == A.KEY_U64:
+            return rows.view("<u8").ravel()
+        return rows.view(f"S{self.schema.key_row}").ravel()
+
+    def _owners(self, keys: np.ndarray) -> np.ndarray:
+        """_shard_of for every key row at once (np.searchsorted, side='right' = bisect_right)."""
+        n = len(keys) // max(self.schema.key_row, 1) if keys.ndim == 1 else len(keys)
+        if not self.splitters:
+            return np.zeros(n, np.int64)
+        if self.schema.key_row == 0:  # unit keys: every row is the one key
+            return np.full(n, self._shard_of(self.shards[0]._key_out(b"")), np.int64)
+        split = self._order_view(np.frombuffer(b"".join(self.shards[0]._key_bytes(k) for k in self.splitters),
+                                               np.uint8))
+        return np.searchsorted(split, self._order_view(keys), side="right").astype(np.int64)
+
     # ---- fill ----------------------------------------------------------------------------
     def load_bulk(self, cols: Dict[str, np.ndarray]) -> None:
         """Records sorted by key, without duplicates: cut into equal-count contiguous shards."""
@@ -69,10 +92,7 @@ class ShardedStore:
 
     def apply(self, cols: Dict[str, np.ndarray], ops: np.ndarray) -> Tuple[int, int, int]:
         """Batched insert (op 0) / delete (op 1), each row applied on its key's shard."""
-        key_out = self.shards[0]._key_out
-        kl = self.schema.key_row
-        keys = np.ascontiguousarray(cols["keys"]).reshape(len(ops), kl)
-        owner = np.array([self._shard_of(key_out(keys[i].tobytes())) for i in range(len(ops))], np.int64)
+        owner = self._owners(np.ascontiguousarray(cols["keys"]).reshape(len(ops), self.schema.key_row))
         jobs = []
         for s, st in enumerate(self.shards):
             rows = np.nonzero(owner == s)[0]

@@ -153,3 +153,32 @@ def test_host_tensors_are_rejected(rsos_hip_lib):
     cols = {"keys": torch.zeros((4, 4), dtype=torch.uint8), "values": torch.zeros((4, 4), dtype=torch.uint8)}
     with pytest.raises((ValueError, RuntimeError)):
         lift_records(s, cols)
+
+
+@pytest.mark.parametrize("kind,key", [("u32", "u32"), ("u64", "u64"), ("b16", "bytes16"), ("b32", "bytes32")])
+def test_sharded_routing_is_bisect_right(kind, key):
+    """ShardedStore.apply routes a batch with one np.searchsorted over the load-time splitters;
+    it must equal bisect_right on the keys' Ord (numeric for integers, memcmp for byte arrays,
+    including rows with trailing zero bytes and rows equal to a splitter)."""
+    import bisect
+    from rsos_hip import RecordSchema
+    from rsos_hip.sharded import ShardedStore
+    from rsos_hip.store import GpuFingerprintStore
+    schema = RecordSchema.plain(key, "u64")
+    kl = schema.key_row
+    probe = GpuFingerprintStore.__new__(GpuFingerprintStore)  # key conversion only: no device
+    probe.schema = schema
+    sh = ShardedStore.__new__(ShardedStore)
+    sh.schema, sh.shards = schema, [probe]
+    rng = np.random.default_rng(5)
+    rows = rng.integers(0, 256, (4000, kl), dtype=np.uint8)
+    rows[::7, kl // 2:] = 0  # trailing zero bytes
+    rows[::11, 0] = rows[0, 0]  # shared leading byte
+    keys = [probe._key_out(r.tobytes()) for r in rows]
+    sh.splitters = sorted(keys[j] for j in (3, 500, 1200, 2500, 3999))
+    rows[1] = rows[500]  # a key equal to a splitter goes to the shard it starts
+    keys[1] = keys[500]
+    want = [bisect.bisect_right(sh.splitters, k) for k in keys]
+    assert sh._owners(rows).tolist() == want
+    sh.splitters = []
+    assert sh._owners(rows).tolist() == [0] * len(rows)

@@ -911,20 +911,23 @@ struct rh_store {
         } catch (const std::bad_alloc &) {
             return fail(RH_ERR_OOM, "pinned result buffer");
         }
-        uint64_t *c = res_host.data();  // pinned: an asynchronous copy that sync() polls for
+        // the merged size is known on the host (size() = base rows + the delta run's count total),
+        // so the sums and the search table are enqueued behind the merge without a round trip; the
+        // merge's own counts (pinned, asynchronous) are checked against it after the one sync
+        uint64_t *c = res_host.data();
         RH_HIP(hipMemcpyAsync(c, mcnt.p, 24, hipMemcpyDeviceToHost, stream));
-        if ((rc = sync())) return rc;
-        const uint64_t want = size();
+        const uint64_t want = size(), nb_old = nb;
         cb = nxt;
-        nb = nb + c[0] - c[2];
+        nb = want;
         nd = 0;
         heap_len = 0;
         dtotal = 0;
         memset(root_d, 0, sizeof root_d);
         compactions++;
-        if (nb != want) return fail(RH_ERR_STATE, "compaction size mismatch (internal error)");
         if ((rc = resum_base(true, nullptr, true))) return rc;
-        return sync();
+        if ((rc = sync())) return rc;
+        if (nb_old + c[0] - c[2] != want) return fail(RH_ERR_STATE, "compaction size mismatch (internal error)");
+        return RH_OK;
     }
     // Capacity for `rows` resident rows taking batches of up to `batch` rows: both base buffers
     // for a compaction's output, both delta buffers for the largest run the policy allows, the
@@ -952,6 +955,7 @@ struct rh_store {
         }
         if ((rc = bsums.ensure(rh_num_blocks(base) * 32 + 32)) || (rc = ssums.ensure(rh_num_superblocks(base) * 32 + 32)) ||
             (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(rh::sample2_entries(base))) ||
+            (rc = btab.ensure((1ull << rh::search_table_bits(base)) + 2)) || (rc = btabp.ensure(2)) ||
             (rc = dsmp[0].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp[1].ensure(rh_num_blocks(plan) + 1)) ||
             (rc = dsmp2[0].ensure(rh::sample2_entries(plan))) || (rc = dsmp2[1].ensure(rh::sample2_entries(plan))) ||
             (rc = cfps.ensure(plan * 32 + 64)) ||

@@ -60,7 +60,7 @@ __device__ __forceinline__ void load_block_bytes(const uint8_t *base, uint64_t a
 // the wave's range (ballot + lane rank).  Lanes stay busy whatever the mix of record lengths,
 // where one record per lane would leave a wave running its longest record's block count.
 // Longer records are left to k_lift_encoded_long.
-constexpr int ENC_PER_WAVE = 64 * 8;
+constexpr int ENC_PER_WAVE = 64 * 4;
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -81,7 +81,11 @@ __device__ __forceinline__ void record_span(const uint64_t *offs, uint64_t i, ui
 }
 
 // 16 message words of the block at byte `addr` with `blen` valid bytes (bytes past blen are
-// zero): 4 x 16-byte + 1 dword loads from the dword-aligned address, then a funnel shift
+// zero): 4 x 16-byte + 1 dword loads from the dword-aligned address, then a funnel shift.  Past
+// blen: whole words below the boundary word are kept, the boundary word is masked to its valid
+// bytes, the rest are zeroed (compares against constants, selects and an AND per word).  A
+// uniform skip of the funnel shift for all-aligned waves measured no faster (the branch's
+// register copies cost what the 16 shifts did: profiles/r02_s3_encoded_ab.log).
 __device__ __forceinline__ void load_block_fast(const uint8_t *base, uint64_t addr, uint32_t blen, bool partial,
                                                 uint32_t m[16]) {
     const uint64_t a4 = addr & ~3ull;
@@ -96,12 +100,9 @@ __device__ __forceinline__ void load_block_fast(const uint8_t *base, uint64_t ad
 #pragma unroll
     for (int j = 0; j < 16; j++) m[j] = __builtin_amdgcn_alignbit(d[j + 1], d[j], sh);
     if (partial) {
+        const uint32_t jb = blen >> 2, bm = (1u << ((blen & 3u) * 8u)) - 1u;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int valid = (int)blen - 4 * j;
-            const uint32_t mask = valid >= 4 ? 0xFFFFFFFFu : valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u);
-            m[j] &= mask;
-        }
+        for (int j = 0; j < 16; j++) m[j] = (uint32_t)j < jb ? m[j] : ((uint32_t)j == jb ? (m[j] & bm) : 0u);
     }
 }
 

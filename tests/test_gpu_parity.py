@@ -202,6 +202,28 @@ def test_encoded_short_mix(gpu, oracle_lib):
     assert int.from_bytes(bs.cpu().numpy()[0].tobytes(), "little") == tot
 
 
+def test_encoded_word_aligned_ragged(gpu, oracle_lib):
+    """Ragged records whose lengths are all multiples of 4 (every block address dword-aligned:
+    the loader's no-funnel-shift branch, partial blocks ending on a word boundary), then one odd
+    length in the middle, which sends its wave down the funnel-shift branch."""
+    import torch
+    from rsos_hip import lift_encoded
+    rng = np.random.default_rng(17)
+    n = 3000
+    lens = 4 * rng.integers(0, 70, n)
+    lens[:4] = [0, 4, 60, 64]
+    for odd in (False, True):
+        if odd:
+            lens[1500] = 61
+        blobs = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in lens]
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+        data = torch.frombuffer(bytearray(b"".join(blobs) + bytes(8)), dtype=torch.uint8).cuda()
+        fps, _ = lift_encoded(data, torch.from_numpy(offs).cuda())
+        want = oracle_lib.lift_encoded(blobs, threads=8)
+        assert np.array_equal(fps.cpu().numpy(), want), odd
+
+
 @pytest.mark.parametrize("length", [0, 1, 4, 63, 64, 65, 120, 128, 1023, 1024, 1025, 2048, 3000])
 def test_fixed_length_records(gpu, oracle_lib, length):
     """rh_lift_fixed_async: one length for every record (one chunk, exact blocks, multi-chunk),

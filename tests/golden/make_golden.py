@@ -104,7 +104,9 @@ def blake3_spec():
         assert O.blake3(data).hex() == h, n
         out.append({"len": n, "hash": h})
     assert P.blake3(b"abc").hex() == "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"
-    return {"source": "BLAKE3 test_vectors.json, input byte i = i % 251", "vectors": out,
+    return {"source": "BLAKE3 test_vectors.json, input byte i = i % 251 -- RECALLED from the published file, "
+                      "not read from it (no network here); pinned by agreement of the two independent "
+                      "restatements (oracle/pyref.py, oracle/oracle.c)", "vectors": out,
             "abc": "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"}
 
 

@@ -90,6 +90,9 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=0,
                    help="records in the CPU baseline sample (0: min(shard, 10M), ~3 s of serial fill)")
     p.add_argument("--batch", type=int, default=1_000_000, help="config5: records per update batch")
+    p.add_argument("--pipeline", type=int, default=1,
+                   help="config5: 1 = the timed batches through one apply_device_many call (batch i + 1 "
+                        "lifted while batch i's result returns); 0 = one apply_device call per batch")
     p.add_argument("--overwrite", type=float, default=0.0,
                    help="config5: fraction of each batch that re-stamps existing keys (the new - old delta)")
     p.add_argument("--e2e", type=int, default=-1,
@@ -422,10 +425,15 @@ def incremental(args, world, rank, dev, dist):
     counts = [0, 0, 0]
     comp0 = st.stats()["compactions"]
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        c = st.apply_device(batches[args.warmup + k])
-        counts = [a + b for a, b in zip(counts, c)]
+    if args.pipeline:  # the queued batches drained in order by one call
+        for c in st.apply_device_many(batches[args.warmup:args.warmup + args.steps]):
+            counts = [a + b for a, b in zip(counts, c)]
         root_agg = st.aggregate()  # the updated root fingerprint (initial_ranges, rbsr/src/protocol.rs:100)
+    else:
+        for k in range(args.steps):
+            c = st.apply_device(batches[args.warmup + k])
+            counts = [a + b for a, b in zip(counts, c)]
+            root_agg = st.aggregate()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -452,8 +460,11 @@ def incremental(args, world, rank, dev, dist):
                        "parallelism": f"key-range shards x{world}"},
             "batch_counts": {"new": counts[0], "overwritten": counts[1], "deleted": counts[2]},
             "final_size": root.size, "bulk_load_s": round(load_s, 3),
-            "step": "apply_device (lift + sort + base/delta search + delta merge; amortised compaction) "
-                    "+ root aggregate",
+            "step": ("apply_device_many over the K queued batches (each: lift + sort + base/delta search + "
+                     "delta merge, amortised compaction; the next batch lifted while this one's result "
+                     "returns) + the root aggregate" if args.pipeline else
+                     "apply_device per batch (lift + sort + base/delta search + delta merge; amortised "
+                     "compaction) + root aggregate"),
             "compactions_in_timed_steps": stats["compactions"] - comp0, "delta_rows_at_end": stats["delta_rows"],
             "reserved_rows": reserved,
         }

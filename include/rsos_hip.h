@@ -292,6 +292,13 @@ int rh_store_apply(rh_store *store, const rh_columns *host_cols, const uint8_t *
                    uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted);
 int rh_store_apply_device(rh_store *store, const rh_columns *dev_cols, const uint8_t *dev_ops, size_t n,
                           uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted, void *after_stream);
+/* k device batches applied in order, each exactly as rh_store_apply_device would apply it
+ * (dev_ops: k pointers, or NULL for all-insert batches; an entry may be NULL too).  Batch i + 1
+ * is lifted while the host waits for batch i's result, so queued batches keep the device busy
+ * (a replica's write path draining several received batches).  counts (nullable): 3 per batch,
+ * new / overwritten / deleted.  On an error the batches before the failing one stay applied.   */
+int rh_store_apply_device_many(rh_store *store, const rh_columns *dev_cols, const uint8_t *const *dev_ops,
+                               const size_t *n, size_t k, uint64_t *counts, void *after_stream);
 
 /* LSM maintenance.  A batch merges into a sorted signed-delta run (O(batch + delta)); the delta
  * run merges into the base run when it exceeds max(base / divisor, min_rows) rows (default

@@ -971,19 +971,62 @@ struct rh_store {
         if ((rc = resum_base())) return rc;
         return sync();
     }
+    hipEvent_t res_ev = nullptr;  // apply_device_many: the result copy of the batch in flight
+    int sync_event(hipEvent_t ev) {  // sync() for one event: poll ~1 ms, then block
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) return RH_OK;
+            if (e != hipErrorNotReady) return fail(RH_ERR_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1)) break;
+        }
+        RH_HIP(hipEventSynchronize(ev));
+        return RH_OK;
+    }
+    // k batches in order, each exactly as apply_device would apply it; batch i + 1 is lifted (into
+    // the other of two fingerprint buffers) while the host waits for batch i's result, so the
+    // device does not idle between batches.  On an error, batches before the failing one stay
+    // applied, the failing one and those after it are not.
+    DevBuf<uint8_t> lfps2;
+    int apply_device_many(const rh_columns *cs, const uint8_t *const *ops, const size_t *ms, size_t k, uint64_t *out) {
+        int rc;
+        size_t mmax = 0;
+        for (size_t i = 0; i < k; i++) {
+            mmax = std::max(mmax, ms[i]);
+            out[3 * i] = out[3 * i + 1] = out[3 * i + 2] = 0;
+        }
+        if ((rc = lfps.ensure(mmax * 32 + 64)) || (rc = lfps2.ensure(mmax * 32 + 64))) return rc;
+        uint8_t *buf[2] = {lfps.p, lfps2.p};
+        bool lifted = false;
+        for (size_t i = 0; i < k; i++) {
+            const bool pipe = ms[i] > 0 && i + 1 < k && ms[i + 1] > 0;
+            if ((rc = apply_device(cs[i], ops ? ops[i] : nullptr, ms[i], out + 3 * i, buf[i & 1], lifted,
+                                   pipe ? &cs[i + 1] : nullptr, pipe ? ms[i + 1] : 0, buf[(i + 1) & 1])))
+                return rc;
+            lifted = pipe;
+        }
+        return RH_OK;
+    }
     PinnedVec<uint64_t> res_host;  // the batch's 96-byte result block
-    int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3]) {
+    // fps_buf: where the batch's fingerprints are (lifted: already there, from the previous batch
+    // of apply_device_many) or go; nullptr: lfps.  next: a batch to lift into next_fps once this
+    // batch's kernels are queued -- the device runs it while the host waits for this batch's result
+    // (an event on the result copy, not the stream) and enqueues the next batch behind it.
+    int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3], uint8_t *fps_buf = nullptr,
+                     bool lifted = false, const rh_columns *next = nullptr, size_t next_m = 0,
+                     uint8_t *next_fps = nullptr) {
         int rc;
         out[0] = out[1] = out[2] = 0;
         if (m == 0) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
-        if ((rc = lfps.ensure(m * 32 + 64)) || (rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) ||
-            (rc = sops.ensure(m + 64)) ||
-            (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
+        if ((!fps_buf && (rc = lfps.ensure(m * 32 + 64))) || (rc = skeys.ensure(m * kl + 64)) ||
+            (rc = sfps.ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)) || (rc = dops.ensure(m + 64)) ||
+            (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
+        uint8_t *const fps = fps_buf ? fps_buf : lfps.p;
         // 1. lift the batch (delete rows are lifted too and ignored)
-        if ((rc = lift_dispatch(schema, c, m, lfps.p, nullptr, nullptr, nullptr, false, stream))) return rc;
+        if (!lifted && (rc = lift_dispatch(schema, c, m, fps, nullptr, nullptr, nullptr, false, stream))) return rc;
         // 2-5 run without a host round trip: everything is written to the delta run's *other*
         // buffers, and one sync at the end brings back the flags and counts.  A duplicate key
         // then leaves the store exactly as it was (nothing is committed); a tie on the leading
@@ -1027,7 +1070,7 @@ struct rh_store {
         for (int full = 0; full < 2; full++) {
             // 2. key order (+ duplicate / leading-digit-tie flags; the sort zeroes them, and every
             //    other word of the result block is written by a later kernel)
-            RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), lfps.p, ops, m, scratch, skeys.p, sfps.p,
+            RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), fps, ops, m, scratch, skeys.p, sfps.p,
                                     sops.p, r_flags, full == 1, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 3. where each key is now: base and delta runs
@@ -1045,7 +1088,15 @@ struct rh_store {
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             // 5. the one round trip
             RH_HIP(hipMemcpyAsync(host, results.p, 96, hipMemcpyDeviceToHost, stream));
-            if ((rc = sync())) return rc;
+            if (full == 0 && next && next_m) {
+                if (!res_ev) RH_HIP(hipEventCreateWithFlags(&res_ev, hipEventDisableTiming));
+                RH_HIP(hipEventRecord(res_ev, stream));
+                if ((rc = lift_dispatch(schema, *next, next_m, next_fps, nullptr, nullptr, nullptr, false, stream)))
+                    return rc;
+                if ((rc = sync_event(res_ev))) return rc;
+            } else if ((rc = sync())) {
+                return rc;
+            }
             memcpy(&flags, &host[6], 4);
             if (!(flags & 6)) break;  // 2: leading-digit tie, 4: skewed buckets
         }
@@ -1353,7 +1404,7 @@ struct rh_store {
             dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release(); dsblk[k].release();
         }
         staging.release();
-        lfps.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); dheap.release(); heap_len = 0;
+        lfps.release(); lfps2.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); dheap.release(); heap_len = 0;
         dops.release(); cfps.release(); cops.release(); counts.release(); flag.release();
         results.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();
@@ -1366,6 +1417,8 @@ struct rh_store {
         scratch.release();
         if (dep) (void)hipEventDestroy(dep);
         dep = nullptr;
+        if (res_ev) (void)hipEventDestroy(res_ev);
+        res_ev = nullptr;
     }
 };
 
@@ -1767,6 +1820,20 @@ int rh_store_apply_device(rh_store *s, const rh_columns *dev_cols, const uint8_t
     if (n_over) *n_over = c[1];
     if (n_del) *n_del = c[2];
     return RH_OK;
+}
+
+int rh_store_apply_device_many(rh_store *s, const rh_columns *dev_cols, const uint8_t *const *dev_ops,
+                               const size_t *n, size_t k, uint64_t *counts, void *after_stream) {
+    if (!s || (k && (!dev_cols || !n))) return fail(RH_ERR_ARG, "NULL");
+    int rc;
+    for (size_t i = 0; i < k; i++)
+        if ((rc = check_cols(s->schema, &dev_cols[i], n[i]))) return rc;
+    RH_LOCK(s);
+    if ((rc = s->after(after_stream))) return rc;
+    std::vector<uint64_t> c(3 * k + 3);
+    rc = s->apply_device_many(dev_cols, dev_ops, n, k, c.data());
+    if (counts) memcpy(counts, c.data(), 3 * k * sizeof(uint64_t));
+    return rc;
 }
 
 }  // extern "C"

@@ -95,6 +95,8 @@ SIGNATURES = [
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rh_store_apply_device", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), VP]),
+    ("rh_store_apply_device_many", C.c_int, [P, C.POINTER(Columns), C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                             SZ, C.POINTER(C.c_uint64), VP]),
     ("rh_store_compact", C.c_int, [P]),
     ("rh_store_set_compaction", C.c_int, [P, C.c_uint64, C.c_uint64]),
     ("rh_store_set_host_tier", C.c_int, [P, C.c_int, C.c_uint64]),

@@ -18,7 +18,7 @@ u32/u64 keys.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, Iterator, Optional, Sequence, Tuple, Union
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -132,6 +132,29 @@ class GpuFingerprintStore:
                                               C.byref(a), C.byref(b), C.byref(d), _torch_stream()),
                 "rh_store_apply_device")
         return int(a.value), int(b.value), int(d.value)
+
+    def apply_device_many(self, batches, ops=None) -> List[Tuple[int, int, int]]:
+        """apply_device over several device batches in order, in one call: batch i + 1 is lifted
+        while the host waits for batch i's result (rh_store_apply_device_many).  ops: None or one
+        entry (None or m device bytes) per batch.  Returns (new, overwritten, deleted) per batch."""
+        from .device import _check_cols, _columns
+        k = len(batches)
+        if ops is not None and len(ops) != k:
+            raise ValueError("ops must have one entry per batch")
+        cols = (A.Columns * max(k, 1))()
+        ns = (C.c_size_t * max(k, 1))()
+        optr = (C.c_void_p * max(k, 1))()
+        for i, b in enumerate(batches):
+            ns[i] = _check_cols(self.schema, b)
+            cols[i] = _columns(b)
+            o = None if ops is None else ops[i]
+            if o is not None and (o.numel() != ns[i] or not o.is_cuda):
+                raise ValueError("ops must be m device bytes")
+            optr[i] = None if o is None else o.data_ptr()
+        out = (C.c_uint64 * (3 * max(k, 1)))()
+        A.check(A.lib().rh_store_apply_device_many(self._h, cols, None if ops is None else optr, ns, k, out,
+                                                   _torch_stream()), "rh_store_apply_device_many")
+        return [(int(out[3 * i]), int(out[3 * i + 1]), int(out[3 * i + 2])) for i in range(k)]
 
     def compact(self) -> None:
         A.check(A.lib().rh_store_compact(self._h), "rh_store_compact")

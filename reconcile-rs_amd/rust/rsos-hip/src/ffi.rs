@@ -155,6 +155,9 @@ extern "C" {
     pub fn rh_store_apply_device(store: *mut rh_store, dev_cols: *const rh_columns, dev_ops: *const u8, n: usize,
                                  n_new: *mut u64, n_over: *mut u64, n_del: *mut u64,
                                  after_stream: *mut c_void) -> c_int;
+    pub fn rh_store_apply_device_many(store: *mut rh_store, dev_cols: *const rh_columns, dev_ops: *const *const u8,
+                                      n: *const usize, k: usize, counts: *mut u64, after_stream: *mut c_void)
+                                      -> c_int;
     pub fn rh_store_compact(store: *mut rh_store) -> c_int;
     pub fn rh_store_stage(store: *mut rh_store, cols: *const rh_columns, ops: *const u8, n: usize) -> c_int;
     pub fn rh_store_set_host_tier(store: *mut rh_store, enable: c_int, round_max: u64) -> c_int;

@@ -980,3 +980,71 @@ def test_store_device_ranks_skewed_keys(gpu, layout):
              np.zeros(len(extra), np.uint8))
     check(np.concatenate([keys, extra]))
     st.close()
+
+
+@pytest.mark.gpu
+def test_store_apply_device_many_equals_one_by_one(gpu, oracle_lib):
+    """rh_store_apply_device_many (batch i + 1 lifted while batch i's result returns) leaves the
+    store exactly as applying the same batches one call at a time: per-batch counts, root,
+    ranks, selects and every fingerprint, across inserts, overwrites, deletes, an empty batch,
+    a batch whose keys share their leading 8 bytes (the full-sort re-run, with the next batch
+    already lifted), and compactions between batches.  A duplicate key in batch 3 of 5 leaves
+    batches 0-2 applied and the rest not."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema, RsosHipError
+    from rsos_hip.synth import make_records
+    s = RecordSchema.dated("bytes16", "bytes64")
+    base = make_records(s, 300_000, seed=5)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+
+    def batches():
+        out, ops = [], []
+        for k in range(7):
+            if k == 3:  # empty
+                b = {c: t[:0].contiguous() for c, t in make_records(s, 1, seed=50).items()}
+                out.append(b)
+                ops.append(None)
+                continue
+            b = make_records(s, 40_000, seed=100 + k, random_keys=True)
+            if k == 4:  # leading 8 bytes shared by many keys
+                heads = torch.randint(0, 256, (16, 8), dtype=torch.uint8, device="cuda", generator=g)
+                b["keys"][:, :8] = heads[torch.randint(0, 16, (40_000,), device="cuda", generator=g)]
+            rows = torch.randperm(300_000, device="cuda", generator=g)[:5_000]
+            b["keys"][:5_000] = base["keys"][rows]  # overwrites / deletes of resident keys
+            b["phys"][:5_000] = base["phys"][rows] + 7
+            o = torch.zeros(40_000, dtype=torch.uint8, device="cuda")
+            o[:2_000] = 1
+            out.append(b)
+            ops.append(o)
+        return out, ops
+
+    bs, ops = batches()
+    one, many = GpuFingerprintStore(s), GpuFingerprintStore(s)
+    for st in (one, many):
+        st.set_compaction(4, 50_000)  # a compaction every few batches
+        st.load_bulk_device(base)
+    want = [one.apply_device(b, o) for b, o in zip(bs, ops)]
+    got = many.apply_device_many(bs, ops)
+    assert got == want and got[3] == (0, 0, 0)
+    assert many.stats()["compactions"] == one.stats()["compactions"] > 0
+    assert many.size() == one.size() and many.aggregate() == one.aggregate()
+    assert np.array_equal(many.fingerprints(), one.fingerprints())
+    n = one.size()
+    for r in range(0, n, n // 37):
+        k = one.select(r)
+        assert many.select(r) == k and many.rank(k) == r
+    # a duplicate inside batch 3 of 5: 0-2 applied, 3-4 not
+    bs2 = [make_records(s, 20_000, seed=300 + k, random_keys=True) for k in range(5)]
+    bs2[3]["keys"][11] = bs2[3]["keys"][12]
+    ref = GpuFingerprintStore(s)
+    ref.load_bulk_device(base)
+    for b in bs2[:3]:
+        ref.apply_device(b)
+    part = GpuFingerprintStore(s)
+    part.load_bulk_device(base)
+    with pytest.raises(RsosHipError):
+        part.apply_device_many(bs2)
+    assert part.aggregate() == ref.aggregate() and part.size() == ref.size()
+    for st in (one, many, ref, part):
+        st.close()

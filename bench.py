@@ -32,7 +32,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "reconcile-rs_amd"))
+sys.path.insert(0, os.environ.get("RSOS_HIP_TREE") or os.path.join(ROOT, "reconcile-rs_amd"))  # override: A/B of builds
 
 import torch  # noqa: E402
 

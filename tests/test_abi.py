@@ -182,3 +182,12 @@ def test_sharded_routing_is_bisect_right(kind, key):
     assert sh._owners(rows).tolist() == want
     sh.splitters = []
     assert sh._owners(rows).tolist() == [0] * len(rows)
+
+
+def test_apply_device_many_argument_checks(rsos_hip_lib):
+    """rh_store_apply_device_many refuses a NULL store, and NULL column / size arrays for k > 0,
+    before touching a device."""
+    from rsos_hip import _abi as A
+    L = A.lib()
+    assert L.rh_store_apply_device_many(None, None, None, None, 0, None, None) == A.ERR_ARG
+    assert L.rh_store_apply_device_many(None, None, None, None, 3, None, None) == A.ERR_ARG

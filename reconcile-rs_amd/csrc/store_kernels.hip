@@ -785,6 +785,7 @@ __global__ __launch_bounds__(DP_WG) void k_delta_parts(const uint32_t *__restric
     uint32_t sum[DB_PARTS] = {0, 0, 0, 0, 0, 0, 0};
     // a thread's partials are read 8 workgroups at a time, every load issued before the adds: the
     // loop was one load latency per workgroup (87 us for a 12.5 M-row compaction's 24 k partials)
+    // (a batch's ~2 k partials give each thread 4: the 4-wide stage)
     uint64_t g = g0;
     for (; g + PU <= g1; g += PU) {
         uint32_t v[PU][DB_PARTS];
@@ -797,6 +798,17 @@ __global__ __launch_bounds__(DP_WG) void k_delta_parts(const uint32_t *__restric
 #pragma unroll
             for (int k = 0; k < DB_PARTS; k++) sum[k] += v[i][k];  // slot 6: int32 bits, wraps right
     }
+    for (; g + PU / 2 <= g1; g += PU / 2) {
+        uint32_t v[PU / 2][DB_PARTS];
+#pragma unroll
+        for (int i = 0; i < PU / 2; i++)
+#pragma unroll
+            for (int k = 0; k < DB_PARTS; k++) v[i][k] = part[DB_PARTS * (g + i) + k];
+#pragma unroll
+        for (int i = 0; i < PU / 2; i++)
+#pragma unroll
+            for (int k = 0; k < DB_PARTS; k++) sum[k] += v[i][k];
+    }
     for (; g < g1; g++)
 #pragma unroll
         for (int k = 0; k < DB_PARTS; k++) sum[k] += part[DB_PARTS * g + k];
@@ -804,11 +816,29 @@ __global__ __launch_bounds__(DP_WG) void k_delta_parts(const uint32_t *__restric
         __shared__ uint64_t lds[NW * 8];
         Acc a;
         acc_zero(a);
-        for (uint64_t g = g0; g < g1; g++) {
+        uint64_t g2 = g0;
+        for (; g2 + PU / 2 <= g1; g2 += PU / 2) {  // loads first, as above
+            uint64_t v[PU / 2][4];
+#pragma unroll
+            for (int i = 0; i < PU / 2; i++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) v[i][q] = dsum[4 * (g2 + i) + q];
+#pragma unroll
+            for (int i = 0; i < PU / 2; i++) {
+                uint32_t f[8];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    f[2 * q] = (uint32_t)v[i][q];
+                    f[2 * q + 1] = (uint32_t)(v[i][q] >> 32);
+                }
+                acc_add_fp(a, f);
+            }
+        }
+        for (; g2 < g1; g2++) {
             uint32_t f[8];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const uint64_t v = dsum[4 * g + q];
+                const uint64_t v = dsum[4 * g2 + q];
                 f[2 * q] = (uint32_t)v;
                 f[2 * q + 1] = (uint32_t)(v >> 32);
             }
@@ -862,6 +892,21 @@ __global__ __launch_bounds__(DP_WG) void k_delta_parts(const uint32_t *__restric
         }
 #pragma unroll
         for (int i = 0; i < PU; i++) {
+            off[2 * (g + i)] = u;
+            off[2 * (g + i) + 1] = r;
+            u += pu[i];
+            r += pr[i];
+        }
+    }
+    for (; g + PU / 2 <= g1; g += PU / 2) {
+        uint32_t pu[PU / 2], pr[PU / 2];
+#pragma unroll
+        for (int i = 0; i < PU / 2; i++) {
+            pu[i] = part[DB_PARTS * (g + i) + 3];
+            pr[i] = part[DB_PARTS * (g + i) + 4];
+        }
+#pragma unroll
+        for (int i = 0; i < PU / 2; i++) {
             off[2 * (g + i)] = u;
             off[2 * (g + i) + 1] = r;
             u += pu[i];

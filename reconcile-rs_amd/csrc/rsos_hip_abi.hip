@@ -548,6 +548,8 @@ struct rh_store {
     DevBuf<uint8_t> bkeys[2], bfps[2], bsums, ssums;
     DevBuf<uint64_t> bsmp, bsmp2;  // leading digits of every 256th (16th) key: sampled search
     DevBuf<uint32_t> btab;         // the base run's search table over bsmp2 (k_search_table)
+    DevBuf<uint32_t> dtab;         // the delta run's, built before each batch's delta search
+    DevBuf<uint64_t> dtabp;
     DevBuf<uint64_t> btabp;
     rh::SearchTable base_table() const { return rh::SearchTable{btab.p, btabp.p, rh::search_table_bits(nb)}; }
     DevBuf<uint64_t> dsmp[2], dsmp2[2];  // the same for each delta buffer (written by its merge)
@@ -796,6 +798,7 @@ struct rh_store {
         }
         return RH_OK;
     }
+    static constexpr uint64_t DTAB_MIN = 1ull << 16;  // delta rows from which the delta search uses a table
     hipEvent_t dep = nullptr;  // orders the store's stream after a producer stream
     int after(void *producer) {
         if (!dep) RH_HIP(hipEventCreateWithFlags(&dep, hipEventDisableTiming));
@@ -956,6 +959,7 @@ struct rh_store {
         if ((rc = bsums.ensure(rh_num_blocks(base) * 32 + 32)) || (rc = ssums.ensure(rh_num_superblocks(base) * 32 + 32)) ||
             (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(rh::sample2_entries(base))) ||
             (rc = btab.ensure((1ull << rh::search_table_bits(base)) + 2)) || (rc = btabp.ensure(2)) ||
+            (rc = dtab.ensure((1ull << rh::search_table_bits(plan)) + 2)) || (rc = dtabp.ensure(2)) ||
             (rc = dsmp[0].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp[1].ensure(rh_num_blocks(plan) + 1)) ||
             (rc = dsmp2[0].ensure(rh::sample2_entries(plan))) || (rc = dsmp2[1].ensure(rh::sample2_entries(plan))) ||
             (rc = cfps.ensure(plan * 32 + 64)) ||
@@ -1076,8 +1080,17 @@ struct rh_store {
             // 3. where each key is now: base and delta runs
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, skeys.p, m, rank_b, present_b, stream,
                                         base_table()));
+            // a delta run of more than a few blocks is searched through a table over its stride-8
+            // samples too (one L2-resident table line instead of a binary search of the stride-256
+            // samples); the table is built here, where the run's row count is known on the host
+            rh::SearchTable dt{};
+            if (nd >= DTAB_MIN) {
+                if ((rc = dtab.ensure((1ull << rh::search_table_bits(nd)) + 2)) || (rc = dtabp.ensure(2))) return rc;
+                if (full == 0) RH_HIP(rh::launch_search_table(dsmp2[cd].p, nd, dtab.p, dtabp.p, stream));
+                dt = rh::SearchTable{dtab.p, dtabp.p, rh::search_table_bits(nd)};
+            }
             RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, skeys.p, m, rank_d, present_d,
-                                        stream));
+                                        stream, dt));
             // 4. the batch's delta records and counts, merged into the delta run's other buffer
             //    (one pass: the merged run, its block sums, count prefixes and search samples)
             RH_HIP(rh::launch_delta_apply(schema.key_kind, (int)kl, sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p,
@@ -1399,7 +1412,7 @@ struct rh_store {
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dslot[k].release();
         }
-        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); btab.release(); btabp.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); dscnt.release(); fin_ticket.release(); mcnt.release();
+        bsums.release(); ssums.release(); tot.release(); bsmp.release(); bsmp2.release(); btab.release(); btabp.release(); dtab.release(); dtabp.release(); dsmp[0].release(); dsmp[1].release(); dsmp2[0].release(); dsmp2[1].release(); dscnt.release(); fin_ticket.release(); mcnt.release();
         for (int k = 0; k < 2; k++) {
             dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release(); dsblk[k].release();
         }

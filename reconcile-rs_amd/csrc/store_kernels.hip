@@ -1242,6 +1242,27 @@ __global__ void k_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *
 // batch-scatter pass and a re-read of the whole run for its sums.
 constexpr int MT = 2048;  // output rows per workgroup (8 blocks of 256; 2,048 measured best of 1,024 / 2,048 / 4,096)
 
+// The first index in [lo, hi) whose predicate holds (hi if none), for a predicate that is false
+// then true along the range, searched by one whole wave: each step probes 64 evenly spaced
+// positions at once and keeps the 1/64 of the range between the last false and the first true
+// probe -- ~4 dependent loads for a million entries where a one-lane binary search makes ~20.
+// Every lane of the wave calls it and gets the result.
+template <typename Pred>
+__device__ __forceinline__ uint64_t wave_partition_point(uint64_t lo, uint64_t hi, Pred pred) {
+    const uint32_t lane = threadIdx.x & 63;
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        uint64_t p = lo + (lane + 1) * step - 1;
+        p = p < hi ? p : hi - 1;
+        const uint32_t n = (uint32_t)__popcll(__ballot(!pred(p)));  // probes before the boundary
+        const uint64_t nlo = lo + n * step, nhi = lo + (n + 1) * step;
+        lo = nlo < hi ? nlo : hi;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t p = lo + lane;
+    return lo + (uint64_t)__popcll(__ballot(p < hi && !pred(p)));
+}
+
 // smallest k in [lo, hi] with k == R or rlist[k] - k > s: the number of removed A rows before
 // the s-th survivor
 __device__ __forceinline__ uint64_t survivor_k(const uint32_t *rlist, uint64_t R, uint64_t lo, uint64_t hi, uint64_t s) {
@@ -1279,18 +1300,24 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
     const uint64_t U = counts[3], R = counts[4];
     const uint64_t nC = nA + U - R;  // <= nA + m
     const uint64_t o0 = (uint64_t)blockIdx.x * MT;
-    if (t == 0) {
+    if (t < 64) {  // the tile's bounds in the upsert and removed-row lists: wave 0 searches them
         uint64_t o1 = o0, ju0 = 0, ju1 = 0, s0 = 0, k0 = 0, k1 = 0;
         if (o0 < nC) {
             o1 = o0 + MT < nC ? o0 + MT : nC;
-            ju0 = lower_bound_u32(upos, 0, U, o0);
-            ju1 = lower_bound_u32(upos, ju0, U, o1);
+            ju0 = wave_partition_point(0, U, [&](uint64_t i) { return (uint64_t)upos[i] >= o0; });
+            ju1 = wave_partition_point(ju0, U, [&](uint64_t i) { return (uint64_t)upos[i] >= o1; });
             s0 = o0 >= ju0 ? o0 - ju0 : 0;
             const uint64_t s1 = o1 >= ju1 ? o1 - ju1 : 0;
-            k0 = survivor_k(rlist, R, 0, R, s0);
-            k1 = survivor_k(rlist, R, k0, R, s1);
+            // survivor_k's predicate: k == R or rlist[k] - k > s, over k in [lo, R]
+            auto gone = [&](uint64_t s_) {
+                return [=](uint64_t k) { return k >= R || (int64_t)rlist[k] - (int64_t)k > (int64_t)s_; };
+            };
+            k0 = wave_partition_point(0, R, gone(s0));
+            k1 = wave_partition_point(k0, R, gone(s1));
         }
-        prm[0] = o1 - o0; prm[1] = ju0; prm[2] = ju1; prm[3] = s0; prm[4] = k0; prm[5] = k1;
+        if (t == 0) {
+            prm[0] = o1 - o0; prm[1] = ju0; prm[2] = ju1; prm[3] = s0; prm[4] = k0; prm[5] = k1;
+        }
     }
     for (uint32_t q = t; q < MT; q += 256) src[q] = -1;
     __syncthreads();

@@ -269,6 +269,15 @@ int rh_store_protocol_round(rh_store *store, int policy, uint64_t fan_out, const
  * (query.rs:25-167).  Larger rounds stay on the device.  round_max 0 = the default (128).
  * enable = 0 frees the copy.  Answers are identical either way.                              */
 int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
+/* The tier after a batch (host_tier.hpp, host_delta.hpp): the tier holds a copy of the device's
+ * base run plus a B+ tree of the signed deltas of every batch since (the device's own DeltaRecs,
+ * count and contribution per touched key), so a batch updates it in O(batch log n) -- the
+ * reference's O(log n) per insert (mutate.rs:23-88) -- and only a base copy older than
+ * max(base / 8, 2^16) delta entries, a load, or a moved tier buffer costs the O(n) copy again.
+ * Stats (nullable): base rows and delta entries of a fresh tier (0, 0 when stale), full refreshes
+ * and batch folds so far.                                                                       */
+int rh_store_tier_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_entries, uint64_t *refreshes,
+                        uint64_t *folds);
 
 /* Staged single-record updates: Rsos::insert / delete one record at a time (mutate.rs:23-154)
  * without one device round trip each.  rh_store_stage appends m host rows (columns as for

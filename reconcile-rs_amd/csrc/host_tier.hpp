@@ -5,14 +5,18 @@
 // map asks ~155 aggregate, ~152 rank and ~70 select questions (benches/README.md:579-585), each
 // O(log n) on the reference's FingerprintTreeMap (query.rs:25-167), ~45 us in all.  One device
 // round trip per round costs more than that.  The host tier keeps, next to the HBM-resident store,
-//   - the keys in rank order (what select() returns, rbsr/src/rsos_view.rs:70),
-//   - the exclusive prefix sums of the per-row fingerprints, P[i] = Σ lift(row j), j < i, mod 2^256,
-//     computed on the device (launch_prefix) from the fingerprints the GPU lift produced, so
-//     summary-folds-lift holds by construction (rsos_trait.rs:46-60): aggregate over rank range
-//     [lo, hi) = (P[hi] - P[lo], hi - lo) -- the Fingerprint group's inverse (fingerprint.rs:159-173),
-//   - the leading 8 key bytes (order-preserving) of every 64th key, so a rank is a search of a
-//     cache-resident sample array and then of one 64-key window.
-// It is refreshed from the device on the first question after the store changes.
+//   - the base run: its keys in rank order and the exclusive prefix sums of its per-row
+//     fingerprints, P[i] = Σ lift(row j), j < i, mod 2^256, computed on the device (launch_prefix)
+//     from the fingerprints the GPU lift produced, so summary-folds-lift holds by construction
+//     (rsos_trait.rs:46-60), plus the leading 8 key bytes (order-preserving) of every 64th key, so
+//     a base rank is a search of a cache-resident sample array and then of one 64-key window;
+//   - the delta run: every batch since the base was copied, as the signed deltas the device
+//     computed for it (host_delta.hpp), folded in per batch -- O(batch), not O(n).
+// A question composes the two as the device does and as FingerprintTreeMap composes its cached
+// aggregates (mutate.rs:31-41, :93-154): rank(z) = rank_B(z) + Σ count deltas below z, the prefix
+// of the fingerprints at z = P[rank_B(z)] + Σ contribs below z, and an aggregate is the
+// difference of two prefixes -- the Fingerprint group's inverse (fingerprint.rs:159-173).  The
+// base part is copied down again only when the device base changes (a compaction), not per batch.
 #pragma once
 #include <algorithm>
 #include <cmath>
@@ -21,55 +25,85 @@
 #include <vector>
 
 #include "../../include/rsos_hip.h"
+#include "host_delta.hpp"
 #include "internal.hpp"
 
 namespace rh {
 
 struct HostTier {
+    KeyOrder ko;
     uint32_t kl = 0;
-    int kk = RH_KEY_BYTES;
-    uint64_t n = 0;
-    const uint8_t *keys = nullptr;     // n * kl bytes, rank order
-    const uint64_t *prefix = nullptr;  // (n + 1) * 4 LE limbs
+    uint64_t nb = 0;                   // base rows
+    uint64_t n = 0;                    // live keys: nb + Σ count deltas
+    const uint8_t *keys = nullptr;     // nb * kl bytes, rank order
+    const uint64_t *prefix = nullptr;  // (nb + 1) * 4 LE limbs
     std::vector<uint64_t> samp;        // digit(keys[64 j])
+    DeltaTree dt;
     static constexpr unsigned SHIFT = 6;
 
-    // an order-preserving u64 of a key's leading bytes: the integer for u32 / u64 keys, the first 8
-    // bytes big-endian for byte keys (memcmp order, the Ord of [u8; L])
-    uint64_t digit(const uint8_t *k) const {
-        if (kk == RH_KEY_U32) {
-            uint32_t v;
-            memcpy(&v, k, 4);
-            return v;
-        }
-        uint64_t v;
-        memcpy(&v, k, 8);
-        return kk == RH_KEY_U64 ? v : __builtin_bswap64(v);
-    }
-    int cmp(const uint8_t *a, const uint8_t *b) const {
-        const uint64_t x = digit(a), y = digit(b);
-        if (x != y) return x < y ? -1 : 1;
-        return kk == RH_KEY_BYTES && kl > 8 ? memcmp(a + 8, b + 8, kl - 8) : 0;
-    }
+    uint64_t digit(const uint8_t *k) const { return ko.digit(k); }
+    int cmp(const uint8_t *a, const uint8_t *b) const { return ko.cmp(a, b); }
     void build(uint32_t key_len, int key_kind, uint64_t rows, const uint8_t *k, const uint64_t *p) {
+        ko = KeyOrder{key_len, key_kind};
         kl = key_len;
-        kk = key_kind;
-        n = rows;
+        nb = n = rows;
         keys = k;
         prefix = p;
+        dt.set_order(ko);
         samp.clear();
         if (!keys) return;  // the encoded store keeps its keys on the host side of the ABI
-        samp.resize((n + 63) >> SHIFT);
+        samp.resize((nb + 63) >> SHIFT);
         for (uint64_t j = 0; j < samp.size(); j++) samp[j] = digit(keys + (j << SHIFT) * kl);
     }
-    // rank(z) = number of keys strictly below z (query.rs:93-121)
-    uint64_t rank(const uint8_t *key) const {
-        if (n == 0) return 0;
+    // forget everything (tier off)
+    void reset() {
+        build(0, RH_KEY_BYTES, 0, nullptr, nullptr);
+        samp = std::vector<uint64_t>();
+        segs = std::vector<Seg>();
+    }
+    bool plain() const { return dt.size() == 0; }
+    // One batch row's entry formed against this tier's own base: the rule of k_delta_build
+    // (store_kernels.hip) -- an upsert is (cur - base, 1 - in_base, live), a delete of a base key
+    // (-base, -1, dead), a delete of any other key drops the key's entry (returns true).
+    // cur == nullptr: a delete.
+    bool entry_vs_base(const uint8_t *key, const uint64_t *cur, DeltaTree::Rec *r) const {
+        const uint64_t b = rank_b(key);
+        const bool in_b = b < nb && cmp(keys + b * kl, key) == 0;
+        r->key = key;
+        if (cur) memcpy(r->fp, cur, 32);
+        else memset(r->fp, 0, 32);
+        if (in_b) {
+            uint64_t base[4];
+            memcpy(base, prefix + 4 * (b + 1), 32);
+            fp4_sub(base, prefix + 4 * b);
+            fp4_sub(r->fp, base);
+        }
+        r->cnt = (int8_t)((cur ? 1 : 0) - (in_b ? 1 : 0));
+        r->live = cur != nullptr;
+        return !cur && !in_b;
+    }
+    // m sorted, distinct rows into the delta tree; drop[j]: remove row j's key.  A batch large
+    // against the tree is one merge pass over the whole tree instead of m walks.
+    void fold(const DeltaTree::Rec *rows, const uint8_t *drop, size_t m) {
+        if (m > 256 && m * 16 > dt.size()) {
+            dt.merge_rebuild(rows, drop, m);
+        } else {
+            for (size_t j = 0; j < m; j++) {
+                if (drop[j]) dt.erase(rows[j].key);
+                else dt.upsert(rows[j]);
+            }
+        }
+        n = (uint64_t)((int64_t)nb + dt.cnt_total());
+    }
+
+    // base rows with key < z
+    uint64_t rank_b(const uint8_t *key) const {
+        if (nb == 0) return 0;
         const uint64_t d = digit(key);
         const uint64_t jl = std::lower_bound(samp.begin(), samp.end(), d) - samp.begin();
         const uint64_t jh = std::upper_bound(samp.begin() + jl, samp.end(), d) - samp.begin();
         uint64_t lo = jl ? ((jl - 1) << SHIFT) + 1 : 0;  // keys[64 (jl - 1)] < key
-        uint64_t hi = std::min<uint64_t>(n, jh << SHIFT);  // keys[64 jh] > key
+        uint64_t hi = std::min<uint64_t>(nb, jh << SHIFT);  // keys[64 jh] > key
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
             if (cmp(keys + mid * kl, key) < 0) lo = mid + 1;
@@ -77,27 +111,146 @@ struct HostTier {
         }
         return lo;
     }
+
+    // A place in the merged key order: r live keys below it, b base rows below it, d delta entries
+    // below it; k = the live key at rank r (set by at(), r < n).
+    struct Cur {
+        uint64_t r = 0, b = 0, d = 0;
+        const uint8_t *k = nullptr;
+    };
+    Cur begin() const { return Cur{0, 0, 0, nullptr}; }
+    Cur end() const { return Cur{n, nb, dt.size(), nullptr}; }
+    // keys < z
+    Cur lt(const uint8_t *z) const {
+        Cur c;
+        c.b = rank_b(z);
+        if (plain()) {
+            c.r = c.b;
+            return c;
+        }
+        const DeltaTree::Pos p = dt.lt(z);
+        c.d = p.idx;
+        c.r = (uint64_t)((int64_t)c.b + p.cnt);
+        return c;
+    }
+    // keys <= z
+    Cur le(const uint8_t *z) const {
+        Cur c;
+        c.b = rank_b(z);
+        if (c.b < nb && cmp(keys + c.b * kl, z) == 0) c.b++;
+        if (plain()) {
+            c.r = c.b;
+            return c;
+        }
+        const DeltaTree::Pos p = dt.lt(z);
+        c.d = p.idx + (p.found ? 1 : 0);
+        c.r = (uint64_t)((int64_t)c.b + p.cnt + (p.found ? p.fcnt : 0));
+        return c;
+    }
+    // select: the place of the r-th live key (r <= n; r == n is end())
+    Cur at(uint64_t r) const {
+        if (r >= n) return end();
+        if (plain()) return Cur{r, r, 0, keys + r * kl};
+        // F(b) = live keys <= base key b, non-decreasing in b; find the smallest b with F(b) > r.
+        // |F(b) - b| <= delta entries + 1 brackets the search.
+        const uint64_t nd = dt.size();
+        uint64_t lo = r > nd ? r - nd : 0, hi = std::min<uint64_t>(nb, r + nd + 1);
+        auto F = [&](uint64_t b, DeltaTree::Pos *pp) {
+            const DeltaTree::Pos p = dt.lt(keys + b * kl);
+            if (pp) *pp = p;
+            return (uint64_t)((int64_t)b + 1 + p.cnt + (p.found ? p.fcnt : 0));
+        };
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (F(mid, nullptr) > r) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint64_t b = lo;
+        if (b < nb) {
+            DeltaTree::Pos p;
+            const uint64_t f = F(b, &p);
+            const bool live = !p.found || p.flive;
+            if (live && f - 1 == r) return Cur{r, b, p.idx, keys + b * kl};
+        }
+        // the r-th live key is an inserted delta key between base keys b - 1 and b: every delta
+        // entry in that gap is one (a key not in the base is in the delta run only while live)
+        uint64_t fprev = 0, d0 = 0;
+        if (b > 0) {
+            DeltaTree::Pos q;
+            fprev = F(b - 1, &q);
+            d0 = q.idx + (q.found ? 1 : 0);
+        }
+        const uint64_t d = d0 + (r - fprev);
+        return Cur{r, b, d, dt.key_at(d)};
+    }
+    // Σ fingerprints of the live keys below c
+    void pre(const Cur &c, uint64_t out[4]) const {
+        memcpy(out, prefix + 4 * c.b, 32);
+        if (!plain() && c.d) {
+            uint64_t t[4];
+            dt.fp_prefix(c.d, t);
+            fp4_add(out, t);
+        }
+    }
+    // aggregate between two places (ZERO when hi is below lo: the inverted range)
+    void agg(const Cur &lo, const Cur &hi, rh_aggregate *o) const {
+        if (hi.r <= lo.r) {
+            memset(o, 0, sizeof *o);
+            return;
+        }
+        uint64_t a[4], b[4];
+        pre(hi, a);
+        pre(lo, b);
+        fp4_sub(a, b);
+        memcpy(o->fingerprint, a, 32);
+        o->size = hi.r - lo.r;
+    }
+    // rank(z) = number of keys strictly below z (query.rs:93-121)
+    uint64_t rank(const uint8_t *key) const { return lt(key).r; }
     // Aggregate over rank range [lo, hi), clamped as the device query clamps (hi <= n, lo <= hi)
     void agg(uint64_t lo, uint64_t hi, rh_aggregate *o) const {
         if (hi > n) hi = n;
         if (lo > hi) lo = hi;
-        const uint64_t *a = prefix + 4 * hi, *b = prefix + 4 * lo;
-        unsigned char borrow = 0;
-        for (int q = 0; q < 4; q++) {
-            const uint64_t x = a[q], y = b[q];
-            const uint64_t d = x - y - borrow;
-            borrow = (x < y) || (x == y && borrow);
-            o->fingerprint[q] = d;
+        if (plain()) {
+            uint64_t a[4];
+            memcpy(a, prefix + 4 * hi, 32);
+            fp4_sub(a, prefix + 4 * lo);
+            memcpy(o->fingerprint, a, 32);
+            o->size = hi - lo;
+            return;
         }
-        o->size = hi - lo;
+        agg(at(lo), at(hi), o);
     }
-    // rank of a bound: kind 0 = unbounded (lower: 0, upper: n), 1 = included, 2 = excluded
-    uint64_t bound_rank(int kind, const uint8_t *key, bool lower) const {
-        if (kind == 0) return lower ? 0 : n;
-        const uint64_t r = rank(key);  // keys < key
-        const bool present = r < n && cmp(keys + r * kl, key) == 0;
-        if (lower) return kind == 1 ? r : r + present;   // Included(k): k.., Excluded(k): k is out
-        return kind == 2 ? r : r + present;              // Excluded(k): ..k, Included(k): ..=k
+    // place of a bound: kind 0 = unbounded (lower: begin, upper: end), 1 = included, 2 = excluded
+    Cur bound(int kind, const uint8_t *key, bool lower) const {
+        if (kind == 0) return lower ? begin() : end();
+        if (lower) return kind == 1 ? lt(key) : le(key);  // Included(k): k.., Excluded(k): k is out
+        return kind == 2 ? lt(key) : le(key);             // Excluded(k): ..k, Included(k): ..=k
+    }
+    // the keys of ranks [lo, hi) (hi <= n), in order
+    void copy_keys(uint64_t lo, uint64_t hi, uint8_t *out) const {
+        if (hi <= lo) return;
+        if (plain()) {
+            memcpy(out, keys + lo * kl, (hi - lo) * kl);
+            return;
+        }
+        const Cur c = at(lo);
+        uint64_t b = c.b;
+        DeltaTree::Iter it = dt.iter(c.d);
+        for (uint64_t r = lo; r < hi;) {
+            const int s = !it.l ? -1 : b >= nb ? 1 : cmp(keys + b * kl, it.key());
+            if (s < 0) {  // a base key the delta run does not touch
+                memcpy(out, keys + b * kl, kl);
+                out += kl, r++, b++;
+            } else {
+                if (it.live()) {  // inserted (s > 0) or overwritten (s == 0)
+                    memcpy(out, it.key(), kl);
+                    out += kl, r++;
+                }
+                if (s == 0) b++;
+                it.advance();
+            }
+        }
     }
 
     // ---- one protocol round (protocol_round_with_policy, rbsr/src/protocol.rs:212-317) ------------
@@ -108,7 +261,8 @@ struct HostTier {
     // with the ZERO aggregate, a SPLIT's children cut at every stride-th rank (:288-313).
     struct Seg {
         int kind;  // 0 skip, 1 IDLIST, 2 SPLIT, 3 dropped
-        uint64_t stride, si, ei, children, enums;
+        uint64_t stride, children, enums;
+        Cur cs, ce;
         rh_aggregate loc;
     };
     std::vector<Seg> segs;
@@ -121,13 +275,10 @@ struct HostTier {
         uint64_t nc = 0, ne = 0, cnt[5] = {0, 0, 0, 0, 0};
         for (size_t j = 0; j < r; j++) {
             Seg &g = segs[j];
-            const uint64_t l = sk[j] ? rank(skeys + j * kl) : 0, h = ek[j] ? rank(ekeys + j * kl) : n;
-            agg(l, h, &g.loc);
+            g = Seg{3, 0, 0, 0, sk[j] ? lt(skeys + j * kl) : begin(), ek[j] ? lt(ekeys + j * kl) : end(), {}};
+            agg(g.cs, g.ce, &g.loc);
             const rh_aggregate &R = in.aggregates[j];
-            g = Seg{3, 0, 0, 0, 0, 0, g.loc};
-            if (h >= l) {
-                g.si = std::min(l, n);
-                g.ei = std::min(h, n);
+            if (g.ce.r >= g.cs.r) {
                 const uint64_t span = g.loc.size, rem = R.size;
                 uint64_t st = 0;
                 int k;
@@ -148,7 +299,7 @@ struct HostTier {
                     g.enums = 1;
                     g.children = rem != 0;
                 } else if (k == 2) {
-                    g.children = (g.ei > g.si ? (g.ei - g.si - 1) / st : 0) + 1;
+                    g.children = (g.ce.r > g.cs.r ? (g.ce.r - g.cs.r - 1) / st : 0) + 1;
                 }
             }
             cnt[g.kind == 3 ? 4 : g.kind]++;
@@ -190,12 +341,13 @@ struct HostTier {
                     child(sk[j], s0, ek[j], e0, g.loc);
                     continue;
                 }
+                Cur lo = g.cs;
                 for (uint64_t k = 0; k <= ncuts; k++) {
-                    const uint64_t lo = g.si + k * g.stride, hi = k == ncuts ? g.ei : g.si + (k + 1) * g.stride;
+                    const Cur hi = k == ncuts ? g.ce : at(g.cs.r + (k + 1) * g.stride);
                     rh_aggregate a;
                     agg(lo, hi, &a);
-                    child(k ? 1 : sk[j], k ? keys + lo * kl : s0, k != ncuts ? 1 : ek[j], k != ncuts ? keys + hi * kl : e0,
-                          a);
+                    child(k ? 1 : sk[j], k ? lo.k : s0, k != ncuts ? 1 : ek[j], k != ncuts ? hi.k : e0, a);
+                    lo = hi;
                 }
             }
         }

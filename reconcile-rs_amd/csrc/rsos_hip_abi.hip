@@ -145,9 +145,11 @@ struct DevBuf {
         cap = bytes / sizeof(T);
         return RH_OK;
     }
-    // grow to n elements keeping the first `used` ones (ordered on `st`)
+    // grow to n elements keeping the first `used` ones (ordered on `st`); geometric, as ensure():
+    // an unreserved store's record heap gains a batch per call and must not copy itself each time
     int grow_keep(size_t n, size_t used, hipStream_t st) {
         if (n <= cap && p) return RH_OK;
+        if (p) n = std::max(n, cap + cap / 2);
         T *q = nullptr;
         const size_t bytes = ((std::max<size_t>(n, 1) * sizeof(T)) + 255) & ~size_t(255);
         hipError_t e = hipMalloc(&q, bytes);
@@ -597,6 +599,7 @@ struct rh_store {
         memset(root_b, 0, sizeof root_b);
         memset(root_d, 0, sizeof root_d);
         version++;
+        base_epoch++;
     }
     // ---- the pending batch (rh_store_stage) --------------------------------------------------------
     // Single-record inserts and deletes (Rsos::insert / delete, FingerprintTreeMap::insert /
@@ -682,17 +685,29 @@ struct rh_store {
         return apply_device(staging.view(schema), hops.p, m, c);
     }
     // ---- the host tier (host_tier.hpp) ---------------------------------------------------------
+    // The tier answers from (its copy of a base run) + (its delta tree: every batch since).  It is
+    // fresh while tier_version == version.  A batch keeps it fresh by folding the batch's signed
+    // deltas into the tree (fold_batch, O(batch)); only a load, a tree grown past the policy's bound,
+    // or a change to the tier's buffers sends the next question through tier_refresh (compact, copy
+    // the whole base down: O(n)).
     uint64_t version = 0;       // bumped by every change of contents (load, batch, failed load)
+    uint64_t base_epoch = 0;    // bumped whenever the device's base run changes (load, compaction)
     bool tier_on = false;
     uint64_t tier_version = ~0ull, tier_round_max = 128;
+    uint64_t tier_epoch = ~0ull;  // the device base the tier's copy is (while they agree, the
+                                  // device's DeltaRecs are relative to the tier's base too)
+    uint64_t tier_refreshes = 0, tier_folds = 0;
     rh::HostTier tier;
     PinnedVec<uint8_t> tier_keys;
     PinnedVec<uint64_t> tier_prefix;
     DevBuf<uint8_t> tier_dpre, tier_spre, tier_bpre;
     std::vector<uint8_t> tier_out;  // the last host round, in round_layout()
+    // a batch's rows as the fold reads them: sorted keys, and either the device's DeltaRecs + drop
+    // flags (tier base == device base) or the sorted fingerprints + ops (the tier's own base)
+    PinnedVec<uint8_t> fold_keys, fold_recs, fold_ops;
     bool tier_fresh() const { return tier_on && tier_version == version; }
     // bring the host tier up to date: compact, the prefix sums on the device, one copy of the keys
-    // and one of the prefix sums down.  Costs ~(kl + 32) B per row of PCIe, once per change.
+    // and one of the prefix sums down.  Costs ~(kl + 32) B per row of PCIe, once per base change.
     int tier_refresh() {
         int rc;
         if ((rc = compact())) return rc;
@@ -713,7 +728,76 @@ struct rh_store {
         }
         tier.build((uint32_t)kl, schema.key_kind, n, tier_keys.data(), tier_prefix.data());
         tier_version = version;
+        tier_epoch = base_epoch;
+        tier_refreshes++;
         return RH_OK;
+    }
+    // How a batch reaches the tier (decided before the batch, under the lock):
+    //   0: it does not (tier off or stale: the next question refreshes it anyway),
+    //   1: from the device's DeltaRecs (the tier's base is the device's: contribs relative to it),
+    //   2: from the batch's sorted fingerprints and ops, the deltas formed against the tier's own
+    //      base on the host (the device compacted since the tier's copy was taken).
+    int fold_mode() const {
+        if (!tier_fresh()) return 0;
+        return tier_epoch == base_epoch ? 1 : 2;
+    }
+    // enqueue the copies fold_batch reads (behind the batch's merge, before its result copy)
+    int fold_copies(int mode, const uint8_t *sorted_keys, const uint8_t *sorted_fps, const uint8_t *sorted_ops,
+                    const uint8_t *recs, const uint8_t *drop, size_t m) {
+        try {
+            fold_keys.resize(m * kl + 8);
+            fold_recs.resize(m * (mode == 1 ? sizeof(rh::DeltaRec) : 32) + 8);
+            fold_ops.resize(m + 8);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+        }
+        RH_HIP(hipMemcpyAsync(fold_keys.data(), sorted_keys, m * kl, hipMemcpyDeviceToHost, stream));
+        if (mode == 1) {
+            RH_HIP(hipMemcpyAsync(fold_recs.data(), recs, m * sizeof(rh::DeltaRec), hipMemcpyDeviceToHost, stream));
+            RH_HIP(hipMemcpyAsync(fold_ops.data(), drop, m, hipMemcpyDeviceToHost, stream));
+        } else {
+            RH_HIP(hipMemcpyAsync(fold_recs.data(), sorted_fps, m * 32, hipMemcpyDeviceToHost, stream));
+            RH_HIP(hipMemcpyAsync(fold_ops.data(), sorted_ops, m, hipMemcpyDeviceToHost, stream));
+        }
+        return RH_OK;
+    }
+    // After the batch committed (the copies have landed): the batch's rows into the tier's delta
+    // tree, in key order -- the same rule as k_delta_build: an upsert's entry is (cur - base,
+    // 1 - in_base, live), a delete of a base key (-base, -1, dead), a delete of any other key drops
+    // its entry.  Keeps the tier fresh; a tree past max(base / 8, 2^16) entries is left stale
+    // instead (the next question copies the base again, resetting the tree).
+    std::vector<rh::DeltaTree::Rec> fold_rows;
+    std::vector<uint8_t> fold_drop;
+    void fold_batch(int mode, size_t m) {
+        rh::HostTier &t = tier;
+        const uint64_t limit = std::max<uint64_t>(t.nb / 8, 1ull << 16);
+        if (t.dt.size() + m > limit) return;  // stays stale
+        try {
+            fold_rows.resize(m);
+            fold_drop.resize(m);
+        } catch (const std::bad_alloc &) {
+            return;
+        }
+        const uint8_t *K = fold_keys.data();
+        for (size_t j = 0; j < m; j++) {
+            rh::DeltaTree::Rec &r = fold_rows[j];
+            r.key = K + j * kl;
+            if (mode == 1) {
+                const rh::DeltaRec *d = reinterpret_cast<const rh::DeltaRec *>(fold_recs.data()) + j;
+                memcpy(r.fp, d->contrib, 32);
+                const bool in_b = d->flags & rh::DeltaRec::IN_BASE, live = d->flags & rh::DeltaRec::LIVE;
+                r.cnt = (int8_t)((live ? 1 : 0) - (in_b ? 1 : 0));
+                r.live = live;
+                fold_drop[j] = fold_ops[j] != 0;
+            } else {
+                uint64_t cur[4];
+                memcpy(cur, fold_recs.data() + 32 * j, 32);
+                fold_drop[j] = t.entry_vs_base(r.key, fold_ops[j] ? nullptr : cur, &r);
+            }
+        }
+        t.fold(fold_rows.data(), fold_drop.data(), m);
+        tier_version = version;
+        tier_folds++;
     }
     // Wait for the stream by polling it: the batch path ends in one short wait for a 96-byte
     // result, where an interrupt-driven wake-up costs tens of microseconds per batch.  Long
@@ -821,6 +905,7 @@ struct rh_store {
         // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         version++;
+        base_epoch++;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
             (rc = counts.ensure(4)))
             return rc;
@@ -849,14 +934,19 @@ struct rh_store {
     }
     // page-locked host tier capacity for `rows` rows ahead of the refresh that fills it: pinning
     // fresh pages is most of a first refresh (11-13 ms at 10^6 rows against ~1 ms of copying)
+    // A buffer the tier reads that moves (a larger reservation re-pins and copies) leaves the tier
+    // stale: its pointers are re-taken by the next refresh, never read after the move.
     int tier_reserve(uint64_t rows) {
         if (!tier_on) return RH_OK;
+        const void *k0 = tier_keys.p, *p0 = tier_prefix.p;
         try {
             tier_keys.reserve(rows * kl + 64);
             tier_prefix.reserve((rows + 1) * 4 + 8);
         } catch (const std::bad_alloc &) {
+            tier_version = ~0ull;
             return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
         }
+        if (tier_keys.p != k0 || tier_prefix.p != p0) tier_version = ~0ull;
         return RH_OK;
     }
     int load_finish(size_t m, bool last_wins) {
@@ -920,6 +1010,7 @@ struct rh_store {
         uint64_t *c = res_host.data();
         RH_HIP(hipMemcpyAsync(c, mcnt.p, 24, hipMemcpyDeviceToHost, stream));
         const uint64_t want = size(), nb_old = nb;
+        base_epoch++;  // same contents, a new base: the tier's copy stays valid, not the device's deltas
         cb = nxt;
         nb = want;
         nd = 0;
@@ -1023,6 +1114,7 @@ struct rh_store {
         out[0] = out[1] = out[2] = 0;
         if (m == 0) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        const int fmode = fold_mode();  // how this batch reaches a fresh host tier
         version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
         if ((!fps_buf && (rc = lfps.ensure(m * 32 + 64))) || (rc = skeys.ensure(m * kl + 64)) ||
             (rc = sfps.ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)) || (rc = dops.ensure(m + 64)) ||
@@ -1071,6 +1163,7 @@ struct rh_store {
         }
         uint64_t *host = res_host.data();
         uint32_t flags = 0;
+        int next_rc = RH_OK;
         for (int full = 0; full < 2; full++) {
             // 2. key order (+ duplicate / leading-digit-tie flags; the sort zeroes them, and every
             //    other word of the result block is written by a later kernel)
@@ -1099,14 +1192,19 @@ struct rh_store {
                                           dinb[nxt].p, rh_num_blocks(n_max), mcnt.p, r_merge, dsmp[nxt].p,
                                           dsmp2[nxt].p, results.p + 8, r_dcnt, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            // the batch's rows for the host tier's fold (only while the tier is fresh)
+            if (fmode &&
+                (rc = fold_copies(fmode, skeys.p, sfps.p, sops.p, dheap.p + heap_len * sizeof(rh::DeltaRec), dops.p, m)))
+                return rc;
             // 5. the one round trip
             RH_HIP(hipMemcpyAsync(host, results.p, 96, hipMemcpyDeviceToHost, stream));
             if (full == 0 && next && next_m) {
                 if (!res_ev) RH_HIP(hipEventCreateWithFlags(&res_ev, hipEventDisableTiming));
                 RH_HIP(hipEventRecord(res_ev, stream));
-                if ((rc = lift_dispatch(schema, *next, next_m, next_fps, nullptr, nullptr, nullptr, false, stream)))
-                    return rc;
-                if ((rc = sync_event(res_ev))) return rc;
+                // a failure to queue the next batch's lift is reported after this batch commits
+                // (the batches before the failing one stay applied), never instead of it
+                next_rc = lift_dispatch(schema, *next, next_m, next_fps, nullptr, nullptr, nullptr, false, stream);
+                if ((rc = next_rc ? sync() : sync_event(res_ev))) return rc;
             } else if ((rc = sync())) {
                 return rc;
             }
@@ -1129,10 +1227,13 @@ struct rh_store {
         dtotal += dcnt;
         rh_fp_add(root_d, &host[8], root_d);  // mod 2^256
         dsums_ok = false;
+        if (fmode) fold_batch(fmode, m);
         // the heap also holds records no row points to any more (overwritten or dropped keys)
         const uint64_t thresh_now = std::max<uint64_t>(nb / compact_div, compact_min);
-        if (nd > thresh_now || heap_len > thresh_now) return compact();
-        return RH_OK;
+        if (nd > thresh_now || heap_len > thresh_now) {
+            if ((rc = compact())) return rc;
+        }
+        return next_rc ? next_rc : RH_OK;
     }
     int query(const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {  // rank ranges
         int rc;
@@ -1573,12 +1674,14 @@ int rh_store_keys(rh_store *s, uint64_t lo, uint64_t hi, void *host_out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     std::lock_guard<std::mutex> guard_(s->mu);
     int rc;
+    // the staged rows first: the range is checked against the size they leave
+    if ((rc = flush_locked(s))) return rc;
     if (lo > hi || hi > s->size()) return fail(RH_ERR_ARG, "bad rank range");
     if (hi == lo) return RH_OK;
     if (!host_out) return fail(RH_ERR_ARG, "host_out NULL");
     if ((rc = tier_ready(s)) < 0) return rc;
     if (rc) {
-        memcpy(host_out, s->tier.keys + lo * s->kl, (hi - lo) * s->kl);
+        s->tier.copy_keys(lo, hi, static_cast<uint8_t *>(host_out));
         return RH_OK;
     }
     RH_HIP(hipSetDevice(s->device));
@@ -1606,9 +1709,9 @@ int rh_store_aggregate_keys(rh_store *s, int lo_kind, const void *lo_key, int hi
         const int t = tier_ready(s);
         if (t < 0) return t;
         if (t) {
-            const uint64_t lo = s->tier.bound_rank(lo_kind, static_cast<const uint8_t *>(lo_key), true);
-            const uint64_t hi = s->tier.bound_rank(hi_kind, static_cast<const uint8_t *>(hi_key), false);
-            s->tier.agg(lo, std::max(lo, hi), out);  // inverted -> ZERO
+            const rh::HostTier &t = s->tier;
+            t.agg(t.bound(lo_kind, static_cast<const uint8_t *>(lo_key), true),
+                  t.bound(hi_kind, static_cast<const uint8_t *>(hi_key), false), out);  // inverted -> ZERO
             return RH_OK;
         }
     }
@@ -1633,10 +1736,13 @@ int rh_store_resolve_segments(rh_store *s, size_t r, const uint8_t *start_kinds,
         if (t < 0) return t;
         if (t) {
             const uint8_t *sk = static_cast<const uint8_t *>(start_keys), *ek = static_cast<const uint8_t *>(end_keys);
+            const rh::HostTier &t = s->tier;
             for (size_t j = 0; j < r; j++) {
-                raw_start[j] = start_kinds[j] ? s->tier.rank(sk + j * s->kl) : 0;
-                raw_end[j] = end_kinds[j] ? s->tier.rank(ek + j * s->kl) : s->tier.n;
-                s->tier.agg(raw_start[j], std::max(raw_start[j], raw_end[j]), local + j);  // inverted -> ZERO
+                const rh::HostTier::Cur a = start_kinds[j] ? t.lt(sk + j * s->kl) : t.begin();
+                const rh::HostTier::Cur b = end_kinds[j] ? t.lt(ek + j * s->kl) : t.end();
+                raw_start[j] = a.r;
+                raw_end[j] = b.r;
+                t.agg(a, b, local + j);  // inverted -> ZERO
             }
             return RH_OK;
         }
@@ -1663,7 +1769,7 @@ int rh_store_split_segments(rh_store *s, size_t m, const uint64_t *select_ranks,
             for (size_t i = 0; i < m; i++)
                 if (select_ranks[i] >= s->tier.n) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
             for (size_t i = 0; i < m; i++)
-                memcpy(static_cast<uint8_t *>(keys_out) + i * s->kl, s->tier.keys + select_ranks[i] * s->kl, s->kl);
+                memcpy(static_cast<uint8_t *>(keys_out) + i * s->kl, s->tier.at(select_ranks[i]).k, s->kl);
             for (size_t i = 0; i < q; i++) s->tier.agg(lo[i], hi[i], out + i);
             return RH_OK;
         }
@@ -1756,6 +1862,20 @@ int rh_store_stats(rh_store *s, uint64_t *base_rows, uint64_t *delta_rows, uint6
     return RH_OK;
 }
 
+int rh_store_tier_stats(rh_store *s, uint64_t *base_rows, uint64_t *delta_entries, uint64_t *refreshes,
+                        uint64_t *folds) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const int rc = flush_locked(s);
+    if (rc) return rc;
+    const bool fresh = s->tier_fresh();
+    if (base_rows) *base_rows = fresh ? s->tier.nb : 0;
+    if (delta_entries) *delta_entries = fresh ? s->tier.dt.size() : 0;
+    if (refreshes) *refreshes = s->tier_refreshes;
+    if (folds) *folds = s->tier_folds;
+    return RH_OK;
+}
+
 int rh_store_reserve(rh_store *s, uint64_t rows, uint64_t batch_rows) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     if (rows >= (1ull << 31) || batch_rows >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows)");
@@ -1790,7 +1910,7 @@ int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
     }
     if (!s->tier_on) {  // give the host memory back
         s->tier_version = ~0ull;
-        s->tier = rh::HostTier{};
+        s->tier.reset();
         s->tier_keys.release();
         s->tier_prefix.release();
         s->tier_out = std::vector<uint8_t>();
@@ -2348,7 +2468,7 @@ int rh_estore_set_host_tier(rh_estore *s, int enable) {
     s->tier_on = enable == 1;
     if (!s->tier_on) {
         s->tier_version = ~0ull;
-        s->tier = rh::HostTier{};
+        s->tier.reset();
         s->tier_prefix.release();
     }
     return RH_OK;

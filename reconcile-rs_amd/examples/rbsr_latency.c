@@ -3,7 +3,13 @@
  * through the C ABI: one whole FixedFanOut(16) reconciliation between two stores, timed on the
  * host clock, plus the per-question costs of Rsos::aggregate / rank through the same ABI.
  *
- *   rbsr_latency <n> <d> <reps> <host_tier 0|1>
+ *   rbsr_latency <n> <d> <reps> <host_tier 0|1> [write_rows]
+ *
+ * write_rows > 0: every repetition first writes write_rows fresh records into both replicas
+ * (rh_store_stage, the Rsos::insert path of the Rust binding), then reconciles: the write -> round
+ * cycle of a replica that merges updates and then answers rounds (src/replica/dispatch.rs:188-196).
+ * The write half (staging + the batch each store applies on its next question) and the round half
+ * are timed separately; the host tier folds each batch instead of copying the map again.
  *
  * Stores as the reference bench builds them (benches/protocol.rs:198-232): FingerprintTreeMap<u64,
  * u64> with keys 0..n and values key * 2654435761 (wrapping); the second store lacks d keys
@@ -138,11 +144,12 @@ static cost_t reconcile(rh_store *a, rh_store *b, const rh_schema *sc) {
 
 int main(int argc, char **argv) {
     if (argc < 5) {
-        fprintf(stderr, "usage: rbsr_latency <n> <d> <reps> <host_tier 0|1>\n");
+        fprintf(stderr, "usage: rbsr_latency <n> <d> <reps> <host_tier 0|1> [write_rows]\n");
         return 1;
     }
     const uint64_t n = strtoull(argv[1], NULL, 10), d = strtoull(argv[2], NULL, 10);
     const int reps = atoi(argv[3]), tier = atoi(argv[4]);
+    const uint64_t wrows = argc > 5 ? strtoull(argv[5], NULL, 10) : 0;
     const rh_schema sc = {RH_KEY_U64, 8, RH_VAL_U64, 8, RH_REC_PLAIN, 0};
     uint64_t *keys = malloc(n * 8), *vals = malloc(n * 8), *hk = malloc(n * 8), *hv = malloc(n * 8);
     if (!keys || !vals || !hk || !hv) return 2;
@@ -168,14 +175,46 @@ int main(int argc, char **argv) {
     cost_t c = reconcile(a, b, &sc); /* the first one also refreshes the host tier */
     const double first = now_s() - t0;
     double *ts = malloc(sizeof(double) * (size_t)(reps > 0 ? reps : 1));
-    double total = 0;
+    double *tw = malloc(sizeof(double) * (size_t)(reps > 0 ? reps : 1));
+    double total = 0, wtotal = 0;
+    uint64_t *wk = malloc(sizeof(uint64_t) * (wrows + 1)), *wv = malloc(sizeof(uint64_t) * (wrows + 1));
+    uint8_t *wops = calloc(wrows + 1, 1);
+    if (!wk || !wv || !wops) return 2;
+    uint64_t next_key = n + 1000, refreshes0 = 0, folds0 = 0;
+    CHECK(rh_store_tier_stats(a, NULL, NULL, &refreshes0, &folds0));
     for (int r = 0; r < reps; r++) {
+        tw[r] = 0;
+        if (wrows) {
+            /* fresh keys (the maps hold every key below n): n + a SplitMix64 stream, spread over the
+               rest of the key space */
+            for (uint64_t j = 0; j < wrows; j++) {
+                uint64_t z = (next_key++) * 0x9e3779b97f4a7c15ull;
+                z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+                z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+                wk[j] = n + ((z ^ (z >> 31)) >> 2);
+                wv[j] = wk[j] * 2654435761ull;
+            }
+            uint64_t la = 0, lb = 0;
+            t0 = now_s();
+            for (uint64_t j = 0; j < wrows; j++) {  /* Rsos::insert, one record at a time */
+                const rh_columns one = {wk + j, NULL, NULL, NULL, NULL, wv + j};
+                CHECK(rh_store_stage(a, &one, wops, 1));
+                CHECK(rh_store_stage(b, &one, wops, 1));
+            }
+            CHECK(rh_store_len(a, &la)); /* each store applies its staged batch on its next question */
+            CHECK(rh_store_len(b, &lb));
+            tw[r] = now_s() - t0;
+            wtotal += tw[r];
+        }
         t0 = now_s();
         c = reconcile(a, b, &sc);
         ts[r] = now_s() - t0;
         total += ts[r];
     }
+    uint64_t refreshes = 0, folds = 0, tier_delta = 0;
+    CHECK(rh_store_tier_stats(a, NULL, &tier_delta, &refreshes, &folds));
     qsort(ts, (size_t)reps, sizeof(double), cmp_d);
+    qsort(tw, (size_t)reps, sizeof(double), cmp_d);
     /* per-question costs through the ABI: Rsos::aggregate over a random key range, Rsos::rank */
     const int q = 200000;
     uint64_t x = 12345, sink = 0;
@@ -198,11 +237,16 @@ int main(int argc, char **argv) {
     const double rank_ns = (now_s() - t0) / q * 1e9;
     printf("{\"n\": %llu, \"d\": %llu, \"host_tier\": %d, \"reps\": %d, \"rounds\": %llu, \"ranges\": %llu, \"idlists\": %llu, "
            "\"enumerated\": %llu, \"wire_bytes\": %llu, \"first_us\": %.1f, \"mean_us\": %.2f, \"median_us\": %.2f, "
-           "\"p10_us\": %.2f, \"p90_us\": %.2f, \"aggregate_ns\": %.1f, \"rank_ns\": %.1f, \"sink\": %llu}\n",
+           "\"p10_us\": %.2f, \"p90_us\": %.2f, \"aggregate_ns\": %.1f, \"rank_ns\": %.1f, \"write_rows\": %llu, "
+           "\"write_mean_us\": %.2f, \"write_median_us\": %.2f, \"write_p90_us\": %.2f, \"cycle_mean_us\": %.2f, "
+           "\"tier_refreshes\": %llu, \"tier_folds\": %llu, \"tier_delta_entries\": %llu, \"sink\": %llu}\n",
            (unsigned long long)n, (unsigned long long)d, tier, reps, (unsigned long long)c.rounds,
            (unsigned long long)c.ranges, (unsigned long long)c.idlists, (unsigned long long)c.enumerated, (unsigned long long)c.wire_bytes,
            first * 1e6, reps ? total / reps * 1e6 : 0.0, reps ? ts[reps / 2] * 1e6 : 0.0, reps ? ts[reps / 10] * 1e6 : 0.0,
-           reps ? ts[(reps * 9) / 10] * 1e6 : 0.0, agg_ns, rank_ns, (unsigned long long)(sink & 1));
+           reps ? ts[(reps * 9) / 10] * 1e6 : 0.0, agg_ns, rank_ns, (unsigned long long)wrows,
+           reps ? wtotal / reps * 1e6 : 0.0, reps ? tw[reps / 2] * 1e6 : 0.0, reps ? tw[(reps * 9) / 10] * 1e6 : 0.0,
+           reps ? (wtotal + total) / reps * 1e6 : 0.0, (unsigned long long)(refreshes - refreshes0),
+           (unsigned long long)(folds - folds0), (unsigned long long)tier_delta, (unsigned long long)(sink & 1));
     CHECK(rh_store_destroy(a));
     CHECK(rh_store_destroy(b));
     return 0;

@@ -161,8 +161,9 @@ class GpuFingerprintStore:
 
     def set_host_tier(self, enable: bool = True, round_max: int = 0) -> None:
         """Answer rank / select / aggregate and protocol rounds of at most `round_max` segments
-        (0: the default, 128) from a host copy of the keys and fingerprint prefix sums, refreshed
-        from the device after every change (rh_store_set_host_tier)."""
+        (0: the default, 128) from a host copy of the keys and fingerprint prefix sums plus a tree
+        of every later batch's signed deltas (rh_store_set_host_tier): a batch updates it in
+        O(batch log n); the base is copied again only after a load or a delta grown past base / 8."""
         A.check(A.lib().rh_store_set_host_tier(self._h, 1 if enable else 0, round_max), "rh_store_set_host_tier")
 
     def set_compaction(self, divisor: int, min_rows: int) -> None:
@@ -177,6 +178,15 @@ class GpuFingerprintStore:
         b, d, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         A.check(A.lib().rh_store_stats(self._h, C.byref(b), C.byref(d), C.byref(c)), "rh_store_stats")
         return {"base_rows": int(b.value), "delta_rows": int(d.value), "compactions": int(c.value)}
+
+    def tier_stats(self) -> Dict[str, int]:
+        """The host tier's bookkeeping (rh_store_tier_stats): rows of its base copy and entries of
+        its delta tree while fresh, full refreshes (base copies) and batch folds so far."""
+        b, d, r, f = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        A.check(A.lib().rh_store_tier_stats(self._h, C.byref(b), C.byref(d), C.byref(r), C.byref(f)),
+                "rh_store_tier_stats")
+        return {"base_rows": int(b.value), "delta_entries": int(d.value), "refreshes": int(r.value),
+                "folds": int(f.value)}
 
     # ---- Rsos<K> -------------------------------------------------------------------------
     def size(self) -> int:

@@ -866,6 +866,7 @@ def test_host_tier_equals_device_answers(gpu, oracle_lib):
         assert tier.aggregates_ranks(list(lo), list(hi)) == dev.aggregates_ranks(list(lo), list(hi))
 
     probe()
+    assert tier.tier_stats()["refreshes"] == 1
     for k in range(3):  # inserts, then overwrites + deletes of existing keys
         b = make_records(s, 20_000, seed=300 + k, random_keys=True)
         ops = None
@@ -876,8 +877,75 @@ def test_host_tier_equals_device_answers(gpu, oracle_lib):
             ops[10_000:] = 1
         assert tier.apply_device(b, ops) == dev.apply_device(b, ops)
         probe()
+    # the batches were folded into the tier's delta tree: no second copy of the base
+    st = tier.tier_stats()
+    assert st["refreshes"] == 1 and st["folds"] == 3 and st["base_rows"] == n
+    assert st["delta_entries"] == tier.stats()["delta_rows"]
+    # deletes of keys inserted since the base copy drop their entries; a key inserted and deleted
+    # and inserted again; a compaction between batches (the next fold forms its deltas against the
+    # tier's own base, not the device's new one)
+    ins = make_records(s, 3_000, seed=400, random_keys=True)
+    gone = {c: t[:1_000].clone() for c, t in ins.items()}
+    dels = torch.ones(1_000, dtype=torch.uint8, device="cuda")
+    for st_ in (dev, tier):
+        assert st_.apply_device(ins) == (3_000, 0, 0)
+        assert st_.apply_device(gone, dels) == (0, 0, 1_000)
+        st_.compact()
+    probe()
+    again = {c: t[:500].clone() for c, t in ins.items()}
+    again["values"] ^= 0x5A
+    for st_ in (dev, tier):
+        assert st_.apply_device(again) == (500, 0, 0)
+        assert st_.apply_device(gone, dels) == (0, 0, 500)
+    probe()
+    assert tier.tier_stats()["refreshes"] == 1
+    # a larger reservation moves the tier's page-locked buffers: the next question copies the base
+    # again instead of reading the old ones (a use-after-free before)
+    tier.reserve(4 * n, 20_000)
+    probe()
+    assert tier.tier_stats()["refreshes"] == 2
+    # small batches (the staged-insert shape): one row, then 1,000 rows
+    one = make_records(s, 1, seed=501, random_keys=True)
+    thousand = make_records(s, 1_000, seed=502, random_keys=True)
+    for b in (one, thousand):
+        assert tier.apply_device(b) == dev.apply_device(b)
+        probe()
+    assert tier.tier_stats()["refreshes"] == 2
     dev.close()
     tier.close()
+
+
+@pytest.mark.gpu
+def test_keys_checked_after_staged_rows(gpu):
+    """rh_store_keys / select check the rank range against the size the staged rows leave (the
+    batch is applied first): ranks past the end after staged deletes are refused, ranks made valid
+    by staged inserts are answered -- with and without the host tier."""
+    import ctypes as C
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip import _abi as A
+    s = RecordSchema.plain("u64", "u64")
+    for tier in (False, True):
+        st = GpuFingerprintStore(s, host_tier=tier)
+        keys = np.arange(0, 2_000, 2, dtype=np.uint64)
+        st.load_bulk({"keys": keys.view(np.uint8).reshape(-1, 8), "values": (keys * 3).view(np.uint8).reshape(-1, 8)})
+        assert st.size() == 1_000 and st.select(999) == 1998
+        # stage 10 deletes of the top keys: rank 995 is now past the end
+        dk = keys[-10:].copy()
+        cols = A.Columns(dk.ctypes.data, None, None, None, None, dk.ctypes.data)
+        ops = np.ones(10, np.uint8)
+        A.check(A.lib().rh_store_stage(st._h, C.byref(cols), ops.ctypes.data, 10), "stage")
+        buf = np.zeros(8, np.uint8)
+        assert A.lib().rh_store_keys(st._h, 995, 996, buf.ctypes.data) == A.ERR_ARG
+        assert st.size() == 990
+        # stage 20 inserts above the top: ranks up to 1,009 answer
+        ik = np.arange(5_001, 5_041, 2, dtype=np.uint64)
+        cols = A.Columns(ik.ctypes.data, None, None, None, None, ik.ctypes.data)
+        A.check(A.lib().rh_store_stage(st._h, C.byref(cols), np.zeros(20, np.uint8).ctypes.data, 20), "stage")
+        out = np.zeros(20, np.uint64)
+        A.check(A.lib().rh_store_keys(st._h, 990, 1_010, out.ctypes.data), "keys")
+        assert np.array_equal(out, ik)
+        assert st.select(1_009) == 5_039
+        st.close()
 
 
 @pytest.mark.gpu

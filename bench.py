@@ -348,7 +348,9 @@ def main():
         "unit": "GiB/s",
         "mrec_per_s": round(recs / elapsed / 1e6, 1),
         "n_gpus": world,
-        "rccl_world_size": dist.get_world_size() if dist is not None else 1,
+        # the process group actually in use: "nccl" is RCCL on ROCm; "gloo" only in CPU-side rehearsals
+        "dist": {"backend": dist.get_backend() if dist is not None else None,
+                 "world_size": dist.get_world_size() if dist is not None else 1},
         "steps": args.steps,
         "warmup": args.warmup, "spinup": spin,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -373,7 +375,7 @@ def main():
     valu = None if dual else load_valu(args.config, n, lift_avg_s)
     if valu:
         line["valu"] = valu
-    if args.cpu_baseline and world == 1:
+    if args.cpu_baseline:  # rank 0 only, on the host's cores, once per run at every N
         line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample or min(n, 10_000_000), dual)
     if args.e2e == 1 or (args.e2e < 0 and args.config in ("config2", "config4") and world == 1):
         line["end_to_end"] = end_to_end(schema, cols, n)
@@ -382,17 +384,53 @@ def main():
         dist.destroy_process_group()
 
 
+def _agg_row(a) -> list:
+    """An Aggregate as the (fp limbs as int64 bit patterns, size) row the device combine takes."""
+    return [x - (1 << 64) if x >> 63 else x for x in a.fingerprint.limbs] + [a.size]
+
+
+def _route_keys(keys: torch.Tensor, splitters: torch.Tensor) -> torch.Tensor:
+    """Owner shard of each 16-byte key: the number of shard splitters (the first key of shards
+    1..N-1, memcmp order = the Ord of [u8; 16]) at or below it -- bisect_right over the splitters,
+    as ShardedStore.apply routes (rsos_hip/sharded.py), on the device."""
+    def words(k):  # big-endian u64 halves, sign-flipped so signed int64 order = unsigned order
+        hi = k[:, :8].flip(1).contiguous().view(torch.int64).view(-1)
+        lo = k[:, 8:16].flip(1).contiguous().view(torch.int64).view(-1)
+        flip = torch.iinfo(torch.int64).min
+        return hi ^ flip, lo ^ flip
+    kh, kl = words(keys)
+    sh, sl = words(splitters)
+    owner = torch.zeros(keys.shape[0], dtype=torch.int64, device=keys.device)
+    for j in range(splitters.shape[0]):
+        owner += ((kh > sh[j]) | ((kh == sh[j]) & (kl >= sl[j]))).to(torch.int64)
+    return owner
+
+
 def incremental(args, world, rank, dev, dist):
-    """config5: GPU-resident store of N records; each step applies one batch of `--batch` random
-    records (insert-or-overwrite; fresh random 128-bit keys are essentially all new) through the
-    device sort / search / merge / re-sum path.  Timed: apply_device, which ends synchronised."""
-    from rsos_hip import GpuFingerprintStore, RecordSchema
+    """config5: GPU-resident store of N records per GPU; each step applies one batch of `--batch`
+    random records per GPU (insert-or-overwrite; fresh random 128-bit keys are essentially all new)
+    through the device sort / search / merge / re-sum path.  Timed: apply_device_many over the
+    steps' batches (or apply_device per batch), then the whole map's root.
+
+    N > 1 ("the incremental config"): the resident set is one key-sorted set of N x n
+    records cut into N equal-count key-range shards; every step's update batch is one global batch
+    of N x --batch uniformly random records, routed by key range (the shard splitters) so that each
+    rank applies exactly the updates its range owns -- the multi-GPU form of a replica's network
+    merge (src/replica/dispatch.rs:188-196).  The per-shard roots (1 x 40 B each) are all_gathered
+    over RCCL and carry-added on the device: the whole map's root (initial_ranges,
+    rbsr/src/protocol.rs:100).  The routing is data preparation (untimed): a sender routes by key
+    range before the records reach a shard."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, combine_aggregates
     from rsos_hip.synth import make_records
+    from rsos_hip.shard import gather
     kname, vname, kind, n_default, desc = CONFIGS["config5"]
     n = args.records or n_default
     schema = getattr(RecordSchema, kind)(kname, vname)
     st = GpuFingerprintStore(schema, device=dev.index)
     base = make_records(schema, n, seed=42, device=dev, first_index=rank * n, key_space=n * world)
+    # shard splitters: the first key of every shard but the first (the generator is counter-based)
+    splitters = torch.cat([make_records(schema, 1, seed=42, device=dev, first_index=r * n, key_space=n * world)["keys"]
+                           for r in range(1, world)]) if world > 1 else None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     st.load_bulk_device(base)
@@ -403,50 +441,97 @@ def incremental(args, world, rank, dev, dist):
     gen = torch.Generator(device=dev)
     gen.manual_seed(7 + rank)
     for k in range(args.warmup + args.steps):
-        b = make_records(schema, m, seed=1000 * (rank + 1) + k, device=dev, random_keys=True)
-        if m_over:  # re-stamp distinct existing keys: an overwrite, the new - old delta (mutate.rs:31-41)
+        if world > 1:  # one global batch, routed by key range
+            g = make_records(schema, m * world, seed=1000 + k, device=dev, random_keys=True)
+            mine = (_route_keys(g["keys"], splitters) == rank).nonzero().view(-1)
+            b = {c: t.index_select(0, mine).contiguous() for c, t in g.items()}
+            del g
+        else:
+            b = make_records(schema, m, seed=1000 + k, device=dev, random_keys=True)
+        if m_over:  # re-stamp distinct existing keys of this shard: an overwrite, the new - old delta (mutate.rs:31-41)
             rows = torch.randperm(n, generator=gen, device=dev)[:m_over]
-            b["keys"][:m_over] = base["keys"][rows]
-            b["phys"][:m_over] = base["phys"][rows] + 1_000_000
+            mo = min(m_over, b["keys"].shape[0])
+            b["keys"][:mo] = base["keys"][rows[:mo]]
+            b["phys"][:mo] = base["phys"][rows[:mo]] + 1_000_000
         batches.append(b)
     del base
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     # capacity for the map this run grows into (its resident rows plus every batch), reserved
     # before the first batch the way a replica sizes its store: no reallocation in the loop
-    reserved = n + m * (args.warmup + args.steps)
-    st.reserve(reserved, m)
+    mmax = max(b["keys"].shape[0] for b in batches)
+    reserved = n + sum(b["keys"].shape[0] for b in batches)
+    st.reserve(reserved, mmax)
     spin = gpu_spinup(args.spinup_ms, dev)
     for k in range(args.warmup):
         st.apply_device(batches[k])
+    def global_root():
+        """The whole map's root: this shard's root, all_gathered with the others' and carry-added
+        on the device (one shard: the root itself)."""
+        a = st.aggregate()  # the shard's root, O(1) (the store keeps it on the host)
+        if dist is None:
+            return a
+        root_t = torch.tensor([_agg_row(a)], dtype=torch.int64, device=dev)
+        return combine_aggregates(gather(dist, root_t))
+
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     counts = [0, 0, 0]
     comp0 = st.stats()["compactions"]
     t0 = time.perf_counter()
-    if args.pipeline:  # the queued batches drained in order by one call
+    if args.pipeline:  # the queued batches drained in order by one call, then the root
         for c in st.apply_device_many(batches[args.warmup:args.warmup + args.steps]):
             counts = [a + b for a, b in zip(counts, c)]
-        root_agg = st.aggregate()  # the updated root fingerprint (initial_ranges, rbsr/src/protocol.rs:100)
-    else:
+        root_g = global_root()
+    else:  # one batch at a time, the root exchanged after each
         for k in range(args.steps):
             c = st.apply_device(batches[args.warmup + k])
             counts = [a + b for a, b in zip(counts, c)]
-            root_agg = st.aggregate()
+            root_g = global_root()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    applied = [sum(b["keys"].shape[0] for b in batches[args.warmup:args.warmup + args.steps])]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    root = st.aggregate()
+        tot = torch.tensor(counts + applied, dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        counts, applied = [int(x) for x in tot[:3].tolist()], [int(tot[3].item())]
     stats = st.stats()
-    assert root == root_agg
+    root_size = root_g.size if dist is None else int(root_g[0, 4].item())
+    size_all = torch.tensor([st.size()], dtype=torch.int64, device=dev)
+    if dist is not None:
+        dist.all_reduce(size_all)
+    if root_size != int(size_all.item()):  # the combined root counts every shard's rows
+        raise SystemExit(f"bench: combined root counts {root_size} rows, the shards hold {int(size_all.item())}")
+    dump = None
+    if args.dump_aggregates:
+        # the combined root and 16 key-range aggregates (bounds: the keys of equal-count rows of the
+        # original resident set), for tests/test_bench_path.py to check against one store
+        total = n * world
+        bk = [make_records(schema, 1, seed=42, device=dev, first_index=total * j // 16, key_space=total)["keys"]
+              for j in range(1, 16)]
+        from rsos_hip.store import KeyRange
+        parts = []
+        for j in range(16):
+            lo = None if j == 0 else bytes(bk[j - 1].cpu().numpy().tobytes())
+            hi = None if j == 15 else bytes(bk[j].cpu().numpy().tobytes())
+            a = st.aggregate(KeyRange(lo, hi))
+            parts.append(_agg_row(a))
+        loc = torch.tensor(parts, dtype=torch.int64, device=dev)
+        comb = combine_aggregates(gather(dist, loc)) if dist is not None else loc
+        rt = root_g if dist is not None else torch.tensor([_agg_row(root_g)], dtype=torch.int64)
+        dump = {"world": world, "root": [int(x) for x in rt.cpu().view(-1).tolist()],
+                "ranges": [[int(x) for x in row] for row in comb.cpu().tolist()]}
     if rank == 0:
-        recs = m * args.steps * world
+        if dump is not None:
+            with open(args.dump_aggregates, "w") as f:
+                json.dump(dump, f)
+        recs = applied[0]
         line = {
             "metric": "incremental update: batched inserts into a GPU-resident map (M records/s)",
             "value": round(recs / elapsed / 1e6, 2), "unit": "M records/s",
@@ -457,18 +542,21 @@ def incremental(args, world, rank, dev, dist):
             "config": {"workload": desc + (f"; {args.overwrite:.0%} of each batch overwrites existing keys"
                                            if m_over else ""),
                        "resident_records_per_gpu": n, "batch": m, "overwrites_per_batch": m_over,
-                       "parallelism": f"key-range shards x{world}"},
+                       "parallelism": f"key-range shards x{world}" + (
+                           " (each global batch of N x --batch records routed by key range; per-shard roots "
+                           "all_gathered and carry-added on the device)" if world > 1 else "")},
+            "dist": {"backend": (dist.get_backend() if dist is not None else None), "world_size": world},
             "batch_counts": {"new": counts[0], "overwritten": counts[1], "deleted": counts[2]},
-            "final_size": root.size, "bulk_load_s": round(load_s, 3),
+            "root_size": root_size, "bulk_load_s": round(load_s, 3),
             "step": ("apply_device_many over the K queued batches (each: lift + sort + base/delta search + "
                      "delta merge, amortised compaction; the next batch lifted while this one's result "
-                     "returns) + the root aggregate" if args.pipeline else
+                     "returns) + the whole map's root" if args.pipeline else
                      "apply_device per batch (lift + sort + base/delta search + delta merge; amortised "
-                     "compaction) + root aggregate"),
+                     "compaction) + the whole map's root after each"),
             "compactions_in_timed_steps": stats["compactions"] - comp0, "delta_rows_at_end": stats["delta_rows"],
             "reserved_rows": reserved,
         }
-        if args.cpu_baseline and world == 1:
+        if args.cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_incremental(schema, m, args.cpu_sample or 10_000_000)
         print(json.dumps(line), flush=True)
     st.close()

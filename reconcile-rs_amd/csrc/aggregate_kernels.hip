@@ -320,6 +320,35 @@ __global__ __launch_bounds__(256) void k_lift_fixed_long(const uint8_t *bytes, u
     fixed_epilogue(fps, bsums, i, live, cv);
 }
 
+// Fixed-length records whose length is a compile-time constant: the encoded forms of the shapes
+// the schema kernels instantiate (120 B = [u8; 16] key + Entry<Timestamp, Vec<u8>> of 64 B, the
+// north_star record; 100 B its projection State<Vec<u8>>; 104 / 80 B the u64-key dated / plain
+// 64 B records; 48 B a 16-byte-key tombstone).  The record is loaded whole into registers with
+// 32-bit lane offsets off a workgroup-rebased scalar base -- the schema kernels' loads -- and
+// hashed by the same compile-time block schedule (hash_words): no per-block loop, branches,
+// masks or funnel shifts, which the runtime-length kernel above pays per block.
+template <int LEN>
+__global__ __launch_bounds__(256) void k_lift_fixed_ct(const uint8_t *bytes, uint64_t n, uint8_t *fps,
+                                                       uint8_t *bsums) {
+    static_assert(LEN % 4 == 0 && LEN > 0 && LEN <= 192, "whole words, in registers");
+    __shared__ SumTile tile;
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256;
+    const uint32_t t = threadIdx.x;
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (b0 + t < n) {
+        const uint8_t *base = bytes + b0 * LEN;
+        uint32_t w[LEN / 4];
+        ldw<LEN / 4, cmin(16, lowbit(LEN))>(base + t * (uint32_t)LEN, w);
+        hash_words<LEN>(w, h);
+        store_fp(fps + b0 * 32, t, h);
+    }
+    if (bsums) {  // uniform: every lane reaches the workgroup barriers; absent rows add zero
+        uint32_t f[8];
+        block_sum_fps256(h, tile, f);
+        if (t == 0) store_sum(bsums, blockIdx.x, f);
+    }
+}
+
 // ---- reductions ------------------------------------------------------------------------------
 
 
@@ -940,6 +969,25 @@ hipError_t launch_lift_fixed(const uint8_t *bytes, uint64_t len, uint64_t n, uin
                              uint8_t *bsums, hipStream_t st) {
     if (n == 0) return hipSuccess;
     const dim3 g((uint32_t)((n + 255) / 256));
+    // compile-time lengths: the record is read exactly (n * len <= limit is the caller's check),
+    // with loads as wide as the records' alignment allows
+    const uint64_t align = len < 16 ? 16 : std::min<uint64_t>(16, len & (~len + 1));
+    if (len && n * len <= limit && reinterpret_cast<uintptr_t>(bytes) % align == 0) {
+        switch (len) {
+#define RH_FIXED_CT(L)                                                                           \
+    case L:                                                                                      \
+        hipLaunchKernelGGL(k_lift_fixed_ct<L>, g, dim3(256), 0, st, bytes, n, fps, bsums);       \
+        return hipGetLastError();
+            RH_FIXED_CT(48)
+            RH_FIXED_CT(80)
+            RH_FIXED_CT(100)
+            RH_FIXED_CT(104)
+            RH_FIXED_CT(120)
+#undef RH_FIXED_CT
+            default:
+                break;
+        }
+    }
     if (len <= (uint64_t)CHUNK_LEN && len % 4 == 0)
         hipLaunchKernelGGL(k_lift_fixed_short<true>, g, dim3(256), 0, st, bytes, (uint32_t)len, n, limit, fps, bsums);
     else if (len <= (uint64_t)CHUNK_LEN)

@@ -2238,12 +2238,19 @@ struct rh_estore {
     int lift_host(const uint8_t *b, const uint64_t *o, size_t m, uint8_t *out, uint8_t *bs) {
         int rc;
         if (!m) return RH_OK;
-        for (size_t i = 0; i < m; i++)
+        bool fixed = true;  // every record the same length: the fixed-length kernels, no offsets
+        for (size_t i = 0; i < m; i++) {
             if (o[i + 1] < o[i]) return fail(RH_ERR_ARG, "record offsets must not decrease");
+            fixed = fixed && o[i + 1] - o[i] == o[1] - o[0];
+        }
         const uint64_t len = o[m] - o[0], padded = ((len + 3) & ~3ull) + 64;
         if ((rc = bytes.ensure(padded)) || (rc = offs.ensure(m + 1))) return rc;
         RH_HIP(hipMemsetAsync(bytes.p + (len & ~3ull), 0, padded - (len & ~3ull), stream));
         if (len) RH_HIP(hipMemcpyAsync(bytes.p, b + o[0], len, hipMemcpyHostToDevice, stream));
+        if (fixed) {  // e.g. a batch of Entry<Timestamp, Vec<u8>> whose values all have one length
+            RH_HIP(rh::launch_lift_fixed(bytes.p, o[1] - o[0], m, padded - 64, out, bs, stream));
+            return RH_OK;
+        }
         if (o[0] == 0) {
             RH_HIP(hipMemcpyAsync(offs.p, o, (m + 1) * 8, hipMemcpyHostToDevice, stream));
         } else {  // rebase to the uploaded span

@@ -165,3 +165,38 @@ def make_snapshot(cols: Dict[str, torch.Tensor], schema: RecordSchema, key_form:
             idx = (oo + rel)[:, None] + torch.arange(w, device=dev)[None, :]
             buf[idx.reshape(-1)] = dd.reshape(-1)
     return buf
+
+
+def encode_rows(schema: RecordSchema, cols: Dict[str, torch.Tensor]) -> torch.Tensor:
+    """(n, L) uint8: the canonical bytes lift hashes for every record of `cols` (present records
+    only), built on the device -- what rsos::encoding::encode_to_vec of the key then the value gives
+    (rsos/src/encoding.rs:17-35): a byte key [u8; L] is a serde tuple (u64 length L, then the bytes),
+    u32 / u64 keys and values are fixed LE, Vec<u8> values are u64 length + bytes, a dated record
+    is Timestamp (u64 physical, u32 logical, u64 node) then State::Present (u32 0) then the value,
+    a projection State::Present then the value.  The drop-in encoded map's input for the
+    fixed-width shapes (bench.py --config encoded, tests)."""
+    if cols.get("tags") is not None and bool((cols["tags"] != 0).any()):
+        raise ValueError("encode_rows: present records only (a tombstone's encoding is shorter)")
+    n = (cols["keys"] if "keys" in cols else cols["values"]).shape[0]
+    dev = (cols["keys"] if "keys" in cols else cols["values"]).device
+
+    def const(v: int, w: int) -> torch.Tensor:
+        return torch.tensor(list(v.to_bytes(w, "little")), dtype=torch.uint8, device=dev).expand(n, w)
+
+    def u8(t: torch.Tensor, w: int) -> torch.Tensor:
+        return t.contiguous().view(torch.uint8).view(n, w)
+
+    parts = []
+    if schema.key_kind == A.KEY_BYTES:
+        parts += [const(schema.key_len, 8), cols["keys"]]
+    elif schema.key_kind != A.KEY_UNIT:
+        parts.append(cols["keys"])
+    if schema.record_kind == A.REC_DATED:
+        parts += [u8(cols["phys"], 8), u8(cols["logical"], 4), u8(cols["node"], 8)]
+    if schema.record_kind != A.REC_PLAIN:
+        parts.append(const(0, 4))
+    if schema.value_kind == A.VAL_BYTES:
+        parts.append(const(schema.value_row, 8))
+    if schema.value_row:
+        parts.append(cols["values"])
+    return torch.cat(parts, dim=1).contiguous()

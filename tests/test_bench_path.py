@@ -61,7 +61,8 @@ def test_bench_world2_gloo_equals_single_process(tmp_path, gpu):
     r2 = _bench(common + ["--gpus", "2", "--dump-aggregates", str(two)], env_extra={"BENCH_BACKEND": "gloo"})
     assert r2.returncode == 0, r2.stderr[-3000:]
     line2 = json.loads(r2.stdout.strip().splitlines()[-1])
-    assert line2["n_gpus"] == 2 and line2["rccl_world_size"] == 2 and line2["scaling"] == "strong"
+    assert line2["n_gpus"] == 2 and line2["dist"] == {"backend": "gloo", "world_size": 2}
+    assert line2["scaling"] == "strong"
     assert line2["config"]["records_per_rank"] == [1_500_000, 1_500_001]
     a, b = json.loads(one.read_text()), json.loads(two.read_text())
     assert a["world"] == 1 and b["world"] == 2
@@ -98,7 +99,46 @@ def test_bench_world_n_gloo_equals_single_process(tmp_path, gpu, world):
                 timeout=300)
     assert rn.returncode == 0, rn.stderr[-3000:]
     line = json.loads(rn.stdout.strip().splitlines()[-1])
-    assert line["n_gpus"] == world and line["rccl_world_size"] == world
+    assert line["n_gpus"] == world and line["dist"] == {"backend": "gloo", "world_size": world}
     assert line["config"]["records_per_rank"] == [total * (r + 1) // world - total * r // world for r in range(world)]
     a, b = json.loads(one.read_text()), json.loads(many.read_text())
     assert b["world"] == world and a["ranges"] == b["ranges"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_config5_routed_batches_equal_one_store(tmp_path, gpu, world):
+    """config5 at N ranks (gloo rehearsal on one GPU): every step's global batch of N x --batch
+    random records is routed by key range, each rank applies what its shard owns, and the per-shard
+    roots are all_gathered and carry-added on the device.  The combined root and 16 key-range
+    aggregates must equal, bit for bit, one store that loaded the whole resident set and applied
+    every global batch (src/replica/dispatch.rs:188-196)."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    from rsos_hip.synth import make_records
+    n, m, warm, steps = 200_000, 20_000, 1, 3
+    out = tmp_path / "c5.json"
+    r = _bench(["--config", "config5", "--records", str(n), "--batch", str(m), "--steps", str(steps), "--warmup",
+                str(warm), "--cpu-baseline", "0", "--spinup-ms", "0", "--gpus", str(world), "--dump-aggregates",
+                str(out)], env_extra={"BENCH_BACKEND": "gloo"}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world and line["dist"] == {"backend": "gloo", "world_size": world}
+    got = json.loads(out.read_text())
+    s = RecordSchema.dated("bytes16", "bytes64")
+    total = n * world
+    st = GpuFingerprintStore(s)
+    st.load_bulk_device(make_records(s, total, seed=42, key_space=total))
+    for k in range(warm + steps):
+        st.apply_device(make_records(s, m * world, seed=1000 + k, random_keys=True))
+    root = st.aggregate()
+    assert got["root"] == [x - (1 << 64) if x >> 63 else x for x in root.fingerprint.limbs] + [root.size]
+    assert line["root_size"] == root.size
+    bk = [bytes(make_records(s, 1, seed=42, first_index=total * j // 16, key_space=total)["keys"].cpu().numpy().tobytes())
+          for j in range(1, 16)]
+    for j in range(16):
+        a = st.aggregate(KeyRange(None if j == 0 else bk[j - 1], None if j == 15 else bk[j]))
+        assert got["ranges"][j] == [x - (1 << 64) if x >> 63 else x for x in a.fingerprint.limbs] + [a.size]
+    st.close()
+    torch.cuda.synchronize()

@@ -423,3 +423,190 @@ impl<K: GpuKey, V: GpuRecord> Rsos<K> for HipFingerprintMap<K, V> {
         Some(old)
     }
 }
+
+// ---- the inherent FingerprintTreeMap surface the facade calls (public-api/rsos.txt:129-194) ----
+// The same surface HipEncodedMap has, on the fixed-width column store, so the drop-in at
+// src/replica.rs:69,74 gets the schema kernels (the canonical encoding synthesised in registers,
+// no host-side encode_to_vec per record): `FingerprintTreeMap<[u8; 16], Entry<Timestamp, V>>` ->
+// `HipFingerprintMap<[u8; 16], Entry<Timestamp, V>>` when V has a GpuRecord form.  Every mutation
+// is one staged row (rh_store_stage); every fingerprint is still the GPU lift.
+
+impl<K: GpuKey, V: GpuRecord> Default for HipFingerprintMap<K, V> {
+    fn default() -> Self {
+        HipFingerprintMap::new(0)
+    }
+}
+
+impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
+    pub fn len(&self) -> usize {
+        self.entries.len()
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.entries.len() == 0
+    }
+
+    pub fn clear(&mut self) {
+        let keys: Vec<K> = self.entries.iter().map(|(k, _)| k.clone()).collect();
+        for k in &keys {
+            self.stage(k, None);
+        }
+        self.entries.clear();
+    }
+
+    pub fn get<Q: Ord + ?Sized>(&self, key: &Q) -> Option<&V>
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.get(key)
+    }
+
+    pub fn contains_key<Q: Ord + ?Sized>(&self, key: &Q) -> bool
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.get(key).is_some()
+    }
+
+    pub fn position<Q: Ord + ?Sized>(&self, key: &Q) -> Option<usize>
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.position(key)
+    }
+
+    pub fn insert(&mut self, key: K, value: V) -> Option<V> {
+        <Self as Rsos<K>>::insert(self, key, value)
+    }
+
+    pub fn remove<Q: Ord + ?Sized>(&mut self, key: &Q) -> Option<V>
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        let k = self.entries.at(self.entries.position(key)?).0.clone();
+        <Self as Rsos<K>>::delete(self, &k)
+    }
+
+    /// Keep the entries `f` accepts (FingerprintTreeMap::retain): the others are deleted, each a
+    /// staged row of one batch.
+    pub fn retain<F: FnMut(&K, &V) -> bool>(&mut self, mut f: F) {
+        let gone: Vec<K> = self.entries.iter().filter(|(k, v)| !f(k, v)).map(|(k, _)| k.clone()).collect();
+        for k in gone {
+            <Self as Rsos<K>>::delete(self, &k);
+        }
+    }
+
+    /// In-place edit (FingerprintTreeMap::with_mut + Relift, rsos/src/fingerprint_tree_map/access.rs:46-76):
+    /// `f` sees the value (or None); the edited value is staged again, so its fingerprint replaces
+    /// the old one -- the `new - old` delta -- in the next batch.
+    pub fn with_mut<R, F: FnOnce(Option<&mut V>) -> R>(&mut self, key: &K, f: F) -> R {
+        let r = f(self.entries.get_mut(key));
+        if let Some(v) = self.entries.get(key) {
+            let batch = Batch::new(std::iter::once((key, Some(v))));
+            let cols = batch.columns();
+            let op = [0u8];
+            // SAFETY: the library copies the row before returning.
+            check(unsafe { ffi::rh_store_stage(self.store, &cols, op.as_ptr(), 1) }, "rh_store_stage");
+        }
+        r
+    }
+
+    pub fn entry(&mut self, key: K) -> HipEntry<'_, K, V> {
+        HipEntry { map: self, key }
+    }
+
+    pub fn range<R: RangeBounds<K>>(&self, range: R) -> impl Iterator<Item = (&K, &V)> + '_ {
+        let lo = self.bound_rank(range.start_bound(), true);
+        let hi = self.bound_rank(range.end_bound(), false).max(lo);
+        self.entries.range(lo, hi).map(|(k, v)| (k, v))
+    }
+
+    pub fn iter(&self) -> impl Iterator<Item = (&K, &V)> + '_ {
+        self.entries.iter().map(|(k, v)| (k, v))
+    }
+
+    pub fn keys(&self) -> impl Iterator<Item = &K> + '_ {
+        self.entries.iter().map(|(k, _)| k)
+    }
+
+    pub fn values(&self) -> impl Iterator<Item = &V> + '_ {
+        self.entries.iter().map(|(_, v)| v)
+    }
+
+    pub fn first_key_value(&self) -> Option<(&K, &V)> {
+        self.entries.first().map(|(k, v)| (k, v))
+    }
+
+    pub fn last_key_value(&self) -> Option<(&K, &V)> {
+        self.entries.last().map(|(k, v)| (k, v))
+    }
+
+    pub fn aggregate<R: RangeBounds<K>>(&self, range: R) -> Aggregate {
+        <Self as Rsos<K>>::aggregate(self, range)
+    }
+
+    pub fn rank<Q: Ord + ?Sized>(&self, key: &Q) -> usize
+    where
+        K: std::borrow::Borrow<Q>,
+    {
+        self.entries.rank(key)
+    }
+
+    pub fn select(&self, r: usize) -> &K {
+        &self.entries.at(r).0
+    }
+
+    /// The device holds exactly the host index (sizes agree after the staged rows apply).
+    pub fn check_invariants(&self) {
+        let mut n = 0u64;
+        // SAFETY: out-pointer.
+        check(unsafe { ffi::rh_store_len(self.store, &mut n) }, "rh_store_len");
+        assert_eq!(n as usize, self.entries.len(), "rsos-hip: device and host sizes differ");
+    }
+}
+
+/// The reference's `rsos::Entry` (public-api/rsos.txt:118-121) for the column store.
+pub struct HipEntry<'a, K: GpuKey, V: GpuRecord> {
+    map: &'a mut HipFingerprintMap<K, V>,
+    key: K,
+}
+
+impl<'a, K: GpuKey, V: GpuRecord> HipEntry<'a, K, V> {
+    pub fn and_modify(self, f: impl FnOnce(&mut V)) -> Self {
+        let key = self.key.clone();
+        self.map.with_mut(&key, |v| {
+            if let Some(v) = v {
+                f(v)
+            }
+        });
+        self
+    }
+
+    pub fn or_insert_with(self, f: impl FnOnce() -> V) -> &'a V {
+        let HipEntry { map, key } = self;
+        if map.entries.get(&key).is_none() {
+            <HipFingerprintMap<K, V> as Rsos<K>>::insert(map, key.clone(), f());
+        }
+        let map: &'a HipFingerprintMap<K, V> = map;
+        map.entries.get(&key).expect("just inserted")
+    }
+
+    pub fn or_insert(self, value: V) -> &'a V {
+        self.or_insert_with(|| value)
+    }
+
+    pub fn or_default(self) -> &'a V
+    where
+        V: Default,
+    {
+        self.or_insert_with(V::default)
+    }
+}
+
+impl<K: GpuKey, V: GpuRecord> FromIterator<(K, V)> for HipFingerprintMap<K, V> {
+    fn from_iter<T: IntoIterator<Item = (K, V)>>(iter: T) -> Self {
+        let mut m = HipFingerprintMap::new(0);
+        m.load_bulk(iter.into_iter().collect());
+        m
+    }
+}

@@ -170,3 +170,43 @@ def test_inherent_surface_with_mut_retain_entry(gpu, oracle_lib):
     assert m.remove("k0010") == 10 and m.remove("k0010") is None
     check()
     m.close()
+
+
+@pytest.mark.gpu
+def test_fixed_length_records_take_fixed_kernel(gpu, oracle_lib):
+    """A map whose records all encode to one length -- u64 keys with Entry<Timestamp, Vec<u8>> values
+    of 64 bytes, 104 B each, the shape the fixed-length kernels (k_lift_fixed_ct) take -- loaded and
+    updated through the encoded store: the root and random rank-range aggregates equal a fold of the
+    oracle's lift, with the host tier on and off; a batch mixing lengths (a tombstone, 32 B) takes
+    the offsets kernel and stays equal too."""
+    from rsos_hip.emap import EncodedFingerprintMap
+    from rsos_hip.fmap import Entry
+    O = oracle_lib
+    rng = np.random.default_rng(11)
+
+    def rec(k, e):
+        return P.encode(P.U64(k)) + (P.encode(P.entry(P.timestamp(e.phys, e.logical, e.node), P.TOMBSTONE))
+                                     if e.tombstone else
+                                     P.encode(P.entry(P.timestamp(e.phys, e.logical, e.node), P.present(P.Str(e.value)))))
+
+    for tier in (False, True):
+        m = EncodedFingerprintMap("u64", ("entry", "bytes"), host_tier=tier)
+        want = {int(k): Entry(rng.bytes(64), int(k) + 5, 0, 1) for k in rng.integers(0, 2**62, 5_000)}
+        m.load_bulk(want.items())
+        for step in range(3):
+            for _ in range(400):
+                k = int(rng.integers(0, 2**62))
+                e = Entry(rng.bytes(64), k, step, 2, tombstone=(step == 2 and rng.random() < 0.3))
+                m.insert(k, e)
+                want[k] = e
+            keys = sorted(want)
+            recs = [rec(k, want[k]) for k in keys]
+            assert m.root().fingerprint.to_int() == _oracle_root(O, recs) and m.size() == len(keys)
+            fps = O.lift_encoded(recs, threads=8)
+            for _ in range(20):
+                lo = int(rng.integers(0, len(keys)))
+                hi = int(rng.integers(lo, len(keys) + 1))
+                a = m.aggregates_ranks([lo], [hi])[0]
+                assert a.size == hi - lo
+                assert a.fingerprint.to_int() == sum(int.from_bytes(f.tobytes(), "little") for f in fps[lo:hi]) % M256
+        m.close()

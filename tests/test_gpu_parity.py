@@ -224,21 +224,51 @@ def test_encoded_word_aligned_ragged(gpu, oracle_lib):
         assert np.array_equal(fps.cpu().numpy(), want), odd
 
 
-@pytest.mark.parametrize("length", [0, 1, 4, 63, 64, 65, 120, 128, 1023, 1024, 1025, 2048, 3000])
-def test_fixed_length_records(gpu, oracle_lib, length):
+@pytest.mark.parametrize("length,offset", [(L, 0) for L in (0, 1, 4, 63, 64, 65, 120, 128, 1023, 1024, 1025, 2048,
+                                                              3000)] +
+                         [(L, o) for L in (48, 80, 100, 104, 120) for o in (0, 4)])
+def test_fixed_length_records(gpu, oracle_lib, length, offset):
     """rh_lift_fixed_async: one length for every record (one chunk, exact blocks, multi-chunk),
-    several workgroups and a ragged last one; block sums over the fingerprints."""
+    several workgroups and a ragged last one; block sums over the fingerprints.  The lengths with
+    a compile-time kernel (k_lift_fixed_ct: 48, 80, 100, 104, 120) also from a buffer 4 bytes off
+    its alignment, which takes the runtime-length kernel instead."""
     import torch
     from rsos_hip import lift_fixed
     rng = np.random.default_rng(length)
     n = 700
     raw = rng.integers(0, 256, n * length + 3, dtype=np.uint8)  # + bytes past the last record
     blobs = [raw[i * length:(i + 1) * length].tobytes() for i in range(n)]
-    fps, bs = lift_fixed(torch.from_numpy(raw).cuda(), length, n=n)
+    dev = torch.zeros(raw.size + 16, dtype=torch.uint8, device="cuda")
+    dev[offset:offset + raw.size] = torch.from_numpy(raw).cuda()
+    fps, bs = lift_fixed(dev[offset:offset + raw.size], length, n=n)
     want = oracle_lib.lift_encoded(blobs, threads=8)
     assert np.array_equal(fps.cpu().numpy(), want)
     tot = sum(int.from_bytes(f.tobytes(), "little") for f in want[256:512]) % (1 << 256)
     assert int.from_bytes(bs.cpu().numpy()[1].tobytes(), "little") == tot
+
+
+def test_encoded_rows_lift_equals_schema_kernel(gpu):
+    """The north_star record's canonical bytes (rsos_hip.synth.encode_rows) hashed by the fixed-length
+    kernels -- compile-time (aligned) and runtime (4 bytes off) -- and by the offsets kernel equal the
+    schema kernel's lift from the columns, for 16 B / 64 B dated and projection and u64 / 64 B
+    dated and plain records (120, 100, 104, 80 B)."""
+    import torch
+    from rsos_hip import RecordSchema, lift_encoded, lift_fixed, lift_records
+    from rsos_hip.synth import encode_rows, make_records
+    for s in (RecordSchema.dated("bytes16", "bytes64"), RecordSchema.projection("bytes16", "bytes64"),
+              RecordSchema.dated("u64", "bytes64"), RecordSchema.plain("u64", "bytes64")):
+        n = 300_001
+        cols = make_records(s, n, seed=8)
+        rows = encode_rows(s, cols)
+        assert rows.shape == (n, s.record_len())
+        flat = rows.view(-1)
+        ref, rb = lift_records(s, cols)
+        mis = torch.zeros(flat.numel() + 16, dtype=torch.uint8, device="cuda")
+        mis[4:4 + flat.numel()] = flat
+        offs = torch.arange(0, n + 1, dtype=torch.int64, device="cuda") * rows.shape[1]
+        for got, gb in (lift_fixed(flat, rows.shape[1]), lift_fixed(mis[4:4 + flat.numel()], rows.shape[1]),
+                        lift_encoded(flat, offs)):
+            assert torch.equal(got, ref) and torch.equal(gb, rb)
 
 
 def test_fixed_equals_encoded_full_size(gpu, oracle_lib):

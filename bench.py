@@ -13,7 +13,7 @@ canonical bytes per record), one globally key-sorted set cut into N equal-count 
 shards.  Strong scaling: at N = 1 one MI355X holds all 100 M records (the north_star target);
 at N = 8 each GPU holds 12.5 M.  `--config config2` is BASELINE configs[1] (10 M per GPU, weak).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config1|config2|config3|config3_full|config4|config5|snapshot|rbsr|bench_u32]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config1|config2|config3|config3_full|config4|config5|encoded|snapshot|rbsr|bench_u32]
 
 --gpus N > 1 without a launcher: bench.py starts `python -m torch.distributed.run
 --nproc-per-node N` as a child process (no exec) and exits with its status; under a launcher
@@ -59,6 +59,10 @@ CONFIGS = {
              "rbsr reconciliation (SURVEY 8a row a13): two GPU-resident replicas of 10M records/GPU "
              "(16 B key / 64 B value, dated) differing in --diffs keys, FixedFanOut(16) rounds until no "
              "segment is left"),
+    "encoded": ("bytes16", "bytes64", "dated", 10_000_000,
+                "the drop-in encoded map (HipEncodedMap / EncodedFingerprintMap over rh_estore_*): {per} records "
+                "per GPU of Entry<Timestamp, Vec<u8>> with [u8; 16] keys and 64 B values as canonical bytes "
+                "(120 B each, what rsos::encoding::encode_to_vec gives), hashed by the fixed-length kernel"),
     "snapshot": ("bytes16", "bytes64", "dated", 10_000_000,
                  "snapshot reload (SURVEY 8f row 4): RCNL v1 file of 10M entries (16 B key / 64 B value, "
                  "10% tombstones) resident in HBM -> dated + projection stores"),
@@ -202,6 +206,8 @@ def main():
         return incremental(args, world, rank, dev, dist)
     if args.config == "snapshot":
         return reload(args, world, rank, dev, dist)
+    if args.config == "encoded":
+        return encoded(args, world, rank, dev, dist)
     if args.config == "rbsr":
         return reconcile(args, world, rank, dev, dist)
     kname, vname, kind, n_default, _ = CONFIGS[args.config]
@@ -560,6 +566,168 @@ def incremental(args, world, rank, dev, dist):
             line["cpu_baseline"] = cpu_baseline_incremental(schema, m, args.cpu_sample or 10_000_000)
         print(json.dumps(line), flush=True)
     st.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _encode_host(h) -> "np.ndarray":
+    """(n, 120) canonical bytes of dated 16 B / 64 B present records from host columns (numpy,
+    vectorised): u64 16 ‖ key ‖ phys ‖ logical ‖ node ‖ u32 0 ‖ u64 64 ‖ value -- the bytes
+    rsos::encoding::encode_to_vec of the key then the Entry gives (rsos/src/encoding.rs:17-35)."""
+    import numpy as np
+    n = h["keys"].shape[0]
+    out = np.empty((n, 120), np.uint8)
+    out[:, 0:8] = np.frombuffer((16).to_bytes(8, "little"), np.uint8)
+    out[:, 8:24] = h["keys"]
+    out[:, 24:32] = h["phys"].view(np.uint8).reshape(n, 8)
+    out[:, 32:36] = h["logical"].view(np.uint8).reshape(n, 4)
+    out[:, 36:44] = h["node"].view(np.uint8).reshape(n, 8)
+    out[:, 44:48] = 0
+    out[:, 48:56] = np.frombuffer((64).to_bytes(8, "little"), np.uint8)
+    out[:, 56:120] = h["values"]
+    return out
+
+
+def encoded(args, world, rank, dev, dist):
+    """--config encoded: the drop-in map for serde K / V (HipEncodedMap, rust/rsos-hip/src/encoded.rs;
+    its Python twin rsos_hip.emap.EncodedFingerprintMap) on the north_star record.  Records reach the
+    library as canonical bytes (rsos::encoding::encode_to_vec of the key then the value,
+    public-api/rsos.txt:61): here [u8; 16] keys and Entry<Timestamp, Vec<u8>> of 64 B, 120 B each.
+    A batch whose records share one length is hashed by the compile-time fixed-length kernel
+    (k_lift_fixed_ct<120>).  One step = one device-resident lift + block sums of the n encoded
+    records (what rh_estore_load runs after its upload).  Also timed, once: the host encode
+    (numpy, vectorised, for this fixed shape -- the Rust binding runs encode_to_vec per record), the
+    fill (rh_estore_load from host bytes: the bulk path of just_insert_bulk /
+    src/replica/write.rs:107-121 through the encoded store) and one 1 M-record batch
+    (rh_estore_apply of rank-addressed inserts, the map's staged-batch flush).  The ABI calls are the
+    ones HipEncodedMap::load_bulk / flush make; the Python map's own per-key index (a SortedList of
+    Python objects) is not what is timed."""
+    import ctypes as C
+    import numpy as np
+    from rsos_hip import RecordSchema, lift_fixed, lift_records, reduce_blocks
+    from rsos_hip import _abi as A
+    from rsos_hip.synth import make_records, to_host
+    kname, vname, kind, n_default, desc = CONFIGS["encoded"]
+    n = args.records or n_default
+    m = min(args.batch, n)
+    schema = getattr(RecordSchema, kind)(kname, vname)
+    L = schema.record_len()
+    cols = make_records(schema, n, seed=42, device=dev, first_index=rank * n, key_space=n * world)
+    h = to_host(cols)
+    t0 = time.perf_counter()
+    rows = _encode_host(h)
+    encode_s = time.perf_counter() - t0
+    offs = np.arange(n + 1, dtype=np.uint64) * np.uint64(L)
+    es = C.c_void_p()
+    A.check(A.lib().rh_estore_create(dev.index, C.byref(es)), "rh_estore_create")
+    t0 = time.perf_counter()
+    A.check(A.lib().rh_estore_load(es, rows.ctypes.data, offs.ctypes.data, n), "rh_estore_load")
+    fill_s = time.perf_counter() - t0
+    root0 = A.Aggregate()
+    A.check(A.lib().rh_estore_root(es, C.byref(root0)), "rh_estore_root")
+    # one batch of m fresh records, rank-addressed into the key order (the map's flush)
+    b = make_records(schema, m, seed=1000 + rank, device=dev, random_keys=True)
+    bh = to_host(b)
+    order = np.argsort(bh["keys"].copy().view("S16").ravel(), kind="stable")
+    bh = {k: np.ascontiguousarray(v[order]) for k, v in bh.items()}
+    existing = h["keys"].copy().view("S16").ravel()
+    bk = bh["keys"].copy().view("S16").ravel()
+    pos = np.searchsorted(existing, bk).astype(np.uint64)
+    present = (pos < n) & (existing[np.minimum(pos, n - 1)] == bk)
+    kinds = present.astype(np.uint8)  # 0 insert, 1 overwrite
+    t1 = time.perf_counter()
+    brows = _encode_host(bh)
+    bencode_s = time.perf_counter() - t1
+    boffs = np.arange(m + 1, dtype=np.uint64) * np.uint64(L)
+    t1 = time.perf_counter()
+    A.check(A.lib().rh_estore_apply(es, pos.ctypes.data, kinds.ctypes.data, m, brows.ctypes.data, boffs.ctypes.data, m),
+            "rh_estore_apply")
+    apply_s = time.perf_counter() - t1
+    root1 = A.Aggregate()
+    A.check(A.lib().rh_estore_root(es, C.byref(root1)), "rh_estore_root")
+    # the root moved by exactly the batch's lifts (all fresh keys): the schema kernel's sum of them
+    bfps, _ = lift_records(schema, {k: v.clone() for k, v in b.items()})
+    lim = bfps.view(torch.int16).to(torch.int64) & 0xFFFF
+    bsum = sum(int(c) << (16 * i) for i, c in enumerate(lim.sum(dim=0).cpu().tolist())) % (1 << 256)
+    r0 = sum(int(x) << (64 * i) for i, x in enumerate(root0.fingerprint))
+    r1 = sum(int(x) << (64 * i) for i, x in enumerate(root1.fingerprint))
+    if int(present.sum()) == 0 and ((r1 - r0) % (1 << 256) != bsum or root1.size != n + m):
+        raise SystemExit("bench: the encoded store's root after the batch differs from root + Σ batch lifts")
+    A.lib().rh_estore_destroy(es)
+    # device-resident steps: the encoded records' lift over bytes already in HBM
+    flat = torch.from_numpy(rows).to(dev).view(-1)
+    ref, _ = lift_records(schema, cols)
+    got, _ = lift_fixed(flat, L)
+    if not torch.equal(got, ref):
+        raise SystemExit("bench: encoded-bytes lift differs from the schema kernel's")
+    del got
+    spin = gpu_spinup(args.spinup_ms, dev)
+    for _ in range(args.warmup):
+        lift_fixed(flat, L)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _, bs = lift_fixed(flat, L)
+        e1.record()
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_s = sum(a.elapsed_time(c) for a, c in ev) / len(ev) / 1e3
+    # the schema kernel on the same records, for the ratio (median of 10)
+    sev = []
+    for _ in range(10):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        lift_records(schema, cols)
+        e1.record()
+        sev.append((e0, e1))
+    torch.cuda.synchronize()
+    schema_s = sorted(a.elapsed_time(c) for a, c in sev)[5] / 1e3
+    if rank == 0:
+        recs = n * args.steps * world
+        hbm = (L + 32) * n / kern_s / 1e9
+        line = {
+            "metric": "fingerprint-hash GiB/s + M records/s (device-resident) at 1/2/4/8 MI355X",
+            "value": round(recs * L / elapsed / 2**30, 2), "unit": "GiB/s",
+            "mrec_per_s": round(recs / elapsed / 1e6, 1),
+            "n_gpus": world, "dist": {"backend": dist.get_backend() if dist is not None else None, "world_size": world},
+            "steps": args.steps, "warmup": args.warmup, "spinup": spin,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded, SURVEY §8d generator) encoded to canonical bytes on the host; "
+                    "device-resident bytes for the timed steps",
+            "config": {"workload": describe("encoded", n * world, n, world), "records_per_gpu": n,
+                       "canonical_bytes_per_record": L, "hbm_bytes_per_record": L + 32,
+                       "parallelism": f"key-range shards x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(hbm / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "rh::k_lift_fixed_ct<120> (lift + block sums)", "kernel_avg_us": round(kern_s * 1e6, 2)},
+            "schema_kernel_us": round(schema_s * 1e6, 2), "encoded_over_schema": round(kern_s / schema_s, 4),
+            "map_path": {"host_encode_s": round(encode_s, 4), "host_encode_ns_per_record": round(encode_s / n * 1e9, 1),
+                         "encoder": "numpy, vectorised for this fixed shape",
+                         "fill_s": round(fill_s, 4), "fill_m_rec_per_s": round(n / fill_s / 1e6, 1),
+                         "fill": "rh_estore_load from pageable host bytes (H2D + lift + sums + root)",
+                         "batch": m, "batch_encode_s": round(bencode_s, 4), "apply_s": round(apply_s, 4),
+                         "apply_m_rec_per_s": round(m / apply_s / 1e6, 1),
+                         "apply": "rh_estore_apply: rank-addressed inserts (H2D + lift + segment merge + sums + root)",
+                         "root_check": "root after the batch == root before + Σ schema-kernel lifts of the batch"},
+        }
+        if args.cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(schema, cols, args.cpu_sample or min(n, 10_000_000))
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

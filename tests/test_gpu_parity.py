@@ -1148,44 +1148,45 @@ def test_store_apply_device_many_equals_one_by_one(gpu, oracle_lib):
         st.close()
 
 
-def _sort_keys16(torch, keys):
-    """Permutation sorting (n, 16) byte keys in memcmp order (the Ord of [u8; 16]): two stable
-    sorts on the big-endian u64 halves (sign-flipped so signed order is unsigned order)."""
-    flip = torch.iinfo(torch.int64).min
-    hi = keys[:, :8].flip(1).contiguous().view(torch.int64).view(-1) ^ flip
-    lo = keys[:, 8:].flip(1).contiguous().view(torch.int64).view(-1) ^ flip
-    p = torch.argsort(lo, stable=True)
-    return p[torch.argsort(hi[p], stable=True)], hi, lo
-
-
-def _torch_root_chunked(torch, fps, chunk=8_000_000) -> int:
-    return sum(_torch_root(torch, fps[i:i + chunk]) for i in range(0, fps.shape[0], chunk)) % M256
-
-
-def test_full_size_config5_100m(gpu, oracle_lib):
+@pytest.mark.parametrize("n", [10_000_000, 100_000_000], ids=["10m", "100m"])
+def test_full_size_config5_100m(gpu, oracle_lib, n):
     """config5 at its stated size (BASELINE configs[4]): 100 M resident 16 B / 64 B dated records,
     then 15 batches of 1 M rows -- 900 k fresh random keys, 50 k overwrites and 50 k deletes of
     resident keys each -- so the delta run passes the compaction threshold at this size (a
-    112 M-row base is merged at least once).  Afterwards, against an independent torch reduction and
-    sort of exactly the records that should be live: the root and size; select at 200 ranks; rank
-    of present and absent keys; 40 rank-range and key-range aggregates; and the fingerprints at 20
-    sampled ranks against the oracle's lift of those records (mutate.rs:23-154 semantics)."""
+    111 M-row base is merged at least once).  Afterwards, against exactly the records that should be
+    live (assembled and key-sorted on the host with numpy; torch's gathers and sorts of 10^8-row
+    tensors gave wrong rows on this image): the root and size (an independent torch reduction of
+    their lifts); the store's whole rank order dumped -- every key and fingerprint, row for row;
+    select at 200 ranks; rank of present and absent keys; 20 rank-range and key-range aggregates;
+    and the fingerprints at 20 sampled ranks against the oracle's lift of those records
+    (mutate.rs:23-154 semantics)."""
     import torch
     from rsos_hip import GpuFingerprintStore, RecordSchema, lift_records
+    from rsos_hip import _abi as A
     from rsos_hip.store import KeyRange
     from rsos_hip.synth import make_records, to_host
     O = oracle_lib
     s = RecordSchema.dated("bytes16", "bytes64")
-    n, m, K, touch = 100_000_000, 1_000_000, 15, 50_000
+    m, K, touch = 1_000_000, 15, 50_000
     base = make_records(s, n, seed=5)
+
+    def lift_host(cols):  # (rows, 32) uint8 lifts on the host, lifted in 16 M-row chunks
+        rows = cols["keys"].shape[0]
+        out = np.empty((rows, 32), np.uint8)
+        for i in range(0, rows, 16_000_000):
+            f = lift_records(s, {c: t[i:i + 16_000_000] for c, t in cols.items()}, block_sums=False)[0]
+            out[i:i + 16_000_000] = f.cpu().numpy()
+        return out
+
+    bf = lift_host(base)
     st = GpuFingerprintStore(s)
     st.load_bulk_device(base)
     st.reserve(n + K * m, m)
-    perm = torch.randperm(n, generator=torch.Generator(device="cuda").manual_seed(9), device="cuda")
+    perm = np.random.default_rng(9).permutation(n)[:K * 2 * touch]
     batches, ops = [], []
     for k in range(K):
         ins = make_records(s, m - 2 * touch, seed=700 + k, random_keys=True)
-        rows = perm[k * 2 * touch:(k + 1) * 2 * touch]
+        rows = torch.from_numpy(perm[k * 2 * touch:(k + 1) * 2 * touch]).cuda()
         ex = {c: t[rows].clone() for c, t in base.items()}
         ex["values"][:touch] ^= 0x3C  # overwrites: new values for existing keys
         ex["phys"][:touch] += 7
@@ -1198,57 +1199,66 @@ def test_full_size_config5_100m(gpu, oracle_lib):
     counts = st.apply_device_many(batches, ops)
     assert counts == [(m - 2 * touch, touch, touch)] * K
     assert st.stats()["compactions"] - comp0 >= 1
-    # the live set: resident rows not touched, the overwritten rows' new records, the inserted rows
-    keep = torch.ones(n, dtype=torch.bool, device="cuda")
-    keep[perm[:K * 2 * touch]] = False
-    parts = [{c: t[keep] for c, t in base.items()}]
-    for b in batches:
-        parts.append({c: t[:m - touch] for c, t in b.items()})  # inserts + overwrites
-    del base
-    live = {c: torch.cat([p[c] for p in parts]).contiguous() for c in parts[0]}
-    del parts
-    N = live["keys"].shape[0]
+    # the live set on the host: resident rows not touched, the overwritten rows' new records, the
+    # inserted rows; origin r < n: base row r, n + k * m + j: row j of batch k
+    keep = np.ones(n, bool)
+    keep[perm] = False
+    ek = [base["keys"].cpu().numpy()[keep]]
+    ef = [bf[keep]]
+    origin = [np.nonzero(keep)[0]]
+    del bf
+    for k, b in enumerate(batches):
+        part = {c: t[:m - touch] for c, t in b.items()}  # inserts + overwrites
+        ek.append(part["keys"].cpu().numpy())
+        ef.append(lift_host(part))
+        origin.append(n + k * m + np.arange(m - touch))
+    ek, ef, origin = np.concatenate(ek), np.concatenate(ef), np.concatenate(origin)
+    N = ek.shape[0]
     assert N == n + K * (m - 3 * touch)
-    fps = torch.empty((N, 32), dtype=torch.uint8, device="cuda")
-    for i in range(0, N, 16_000_000):
-        fps[i:i + 16_000_000] = lift_records(s, {c: t[i:i + 16_000_000] for c, t in live.items()},
-                                             block_sums=False)[0]
     root = st.aggregate()
     assert root.size == N == st.size()
-    assert root.fingerprint.to_int() == _torch_root_chunked(torch, fps)
-    order, hi, lo = _sort_keys16(torch, live["keys"])
-    skeys = live["keys"][order]
-    sfps = fps[order]
+    want_root = sum(_torch_root(torch, torch.from_numpy(ef[i:i + 8_000_000]).cuda()) for i in range(0, N, 8_000_000))
+    assert root.fingerprint.to_int() == want_root % M256
+    # memcmp order: the big-endian leading u64 (unique across these keys), then the rest
+    hi = ek[:, :8].copy().view(">u8").ravel().astype(np.uint64)
+    lo = ek[:, 8:].copy().view(">u8").ravel().astype(np.uint64)
+    order = np.lexsort((lo, hi))
+    ek, ef, origin, hi, lo = ek[order], ef[order], origin[order], hi[order], lo[order]
+    # the store's whole rank order, row for row
+    dk = np.zeros(N * 16, np.uint8)
+    A.check(A.lib().rh_store_keys(st._h, 0, N, dk.ctypes.data), "rh_store_keys")
+    assert np.array_equal(dk.reshape(N, 16), ek)
+    del dk
+    assert np.array_equal(st.fingerprints(), ef)
     rng = np.random.default_rng(17)
     rs = [0, N - 1] + [int(x) for x in rng.integers(0, N, 198)]
     for r in rs:
-        assert st.select(r) == skeys[r].cpu().numpy().tobytes()
-    flip = torch.iinfo(torch.int64).min
-    for r in rs[:40]:  # present keys: their own rank; a key just above: one more
-        k = skeys[r].cpu().numpy().tobytes()
-        assert st.rank(k) == r
-        k2 = bytearray(k)
+        assert st.select(r) == ek[r].tobytes()
+    for r in rs[:40]:  # present keys: their own rank; a key with its last bit flipped: counted
+        assert st.rank(ek[r].tobytes()) == r
+        k2 = bytearray(ek[r].tobytes())
         k2[15] ^= 1
-        k2 = bytes(k2)
-        t = torch.frombuffer(bytearray(k2), dtype=torch.uint8).cuda()
-        khi = int(t[:8].flip(0).contiguous().view(torch.int64)) ^ flip
-        klo = int(t[8:].flip(0).contiguous().view(torch.int64)) ^ flip
-        want = int(((hi < khi) | ((hi == khi) & (lo < klo))).sum())
-        assert st.rank(k2) == want
+        khi, klo = int.from_bytes(k2[:8], "big"), int.from_bytes(k2[8:], "big")
+        i = int(np.searchsorted(hi, np.uint64(khi), "left"))
+        while i < N and int(hi[i]) == khi and int(lo[i]) < klo:
+            i += 1
+        assert st.rank(bytes(k2)) == i
     for _ in range(20):
         a = int(rng.integers(0, N))
         b = min(N, a + int(rng.integers(0, 2_000_000)))
         g = st.aggregates_ranks([a], [b])[0]
-        assert g.size == b - a and g.fingerprint.to_int() == _torch_root(torch, sfps[a:b])
-        ka, kb = skeys[a].cpu().numpy().tobytes(), skeys[b].cpu().numpy().tobytes() if b < N else None
-        g2 = st.aggregate(KeyRange(ka, kb))
+        assert g.size == b - a and g.fingerprint.to_int() == _torch_root(torch, torch.from_numpy(ef[a:b]).cuda())
+        g2 = st.aggregate(KeyRange(ek[a].tobytes(), ek[b].tobytes() if b < N else None))
         assert g2.size == b - a and g2.fingerprint.to_int() == g.fingerprint.to_int()
-    # the stored fingerprints at sampled ranks against the oracle's lift of the same records
-    pick = torch.tensor(sorted(rs[:20]), dtype=torch.int64, device="cuda")
-    src = order[pick]
-    h = to_host({c: t[src] for c, t in live.items()})
+    # the fingerprints at sampled ranks against the oracle's lift of the same source records
+    pick = sorted(rs[:20])
+    recs = []
+    for r in pick:
+        o = int(origin[r])
+        src, row = (base, o) if o < n else (batches[(o - n) // m], (o - n) % m)
+        recs.append(to_host({c: t[row:row + 1] for c, t in src.items()}))
+    h = {c: np.concatenate([x[c] for x in recs]) for c in recs[0]}
     sc = O.Schema(s.key_kind, s.key_len, s.value_kind, s.value_len, s.record_kind, 0)
     want = O.Records(sc, h["keys"], h["values"], h["phys"], h["logical"], h["node"], None).lift()
-    got = np.stack([st.fingerprints(int(r), int(r) + 1)[0] for r in pick.cpu().tolist()])
-    assert np.array_equal(got, want)
+    assert np.array_equal(ef[pick], want)
     st.close()

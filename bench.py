@@ -97,6 +97,9 @@ def parse():
     p.add_argument("--pipeline", type=int, default=1,
                    help="config5: 1 = the timed batches through one apply_device_many call (batch i + 1 "
                         "lifted while batch i's result returns); 0 = one apply_device call per batch")
+    p.add_argument("--compact-div", type=int, default=0,
+                   help="config5: compaction divisor (the delta run merges into the base past base / divisor rows; "
+                        "0 = the library's default)")
     p.add_argument("--overwrite", type=float, default=0.0,
                    help="config5: fraction of each batch that re-stamps existing keys (the new - old delta)")
     p.add_argument("--e2e", type=int, default=-1,
@@ -433,6 +436,8 @@ def incremental(args, world, rank, dev, dist):
     n = args.records or n_default
     schema = getattr(RecordSchema, kind)(kname, vname)
     st = GpuFingerprintStore(schema, device=dev.index)
+    if args.compact_div:
+        st.set_compaction(args.compact_div, 65536)
     base = make_records(schema, n, seed=42, device=dev, first_index=rank * n, key_space=n * world)
     # shard splitters: the first key of every shard but the first (the generator is counter-based)
     splitters = torch.cat([make_records(schema, 1, seed=42, device=dev, first_index=r * n, key_space=n * world)["keys"]
@@ -560,7 +565,7 @@ def incremental(args, world, rank, dev, dist):
                      "apply_device per batch (lift + sort + base/delta search + delta merge; amortised "
                      "compaction) + the whole map's root after each"),
             "compactions_in_timed_steps": stats["compactions"] - comp0, "delta_rows_at_end": stats["delta_rows"],
-            "reserved_rows": reserved,
+            "reserved_rows": reserved, "compaction_divisor": args.compact_div or 6,
         }
         if args.cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_incremental(schema, m, args.cpu_sample or 10_000_000)

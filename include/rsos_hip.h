@@ -311,7 +311,7 @@ int rh_store_apply_device_many(rh_store *store, const rh_columns *dev_cols, cons
 
 /* LSM maintenance.  A batch merges into a sorted signed-delta run (O(batch + delta)); the delta
  * run merges into the base run when it exceeds max(base / divisor, min_rows) rows (default
- * 8, 65536), and before rank-order queries (select, rank-range aggregates, key / fingerprint
+ * 6, 65536), and before rank-order queries (select, rank-range aggregates, key / fingerprint
  * dumps).  Results never depend on the policy, only timings do.                            */
 int rh_store_compact(rh_store *store);
 int rh_store_set_compaction(rh_store *store, uint64_t divisor, uint64_t min_rows);

@@ -569,7 +569,7 @@ struct rh_store {
     DevBuf<int32_t> dscnt;     // k_delta_finish's per-super-block count totals
     DevBuf<uint32_t> fin_ticket;
     DevBuf<uint64_t> mcnt;    // merge counters
-    uint64_t compact_div = 8, compact_min = 65536, compactions = 0;
+    uint64_t compact_div = 6, compact_min = 65536, compactions = 0;  // 6: the measured optimum (profiles/r03_c5_divisor_sweep_64.txt)
     // the whole-map fingerprint = base total + delta contribution total, kept on the host after
     // every load / batch / compaction (the reference's root node Aggregate): aggregate(..) is O(1)
     uint64_t root_b[4] = {0, 0, 0, 0}, root_d[4] = {0, 0, 0, 0};

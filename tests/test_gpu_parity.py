@@ -1151,7 +1151,7 @@ def test_store_apply_device_many_equals_one_by_one(gpu, oracle_lib):
 @pytest.mark.parametrize("n", [10_000_000, 100_000_000], ids=["10m", "100m"])
 def test_full_size_config5_100m(gpu, oracle_lib, n):
     """config5 at its stated size (BASELINE configs[4]): 100 M resident 16 B / 64 B dated records,
-    then 15 batches of 1 M rows -- 900 k fresh random keys, 50 k overwrites and 50 k deletes of
+    then 18 batches of 1 M rows -- 900 k fresh random keys, 50 k overwrites and 50 k deletes of
     resident keys each -- so the delta run passes the compaction threshold at this size (a
     111 M-row base is merged at least once).  Afterwards, against exactly the records that should be
     live (assembled and key-sorted on the host with numpy; torch's gathers and sorts of 10^8-row
@@ -1167,7 +1167,7 @@ def test_full_size_config5_100m(gpu, oracle_lib, n):
     from rsos_hip.synth import make_records, to_host
     O = oracle_lib
     s = RecordSchema.dated("bytes16", "bytes64")
-    m, K, touch = 1_000_000, 15, 50_000
+    m, K, touch = 1_000_000, 18, 50_000
     base = make_records(s, n, seed=5)
 
     def lift_host(cols):  # (rows, 32) uint8 lifts on the host, lifted in 16 M-row chunks

@@ -311,11 +311,16 @@ __device__ __forceinline__ void hash_merged(const uint32_t *kw, const uint32_t *
     }
 }
 
-// lift one record (present or tombstone) of schema (KK,KL,VK,VL,RK); TAGS: tomb varies per lane
-template <int KK, int KL, int VK, int VL, int RK, bool TAGS = true>
-__device__ __forceinline__ void lift_record(const uint32_t *kw, const uint32_t *sw, bool tomb,
-                                            const uint8_t *vrow, uint32_t h[8]) {
-    using L = Layout<KK, KL, VK, VL, RK>;
+// A layout whose value rows are only known to be A-byte aligned (rows read from a staged file)
+template <class L, int A>
+struct LayoutAligned : L {
+    static constexpr int ROW_ALIGN = cmin(L::ROW_ALIGN, A);
+};
+
+// lift one record (present or tombstone) of layout L; TAGS: tomb varies per lane
+template <class L, int KK, int RK, bool TAGS>
+__device__ __forceinline__ void lift_record_l(const uint32_t *kw, const uint32_t *sw, bool tomb,
+                                              const uint8_t *vrow, uint32_t h[8]) {
     if constexpr (TAGS && RK != REC_PLAIN && L::SMALL && L::LEN_TOMB <= 64) {
         hash_merged<L, KK, RK>(kw, sw, tomb, vrow, h);
     } else if (RK != REC_PLAIN && tomb) {
@@ -328,6 +333,13 @@ __device__ __forceinline__ void lift_record(const uint32_t *kw, const uint32_t *
         build_prefix<L, KK, RK>(kw, sw, false, pw);
         hash_present<L>(pw, vrow, h);
     }
+}
+
+// lift one record (present or tombstone) of schema (KK,KL,VK,VL,RK); TAGS: tomb varies per lane
+template <int KK, int KL, int VK, int VL, int RK, bool TAGS = true>
+__device__ __forceinline__ void lift_record(const uint32_t *kw, const uint32_t *sw, bool tomb,
+                                            const uint8_t *vrow, uint32_t h[8]) {
+    lift_record_l<Layout<KK, KL, VK, VL, RK>, KK, RK, TAGS>(kw, sw, tomb, vrow, h);
 }
 
 constexpr int LIFT_THREADS = 256;

@@ -209,6 +209,21 @@ hipError_t launch_lift_schema(int kk, int kl, int vk, int vl, int rk, bool tags,
     *supported = false;
     return hipSuccess;
 }
+
+#define X(name, kk, kl, vk, vl) \
+    hipError_t launch_snap_lift_##name(int mode, const SnapLift &a, uint64_t lds, hipStream_t st, bool *supported);
+#include "schemas.def"
+#undef X
+
+hipError_t launch_snap_lift_schema(int kk, int kl, int vk, int vl, int mode, const SnapLift &a, uint64_t lds,
+                                   hipStream_t st, bool *supported) {
+#define X(name, KK, KL, VK, VL) \
+    if (kk == KK && kl == KL && vk == VK && vl == VL) return launch_snap_lift_##name(mode, a, lds, st, supported);
+#include "schemas.def"
+#undef X
+    *supported = false;
+    return hipSuccess;
+}
 }  // namespace rh
 
 // =================================================================================================
@@ -901,6 +916,21 @@ struct rh_store {
     // finish waits, and re-orders the rows if the keys were not sorted
     PinnedVec<uint32_t> load_flag;
     int load_begin(const rh_columns &c, size_t m, bool lifted) {
+        int rc = load_prep(m);
+        if (rc) return rc;
+        if (m) {
+            RH_HIP(hipMemcpyAsync(bkeys[cb].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
+            if (!lifted &&
+                (rc = lift_dispatch(schema, c, m, bfps[cb].p, bsums.p, nullptr, nullptr, false, stream)))
+                return rc;
+            RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
+            RH_HIP(kops->check_sorted(bkeys[cb].p, m, flag.p, stream));
+        }
+        return load_sums(m, flag.p);
+    }
+    // a load's first part: an empty run with room for m base rows, whose keys, fingerprints and
+    // block sums the caller then writes into bkeys[cb], bfps[cb] and bsums
+    int load_prep(size_t m) {
         int rc;
         // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
@@ -916,21 +946,44 @@ struct rh_store {
         memset(root_d, 0, sizeof root_d);
         // the lift writes the block sums as it goes; they stand unless the keys turn out to be
         // unsorted (then the rows are re-ordered and everything is re-summed)
-        if ((rc = bsums.ensure(rh_num_blocks(m) * 32 + 32))) return rc;
-        if (m) {
-            RH_HIP(hipMemcpyAsync(bkeys[cb].p, c.keys, m * kl, hipMemcpyDeviceToDevice, stream));
-            if (!lifted &&
-                (rc = lift_dispatch(schema, c, m, bfps[cb].p, bsums.p, nullptr, nullptr, false, stream)))
-                return rc;
-            RH_HIP(hipMemsetAsync(flag.p, 0, 4, stream));
-            RH_HIP(kops->check_sorted(bkeys[cb].p, m, flag.p, stream));
-        }
+        return bsums.ensure(rh_num_blocks(m) * 32 + 32);
+    }
+    // the second part, once the m rows are in place (enqueued behind them on this stream):
+    // super sums, samples and the root; *unsorted (device) -> the host copy load_finish checks
+    int load_sums(size_t m, const uint32_t *unsorted) {
         nb = m;
         load_flag.assign(10, 0);  // [0] unsorted flag, [2..9] the base total (8-byte aligned)
         uint64_t *root_pin = reinterpret_cast<uint64_t *>(load_flag.data() + 2);
-        if ((rc = resum_base(true, root_pin))) return rc;
-        if (m) RH_HIP(hipMemcpyAsync(load_flag.data(), flag.p, 4, hipMemcpyDeviceToHost, stream));
+        int rc = resum_base(true, root_pin);
+        if (rc) return rc;
+        if (m) RH_HIP(hipMemcpyAsync(load_flag.data(), unsorted, 4, hipMemcpyDeviceToHost, stream));
         return RH_OK;
+    }
+    PinnedVec<uint64_t> snap_words;  // a fused snapshot reload's result words (snapshot_locate)
+    // A load whose rows are written before it is known to succeed (the fused snapshot reload):
+    // the rows go to the spare base buffers, and the store changes only at load_commit -- a
+    // corrupt file leaves it as it was, as Replica::load_snapshot does (src/snapshot.rs:76-98)
+    DevBuf<uint8_t> sbsums;
+    int load_target(size_t m) {
+        if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        const int nxt = 1 - cb;
+        int rc;
+        if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) ||
+            (rc = sbsums.ensure(rh_num_blocks(m) * 32 + 32)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
+            return rc;
+        return RH_OK;
+    }
+    int load_commit(size_t m, const uint32_t *unsorted) {
+        cb = 1 - cb;
+        std::swap(bsums.p, sbsums.p);
+        std::swap(bsums.cap, sbsums.cap);
+        version++;
+        base_epoch++;
+        nd = 0;
+        heap_len = 0;
+        dtotal = 0;
+        memset(root_d, 0, sizeof root_d);
+        return load_sums(m, unsorted);
     }
     // page-locked host tier capacity for `rows` rows ahead of the refresh that fills it: pinning
     // fresh pages is most of a first refresh (11-13 ms at 10^6 rows against ~1 ms of copying)
@@ -2056,6 +2109,88 @@ int snapshot_decode_into(const rh_schema &s, int key_form, const uint8_t *dev, s
     return RH_OK;
 }
 
+// The reload through the fused pass (snap_lift.hpp): locate the entries, then lift and load them
+// straight from the file into the stores' spare base buffers; one wait, then the stores commit
+// (a corrupt file leaves both as they were).  The caller holds both stores' locks and n > 0.
+int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::SnapFmt &f, const uint8_t *dev,
+                          uint64_t n, uint32_t nsmax, uint64_t lds, rh_snapshot_info *info) {
+    rh_store *a = dated ? dated : proj;
+    int rc;
+    for (rh_store *x : {dated, proj})
+        if (x && (rc = x->load_target(n))) return rc;
+    rh::SnapTables t;
+    RH_HIP(rh::snapshot_locate(f, dev, n, true, a->scratch, a->stream, &t));
+    const uint64_t nblk = (n + 255) / 256;
+    uint32_t *part = static_cast<uint32_t *>(a->scratch.get(98, nblk * 4));
+    if (a->scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+    RH_HIP(hipMemsetAsync(a->flag.p, 0, 4, a->stream));
+    rh::SnapLift L;
+    L.blob = dev;
+    L.f = f;
+    L.n = n;
+    L.nseg = t.nseg;
+    L.start = t.start;
+    L.segq = t.segq;
+    L.basev = t.basev;
+    L.nsmax = nsmax;
+    L.keys = a->bkeys[1 - a->cb].p;
+    L.fps = a->bfps[1 - a->cb].p;
+    L.bsums = a->sbsums.p;
+    if (mode == 2) {
+        L.keys2 = proj->bkeys[1 - proj->cb].p;
+        L.fps2 = proj->bfps[1 - proj->cb].p;
+        L.bsums2 = proj->sbsums.p;
+    }
+    L.words = t.words;
+    L.tomb_part = part;
+    L.unsorted = a->flag.p;
+    const rh_schema &s = a->schema;
+    bool sup = false;
+    RH_HIP(rh::launch_snap_lift_schema(s.key_kind, (int)s.key_len, s.value_kind, (int)s.value_len, mode, L, lds,
+                                       a->stream, &sup));
+    if (!sup) return fail(RH_ERR_STATE, "fused snapshot pass unavailable (internal error)");
+    RH_HIP(rh::snapshot_sum_tombstones(part, nblk, t.words, a->stream));
+    try {
+        a->snap_words.assign(4, 0);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "pinned result buffer");
+    }
+    RH_HIP(hipMemcpyAsync(a->snap_words.data(), t.words, 32, hipMemcpyDeviceToHost, a->stream));
+    if ((rc = a->sync())) return rc;
+    const uint64_t *w = a->snap_words.data();
+    if (w[3] < n || w[1])
+        return fail(RH_ERR_DATA, "snapshot entries are corrupt: " + std::to_string(std::min<uint64_t>(w[3], n)) +
+                                     " of " + std::to_string(n) +
+                                     " entries parse (bad State variant, Vec length or end of file)");
+    rh_snapshot_info inf{};
+    inf.entries = n;
+    inf.tombstones = w[2];
+    inf.entries_end = w[0];
+    // the stores change from here on.  A failure in either half of either store leaves BOTH
+    // stores empty (streams drained): never a new size beside an old root, nor one store
+    // replaced and the other not
+    for (rh_store *x : {dated, proj}) {
+        if (!x) continue;
+        if (x == proj && fail_point("snapshot.load_begin")) rc = fail(RH_ERR_OOM, "injected failure (load_begin)");
+        else rc = x->load_commit(n, a->flag.p);
+        if (rc) break;
+    }
+    for (rh_store *x : {dated, proj}) {
+        if (rc || !x) break;
+        if (x == dated && fail_point("snapshot.load_finish")) rc = fail(RH_ERR_OOM, "injected failure (load_finish)");
+        else rc = x->load_finish(n, true);
+        inf.keys = x->nb;
+    }
+    if (rc) {
+        const std::string msg = g_err;
+        for (rh_store *x : {dated, proj})
+            if (x) x->reset_empty();
+        return fail(rc, msg);
+    }
+    if (info) *info = inf;
+    return RH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2147,6 +2282,20 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
         if ((rc = a->snap.ensure(len + 16))) return rc;
         RH_HIP(hipMemcpyAsync(a->snap.p, bytes, len, hipMemcpyHostToDevice, a->stream));
         dev = a->snap.p;
+    }
+    {  // the fused pass, where the shape has one (records up to 192 B)
+        const int mode = dated && proj ? 2 : dated ? 0 : 1;
+        uint32_t nsmax = 0;
+        const uint64_t lds = n ? rh::snap_lift_lds_bytes(f, &nsmax) : 0;
+        bool fused = false;
+        if (lds)
+            RH_HIP(rh::launch_snap_lift_schema(ds.key_kind, (int)ds.key_len, ds.value_kind, (int)ds.value_len, mode,
+                                               rh::SnapLift{}, lds, a->stream, &fused));
+        if (fused) {
+            rc = snapshot_reload_fused(dated, proj, mode, f, dev, n, nsmax, lds, info);
+            if (!on_device) a->snap.release();
+            return rc;
+        }
     }
     DevColumns &stg = a->staging;
     const size_t kr = key_row(ds), vr = value_row(ds);

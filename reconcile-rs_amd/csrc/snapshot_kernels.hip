@@ -24,94 +24,21 @@
 #include <algorithm>
 #include <vector>
 
+#include "snap_device.hpp"
 #include "snapshot_kernels.hpp"
 
 namespace rh {
 
 namespace {
 
-constexpr uint32_t SNAP_BAD = 0xffffffffu;
+constexpr uint32_t SNAP_BAD = snap::BAD;
 constexpr uint32_t SNAP_FAN = 32;
 constexpr uint32_t SNAP_LDS = 32768;  // staged bytes per workgroup
-
-// A run of the blob staged in LDS: bytes [a, a + 4 * words) (a 16-aligned), zero past the end.
-struct Img {
-    const uint32_t *w;
-    uint64_t a;
-    __device__ __forceinline__ uint32_t ld32(uint64_t p) const { return w[(p - a) >> 2]; }
-    __device__ __forceinline__ uint64_t ld64(uint64_t p) const {
-        return (uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32);
-    }
-};
-
-// the 16 bytes at q, zero past `len`
-__device__ __forceinline__ uint4 load16(const uint8_t *blob, uint64_t len, uint64_t q) {
-    if (q + 16 <= len) return *reinterpret_cast<const uint4 *>(blob + q);
-    uint32_t t[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-        uint32_t x = 0;
-        for (int k = 0; k < 4; k++) {
-            const uint64_t o = q + 4 * d + k;
-            if (o < len) x |= (uint32_t)blob[o] << (8 * k);
-        }
-        t[d] = x;
-    }
-    return make_uint4(t[0], t[1], t[2], t[3]);
-}
-
-// stage blob bytes [a, b) (a 16-aligned) into lds; bytes at or past `len` read as 0.  Each lane
-// issues up to STAGE_U 16-byte loads before its first LDS store, so a one-wave workgroup keeps
-// several KiB in flight instead of one load per round trip.
-constexpr int STAGE_U = 8;
-__device__ __forceinline__ void stage(const uint8_t *blob, uint64_t len, uint64_t a, uint64_t b, uint32_t *lds) {
-    const uint64_t step = 16ull * blockDim.x;
-    for (uint64_t q0 = a + 16ull * threadIdx.x; q0 < b; q0 += step * STAGE_U) {
-        uint4 v[STAGE_U];
-#pragma unroll
-        for (int u = 0; u < STAGE_U; u++) {
-            const uint64_t q = q0 + step * u;
-            if (q < b) v[u] = load16(blob, len, q);
-        }
-#pragma unroll
-        for (int u = 0; u < STAGE_U; u++) {
-            const uint64_t q = q0 + step * u;
-            if (q < b) *reinterpret_cast<uint4 *>(lds + ((q - a) >> 2)) = v[u];
-        }
-    }
-}
-
-// length of the entry starting at p, or 0 if no valid entry starts there.  The image must
-// cover p + lp or the end of the file.
-__device__ __forceinline__ uint32_t entry_len(const Img &m, const SnapFmt &f, uint64_t p) {
-    if (p + f.lt > f.len) return 0;
-    if (f.key_pre && m.ld64(p) != f.key_len) return 0;
-    const uint32_t v = m.ld32(p + f.key_pre + f.key_len + 20);
-    if (v == 1) return f.lt;
-    if (v != 0 || p + f.lp > f.len) return 0;
-    if (f.val_pre && m.ld64(p + f.lt) != f.val_len) return 0;
-    return f.lp;
-}
-
-__device__ __forceinline__ uint64_t seg_start(const SnapFmt &f, uint64_t s) { return f.base + s * f.seg; }
-
-// lane-strided walk over cnt rows of W dwords: fn(j, row, dword) with j = row * W + dword; the
-// (row, dword) pair is advanced incrementally -- one division per lane, not one per dword
-template <class Fn>
-__device__ __forceinline__ void for_dwords(uint32_t cnt, uint32_t W, Fn fn) {
-    if (W == 0) return;
-    uint32_t e = threadIdx.x / W, q = threadIdx.x - e * W;
-    const uint32_t de = blockDim.x / W, dq = blockDim.x - de * W;
-    for (uint32_t j = threadIdx.x; j < cnt * W; j += blockDim.x) {
-        fn(j, e, q);
-        q += dq;
-        e += de;
-        if (q >= W) {
-            q -= W;
-            e++;
-        }
-    }
-}
+using snap::Img;
+using snap::entry_len;
+using snap::for_dwords;
+using snap::seg_start;
+using snap::stage;
 
 // step 1: transfer function of every (segment, candidate first-entry position); G segments
 // per workgroup, lane = segment * P + candidate
@@ -168,14 +95,19 @@ __global__ void k_snap_up(const uint32_t *ex, const CIn *cnt, uint64_t nin, uint
     cnt_out[t] = c;
 }
 
-// step 2 (down): true entry position and entry index at the start of every child group
+// step 2 (down): true entry position and entry index at the start of every child group.  At
+// level 0 with segq given (the fused reload): segq[b] = the segment holding entry
+// min(256 b, n) - 1 for b in [1, ceil(n / 256)] -- the first and last segments a 256-entry
+// block of the lift reads (segq[0] = 0 is set by the caller)
 template <class CIn>
 __global__ void k_snap_down(const uint32_t *ex, const CIn *cnt, uint64_t nl, uint32_t P, const uint32_t *start_up,
-                            const uint64_t *base_up, uint64_t nup, uint32_t *start, uint64_t *basev) {
+                            const uint64_t *base_up, uint64_t nup, uint32_t *start, uint64_t *basev,
+                            uint32_t *segq = nullptr, uint64_t n = 0) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nup) return;
     uint32_t x = start_up[g];
     uint64_t c = base_up[g];
+    const uint64_t nblk = (n + 255) / 256;
     for (uint32_t j = 0; j < SNAP_FAN; j++) {
         const uint64_t s = g * SNAP_FAN + j;
         if (s >= nl) break;
@@ -183,7 +115,13 @@ __global__ void k_snap_down(const uint32_t *ex, const CIn *cnt, uint64_t nl, uin
         basev[s] = c;
         if (x != SNAP_BAD) {
             const uint64_t i = s * P + x;
-            c += cnt[i];
+            const uint64_t c1 = c + cnt[i];  // entries [c, c1) start in segment s
+            if (segq && c < n) {
+                for (uint64_t b = std::max<uint64_t>(1, (c + 256) / 256); b < nblk && 256 * b - 1 < c1; b++)
+                    segq[b] = (uint32_t)s;
+                if (n - 1 < c1) segq[nblk] = (uint32_t)s;
+            }
+            c = c1;
             x = ex[i];
         }
     }
@@ -305,15 +243,11 @@ inline dim3 grid_for(uint64_t threads) { return dim3((uint32_t)((threads + 255) 
 
 }  // namespace
 
-hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, uint8_t *keys, uint64_t *phys,
-                           uint32_t *logical, uint64_t *node, uint8_t *tags, uint8_t *values, Scratch &s,
-                           hipStream_t st, SnapResult *res, int *corrupt) {
-    *res = SnapResult{};
-    *corrupt = 0;
-    if (n == 0) {
-        res->entries_end = f.base;
-        return hipSuccess;
-    }
+// steps 1 and 2: the true first-entry position and entry index of every segment (and with
+// segq, every 256-entry block's first and last segment).  words[3] = entries on the chain from
+// the file's first entry; words[0..2] zeroed for the pass that follows.  Nothing is waited for.
+hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bool with_segq, Scratch &s,
+                           hipStream_t st, SnapTables *t) {
     hipError_t e;
     const uint32_t P = f.phases;
     if (P > 256 || f.seg + f.lp + 32 > SNAP_LDS) return hipErrorInvalidValue;
@@ -333,6 +267,8 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
         basev[l] = static_cast<uint64_t *>(s.get(67 + 4 * l, sizes[l] * 8));
     }
     unsigned long long *words = static_cast<unsigned long long *>(s.get(97, 64));
+    const uint64_t nblk = (n + 255) / 256;
+    uint32_t *segq = with_segq ? static_cast<uint32_t *>(s.get(99, (nblk + 1) * 4)) : nullptr;
     if (s.err) return s.err;
     // staged bytes of a run of G segments: G * seg + lp (+ 16 for the aligned start)
     auto img_bytes = [&](uint32_t G) { return ((uint64_t)G * f.seg + f.lp + 16 + 15) / 16 * 16; };
@@ -362,25 +298,61 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
     if ((e = hipMemsetAsync(start[L - 1], 0, 4, st)) || (e = hipMemsetAsync(basev[L - 1], 0, 8, st)) ||
         (e = hipMemsetAsync(words, 0, 64, st)))
         return e;
-    // entries on the chain from the file's first entry (checked against n at the end: a short
-    // chain only leaves rows unwritten, every access stays inside the blob and the columns)
-    uint64_t parsed = 0;
-    uint32_t parsed32 = 0;
-    if (L == 1) {
-        if ((e = hipMemcpyAsync(&parsed32, cnt[0], 4, hipMemcpyDeviceToHost, st))) return e;
-    } else {
-        if ((e = hipMemcpyAsync(&parsed, cnt[L - 1], 8, hipMemcpyDeviceToHost, st))) return e;
-    }
+    if (segq && (e = hipMemsetAsync(segq, 0, (nblk + 1) * 4, st))) return e;
+    // entries on the chain from the file's first entry (checked against n by the caller: a short
+    // chain only leaves rows unwritten, every access stays inside the blob and the outputs)
+    if ((e = hipMemcpyAsync(words + 3, cnt[L - 1], L == 1 ? 4 : 8, hipMemcpyDeviceToDevice, st))) return e;
     for (size_t l = L - 1; l-- > 0;) {
         if (l == 0)
             hipLaunchKernelGGL(k_snap_down<uint32_t>, grid_for(sizes[1]), dim3(256), 0, st, ex[0],
                                static_cast<const uint32_t *>(cnt[0]), sizes[0], P, start[1], basev[1], sizes[1],
-                               start[0], basev[0]);
+                               start[0], basev[0], segq, n);
         else
             hipLaunchKernelGGL(k_snap_down<uint64_t>, grid_for(sizes[l + 1]), dim3(256), 0, st, ex[l],
                                static_cast<const uint64_t *>(cnt[l]), sizes[l], P, start[l + 1], basev[l + 1],
-                               sizes[l + 1], start[l], basev[l]);
+                               sizes[l + 1], start[l], basev[l], nullptr, 0);
     }
+    if ((e = hipGetLastError())) return e;
+    t->start = start[0];
+    t->basev = basev[0];
+    t->segq = segq;
+    t->words = words;
+    t->nseg = nseg;
+    return hipSuccess;
+}
+
+// LDS of one fused-reload workgroup: the staged run of segments holding 257 consecutive entries.
+// A segment holds at least floor(seg / lp) entry starts, so 257 entries span at most
+// 257 / that + 2 segments.  0 when that exceeds 64 KiB (or 256 walker lanes).
+uint64_t snap_lift_lds_bytes(const SnapFmt &f, uint32_t *nsmax) {
+    const uint64_t per = f.lp ? f.seg / f.lp : 0;
+    if (per == 0) return 0;
+    const uint64_t ns = 257 / per + 2;
+    const uint64_t bytes = std::max<uint64_t>((ns * f.seg + f.lp + 16 + 15) / 16 * 16, sizeof(SumTile));
+    if (ns > 256 || bytes > 65536) return 0;
+    *nsmax = (uint32_t)ns;
+    return bytes;
+}
+
+hipError_t snapshot_sum_tombstones(const uint32_t *part, uint64_t groups, unsigned long long *words, hipStream_t st) {
+    const uint32_t sum_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, (groups + 1023) / 1024));
+    hipLaunchKernelGGL(k_snap_sum, dim3(sum_grid), dim3(1024), 0, st, part, groups, words);
+    return hipGetLastError();
+}
+
+hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, uint8_t *keys, uint64_t *phys,
+                           uint32_t *logical, uint64_t *node, uint8_t *tags, uint8_t *values, Scratch &s,
+                           hipStream_t st, SnapResult *res, int *corrupt) {
+    *res = SnapResult{};
+    *corrupt = 0;
+    if (n == 0) {
+        res->entries_end = f.base;
+        return hipSuccess;
+    }
+    hipError_t e;
+    SnapTables t;
+    if ((e = snapshot_locate(f, blob, n, false, s, st, &t))) return e;
+    auto img_bytes = [&](uint32_t G) { return ((uint64_t)G * f.seg + f.lp + 16 + 15) / 16 * 16; };
     // 3. list + scatter: one wave per run of G segments (G walker lanes, then all 64 lanes scatter)
     {
         uint32_t G = 4;
@@ -390,23 +362,20 @@ hipError_t snapshot_decode(const SnapFmt &f, const uint8_t *blob, uint64_t n, ui
         };
         while (G > 1 && lds_bytes(G) > SNAP_LDS) G--;
         const uint32_t cap = G * (uint32_t)(f.seg / f.lt + 1);
-        const uint64_t groups = (nseg + G - 1) / G;
+        const uint64_t groups = (t.nseg + G - 1) / G;
         uint32_t *part = static_cast<uint32_t *>(s.get(98, groups * 4));
         if (s.err) return s.err;
-        hipLaunchKernelGGL(k_snap_decode, dim3((uint32_t)groups), dim3(64), (size_t)lds_bytes(G), st, blob, f, nseg,
-                           G, cap, start[0], basev[0], n, reinterpret_cast<uint32_t *>(keys),
+        hipLaunchKernelGGL(k_snap_decode, dim3((uint32_t)groups), dim3(64), (size_t)lds_bytes(G), st, blob, f, t.nseg,
+                           G, cap, t.start, t.basev, n, reinterpret_cast<uint32_t *>(keys),
                            reinterpret_cast<uint32_t *>(phys), logical, reinterpret_cast<uint32_t *>(node), tags,
-                           reinterpret_cast<uint32_t *>(values), words, part);
-        const uint32_t sum_grid = (uint32_t)std::min<uint64_t>(256, (groups + 1023) / 1024);
-        hipLaunchKernelGGL(k_snap_sum, dim3(sum_grid), dim3(1024), 0, st, part, groups, words);
+                           reinterpret_cast<uint32_t *>(values), t.words, part);
+        if ((e = snapshot_sum_tombstones(part, groups, t.words, st))) return e;
     }
-    if ((e = hipGetLastError())) return e;
-    unsigned long long w[3] = {0, 0, 0};
-    if ((e = hipMemcpyAsync(w, words, 24, hipMemcpyDeviceToHost, st))) return e;
+    unsigned long long w[4] = {0, 0, 0, 0};
+    if ((e = hipMemcpyAsync(w, t.words, 32, hipMemcpyDeviceToHost, st))) return e;
     if ((e = hipStreamSynchronize(st))) return e;
-    if (L == 1) parsed = parsed32;
-    res->parsed = parsed;
-    if (parsed < n) {  // the file ends, or stops parsing, before entry n
+    res->parsed = w[3];
+    if (w[3] < n) {  // the file ends, or stops parsing, before entry n
         *corrupt = 1;
         return hipSuccess;
     }

@@ -27,6 +27,44 @@ struct SnapResult {
     uint64_t entries_end = 0;  // file offset just past entry n-1
 };
 
+// Where every segment's entries start (snapshot_locate's device tables).  words: [0] end of
+// entry n-1, [1] listing inconsistency, [2] tombstones, [3] entries on the chain.
+struct SnapTables {
+    uint32_t *start = nullptr;   // per segment: first entry position (candidate index) or BAD
+    uint64_t *basev = nullptr;   // per segment: index of its first entry
+    uint32_t *segq = nullptr;    // per 256-entry block b: segment of entry min(256 b, n) - 1
+    unsigned long long *words = nullptr;
+    uint64_t nseg = 0;
+};
+hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bool with_segq, Scratch &s,
+                           hipStream_t st, SnapTables *t);
+// words[2] += Σ part[0 .. groups)
+hipError_t snapshot_sum_tombstones(const uint32_t *part, uint64_t groups, unsigned long long *words, hipStream_t st);
+
+// The fused reload pass (snap_lift.hpp): block b of 256 entries stages its segments, lists its
+// entries, lifts them straight from the staged file bytes (dated, projection or both), writes
+// the fingerprints and block sums, the keys into one or two stores' key arrays, and flags an
+// out-of-order key.
+struct SnapLift {
+    const uint8_t *blob = nullptr;
+    SnapFmt f;
+    uint64_t n = 0, nseg = 0;
+    const uint32_t *start = nullptr, *segq = nullptr;
+    const uint64_t *basev = nullptr;
+    uint32_t nsmax = 0;                        // most segments one block's entries (+ predecessor) span
+    uint8_t *keys = nullptr, *keys2 = nullptr;  // key rows of the two stores (keys2 may be null)
+    uint8_t *fps = nullptr, *bsums = nullptr;   // the dated (or the only) store
+    uint8_t *fps2 = nullptr, *bsums2 = nullptr; // the projection store of a dual reload
+    unsigned long long *words = nullptr;
+    uint32_t *tomb_part = nullptr;              // per block
+    uint32_t *unsorted = nullptr;               // set to 1 if a key is not above its predecessor
+};
+// mode: 0 dated, 1 projection, 2 both.  0 bytes: the fused pass does not apply to the format
+uint64_t snap_lift_lds_bytes(const SnapFmt &f, uint32_t *nsmax);
+// the schema-specialised launch (rsos_hip_abi.hip dispatches over schemas.def)
+hipError_t launch_snap_lift_schema(int kk, int kl, int vk, int vl, int mode, const SnapLift &a, uint64_t lds,
+                                   hipStream_t st, bool *supported);
+
 // Locate and decode entries [0, n) of the device blob into SoA columns (keys key_len B,
 // phys u64, logical u32, node u64, tags u8 = variant, values val_len B; tombstone values are
 // zero-filled).  Synchronises `st`.  *corrupt = 1 if fewer than n entries parse.

@@ -563,7 +563,7 @@ struct rh_store {
     uint64_t nb = 0;
     int cb = 0;
     DevBuf<uint8_t> bkeys[2], bfps[2], bsums, ssums;
-    DevBuf<uint64_t> bsmp, bsmp2;  // leading digits of every 256th (16th) key: sampled search
+    DevBuf<uint64_t> bsmp, bsmp2;  // leading digits of every 256th (8th) key: sampled search
     DevBuf<uint32_t> btab;         // the base run's search table over bsmp2 (k_search_table)
     DevBuf<uint32_t> dtab;         // the delta run's, built before each batch's delta search
     DevBuf<uint64_t> dtabp;
@@ -950,11 +950,11 @@ struct rh_store {
     }
     // the second part, once the m rows are in place (enqueued behind them on this stream):
     // super sums, samples and the root; *unsorted (device) -> the host copy load_finish checks
-    int load_sums(size_t m, const uint32_t *unsorted) {
+    int load_sums(size_t m, const uint32_t *unsorted, bool have_samples = false) {
         nb = m;
         load_flag.assign(10, 0);  // [0] unsorted flag, [2..9] the base total (8-byte aligned)
         uint64_t *root_pin = reinterpret_cast<uint64_t *>(load_flag.data() + 2);
-        int rc = resum_base(true, root_pin);
+        int rc = resum_base(true, root_pin, have_samples);
         if (rc) return rc;
         if (m) RH_HIP(hipMemcpyAsync(load_flag.data(), unsorted, 4, hipMemcpyDeviceToHost, stream));
         return RH_OK;
@@ -964,26 +964,33 @@ struct rh_store {
     // the rows go to the spare base buffers, and the store changes only at load_commit -- a
     // corrupt file leaves it as it was, as Replica::load_snapshot does (src/snapshot.rs:76-98)
     DevBuf<uint8_t> sbsums;
+    DevBuf<uint64_t> sbsmp, sbsmp2;
     int load_target(size_t m) {
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         const int nxt = 1 - cb;
         int rc;
         if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) ||
-            (rc = sbsums.ensure(rh_num_blocks(m) * 32 + 32)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
+            (rc = sbsums.ensure(rh_num_blocks(m) * 32 + 32)) || (rc = sbsmp.ensure(rh_num_blocks(m) + 1)) ||
+            (rc = sbsmp2.ensure(rh::sample2_entries(m))) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
         return RH_OK;
     }
+    // the target's rows, block sums and search samples become the base run
     int load_commit(size_t m, const uint32_t *unsorted) {
         cb = 1 - cb;
         std::swap(bsums.p, sbsums.p);
         std::swap(bsums.cap, sbsums.cap);
+        std::swap(bsmp.p, sbsmp.p);
+        std::swap(bsmp.cap, sbsmp.cap);
+        std::swap(bsmp2.p, sbsmp2.p);
+        std::swap(bsmp2.cap, sbsmp2.cap);
         version++;
         base_epoch++;
         nd = 0;
         heap_len = 0;
         dtotal = 0;
         memset(root_d, 0, sizeof root_d);
-        return load_sums(m, unsorted);
+        return load_sums(m, unsorted, true);
     }
     // page-locked host tier capacity for `rows` rows ahead of the refresh that fills it: pinning
     // fresh pages is most of a first refresh (11-13 ms at 10^6 rows against ~1 ms of copying)
@@ -2119,11 +2126,10 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     for (rh_store *x : {dated, proj})
         if (x && (rc = x->load_target(n))) return rc;
     rh::SnapTables t;
-    RH_HIP(rh::snapshot_locate(f, dev, n, true, a->scratch, a->stream, &t));
+    RH_HIP(rh::snapshot_locate(f, dev, n, true, a->scratch, a->stream, &t, a->flag.p));
     const uint64_t nblk = (n + 255) / 256;
     uint32_t *part = static_cast<uint32_t *>(a->scratch.get(98, nblk * 4));
     if (a->scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-    RH_HIP(hipMemsetAsync(a->flag.p, 0, 4, a->stream));
     rh::SnapLift L;
     L.blob = dev;
     L.f = f;
@@ -2136,10 +2142,14 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     L.keys = a->bkeys[1 - a->cb].p;
     L.fps = a->bfps[1 - a->cb].p;
     L.bsums = a->sbsums.p;
+    L.smp = a->sbsmp.p;
+    L.smp2 = a->sbsmp2.p;
     if (mode == 2) {
         L.keys2 = proj->bkeys[1 - proj->cb].p;
         L.fps2 = proj->bfps[1 - proj->cb].p;
         L.bsums2 = proj->sbsums.p;
+        L.smp_2 = proj->sbsmp.p;
+        L.smp2_2 = proj->sbsmp2.p;
     }
     L.words = t.words;
     L.tomb_part = part;

@@ -63,11 +63,14 @@ __device__ __forceinline__ void stage(const uint8_t *blob, uint64_t len, uint64_
 // cover p + lp or the end of the file.
 __device__ __forceinline__ uint32_t entry_len(const Img &m, const SnapFmt &f, uint64_t p) {
     if (p + f.lt > f.len) return 0;
-    if (f.key_pre && m.ld64(p) != f.key_len) return 0;
+    // the variant and both Vec lengths in one LDS round trip (the value's length word is read
+    // even for a tombstone: it lies inside the staged run, and only a present entry checks it)
     const uint32_t v = m.ld32(p + f.key_pre + f.key_len + 20);
+    const uint64_t kl = f.key_pre ? m.ld64(p) : f.key_len;
+    const uint64_t vl = f.val_pre ? m.ld64(p + f.lt) : f.val_len;
+    if (kl != f.key_len) return 0;
     if (v == 1) return f.lt;
-    if (v != 0 || p + f.lp > f.len) return 0;
-    if (f.val_pre && m.ld64(p + f.lt) != f.val_len) return 0;
+    if (v != 0 || p + f.lp > f.len || vl != f.val_len) return 0;
     return f.lp;
 }
 

@@ -14,7 +14,7 @@
 // entries from the true start listing their LDS offsets (entry 256 b - 1 included, for the
 // order check), then every lane hashes its own entry reading key, stamp, variant and value
 // from LDS.  HBM traffic per entry: its file bytes once, 32 B per fingerprint written and the
-// key written once per store.
+// key written once per store (with the stores' search samples: 1 u64 per 8 keys).
 #pragma once
 #include "lift_kernels.hpp"
 #include "snap_device.hpp"
@@ -108,6 +108,20 @@ __global__ __launch_bounds__(256) void k_snap_lift(SnapLift a) {
         store_fp(a.fps + e0 * 32, t, h);
         if constexpr (MODE == 2) store_fp(a.fps2 + e0 * 32, t, h2);
         tomb_c = tomb;
+        // the stores' search samples (k_sample's): the leading u64 digit in key order
+        if (t % SMP2_STRIDE == 0) {
+            uint64_t d = 0;
+            if constexpr (KK == KEY_BYTES) d = ((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
+            else if constexpr (KK == KEY_U64) d = ((uint64_t)w[1] << 32) | w[0];
+            else if constexpr (KK == KEY_U32) d = w[0];
+            const uint64_t e = e0 + t;
+            a.smp2[e / SMP2_STRIDE] = d;
+            if (a.smp2_2) a.smp2_2[e / SMP2_STRIDE] = d;
+            if (t == 0) {
+                a.smp[b] = d;
+                if (a.smp_2) a.smp_2[b] = d;
+            }
+        }
         // strictly increasing keys (k_check_sorted's rule): compare with entry e - 1, in the
         // key's Ord -- bytes: memcmp (big-endian words); u32 / u64: numeric
         if (e0 + t > 0) {

@@ -13,12 +13,15 @@
 //      (16-byte coalesced loads) and one lane per (segment, candidate) walks its segment in LDS,
 //      recording where the chain leaves the segment and how many entries it crossed (or that
 //      no valid entry starts there: bad variant, wrong Vec length, past the end of the file);
-//   2. the per-segment transfer functions are composed up a tree (fan-out 32) and the true
-//      first-entry position and entry index of every segment are pushed back down from the
-//      file's first entry;
+//   2. the per-segment transfer functions are composed up a tree (fan-out 32; a node stages
+//      its children's tables in LDS and chains through them there) and the true first-entry
+//      position and entry index of every segment are pushed back down from the file's first
+//      entry;
 //   3. a workgroup stages a run of segments in LDS again, one lane per segment re-walks it from
 //      the true position listing entry offsets in LDS, and the workgroup writes its contiguous
 //      range of entries into every column with coalesced stores (the AoS -> SoA transpose).
+//      A reload into stores takes the fused pass instead (snap_lift.hpp): the same listing,
+//      then the lifts and the key rows straight from the staged bytes, no columns.
 // HBM traffic: the body is read twice (steps 1 and 3) and the columns written once; step 2
 // touches P words per segment.
 #include <algorithm>
@@ -33,6 +36,7 @@ namespace {
 
 constexpr uint32_t SNAP_BAD = snap::BAD;
 constexpr uint32_t SNAP_FAN = 32;
+constexpr uint32_t SNAP_TREE_LDS = 24576;  // a tree node's staged child tables
 constexpr uint32_t SNAP_LDS = 32768;  // staged bytes per workgroup
 using snap::Img;
 using snap::entry_len;
@@ -74,57 +78,98 @@ __global__ __launch_bounds__(256) void k_snap_walk(const uint8_t *blob, SnapFmt 
     cnt[s * f.phases + ph] = c;
 }
 
-// step 2 (up): compose the transfer functions of SNAP_FAN consecutive groups
+// step 2 (up): compose the transfer functions of F consecutive groups; one 64-lane workgroup per
+// parent stages its children's tables in LDS (coalesced), then lane x chains candidate x
+// through them -- F dependent LDS reads instead of F dependent global loads
 template <class CIn>
-__global__ void k_snap_up(const uint32_t *ex, const CIn *cnt, uint64_t nin, uint32_t P, uint64_t nout,
-                          uint32_t *ex_out, uint64_t *cnt_out) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nout * P) return;
-    const uint64_t g = t / P;
-    uint32_t x = (uint32_t)(t - g * P);
-    uint64_t c = 0;
-    for (uint32_t j = 0; j < SNAP_FAN; j++) {
-        const uint64_t s = g * SNAP_FAN + j;
-        if (s >= nin) break;
-        const uint64_t i = s * P + x;
-        c += cnt[i];
-        x = ex[i];
-        if (x == SNAP_BAD) break;
+__global__ __launch_bounds__(64) void k_snap_up(const uint32_t *ex, const CIn *cnt, uint64_t nin, uint32_t P,
+                                                uint32_t F, uint32_t *ex_out, uint64_t *cnt_out) {
+    extern __shared__ uint64_t tab[];  // F * P counts, then F * P exits
+    uint64_t *sc = tab;
+    uint32_t *sx = reinterpret_cast<uint32_t *>(tab + (uint64_t)F * P);
+    const uint64_t g = blockIdx.x, c0 = g * F;
+    const uint32_t nc = (uint32_t)std::min<uint64_t>(F, nin - c0);
+    for (uint32_t j = threadIdx.x; j < nc * P; j += blockDim.x) {
+        sx[j] = ex[c0 * P + j];
+        sc[j] = cnt[c0 * P + j];
     }
-    ex_out[t] = x;
-    cnt_out[t] = c;
+    __syncthreads();
+    for (uint32_t x0 = threadIdx.x; x0 < P; x0 += blockDim.x) {
+        uint32_t x = x0;
+        uint64_t c = 0;
+        for (uint32_t j = 0; j < nc; j++) {
+            const uint32_t i = j * P + x;
+            c += sc[i];
+            x = sx[i];
+            if (x == SNAP_BAD) break;
+        }
+        ex_out[g * P + x0] = x;
+        cnt_out[g * P + x0] = c;
+    }
 }
 
-// step 2 (down): true entry position and entry index at the start of every child group.  At
+// step 2 (down): true entry position and entry index at the start of every child of a parent
+// (one workgroup per parent, its children's tables in LDS, one lane follows the chain).  At
 // level 0 with segq given (the fused reload): segq[b] = the segment holding entry
 // min(256 b, n) - 1 for b in [1, ceil(n / 256)] -- the first and last segments a 256-entry
-// block of the lift reads (segq[0] = 0 is set by the caller)
+// block of the lift reads (segq[0] = 0 is set by k_snap_init)
 template <class CIn>
-__global__ void k_snap_down(const uint32_t *ex, const CIn *cnt, uint64_t nl, uint32_t P, const uint32_t *start_up,
-                            const uint64_t *base_up, uint64_t nup, uint32_t *start, uint64_t *basev,
-                            uint32_t *segq = nullptr, uint64_t n = 0) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= nup) return;
-    uint32_t x = start_up[g];
-    uint64_t c = base_up[g];
-    const uint64_t nblk = (n + 255) / 256;
-    for (uint32_t j = 0; j < SNAP_FAN; j++) {
-        const uint64_t s = g * SNAP_FAN + j;
-        if (s >= nl) break;
-        start[s] = x;
-        basev[s] = c;
-        if (x != SNAP_BAD) {
-            const uint64_t i = s * P + x;
-            const uint64_t c1 = c + cnt[i];  // entries [c, c1) start in segment s
-            if (segq && c < n) {
-                for (uint64_t b = std::max<uint64_t>(1, (c + 256) / 256); b < nblk && 256 * b - 1 < c1; b++)
-                    segq[b] = (uint32_t)s;
-                if (n - 1 < c1) segq[nblk] = (uint32_t)s;
+__global__ __launch_bounds__(64) void k_snap_down(const uint32_t *ex, const CIn *cnt, uint64_t nl, uint32_t P,
+                                                  uint32_t F, const uint32_t *start_up, const uint64_t *base_up,
+                                                  uint32_t *start, uint64_t *basev, uint32_t *segq, uint64_t n) {
+    extern __shared__ uint64_t tab[];  // F * P counts, F * P exits, then F chain positions
+    uint64_t *sc = tab;
+    uint64_t *qc = tab + (uint64_t)F * P;      // entry index at each child's start (F + 1)
+    uint32_t *sx = reinterpret_cast<uint32_t *>(qc + F + 1);
+    uint32_t *qx = sx + (uint64_t)F * P;        // position at each child's start
+    const uint64_t g = blockIdx.x, c0 = g * F;
+    const uint32_t nc = (uint32_t)std::min<uint64_t>(F, nl - c0);
+    for (uint32_t j = threadIdx.x; j < nc * P; j += blockDim.x) {
+        sx[j] = ex[c0 * P + j];
+        sc[j] = cnt[c0 * P + j];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x = start_up[g];
+        uint64_t c = base_up[g];
+        for (uint32_t j = 0; j < nc; j++) {
+            qx[j] = x;
+            qc[j] = c;
+            if (x != SNAP_BAD) {
+                const uint32_t i = j * P + x;
+                c += sc[i];
+                x = sx[i];
             }
-            c = c1;
-            x = ex[i];
+        }
+        qc[nc] = c;
+    }
+    __syncthreads();
+    const uint64_t nblk = (n + 255) / 256;
+    for (uint32_t j = threadIdx.x; j < nc; j += blockDim.x) {
+        const uint64_t s = c0 + j;
+        start[s] = qx[j];
+        basev[s] = qc[j];
+        const uint64_t c = qc[j], c1 = qc[j + 1];  // entries [c, c1) start in segment s
+        if (segq && qx[j] != SNAP_BAD && c < n) {
+            for (uint64_t b = std::max<uint64_t>(1, (c + 256) / 256); b < nblk && 256 * b - 1 < c1; b++)
+                segq[b] = (uint32_t)s;
+            if (n - 1 < c1) segq[nblk] = (uint32_t)s;
         }
     }
+}
+
+// the chain enters the top group at candidate 0 (the body's first entry) with 0 entries before
+// it; words zeroed, words[3] = the entries on the chain (the top group's count for candidate 0);
+// the caller's flag word (the fused pass's out-of-order flag) zeroed
+__global__ void k_snap_init(uint32_t *start_top, uint64_t *base_top, const void *cnt_top, int top_u64,
+                            unsigned long long *words, uint32_t *segq, uint32_t *flag) {
+    if (threadIdx.x != 0) return;
+    *start_top = 0;
+    *base_top = 0;
+    for (int k = 0; k < 8; k++) words[k] = 0;
+    words[3] = top_u64 ? *static_cast<const uint64_t *>(cnt_top) : *static_cast<const uint32_t *>(cnt_top);
+    if (segq) segq[0] = 0;
+    if (flag) *flag = 0;
 }
 
 // step 3: G segments per workgroup -> their entries [r0, r1) into the columns.
@@ -239,24 +284,24 @@ __global__ __launch_bounds__(1024) void k_snap_sum(const uint32_t *part, uint64_
     }
 }
 
-inline dim3 grid_for(uint64_t threads) { return dim3((uint32_t)((threads + 255) / 256)); }
-
 }  // namespace
 
 // steps 1 and 2: the true first-entry position and entry index of every segment (and with
 // segq, every 256-entry block's first and last segment).  words[3] = entries on the chain from
 // the file's first entry; words[0..2] zeroed for the pass that follows.  Nothing is waited for.
 hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bool with_segq, Scratch &s,
-                           hipStream_t st, SnapTables *t) {
+                           hipStream_t st, SnapTables *t, uint32_t *flag) {
     hipError_t e;
     const uint32_t P = f.phases;
     if (P > 256 || f.seg + f.lp + 32 > SNAP_LDS) return hipErrorInvalidValue;
     const uint64_t body = f.len > f.base ? f.len - f.base : 0;
     const uint64_t nseg = std::max<uint64_t>(1, (body + f.seg - 1) / f.seg);
+    // tree fan-out: a node stages its children's tables (F * P * 12 B) in LDS
+    const uint32_t F = std::max<uint32_t>(8, std::min<uint32_t>(SNAP_FAN, SNAP_TREE_LDS / (12 * P)));
     std::vector<uint64_t> sizes{nseg};
-    while (sizes.back() > 1) sizes.push_back((sizes.back() + SNAP_FAN - 1) / SNAP_FAN);
+    while (sizes.back() > 1) sizes.push_back((sizes.back() + F - 1) / F);
     const size_t L = sizes.size();
-    if (L > 7) return hipErrorInvalidValue;
+    if (L > 12) return hipErrorInvalidValue;
     std::vector<uint32_t *> ex(L), start(L);
     std::vector<void *> cnt(L);  // level 0: u32 per segment, above: u64
     std::vector<uint64_t *> basev(L);
@@ -284,33 +329,30 @@ hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bo
                            ex[0], static_cast<uint32_t *>(cnt[0]));
     }
     // 2. compose up to one group, then push the true positions down
+    const size_t up_lds = (size_t)F * P * 12, down_lds = up_lds + 8ull * (F + 1) + 4ull * F;
     for (size_t l = 0; l + 1 < L; l++) {
         if (l == 0)
-            hipLaunchKernelGGL(k_snap_up<uint32_t>, grid_for(sizes[1] * P), dim3(256), 0, st, ex[0],
-                               static_cast<const uint32_t *>(cnt[0]), sizes[0], P, sizes[1], ex[1],
+            hipLaunchKernelGGL(k_snap_up<uint32_t>, dim3((uint32_t)sizes[1]), dim3(64), up_lds, st, ex[0],
+                               static_cast<const uint32_t *>(cnt[0]), sizes[0], P, F, ex[1],
                                static_cast<uint64_t *>(cnt[1]));
         else
-            hipLaunchKernelGGL(k_snap_up<uint64_t>, grid_for(sizes[l + 1] * P), dim3(256), 0, st, ex[l],
-                               static_cast<const uint64_t *>(cnt[l]), sizes[l], P, sizes[l + 1], ex[l + 1],
+            hipLaunchKernelGGL(k_snap_up<uint64_t>, dim3((uint32_t)sizes[l + 1]), dim3(64), up_lds, st, ex[l],
+                               static_cast<const uint64_t *>(cnt[l]), sizes[l], P, F, ex[l + 1],
                                static_cast<uint64_t *>(cnt[l + 1]));
     }
-    // the chain enters the top group at candidate 0 (the body's first entry) with 0 entries before it
-    if ((e = hipMemsetAsync(start[L - 1], 0, 4, st)) || (e = hipMemsetAsync(basev[L - 1], 0, 8, st)) ||
-        (e = hipMemsetAsync(words, 0, 64, st)))
-        return e;
-    if (segq && (e = hipMemsetAsync(segq, 0, (nblk + 1) * 4, st))) return e;
-    // entries on the chain from the file's first entry (checked against n by the caller: a short
-    // chain only leaves rows unwritten, every access stays inside the blob and the outputs)
-    if ((e = hipMemcpyAsync(words + 3, cnt[L - 1], L == 1 ? 4 : 8, hipMemcpyDeviceToDevice, st))) return e;
+    hipLaunchKernelGGL(k_snap_init, dim3(1), dim3(64), 0, st, start[L - 1], basev[L - 1], cnt[L - 1], L > 1 ? 1 : 0,
+                       words, segq, flag);
+    // entries on the chain from the file's first entry are checked against n by the caller: a
+    // short chain only leaves rows unwritten, every access stays inside the blob and the outputs
     for (size_t l = L - 1; l-- > 0;) {
         if (l == 0)
-            hipLaunchKernelGGL(k_snap_down<uint32_t>, grid_for(sizes[1]), dim3(256), 0, st, ex[0],
-                               static_cast<const uint32_t *>(cnt[0]), sizes[0], P, start[1], basev[1], sizes[1],
-                               start[0], basev[0], segq, n);
+            hipLaunchKernelGGL(k_snap_down<uint32_t>, dim3((uint32_t)sizes[1]), dim3(64), down_lds, st, ex[0],
+                               static_cast<const uint32_t *>(cnt[0]), sizes[0], P, F, start[1], basev[1], start[0],
+                               basev[0], segq, n);
         else
-            hipLaunchKernelGGL(k_snap_down<uint64_t>, grid_for(sizes[l + 1]), dim3(256), 0, st, ex[l],
-                               static_cast<const uint64_t *>(cnt[l]), sizes[l], P, start[l + 1], basev[l + 1],
-                               sizes[l + 1], start[l], basev[l], nullptr, 0);
+            hipLaunchKernelGGL(k_snap_down<uint64_t>, dim3((uint32_t)sizes[l + 1]), dim3(64), down_lds, st, ex[l],
+                               static_cast<const uint64_t *>(cnt[l]), sizes[l], P, F, start[l + 1], basev[l + 1],
+                               start[l], basev[l], nullptr, 0);
     }
     if ((e = hipGetLastError())) return e;
     t->start = start[0];

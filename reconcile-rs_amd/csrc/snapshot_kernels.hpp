@@ -37,14 +37,14 @@ struct SnapTables {
     uint64_t nseg = 0;
 };
 hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bool with_segq, Scratch &s,
-                           hipStream_t st, SnapTables *t);
+                           hipStream_t st, SnapTables *t, uint32_t *flag = nullptr);  // *flag zeroed on st
 // words[2] += Σ part[0 .. groups)
 hipError_t snapshot_sum_tombstones(const uint32_t *part, uint64_t groups, unsigned long long *words, hipStream_t st);
 
 // The fused reload pass (snap_lift.hpp): block b of 256 entries stages its segments, lists its
 // entries, lifts them straight from the staged file bytes (dated, projection or both), writes
-// the fingerprints and block sums, the keys into one or two stores' key arrays, and flags an
-// out-of-order key.
+// the fingerprints and block sums, the keys and search samples into one or two stores, and flags
+// an out-of-order key.
 struct SnapLift {
     const uint8_t *blob = nullptr;
     SnapFmt f;
@@ -58,6 +58,8 @@ struct SnapLift {
     unsigned long long *words = nullptr;
     uint32_t *tomb_part = nullptr;              // per block
     uint32_t *unsorted = nullptr;               // set to 1 if a key is not above its predecessor
+    uint64_t *smp = nullptr, *smp2 = nullptr;   // the stores' search samples (SMP_STRIDE, SMP2_STRIDE)
+    uint64_t *smp_2 = nullptr, *smp2_2 = nullptr;
 };
 // mode: 0 dated, 1 projection, 2 both.  0 bytes: the fused pass does not apply to the format
 uint64_t snap_lift_lds_bytes(const SnapFmt &f, uint32_t *nsmax);

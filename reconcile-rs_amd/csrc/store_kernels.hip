@@ -514,7 +514,6 @@ __global__ void k_search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint
 // A second level (every SMP2_STRIDE-th key; 8 B per 8 keys) narrows the window to one line of
 // 16-byte keys (the key lines are what a batch of searches pays for: 2.4 -> ~1.9 distinct lines
 // per query against a 100 M-row base).
-constexpr uint64_t SMP_STRIDE = 256, SMP2_STRIDE = 8;  // 8 x 16-byte keys = one 128-byte line
 
 uint64_t sample2_entries(uint64_t n) { return (n + SMP2_STRIDE - 1) / SMP2_STRIDE + 2; }
 

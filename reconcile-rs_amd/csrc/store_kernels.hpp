@@ -71,6 +71,8 @@ struct alignas(8) DeltaRec {
 };
 static_assert(sizeof(DeltaRec) == 40, "DeltaRec layout (k_merge_run reads flags as word 9)");
 
+// a run's search samples: the leading key digit of every SMP_STRIDE-th and SMP2_STRIDE-th row
+constexpr uint64_t SMP_STRIDE = 256, SMP2_STRIDE = 8;  // 8 x 16-byte keys = one 128-byte line
 // entries of a run's second-level (stride SMP2_STRIDE) sample array for n rows, with slack
 uint64_t sample2_entries(uint64_t n);
 // A run's search table (k_search_table): tab has 2^bits + 1 entries, par = (min digit, shift).

@@ -16,7 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
   python bench.py --config snapshot --steps 10 --warmup 2 --cpu-baseline 0 --spinup-ms 0 > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 find $O/trace -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
 f=$(find $O/trace -name "*kernel_trace.csv" | head -1)
-python scripts/snap_timeline.py "$f" > $O/timeline.txt 2>&1
+python scripts/snap_timeline.py "$f" 10 > $O/timeline.txt 2>&1
 rm -rf $O/trace
 head -14 $O/kernel_stats.csv | cut -d, -f1-5 | cut -c1-160
 cat $O/timeline.txt

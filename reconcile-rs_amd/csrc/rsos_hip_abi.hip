@@ -963,34 +963,54 @@ struct rh_store {
     // A load whose rows are written before it is known to succeed (the fused snapshot reload):
     // the rows go to the spare base buffers, and the store changes only at load_commit -- a
     // corrupt file leaves it as it was, as Replica::load_snapshot does (src/snapshot.rs:76-98)
-    DevBuf<uint8_t> sbsums;
-    DevBuf<uint64_t> sbsmp, sbsmp2;
+    DevBuf<uint8_t> sbsums, sssums;
+    DevBuf<uint64_t> sbsmp, sbsmp2, sbtabp, stot;
+    DevBuf<uint32_t> sbtab;
     int load_target(size_t m) {
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         const int nxt = 1 - cb;
         int rc;
         if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) ||
-            (rc = sbsums.ensure(rh_num_blocks(m) * 32 + 32)) || (rc = sbsmp.ensure(rh_num_blocks(m) + 1)) ||
-            (rc = sbsmp2.ensure(rh::sample2_entries(m))) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
+            (rc = sbsums.ensure(rh_num_blocks(m) * 32 + 32)) || (rc = sssums.ensure(rh_num_superblocks(m) * 32 + 32)) ||
+            (rc = sbsmp.ensure(rh_num_blocks(m) + 1)) || (rc = sbsmp2.ensure(rh::sample2_entries(m))) ||
+            (rc = sbtab.ensure((1ull << rh::search_table_bits(m)) + 2)) || (rc = sbtabp.ensure(2)) ||
+            (rc = stot.ensure(4)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
         return RH_OK;
     }
-    // the target's rows, block sums and search samples become the base run
-    int load_commit(size_t m, const uint32_t *unsorted) {
+    // behind the target's rows, block sums and samples (on st): its super sums, search table and
+    // total, and the total and *unsorted into the pinned load_flag -- all in the spare buffers
+    int load_stage_sums(size_t m, const uint32_t *unsorted, hipStream_t st) {
+        const size_t nbk = rh_num_blocks(m), ns = rh_num_superblocks(m);
+        load_flag.assign(10, 0);  // [0] unsorted flag, [2..9] the base total (8-byte aligned)
+        RH_HIP(rh::launch_search_table(sbsmp2.p, m, sbtab.p, sbtabp.p, st));
+        RH_HIP(rh::launch_reduce(sbsums.p, nbk, sssums.p, st));
+        RH_HIP(rh::launch_total(sssums.p, ns, stot.p, st));
+        RH_HIP(hipMemcpyAsync(load_flag.data() + 2, stot.p, 32, hipMemcpyDeviceToHost, st));
+        RH_HIP(hipMemcpyAsync(load_flag.data(), unsorted, 4, hipMemcpyDeviceToHost, st));
+        return RH_OK;
+    }
+    // the target becomes the base run (host state only: load_finish then takes the root and
+    // checks the order flag)
+    void load_commit(size_t m) {
+        auto swap_buf = [](auto &x, auto &y) {
+            std::swap(x.p, y.p);
+            std::swap(x.cap, y.cap);
+        };
         cb = 1 - cb;
-        std::swap(bsums.p, sbsums.p);
-        std::swap(bsums.cap, sbsums.cap);
-        std::swap(bsmp.p, sbsmp.p);
-        std::swap(bsmp.cap, sbsmp.cap);
-        std::swap(bsmp2.p, sbsmp2.p);
-        std::swap(bsmp2.cap, sbsmp2.cap);
+        swap_buf(bsums, sbsums);
+        swap_buf(ssums, sssums);
+        swap_buf(bsmp, sbsmp);
+        swap_buf(bsmp2, sbsmp2);
+        swap_buf(btab, sbtab);
+        swap_buf(btabp, sbtabp);
         version++;
         base_epoch++;
         nd = 0;
         heap_len = 0;
         dtotal = 0;
         memset(root_d, 0, sizeof root_d);
-        return load_sums(m, unsorted, true);
+        nb = m;
     }
     // page-locked host tier capacity for `rows` rows ahead of the refresh that fills it: pinning
     // fresh pages is most of a first refresh (11-13 ms at 10^6 rows against ~1 ms of copying)
@@ -2166,6 +2186,11 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
         return fail(RH_ERR_OOM, "pinned result buffer");
     }
     RH_HIP(hipMemcpyAsync(a->snap_words.data(), t.words, 32, hipMemcpyDeviceToHost, a->stream));
+    // both stores' super sums, search tables and totals into their spare buffers, on their own
+    // streams, before the one wait
+    if (mode == 2 && (rc = proj->after(a->stream))) return rc;
+    for (rh_store *x : {dated, proj})
+        if (x && (rc = x->load_stage_sums(n, a->flag.p, x->stream))) return rc;
     if ((rc = a->sync())) return rc;
     const uint64_t *w = a->snap_words.data();
     if (w[3] < n || w[1])
@@ -2182,7 +2207,7 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     for (rh_store *x : {dated, proj}) {
         if (!x) continue;
         if (x == proj && fail_point("snapshot.load_begin")) rc = fail(RH_ERR_OOM, "injected failure (load_begin)");
-        else rc = x->load_commit(n, a->flag.p);
+        else x->load_commit(n);
         if (rc) break;
     }
     for (rh_store *x : {dated, proj}) {

@@ -363,14 +363,16 @@ hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bo
     return hipSuccess;
 }
 
-// LDS of one fused-reload workgroup: the staged run of segments holding 257 consecutive entries.
-// A segment holds at least floor(seg / lp) entry starts, so 257 entries span at most
-// 257 / that + 2 segments.  0 when that exceeds 64 KiB (or 256 walker lanes).
+// LDS of one fused-reload workgroup: the candidate words of the run of segments holding 257
+// consecutive entries (or the block-sum tile, which reuses it).  A segment holds at least
+// floor(seg / lp) entry starts, so 257 entries span at most 257 / that + 2 segments.  0 when
+// that exceeds 64 KiB (or 256 walker lanes).
 uint64_t snap_lift_lds_bytes(const SnapFmt &f, uint32_t *nsmax) {
     const uint64_t per = f.lp ? f.seg / f.lp : 0;
     if (per == 0) return 0;
     const uint64_t ns = 257 / per + 2;
-    const uint64_t bytes = std::max<uint64_t>((ns * f.seg + f.lp + 16 + 15) / 16 * 16, sizeof(SumTile));
+    const uint64_t words = (ns * f.seg + f.lp + 16 + 3) / 4 / snap_lift_stride(f) + 8;
+    const uint64_t bytes = std::max<uint64_t>((4 * words + 15) / 16 * 16, sizeof(SumTile));
     if (ns > 256 || bytes > 65536) return 0;
     *nsmax = (uint32_t)ns;
     return bytes;

@@ -61,7 +61,11 @@ struct SnapLift {
     uint64_t *smp = nullptr, *smp2 = nullptr;   // the stores' search samples (SMP_STRIDE, SMP2_STRIDE)
     uint64_t *smp_2 = nullptr, *smp2_2 = nullptr;
 };
-// mode: 0 dated, 1 projection, 2 both.  0 bytes: the fused pass does not apply to the format
+// the fused pass's candidate-word stride: entries start every g bytes, so only every (g / 4)-th
+// word can hold a State variant; a power of two dividing g / 4, at most 2
+inline int snap_lift_stride(const SnapFmt &f) { return (f.g / 4) % 2 == 0 ? 2 : 1; }
+// LDS of one fused-pass workgroup (mode: 0 dated, 1 projection, 2 both); 0: the pass does not
+// apply to the format
 uint64_t snap_lift_lds_bytes(const SnapFmt &f, uint32_t *nsmax);
 // the schema-specialised launch (rsos_hip_abi.hip dispatches over schemas.def)
 hipError_t launch_snap_lift_schema(int kk, int kl, int vk, int vl, int mode, const SnapLift &a, uint64_t lds,

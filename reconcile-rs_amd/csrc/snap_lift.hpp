@@ -45,6 +45,7 @@ __device__ __forceinline__ void stw(uint8_t *p, const uint32_t *v) {
 // R = a power of two dividing g / 4, at most 2); entries are then 4R-byte aligned in the file.
 template <int KK, int KL, int VK, int VL, int MODE, int R>
 __global__ __launch_bounds__(256) void k_snap_lift(SnapLift a) {
+    static_assert(R == 1 || R == 2, "candidate stride");
     constexpr int A = 4 * R;
     using LD = LayoutAligned<Layout<KK, KL, VK, VL, REC_DATED>, A>;
     using LP = LayoutAligned<Layout<KK, KL, VK, VL, REC_PROJECTION>, A>;
@@ -66,26 +67,36 @@ __global__ __launch_bounds__(256) void k_snap_lift(SnapLift a) {
     const uint64_t end = std::min<uint64_t>(snap::seg_start(f, s_hi + 1) + f.lp, f.len);
     const uint32_t o_var = f.key_pre + f.key_len + 20;
     // candidate words: file word w holds a variant only if w = (f.base + o_var) / 4 (mod R);
-    // image word k <-> file word wb + k R
+    // image word k <-> file word wb + k R.  With R = 2 they are words vb and vb + 2 of every
+    // 16-byte chunk (vb = 0 or 1, the same for the whole range), so chunk c lands in image words
+    // 2c and 2c + 1.  32-bit offsets from the range start.
     const uint64_t w0 = base >> 2;
     const uint64_t wb = w0 + ((((f.base + o_var) >> 2) - w0) & (R - 1));
-    // every lane's loads in flight before its first LDS store (snap::stage's batching)
-    for (uint64_t qs = base + 16ull * t; qs < end; qs += 16ull * blockDim.x * snap::STAGE_U) {
-        uint4 v[snap::STAGE_U];
+    const uint32_t vb = (uint32_t)(wb - w0);
+    {
+        const uint32_t span = (uint32_t)(end - base);
+        const uint32_t avail = (uint32_t)std::min<uint64_t>(f.len - base, 1u << 31);  // file bytes from base
+        const uint8_t *src = a.blob + base;
+        // every lane's loads in flight before its first LDS store (snap::stage's batching)
+        for (uint32_t r0 = 16 * t; r0 < span; r0 += 16 * 256 * snap::STAGE_U) {
+            uint4 v[snap::STAGE_U];
 #pragma unroll
-        for (int u = 0; u < snap::STAGE_U; u++) {
-            const uint64_t q = qs + 16ull * blockDim.x * u;
-            if (q < end) v[u] = snap::load16(a.blob, f.len, q);
-        }
+            for (int u = 0; u < snap::STAGE_U; u++) {
+                const uint32_t rel = r0 + 4096 * u;
+                if (rel < span)
+                    v[u] = rel + 16 <= avail ? *reinterpret_cast<const uint4 *>(src + rel)
+                                             : snap::load16(a.blob, f.len, base + rel);
+            }
 #pragma unroll
-        for (int u = 0; u < snap::STAGE_U; u++) {
-            const uint64_t q = qs + 16ull * blockDim.x * u;
-            if (q >= end) continue;
-            const uint32_t vw[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint64_t w = (q >> 2) + j;
-                if (((w - wb) & (R - 1)) == 0 && w >= wb) img[(w - wb) / R] = vw[j];
+            for (int u = 0; u < snap::STAGE_U; u++) {
+                const uint32_t rel = r0 + 4096 * u;
+                if (rel >= span) continue;
+                if constexpr (R == 1) {
+                    *reinterpret_cast<uint4 *>(img + (rel >> 2)) = v[u];
+                } else {
+                    *reinterpret_cast<uint2 *>(img + (rel >> 3)) =
+                        vb ? make_uint2(v[u].y, v[u].w) : make_uint2(v[u].x, v[u].z);
+                }
             }
         }
     }
@@ -104,7 +115,6 @@ __global__ __launch_bounds__(256) void k_snap_lift(SnapLift a) {
         if (x != snap::BAD) {
             // 32-bit offsets from the range start
             const uint32_t send = (uint32_t)(snap::seg_start(f, s + 1) - base);
-            const uint32_t vb = (uint32_t)(wb - w0);  // image word 0, in words from the range start
             uint32_t p = (uint32_t)(snap::seg_start(f, s) + (uint64_t)x * f.g - base);
             uint32_t k = (uint32_t)(i - q0);  // list index (wraps below q0: skipped)
             const uint32_t kend = (uint32_t)(e1 - q0);

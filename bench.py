@@ -739,10 +739,11 @@ def encoded(args, world, rank, dev, dist):
 
 def reload(args, world, rank, dev, dist):
     """Snapshot reload: one step = rh_store_load_snapshot of a device-resident RCNL file into the
-    dated and the projection store (entry walk + decode + two lifts + sort check + sums), i.e.
+    dated and the projection store (entry walk + transfer-function tree + the fused pass: listing,
+    both lifts, keys, samples, block sums + the stores' super sums), i.e.
     ReplicatedMap::with_persistence's replay (src/replicated_map/persistence.rs:108-143)."""
     from rsos_hip import GpuFingerprintStore, RecordSchema, lift_records, range_aggregates, reduce_blocks
-    from rsos_hip.snapshot import decode_entries_device, load_snapshot
+    from rsos_hip.snapshot import load_snapshot
     from rsos_hip.synth import make_records, make_snapshot
     kname, vname, kind, n_default, desc = CONFIGS["snapshot"]
     n = args.records or n_default
@@ -778,20 +779,24 @@ def reload(args, world, rank, dev, dist):
     ok = root.size == n == info.keys and root.fingerprint.limbs == tuple(int(x) & (2**64 - 1) for x in want[0, :4])
     if not ok:
         raise SystemExit("bench: reloaded root aggregate differs from the lifted source rows")
-    # roofline of the entry decode (walk + offsets + column scatter), timed on torch's stream:
-    # algorithmic bytes = the file read once + the decoded columns written once
-    ev = []
+    # roofline of the dominant kernel, the fused pass k_snap_lift (listing + both lifts + keys +
+    # samples + block sums), timed with HIP events on the loading store's stream
+    # (rh_debug_reload_timing): algorithmic bytes = the file read once + per entry two
+    # fingerprints, the key once per store and the two stores' search samples (1 u64 per 8 keys)
+    import ctypes as C
+    from rsos_hip import _abi as A
+    lib = A.lib()
+    lib.rh_debug_reload_timing(1)
+    stages = []
     for _ in range(3):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        got, _ = decode_entries_device(sd, blob)
-        e1.record()
-        ev.append((e0, e1))
-        del got
-    torch.cuda.synchronize()
-    dec_s = min(a.elapsed_time(b) for a, b in ev) / 1e3
-    col_bytes = n * (sd.key_row + 8 + 4 + 8 + 1 + sd.value_row)
-    achieved = (file_bytes + col_bytes) / dec_s / 1e9
+        load_snapshot(blob, dated, proj)
+        loc, lift = C.c_double(), C.c_double()
+        lib.rh_debug_last_reload_us(C.byref(loc), C.byref(lift))
+        stages.append((lift.value, loc.value))
+    lib.rh_debug_reload_timing(0)
+    lift_us, locate_us = min(stages)
+    alg_bytes = file_bytes + n * (2 * 32 + 2 * sd.key_row + 2)
+    achieved = alg_bytes / (lift_us * 1e-6) / 1e9
     if rank == 0:
         recs = n * args.steps * world
         line = {
@@ -806,11 +811,17 @@ def reload(args, world, rank, dev, dist):
                        "parallelism": f"key-range shards x{world}"},
             "tombstones": info.tombstones,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "snapshot decode (k_snap_walk/up/down/offsets + k_snap_decode)",
-                         "kernel_avg_us": round(dec_s * 1e6, 1)},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic("snapshot", n),
+                         "kernel": "rh::k_snap_lift (fused listing + dated and projection lifts + keys + "
+                                   "samples + block sums)",
+                         "kernel_avg_us": round(lift_us, 1), "algorithmic_bytes": alg_bytes,
+                         "locate_us": round(locate_us, 1)},
             "root_check": "dated root == Σ lift(source rows)",
         }
+        valu = load_valu("snapshot", n, lift_us * 1e-6)  # the fused pass is VALU-bound, like the lift
+        if valu:
+            line["valu"] = valu
         if args.e2e == 1:  # the file's bytes in (pinned) host memory: H2D inside the reload
             host = blob.cpu().pin_memory()
             best = None
@@ -822,7 +833,7 @@ def reload(args, world, rank, dev, dist):
                 best = dt if best is None else min(best, dt)
             line["end_to_end"] = {"entries": n, "seconds": round(best, 5), "m_entries_per_s": round(n / best / 1e6, 1),
                                   "from": "pinned host bytes (H2D of the whole file inside the call)"}
-        if args.cpu_baseline and world == 1:
+        if args.cpu_baseline:  # rank 0 at every N: the same per-GPU workload's sample on this host
             line["cpu_baseline"] = cpu_baseline_reload(sd, sp, cols, args.cpu_sample or 1_000_000)
         print(json.dumps(line), flush=True)
     dated.close()

@@ -418,6 +418,15 @@ int rh_estore_set_host_tier(rh_estore *store, int enable);
  * "snapshot.load_finish" (the dated store's).  For tests of error paths only.              */
 int rh_debug_fail_point(const char *name);
 
+/* ---- measurement -----------------------------------------------------------------------
+ * on != 0: time every following snapshot reload's two device stages with HIP events on the
+ * loading store's stream; rh_debug_last_reload_us reads the last reload's times back in
+ * microseconds: locate = the entry walk and the transfer-function tree, lift = the fused pass
+ * (listing, both lifts, keys, samples and block sums; snapshot reloads of records up to 192 B).
+ * Both are 0 until a timed reload has run.                                                  */
+int rh_debug_reload_timing(int on);
+int rh_debug_last_reload_us(double *locate_us, double *lift_us);
+
 #ifdef __cplusplus
 }
 #endif

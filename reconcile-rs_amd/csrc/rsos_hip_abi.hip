@@ -18,6 +18,7 @@
 #include <chrono>
 #include <memory>
 #include <new>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -2139,10 +2140,27 @@ int snapshot_decode_into(const rh_schema &s, int key_form, const uint8_t *dev, s
 // The reload through the fused pass (snap_lift.hpp): locate the entries, then lift and load them
 // straight from the file into the stores' spare base buffers; one wait, then the stores commit
 // (a corrupt file leaves both as they were).  The caller holds both stores' locks and n > 0.
+// rh_debug_reload_timing: HIP events around the locate stage and the fused pass
+std::atomic<int> g_time_reload{0};
+std::mutex g_reload_mu;
+double g_reload_us[2] = {0, 0};
+
 int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::SnapFmt &f, const uint8_t *dev,
                           uint64_t n, uint32_t nsmax, uint64_t lds, rh_snapshot_info *info) {
     rh_store *a = dated ? dated : proj;
     int rc;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    struct EvGuard {
+        hipEvent_t *e;
+        ~EvGuard() {
+            for (int k = 0; k < 3; k++)
+                if (e[k]) (void)hipEventDestroy(e[k]);
+        }
+    } ev_guard{ev};
+    if (g_time_reload.load()) {
+        for (auto &e : ev) RH_HIP(hipEventCreate(&e));
+        RH_HIP(hipEventRecord(ev[0], a->stream));
+    }
     for (rh_store *x : {dated, proj})
         if (x && (rc = x->load_target(n))) return rc;
     rh::SnapTables t;
@@ -2150,6 +2168,7 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     const uint64_t nblk = (n + 255) / 256;
     uint32_t *part = static_cast<uint32_t *>(a->scratch.get(98, nblk * 4));
     if (a->scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+    if (ev[1]) RH_HIP(hipEventRecord(ev[1], a->stream));
     rh::SnapLift L;
     L.blob = dev;
     L.f = f;
@@ -2179,6 +2198,7 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     RH_HIP(rh::launch_snap_lift_schema(s.key_kind, (int)s.key_len, s.value_kind, (int)s.value_len, mode, L, lds,
                                        a->stream, &sup));
     if (!sup) return fail(RH_ERR_STATE, "fused snapshot pass unavailable (internal error)");
+    if (ev[2]) RH_HIP(hipEventRecord(ev[2], a->stream));
     RH_HIP(rh::snapshot_sum_tombstones(part, nblk, t.words, a->stream));
     try {
         a->snap_words.assign(4, 0);
@@ -2192,6 +2212,14 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     for (rh_store *x : {dated, proj})
         if (x && (rc = x->load_stage_sums(n, a->flag.p, x->stream))) return rc;
     if ((rc = a->sync())) return rc;
+    if (ev[2]) {
+        float ms[2] = {0, 0};
+        RH_HIP(hipEventElapsedTime(&ms[0], ev[0], ev[1]));
+        RH_HIP(hipEventElapsedTime(&ms[1], ev[1], ev[2]));
+        std::lock_guard<std::mutex> g(g_reload_mu);
+        g_reload_us[0] = 1e3 * ms[0];
+        g_reload_us[1] = 1e3 * ms[1];
+    }
     const uint64_t *w = a->snap_words.data();
     if (w[3] < n || w[1])
         return fail(RH_ERR_DATA, "snapshot entries are corrupt: " + std::to_string(std::min<uint64_t>(w[3], n)) +
@@ -2377,6 +2405,19 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
         return fail(rc, msg);
     }
     if (info) *info = inf;
+    return RH_OK;
+}
+
+int rh_debug_reload_timing(int on) {
+    g_time_reload.store(on ? 1 : 0);
+    return RH_OK;
+}
+
+int rh_debug_last_reload_us(double *locate_us, double *lift_us) {
+    if (!locate_us || !lift_us) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(g_reload_mu);
+    *locate_us = g_reload_us[0];
+    *lift_us = g_reload_us[1];
     return RH_OK;
 }
 

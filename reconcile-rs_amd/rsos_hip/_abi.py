@@ -123,6 +123,8 @@ SIGNATURES = [
     ("rh_estore_fingerprints", C.c_int, [P, C.c_uint64, C.c_uint64, U8P]),
     ("rh_estore_set_host_tier", C.c_int, [P, C.c_int]),
     ("rh_debug_fail_point", C.c_int, [C.c_char_p]),
+    ("rh_debug_reload_timing", C.c_int, [C.c_int]),
+    ("rh_debug_last_reload_us", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),
 ]
 
 _lib = None

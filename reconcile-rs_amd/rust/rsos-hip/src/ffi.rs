@@ -194,4 +194,6 @@ extern "C" {
     pub fn rh_estore_fingerprints(store: *mut rh_estore, lo: u64, hi: u64, host_out: *mut u8) -> c_int;
     pub fn rh_estore_set_host_tier(store: *mut rh_estore, enable: c_int) -> c_int;
     pub fn rh_debug_fail_point(name: *const c_char) -> c_int;
+    pub fn rh_debug_reload_timing(on: c_int) -> c_int;
+    pub fn rh_debug_last_reload_us(locate_us: *mut f64, lift_us: *mut f64) -> c_int;
 }

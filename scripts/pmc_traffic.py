@@ -4,7 +4,7 @@ the lift kernel, with the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_
 the bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is exact for 16-B
 stores.  Both counters are in KiB.
 
-usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <config> <records> <out.json>
+usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <config> <records> <out.json> [kernel]
 """
 import csv
 import json
@@ -31,13 +31,14 @@ def per_dispatch(path, counter, name_sub):
 
 def main():
     fetch_csv, write_csv, config, records, out = sys.argv[1:6]
-    fetch = per_dispatch(fetch_csv, "FETCH_SIZE", "k_lift")
-    write = per_dispatch(write_csv, "WRITE_SIZE", "k_lift")
+    kernel = sys.argv[6] if len(sys.argv) > 6 else "k_lift"
+    fetch = per_dispatch(fetch_csv, "FETCH_SIZE", kernel)
+    write = per_dispatch(write_csv, "WRITE_SIZE", kernel)
     if not fetch or not write:
-        raise SystemExit("no k_lift dispatches found in the PMC CSVs")
+        raise SystemExit(f"no {kernel} dispatches found in the PMC CSVs")
     f_kib, w_kib = statistics.median(fetch), statistics.median(write)
     doc = {
-        "config": config, "records": int(records),
+        "config": config, "records": int(records), "kernel": kernel,
         "fetch_size_kib_raw": f_kib, "write_size_kib": w_kib,
         "hbm_read_bytes_per_launch": 2 * f_kib * 1024,
         "hbm_write_bytes_per_launch": w_kib * 1024,

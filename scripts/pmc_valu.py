@@ -7,7 +7,7 @@ SQ_INSTS_VALU counts wave-level VALU instructions (summed over the chip).  Peak 
 measured rate of the 3-operand / shift-rotate forms BLAKE3 needs is ~4 cycles, see
 profiles/r01_micro_valu_*.log).
 
-usage: pmc_valu.py <counter_collection.csv> <kernel_stats.csv> <config> <records> <out.json>
+usage: pmc_valu.py <counter_collection.csv> <kernel_stats.csv> <config> <records> <out.json> [kernel]
 """
 import csv
 import json
@@ -17,9 +17,10 @@ import sys
 
 def main():
     pmc, stats, config, records, out = sys.argv[1:6]
+    kernel = sys.argv[6] if len(sys.argv) > 6 else "k_lift"
     per, names = {}, {}
     for row in csv.DictReader(open(pmc)):
-        if "k_lift" not in row.get("Kernel_Name", ""):
+        if kernel not in row.get("Kernel_Name", ""):
             continue
         d = row.get("Dispatch_Id") or row.get("Correlation_Id")
         names[d] = row["Kernel_Name"]

@@ -2239,7 +2239,8 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
         if (rc) break;
     }
     for (rh_store *x : {dated, proj}) {
-        if (rc || !x) break;
+        if (rc) break;
+        if (!x) continue;
         if (x == dated && fail_point("snapshot.load_finish")) rc = fail(RH_ERR_OOM, "injected failure (load_finish)");
         else rc = x->load_finish(n, true);
         inf.keys = x->nb;
@@ -2393,7 +2394,8 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
         if (rc) break;
     }
     for (rh_store *x : {dated, proj}) {
-        if (rc || !x) break;
+        if (rc) break;
+        if (!x) continue;
         if (x == dated && fail_point("snapshot.load_finish")) rc = fail(RH_ERR_OOM, "injected failure (load_finish)");
         else rc = x->load_finish(n, true);
         inf.keys = x->nb;

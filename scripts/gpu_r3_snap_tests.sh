@@ -1,0 +1,9 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r3_full
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q -rf --timeout 300 --timeout-method thread -m gpu tests/test_snapshot.py tests/test_wire.py > $O/pytest_snap.log 2>&1
+rc=$?; tail -n 5 $O/pytest_snap.log
+if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $O/pytest_snap.log | head -20; exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?; tail -3 $O/smoke.log; exit $rc

@@ -298,3 +298,76 @@ def test_reload_failure_leaves_both_stores_empty(gpu, point):
     info = load_snapshot(blob, dated, proj)
     assert info.keys == 5000 == dated.size() == proj.size()
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["b16_b64", "u32_u32", "b32_b64", "b16v_b64"])
+@pytest.mark.parametrize("which", ["dated", "projection"])
+def test_reload_into_one_store(gpu, oracle_lib, shape, which):
+    """The fused pass for a single store (dated-only and projection-only reloads; candidate-word
+    strides 2 (g = 8, 24) and 1 (u32 / u32: g = 4)): fingerprints, keys, root, ranks and sampled
+    searches equal the oracle's."""
+    from rsos_hip import GpuFingerprintStore
+    from rsos_hip.snapshot import load_snapshot
+    O = oracle_lib
+    key, value, okind, form = SHAPES[shape]
+    n = 25_000
+    cols = make_cols(key, value, n, 17, tomb=0.15)
+    data = encode(shape, cols, [], {})
+    sd, sp, _ = _schemas(shape)
+    schema = sd if which == "dated" else sp
+    st = GpuFingerprintStore(schema)
+    info = load_snapshot(data, st if which == "dated" else None, st if which == "projection" else None, form)
+    assert info.entries == info.keys == n == st.size() and info.tombstones == int(cols["tags"].sum())
+    rows = np.arange(n)
+    want = _oracle_lift(O, schema, cols, rows)
+    assert np.array_equal(st.fingerprints(), want)
+    # ranks through the search samples the fused pass wrote, for present keys and their successors
+    probe = np.linspace(0, n - 1, 97).astype(np.int64)
+    assert np.array_equal(st.ranks(np.ascontiguousarray(cols["keys"][probe])), probe)
+    limbs = want.view(np.uint64).reshape(n, 4)
+    total = sum(int(limbs[:, j].astype(object).sum()) << (64 * j) for j in range(4)) % (1 << 256)
+    assert st.aggregate().fingerprint.to_int() == total
+
+
+@pytest.mark.gpu
+def test_corrupt_reload_leaves_stores_unchanged(gpu):
+    """A corrupt file fails the fused reload before either store changes (Replica::load_snapshot
+    decodes the whole file first, src/snapshot.rs:76-98): with a batch pending in the delta run,
+    sizes, roots and key-range aggregates are what they were, and the rank-order contents equal a
+    twin pair of stores that never saw the file; both stores keep working."""
+    from rsos_hip import GpuFingerprintStore, _abi as A
+    from rsos_hip.store import KeyRange
+    from rsos_hip.snapshot import load_snapshot
+    cols = make_cols("bytes16", "bytes64", 20_000, 23, tomb=0.1)
+    batch = make_cols("bytes16", "bytes64", 3000, 29)
+    batch_cols = {c: batch[c] for c in ("keys", "values", "phys", "logical", "node", "tags")}
+    sd, sp, _ = _schemas("b16_b64")
+    pairs = []
+    for _ in range(2):  # the stores under test, and their twins
+        dated, proj = GpuFingerprintStore(sd), GpuFingerprintStore(sp)
+        load_snapshot(encode("b16_b64", cols, [], {}), dated, proj)
+        for st in (dated, proj):
+            st.apply(batch_cols, np.zeros(3000, np.uint8))
+        pairs.append((dated, proj))
+    (dated, proj), twins = pairs
+    cuts = [bytes(cols["keys"][i]) for i in range(0, 20_000, 1999)]
+
+    def state(st):  # no rank-order question: the delta run stays pending
+        aggs = [st.aggregate(KeyRange(lo, hi)) for lo, hi in zip(cuts, cuts[1:])]
+        return st.size(), st.aggregate().fingerprint.to_int(), [(a.size, a.fingerprint.to_int()) for a in aggs]
+    before = [state(dated), state(proj)]
+    bad_cols = make_cols("bytes16", "bytes64", 30_000, 31, tomb=0.1)
+    off = 16 + int(np.sum(np.where(bad_cols["tags"][:20_000] == 1, 40, 112)))
+    bad = bytearray(encode("b16_b64", bad_cols, [], {}))
+    bad[off + 36] = 5  # a State variant of 5 at entry 20,000
+    for blob in (bytes(bad), bytes(bad[: len(bad) // 3])):
+        with pytest.raises(A.RsosHipError) as e:
+            load_snapshot(blob, dated, proj)
+        assert e.value.code == A.ERR_DATA
+        assert [state(dated), state(proj)] == before
+    for st, twin in zip((dated, proj), twins):
+        assert np.array_equal(st.fingerprints(), twin.fingerprints())
+        assert [k for k, _ in st.enumerate()] == [k for k, _ in twin.enumerate()]
+    info = load_snapshot(encode("b16_b64", bad_cols, [], {}), dated, proj)
+    assert info.keys == 30_000 == dated.size() == proj.size()

@@ -961,6 +961,8 @@ struct rh_store {
         return RH_OK;
     }
     PinnedVec<uint64_t> snap_words;  // a fused snapshot reload's result words (snapshot_locate)
+    PinnedVec<uint64_t> snap_hdr;    // a device snapshot's 16-byte header, read back during the walk
+    hipEvent_t hdr_ev = nullptr;
     // A load whose rows are written before it is known to succeed (the fused snapshot reload):
     // the rows go to the spare base buffers, and the store changes only at load_commit -- a
     // corrupt file leaves it as it was, as Replica::load_snapshot does (src/snapshot.rs:76-98)
@@ -1609,8 +1611,11 @@ struct rh_store {
         r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); pr_out.release();
         tier_keys.release(); tier_prefix.release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release();
         snap.release();
+        sbsums.release(); sssums.release(); sbsmp.release(); sbsmp2.release(); sbtab.release(); sbtabp.release();
+        stot.release(); snap_words.release(); snap_hdr.release();
         scratch.release();
         if (dep) (void)hipEventDestroy(dep);
+        if (hdr_ev) (void)hipEventDestroy(hdr_ev);
         dep = nullptr;
         if (res_ev) (void)hipEventDestroy(res_ev);
         res_ev = nullptr;
@@ -2089,7 +2094,9 @@ uint32_t gcd32(uint32_t a, uint32_t b) {
     return a;
 }
 
-int snapshot_format(const rh_schema &s, int key_form, size_t len, uint64_t n, rh::SnapFmt *f) {
+// the entry layout of a file of len bytes (what the walk needs); snapshot_format adds the checks
+// against the header's entry count
+int snapshot_layout(const rh_schema &s, int key_form, size_t len, rh::SnapFmt *f) {
     if (key_form != RH_FORM_ARRAY && key_form != RH_FORM_VEC) return fail(RH_ERR_ARG, "bad key_form");
     if (key_form == RH_FORM_VEC && s.key_kind != RH_KEY_BYTES) return fail(RH_ERR_ARG, "RH_FORM_VEC needs byte keys");
     f->key_pre = key_form == RH_FORM_VEC ? 8 : 0;
@@ -2109,6 +2116,12 @@ int snapshot_format(const rh_schema &s, int key_form, size_t len, uint64_t n, rh
         return fail(RH_ERR_UNSUPPORTED, "snapshot entries too long for the device decoder");
     f->len = len;
     f->base = 16;
+    return RH_OK;
+}
+
+int snapshot_format(const rh_schema &s, int key_form, size_t len, uint64_t n, rh::SnapFmt *f) {
+    int rc = snapshot_layout(s, key_form, len, f);
+    if (rc) return rc;
     if (n >= (1ull << 31)) return fail(RH_ERR_UNSUPPORTED, "snapshot has more than 2^31 entries");
     if (n > (len - 16) / f->lt)
         return fail(RH_ERR_DATA, "snapshot entry count " + std::to_string(n) + " exceeds what its " +
@@ -2146,7 +2159,8 @@ std::mutex g_reload_mu;
 double g_reload_us[2] = {0, 0};
 
 int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::SnapFmt &f, const uint8_t *dev,
-                          uint64_t n, uint32_t nsmax, uint64_t lds, rh_snapshot_info *info) {
+                          uint64_t n, uint32_t nsmax, uint64_t lds, rh_snapshot_info *info, rh::SnapTables &t,
+                          bool walked) {
     rh_store *a = dated ? dated : proj;
     int rc;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -2163,8 +2177,8 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     }
     for (rh_store *x : {dated, proj})
         if (x && (rc = x->load_target(n))) return rc;
-    rh::SnapTables t;
-    RH_HIP(rh::snapshot_locate(f, dev, n, true, a->scratch, a->stream, &t, a->flag.p));
+    if (walked) RH_HIP(rh::snapshot_place(f, n, true, a->scratch, a->stream, &t, a->flag.p));
+    else RH_HIP(rh::snapshot_locate(f, dev, n, true, a->scratch, a->stream, &t, a->flag.p));
     const uint64_t nblk = (n + 255) / 256;
     uint32_t *part = static_cast<uint32_t *>(a->scratch.get(98, nblk * 4));
     if (a->scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -2327,18 +2341,55 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
     int rc;
     uint8_t h[16] = {0};
     const size_t hl = std::min<size_t>(len, 16);
+    rh_schema ds = a->schema;
+    ds.record_kind = RH_REC_DATED;
+    const int mode = dated && proj ? 2 : dated ? 0 : 1;
+    rh::SnapTables t;
+    bool walked = false;
     if (on_device) {
         if (!aligned16(bytes)) return fail(RH_ERR_ARG, "snapshot bytes must be 16-byte aligned");
         if ((rc = a->after(after_stream))) return rc;
-        if (hl) RH_HIP(hipMemcpyAsync(h, bytes, hl, hipMemcpyDeviceToHost, a->stream));
-        RH_HIP(hipStreamSynchronize(a->stream));
+        try {
+            a->snap_hdr.assign(2, 0);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "pinned header buffer");
+        }
+        if (hl) RH_HIP(hipMemcpyAsync(a->snap_hdr.data(), bytes, hl, hipMemcpyDeviceToHost, a->stream));
+        if (!a->hdr_ev) RH_HIP(hipEventCreateWithFlags(&a->hdr_ev, hipEventDisableTiming));
+        RH_HIP(hipEventRecord(a->hdr_ev, a->stream));
+        // the walk needs the file length, not the entry count: for a shape with the fused pass it
+        // starts now, behind the header's copy, and the header is read back while it runs
+        rh::SnapFmt fl;
+        uint32_t nsm = 0;
+        bool sup = false;
+        if (hl == 16 && snapshot_layout(ds, key_form, len, &fl) == RH_OK && rh::snap_lift_lds_bytes(fl, &nsm)) {
+            RH_HIP(rh::launch_snap_lift_schema(ds.key_kind, (int)ds.key_len, ds.value_kind, (int)ds.value_len, mode,
+                                               rh::SnapLift{}, 0, a->stream, &sup));
+            if (sup) {
+                RH_HIP(rh::snapshot_walk(fl, static_cast<const uint8_t *>(bytes), a->scratch, a->stream, &t));
+                if (a->scratch.err) {
+                    (void)hipStreamSynchronize(a->stream);
+                    return fail(RH_ERR_OOM, "scratch allocation failed");
+                }
+                walked = true;
+            }
+        }
+        g_err.clear();  // a layout the walk could not take is reported below, after the header
+        RH_HIP(hipEventSynchronize(a->hdr_ev));
+        memcpy(h, a->snap_hdr.data(), hl);
     } else if (hl) {
         memcpy(h, bytes, hl);
     }
+    // a started walk reads the caller's bytes: every early return below waits for it first
+    struct WalkGuard {
+        rh_store *a;
+        bool *on;
+        ~WalkGuard() {
+            if (*on) (void)hipStreamSynchronize(a->stream);
+        }
+    } walk_guard{a, &walked};
     uint64_t n = 0;
     if ((rc = snapshot_header(h, len, &n))) return rc;
-    rh_schema ds = a->schema;
-    ds.record_kind = RH_REC_DATED;
     rh::SnapFmt f;
     if ((rc = snapshot_format(ds, key_form, len, n, &f))) return rc;
     const uint8_t *dev = static_cast<const uint8_t *>(bytes);
@@ -2348,7 +2399,6 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
         dev = a->snap.p;
     }
     {  // the fused pass, where the shape has one (records up to 192 B)
-        const int mode = dated && proj ? 2 : dated ? 0 : 1;
         uint32_t nsmax = 0;
         const uint64_t lds = n ? rh::snap_lift_lds_bytes(f, &nsmax) : 0;
         bool fused = false;
@@ -2356,7 +2406,7 @@ int rh_store_load_snapshot(rh_store *dated, rh_store *proj, int key_form, const 
             RH_HIP(rh::launch_snap_lift_schema(ds.key_kind, (int)ds.key_len, ds.value_kind, (int)ds.value_len, mode,
                                                rh::SnapLift{}, lds, a->stream, &fused));
         if (fused) {
-            rc = snapshot_reload_fused(dated, proj, mode, f, dev, n, nsmax, lds, info);
+            rc = snapshot_reload_fused(dated, proj, mode, f, dev, n, nsmax, lds, info, t, walked);
             if (!on_device) a->snap.release();
             return rc;
         }

@@ -286,38 +286,38 @@ __global__ __launch_bounds__(1024) void k_snap_sum(const uint32_t *part, uint64_
 
 }  // namespace
 
-// steps 1 and 2: the true first-entry position and entry index of every segment (and with
-// segq, every 256-entry block's first and last segment).  words[3] = entries on the chain from
-// the file's first entry; words[0..2] zeroed for the pass that follows.  Nothing is waited for.
-hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bool with_segq, Scratch &s,
-                           hipStream_t st, SnapTables *t, uint32_t *flag) {
-    hipError_t e;
+// step 1 and the up-sweep of step 2 (independent of the entry count: a reload starts them before
+// it has read the file's header back)
+hipError_t snapshot_walk(const SnapFmt &f, const uint8_t *blob, Scratch &s, hipStream_t st, SnapTables *t) {
     const uint32_t P = f.phases;
     if (P > 256 || f.seg + f.lp + 32 > SNAP_LDS) return hipErrorInvalidValue;
     const uint64_t body = f.len > f.base ? f.len - f.base : 0;
     const uint64_t nseg = std::max<uint64_t>(1, (body + f.seg - 1) / f.seg);
     // tree fan-out: a node stages its children's tables (F * P * 12 B) in LDS
     const uint32_t F = std::max<uint32_t>(8, std::min<uint32_t>(SNAP_FAN, SNAP_TREE_LDS / (12 * P)));
-    std::vector<uint64_t> sizes{nseg};
-    while (sizes.back() > 1) sizes.push_back((sizes.back() + F - 1) / F);
-    const size_t L = sizes.size();
+    t->sizes.assign(1, nseg);
+    while (t->sizes.back() > 1) t->sizes.push_back((t->sizes.back() + F - 1) / F);
+    const size_t L = t->sizes.size();
     if (L > 12) return hipErrorInvalidValue;
-    std::vector<uint32_t *> ex(L), start(L);
-    std::vector<void *> cnt(L);  // level 0: u32 per segment, above: u64
-    std::vector<uint64_t *> basev(L);
+    t->ex.assign(L, nullptr);
+    t->cnt.assign(L, nullptr);  // level 0: u32 per segment, above: u64
+    t->lstart.assign(L, nullptr);
+    t->lbase.assign(L, nullptr);
     for (size_t l = 0; l < L; l++) {
-        ex[l] = static_cast<uint32_t *>(s.get(64 + 4 * l, sizes[l] * P * 4));
-        cnt[l] = s.get(65 + 4 * l, sizes[l] * P * (l ? 8 : 4));
-        start[l] = static_cast<uint32_t *>(s.get(66 + 4 * l, sizes[l] * 4));
-        basev[l] = static_cast<uint64_t *>(s.get(67 + 4 * l, sizes[l] * 8));
+        t->ex[l] = static_cast<uint32_t *>(s.get(64 + 4 * l, t->sizes[l] * P * 4));
+        t->cnt[l] = s.get(65 + 4 * l, t->sizes[l] * P * (l ? 8 : 4));
+        t->lstart[l] = static_cast<uint32_t *>(s.get(66 + 4 * l, t->sizes[l] * 4));
+        t->lbase[l] = static_cast<uint64_t *>(s.get(67 + 4 * l, t->sizes[l] * 8));
     }
-    unsigned long long *words = static_cast<unsigned long long *>(s.get(97, 64));
-    const uint64_t nblk = (n + 255) / 256;
-    uint32_t *segq = with_segq ? static_cast<uint32_t *>(s.get(99, (nblk + 1) * 4)) : nullptr;
+    t->words = static_cast<unsigned long long *>(s.get(97, 64));
     if (s.err) return s.err;
+    t->F = F;
+    t->nseg = nseg;
+    const auto &sizes = t->sizes;
+    const auto &ex = t->ex;
+    const auto &cnt = t->cnt;
     // staged bytes of a run of G segments: G * seg + lp (+ 16 for the aligned start)
     auto img_bytes = [&](uint32_t G) { return ((uint64_t)G * f.seg + f.lp + 16 + 15) / 16 * 16; };
-
     // 1. transfer functions.  Small workgroups (one wave when P <= 64) keep the LDS stage small,
     // so many workgroups per CU overlap their dependent walks
     {
@@ -328,8 +328,8 @@ hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bo
         hipLaunchKernelGGL(k_snap_walk, dim3((uint32_t)groups), dim3(bd), (size_t)img_bytes(G), st, blob, f, nseg, G,
                            ex[0], static_cast<uint32_t *>(cnt[0]));
     }
-    // 2. compose up to one group, then push the true positions down
-    const size_t up_lds = (size_t)F * P * 12, down_lds = up_lds + 8ull * (F + 1) + 4ull * F;
+    // 2 (up). compose up to one group
+    const size_t up_lds = (size_t)F * P * 12;
     for (size_t l = 0; l + 1 < L; l++) {
         if (l == 0)
             hipLaunchKernelGGL(k_snap_up<uint32_t>, dim3((uint32_t)sizes[1]), dim3(64), up_lds, st, ex[0],
@@ -340,8 +340,27 @@ hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bo
                                static_cast<const uint64_t *>(cnt[l]), sizes[l], P, F, ex[l + 1],
                                static_cast<uint64_t *>(cnt[l + 1]));
     }
+    return hipGetLastError();
+}
+
+// the down-sweep of step 2 (after snapshot_walk on the same stream): every segment's true first
+// entry, and with segq the fused pass's per-block segments; words zeroed, words[3] = entries on
+// the chain; *flag zeroed
+hipError_t snapshot_place(const SnapFmt &f, uint64_t n, bool with_segq, Scratch &s, hipStream_t st, SnapTables *t,
+                          uint32_t *flag) {
+    const uint32_t P = f.phases, F = t->F;
+    const auto &sizes = t->sizes;
+    const auto &ex = t->ex;
+    const auto &cnt = t->cnt;
+    const auto &start = t->lstart;
+    const auto &basev = t->lbase;
+    const size_t L = sizes.size();
+    const uint64_t nblk = (n + 255) / 256;
+    uint32_t *segq = with_segq ? static_cast<uint32_t *>(s.get(99, (nblk + 1) * 4)) : nullptr;
+    if (s.err) return s.err;
+    const size_t down_lds = (size_t)F * P * 12 + 8ull * (F + 1) + 4ull * F;
     hipLaunchKernelGGL(k_snap_init, dim3(1), dim3(64), 0, st, start[L - 1], basev[L - 1], cnt[L - 1], L > 1 ? 1 : 0,
-                       words, segq, flag);
+                       t->words, segq, flag);
     // entries on the chain from the file's first entry are checked against n by the caller: a
     // short chain only leaves rows unwritten, every access stays inside the blob and the outputs
     for (size_t l = L - 1; l-- > 0;) {
@@ -354,13 +373,16 @@ hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bo
                                static_cast<const uint64_t *>(cnt[l]), sizes[l], P, F, start[l + 1], basev[l + 1],
                                start[l], basev[l], nullptr, 0);
     }
-    if ((e = hipGetLastError())) return e;
     t->start = start[0];
     t->basev = basev[0];
     t->segq = segq;
-    t->words = words;
-    t->nseg = nseg;
-    return hipSuccess;
+    return hipGetLastError();
+}
+
+hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bool with_segq, Scratch &s,
+                           hipStream_t st, SnapTables *t, uint32_t *flag) {
+    hipError_t e = snapshot_walk(f, blob, s, st, t);
+    return e ? e : snapshot_place(f, n, with_segq, s, st, t, flag);
 }
 
 // LDS of one fused-reload workgroup: the candidate words of the run of segments holding 257

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "store_kernels.hpp"
 
 namespace rh {
@@ -35,9 +37,20 @@ struct SnapTables {
     uint32_t *segq = nullptr;    // per 256-entry block b: segment of entry min(256 b, n) - 1
     unsigned long long *words = nullptr;
     uint64_t nseg = 0;
+    // the transfer-function tree between snapshot_walk and snapshot_place (level 0 = segments)
+    uint32_t F = 0;
+    std::vector<uint64_t> sizes;
+    std::vector<uint32_t *> ex, lstart;
+    std::vector<void *> cnt;
+    std::vector<uint64_t *> lbase;
 };
+// walk (segments' transfer functions) + the tree's up-sweep: needs the file length, not the
+// entry count; snapshot_place then (same stream) pushes the true positions down
+hipError_t snapshot_walk(const SnapFmt &f, const uint8_t *blob, Scratch &s, hipStream_t st, SnapTables *t);
+hipError_t snapshot_place(const SnapFmt &f, uint64_t n, bool with_segq, Scratch &s, hipStream_t st, SnapTables *t,
+                          uint32_t *flag = nullptr);  // *flag zeroed on st
 hipError_t snapshot_locate(const SnapFmt &f, const uint8_t *blob, uint64_t n, bool with_segq, Scratch &s,
-                           hipStream_t st, SnapTables *t, uint32_t *flag = nullptr);  // *flag zeroed on st
+                           hipStream_t st, SnapTables *t, uint32_t *flag = nullptr);  // both
 // words[2] += Σ part[0 .. groups)
 hipError_t snapshot_sum_tombstones(const uint32_t *part, uint64_t groups, unsigned long long *words, hipStream_t st);
 

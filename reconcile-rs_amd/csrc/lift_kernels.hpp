@@ -30,6 +30,10 @@ struct DevCols {
     const uint64_t *node;
     const uint8_t *tags;
     const uint8_t *values;
+    // optional: record i's fingerprint goes to row dst[i] of fps (the batch path's sorted slot,
+    // written by the key sort that runs before the lift; rows with dst[i] >= n are not written);
+    // block sums are not formed then
+    const uint32_t *dst = nullptr;
 };
 
 constexpr int lowbit(int x) { return x & -x; }
@@ -376,7 +380,14 @@ __global__ __launch_bounds__(LIFT_THREADS) void k_lift(DevCols c, uint64_t n, ui
         const bool tomb = TAGS ? (cb.tags[t] != 0) : false;
         const uint8_t *vrow = cb.values + t * (uint32_t)L::VAL_ROW;
         lift_record<KK, KL, VK, VL, RK, TAGS>(kw, sw, tomb, vrow, h);
-        store_fp(fps + b0 * 32, t, h);
+        if (c.dst) {
+            // bounded: a bucket the key sort could not order leaves its rows' slots unwritten
+            // (the sort flags it and the batch is sorted and lifted again)
+            const uint32_t r = c.dst[i];
+            if (r < n) store_fp(fps, r, h);
+        } else {
+            store_fp(fps + b0 * 32, t, h);
+        }
         if constexpr (DUAL) {
             lift_record<KK, KL, VK, VL, REC_PROJECTION, TAGS>(kw, sw, tomb, vrow, h2);
             store_fp(fps2 + b0 * 32, t, h2);

@@ -112,11 +112,15 @@ int check_cols(const rh_schema &s, const rh_columns *c, size_t n) {
     return RH_OK;
 }
 
+// dst_row (optional, single lift without block sums): record i's fingerprint to row dst_row[i]
 int lift_dispatch(const rh_schema &s, const rh_columns &c, size_t n, uint8_t *fps, uint8_t *bs,
-                  uint8_t *fps2, uint8_t *bs2, bool dual, hipStream_t st) {
+                  uint8_t *fps2, uint8_t *bs2, bool dual, hipStream_t st, const uint32_t *dst_row = nullptr) {
     bool supported = false;
+    if (dst_row && (bs || dual)) return fail(RH_ERR_STATE, "lift to sorted rows: no block sums (internal error)");
+    rh::DevCols dc = to_dev(c);
+    dc.dst = dst_row;
     hipError_t e = rh::launch_lift_schema(s.key_kind, (int)s.key_len, s.value_kind, (int)s.value_len,
-                                          s.record_kind, c.tags != nullptr, dual, to_dev(c), n, fps, bs,
+                                          s.record_kind, c.tags != nullptr, dual, dc, n, fps, bs,
                                           fps2, bs2, st, &supported);
     if (!supported)
         return fail(RH_ERR_UNSUPPORTED,
@@ -592,7 +596,7 @@ struct rh_store {
     DevBuf<uint64_t> tot;
     // batch scratch
     DevColumns staging;
-    DevBuf<uint8_t> lfps, skeys, sfps, sops, hops, dops, cfps, cops;
+    DevBuf<uint8_t> skeys, sfps, sops, hops, dops, cfps, cops;
     DevBuf<uint64_t> counts, results;
     DevBuf<uint32_t> flag;
     // query scratch
@@ -1133,11 +1137,11 @@ struct rh_store {
         if ((rc = bsums.ensure(rh_num_blocks(base) * 32 + 32)) || (rc = ssums.ensure(rh_num_superblocks(base) * 32 + 32)) ||
             (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(rh::sample2_entries(base))) ||
             (rc = btab.ensure((1ull << rh::search_table_bits(base)) + 2)) || (rc = btabp.ensure(2)) ||
-            (rc = dtab.ensure((1ull << rh::search_table_bits(plan)) + 2)) || (rc = dtabp.ensure(2)) ||
+            (rc = dtab.ensure((1ull << rh::search_table_bits(plan, false)) + 2)) || (rc = dtabp.ensure(2)) ||
             (rc = dsmp[0].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp[1].ensure(rh_num_blocks(plan) + 1)) ||
             (rc = dsmp2[0].ensure(rh::sample2_entries(plan))) || (rc = dsmp2[1].ensure(rh::sample2_entries(plan))) ||
             (rc = cfps.ensure(plan * 32 + 64)) ||
-            (rc = cops.ensure(plan + 64)) || (rc = lfps.ensure(batch * 32 + 64)) || (rc = skeys.ensure(batch * kl + 64)) ||
+            (rc = cops.ensure(plan + 64)) || (rc = skeys.ensure(batch * kl + 64)) ||
             (rc = sfps.ensure(batch * 32 + 64)) || (rc = sops.ensure(std::max(batch, base) + 64)) ||
             (rc = dheap.ensure(plan * sizeof(rh::DeltaRec) + 64)) || (rc = dops.ensure(batch + 64)) ||
             (rc = mcnt.ensure(8)) || (rc = results.ensure(12)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
@@ -1161,11 +1165,10 @@ struct rh_store {
         RH_HIP(hipEventSynchronize(ev));
         return RH_OK;
     }
-    // k batches in order, each exactly as apply_device would apply it; batch i + 1 is lifted (into
-    // the other of two fingerprint buffers) while the host waits for batch i's result, so the
-    // device does not idle between batches.  On an error, batches before the failing one stay
-    // applied, the failing one and those after it are not.
-    DevBuf<uint8_t> lfps2;
+    // k batches in order, each exactly as apply_device would apply it; batch i + 1 is sorted and
+    // lifted while the host waits for batch i's result, so the device does not idle between
+    // batches.  On an error, batches before the failing one stay applied, the failing one and
+    // those after it are not.
     int apply_device_many(const rh_columns *cs, const uint8_t *const *ops, const size_t *ms, size_t k, uint64_t *out) {
         int rc;
         size_t mmax = 0;
@@ -1173,40 +1176,63 @@ struct rh_store {
             mmax = std::max(mmax, ms[i]);
             out[3 * i] = out[3 * i + 1] = out[3 * i + 2] = 0;
         }
-        if ((rc = lfps.ensure(mmax * 32 + 64)) || (rc = lfps2.ensure(mmax * 32 + 64))) return rc;
-        uint8_t *buf[2] = {lfps.p, lfps2.p};
-        bool lifted = false;
+        // every batch's buffers at the largest size first: growing one later frees it (a device drain)
+        if ((rc = batch_buffers(mmax))) return rc;
+        bool prepared = false;
         for (size_t i = 0; i < k; i++) {
             const bool pipe = ms[i] > 0 && i + 1 < k && ms[i + 1] > 0;
-            if ((rc = apply_device(cs[i], ops ? ops[i] : nullptr, ms[i], out + 3 * i, buf[i & 1], lifted,
-                                   pipe ? &cs[i + 1] : nullptr, pipe ? ms[i + 1] : 0, buf[(i + 1) & 1])))
-                return rc;
-            lifted = pipe;
+            bool next_prepared = false;
+            rc = apply_device(cs[i], ops ? ops[i] : nullptr, ms[i], out + 3 * i, prepared, pipe ? &cs[i + 1] : nullptr,
+                              pipe && ops ? ops[i + 1] : nullptr, pipe ? ms[i + 1] : 0, &next_prepared);
+            if (rc) return rc;
+            prepared = next_prepared;
         }
         return RH_OK;
     }
+    // the batch buffers for batches of up to m rows (sorted keys / fingerprints / ops, the sort's
+    // positions, the per-key search results)
+    int batch_buffers(size_t m) {
+        int rc;
+        if ((rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)) ||
+            (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)) || (rc = results.ensure(12)))
+            return rc;
+        (void)scratch.u32(7, m), (void)scratch.u32(9, m), (void)scratch.u32(10, m);
+        (void)scratch.u8(2, m), (void)scratch.u8(3, m);
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        return RH_OK;
+    }
+    // Steps 1-2 of a batch: the key sort (sorted keys / ops into skeys / sops, each input row's
+    // sorted row into the position scratch, the sort's flags into the result block), then the lift,
+    // which writes each fingerprint straight to its sorted row of sfps -- the sort gathers no
+    // fingerprints.  Queued only; needs batch_buffers(m).
+    int prepare_batch(const rh_columns &c, const uint8_t *ops, size_t m, bool full) {
+        uint32_t *pos = scratch.u32(7, m);
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
+        RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), nullptr, ops, m, scratch, skeys.p, nullptr, sops.p,
+                                r_flags, full, stream, pos));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        return lift_dispatch(schema, c, m, sfps.p, nullptr, nullptr, nullptr, false, stream, pos);
+    }
     PinnedVec<uint64_t> res_host;  // the batch's 96-byte result block
-    // fps_buf: where the batch's fingerprints are (lifted: already there, from the previous batch
-    // of apply_device_many) or go; nullptr: lfps.  next: a batch to lift into next_fps once this
-    // batch's kernels are queued -- the device runs it while the host waits for this batch's result
-    // (an event on the result copy, not the stream) and enqueues the next batch behind it.
-    int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3], uint8_t *fps_buf = nullptr,
-                     bool lifted = false, const rh_columns *next = nullptr, size_t next_m = 0,
-                     uint8_t *next_fps = nullptr) {
+    // prepared: steps 1-2 of this batch were queued by the previous call (apply_device_many).
+    // next: a batch whose steps 1-2 are queued once this batch's kernels are -- the device runs them
+    // while the host waits for this batch's result (an event on the result copy, not the stream);
+    // *next_prepared says whether they were (a re-sort of this batch overwrites them).
+    int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3], bool prepared = false,
+                     const rh_columns *next = nullptr, const uint8_t *next_ops = nullptr, size_t next_m = 0,
+                     bool *next_prepared = nullptr) {
         int rc;
         out[0] = out[1] = out[2] = 0;
+        if (next_prepared) *next_prepared = false;
         if (m == 0) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         const int fmode = fold_mode();  // how this batch reaches a fresh host tier
         version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
-        if ((!fps_buf && (rc = lfps.ensure(m * 32 + 64))) || (rc = skeys.ensure(m * kl + 64)) ||
-            (rc = sfps.ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)) || (rc = dops.ensure(m + 64)) ||
-            (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
-            return rc;
-        uint8_t *const fps = fps_buf ? fps_buf : lfps.p;
-        // 1. lift the batch (delete rows are lifted too and ignored)
-        if (!lifted && (rc = lift_dispatch(schema, c, m, fps, nullptr, nullptr, nullptr, false, stream))) return rc;
-        // 2-5 run without a host round trip: everything is written to the delta run's *other*
+        if ((rc = batch_buffers(m))) return rc;
+        // 1-2. key sort, lift into the sorted rows (delete rows are lifted too and ignored)
+        if (!prepared && (rc = prepare_batch(c, ops, m, false))) return rc;
+        // 3-5 run without a host round trip: everything is written to the delta run's *other*
         // buffers, and one sync at the end brings back the flags and counts.  A duplicate key
         // then leaves the store exactly as it was (nothing is committed); a tie on the leading
         // key digit re-runs the steps with the full sort.
@@ -1233,9 +1259,7 @@ struct rh_store {
         // one 96-byte result block, one D2H copy: [0..2] batch counts, [3..5] merge counts,
         // [6] sort flags, [7] the change of the delta run's count total (int64), [8..11] the change
         // of its contribution total
-        if ((rc = results.ensure(12))) return rc;
         uint64_t *r_counts = results.p, *r_merge = results.p + 3;
-        uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
         int64_t *r_dcnt = reinterpret_cast<int64_t *>(results.p + 7);
         // pinned: the copy stays asynchronous and sync() polls for it (a pageable destination
         // makes the runtime stage the copy and block in an interrupt-driven wait)
@@ -1248,11 +1272,8 @@ struct rh_store {
         uint32_t flags = 0;
         int next_rc = RH_OK;
         for (int full = 0; full < 2; full++) {
-            // 2. key order (+ duplicate / leading-digit-tie flags; the sort zeroes them, and every
-            //    other word of the result block is written by a later kernel)
-            RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), fps, ops, m, scratch, skeys.p, sfps.p,
-                                    sops.p, r_flags, full == 1, stream));
-            if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            // 1-2 again with the full sort (the bucket sort's order was not final)
+            if (full == 1 && (rc = prepare_batch(c, ops, m, true))) return rc;
             // 3. where each key is now: base and delta runs
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, skeys.p, m, rank_b, present_b, stream,
                                         base_table()));
@@ -1261,9 +1282,9 @@ struct rh_store {
             // samples); the table is built here, where the run's row count is known on the host
             rh::SearchTable dt{};
             if (nd >= DTAB_MIN) {
-                if ((rc = dtab.ensure((1ull << rh::search_table_bits(nd)) + 2)) || (rc = dtabp.ensure(2))) return rc;
-                if (full == 0) RH_HIP(rh::launch_search_table(dsmp2[cd].p, nd, dtab.p, dtabp.p, stream));
-                dt = rh::SearchTable{dtab.p, dtabp.p, rh::search_table_bits(nd)};
+                if ((rc = dtab.ensure((1ull << rh::search_table_bits(nd, false)) + 2)) || (rc = dtabp.ensure(2))) return rc;
+                if (full == 0) RH_HIP(rh::launch_search_table(dsmp2[cd].p, nd, dtab.p, dtabp.p, stream, false));
+                dt = rh::SearchTable{dtab.p, dtabp.p, rh::search_table_bits(nd, false)};
             }
             RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, skeys.p, m, rank_d, present_d,
                                         stream, dt));
@@ -1284,15 +1305,18 @@ struct rh_store {
             if (full == 0 && next && next_m) {
                 if (!res_ev) RH_HIP(hipEventCreateWithFlags(&res_ev, hipEventDisableTiming));
                 RH_HIP(hipEventRecord(res_ev, stream));
-                // a failure to queue the next batch's lift is reported after this batch commits
-                // (the batches before the failing one stay applied), never instead of it
-                next_rc = lift_dispatch(schema, *next, next_m, next_fps, nullptr, nullptr, nullptr, false, stream);
+                // a failure to queue the next batch is reported after this batch commits (the
+                // batches before the failing one stay applied), never instead of it
+                next_rc = batch_buffers(next_m);
+                if (!next_rc) next_rc = prepare_batch(*next, next_ops, next_m, false);
                 if ((rc = next_rc ? sync() : sync_event(res_ev))) return rc;
+                if (next_prepared) *next_prepared = !next_rc;
             } else if ((rc = sync())) {
                 return rc;
             }
             memcpy(&flags, &host[6], 4);
             if (!(flags & 6)) break;  // 2: leading-digit tie, 4: skewed buckets
+            if (next_prepared) *next_prepared = false;  // the re-sort overwrites the next batch's steps 1-2
         }
         int64_t dcnt;
         memcpy(&dcnt, &host[7], 8);
@@ -1601,7 +1625,7 @@ struct rh_store {
             dbsums[k].release(); dssums[k].release(); dblk[k].release(); dinb[k].release(); dsblk[k].release();
         }
         staging.release();
-        lfps.release(); lfps2.release(); skeys.release(); sfps.release(); sops.release(); hops.release(); dheap.release(); heap_len = 0;
+        skeys.release(); sfps.release(); sops.release(); hops.release(); dheap.release(); heap_len = 0;
         dops.release(); cfps.release(); cops.release(); counts.release(); flag.release();
         results.release();
         q_lo.release(); q_hi.release(); q_dlo.release(); q_dhi.release(); q_merged.release();

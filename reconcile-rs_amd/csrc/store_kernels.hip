@@ -156,12 +156,14 @@ __global__ void k_iota(uint32_t *p, uint64_t m) {
 // adjacent keys share their most significant digit (order not final)
 template <int KK, int KL>
 __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, const uint32_t *perm,
-                         uint64_t m, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, int msd_only) {
+                         uint64_t m, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *pos, uint32_t *flags,
+                         int msd_only) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const uint64_t s = perm[j];
     copy_bytes<KL>(skeys + j * KL, keys + s * KL);
-    copy_bytes<32>(sfps + 32 * j, fps + 32 * s);
+    if (fps) copy_bytes<32>(sfps + 32 * j, fps + 32 * s);
+    else pos[s] = (uint32_t)j;
     sops[j] = ops ? ops[s] : 0;
     if (j > 0) {
         const uint8_t *prev = keys + (uint64_t)perm[j - 1] * KL;
@@ -347,91 +349,154 @@ __global__ __launch_bounds__(1024) void k_cs_bucketscan(const uint32_t *total, u
     if (__ballot(big) && (t & 63) == 0) atomicOr(flags, 4u);
 }
 
+// a key's KL bytes as dwords (widest aligned accesses), and back
+template <int KL>
+__device__ __forceinline__ void key_words_load(const uint8_t *p, uint32_t *w) {
+    if constexpr (KL % 16 == 0) {
+#pragma unroll
+        for (int o = 0; o < KL; o += 16) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(p + o);
+            w[o / 4] = v.x; w[o / 4 + 1] = v.y; w[o / 4 + 2] = v.z; w[o / 4 + 3] = v.w;
+        }
+    } else if constexpr (KL % 8 == 0) {
+#pragma unroll
+        for (int o = 0; o < KL; o += 8) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(p + o);
+            w[o / 4] = v.x; w[o / 4 + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int o = 0; o < KL; o += 4) w[o / 4] = *reinterpret_cast<const uint32_t *>(p + o);
+    }
+}
+template <int KL>
+__device__ __forceinline__ void key_words_store(uint8_t *p, const uint32_t *w) {
+    if constexpr (KL % 16 == 0) {
+#pragma unroll
+        for (int o = 0; o < KL; o += 16)
+            *reinterpret_cast<uint4 *>(p + o) = make_uint4(w[o / 4], w[o / 4 + 1], w[o / 4 + 2], w[o / 4 + 3]);
+    } else if constexpr (KL % 8 == 0) {
+#pragma unroll
+        for (int o = 0; o < KL; o += 8) *reinterpret_cast<uint2 *>(p + o) = make_uint2(w[o / 4], w[o / 4 + 1]);
+    } else {
+#pragma unroll
+        for (int o = 0; o < KL; o += 4) *reinterpret_cast<uint32_t *>(p + o) = w[o / 4];
+    }
+}
+// the leading digit (key_digit d = 0) of a key held as dwords
+template <int KK, int KL>
+__device__ __forceinline__ uint64_t digit_of_words(const uint32_t *w) {
+    if constexpr (KK == KEY_U32) return w[0];
+    else if constexpr (KK == KEY_U64) return ((uint64_t)w[1] << 32) | w[0];
+    else return __builtin_bswap64(((uint64_t)w[1] << 32) | w[0]);
+}
+
+// (key, row) pairs into coarse-bucket order: the whole key travels, so the per-bucket sort
+// reads its keys from one contiguous stretch instead of gathering them from the input rows
 template <int KK, int KL>
 __global__ __launch_bounds__(CS_WG) void k_cs_scatter(const uint8_t *keys, uint64_t m, const uint64_t *params,
                                                       uint32_t C, const uint32_t *hist, const uint32_t *start,
-                                                      uint64_t *odig, uint32_t *oidx) {
+                                                      uint8_t *okey, uint32_t *oidx) {
     __shared__ uint32_t cur[CS_MAX_C];
     const uint64_t mn = params[0], sh = params[1];
     const uint32_t *h = hist + (uint64_t)blockIdx.x * C;
     for (uint32_t b = threadIdx.x; b < C; b += CS_WG) cur[b] = start[b] + h[b];
     __syncthreads();
     const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
-    uint64_t d[CS_TILE / CS_WG];
+    // four keys per lane at a time, each group's loads before its stores (eight at once spill)
+    auto group = [&](int k0) {
+        constexpr int W = KL / 4;
+        uint32_t kw[4][W];
 #pragma unroll
-    for (int k = 0; k < CS_TILE / CS_WG; k++) {
-        const uint64_t i = i0 + CS_WG * k + threadIdx.x;
-        d[k] = i < m ? key_digit<KK, KL>(keys + i * KL, 0) : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < CS_TILE / CS_WG; k++) {
-        const uint64_t i = i0 + CS_WG * k + threadIdx.x;
-        if (i < m) {
-            const uint32_t pos = atomicAdd(&cur[(uint32_t)((d[k] - mn) >> sh) >> CS_FINE_BITS], 1u);
-            odig[pos] = d[k];
-            oidx[pos] = (uint32_t)i;
+        for (int k = 0; k < 4; k++) {
+            const uint64_t i = i0 + CS_WG * (k0 + k) + threadIdx.x;
+            if (i < m) key_words_load<KL>(keys + i * KL, kw[k]);
         }
-    }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t i = i0 + CS_WG * (k0 + k) + threadIdx.x;
+            if (i < m) {
+                const uint64_t d = digit_of_words<KK, KL>(kw[k]);
+                const uint32_t pos = atomicAdd(&cur[(uint32_t)((d - mn) >> sh) >> CS_FINE_BITS], 1u);
+                key_words_store<KL>(okey + (uint64_t)pos * KL, kw[k]);
+                oidx[pos] = (uint32_t)i;
+            }
+        }
+    };
+    static_assert(CS_TILE / CS_WG == 8, "two groups of four keys per lane");
+    group(0);
+    group(4);
 }
 
-// rows 256 (K0 + k) + lane, k < 4, of a bucket's sorted order: key / fingerprint / op from the
-// input rows sx[] into place
+// rows 256 (K0 + k) + lane, k < 4, of a bucket's sorted order: the key from the bucket's stretch
+// of scattered keys, the op (and, with fps, the fingerprint) from the input row; pos (when given):
+// pos[input row] = its sorted row, for a lift that runs after the sort
 template <int KL, int K0>
-__device__ __forceinline__ void cs_gather(const uint32_t *sx, uint32_t n, uint32_t s0, const uint8_t *keys,
-                                          const uint8_t *fps, const uint8_t *ops, uint8_t *skeys, uint8_t *sfps,
-                                          uint8_t *sops) {
+__device__ __forceinline__ void cs_gather(const uint16_t *sx, const uint32_t *tx, const uint16_t *tl, uint32_t n,
+                                          uint32_t s0, const uint8_t *okey, const uint8_t *fps, const uint8_t *ops,
+                                          uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *pos) {
     static_assert(KL % 4 == 0, "keys: whole dwords");
     const uint32_t t = threadIdx.x;
-    uint32_t kw[4][KL / 4], ov[4];
+    uint32_t kw[4][KL / 4], ov[4], xr[4];
     uint4 f0[4], f1[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint32_t j = 256 * (K0 + k) + t;
-        const uint64_t src = j < n ? sx[j] : 0;  // row 0 stands in past n (not stored)
-#pragma unroll
-        for (int q = 0; q < KL / 4; q++) kw[k][q] = reinterpret_cast<const uint32_t *>(keys + src * KL)[q];
-        f0[k] = reinterpret_cast<const uint4 *>(fps + 32 * src)[0];
-        f1[k] = reinterpret_cast<const uint4 *>(fps + 32 * src)[1];
+        const uint32_t q = j < n ? sx[j] : 0;  // slot 0 stands in past n (not stored)
+        const uint64_t src = tx[q];
+        xr[k] = (uint32_t)src;
+        key_words_load<KL>(okey + (uint64_t)(s0 + tl[q]) * KL, kw[k]);
+        if (fps) {
+            f0[k] = reinterpret_cast<const uint4 *>(fps + 32 * src)[0];
+            f1[k] = reinterpret_cast<const uint4 *>(fps + 32 * src)[1];
+        }
         ov[k] = ops ? ops[src] : 0u;
     }
     // written out per row: a loop here is rotated into a variable trip count, which indexes the
     // arrays dynamically and puts them in scratch memory
-    auto put = [&](int k, const uint32_t *w, uint4 a, uint4 b, uint32_t op) {
+    auto put = [&](int k, const uint32_t *w, uint4 a, uint4 b, uint32_t op, uint32_t x) {
         const uint32_t j = 256 * (K0 + k) + t;
         if (j >= n) return;
         const uint64_t o = (uint64_t)s0 + j;
-#pragma unroll
-        for (int q = 0; q < KL / 4; q++) reinterpret_cast<uint32_t *>(skeys + o * KL)[q] = w[q];
-        reinterpret_cast<uint4 *>(sfps + 32 * o)[0] = a;
-        reinterpret_cast<uint4 *>(sfps + 32 * o)[1] = b;
+        key_words_store<KL>(skeys + o * KL, w);
+        if (fps) {
+            reinterpret_cast<uint4 *>(sfps + 32 * o)[0] = a;
+            reinterpret_cast<uint4 *>(sfps + 32 * o)[1] = b;
+        }
+        if (pos) pos[x] = (uint32_t)o;
         sops[o] = (uint8_t)op;
     };
-    put(0, kw[0], f0[0], f1[0], ov[0]);
-    put(1, kw[1], f0[1], f1[1], ov[1]);
-    put(2, kw[2], f0[2], f1[2], ov[2]);
-    put(3, kw[3], f0[3], f1[3], ov[3]);
+    put(0, kw[0], f0[0], f1[0], ov[0], xr[0]);
+    put(1, kw[1], f0[1], f1[1], ov[1], xr[1]);
+    put(2, kw[2], f0[2], f1[2], ov[2], xr[2]);
+    put(3, kw[3], f0[3], f1[3], ov[3], xr[3]);
 }
 
 // one workgroup per coarse bucket (n <= CS_CAP keys, CS_CAP / 256 per lane, held in registers)
 template <int KK, int KL>
-__global__ __launch_bounds__(256) void k_cs_sort(const uint64_t *dig, const uint32_t *idx, const uint32_t *start,
-                                                 const uint32_t *total, const uint64_t *params, const uint8_t *keys,
-                                                 const uint8_t *fps, const uint8_t *ops, uint8_t *skeys, uint8_t *sfps,
-                                                 uint8_t *sops, uint32_t *flags) {
+__global__ __launch_bounds__(256) void k_cs_sort(const uint8_t *okey, const uint32_t *idx, const uint32_t *start,
+                                                 const uint32_t *total, const uint64_t *params, const uint8_t *fps,
+                                                 const uint8_t *ops, uint8_t *skeys, uint8_t *sfps, uint8_t *sops,
+                                                 uint32_t *pos, uint32_t *flags) {
     constexpr int D = KK == KEY_BYTES ? KL / 8 : 1, PER = CS_CAP / 256;
     static_assert(CS_FINE == 256, "one fine bucket per lane");
+    // fine-bucket order: td digit, tx input row, tl index in the bucket's stretch; sx: sorted
+    // position -> slot of that order
     __shared__ uint64_t td[CS_CAP];
-    __shared__ uint32_t tx[CS_CAP], sx[CS_CAP];
+    __shared__ uint32_t tx[CS_CAP];
+    __shared__ uint16_t tl[CS_CAP], sx[CS_CAP];
+    static_assert(CS_CAP <= 65536, "16-bit slots");
     __shared__ uint32_t fst[CS_FINE], fcur[CS_FINE], wsum[4];
     const uint32_t b = blockIdx.x, t = threadIdx.x, n = total[b], s0 = start[b];
     if (n == 0 || n > (uint32_t)CS_CAP) return;  // uniform; too large: flagged by k_cs_bucketscan
     const uint64_t mn = params[0], sh = params[1];
+    const uint8_t *bk = okey + (uint64_t)s0 * KL;
     uint64_t d[PER];
     uint32_t x[PER], f[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const uint32_t i = 256 * k + t;
-        d[k] = i < n ? dig[s0 + i] : 0;
+        d[k] = i < n ? key_digit<KK, KL>(bk + (uint64_t)i * KL, 0) : 0;
         x[k] = i < n ? idx[s0 + i] : 0;
         f[k] = (uint32_t)((d[k] - mn) >> sh) & (CS_FINE - 1);
     }
@@ -462,6 +527,7 @@ __global__ __launch_bounds__(256) void k_cs_sort(const uint64_t *dig, const uint
             const uint32_t p = atomicAdd(&fcur[f[k]], 1u);
             td[p] = d[k];
             tx[p] = x[k];
+            tl[p] = (uint16_t)(256 * k + t);
         }
     }
     __syncthreads();
@@ -478,18 +544,19 @@ __global__ __launch_bounds__(256) void k_cs_sort(const uint64_t *dig, const uint
                 r += dq < dp ? 1u : 0u;
             } else if (q != p) {
                 const uint32_t xq = tx[q];
-                const int cmp = D == 1 ? 0 : key_cmp<KK, KL>(keys + (uint64_t)xq * KL, keys + (uint64_t)xp * KL);
+                const int cmp =
+                    D == 1 ? 0 : key_cmp<KK, KL>(bk + (uint64_t)tl[q] * KL, bk + (uint64_t)tl[p] * KL);
                 if (cmp == 0) dup = true;
                 r += (cmp < 0 || (cmp == 0 && xq < xp)) ? 1u : 0u;
             }
         }
-        sx[r] = xp;
+        sx[r] = (uint16_t)p;
     }
     __syncthreads();
-    // gather key / fingerprint / op of the sorted rows, 4 per lane at a time with all of the
+    // gather key / op (/ fingerprint) of the sorted rows, 4 per lane at a time with all of the
     // group's loads before its stores
-    cs_gather<KL, 0>(sx, n, s0, keys, fps, ops, skeys, sfps, sops);
-    if (n > 4 * 256) cs_gather<KL, 4>(sx, n, s0, keys, fps, ops, skeys, sfps, sops);
+    cs_gather<KL, 0>(sx, tx, tl, n, s0, okey, fps, ops, skeys, sfps, sops, pos);
+    if (n > 4 * 256) cs_gather<KL, 4>(sx, tx, tl, n, s0, okey, fps, ops, skeys, sfps, sops, pos);
     if (__ballot(dup) && (t & 63) == 0) atomicOr(flags, 1u);
 }
 
@@ -604,7 +671,9 @@ __global__ void k_search_sampled(const uint8_t *keys, uint64_t n, const uint64_t
     } else {
         sample_window(smp, (n + SMP_STRIDE - 1) / SMP_STRIDE, SMP_STRIDE, d, lo, hi);
     }
-    if (smp2) sample_window(smp2, (n + SMP2_STRIDE - 1) / SMP2_STRIDE, SMP2_STRIDE, d, lo, hi);
+    // the samples narrow a window wider than two sample strides (a fine table's window is one
+    // or two strides already: the keys are searched directly, one sample line saved)
+    if (smp2 && hi - lo > 2 * SMP2_STRIDE) sample_window(smp2, (n + SMP2_STRIDE - 1) / SMP2_STRIDE, SMP2_STRIDE, d, lo, hi);
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
         if (key_cmp<KK, KL>(keys + mid * KL, key) < 0) lo = mid + 1;
@@ -1472,8 +1541,9 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
                           uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, bool full,
-                          hipStream_t st) override {
+                          hipStream_t st, uint32_t *pos) override {
         hipError_t e;
+        if (!fps == !pos) return hipErrorInvalidValue;  // exactly one of: gather fps, emit positions
         uint32_t *perm = s.u32(0, m), *perm2 = s.u32(1, m);
         uint64_t *dig = s.u64(0, m), *dig2 = s.u64(1, m);
         if (s.err) return s.err;
@@ -1488,7 +1558,7 @@ struct KeyOps final : StoreKeyOps {
             std::swap(perm, perm2);
             return hipSuccess;
         };
-        if (!full && m <= CS_MAX_M) return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st);
+        if (!full && m <= CS_MAX_M) return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st, pos);
         if ((e = hipMemsetAsync(flags, 0, 4, st))) return e;
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
         // multi-digit keys: the most significant digit alone orders random and spread keys
@@ -1498,16 +1568,18 @@ struct KeyOps final : StoreKeyOps {
         for (int d = lo_digit; d >= 0; d--)
             if ((e = pass(d))) return e;
         hipLaunchKernelGGL((k_gather<KK, KL>), g1(m), dim3(256), 0, st, keys, fps, ops, perm, m, skeys, sfps, sops,
-                           flags, (full || D == 1) ? 0 : 1);
+                           pos, flags, (full || D == 1) ? 0 : 1);
         return hipGetLastError();
     }
 
     hipError_t sort_batch_buckets(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
-                                  uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, hipStream_t st) {
+                                  uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, hipStream_t st,
+                                  uint32_t *pos) {
         uint32_t cb = 0;
         while ((1ull << cb) * 1024 < m) cb++;  // ~1,000 keys per coarse bucket
         const uint32_t C = 1u << cb, nwg = (uint32_t)((m + CS_TILE - 1) / CS_TILE), bbits = cb + CS_FINE_BITS;
-        uint64_t *part = s.u64(2, 2ull * nwg + 2), *dig = s.u64(0, m);
+        uint64_t *part = s.u64(2, 2ull * nwg + 2);
+        uint8_t *okey = reinterpret_cast<uint8_t *>(s.u64(0, (m * KL + 7) / 8));
         uint32_t *hist = s.u32(15, (uint64_t)nwg * C), *idx = s.u32(0, m), *total = s.u32(1, C);
         uint32_t *start = s.u32(2, C);
         if (s.err) return s.err;
@@ -1516,10 +1588,10 @@ struct KeyOps final : StoreKeyOps {
         hipLaunchKernelGGL((k_cs_hist<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, nwg, bbits, C, hist);
         hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(1024), 0, st, hist, nwg, C, total);
         hipLaunchKernelGGL(k_cs_bucketscan, dim3(1), dim3(1024), 0, st, total, C, start, flags, part, nwg, bbits, params);
-        hipLaunchKernelGGL((k_cs_scatter<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, params, C, hist, start, dig,
-                           idx);
-        hipLaunchKernelGGL((k_cs_sort<KK, KL>), dim3(C), dim3(256), 0, st, dig, idx, start, total, params, keys, fps,
-                           ops, skeys, sfps, sops, flags);
+        hipLaunchKernelGGL((k_cs_scatter<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, params, C, hist, start,
+                           okey, idx);
+        hipLaunchKernelGGL((k_cs_sort<KK, KL>), dim3(C), dim3(256), 0, st, okey, idx, start, total, params, fps, ops,
+                           skeys, sfps, sops, pos, flags);
         return hipGetLastError();
     }
 
@@ -1668,17 +1740,22 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
     return hipGetLastError();
 }
 
-uint32_t search_table_bits(uint64_t n) {
+uint32_t search_table_bits(uint64_t n, bool base) {
     const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
+    // the base run: ~one sample per bucket (a table line, then one or two lines of keys: no
+    // sample line); a delta run (rebuilt every batch): ~8 samples (one line of them) per bucket
+    const uint64_t per = base ? 1 : 8;
+    const uint32_t cap = base ? 25 : 24;
     uint32_t b = 0;
-    while ((1ull << b) * 8 < ns2 && b < 24) b++;  // ~8 samples (one line) per bucket
+    while ((1ull << b) * per < ns2 && b < cap) b++;
     return b;
 }
 
-hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st) {
+hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st,
+                               bool base) {
     const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
     if (ns2 == 0) return hipSuccess;
-    const uint32_t bits = search_table_bits(n);
+    const uint32_t bits = search_table_bits(n, base);
     hipLaunchKernelGGL(k_search_table, g1(ns2 + 1), dim3(256), 0, st, smp2, ns2, bits, tab, par);
     return hipGetLastError();
 }

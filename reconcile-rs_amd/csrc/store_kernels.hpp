@@ -82,13 +82,17 @@ struct SearchTable {
     uint32_t bits = 0;
 };
 // table size for a run of n rows, and its build from the run's second-level samples
-uint32_t search_table_bits(uint64_t n);
-hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st);
+// (base: the base run's fine table, ~1 sample per bucket; otherwise a delta run's, ~8)
+uint32_t search_table_bits(uint64_t n, bool base = true);
+hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st,
+                               bool base = true);
 
 // Key-type-specialised device operations of the store.
 struct StoreKeyOps {
     virtual ~StoreKeyOps() = default;
-    // sort a batch by key (stable) and gather keys / fingerprints / ops into key order.
+    // sort a batch by key (stable) and gather keys / fingerprints / ops into key order; with
+    // fps == nullptr, pos[input row] = its sorted row instead (exactly one of fps / pos given),
+    // for the batch path's lift, which runs after the sort and writes each fingerprint in place.
     // full = false: coarse buckets of the most significant u64 digit + a sort of each bucket in
     // LDS (ties on that digit broken by the whole key); *flags |= 4 if the digits are too skewed
     // for the buckets, and (multi-digit keys past the bucket path's size) |= 2 if two keys share
@@ -97,7 +101,7 @@ struct StoreKeyOps {
     // order) by the sort itself.
     virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
                                   Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags,
-                                  bool full, hipStream_t st) = 0;
+                                  bool full, hipStream_t st, uint32_t *pos = nullptr) = 0;
     // lower-bound rank of each query key (and whether it is present)
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <chrono>
@@ -209,6 +210,24 @@ hipError_t launch_lift_schema(int kk, int kl, int vk, int vl, int rk, bool tags,
 #define X(name, KK, KL, VK, VL)                                                                   \
     if (kk == KK && kl == KL && vk == VK && vl == VL)                                            \
         return launch_lift_##name(rk, tags, dual, c, n, fps, bsums, fps2, bsums2, st);
+#include "schemas.def"
+#undef X
+    *supported = false;
+    return hipSuccess;
+}
+
+#define X(name, kk, kl, vk, vl)                                                                               \
+    hipError_t launch_lift_search_##name(int rk, bool tags, const DevCols &c, uint64_t n, uint8_t *fps,          \
+                                         const uint8_t *q, const SearchJob &jb, const SearchJob &jd, hipStream_t st, \
+                                         bool *supported);
+#include "schemas.def"
+#undef X
+
+hipError_t launch_lift_search_schema(int kk, int kl, int vk, int vl, int rk, bool tags, const DevCols &c, uint64_t n,
+                                     uint8_t *fps, const uint8_t *q, const SearchJob &jb, const SearchJob &jd,
+                                     hipStream_t st, bool *supported) {
+#define X(name, KK, KL, VK, VL) \
+    if (kk == KK && kl == KL && vk == VK && vl == VL) return launch_lift_search_##name(rk, tags, c, n, fps, q, jb, jd, st, supported);
 #include "schemas.def"
 #undef X
     *supported = false;
@@ -1165,8 +1184,8 @@ struct rh_store {
         RH_HIP(hipEventSynchronize(ev));
         return RH_OK;
     }
-    // k batches in order, each exactly as apply_device would apply it; batch i + 1 is sorted and
-    // lifted while the host waits for batch i's result, so the device does not idle between
+    // k batches in order, each exactly as apply_device would apply it; batch i + 1 is sorted
+    // while the host waits for batch i's result, so the device does not idle between
     // batches.  On an error, batches before the failing one stay applied, the failing one and
     // those after it are not.
     int apply_device_many(const rh_columns *cs, const uint8_t *const *ops, const size_t *ms, size_t k, uint64_t *out) {
@@ -1201,10 +1220,10 @@ struct rh_store {
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         return RH_OK;
     }
-    // Steps 1-2 of a batch: the key sort (sorted keys / ops into skeys / sops, each input row's
-    // sorted row into the position scratch, the sort's flags into the result block), then the lift,
-    // which writes each fingerprint straight to its sorted row of sfps -- the sort gathers no
-    // fingerprints.  Queued only; needs batch_buffers(m).
+    // Step 1 of a batch: the key sort (sorted keys / ops into skeys / sops, each input row's sorted
+    // row into the position scratch, the sort's flags into the result block).  Queued only; needs
+    // batch_buffers(m).  The lift comes after it (step 2), writing each fingerprint straight to
+    // its sorted row of sfps, so the sort gathers no fingerprints.
     int prepare_batch(const rh_columns &c, const uint8_t *ops, size_t m, bool full) {
         uint32_t *pos = scratch.u32(7, m);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
@@ -1212,11 +1231,36 @@ struct rh_store {
         RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), nullptr, ops, m, scratch, skeys.p, nullptr, sops.p,
                                 r_flags, full, stream, pos));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        return lift_dispatch(schema, c, m, sfps.p, nullptr, nullptr, nullptr, false, stream, pos);
+        return RH_OK;
     }
+    // Steps 2-3: the lift into the sorted rows and the searches of the sorted keys in the base and
+    // delta runs, as one fused launch (lift_search.hpp) -- or, for a shape without one, the lift
+    // and the two search kernels.
+    int lift_and_search(const rh_columns &c, size_t m, const rh::SearchJob &jb, const rh::SearchJob &jd) {
+        const uint32_t *pos = scratch.u32(7, m);
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        if (fused_lift_search) {
+            rh::DevCols dc = to_dev(c);
+            dc.dst = pos;
+            bool supported = false;
+            const hipError_t e =
+                rh::launch_lift_search_schema(schema.key_kind, (int)schema.key_len, schema.value_kind, (int)schema.value_len,
+                                              schema.record_kind, c.tags != nullptr, dc, m, sfps.p, skeys.p, jb, jd,
+                                              stream, &supported);
+            if (e != hipSuccess) return fail(RH_ERR_HIP, std::string("lift + search launch: ") + hipGetErrorString(e));
+            if (supported) return RH_OK;
+        }
+        int rc;
+        if ((rc = lift_dispatch(schema, c, m, sfps.p, nullptr, nullptr, nullptr, false, stream, pos))) return rc;
+        RH_HIP(kops->search_sampled(jb.keys, jb.n, jb.smp, jb.smp2, skeys.p, m, jb.rank, jb.present, stream, jb.tb));
+        RH_HIP(kops->search_sampled(jd.keys, jd.n, jd.smp, jd.smp2, skeys.p, m, jd.rank, jd.present, stream, jd.tb));
+        return RH_OK;
+    }
+    // A/B switch: RSOS_HIP_UNFUSED set (non-empty) = separate lift / search launches
+    bool fused_lift_search = !(getenv("RSOS_HIP_UNFUSED") && *getenv("RSOS_HIP_UNFUSED"));
     PinnedVec<uint64_t> res_host;  // the batch's 96-byte result block
-    // prepared: steps 1-2 of this batch were queued by the previous call (apply_device_many).
-    // next: a batch whose steps 1-2 are queued once this batch's kernels are -- the device runs them
+    // prepared: step 1 of this batch was queued by the previous call (apply_device_many).
+    // next: a batch whose step 1 is queued once this batch's kernels are -- the device runs them
     // while the host waits for this batch's result (an event on the result copy, not the stream);
     // *next_prepared says whether they were (a re-sort of this batch overwrites them).
     int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3], bool prepared = false,
@@ -1230,9 +1274,9 @@ struct rh_store {
         const int fmode = fold_mode();  // how this batch reaches a fresh host tier
         version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
         if ((rc = batch_buffers(m))) return rc;
-        // 1-2. key sort, lift into the sorted rows (delete rows are lifted too and ignored)
+        // 1. key sort (queued by the previous call when prepared)
         if (!prepared && (rc = prepare_batch(c, ops, m, false))) return rc;
-        // 3-5 run without a host round trip: everything is written to the delta run's *other*
+        // 2-5 run without a host round trip: everything is written to the delta run's *other*
         // buffers, and one sync at the end brings back the flags and counts.  A duplicate key
         // then leaves the store exactly as it was (nothing is committed); a tie on the leading
         // key digit re-runs the steps with the full sort.
@@ -1272,22 +1316,23 @@ struct rh_store {
         uint32_t flags = 0;
         int next_rc = RH_OK;
         for (int full = 0; full < 2; full++) {
-            // 1-2 again with the full sort (the bucket sort's order was not final)
+            // 1 again with the full sort (the bucket sort's order was not final)
             if (full == 1 && (rc = prepare_batch(c, ops, m, true))) return rc;
-            // 3. where each key is now: base and delta runs
-            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, skeys.p, m, rank_b, present_b, stream,
-                                        base_table()));
-            // a delta run of more than a few blocks is searched through a table over its stride-8
-            // samples too (one L2-resident table line instead of a binary search of the stride-256
-            // samples); the table is built here, where the run's row count is known on the host
+            // 2-3. the lift, and where each key is now (base and delta runs).  A delta run of more
+            // than a few blocks is searched through a table over its stride-8 samples (one
+            // L2-resident table line instead of a binary search of the stride-256 samples); the
+            // table is built here, where the run's row count is known on the host
             rh::SearchTable dt{};
             if (nd >= DTAB_MIN) {
                 if ((rc = dtab.ensure((1ull << rh::search_table_bits(nd, false)) + 2)) || (rc = dtabp.ensure(2))) return rc;
                 if (full == 0) RH_HIP(rh::launch_search_table(dsmp2[cd].p, nd, dtab.p, dtabp.p, stream, false));
                 dt = rh::SearchTable{dtab.p, dtabp.p, rh::search_table_bits(nd, false)};
             }
-            RH_HIP(kops->search_sampled(dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, skeys.p, m, rank_d, present_d,
-                                        stream, dt));
+            rh::SearchJob jb{bkeys[cb].p, nb, bsmp.p, bsmp2.p, base_table(), rank_b, present_b};
+            rh::SearchJob jd{dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, dt, rank_d, present_d};
+            if (!jb.smp2 || nb == 0) jb.tb = rh::SearchTable{};
+            if (!jd.smp2 || nd == 0) jd.tb = rh::SearchTable{};
+            if ((rc = lift_and_search(c, m, jb, jd))) return rc;
             // 4. the batch's delta records and counts, merged into the delta run's other buffer
             //    (one pass: the merged run, its block sums, count prefixes and search samples)
             RH_HIP(rh::launch_delta_apply(schema.key_kind, (int)kl, sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p,
@@ -1316,7 +1361,7 @@ struct rh_store {
             }
             memcpy(&flags, &host[6], 4);
             if (!(flags & 6)) break;  // 2: leading-digit tie, 4: skewed buckets
-            if (next_prepared) *next_prepared = false;  // the re-sort overwrites the next batch's steps 1-2
+            if (next_prepared) *next_prepared = false;  // the re-sort overwrites the next batch's step 1
         }
         int64_t dcnt;
         memcpy(&dcnt, &host[7], 8);
@@ -2250,6 +2295,9 @@ int snapshot_reload_fused(rh_store *dated, rh_store *proj, int mode, const rh::S
     for (rh_store *x : {dated, proj})
         if (x && (rc = x->load_stage_sums(n, a->flag.p, x->stream))) return rc;
     if ((rc = a->sync())) return rc;
+    // the projection store's staged copy of the unsorted flag (a->flag) must land before the dated
+    // store's re-sort in load_finish reuses that flag word for its sort flags
+    if (mode == 2 && (rc = proj->sync())) return rc;
     if (ev[2]) {
         float ms[2] = {0, 0};
         RH_HIP(hipEventElapsedTime(&ms[0], ev[0], ev[1]));

@@ -81,6 +81,16 @@ struct SearchTable {
     const uint64_t *par = nullptr;
     uint32_t bits = 0;
 };
+// one sampled search over a sorted run (k_search_sampled; the batch path's fused lift + search,
+// lift_search.hpp): the lower-bound rank and presence of each query key
+struct SearchJob {
+    const uint8_t *keys;
+    uint64_t n;
+    const uint64_t *smp, *smp2;
+    SearchTable tb;
+    uint32_t *rank;
+    uint8_t *present;
+};
 // table size for a run of n rows, and its build from the run's second-level samples
 // (base: the base run's fine table, ~1 sample per bucket; otherwise a delta run's, ~8)
 uint32_t search_table_bits(uint64_t n, bool base = true);

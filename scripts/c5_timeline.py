@@ -4,7 +4,11 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-lifts = [i for i, r in enumerate(rows) if "k_lift<" in r["Kernel_Name"] and int(r["Grid_Size_X"]) < 2_000_000]
+# a batch starts at its key sort (round 3 on: the sort runs before the lift, queued behind the
+# previous batch's result copy); older traces start it at the lift
+mark = "k_cs_minmax<" if any("k_cs_minmax<" in r["Kernel_Name"] for r in rows) and any(
+    "k_lift_search<" in r["Kernel_Name"] for r in rows) else "k_lift<"
+lifts = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"] and int(r["Grid_Size_X"]) < 2_000_000]
 batches = [int(b) for b in sys.argv[2:]] or [len(lifts) - 3]
 for b in batches:
     i0, i1 = lifts[b], lifts[b + 1]

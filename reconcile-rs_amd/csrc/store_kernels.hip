@@ -149,19 +149,22 @@ __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t 
 // a bucket index B = (d - min) >> shift of CB + 8 bits (shift chosen from the batch's digit
 // range, so random and dense key ranges both spread): the high CB bits pick one of C = 2^CB
 // coarse buckets (~1,000 keys each), the low 8 bits a fine bucket inside it.
-//   k_cs_minmax      per-workgroup digit min / max; the last workgroup folds them to (min, shift)
+//   k_cs_minmax      per-workgroup digit min / max (every later kernel folds the partials)
 //   k_cs_hist        per-workgroup coarse histograms
-//   k_cs_colscan     each workgroup's offset inside each coarse bucket, and the bucket totals
-//   k_cs_bucketscan  the buckets' starts (and (min, shift) once); *flags |= 4 if one is larger
-//                    than CS_CAP
-//   k_cs_scatter     (digit, row) pairs into coarse-bucket order
+//   k_cs_colscan     each workgroup's offset inside each coarse bucket and the bucket totals;
+//                    its last workgroup scans the totals into the buckets' starts (and (min,
+//                    shift) once); *flags |= 4 if a bucket is larger than CS_CAP
+//   k_cs_scatter     (whole key, row) pairs into coarse-bucket order
 //   k_cs_sort        one workgroup per coarse bucket: fine buckets in LDS, each key ranked inside
 //                    its fine bucket by (digit, whole key, row) -- so the result is the stable
-//                    sort by key -- then key / fingerprint / op gathered into place
+//                    sort by key -- then the keys and ops written in order from the bucket's
+//                    stretch, and either each row's sorted position (the batch path: the lift
+//                    runs after the sort and writes each fingerprint in place) or the
+//                    fingerprints gathered into place (a load)
 // The per-key passes use 8,192-key workgroups of 1,024 lanes (8 keys per lane, loads issued
 // together); an earlier form with 16 K buckets (a 16 MB histogram matrix) and one wave per
 // ~61-key bucket gathering 16- and 32-byte rows from random input rows took 139 us per 1 M
-// batch, this one ~60 (profiles/r02_config5_*).
+// batch, the round-2 form (digits scattered, keys and fingerprints gathered) ~93, this one ~65.
 constexpr int CS_TILE = 8192, CS_WG = 1024;         // keys / lanes per minmax / hist / scatter workgroup
 constexpr int CS_FINE_BITS = 8, CS_FINE = 1 << CS_FINE_BITS;
 constexpr int CS_CAP = 2048;                        // largest coarse bucket ordered in LDS
@@ -189,8 +192,12 @@ __device__ __forceinline__ void minmax_block(uint64_t &a, uint64_t &b, uint64_t 
 }
 
 template <int KK, int KL>
-__global__ __launch_bounds__(CS_WG) void k_cs_minmax(const uint8_t *keys, uint64_t m, uint64_t *part, uint32_t *flags) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *flags = 0;  // the sort's first launch: no memset of its own
+__global__ __launch_bounds__(CS_WG) void k_cs_minmax(const uint8_t *keys, uint64_t m, uint64_t *part, uint32_t *flags,
+                                                     uint32_t *ticket) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the sort's first launch: no memsets of its own
+        *flags = 0;
+        *ticket = 0;
+    }
     __shared__ uint64_t lo[CS_WG / 64], hi[CS_WG / 64];
     uint64_t a = ~0ull, b = 0;
     const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
@@ -254,10 +261,17 @@ __global__ __launch_bounds__(CS_WG) void k_cs_hist(const uint8_t *keys, uint64_t
 // per coarse bucket: each workgroup's running offset within the bucket (in place), and the
 // total.  64 buckets per workgroup (one per lane of a wave, so the row reads are coalesced),
 // 16 lanes per bucket: lane q sums a sixteenth of the rows, the parts' sums are exchanged in LDS,
-// then each lane writes its part's offsets.
-__global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nwg, uint32_t C, uint32_t *total) {
+// then each lane writes its part's offsets.  The last workgroup to finish (an agent-scope ticket
+// after agent-scope stores of the totals; MI355X_MICROARCH.md, inter-workgroup visibility) then
+// scans the C totals into the buckets' starts (C <= 4 * 1024) and folds the minmax partials once
+// into params = (min, shift) for the scatter and the bucket sorts: one launch where the column
+// scan and the bucket scan were two.  *ticket: 0 on entry (k_cs_minmax zeroes it).
+__global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nwg, uint32_t C, uint32_t *total,
+                                                     uint32_t *ticket, uint32_t *start, uint32_t *flags,
+                                                     const uint64_t *part_mm, uint32_t bbits, uint64_t *params) {
     constexpr uint32_t Q = 16;
     __shared__ uint32_t part[Q][64];
+    __shared__ uint32_t last;
     const uint32_t lb = threadIdx.x & 63, qt = threadIdx.x >> 6, b = blockIdx.x * 64 + lb;
     const bool live = b < C;
     const uint32_t per = (nwg + Q - 1) / Q, w0 = qt * per < nwg ? qt * per : nwg, w1 = w0 + per < nwg ? w0 + per : nwg;
@@ -268,35 +282,38 @@ __global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nw
     __syncthreads();
     uint32_t run = 0;
     for (uint32_t q = 0; q < qt; q++) run += part[q][lb];
-    if (!live) return;
-    if (qt == Q - 1) total[b] = run + sum;
-    for (uint32_t w = w0; w < w1; w++) {
-        const uint32_t v = hist[(uint64_t)w * C + b];
-        hist[(uint64_t)w * C + b] = run;
-        run += v;
+    if (live) {
+        if (qt == Q - 1) __hip_atomic_store(total + b, run + sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t w = w0; w < w1; w++) {
+            const uint32_t v = hist[(uint64_t)w * C + b];
+            hist[(uint64_t)w * C + b] = run;
+            run += v;
+        }
     }
-}
-
-// exclusive scan of the C bucket totals (one workgroup of 1024; C <= 4 * 1024); also folds the
-// minmax partials once into params = (min, shift) for the scatter and the bucket sorts
-__global__ __launch_bounds__(1024) void k_cs_bucketscan(const uint32_t *total, uint32_t C, uint32_t *start,
-                                                        uint32_t *flags, const uint64_t *part, uint32_t nwg,
-                                                        uint32_t bbits, uint64_t *params) {
-    __shared__ uint32_t w[16];
-    const uint32_t t = threadIdx.x, per = (C + 1023) / 1024;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u
+                                                                                                              : 0u;
+    __syncthreads();
+    if (!last) return;  // uniform
+    // the bucket scan (exclusive, over the C totals)
+    __shared__ uint32_t ws[16];
+    const uint32_t t = threadIdx.x, pc = (C + 1023) / 1024;
     uint64_t mn;
     uint32_t sh;
-    cs_params(part, nwg, bbits, &mn, &sh);
+    cs_params(part_mm, nwg, bbits, &mn, &sh);
     if (t == 0) {
         params[0] = mn;
         params[1] = sh;
+        *ticket = 0u;
     }
     uint32_t v[4] = {0, 0, 0, 0}, s = 0;
     bool big = false;
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
-        if (k < per && per * t + k < C) {
-            v[k] = total[per * t + k];
+        if (k < pc && pc * t + k < C) {
+            v[k] = __hip_atomic_load(total + pc * t + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             big |= v[k] > (uint32_t)CS_CAP;
             s += v[k];
         }
@@ -307,15 +324,15 @@ __global__ __launch_bounds__(1024) void k_cs_bucketscan(const uint32_t *total, u
         const uint32_t y = __shfl_up(x, o, 64);
         if ((t & 63) >= (uint32_t)o) x += y;
     }
-    if ((t & 63) == 63) w[t >> 6] = x;
+    if ((t & 63) == 63) ws[t >> 6] = x;
     __syncthreads();
-    uint32_t run = x - s;
-    for (uint32_t q = 0; q < (t >> 6); q++) run += w[q];
+    uint32_t r = x - s;
+    for (uint32_t q = 0; q < (t >> 6); q++) r += ws[q];
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
-        if (k < per && per * t + k < C) {
-            start[per * t + k] = run;
-            run += v[k];
+        if (k < pc && pc * t + k < C) {
+            start[pc * t + k] = r;
+            r += v[k];
         }
     }
     if (__ballot(big) && (t & 63) == 0) atomicOr(flags, 4u);
@@ -460,7 +477,7 @@ __global__ __launch_bounds__(256) void k_cs_sort(const uint8_t *okey, const uint
     static_assert(CS_CAP <= 65536, "16-bit slots");
     __shared__ uint32_t fst[CS_FINE], fcur[CS_FINE], wsum[4];
     const uint32_t b = blockIdx.x, t = threadIdx.x, n = total[b], s0 = start[b];
-    if (n == 0 || n > (uint32_t)CS_CAP) return;  // uniform; too large: flagged by k_cs_bucketscan
+    if (n == 0 || n > (uint32_t)CS_CAP) return;  // uniform; too large: flagged by k_cs_colscan
     const uint64_t mn = params[0], sh = params[1];
     const uint8_t *bk = okey + (uint64_t)s0 * KL;
     uint64_t d[PER];
@@ -1500,16 +1517,17 @@ struct KeyOps final : StoreKeyOps {
         uint32_t cb = 0;
         while ((1ull << cb) * 1024 < m) cb++;  // ~1,000 keys per coarse bucket
         const uint32_t C = 1u << cb, nwg = (uint32_t)((m + CS_TILE - 1) / CS_TILE), bbits = cb + CS_FINE_BITS;
-        uint64_t *part = s.u64(2, 2ull * nwg + 2);
+        uint64_t *part = s.u64(2, 2ull * nwg + 3);
         uint8_t *okey = reinterpret_cast<uint8_t *>(s.u64(0, (m * KL + 7) / 8));
         uint32_t *hist = s.u32(15, (uint64_t)nwg * C), *idx = s.u32(0, m), *total = s.u32(1, C);
         uint32_t *start = s.u32(2, C);
         if (s.err) return s.err;
         uint64_t *params = part + 2ull * nwg;
-        hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, flags);
+        uint32_t *ticket = reinterpret_cast<uint32_t *>(part + 2ull * nwg + 2);
+        hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, flags, ticket);
         hipLaunchKernelGGL((k_cs_hist<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, nwg, bbits, C, hist);
-        hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(1024), 0, st, hist, nwg, C, total);
-        hipLaunchKernelGGL(k_cs_bucketscan, dim3(1), dim3(1024), 0, st, total, C, start, flags, part, nwg, bbits, params);
+        hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(1024), 0, st, hist, nwg, C, total, ticket, start,
+                           flags, part, bbits, params);
         hipLaunchKernelGGL((k_cs_scatter<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, params, C, hist, start,
                            okey, idx);
         hipLaunchKernelGGL((k_cs_sort<KK, KL>), dim3(C), dim3(256), 0, st, okey, idx, start, total, params, fps, ops,
@@ -1665,7 +1683,9 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
 uint32_t search_table_bits(uint64_t n, bool base) {
     const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
     // the base run: ~one sample per bucket (a table line, then one or two lines of keys: no
-    // sample line); a delta run (rebuilt every batch): ~8 samples (one line of them) per bucket
+    // sample line); a delta run (rebuilt every batch): ~8 samples (one line of them) per bucket,
+    // a table small enough to stay in the caches -- one sample per bucket there measured slower
+    // (profiles/r03s2_c5_fine_dtab_ab.txt)
     const uint64_t per = base ? 1 : 8;
     const uint32_t cap = base ? 25 : 24;
     uint32_t b = 0;

@@ -96,7 +96,7 @@ def parse():
     p.add_argument("--batch", type=int, default=1_000_000, help="config5: records per update batch")
     p.add_argument("--pipeline", type=int, default=1,
                    help="config5: 1 = the timed batches through one apply_device_many call (batch i + 1 "
-                        "lifted while batch i's result returns); 0 = one apply_device call per batch")
+                        "key-sorted while batch i's result returns); 0 = one apply_device call per batch")
     p.add_argument("--compact-div", type=int, default=0,
                    help="config5: compaction divisor (the delta run merges into the base past base / divisor rows; "
                         "0 = the library's default)")
@@ -559,10 +559,11 @@ def incremental(args, world, rank, dev, dist):
             "dist": {"backend": (dist.get_backend() if dist is not None else None), "world_size": world},
             "batch_counts": {"new": counts[0], "overwritten": counts[1], "deleted": counts[2]},
             "root_size": root_size, "bulk_load_s": round(load_s, 3),
-            "step": ("apply_device_many over the K queued batches (each: lift + sort + base/delta search + "
-                     "delta merge, amortised compaction; the next batch lifted while this one's result "
+            "step": ("apply_device_many over the K queued batches (each: key sort, lift fused with the "
+                     "base/delta searches, delta records + merge, amortised compaction; the next batch key-sorted while this one's result "
                      "returns) + the whole map's root" if args.pipeline else
-                     "apply_device per batch (lift + sort + base/delta search + delta merge; amortised "
+                     "apply_device per batch (key sort, lift fused with the base/delta searches, delta "
+                     "records + merge; amortised "
                      "compaction) + the whole map's root after each"),
             "compactions_in_timed_steps": stats["compactions"] - comp0, "delta_rows_at_end": stats["delta_rows"],
             "reserved_rows": reserved, "compaction_divisor": args.compact_div or 6,

@@ -303,7 +303,7 @@ int rh_store_apply_device(rh_store *store, const rh_columns *dev_cols, const uin
                           uint64_t *n_new, uint64_t *n_overwritten, uint64_t *n_deleted, void *after_stream);
 /* k device batches applied in order, each exactly as rh_store_apply_device would apply it
  * (dev_ops: k pointers, or NULL for all-insert batches; an entry may be NULL too).  Batch i + 1
- * is lifted while the host waits for batch i's result, so queued batches keep the device busy
+ * is key-sorted while the host waits for batch i's result, so queued batches keep the device busy
  * (a replica's write path draining several received batches).  counts (nullable): 3 per batch,
  * new / overwritten / deleted.  On an error the batches before the failing one stay applied.   */
 int rh_store_apply_device_many(rh_store *store, const rh_columns *dev_cols, const uint8_t *const *dev_ops,

@@ -134,8 +134,8 @@ class GpuFingerprintStore:
         return int(a.value), int(b.value), int(d.value)
 
     def apply_device_many(self, batches, ops=None) -> List[Tuple[int, int, int]]:
-        """apply_device over several device batches in order, in one call: batch i + 1 is lifted
-        while the host waits for batch i's result (rh_store_apply_device_many).  ops: None or one
+        """apply_device over several device batches in order, in one call: batch i + 1 is
+        key-sorted while the host waits for batch i's result (rh_store_apply_device_many).  ops: None or one
         entry (None or m device bytes) per batch.  Returns (new, overwritten, deleted) per batch."""
         from .device import _check_cols, _columns
         k = len(batches)

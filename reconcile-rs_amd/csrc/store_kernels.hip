@@ -19,6 +19,7 @@
 // batch's DeltaRecs, merge them into the delta run (O(m + nD), one pass that also writes the
 // run's sums); when the delta run passes nB / 8 it is merged into the base the same way
 // (O(nB)) -- amortised, and on demand before rank / select.
+#include <cstdlib>
 #include <type_traits>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -986,6 +987,20 @@ __global__ __launch_bounds__(DB_WG) void k_delta_lists(const uint8_t *dops, cons
     if (pr) rlist[R] = rank[j];
 }
 
+constexpr int MT = 2048;  // output rows per workgroup (8 blocks of 256; 2,048 measured best of 1,024 / 2,048 / 4,096)
+
+// The merge's tiles' bounds in the upsert list, formed once per merge instead of searched by every
+// tile: tileU[t] = the upserts placed before output row t * MT, for t in [0, tiles].  Thread U
+// writes the tiles that start after upsert U - 1's row and at or before upsert U's (thread U of U
+// upserts: the tiles after the last one); upos is strictly increasing.
+__global__ void k_tile_bounds(const uint32_t *upos, const uint64_t *counts, uint64_t m, uint64_t tiles, uint32_t *tileU) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, U = counts[3];
+    if (j > U || j > m) return;
+    const uint64_t lo = j == 0 ? 0 : (uint64_t)upos[j - 1] / MT + 1;
+    const uint64_t hi = j < U ? (uint64_t)upos[j] / MT : tiles;
+    for (uint64_t t = lo; t <= hi && t <= tiles; t++) tileU[t] = (uint32_t)j;
+}
+
 // compaction input: cur fp = contrib + base fp, op = live ? upsert : delete, and the key's
 // place in the base (no search: brank was recorded when the entry was built); plus the
 // per-1024-row partials of k_delta_parts (slots 3 upserts, 4 keys the base holds, 5 both)
@@ -1247,7 +1262,7 @@ __global__ void k_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *
 // block sums of the payload's leading fingerprint -- and, for the delta run, each block's
 // count-delta total and every row's in-block count prefix.  This replaces a row-move pass, a
 // batch-scatter pass and a re-read of the whole run for its sums.
-constexpr int MT = 2048;  // output rows per workgroup (8 blocks of 256; 2,048 measured best of 1,024 / 2,048 / 4,096)
+// (MT, the output rows per workgroup: with k_tile_bounds above)
 
 // The first index in [lo, hi) whose predicate holds (hi if none), for a predicate that is false
 // then true along the range, searched by one whole wave: each step probes 64 evenly spaced
@@ -1293,7 +1308,7 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
                                                    const uint64_t *counts, uint8_t *okeys, uint8_t *opay,
                                                    uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
                                                    uint64_t *osmp, uint64_t *osmp2, const uint8_t *heap,
-                                                   uint32_t heap_base) {
+                                                   uint32_t heap_base, const uint32_t *tileU) {
     static_assert(HEAP ? (P == 4 && COUNTS) : (P % 8 == 0 && P >= 32), "payload: a slot, or a leading fingerprint");
     using V = typename std::conditional<P % 16 == 0, uint4, uint2>::type;  // widest aligned unit
     constexpr int NV = P / (int)sizeof(V) > 0 ? P / (int)sizeof(V) : 1;
@@ -1311,8 +1326,13 @@ __global__ __launch_bounds__(256) void k_merge_run(const uint8_t *akeys, const u
         uint64_t o1 = o0, ju0 = 0, ju1 = 0, s0 = 0, k0 = 0, k1 = 0;
         if (o0 < nC) {
             o1 = o0 + MT < nC ? o0 + MT : nC;
-            ju0 = wave_partition_point(0, U, [&](uint64_t i) { return (uint64_t)upos[i] >= o0; });
-            ju1 = wave_partition_point(ju0, U, [&](uint64_t i) { return (uint64_t)upos[i] >= o1; });
+            if (tileU) {  // k_tile_bounds (the last tile's end: every upsert lies before nC)
+                ju0 = tileU[blockIdx.x];
+                ju1 = o1 == nC ? U : tileU[blockIdx.x + 1];
+            } else {
+                ju0 = wave_partition_point(0, U, [&](uint64_t i) { return (uint64_t)upos[i] >= o0; });
+                ju1 = wave_partition_point(ju0, U, [&](uint64_t i) { return (uint64_t)upos[i] >= o1; });
+            }
             s0 = o0 >= ju0 ? o0 - ju0 : 0;
             const uint64_t s1 = o1 >= ju1 ? o1 - ju1 : 0;
             // survivor_k's predicate: k == R or rlist[k] - k > s, over k in [lo, R]
@@ -1437,12 +1457,12 @@ hipError_t merge_kernel_t(const uint8_t *akeys, const uint8_t *apay, uint64_t nA
                           const uint8_t *bpay, uint64_t m, const uint32_t *upos, const uint32_t *usrc,
                           const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys, uint8_t *opay, uint8_t *obs,
                           int32_t *ocnt, int16_t *oinb, uint64_t nbk, uint64_t *osmp, uint64_t *osmp2, hipStream_t st,
-                          const uint8_t *heap = nullptr, uint32_t heap_base = 0) {
+                          const uint8_t *heap = nullptr, uint32_t heap_base = 0, const uint32_t *tileU = nullptr) {
     const uint64_t tiles = (nA + m + MT - 1) / MT;
     if (tiles)
         hipLaunchKernelGGL((k_merge_run<KK, KL, P, COUNTS, HEAP>), dim3((uint32_t)tiles), dim3(256), 0, st, akeys,
                            apay, nA, bkeys, bpay, m, upos, usrc, rlist, counts, okeys, opay, obs, ocnt, oinb, nbk, osmp,
-                           osmp2, heap, heap_base);
+                           osmp2, heap, heap_base, tileU);
     return hipGetLastError();
 }
 
@@ -1453,17 +1473,18 @@ hipError_t launch_merge_kernel(int kk, int kl, int payload, const uint8_t *akeys
                                const uint32_t *usrc, const uint32_t *rlist, const uint64_t *counts, uint8_t *okeys,
                                uint8_t *opay, uint8_t *obs, int32_t *ocnt, int16_t *oinb, uint64_t nbk,
                                uint64_t *osmp, uint64_t *osmp2, hipStream_t st, const uint8_t *heap = nullptr,
-                               uint32_t heap_base = 0) {
+                               uint32_t heap_base = 0, const uint32_t *tileU = nullptr) {
     if (osmp && !osmp2) return hipErrorInvalidValue;
 #define RH_MK(KKV, KLV)                                                                                            \
     if (kk == KKV && kl == KLV) {                                                                                  \
         if (payload == 32)                                                                                         \
             return merge_kernel_t<KKV, KLV, 32, false>(akeys, apay, nA, bkeys, bpay, m, upos, usrc, rlist, counts,  \
-                                                       okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2, st);        \
+                                                       okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2, st,         \
+                                                       nullptr, 0, tileU);                                         \
         if (payload == 4 && heap)                                                                                  \
             return merge_kernel_t<KKV, KLV, 4, true, true>(akeys, apay, nA, bkeys, bpay, m, upos, usrc, rlist,     \
                                                            counts, okeys, opay, obs, ocnt, oinb, nbk, osmp, osmp2,  \
-                                                           st, heap, heap_base);                                   \
+                                                           st, heap, heap_base, tileU);                            \
     }
     RH_MK(KEY_U32, 4) RH_MK(KEY_U64, 8) RH_MK(KEY_BYTES, 8) RH_MK(KEY_BYTES, 16) RH_MK(KEY_BYTES, 32)
 #undef RH_MK
@@ -1620,6 +1641,22 @@ StoreKeyOps *store_key_ops(int kk, int kl) {
 
 // ---- delta launchers (key-type independent) -------------------------------------------------
 
+// k_tile_bounds for a merge of m rows into a run (nA + m rows at most), into scratch slot u32(8);
+// nullptr (the merge searches its bounds itself) when switched off for an A/B
+static uint32_t *merge_tile_bounds(const uint32_t *upos, const uint64_t *counts, uint64_t m, uint64_t rows, Scratch &s,
+                                   hipStream_t st) {
+    static const bool off = getenv("RSOS_HIP_TILE_SEARCH") && *getenv("RSOS_HIP_TILE_SEARCH") == '1';
+    if (off) return nullptr;
+    const uint64_t tiles = (rows + MT - 1) / MT;
+    // a thread fills the tiles between two upserts: with few upserts per tile on average (a tiny
+    // batch into a large run) the tiles search their bounds themselves
+    if (tiles > 16 * (m + 1)) return nullptr;
+    uint32_t *tileU = s.u32(8, tiles + 1);
+    if (!tileU) return nullptr;
+    hipLaunchKernelGGL(k_tile_bounds, g1(m + 1), dim3(256), 0, st, upos, counts, m, tiles, tileU);
+    return tileU;
+}
+
 hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t *sops, uint64_t m,
                               const uint32_t *rank_b, const uint8_t *present_b, const uint8_t *base_fps,
                               const uint32_t *rank_d, const uint8_t *present_d, const uint8_t *dkeys,
@@ -1641,9 +1678,11 @@ hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t
     hipLaunchKernelGGL(k_delta_parts, dim3(1), dim3(DP_WG), 0, st, part, G, counts3, mcnt, out3, off, dsum, dtot, dcnt);
     hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, dops, present_d, rank_d, off, m, upos,
                        usrc, rlist);
+    uint32_t *tileU = merge_tile_bounds(upos, mcnt, m, nd + m, s, st);
+    if (s.err) return s.err;
     return launch_merge_kernel(kk, kl, 4, dkeys, reinterpret_cast<const uint8_t *>(dslot), nd, skeys, nullptr, m, upos,
                                usrc, rlist, mcnt, okeys, reinterpret_cast<uint8_t *>(oslot), nullptr, nullptr, nullptr,
-                               nbk, osmp, osmp2, st, heap, (uint32_t)heap_base);
+                               nbk, osmp, osmp2, st, heap, (uint32_t)heap_base, tileU);
 }
 
 hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *bfps, uint64_t nb, const uint8_t *dkeys,
@@ -1663,8 +1702,10 @@ hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *b
                        nullptr, nullptr);
     hipLaunchKernelGGL(k_delta_lists, dim3((uint32_t)G), dim3(DB_WG), 0, st, cops, cpres, crank, off, nd, upos, usrc,
                        rlist);
+    uint32_t *tileU = merge_tile_bounds(upos, mcnt, nd, nb + nd, s, st);
+    if (s.err) return s.err;
     return launch_merge_kernel(kk, kl, 32, bkeys, bfps, nb, dkeys, cfps, nd, upos, usrc, rlist, mcnt, okeys, ofps, obs,
-                               nullptr, nullptr, nbk, osmp, osmp2, st);
+                               nullptr, nullptr, nbk, osmp, osmp2, st, nullptr, 0, tileU);
 }
 
 hipError_t launch_agg_merge(const uint64_t *base_agg, const uint64_t *delta_agg, const uint64_t *dlo,

@@ -12,7 +12,7 @@ timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -x -v \
   > $O/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" $O/tests.log | head -20; tail -5 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 fi
-for rep in 1 2; do for v in ${VARIANTS:-D F G}; do
+for rep in $(seq 1 ${REPS:-2}); do for v in ${VARIANTS:-D F G}; do
   # a variant's extra environment: ENV_<v>="NAME=value ..." (e.g. an A/B switch of one build)
   eval "XENV=\${ENV_$v:-}"
   env $XENV RSOS_HIP_TREE=ab/$v timeout -k 10 300 python bench.py --config config5 --cpu-baseline 0 --steps ${STEPS:-40} > $O/$v.$rep.log 2>&1 || { echo "$v failed"; tail -5 $O/$v.$rep.log; exit 1; }

@@ -1645,8 +1645,8 @@ StoreKeyOps *store_key_ops(int kk, int kl) {
 // nullptr (the merge searches its bounds itself) when switched off for an A/B
 static uint32_t *merge_tile_bounds(const uint32_t *upos, const uint64_t *counts, uint64_t m, uint64_t rows, Scratch &s,
                                    hipStream_t st) {
-    static const bool off = getenv("RSOS_HIP_TILE_SEARCH") && *getenv("RSOS_HIP_TILE_SEARCH") == '1';
-    if (off) return nullptr;
+    const char *sw = getenv("RSOS_HIP_TILE_SEARCH");  // read per merge: a test toggles it
+    if (sw && *sw == '1') return nullptr;
     const uint64_t tiles = (rows + MT - 1) / MT;
     // a thread fills the tiles between two upserts: with few upserts per tile on average (a tiny
     // batch into a large run) the tiles search their bounds themselves

@@ -1148,6 +1148,77 @@ def test_store_apply_device_many_equals_one_by_one(gpu, oracle_lib):
         st.close()
 
 
+def test_batch_path_variants_agree(gpu, oracle_lib, monkeypatch):
+    """The batch path's fused lift + search launch (k_lift_search) against the lift and the two
+    searches as separate launches (RSOS_HIP_UNFUSED=1, read when a store is created), and the
+    merges' precomputed tile bounds (k_tile_bounds) against each tile searching its own
+    (RSOS_HIP_TILE_SEARCH=1, read per merge): the same batches -- fresh keys, overwrites, deletes,
+    through apply_device and apply_device_many, across compactions -- leave every store with the
+    same counts, fingerprints, ranks and root, and that root equals the oracle's fold of the live
+    records' lifts."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.synth import make_records
+    O = oracle_lib
+    s = RecordSchema.dated("bytes16", "bytes64")
+    base = make_records(s, 200_000, seed=71)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(72)
+    bs, ops = [], []
+    for k in range(6):
+        b = make_records(s, 30_000, seed=700 + k, random_keys=True)
+        rows = torch.randperm(200_000, device="cuda", generator=g)[:4_000]
+        b["keys"][:4_000] = base["keys"][rows]  # overwrites / deletes of resident keys
+        b["phys"][:4_000] = base["phys"][rows] + 3
+        o = torch.zeros(30_000, dtype=torch.uint8, device="cuda")
+        o[:1_500] = 1
+        bs.append(b)
+        ops.append(o)
+
+    def run(unfused, tile_search, many):
+        monkeypatch.setenv("RSOS_HIP_UNFUSED", "1" if unfused else "")
+        monkeypatch.setenv("RSOS_HIP_TILE_SEARCH", "1" if tile_search else "0")
+        st = GpuFingerprintStore(s)
+        st.set_compaction(4, 40_000)
+        st.load_bulk_device(base)
+        counts = st.apply_device_many(bs, ops) if many else [st.apply_device(b, o) for b, o in zip(bs, ops)]
+        out = (counts, st.size(), st.aggregate(), st.fingerprints(), st.stats()["compactions"],
+               [st.select(r) for r in range(0, st.size(), 9_973)])
+        st.close()
+        return out
+
+    ref = run(False, False, True)
+    assert ref[4] > 0  # compactions happened
+    for variant in [(True, False, True), (False, True, True), (True, True, False), (False, False, False)]:
+        got = run(*variant)
+        assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2] and got[4] == ref[4], variant
+        assert np.array_equal(got[3], ref[3]) and got[5] == ref[5], variant
+    # the root against the oracle: Σ lift over the live records (last write wins, deletes removed)
+    live = {}
+    cols = {c: t.cpu().numpy() for c, t in base.items()}
+    for i in range(len(cols["keys"])):
+        live[cols["keys"][i].tobytes()] = (0, i)
+    for bi, (b, o) in enumerate(zip(bs, ops)):
+        bc = {c: t.cpu().numpy() for c, t in b.items()}
+        oc = o.cpu().numpy()
+        for i in range(len(bc["keys"])):
+            k = bc["keys"][i].tobytes()
+            if oc[i]:
+                live.pop(k, None)
+            else:
+                live[k] = (bi + 1, i)
+    src = [cols] + [{c: t.cpu().numpy() for c, t in b.items()} for b in bs]
+    keys = sorted(live)
+    assert len(keys) == ref[1]
+    sch = O.Schema(O.KEY_BYTES, 16, O.VAL_BYTES, 64, O.REC_DATED, 0)
+    pick = lambda name: np.stack([src[live[k][0]][name][live[k][1]] for k in keys])
+    recs = O.Records(sch, np.ascontiguousarray(pick("keys")), np.ascontiguousarray(pick("values")),
+                     np.ascontiguousarray(pick("phys")), np.ascontiguousarray(pick("logical")),
+                     np.ascontiguousarray(pick("node")), None)
+    want = recs.lift()
+    assert np.array_equal(ref[3], want)
+
+
 @pytest.mark.parametrize("n", [10_000_000, 100_000_000], ids=["10m", "100m"])
 def test_full_size_config5_100m(gpu, oracle_lib, n):
     """config5 at its stated size (BASELINE configs[4]): 100 M resident 16 B / 64 B dated records,

@@ -15,13 +15,55 @@
 
 namespace rh {
 
-// grid: 3 * ceil(n / 256) workgroups; block b lifts (b % 3 == 0) or searches the base (1) or the
-// delta run (2), for rows [256 (b / 3), +256) of the batch.  c.dst: each record's sorted row.
+// The next batch's digit min / max for its key sort (apply_device_many): where the batch path
+// already knows the next batch, the workgroups after the lift and search ones each reduce
+// MINMAX_TILE of its keys' leading digits to one (min, max) pair, which the next sort takes in
+// place of its own k_cs_minmax launch (NextMinmax, store_kernels.hpp).
+// grid: 3 * ceil(n / 256) workgroups, then ceil(nx.m / MINMAX_TILE); block b < 3 ceil(n / 256)
+// lifts (b % 3 == 0) or searches the base (1) or the delta run (2), for rows [256 (b / 3), +256)
+// of the batch; c.dst: each record's sorted row.  The blocks after them: nx's min / max partials.
 template <int KK, int KL, int VK, int VL, int RK, bool TAGS>
 __global__ __launch_bounds__(LIFT_THREADS) void k_lift_search(DevCols c, uint64_t n, uint8_t *fps, const uint8_t *q,
-                                                              SearchJob jb, SearchJob jd) {
+                                                              SearchJob jb, SearchJob jd, NextMinmax nx) {
     using L = Layout<KK, KL, VK, VL, RK>;
-    const uint32_t role = blockIdx.x % 3, t = threadIdx.x;
+    const uint32_t t = threadIdx.x;
+    const uint64_t nblk3 = 3 * ((n + LIFT_THREADS - 1) / LIFT_THREADS);
+    if (blockIdx.x >= nblk3) {  // uniform: the next batch's digit min / max
+        static_assert(MINMAX_TILE % LIFT_THREADS == 0, "whole keys per lane");
+        __shared__ uint64_t lo[LIFT_THREADS / 64], hi[LIFT_THREADS / 64];
+        const uint64_t w = blockIdx.x - nblk3, k0 = w * MINMAX_TILE;
+        uint64_t a = ~0ull, b = 0;
+#pragma unroll
+        for (int k = 0; k < (int)(MINMAX_TILE / LIFT_THREADS); k++) {
+            const uint64_t r = k0 + (uint64_t)LIFT_THREADS * k + t;
+            if (r < nx.m) {
+                const uint64_t d = key_digit<KK, KL>(nx.keys + r * KL, 0);
+                a = d < a ? d : a;
+                b = d > b ? d : b;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64);
+            a = a2 < a ? a2 : a;
+            b = b2 > b ? b2 : b;
+        }
+        if ((t & 63) == 0) {
+            lo[t >> 6] = a;
+            hi[t >> 6] = b;
+        }
+        __syncthreads();
+        if (t == 0) {
+            for (uint32_t v = 1; v < LIFT_THREADS / 64; v++) {
+                a = lo[v] < a ? lo[v] : a;
+                b = hi[v] > b ? hi[v] : b;
+            }
+            nx.part[2 * w] = a;
+            nx.part[2 * w + 1] = b;
+        }
+        return;
+    }
+    const uint32_t role = blockIdx.x % 3;
     const uint64_t b0 = (uint64_t)(blockIdx.x / 3) * LIFT_THREADS, i = b0 + t;
     if (i >= n) return;
     if (role == 0) {

@@ -218,16 +218,17 @@ hipError_t launch_lift_schema(int kk, int kl, int vk, int vl, int rk, bool tags,
 
 #define X(name, kk, kl, vk, vl)                                                                               \
     hipError_t launch_lift_search_##name(int rk, bool tags, const DevCols &c, uint64_t n, uint8_t *fps,          \
-                                         const uint8_t *q, const SearchJob &jb, const SearchJob &jd, hipStream_t st, \
-                                         bool *supported);
+                                         const uint8_t *q, const SearchJob &jb, const SearchJob &jd,             \
+                                         const NextMinmax &nx, hipStream_t st, bool *supported);
 #include "schemas.def"
 #undef X
 
 hipError_t launch_lift_search_schema(int kk, int kl, int vk, int vl, int rk, bool tags, const DevCols &c, uint64_t n,
                                      uint8_t *fps, const uint8_t *q, const SearchJob &jb, const SearchJob &jd,
-                                     hipStream_t st, bool *supported) {
-#define X(name, KK, KL, VK, VL) \
-    if (kk == KK && kl == KL && vk == VK && vl == VL) return launch_lift_search_##name(rk, tags, c, n, fps, q, jb, jd, st, supported);
+                                     const NextMinmax &nx, hipStream_t st, bool *supported) {
+#define X(name, KK, KL, VK, VL)                           \
+    if (kk == KK && kl == KL && vk == VK && vl == VL)     \
+        return launch_lift_search_##name(rk, tags, c, n, fps, q, jb, jd, nx, st, supported);
 #include "schemas.def"
 #undef X
     *supported = false;
@@ -1224,31 +1225,49 @@ struct rh_store {
     // row into the position scratch, the sort's flags into the result block).  Queued only; needs
     // batch_buffers(m).  The lift comes after it (step 2), writing each fingerprint straight to
     // its sorted row of sfps, so the sort gathers no fingerprints.
-    int prepare_batch(const rh_columns &c, const uint8_t *ops, size_t m, bool full) {
+    // pre: the keys' digit min / max partials are in the pre-minmax slot (queued by the previous
+    // batch's k_lift_search, pre_minmax)
+    int prepare_batch(const rh_columns &c, const uint8_t *ops, size_t m, bool full, bool pre = false) {
         uint32_t *pos = scratch.u32(7, m);
+        const uint32_t npart = (uint32_t)((m + rh::MINMAX_TILE - 1) / rh::MINMAX_TILE);
+        const uint64_t *part = pre ? scratch.u64(3, 2ull * npart) : nullptr;
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
         RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), nullptr, ops, m, scratch, skeys.p, nullptr, sops.p,
-                                r_flags, full, stream, pos));
+                                r_flags, full, stream, pos, part, npart));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         return RH_OK;
     }
     // Steps 2-3: the lift into the sorted rows and the searches of the sorted keys in the base and
     // delta runs, as one fused launch (lift_search.hpp) -- or, for a shape without one, the lift
     // and the two search kernels.
-    int lift_and_search(const rh_columns &c, size_t m, const rh::SearchJob &jb, const rh::SearchJob &jd) {
+    // next (nullable): the next batch, whose keys' digit min / max the fused launch also forms
+    // (*pre_minmax = whether it did: its sort then skips that pass)
+    int lift_and_search(const rh_columns &c, size_t m, const rh::SearchJob &jb, const rh::SearchJob &jd,
+                        const rh_columns *next = nullptr, size_t next_m = 0, bool *pre_minmax = nullptr) {
+        if (pre_minmax) *pre_minmax = false;
         const uint32_t *pos = scratch.u32(7, m);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         if (fused_lift_search) {
             rh::DevCols dc = to_dev(c);
             dc.dst = pos;
+            rh::NextMinmax nx{};
+            if (next && next_m && next_m <= rh::SORT_BUCKET_MAX && pre_minmax) {
+                nx.keys = static_cast<const uint8_t *>(next->keys);
+                nx.m = next_m;
+                nx.part = scratch.u64(3, 2 * ((next_m + rh::MINMAX_TILE - 1) / rh::MINMAX_TILE));
+                if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+            }
             bool supported = false;
             const hipError_t e =
                 rh::launch_lift_search_schema(schema.key_kind, (int)schema.key_len, schema.value_kind, (int)schema.value_len,
-                                              schema.record_kind, c.tags != nullptr, dc, m, sfps.p, skeys.p, jb, jd,
+                                              schema.record_kind, c.tags != nullptr, dc, m, sfps.p, skeys.p, jb, jd, nx,
                                               stream, &supported);
             if (e != hipSuccess) return fail(RH_ERR_HIP, std::string("lift + search launch: ") + hipGetErrorString(e));
-            if (supported) return RH_OK;
+            if (supported) {
+                if (pre_minmax) *pre_minmax = nx.keys != nullptr;
+                return RH_OK;
+            }
         }
         int rc;
         if ((rc = lift_dispatch(schema, c, m, sfps.p, nullptr, nullptr, nullptr, false, stream, pos))) return rc;
@@ -1256,6 +1275,8 @@ struct rh_store {
         RH_HIP(kops->search_sampled(jd.keys, jd.n, jd.smp, jd.smp2, skeys.p, m, jd.rank, jd.present, stream, jd.tb));
         return RH_OK;
     }
+    // A/B switch: RSOS_HIP_PRE_MINMAX=0 = the next batch's sort runs its own min / max pass
+    bool pre_minmax_on = !(getenv("RSOS_HIP_PRE_MINMAX") && *getenv("RSOS_HIP_PRE_MINMAX") == '0');
     // A/B switch: RSOS_HIP_UNFUSED set (non-empty) = separate lift / search launches
     bool fused_lift_search = !(getenv("RSOS_HIP_UNFUSED") && *getenv("RSOS_HIP_UNFUSED"));
     PinnedVec<uint64_t> res_host;  // the batch's 96-byte result block
@@ -1315,6 +1336,7 @@ struct rh_store {
         uint64_t *host = res_host.data();
         uint32_t flags = 0;
         int next_rc = RH_OK;
+        bool pre = false;  // the next batch's digit min / max formed by this batch's fused launch
         for (int full = 0; full < 2; full++) {
             // 1 again with the full sort (the bucket sort's order was not final)
             if (full == 1 && (rc = prepare_batch(c, ops, m, true))) return rc;
@@ -1332,7 +1354,10 @@ struct rh_store {
             rh::SearchJob jd{dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, dt, rank_d, present_d};
             if (!jb.smp2 || nb == 0) jb.tb = rh::SearchTable{};
             if (!jd.smp2 || nd == 0) jd.tb = rh::SearchTable{};
-            if ((rc = lift_and_search(c, m, jb, jd))) return rc;
+            // (the first pass also forms the next batch's digit min / max for its sort)
+            const bool want_pre = full == 0 && next && next_m && pre_minmax_on;
+            if ((rc = lift_and_search(c, m, jb, jd, want_pre ? next : nullptr, next_m, want_pre ? &pre : nullptr)))
+                return rc;
             // 4. the batch's delta records and counts, merged into the delta run's other buffer
             //    (one pass: the merged run, its block sums, count prefixes and search samples)
             RH_HIP(rh::launch_delta_apply(schema.key_kind, (int)kl, sfps.p, sops.p, m, rank_b, present_b, bfps[cb].p,
@@ -1353,7 +1378,7 @@ struct rh_store {
                 // a failure to queue the next batch is reported after this batch commits (the
                 // batches before the failing one stay applied), never instead of it
                 next_rc = batch_buffers(next_m);
-                if (!next_rc) next_rc = prepare_batch(*next, next_ops, next_m, false);
+                if (!next_rc) next_rc = prepare_batch(*next, next_ops, next_m, false, pre);
                 if ((rc = next_rc ? sync() : sync_event(res_ev))) return rc;
                 if (next_prepared) *next_prepared = !next_rc;
             } else if ((rc = sync())) {

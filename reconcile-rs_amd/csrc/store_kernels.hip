@@ -150,7 +150,8 @@ __global__ void k_gather(const uint8_t *keys, const uint8_t *fps, const uint8_t 
 // a bucket index B = (d - min) >> shift of CB + 8 bits (shift chosen from the batch's digit
 // range, so random and dense key ranges both spread): the high CB bits pick one of C = 2^CB
 // coarse buckets (~1,000 keys each), the low 8 bits a fine bucket inside it.
-//   k_cs_minmax      per-workgroup digit min / max (every later kernel folds the partials)
+//   k_cs_minmax      per-workgroup digit min / max (every later kernel folds the partials); in
+//                    apply_device_many the previous batch's k_lift_search computes them instead
 //   k_cs_hist        per-workgroup coarse histograms
 //   k_cs_colscan     each workgroup's offset inside each coarse bucket and the bucket totals;
 //                    its last workgroup scans the totals into the buckets' starts (and (min,
@@ -170,7 +171,7 @@ constexpr int CS_TILE = 8192, CS_WG = 1024;         // keys / lanes per minmax /
 constexpr int CS_FINE_BITS = 8, CS_FINE = 1 << CS_FINE_BITS;
 constexpr int CS_CAP = 2048;                        // largest coarse bucket ordered in LDS
 constexpr uint32_t CS_MAX_C = 4096;                 // coarse buckets at most
-constexpr uint64_t CS_MAX_M = 2ull << 20;
+constexpr uint64_t CS_MAX_M = SORT_BUCKET_MAX;
 
 // block-wide min / max (every lane gets the result); lo / hi: one slot per wave
 __device__ __forceinline__ void minmax_block(uint64_t &a, uint64_t &b, uint64_t *lo, uint64_t *hi) {
@@ -193,12 +194,7 @@ __device__ __forceinline__ void minmax_block(uint64_t &a, uint64_t &b, uint64_t 
 }
 
 template <int KK, int KL>
-__global__ __launch_bounds__(CS_WG) void k_cs_minmax(const uint8_t *keys, uint64_t m, uint64_t *part, uint32_t *flags,
-                                                     uint32_t *ticket) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the sort's first launch: no memsets of its own
-        *flags = 0;
-        *ticket = 0;
-    }
+__global__ __launch_bounds__(CS_WG) void k_cs_minmax(const uint8_t *keys, uint64_t m, uint64_t *part) {
     __shared__ uint64_t lo[CS_WG / 64], hi[CS_WG / 64];
     uint64_t a = ~0ull, b = 0;
     const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
@@ -236,12 +232,17 @@ __device__ __forceinline__ void cs_params(const uint64_t *part, uint32_t nwg, ui
 }
 
 template <int KK, int KL>
-__global__ __launch_bounds__(CS_WG) void k_cs_hist(const uint8_t *keys, uint64_t m, const uint64_t *part, uint32_t nwg,
-                                                   uint32_t bbits, uint32_t C, uint32_t *hist) {
+__global__ __launch_bounds__(CS_WG) void k_cs_hist(const uint8_t *keys, uint64_t m, const uint64_t *part, uint32_t npart,
+                                                   uint32_t bbits, uint32_t C, uint32_t *hist, uint32_t *flags,
+                                                   uint32_t *ticket) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // no memsets of the sort's own: the flags and the scan's ticket
+        *flags = 0;
+        *ticket = 0;
+    }
     __shared__ uint32_t h[CS_MAX_C];
     uint64_t mn;
     uint32_t sh;
-    cs_params(part, nwg, bbits, &mn, &sh);
+    cs_params(part, npart, bbits, &mn, &sh);
     for (uint32_t b = threadIdx.x; b < C; b += CS_WG) h[b] = 0;
     __syncthreads();
     const uint64_t i0 = (uint64_t)blockIdx.x * CS_TILE;
@@ -269,7 +270,8 @@ __global__ __launch_bounds__(CS_WG) void k_cs_hist(const uint8_t *keys, uint64_t
 // scan and the bucket scan were two.  *ticket: 0 on entry (k_cs_minmax zeroes it).
 __global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nwg, uint32_t C, uint32_t *total,
                                                      uint32_t *ticket, uint32_t *start, uint32_t *flags,
-                                                     const uint64_t *part_mm, uint32_t bbits, uint64_t *params) {
+                                                     const uint64_t *part_mm, uint32_t npart, uint32_t bbits,
+                                                     uint64_t *params) {
     constexpr uint32_t Q = 16;
     __shared__ uint32_t part[Q][64];
     __shared__ uint32_t last;
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nw
     const uint32_t t = threadIdx.x, pc = (C + 1023) / 1024;
     uint64_t mn;
     uint32_t sh;
-    cs_params(part_mm, nwg, bbits, &mn, &sh);
+    cs_params(part_mm, npart, bbits, &mn, &sh);
     if (t == 0) {
         params[0] = mn;
         params[1] = sh;
@@ -1501,7 +1503,7 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
                           uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, bool full,
-                          hipStream_t st, uint32_t *pos) override {
+                          hipStream_t st, uint32_t *pos, const uint64_t *pre_part, uint32_t pre_npart) override {
         hipError_t e;
         if (!fps == !pos) return hipErrorInvalidValue;  // exactly one of: gather fps, emit positions
         uint32_t *perm = s.u32(0, m), *perm2 = s.u32(1, m);
@@ -1518,7 +1520,8 @@ struct KeyOps final : StoreKeyOps {
             std::swap(perm, perm2);
             return hipSuccess;
         };
-        if (!full && m <= CS_MAX_M) return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st, pos);
+        if (!full && m <= CS_MAX_M)
+            return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st, pos, pre_part, pre_npart);
         if ((e = hipMemsetAsync(flags, 0, 4, st))) return e;
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
         // multi-digit keys: the most significant digit alone orders random and spread keys
@@ -1534,7 +1537,7 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t sort_batch_buckets(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
                                   uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, hipStream_t st,
-                                  uint32_t *pos) {
+                                  uint32_t *pos, const uint64_t *pre_part, uint32_t pre_npart) {
         uint32_t cb = 0;
         while ((1ull << cb) * 1024 < m) cb++;  // ~1,000 keys per coarse bucket
         const uint32_t C = 1u << cb, nwg = (uint32_t)((m + CS_TILE - 1) / CS_TILE), bbits = cb + CS_FINE_BITS;
@@ -1545,10 +1548,14 @@ struct KeyOps final : StoreKeyOps {
         if (s.err) return s.err;
         uint64_t *params = part + 2ull * nwg;
         uint32_t *ticket = reinterpret_cast<uint32_t *>(part + 2ull * nwg + 2);
-        hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, flags, ticket);
-        hipLaunchKernelGGL((k_cs_hist<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part, nwg, bbits, C, hist);
+        // the digit min / max partials: precomputed (k_lift_search of the previous batch) or here
+        const uint64_t *mm = pre_part ? pre_part : part;
+        const uint32_t npart = pre_part ? pre_npart : nwg;
+        if (!pre_part) hipLaunchKernelGGL((k_cs_minmax<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, part);
+        hipLaunchKernelGGL((k_cs_hist<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, mm, npart, bbits, C, hist, flags,
+                           ticket);
         hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(1024), 0, st, hist, nwg, C, total, ticket, start,
-                           flags, part, bbits, params);
+                           flags, mm, npart, bbits, params);
         hipLaunchKernelGGL((k_cs_scatter<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, params, C, hist, start,
                            okey, idx);
         hipLaunchKernelGGL((k_cs_sort<KK, KL>), dim3(C), dim3(256), 0, st, okey, idx, start, total, params, fps, ops,

@@ -91,11 +91,23 @@ struct SearchJob {
     uint32_t *rank;
     uint8_t *present;
 };
+// the next batch's keys whose leading-digit (min, max) partials a k_lift_search also forms:
+// ceil(m / MINMAX_TILE) pairs into part (keys == nullptr: none)
+struct NextMinmax {
+    const uint8_t *keys = nullptr;
+    uint64_t m = 0;
+    uint64_t *part = nullptr;
+};
 // table size for a run of n rows, and its build from the run's second-level samples
 // (base: the base run's fine table, ~1 sample per bucket; otherwise a delta run's, ~8)
 uint32_t search_table_bits(uint64_t n, bool base = true);
 hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, uint64_t *par, hipStream_t st,
                                bool base = true);
+
+// largest batch the bucket sort orders (larger ones take the LSD radix sort)
+constexpr uint64_t SORT_BUCKET_MAX = 2ull << 20;
+// keys per workgroup of k_lift_search's digit min / max role (its partials replace k_cs_minmax's)
+constexpr uint64_t MINMAX_TILE = 2048;
 
 // Key-type-specialised device operations of the store.
 struct StoreKeyOps {
@@ -103,6 +115,8 @@ struct StoreKeyOps {
     // sort a batch by key (stable) and gather keys / fingerprints / ops into key order; with
     // fps == nullptr, pos[input row] = its sorted row instead (exactly one of fps / pos given),
     // for the batch path's lift, which runs after the sort and writes each fingerprint in place.
+    // pre_part (bucket sort only): pre_npart (min, max) pairs of the keys' leading digits already
+    // computed (k_lift_search of the previous batch), in place of the sort's own min / max pass.
     // full = false: coarse buckets of the most significant u64 digit + a sort of each bucket in
     // LDS (ties on that digit broken by the whole key); *flags |= 4 if the digits are too skewed
     // for the buckets, and (multi-digit keys past the bucket path's size) |= 2 if two keys share
@@ -111,7 +125,8 @@ struct StoreKeyOps {
     // order) by the sort itself.
     virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
                                   Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags,
-                                  bool full, hipStream_t st, uint32_t *pos = nullptr) = 0;
+                                  bool full, hipStream_t st, uint32_t *pos = nullptr,
+                                  const uint64_t *pre_part = nullptr, uint32_t pre_npart = 0) = 0;
     // lower-bound rank of each query key (and whether it is present)
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;

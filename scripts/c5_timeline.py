@@ -4,9 +4,9 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-# a batch starts at its key sort (round 3 on: the sort runs before the lift, queued behind the
+# a batch starts at its key sort's histogram pass (round 3 on: the sort runs before the lift, queued behind the
 # previous batch's result copy); older traces start it at the lift
-mark = "k_cs_minmax<" if any("k_cs_minmax<" in r["Kernel_Name"] for r in rows) and any(
+mark = "k_cs_hist<" if any("k_cs_hist<" in r["Kernel_Name"] for r in rows) and any(
     "k_lift_search<" in r["Kernel_Name"] for r in rows) else "k_lift<"
 lifts = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"] and int(r["Grid_Size_X"]) < 2_000_000]
 batches = [int(b) for b in sys.argv[2:]] or [len(lifts) - 3]

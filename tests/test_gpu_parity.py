@@ -1150,9 +1150,11 @@ def test_store_apply_device_many_equals_one_by_one(gpu, oracle_lib):
 
 def test_batch_path_variants_agree(gpu, oracle_lib, monkeypatch):
     """The batch path's fused lift + search launch (k_lift_search) against the lift and the two
-    searches as separate launches (RSOS_HIP_UNFUSED=1, read when a store is created), and the
-    merges' precomputed tile bounds (k_tile_bounds) against each tile searching its own
-    (RSOS_HIP_TILE_SEARCH=1, read per merge): the same batches -- fresh keys, overwrites, deletes,
+    searches as separate launches (RSOS_HIP_UNFUSED=1, read when a store is created), the next
+    batch's digit min / max formed by that launch against the sort's own pass
+    (RSOS_HIP_PRE_MINMAX=0, read when a store is created), and the merges' precomputed tile bounds
+    (k_tile_bounds) against each tile searching its own (RSOS_HIP_TILE_SEARCH=1, read per
+    merge): the same batches -- fresh keys, overwrites, deletes,
     through apply_device and apply_device_many, across compactions -- leave every store with the
     same counts, fingerprints, ranks and root, and that root equals the oracle's fold of the live
     records' lifts."""
@@ -1175,9 +1177,10 @@ def test_batch_path_variants_agree(gpu, oracle_lib, monkeypatch):
         bs.append(b)
         ops.append(o)
 
-    def run(unfused, tile_search, many):
+    def run(unfused, tile_search, many, pre_minmax=True):
         monkeypatch.setenv("RSOS_HIP_UNFUSED", "1" if unfused else "")
         monkeypatch.setenv("RSOS_HIP_TILE_SEARCH", "1" if tile_search else "0")
+        monkeypatch.setenv("RSOS_HIP_PRE_MINMAX", "1" if pre_minmax else "0")
         st = GpuFingerprintStore(s)
         st.set_compaction(4, 40_000)
         st.load_bulk_device(base)
@@ -1189,7 +1192,8 @@ def test_batch_path_variants_agree(gpu, oracle_lib, monkeypatch):
 
     ref = run(False, False, True)
     assert ref[4] > 0  # compactions happened
-    for variant in [(True, False, True), (False, True, True), (True, True, False), (False, False, False)]:
+    for variant in [(True, False, True), (False, True, True), (True, True, False), (False, False, False),
+                    (False, False, True, False)]:
         got = run(*variant)
         assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2] and got[4] == ref[4], variant
         assert np.array_equal(got[3], ref[3]) and got[5] == ref[5], variant

@@ -322,6 +322,12 @@ int rh_store_set_compaction(rh_store *store, uint64_t divisor, uint64_t min_rows
  * contents and every answer are unchanged.  Optional: buffers otherwise grow on demand.    */
 int rh_store_reserve(rh_store *store, uint64_t rows, uint64_t batch_rows);
 int rh_store_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_rows, uint64_t *compactions);
+/* Which batch path ran (nullable outputs): batches of up to 1,024 rows (512 for 32-byte keys) take
+ * the small-batch path -- one workgroup sorts, lifts and searches them and forms their deltas, then
+ * one merge launch, the rows and the results read and written in place in page-locked host memory
+ * (a replica's network merge, src/replica/dispatch.rs:188-196); larger ones the large-batch path.
+ * Env RSOS_HIP_SMALL_MAX=<rows> (read when a store is created) caps the small path; 0 turns it off. */
+int rh_store_batch_stats(rh_store *store, uint64_t *small_batches, uint64_t *large_batches);
 
 /* ---- snapshot reload ------------------------------------------------------------------
  * FileSnapshot (src/snapshot.rs:30-58): "RCNL", u32 LE format version 1, then bincode 1.3.3

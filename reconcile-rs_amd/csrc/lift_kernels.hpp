@@ -384,7 +384,7 @@ __global__ __launch_bounds__(LIFT_THREADS) void k_lift(DevCols c, uint64_t n, ui
             // bounded: a bucket the key sort could not order leaves its rows' slots unwritten
             // (the sort flags it and the batch is sorted and lifted again)
             const uint32_t r = c.dst[i];
-            if (r < n) store_fp(fps, r, h);
+            if (r < n) store_fp<uint64_t>(fps, r, h);
         } else {
             store_fp(fps + b0 * 32, t, h);
         }

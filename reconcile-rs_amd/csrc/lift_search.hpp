@@ -84,7 +84,7 @@ __global__ __launch_bounds__(LIFT_THREADS) void k_lift_search(DevCols c, uint64_
         uint32_t h[8];
         lift_record<KK, KL, VK, VL, RK, TAGS>(kw, sw, tomb, vrow, h);
         const uint32_t r = c.dst[i];
-        if (r < n) store_fp(fps, r, h);  // bounded as in k_lift
+        if (r < n) store_fp<uint64_t>(fps, r, h);  // bounded as in k_lift
     } else {
         const SearchJob &j = role == 1 ? jb : jd;
         search_sampled_one<KK, KL>(j.keys, j.n, j.smp, j.smp2, j.tb, q + i * KL, j.rank + i, j.present + i);

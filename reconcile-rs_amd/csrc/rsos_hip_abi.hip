@@ -28,6 +28,7 @@
 #include "internal.hpp"
 #include "host_tier.hpp"
 #include "lift_kernels.hpp"
+#include "small_batch.hpp"
 #include "snapshot_kernels.hpp"
 #include "store_kernels.hpp"
 
@@ -244,6 +245,21 @@ hipError_t launch_snap_lift_schema(int kk, int kl, int vk, int vl, int mode, con
                                    hipStream_t st, bool *supported) {
 #define X(name, KK, KL, VK, VL) \
     if (kk == KK && kl == KL && vk == VK && vl == VL) return launch_snap_lift_##name(mode, a, lds, st, supported);
+#include "schemas.def"
+#undef X
+    *supported = false;
+    return hipSuccess;
+}
+
+#define X(name, kk, kl, vk, vl) \
+    hipError_t launch_small_batch_##name(int rk, bool tags, const SmallBatch &a, hipStream_t st, bool *supported);
+#include "schemas.def"
+#undef X
+
+hipError_t launch_small_batch_schema(int kk, int kl, int vk, int vl, int rk, bool tags, const SmallBatch &a,
+                                     hipStream_t st, bool *supported) {
+#define X(name, KK, KL, VK, VL) \
+    if (kk == KK && kl == KL && vk == VK && vl == VL) return launch_small_batch_##name(rk, tags, a, st, supported);
 #include "schemas.def"
 #undef X
     *supported = false;
@@ -685,45 +701,199 @@ struct rh_store {
         }
         return memcmp(a, b, kl);
     }
-    // one batch: the staged rows in key order, the last operation of each key kept
+    // One batch: the staged rows as they were staged, in one call -- the device sorts them (stably,
+    // so the last operation staged for a key is the last of its run) and keeps the last row of each
+    // repeated key: the result of applying them in order (just_insert_bulk,
+    // src/replica/write.rs:107-121).  A batch of up to small_batch_max rows takes the one-workgroup
+    // path (apply_small, reading the rows from page-locked host memory); larger ones go up in one
+    // copy per column.  No host sort, no per-row host work.
     int flush() {
         if (!pend.n) return RH_OK;
-        const size_t m = pend.n, kr = kl, vr = value_row(schema);
+        const size_t m = pend.n;
         const bool dated = schema.record_kind == RH_REC_DATED;
-        std::vector<uint32_t> idx(m);
-        for (size_t i = 0; i < m; i++) idx[i] = (uint32_t)i;
-        const uint8_t *K = pend.keys.data();
-        std::stable_sort(idx.begin(), idx.end(),
-                         [&](uint32_t a, uint32_t b) { return key_cmp(K + (size_t)a * kr, K + (size_t)b * kr) < 0; });
-        Pending b;
-        size_t out = 0;
-        for (size_t i = 0; i < m; i++) {
-            if (i + 1 < m && key_cmp(K + (size_t)idx[i] * kr, K + (size_t)idx[i + 1] * kr) == 0) continue;
-            const size_t r = idx[i];
-            b.keys.insert(b.keys.end(), K + r * kr, K + r * kr + kr);
-            b.vals.insert(b.vals.end(), pend.vals.data() + r * vr, pend.vals.data() + r * vr + vr);
-            b.tags.push_back(pend.tags[r]);
-            b.ops.push_back(pend.ops[r]);
-            if (dated) {
-                b.phys.push_back(pend.phys[r]);
-                b.node.push_back(pend.node[r]);
-                b.logical.push_back(pend.logical[r]);
-            }
-            out++;
-        }
-        pend.clear();
-        const rh_columns h{b.keys.data(), dated ? b.phys.data() : nullptr, dated ? b.logical.data() : nullptr,
-                           dated ? b.node.data() : nullptr, schema.record_kind == RH_REC_PLAIN ? nullptr : b.tags.data(),
-                           b.vals.data()};
+        const rh_columns h{pend.keys.data(), dated ? pend.phys.data() : nullptr, dated ? pend.logical.data() : nullptr,
+                           dated ? pend.node.data() : nullptr,
+                           schema.record_kind == RH_REC_PLAIN ? nullptr : pend.tags.data(), pend.vals.data()};
         uint64_t c[3];
-        return apply_host(h, b.ops.data(), out, c);
+        const int rc = apply_host(h, pend.ops.data(), m, c, true);
+        pend.clear();
+        return rc;
     }
-    int apply_host(const rh_columns &h, const uint8_t *ops, size_t m, uint64_t c[3]) {
+    // host columns: a small batch is packed into page-locked memory the device reads in place;
+    // a large one is uploaded (one copy per column) and applied by the large-batch path
+    int apply_host(const rh_columns &h, const uint8_t *ops, size_t m, uint64_t c[3], bool last_wins = false) {
         int rc;
+        bool done = false;
+        if (m && m <= small_limit()) {
+            rh_columns d;
+            const uint8_t *dops = nullptr;
+            if ((rc = pack_small(h, ops, m, &d, &dops))) return rc;
+            if ((rc = apply_small(d, dops, m, last_wins, c, &done))) return rc;
+            if (done) return RH_OK;
+        }
         if ((rc = staging.upload(schema, h, m, stream)) || (rc = hops.ensure(m + 64))) return rc;
         if (m) RH_HIP(hipMemcpyAsync(hops.p, ops, m, hipMemcpyHostToDevice, stream));
-        return apply_device(staging.view(schema), hops.p, m, c);
+        return apply_device(staging.view(schema), hops.p, m, c, false, nullptr, nullptr, 0, nullptr, last_wins);
     }
+    // ---- the small-batch path (small_batch.hpp) --------------------------------------------------
+    // A/B switch: RSOS_HIP_SMALL_MAX=<rows> caps the small path (0: off), read when a store is created
+    uint64_t small_env = getenv("RSOS_HIP_SMALL_MAX") ? strtoull(getenv("RSOS_HIP_SMALL_MAX"), nullptr, 10) : ~0ull;
+    uint64_t small_limit() const {
+        if (schema.key_kind == RH_KEY_UNIT) return 0;
+        return std::min<uint64_t>(small_env, rh::small_batch_max((int)kl));
+    }
+    PinnedVec<uint8_t> sb_in;    // a small host batch, packed (the device reads it in place)
+    PinnedVec<uint64_t> sb_res;  // the small path's result block (written by the device in place)
+    template <class T>
+    int dev_ptr(T *host, T **dev) {  // the device address of mapped page-locked memory
+        void *d = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&d, host, 0);
+        if (e != hipSuccess || !d) {
+            (void)hipGetLastError();
+            return fail(RH_ERR_HIP, "page-locked buffer has no device address");
+        }
+        *dev = static_cast<T *>(d);
+        return RH_OK;
+    }
+    int pack_small(const rh_columns &h, const uint8_t *ops, size_t m, rh_columns *d, const uint8_t **dops) {
+        const size_t kr = kl, vr = value_row(schema);
+        const bool dated = schema.record_kind == RH_REC_DATED;
+        const bool tags = h.tags && schema.record_kind != RH_REC_PLAIN;
+        auto pad = [](size_t x) { return (x + 15) & ~size_t(15); };
+        const size_t o_val = pad(m * kr), o_ph = o_val + pad(m * vr), o_nd = o_ph + (dated ? pad(m * 8) : 0),
+                     o_lg = o_nd + (dated ? pad(m * 8) : 0), o_tg = o_lg + (dated ? pad(m * 4) : 0),
+                     o_op = o_tg + (tags ? pad(m) : 0), end = o_op + pad(m);
+        try {
+            sb_in.resize(end + 16);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "small batch: page-locked allocation failed");
+        }
+        uint8_t *b = sb_in.data();
+        auto put = [&](size_t off, const void *src, size_t bytes) {
+            if (src) memcpy(b + off, src, bytes);
+            else memset(b + off, 0, bytes);  // a NULL column (the values of a delete-only batch)
+        };
+        put(0, h.keys, m * kr);
+        put(o_val, h.values, m * vr);
+        if (dated) {
+            put(o_ph, h.phys, m * 8);
+            put(o_nd, h.node, m * 8);
+            put(o_lg, h.logical, m * 4);
+        }
+        if (tags) put(o_tg, h.tags, m);
+        put(o_op, ops, m);
+        uint8_t *db;
+        int rc = dev_ptr(b, &db);
+        if (rc) return rc;
+        *d = rh_columns{db, dated ? reinterpret_cast<const uint64_t *>(db + o_ph) : nullptr,
+                        dated ? reinterpret_cast<const uint32_t *>(db + o_lg) : nullptr,
+                        dated ? reinterpret_cast<const uint64_t *>(db + o_nd) : nullptr, tags ? db + o_tg : nullptr,
+                        db + o_val};
+        *dops = db + o_op;
+        return RH_OK;
+    }
+    // capacity of the delta run's other buffers for a batch of m rows into it (the largest run the
+    // policy allows: threshold + one batch), and of the record heap
+    int delta_capacity(size_t m) {
+        int rc;
+        const int nxt = 1 - cd;
+        const uint64_t n_max = nd + m;
+        const uint64_t thresh = std::max<uint64_t>(nb / compact_div, compact_min);
+        const uint64_t plan = std::max<uint64_t>(n_max, std::min<uint64_t>(thresh, nb + nd) + m);
+        if ((rc = dheap.grow_keep((heap_len + m) * sizeof(rh::DeltaRec) + 64, heap_len * sizeof(rh::DeltaRec), stream)))
+            return rc;
+        if ((rc = dkeys[nxt].ensure(plan * kl + 64)) || (rc = dslot[nxt].ensure(plan + 16)) ||
+            (rc = dbsums[nxt].ensure(rh_num_blocks(plan) * 32 + 32)) ||
+            (rc = dssums[nxt].ensure(rh_num_superblocks(plan) * 32 + 32)) ||
+            (rc = dsblk[nxt].ensure(rh_num_superblocks(plan) + 16)) || (rc = dscnt.ensure(rh_num_superblocks(plan) + 16)) ||
+            (rc = dblk[nxt].ensure(rh_num_blocks(plan) + 16)) || (rc = dinb[nxt].ensure(plan + 16)) ||
+            (rc = dsmp[nxt].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp2[nxt].ensure(rh::sample2_entries(plan))) ||
+            (rc = dsmp[cd].ensure(1)) || (rc = dsmp2[cd].ensure(1)) || (rc = mcnt.ensure(8)))
+            return rc;
+        return RH_OK;
+    }
+    // A batch of m <= small_limit() rows in two launches (the one-workgroup front, then the delta
+    // merge) and no copy command: the columns may live in device memory or in mapped page-locked
+    // host memory; the result block and the host tier's fold rows are written into mapped
+    // page-locked memory.  *done = false: the shape has no small path (the caller takes the large one).
+    int apply_small(const rh_columns &c, const uint8_t *ops, size_t m, bool last_wins, uint64_t out[3], bool *done) {
+        int rc;
+        *done = false;
+        out[0] = out[1] = out[2] = 0;
+        if (m == 0 || m > small_limit()) return RH_OK;
+        if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        const int fmode = fold_mode();
+        if ((rc = skeys.ensure(m * kl + 64)) || (rc = delta_capacity(m))) return rc;
+        uint32_t *upos = scratch.u32(3, m + 1), *usrc = scratch.u32(4, m + 1), *rlist = scratch.u32(5, m + 1);
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        uint64_t *res = nullptr;
+        uint8_t *fk = nullptr, *fr = nullptr, *fd = nullptr;
+        try {
+            sb_res.resize(16);
+            if (fmode) {
+                fold_keys.resize(m * kl + 8);
+                fold_recs.resize(m * sizeof(rh::DeltaRec) + 8);
+                fold_ops.resize(m + 8);
+            }
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "small batch: page-locked allocation failed");
+        }
+        if ((rc = dev_ptr(sb_res.data(), &res))) return rc;
+        if (fmode && ((rc = dev_ptr(fold_keys.data(), &fk)) || (rc = dev_ptr(fold_recs.data(), &fr)) ||
+                      (rc = dev_ptr(fold_ops.data(), &fd))))
+            return rc;
+        const int nxt = 1 - cd;
+        rh::SmallBatch a{};
+        a.c = to_dev(c);
+        a.ops = ops;
+        a.m = (uint32_t)m;
+        a.last_wins = last_wins ? 1 : 0;
+        a.jb = rh::SearchJob{bkeys[cb].p, nb, bsmp.p, bsmp2.p, base_table(), nullptr, nullptr};
+        a.jd = rh::SearchJob{dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, rh::SearchTable{}, nullptr, nullptr};
+        if (!a.jb.smp2 || nb == 0) a.jb.tb = rh::SearchTable{};
+        a.base_fps = bfps[cb].p;
+        a.dslot = dslot[cd].p;
+        a.heap = dheap.p;
+        a.heap_base = (uint32_t)heap_len;
+        a.skeys = skeys.p;
+        a.upos = upos, a.usrc = usrc, a.rlist = rlist;
+        a.mcnt = mcnt.p;
+        a.res = res;
+        a.fold = fmode;
+        a.fkeys = fk, a.frecs = fr, a.fdrop = fd;
+        bool supported = false;
+        hipError_t e = rh::launch_small_batch_schema(schema.key_kind, (int)schema.key_len, schema.value_kind,
+                                                     (int)schema.value_len, schema.record_kind, c.tags != nullptr, a,
+                                                     stream, &supported);
+        if (e != hipSuccess) return fail(RH_ERR_HIP, std::string("small batch launch: ") + hipGetErrorString(e));
+        if (!supported) return RH_OK;
+        version++;  // from here on the batch may commit
+        RH_HIP(rh::launch_delta_merge(schema.key_kind, (int)kl, dkeys[cd].p, dslot[cd].p, nd, skeys.p, m, upos, usrc, rlist,
+                                      mcnt.p, dkeys[nxt].p, dslot[nxt].p, rh_num_blocks(nd + m), dsmp[nxt].p,
+                                      dsmp2[nxt].p, dheap.p, heap_len, stream));
+        if ((rc = sync())) return rc;
+        const uint64_t *h = sb_res.data();
+        if (h[6] & 1) return fail(RH_ERR_ARG, "duplicate key within one batch");
+        const uint64_t kept = h[12];
+        int64_t dcnt;
+        memcpy(&dcnt, &h[7], 8);
+        out[0] = h[0], out[1] = h[1], out[2] = h[2];
+        cd = nxt;
+        nd = nd + h[3] - h[5];
+        heap_len += kept;
+        dtotal += dcnt;
+        rh_fp_add(root_d, &h[8], root_d);  // mod 2^256
+        dsums_ok = false;
+        small_batches++;
+        *done = true;
+        if (fmode) fold_batch(fmode, kept);
+        const uint64_t thresh_now = std::max<uint64_t>(nb / compact_div, compact_min);
+        if (nd > thresh_now || heap_len > thresh_now) {
+            if ((rc = compact())) return rc;
+        }
+        return RH_OK;
+    }
+    uint64_t small_batches = 0, large_batches = 0;
     // ---- the host tier (host_tier.hpp) ---------------------------------------------------------
     // The tier answers from (its copy of a base run) + (its delta tree: every batch since).  It is
     // fresh while tier_version == version.  A batch keeps it fresh by folding the batch's signed
@@ -1284,15 +1454,22 @@ struct rh_store {
     // next: a batch whose step 1 is queued once this batch's kernels are -- the device runs them
     // while the host waits for this batch's result (an event on the result copy, not the stream);
     // *next_prepared says whether they were (a re-sort of this batch overwrites them).
+    // last_wins: repeated keys keep their last row (the staged batch); otherwise they reject the batch
     int apply_device(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3], bool prepared = false,
                      const rh_columns *next = nullptr, const uint8_t *next_ops = nullptr, size_t next_m = 0,
-                     bool *next_prepared = nullptr) {
+                     bool *next_prepared = nullptr, bool last_wins = false) {
         int rc;
         out[0] = out[1] = out[2] = 0;
         if (next_prepared) *next_prepared = false;
         if (m == 0) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if (!prepared && !next && m <= small_limit()) {  // the small-batch path: two launches
+            bool done = false;
+            if ((rc = apply_small(c, ops, m, last_wins, out, &done))) return rc;
+            if (done) return RH_OK;
+        }
         const int fmode = fold_mode();  // how this batch reaches a fresh host tier
+        const uint64_t version0 = version;
         version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
         if ((rc = batch_buffers(m))) return rc;
         // 1. key sort (queued by the previous call when prepared)
@@ -1396,11 +1573,17 @@ struct rh_store {
         out[2] = host[2];
         if (flags & 1) {
             out[0] = out[1] = out[2] = 0;
-            return fail(RH_ERR_ARG, "duplicate key within one batch");
+            if (!last_wins) return fail(RH_ERR_ARG, "duplicate key within one batch");
+            // nothing was committed: reduce the batch to the last row of each key (the sort's
+            // positions and sorted keys are still in place) and apply that
+            version = version0;
+            if (next_prepared) *next_prepared = false;
+            return apply_last_rows(c, ops, m, out);
         }
         cd = nxt;
         nd = nd + c2[0] - c2[2];
         heap_len += m;
+        large_batches++;
         dtotal += dcnt;
         rh_fp_add(root_d, &host[8], root_d);  // mod 2^256
         dsums_ok = false;
@@ -1411,6 +1594,55 @@ struct rh_store {
             if ((rc = compact())) return rc;
         }
         return next_rc ? next_rc : RH_OK;
+    }
+    // A batch with repeated keys, after its sort (scratch u32(7): each input row's sorted row; skeys:
+    // the stable sort): the last row of each key, in input order, into the second column set, then
+    // applied as a batch without repeats.
+    DevColumns lastcols;
+    DevBuf<uint8_t> lastops;
+    int apply_last_rows(const rh_columns &c, const uint8_t *ops, size_t m, uint64_t out[3]) {
+        int rc;
+        const uint32_t *pos = scratch.u32(7, m);
+        uint32_t *keep = scratch.u32(11, m + 1), *dst = scratch.u32(12, m + 1);
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        RH_HIP(kops->keep_last_rows(skeys.p, pos, m, keep, stream));
+        RH_HIP(rh::launch_exclusive_scan_u32(keep, dst, m + 1, scratch, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        try {
+            res_host.resize(12);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "pinned result buffer");
+        }
+        RH_HIP(hipMemcpyAsync(res_host.data(), dst + m, 4, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) return rc;
+        uint32_t kept;
+        memcpy(&kept, res_host.data(), 4);
+        const size_t kr = kl, vr = value_row(schema);
+        const bool dated = schema.record_kind == RH_REC_DATED, tags = c.tags != nullptr;
+        if ((rc = lastcols.keys.ensure(kept * kr + 16)) || (rc = lastcols.values.ensure(kept * vr + 16)) ||
+            (rc = lastops.ensure(kept + 64)))
+            return rc;
+        if (dated && ((rc = lastcols.phys.ensure(kept + 1)) || (rc = lastcols.node.ensure(kept + 1)) ||
+                      (rc = lastcols.logical.ensure(kept + 1))))
+            return rc;
+        if (tags && (rc = lastcols.tags.ensure(kept + 16))) return rc;
+        lastcols.has_tags = tags;
+        auto cp = [&](const void *src, uint32_t row, void *o) -> hipError_t {
+            return rh::launch_compact_rows(static_cast<const uint8_t *>(src), row, keep, dst, m, static_cast<uint8_t *>(o),
+                                           stream);
+        };
+        RH_HIP(cp(c.keys, (uint32_t)kr, lastcols.keys.p));
+        RH_HIP(cp(c.values, (uint32_t)vr, lastcols.values.p));
+        if (dated) {
+            RH_HIP(cp(c.phys, 8, lastcols.phys.p));
+            RH_HIP(cp(c.node, 8, lastcols.node.p));
+            RH_HIP(cp(c.logical, 4, lastcols.logical.p));
+        }
+        if (tags) RH_HIP(cp(c.tags, 1, lastcols.tags.p));
+        if (ops) RH_HIP(cp(ops, 1, lastops.p));
+        else RH_HIP(hipMemsetAsync(lastops.p, 0, kept, stream));
+        if (!c.values && kept) RH_HIP(hipMemsetAsync(lastcols.values.p, 0, kept * vr, stream));
+        return apply_device(lastcols.view(schema), lastops.p, kept, out);
     }
     int query(const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {  // rank ranges
         int rc;
@@ -2039,6 +2271,16 @@ int rh_store_stats(rh_store *s, uint64_t *base_rows, uint64_t *delta_rows, uint6
     if (base_rows) *base_rows = s->nb;
     if (delta_rows) *delta_rows = s->nd;
     if (compactions) *compactions = s->compactions;
+    return RH_OK;
+}
+
+int rh_store_batch_stats(rh_store *s, uint64_t *small_batches, uint64_t *large_batches) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const int rc = flush_locked(s);
+    if (rc) return rc;
+    if (small_batches) *small_batches = s->small_batches;
+    if (large_batches) *large_batches = s->large_batches;
     return RH_OK;
 }
 

@@ -28,6 +28,7 @@
 #include "internal.hpp"
 #include "store_kernels.hpp"
 #include "search_device.hpp"
+#include "fp_device.hpp"
 
 namespace rh {
 
@@ -70,46 +71,6 @@ __device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t *a, uint64_t 
         else hi = mid;
     }
     return lo;
-}
-
-// ---- 256-bit helpers (the Fingerprint group, rsos/src/fingerprint.rs:145-173) ----------------
-
-__device__ __forceinline__ void fp_load(const uint8_t *p, uint32_t f[8]) {
-    const uint4 a = reinterpret_cast<const uint4 *>(p)[0], b = reinterpret_cast<const uint4 *>(p)[1];
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
-}
-__device__ __forceinline__ void fp_store(uint8_t *p, const uint32_t f[8]) {
-    reinterpret_cast<uint4 *>(p)[0] = make_uint4(f[0], f[1], f[2], f[3]);
-    reinterpret_cast<uint4 *>(p)[1] = make_uint4(f[4], f[5], f[6], f[7]);
-}
-__device__ __forceinline__ void fp_add(const uint32_t a[8], const uint32_t b[8], uint32_t o[8]) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint64_t t = (uint64_t)a[i] + b[i] + c;
-        o[i] = (uint32_t)t;
-        c = t >> 32;
-    }
-}
-__device__ __forceinline__ void fp_sub(const uint32_t a[8], const uint32_t b[8], uint32_t o[8]) {
-    uint64_t br = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint64_t t = (uint64_t)a[i] - b[i] - br;
-        o[i] = (uint32_t)t;
-        br = (t >> 63) & 1;  // borrow out
-    }
-}
-
-__device__ __forceinline__ void words_of(const uint4 &v, uint32_t *w) {
-    w[0] = v.x;
-    w[1] = v.y;
-    w[2] = v.z;
-    w[3] = v.w;
-}
-__device__ __forceinline__ void words_of(const uint2 &v, uint32_t *w) {
-    w[0] = v.x;
-    w[1] = v.y;
 }
 
 // ---- batch sort ------------------------------------------------------------------------------
@@ -296,7 +257,7 @@ __global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nw
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u
                                                                                                               : 0u;
     __syncthreads();
     if (!last) return;  // uniform
@@ -316,7 +277,7 @@ __global__ __launch_bounds__(1024) void k_cs_colscan(uint32_t *hist, uint32_t nw
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
         if (k < pc && pc * t + k < C) {
-            v[k] = __hip_atomic_load(total + pc * t + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[k] = __hip_atomic_load(total + pc * t + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             big |= v[k] > (uint32_t)CS_CAP;
             s += v[k];
         }
@@ -652,6 +613,31 @@ __global__ void k_dedup_scatter(const uint8_t *keys, const uint8_t *fps, const u
         copy_bytes<32>(ofps + 32ull * pos[j], fps + 32 * j);
     }
     if (j + 1 == n) counts[0] = (uint64_t)pos[j] + keep[j];
+}
+
+template <int KK, int KL>
+__global__ void k_keep_last(const uint8_t *skeys, const uint32_t *pos, uint64_t m, uint32_t *keep) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > m) return;
+    if (i == m) {
+        keep[m] = 0;
+        return;
+    }
+    const uint64_t j = pos[i];
+    keep[i] = (j + 1 < m && key_cmp<KK, KL>(skeys + j * KL, skeys + (j + 1) * KL) == 0) ? 0u : 1u;
+}
+
+__global__ void k_compact_rows(const uint8_t *src, uint32_t row, const uint32_t *keep, const uint32_t *dst, uint64_t m,
+                               uint8_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m || !keep[i]) return;
+    const uint8_t *s = src + i * row;
+    uint8_t *d = out + (uint64_t)dst[i] * row;
+    if (row % 4 == 0) {
+        for (uint32_t o = 0; o < row; o += 4) *reinterpret_cast<uint32_t *>(d + o) = *reinterpret_cast<const uint32_t *>(s + o);
+    } else {
+        for (uint32_t o = 0; o < row; o++) d[o] = s[o];
+    }
 }
 
 template <int KK, int KL>
@@ -1146,7 +1132,7 @@ __global__ __launch_bounds__(256) void k_delta_finish(const uint8_t *bsums, int3
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0)
-        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u
                                                                                                               : 0u;
     __syncthreads();
     if (!last) return;  // uniform
@@ -1158,7 +1144,7 @@ __global__ __launch_bounds__(256) void k_delta_finish(const uint8_t *bsums, int3
         uint32_t g[8];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint64_t v = __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t v = __hip_atomic_load(p + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             g[2 * k] = (uint32_t)v;
             g[2 * k + 1] = (uint32_t)(v >> 32);
         }
@@ -1173,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_delta_finish(const uint8_t *bsums, int3
     const uint32_t chunk = (ns + 255) / 256, q0 = t * chunk < ns ? t * chunk : ns,
                    q1 = q0 + chunk < ns ? q0 + chunk : ns;
     int32_t run = 0;
-    for (uint32_t q = q0; q < q1; q++) run += __hip_atomic_load(scnt + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t q = q0; q < q1; q++) run += __hip_atomic_load(scnt + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     int32_t x = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1187,7 +1173,7 @@ __global__ __launch_bounds__(256) void k_delta_finish(const uint8_t *bsums, int3
     for (uint32_t w = 0; w < (t >> 6); w++) pre += wsum[w];
     for (uint32_t q = q0; q < q1; q++) {
         sblk[q] = pre;
-        pre += __hip_atomic_load(scnt + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pre += __hip_atomic_load(scnt + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t == 255) *total = pre;
     if (t == 0) *ticket = 0u;
@@ -1617,6 +1603,19 @@ struct KeyOps final : StoreKeyOps {
         return hipGetLastError();
     }
 
+    hipError_t keep_last_rows(const uint8_t *skeys, const uint32_t *pos, uint64_t m, uint32_t *keep,
+                              hipStream_t st) override {
+        hipLaunchKernelGGL((k_keep_last<KK, KL>), g1(m + 1), dim3(256), 0, st, skeys, pos, m, keep);
+        return hipGetLastError();
+    }
+
+    hipError_t sample_stride(const uint8_t *keys, uint64_t n, uint64_t stride, uint64_t *smp, hipStream_t st) override {
+        const uint64_t ns = (n + stride - 1) / stride;
+        if (ns == 0) return hipSuccess;
+        hipLaunchKernelGGL((k_sample<KK, KL>), g1(ns), dim3(256), 0, st, keys, n, stride, smp);
+        return hipGetLastError();
+    }
+
     int compare_keys_host(const uint8_t *a, const uint8_t *b) const override {
         if constexpr (KK == KEY_U32) {
             uint32_t x, y;
@@ -1690,6 +1689,34 @@ hipError_t launch_delta_apply(int kk, int kl, const uint8_t *sfps, const uint8_t
     return launch_merge_kernel(kk, kl, 4, dkeys, reinterpret_cast<const uint8_t *>(dslot), nd, skeys, nullptr, m, upos,
                                usrc, rlist, mcnt, okeys, reinterpret_cast<uint8_t *>(oslot), nullptr, nullptr, nullptr,
                                nbk, osmp, osmp2, st, heap, (uint32_t)heap_base, tileU);
+}
+
+hipError_t launch_delta_merge(int kk, int kl, const uint8_t *dkeys, const uint32_t *dslot, uint64_t nd,
+                              const uint8_t *skeys, uint64_t m, const uint32_t *upos, const uint32_t *usrc,
+                              const uint32_t *rlist, const uint64_t *mcnt, uint8_t *okeys, uint32_t *oslot,
+                              uint64_t nbk, uint64_t *osmp, uint64_t *osmp2, const uint8_t *heap, uint64_t heap_base,
+                              hipStream_t st) {
+    if (m == 0 || heap_base + m >= (1ull << 32)) return hipErrorInvalidValue;
+    // a few rows into the run: every tile finds its bounds in the short lists itself
+    return launch_merge_kernel(kk, kl, 4, dkeys, reinterpret_cast<const uint8_t *>(dslot), nd, skeys, nullptr, m, upos,
+                               usrc, rlist, mcnt, okeys, reinterpret_cast<uint8_t *>(oslot), nullptr, nullptr, nullptr,
+                               nbk, osmp, osmp2, st, heap, (uint32_t)heap_base, nullptr);
+}
+
+hipError_t launch_compact_rows(const uint8_t *src, uint32_t row_bytes, const uint32_t *keep, const uint32_t *dst,
+                               uint64_t m, uint8_t *out, hipStream_t st) {
+    if (m == 0 || row_bytes == 0 || !src) return hipSuccess;
+    hipLaunchKernelGGL(k_compact_rows, g1(m), dim3(256), 0, st, src, row_bytes, keep, dst, m, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, Scratch &s, hipStream_t st) {
+    size_t tb = 0;
+    hipError_t e;
+    if ((e = rocprim::exclusive_scan(nullptr, tb, in, out, 0u, n, rocprim::plus<uint32_t>(), st))) return e;
+    void *tmp = s.bytes(tb);
+    if (s.err) return s.err;
+    return rocprim::exclusive_scan(tmp, tb, in, out, 0u, n, rocprim::plus<uint32_t>(), st);
 }
 
 hipError_t launch_compact(int kk, int kl, const uint8_t *bkeys, const uint8_t *bfps, uint64_t nb, const uint8_t *dkeys,

@@ -144,6 +144,11 @@ struct StoreKeyOps {
                                   uint8_t *ofps, uint64_t *counts, hipStream_t st) = 0;
     virtual hipError_t bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key, int lo_kind,
                               const uint8_t *hi_key, int hi_kind, uint64_t *qlo, uint64_t *qhi, hipStream_t st) = 0;
+    // keep[i] (i < m) = 1 unless input row i's sorted successor has its key; keep[m] = 0
+    virtual hipError_t keep_last_rows(const uint8_t *skeys, const uint32_t *pos, uint64_t m, uint32_t *keep,
+                                      hipStream_t st) = 0;
+    // keys[64 j] leading digits, j < ceil(n / stride): the host tier's sample array
+    virtual hipError_t sample_stride(const uint8_t *keys, uint64_t n, uint64_t stride, uint64_t *smp, hipStream_t st) = 0;
     // the key type's Ord on the host (for argument checks)
     virtual int compare_keys_host(const uint8_t *a, const uint8_t *b) const = 0;
 };
@@ -204,6 +209,22 @@ hipError_t launch_resolve_bounds(const uint32_t *rank, const uint8_t *skind, con
                                  uint64_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
 hipError_t launch_gather_keys(const uint8_t *keys, uint32_t kl, const uint64_t *sel, uint64_t m, uint8_t *out,
                               hipStream_t st);
+// The delta merge alone (the small-batch path, small_batch.hpp): batch rows skeys [0, m) with the
+// lists and counts (mcnt) its front wrote, merged into the delta run (keys + slots) -- the last
+// step of launch_delta_apply.
+hipError_t launch_delta_merge(int kk, int kl, const uint8_t *dkeys, const uint32_t *dslot, uint64_t nd,
+                              const uint8_t *skeys, uint64_t m, const uint32_t *upos, const uint32_t *usrc,
+                              const uint32_t *rlist, const uint64_t *mcnt, uint8_t *okeys, uint32_t *oslot,
+                              uint64_t nbk, uint64_t *osmp, uint64_t *osmp2, const uint8_t *heap, uint64_t heap_base,
+                              hipStream_t st);
+// A batch with repeated keys reduced to the last row of each key, in input order (the staged
+// batch's rule, rh_store_stage): keep[i] = 1 unless input row i's sorted successor (pos: each input
+// row's sorted row, skeys: the stable key sort) has the same key; keep[m] = 0 (for the scan).
+// Then dst = the exclusive scan of keep over m + 1 entries (dst[m] = rows kept), and each column
+// compacted with launch_compact_rows.
+hipError_t launch_compact_rows(const uint8_t *src, uint32_t row_bytes, const uint32_t *keep, const uint32_t *dst,
+                               uint64_t m, uint8_t *out, hipStream_t st);
+hipError_t launch_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, Scratch &s, hipStream_t st);
 // pre-size the scratch slots a compaction of up to `plan` delta rows and a batch of `batch` rows use
 hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch);
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);

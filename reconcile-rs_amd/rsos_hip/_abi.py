@@ -103,6 +103,7 @@ SIGNATURES = [
     ("rh_store_stage", C.c_int, [P, C.POINTER(Columns), U8P, SZ]),
     ("rh_store_reserve", C.c_int, [P, C.c_uint64, C.c_uint64]),
     ("rh_store_stats", C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("rh_store_batch_stats", C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("rh_store_tier_stats", C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64)]),
     ("rh_snapshot_header", C.c_int, [VP, SZ, C.POINTER(C.c_uint64)]),

@@ -179,6 +179,19 @@ class GpuFingerprintStore:
         A.check(A.lib().rh_store_stats(self._h, C.byref(b), C.byref(d), C.byref(c)), "rh_store_stats")
         return {"base_rows": int(b.value), "delta_rows": int(d.value), "compactions": int(c.value)}
 
+    def batch_stats(self) -> Dict[str, int]:
+        """Batches applied by the small-batch path and by the large-batch path (rh_store_batch_stats)."""
+        a, b = C.c_uint64(), C.c_uint64()
+        A.check(A.lib().rh_store_batch_stats(self._h, C.byref(a), C.byref(b)), "rh_store_batch_stats")
+        return {"small": int(a.value), "large": int(b.value)}
+
+    def stage(self, cols: Dict[str, np.ndarray], ops: np.ndarray) -> None:
+        """Queue host rows (rh_store_stage): applied as one batch by the next call that reads the
+        store; a key staged more than once keeps its last operation."""
+        c, held = self._columns(cols)
+        ops_a = np.ascontiguousarray(ops, dtype=np.uint8)
+        A.check(A.lib().rh_store_stage(self._h, C.byref(c), _np_ptr(ops_a), len(ops_a)), "rh_store_stage")
+
     def tier_stats(self) -> Dict[str, int]:
         """The host tier's bookkeeping (rh_store_tier_stats): rows of its base copy and entries of
         its delta tree while fresh, full refreshes (base copies) and batch folds so far."""

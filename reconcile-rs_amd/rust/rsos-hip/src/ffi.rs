@@ -167,6 +167,7 @@ extern "C" {
     pub fn rh_store_reserve(store: *mut rh_store, rows: u64, batch_rows: u64) -> c_int;
     pub fn rh_store_stats(store: *mut rh_store, base_rows: *mut u64, delta_rows: *mut u64,
                           compactions: *mut u64) -> c_int;
+    pub fn rh_store_batch_stats(store: *mut rh_store, small_batches: *mut u64, large_batches: *mut u64) -> c_int;
     pub fn rh_snapshot_header(bytes: *const c_void, len: usize, entries: *mut u64) -> c_int;
     pub fn rh_snapshot_decode_device(schema: *const rh_schema, key_form: c_int, dev_bytes: *const c_void, len: usize,
                                      dev_out: *const rh_columns, cap: usize, info: *mut rh_snapshot_info,

@@ -271,13 +271,21 @@ int rh_store_protocol_round(rh_store *store, int policy, uint64_t fan_out, const
 int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
 /* The tier after a batch (host_tier.hpp, host_delta.hpp): the tier holds a copy of the device's
  * base run plus a B+ tree of the signed deltas of every batch since (the device's own DeltaRecs,
- * count and contribution per touched key), so a batch updates it in O(batch log n) -- the
- * reference's O(log n) per insert (mutate.rs:23-88) -- and only a base copy older than
- * max(base / 8, 2^16) delta entries, a load, or a moved tier buffer costs the O(n) copy again.
- * Stats (nullable): base rows and delta entries of a fresh tier (0, 0 when stale), full refreshes
- * and batch folds so far.                                                                       */
+ * count and contribution per touched key), so a batch of up to max(2^16, min(base / 8, 2^18)) rows
+ * updates it in O(batch log n) -- the reference's O(log n) per insert (mutate.rs:23-88).  A load,
+ * a larger batch, or a tree past that size refreshes the copy IN THE BACKGROUND: the device
+ * compacts and a copy stream brings the new base down into a second page-locked set; a tier
+ * that is still fresh keeps answering meanwhile (the batches applied meanwhile are logged and
+ * replayed into the new copy's tree), a stale one hands the questions to the device (its delta
+ * run is then empty: no question compacts) -- so no question waits for the O(n) copy.  The next
+ * write after a load or a large batch waits for the copy instead.
+ * Stats (nullable): base rows and delta entries of a fresh tier (0, 0 when stale), refreshes
+ * swapped in and batch folds so far.                                                            */
 int rh_store_tier_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_entries, uint64_t *refreshes,
                         uint64_t *folds);
+/* Wait until the host tier is fresh (a background refresh landed and swapped in, one started if
+ * none was under way): a warm store for benchmarks and tests.  No-op with the tier off.          */
+int rh_store_tier_sync(rh_store *store);
 
 /* Staged single-record updates: Rsos::insert / delete one record at a time (mutate.rs:23-154)
  * without one device round trip each.  rh_store_stage appends m host rows (columns as for

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "../../include/rsos_hip.h"
@@ -184,7 +185,7 @@ public:
     // insert or replace the entry of r.key
     void upsert(const Rec &r) {
         if (!root) {
-            root = new Leaf();
+            root = new_leaf();
             first_leaf = static_cast<Leaf *>(root);
         }
         if (height == 0 ? static_cast<Leaf *>(root)->n == LF : static_cast<Node *>(root)->n == NF) grow_root();
@@ -324,7 +325,7 @@ public:
         std::vector<Sum> sums;
         Leaf *prev = nullptr;
         for (size_t i = 0; i < n; i += FILL) {
-            Leaf *l = new Leaf();
+            Leaf *l = new_leaf();
             const int k = (int)std::min<size_t>(FILL, n - i);
             memcpy(l->keys, keys + i * ko.kl, (size_t)k * ko.kl);
             memcpy(l->fp, fps + 4 * i, (size_t)k * 32);
@@ -347,7 +348,7 @@ public:
             std::vector<void *> up;
             std::vector<Sum> upsums;
             for (size_t i = 0; i < level.size(); i += FILL) {
-                Node *nd = new Node();
+                Node *nd = new_node();
                 const int k = (int)std::min<size_t>(FILL, level.size() - i);
                 Sum s{0, 0, {0, 0, 0, 0}};
                 for (int q = 0; q < k; q++) {
@@ -371,22 +372,34 @@ public:
     }
 
 private:
+    // Key storage is sized by the store's key length (LF * kl bytes after the fixed part), not by
+    // the longest key: ~57 B per entry at the bulk fill for 8- and 16-byte keys.
     struct Leaf {
         int n = 0;
         Leaf *next = nullptr;
-        uint8_t keys[LF * KMAX];
         uint64_t fp[LF][4];
         int8_t cnt[LF];
         uint8_t live[LF];
+        uint8_t keys[];  // LF * kl bytes
     };
     struct Node {
         int n = 0;
         void *ch[NF];
-        uint8_t sep[NF * KMAX];  // sep[c] <= every key of child c (c >= 1), > every key of child c - 1
         uint64_t size[NF];
         int64_t cnt[NF];
         uint64_t fp[NF][4];
+        uint8_t sep[];  // NF * kl bytes: sep[c] <= every key of child c (c >= 1), > every key of child c - 1
     };
+    Leaf *new_leaf() const { return new (::operator new(sizeof(Leaf) + (size_t)LF * ko.kl)) Leaf(); }
+    Node *new_node() const { return new (::operator new(sizeof(Node) + (size_t)NF * ko.kl)) Node(); }
+    static void del_leaf(Leaf *l) {
+        l->~Leaf();
+        ::operator delete(l);
+    }
+    static void del_node(Node *nd) {
+        nd->~Node();
+        ::operator delete(nd);
+    }
     KeyOrder ko{};
     void *root = nullptr;
     int height = 0;  // inner levels above the leaves
@@ -398,12 +411,12 @@ private:
     void free_sub(void *p, int h) {
         if (!p) return;
         if (h == 0) {
-            delete static_cast<Leaf *>(p);
+            del_leaf(static_cast<Leaf *>(p));
             return;
         }
         Node *nd = static_cast<Node *>(p);
         for (int i = 0; i < nd->n; i++) free_sub(nd->ch[i], h - 1);
-        delete nd;
+        del_node(nd);
     }
     // child of nd that holds z: the number of separators sep[1..n) that are <= z
     int route(const Node *nd, const uint8_t *z) const {
@@ -439,7 +452,7 @@ private:
         return static_cast<const Node *>(p)->sep;
     }
     void grow_root() {
-        Node *r = new Node();
+        Node *r = new_node();
         r->n = 1;
         r->ch[0] = root;
         r->size[0] = total_size;
@@ -459,7 +472,7 @@ private:
         const uint8_t *ysep;
         if (leaf) {
             Leaf *x = static_cast<Leaf *>(nd->ch[c]);
-            Leaf *l = new Leaf();
+            Leaf *l = new_leaf();
             const int mid = x->n / 2, k = x->n - mid;
             memcpy(l->keys, x->keys + mid * ko.kl, (size_t)k * ko.kl);
             memcpy(l->fp, x->fp[mid], (size_t)k * 32);
@@ -475,7 +488,7 @@ private:
             ysep = l->keys;
         } else {
             Node *x = static_cast<Node *>(nd->ch[c]);
-            Node *r = new Node();
+            Node *r = new_node();
             const int mid = x->n / 2, k = x->n - mid;
             memcpy(r->ch, x->ch + mid, (size_t)k * sizeof(void *));
             memcpy(r->sep, x->sep + mid * ko.kl, (size_t)k * ko.kl);

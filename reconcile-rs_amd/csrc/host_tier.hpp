@@ -37,28 +37,40 @@ struct HostTier {
     uint64_t n = 0;                    // live keys: nb + Σ count deltas
     const uint8_t *keys = nullptr;     // nb * kl bytes, rank order
     const uint64_t *prefix = nullptr;  // (nb + 1) * 4 LE limbs
-    std::vector<uint64_t> samp;        // digit(keys[64 j])
+    const uint64_t *samp = nullptr;    // digit(keys[64 j]), j < ns
+    uint64_t ns = 0;
+    std::vector<uint64_t> samp_own;    // ... when build() forms them itself
     DeltaTree dt;
     static constexpr unsigned SHIFT = 6;
 
     uint64_t digit(const uint8_t *k) const { return ko.digit(k); }
     int cmp(const uint8_t *a, const uint8_t *b) const { return ko.cmp(a, b); }
-    void build(uint32_t key_len, int key_kind, uint64_t rows, const uint8_t *k, const uint64_t *p) {
+    // smp (optional): the samples, formed on the device with the copy (k_sample, stride 64)
+    void build(uint32_t key_len, int key_kind, uint64_t rows, const uint8_t *k, const uint64_t *p,
+               const uint64_t *smp = nullptr) {
         ko = KeyOrder{key_len, key_kind};
         kl = key_len;
         nb = n = rows;
         keys = k;
         prefix = p;
         dt.set_order(ko);
-        samp.clear();
+        samp_own.clear();
+        samp = nullptr;
+        ns = 0;
         if (!keys) return;  // the encoded store keeps its keys on the host side of the ABI
-        samp.resize((nb + 63) >> SHIFT);
-        for (uint64_t j = 0; j < samp.size(); j++) samp[j] = digit(keys + (j << SHIFT) * kl);
+        ns = (nb + 63) >> SHIFT;
+        if (smp) {
+            samp = smp;
+            return;
+        }
+        samp_own.resize(ns);
+        for (uint64_t j = 0; j < ns; j++) samp_own[j] = digit(keys + (j << SHIFT) * kl);
+        samp = samp_own.data();
     }
     // forget everything (tier off)
     void reset() {
         build(0, RH_KEY_BYTES, 0, nullptr, nullptr);
-        samp = std::vector<uint64_t>();
+        samp_own = std::vector<uint64_t>();
         segs = std::vector<Seg>();
     }
     bool plain() const { return dt.size() == 0; }
@@ -100,8 +112,8 @@ struct HostTier {
     uint64_t rank_b(const uint8_t *key) const {
         if (nb == 0) return 0;
         const uint64_t d = digit(key);
-        const uint64_t jl = std::lower_bound(samp.begin(), samp.end(), d) - samp.begin();
-        const uint64_t jh = std::upper_bound(samp.begin() + jl, samp.end(), d) - samp.begin();
+        const uint64_t jl = std::lower_bound(samp, samp + ns, d) - samp;
+        const uint64_t jh = std::upper_bound(samp + jl, samp + ns, d) - samp;
         uint64_t lo = jl ? ((jl - 1) << SHIFT) + 1 : 0;  // keys[64 (jl - 1)] < key
         uint64_t hi = std::min<uint64_t>(nb, jh << SHIFT);  // keys[64 jh] > key
         while (lo < hi) {

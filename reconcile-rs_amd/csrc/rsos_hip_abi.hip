@@ -822,25 +822,24 @@ struct rh_store {
         out[0] = out[1] = out[2] = 0;
         if (m == 0 || m > small_limit()) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
-        const int fmode = fold_mode();
+        if ((rc = pre_batch())) return rc;
+        int fmode = fold_mode(m);
+        bool want = fold_rows_wanted(fmode);
+        if (want && !fold_room(m)) fmode = 0, want = false, rf_log_ok = false;  // the tier goes stale
         if ((rc = skeys.ensure(m * kl + 64)) || (rc = delta_capacity(m))) return rc;
         uint32_t *upos = scratch.u32(3, m + 1), *usrc = scratch.u32(4, m + 1), *rlist = scratch.u32(5, m + 1);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         uint64_t *res = nullptr;
-        uint8_t *fk = nullptr, *fr = nullptr, *fd = nullptr;
+        uint8_t *fk = nullptr, *fr = nullptr, *fd = nullptr, *ff = nullptr, *fo = nullptr;
         try {
             sb_res.resize(16);
-            if (fmode) {
-                fold_keys.resize(m * kl + 8);
-                fold_recs.resize(m * sizeof(rh::DeltaRec) + 8);
-                fold_ops.resize(m + 8);
-            }
         } catch (const std::bad_alloc &) {
             return fail(RH_ERR_OOM, "small batch: page-locked allocation failed");
         }
         if ((rc = dev_ptr(sb_res.data(), &res))) return rc;
-        if (fmode && ((rc = dev_ptr(fold_keys.data(), &fk)) || (rc = dev_ptr(fold_recs.data(), &fr)) ||
-                      (rc = dev_ptr(fold_ops.data(), &fd))))
+        if (want && ((rc = dev_ptr(fold_keys.data(), &fk)) || (rc = dev_ptr(fold_recs.data(), &fr)) ||
+                     (rc = dev_ptr(fold_ops.data(), &fd)) || (rc = dev_ptr(fold_fps.data(), &ff)) ||
+                     (rc = dev_ptr(fold_sops.data(), &fo))))
             return rc;
         const int nxt = 1 - cd;
         rh::SmallBatch a{};
@@ -859,21 +858,24 @@ struct rh_store {
         a.upos = upos, a.usrc = usrc, a.rlist = rlist;
         a.mcnt = mcnt.p;
         a.res = res;
-        a.fold = fmode;
-        a.fkeys = fk, a.frecs = fr, a.fdrop = fd;
+        a.fkeys = fk, a.frecs = fr, a.fdrop = fd, a.ffps = ff, a.fops = fo;
         bool supported = false;
         hipError_t e = rh::launch_small_batch_schema(schema.key_kind, (int)schema.key_len, schema.value_kind,
                                                      (int)schema.value_len, schema.record_kind, c.tags != nullptr, a,
                                                      stream, &supported);
         if (e != hipSuccess) return fail(RH_ERR_HIP, std::string("small batch launch: ") + hipGetErrorString(e));
         if (!supported) return RH_OK;
+        const uint64_t version0 = version;
         version++;  // from here on the batch may commit
         RH_HIP(rh::launch_delta_merge(schema.key_kind, (int)kl, dkeys[cd].p, dslot[cd].p, nd, skeys.p, m, upos, usrc, rlist,
                                       mcnt.p, dkeys[nxt].p, dslot[nxt].p, rh_num_blocks(nd + m), dsmp[nxt].p,
                                       dsmp2[nxt].p, dheap.p, heap_len, stream));
         if ((rc = sync())) return rc;
         const uint64_t *h = sb_res.data();
-        if (h[6] & 1) return fail(RH_ERR_ARG, "duplicate key within one batch");
+        if (h[6] & 1) {  // nothing committed
+            version = version0;
+            return fail(RH_ERR_ARG, "duplicate key within one batch");
+        }
         const uint64_t kept = h[12];
         int64_t dcnt;
         memcpy(&dcnt, &h[7], 8);
@@ -886,123 +888,272 @@ struct rh_store {
         dsums_ok = false;
         small_batches++;
         *done = true;
-        if (fmode) fold_batch(fmode, kept);
+        fold_batch(fmode, kept, want);
         const uint64_t thresh_now = std::max<uint64_t>(nb / compact_div, compact_min);
         if (nd > thresh_now || heap_len > thresh_now) {
             if ((rc = compact())) return rc;
         }
-        return RH_OK;
+        return post_batch();
     }
     uint64_t small_batches = 0, large_batches = 0;
     // ---- the host tier (host_tier.hpp) ---------------------------------------------------------
     // The tier answers from (its copy of a base run) + (its delta tree: every batch since).  It is
-    // fresh while tier_version == version.  A batch keeps it fresh by folding the batch's signed
-    // deltas into the tree (fold_batch, O(batch)); only a load, a tree grown past the policy's bound,
-    // or a change to the tier's buffers sends the next question through tier_refresh (compact, copy
-    // the whole base down: O(n)).
+    // fresh while tier_version == version.  A batch of up to tree_limit() rows keeps it fresh by
+    // folding the batch's signed deltas into the tree (fold_batch, O(batch log)).  Anything the
+    // tree cannot absorb cheaply -- a load, a larger batch, a tree grown past tree_limit() --
+    // starts a refresh in the background (start_refresh): the device compacts (so its base run is
+    // the whole map), forms the prefix sums and the search samples, and a copy stream brings keys,
+    // prefix sums and samples down into the tier's spare page-locked set.  Meanwhile:
+    //   - if the tier is still fresh (a tree past its limit), it keeps answering, the batches
+    //     applied meanwhile fold into it and are logged for the new copy; the copy is swapped in
+    //     (finish_refresh: the log replayed into a new tree) by the next write or compaction;
+    //   - if it is stale (a load, a large batch), questions are answered by the device (the delta
+    //     run is empty, so no question compacts), and the next write first waits for the copy.
+    // So no question ever pays the O(n) copy (rsos/src/fingerprint_tree_map/query.rs:25-76 never
+    // does); writes pay the compaction, and a write right behind a refresh waits for its copy.
     uint64_t version = 0;       // bumped by every change of contents (load, batch, failed load)
     uint64_t base_epoch = 0;    // bumped whenever the device's base run changes (load, compaction)
     bool tier_on = false;
     uint64_t tier_version = ~0ull, tier_round_max = 128;
     uint64_t tier_epoch = ~0ull;  // the device base the tier's copy is (while they agree, the
                                   // device's DeltaRecs are relative to the tier's base too)
-    uint64_t tier_refreshes = 0, tier_folds = 0;
+    uint64_t tier_refreshes = 0, tier_folds = 0, tier_waits = 0;
     rh::HostTier tier;
-    PinnedVec<uint8_t> tier_keys;
-    PinnedVec<uint64_t> tier_prefix;
+    struct TierSet {  // a base copy: keys in rank order, exclusive prefix sums, every 64th key's digit
+        PinnedVec<uint8_t> keys;
+        PinnedVec<uint64_t> prefix, samp;
+        void release() { keys.release(), prefix.release(), samp.release(); }
+    };
+    TierSet tsets[2];
+    int tact = 0;  // the set the tier reads
     DevBuf<uint8_t> tier_dpre, tier_spre, tier_bpre;
+    DevBuf<uint64_t> tier_dsmp;
     std::vector<uint8_t> tier_out;  // the last host round, in round_layout()
-    // a batch's rows as the fold reads them: sorted keys, and either the device's DeltaRecs + drop
-    // flags (tier base == device base) or the sorted fingerprints + ops (the tier's own base)
-    PinnedVec<uint8_t> fold_keys, fold_recs, fold_ops;
+    // A/B switch and test hook: RSOS_HIP_TIER_TREE=<entries> sets the tree limit (read at creation)
+    uint64_t tree_env = getenv("RSOS_HIP_TIER_TREE") ? strtoull(getenv("RSOS_HIP_TIER_TREE"), nullptr, 10) : 0;
+    // the largest delta tree the tier keeps, and the largest batch it folds: a tree of this size
+    // still answers a question in about a microsecond (host_delta.hpp)
+    uint64_t tree_limit() const {
+        if (tree_env) return tree_env;
+        return std::max<uint64_t>(1ull << 16, std::min<uint64_t>(tier.nb / 8, 1ull << 18));
+    }
+    // the refresh in flight (one at a time): its copy into tsets[rf_set] lands at rf_ev on cstream
+    bool rf_on = false, refresh_wanted = false;
+    int rf_set = 1;
+    uint64_t rf_version = 0, rf_epoch = 0, rf_nb = 0;
+    hipStream_t cstream = nullptr;
+    hipEvent_t rf_ready = nullptr, rf_ev = nullptr;
+    // the batches applied while the copy is in flight, as mode-1 rows against its base (which is
+    // the device's base until the next compaction, and no compaction runs while a copy is in
+    // flight): replayed into the new copy's tree when it is swapped in
+    struct LogBatch {
+        size_t off, m;
+    };
+    std::vector<LogBatch> rf_log;
+    std::vector<uint8_t> rf_keys, rf_recs, rf_drop;
+    bool rf_log_ok = true;
+    uint64_t rf_log_version = 0;
+    // a batch's rows as the folds read them, in key order: keys, the device's DeltaRecs and drop
+    // flags (against the device's base), the fingerprints and ops (against the tier's own base)
+    PinnedVec<uint8_t> fold_keys, fold_recs, fold_ops, fold_fps, fold_sops;
     bool tier_fresh() const { return tier_on && tier_version == version; }
-    // bring the host tier up to date: compact, the prefix sums on the device, one copy of the keys
-    // and one of the prefix sums down.  Costs ~(kl + 32) B per row of PCIe, once per base change.
-    int tier_refresh() {
+    // Start a refresh of the host tier: compact, the prefix sums and samples on the device, and
+    // their copy down on the copy stream into the spare set.  Returns at once (no wait).
+    int start_refresh() {
         int rc;
-        if ((rc = compact())) return rc;
-        const uint64_t n = nb, nbk = rh_num_blocks(n), ns = rh_num_superblocks(n);
-        if ((rc = tier_dpre.ensure((n + 1) * 32 + 64)) || (rc = tier_spre.ensure((ns + 1) * 32 + 64)) ||
-            (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)))
-            return rc;
-        if ((rc = tier_reserve(n + n / 4))) return rc;  // headroom: a growing map re-pins rarely
-        tier_keys.resize(n * kl + 64);
-        tier_prefix.resize((n + 1) * 4 + 8);
-        if (n) {
-            RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, stream));
-            RH_HIP(hipMemcpyAsync(tier_keys.data(), bkeys[cb].p, n * kl, hipMemcpyDeviceToHost, stream));
-            RH_HIP(hipMemcpyAsync(tier_prefix.data(), tier_dpre.p, (n + 1) * 32, hipMemcpyDeviceToHost, stream));
-            if ((rc = sync())) return rc;
-        } else {
-            memset(tier_prefix.data(), 0, 32);
+        if (!tier_on) return RH_OK;
+        if (rf_on) {  // one copy at a time: the next one starts once it has landed
+            refresh_wanted = true;
+            return RH_OK;
         }
-        tier.build((uint32_t)kl, schema.key_kind, n, tier_keys.data(), tier_prefix.data());
-        tier_version = version;
-        tier_epoch = base_epoch;
-        tier_refreshes++;
-        return RH_OK;
-    }
-    // How a batch reaches the tier (decided before the batch, under the lock):
-    //   0: it does not (tier off or stale: the next question refreshes it anyway),
-    //   1: from the device's DeltaRecs (the tier's base is the device's: contribs relative to it),
-    //   2: from the batch's sorted fingerprints and ops, the deltas formed against the tier's own
-    //      base on the host (the device compacted since the tier's copy was taken).
-    int fold_mode() const {
-        if (!tier_fresh()) return 0;
-        return tier_epoch == base_epoch ? 1 : 2;
-    }
-    // enqueue the copies fold_batch reads (behind the batch's merge, before its result copy)
-    int fold_copies(int mode, const uint8_t *sorted_keys, const uint8_t *sorted_fps, const uint8_t *sorted_ops,
-                    const uint8_t *recs, const uint8_t *drop, size_t m) {
-        try {
-            fold_keys.resize(m * kl + 8);
-            fold_recs.resize(m * (mode == 1 ? sizeof(rh::DeltaRec) : 32) + 8);
-            fold_ops.resize(m + 8);
+        if ((rc = compact())) return rc;
+        if (!cstream) {
+            RH_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+            RH_HIP(hipEventCreateWithFlags(&rf_ready, hipEventDisableTiming));
+            RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
+        }
+        const uint64_t n = nb, nbk = rh_num_blocks(n), ns = rh_num_superblocks(n), nsmp = (n + 63) / 64;
+        if ((rc = tier_dpre.ensure((n + 1) * 32 + 64)) || (rc = tier_spre.ensure((ns + 1) * 32 + 64)) ||
+            (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)) || (rc = tier_dsmp.ensure(nsmp + 8)))
+            return rc;
+        const int spare = 1 - tact;
+        TierSet &S = tsets[spare];
+        try {  // headroom: a growing map re-pins rarely
+            S.keys.reserve((n + n / 4) * kl + 64);
+            S.prefix.reserve((n + n / 4 + 1) * 4 + 8);
+            S.samp.reserve((n + n / 4) / 64 + 16);
+            S.keys.resize(n * kl + 64);
+            S.prefix.resize((n + 1) * 4 + 8);
+            S.samp.resize(nsmp + 8);
         } catch (const std::bad_alloc &) {
             return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
         }
-        RH_HIP(hipMemcpyAsync(fold_keys.data(), sorted_keys, m * kl, hipMemcpyDeviceToHost, stream));
-        if (mode == 1) {
-            RH_HIP(hipMemcpyAsync(fold_recs.data(), recs, m * sizeof(rh::DeltaRec), hipMemcpyDeviceToHost, stream));
-            RH_HIP(hipMemcpyAsync(fold_ops.data(), drop, m, hipMemcpyDeviceToHost, stream));
-        } else {
-            RH_HIP(hipMemcpyAsync(fold_recs.data(), sorted_fps, m * 32, hipMemcpyDeviceToHost, stream));
-            RH_HIP(hipMemcpyAsync(fold_ops.data(), sorted_ops, m, hipMemcpyDeviceToHost, stream));
+        if (n) {
+            RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, stream));
+            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 64, tier_dsmp.p, stream));
         }
+        RH_HIP(hipEventRecord(rf_ready, stream));
+        RH_HIP(hipStreamWaitEvent(cstream, rf_ready, 0));
+        if (n) {
+            RH_HIP(hipMemcpyAsync(S.keys.data(), bkeys[cb].p, n * kl, hipMemcpyDeviceToHost, cstream));
+            RH_HIP(hipMemcpyAsync(S.prefix.data(), tier_dpre.p, (n + 1) * 32, hipMemcpyDeviceToHost, cstream));
+            RH_HIP(hipMemcpyAsync(S.samp.data(), tier_dsmp.p, nsmp * 8, hipMemcpyDeviceToHost, cstream));
+        } else {
+            memset(S.prefix.data(), 0, 32);
+        }
+        RH_HIP(hipEventRecord(rf_ev, cstream));
+        rf_on = true;
+        refresh_wanted = false;
+        rf_set = spare;
+        rf_version = rf_log_version = version;
+        rf_epoch = base_epoch;
+        rf_nb = n;
+        rf_log.clear();
+        rf_keys.clear(), rf_recs.clear(), rf_drop.clear();
+        rf_log_ok = true;
         return RH_OK;
+    }
+    // The copy has landed: the new set becomes the tier's, the logged batches folded into its tree.
+    void finish_refresh() {
+        rf_on = false;
+        tact = rf_set;
+        TierSet &S = tsets[tact];
+        tier.build((uint32_t)kl, schema.key_kind, rf_nb, S.keys.data(), S.prefix.data(), S.samp.data());
+        tier_epoch = rf_epoch;
+        tier_refreshes++;
+        bool ok = rf_log_ok && rf_log_version == version;
+        std::vector<rh::DeltaTree::Rec> rows;
+        try {
+            for (const LogBatch &b : rf_log) {
+                rows.resize(b.m);
+                for (size_t j = 0; j < b.m; j++) {
+                    const size_t i = b.off + j;
+                    rec_row(rf_keys.data() + i * kl, reinterpret_cast<const rh::DeltaRec *>(rf_recs.data()) + i, &rows[j]);
+                }
+                tier.fold(rows.data(), rf_drop.data() + b.off, b.m);
+            }
+        } catch (const std::bad_alloc &) {
+            ok = false;
+        }
+        tier_version = ok ? version : ~0ull;
+        if (!ok) refresh_wanted = true;
+        rf_log.clear();
+        rf_keys = std::vector<uint8_t>(), rf_recs = std::vector<uint8_t>(), rf_drop = std::vector<uint8_t>();
+    }
+    // Has the copy landed?  wait: block until it has.  Then swap it in.
+    int poll_refresh(bool wait) {
+        if (!rf_on) return RH_OK;
+        const hipError_t e = wait ? hipEventSynchronize(rf_ev) : hipEventQuery(rf_ev);
+        if (e == hipErrorNotReady) return RH_OK;
+        if (e != hipSuccess) {
+            rf_on = false;
+            tier_version = ~0ull;
+            return fail(RH_ERR_HIP, std::string("host tier copy: ") + hipGetErrorString(e));
+        }
+        if (wait) tier_waits++;
+        finish_refresh();
+        return RH_OK;
+    }
+    // Before anything writes what an in-flight copy reads (a compaction, a load, a reservation),
+    // or before a batch while the tier is stale: let the copy land and swap it in.
+    int settle() { return rf_on ? poll_refresh(true) : RH_OK; }
+    // Before a batch: a stale tier waiting for its copy takes it now (so the batch folds into a
+    // fresh tier); a landed copy is swapped in.
+    int pre_batch() { return poll_refresh(rf_on && !tier_fresh()); }
+    // After a batch (committed, folded, logged): start the refresh the tier needs.  A batch the
+    // tier could not take while a copy is in flight hands over to that copy now (the write waits
+    // for it and replays the log), so a question never replays a long log.
+    int post_batch() {
+        int rc;
+        if (!tier_on) return RH_OK;
+        if (rf_on && !tier_fresh() && (rc = settle())) return rc;
+        if (rf_on) return RH_OK;
+        if (!tier_fresh() || refresh_wanted || tier.dt.size() > tree_limit()) return start_refresh();
+        return RH_OK;
+    }
+    // How a batch of m rows reaches the tier (decided before the batch, under the lock):
+    //   0: it does not (tier off or stale, or the batch is larger than the tree takes: the tier
+    //      goes stale and a refresh follows the batch),
+    //   1: from the device's DeltaRecs (the tier's base is the device's: contribs relative to it),
+    //   2: from the batch's sorted fingerprints and ops, the deltas formed against the tier's own
+    //      base on the host (the device compacted since the tier's copy was taken).
+    int fold_mode(size_t m) const {
+        if (!tier_fresh() || m > tree_limit()) return 0;
+        return tier_epoch == base_epoch ? 1 : 2;
+    }
+    // whether the batch's rows must come down at all (a fold, or a refresh in flight to log for)
+    bool fold_rows_wanted(int fmode) const { return fmode != 0 || rf_on; }
+    // page-locked room for a batch's fold rows (a failure leaves the tier stale, never fails the batch)
+    bool fold_room(size_t m) {
+        try {
+            fold_keys.resize(m * kl + 8);
+            fold_recs.resize(m * sizeof(rh::DeltaRec) + 8);
+            fold_ops.resize(m + 8);
+            fold_fps.resize(m * 32 + 8);
+            fold_sops.resize(m + 8);
+        } catch (const std::bad_alloc &) {
+            return false;
+        }
+        return true;
+    }
+    // enqueue the copies the folds read (behind the batch's merge, before its result copy)
+    int fold_copies(const uint8_t *sorted_keys, const uint8_t *sorted_fps, const uint8_t *sorted_ops,
+                    const uint8_t *recs, const uint8_t *drop, size_t m) {
+        RH_HIP(hipMemcpyAsync(fold_keys.data(), sorted_keys, m * kl, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(fold_recs.data(), recs, m * sizeof(rh::DeltaRec), hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(fold_ops.data(), drop, m, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(fold_fps.data(), sorted_fps, m * 32, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(fold_sops.data(), sorted_ops, m, hipMemcpyDeviceToHost, stream));
+        return RH_OK;
+    }
+    // a mode-1 row: the device's DeltaRec of a key
+    static void rec_row(const uint8_t *key, const rh::DeltaRec *d, rh::DeltaTree::Rec *r) {
+        r->key = key;
+        memcpy(r->fp, d->contrib, 32);
+        const bool in_b = d->flags & rh::DeltaRec::IN_BASE, live = d->flags & rh::DeltaRec::LIVE;
+        r->cnt = (int8_t)((live ? 1 : 0) - (in_b ? 1 : 0));
+        r->live = live;
     }
     // After the batch committed (the copies have landed): the batch's rows into the tier's delta
     // tree, in key order -- the same rule as k_delta_build: an upsert's entry is (cur - base,
     // 1 - in_base, live), a delete of a base key (-base, -1, dead), a delete of any other key drops
-    // its entry.  Keeps the tier fresh; a tree past max(base / 8, 2^16) entries is left stale
-    // instead (the next question copies the base again, resetting the tree).
+    // its entry.  Keeps the tier fresh.  With a refresh in flight the rows are also logged for it.
     std::vector<rh::DeltaTree::Rec> fold_rows;
     std::vector<uint8_t> fold_drop;
-    void fold_batch(int mode, size_t m) {
+    void fold_batch(int mode, size_t m, bool copied) {
+        if (rf_on) {  // the log for the copy in flight (mode-1 rows against its base)
+            if (!copied || rf_keys.size() / kl + m > 2 * tree_limit()) {
+                rf_log_ok = false;
+            } else if (rf_log_ok) {
+                try {
+                    rf_log.push_back(LogBatch{rf_keys.size() / kl, m});
+                    rf_keys.insert(rf_keys.end(), fold_keys.data(), fold_keys.data() + m * kl);
+                    rf_recs.insert(rf_recs.end(), fold_recs.data(), fold_recs.data() + m * sizeof(rh::DeltaRec));
+                    rf_drop.insert(rf_drop.end(), fold_ops.data(), fold_ops.data() + m);
+                    rf_log_version = version;
+                } catch (const std::bad_alloc &) {
+                    rf_log_ok = false;
+                }
+            }
+        }
+        if (!mode || !copied) return;
         rh::HostTier &t = tier;
-        const uint64_t limit = std::max<uint64_t>(t.nb / 8, 1ull << 16);
-        if (t.dt.size() + m > limit) return;  // stays stale
         try {
             fold_rows.resize(m);
             fold_drop.resize(m);
         } catch (const std::bad_alloc &) {
-            return;
+            return;  // stays stale
         }
         const uint8_t *K = fold_keys.data();
         for (size_t j = 0; j < m; j++) {
             rh::DeltaTree::Rec &r = fold_rows[j];
-            r.key = K + j * kl;
             if (mode == 1) {
-                const rh::DeltaRec *d = reinterpret_cast<const rh::DeltaRec *>(fold_recs.data()) + j;
-                memcpy(r.fp, d->contrib, 32);
-                const bool in_b = d->flags & rh::DeltaRec::IN_BASE, live = d->flags & rh::DeltaRec::LIVE;
-                r.cnt = (int8_t)((live ? 1 : 0) - (in_b ? 1 : 0));
-                r.live = live;
+                rec_row(K + j * kl, reinterpret_cast<const rh::DeltaRec *>(fold_recs.data()) + j, &r);
                 fold_drop[j] = fold_ops[j] != 0;
             } else {
                 uint64_t cur[4];
-                memcpy(cur, fold_recs.data() + 32 * j, 32);
-                fold_drop[j] = t.entry_vs_base(r.key, fold_ops[j] ? nullptr : cur, &r);
+                memcpy(cur, fold_fps.data() + 32 * j, 32);
+                fold_drop[j] = t.entry_vs_base(K + j * kl, fold_sops[j] ? nullptr : cur, &r);
             }
         }
         t.fold(fold_rows.data(), fold_drop.data(), m);
@@ -1129,6 +1280,7 @@ struct rh_store {
         int rc;
         // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
         version++;
         base_epoch++;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
@@ -1167,6 +1319,7 @@ struct rh_store {
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         const int nxt = 1 - cb;
         int rc;
+        if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
         if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) ||
             (rc = sbsums.ensure(rh_num_blocks(m) * 32 + 32)) || (rc = sssums.ensure(rh_num_superblocks(m) * 32 + 32)) ||
             (rc = sbsmp.ensure(rh_num_blocks(m) + 1)) || (rc = sbsmp2.ensure(rh::sample2_entries(m))) ||
@@ -1215,20 +1368,24 @@ struct rh_store {
     // stale: its pointers are re-taken by the next refresh, never read after the move.
     int tier_reserve(uint64_t rows) {
         if (!tier_on) return RH_OK;
-        const void *k0 = tier_keys.p, *p0 = tier_prefix.p;
+        const void *k0 = tsets[tact].keys.p, *p0 = tsets[tact].prefix.p, *s0 = tsets[tact].samp.p;
         try {
-            tier_keys.reserve(rows * kl + 64);
-            tier_prefix.reserve((rows + 1) * 4 + 8);
+            for (TierSet &S : tsets) {
+                S.keys.reserve(rows * kl + 64);
+                S.prefix.reserve((rows + 1) * 4 + 8);
+                S.samp.reserve(rows / 64 + 16);
+            }
         } catch (const std::bad_alloc &) {
             tier_version = ~0ull;
             return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
         }
-        if (tier_keys.p != k0 || tier_prefix.p != p0) tier_version = ~0ull;
+        if (tsets[tact].keys.p != k0 || tsets[tact].prefix.p != p0 || tsets[tact].samp.p != s0) tier_version = ~0ull;
         return RH_OK;
     }
     int load_finish(size_t m, bool last_wins) {
-        const int rc = load_finish_rows(m, last_wins);
-        return rc ? rc : tier_reserve(nb + nb / 4);
+        int rc = load_finish_rows(m, last_wins);
+        if (!rc) rc = tier_reserve(nb + nb / 4);
+        return rc ? rc : start_refresh();  // the tier copies the new base in the background
     }
     int load_finish_rows(size_t m, bool last_wins) {
         int rc;
@@ -1262,6 +1419,7 @@ struct rh_store {
     }
     int compact() {  // merge the delta run into the base run
         int rc;
+        if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
         if (nd == 0) return RH_OK;
         if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64))) return rc;
         const int nxt = 1 - cb;
@@ -1463,12 +1621,15 @@ struct rh_store {
         if (next_prepared) *next_prepared = false;
         if (m == 0) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if ((rc = pre_batch())) return rc;
         if (!prepared && !next && m <= small_limit()) {  // the small-batch path: two launches
             bool done = false;
             if ((rc = apply_small(c, ops, m, last_wins, out, &done))) return rc;
             if (done) return RH_OK;
         }
-        const int fmode = fold_mode();  // how this batch reaches a fresh host tier
+        int fmode = fold_mode(m);  // how this batch reaches a fresh host tier
+        bool want = fold_rows_wanted(fmode);
+        if (want && !fold_room(m)) fmode = 0, want = false, rf_log_ok = false;  // the tier goes stale
         const uint64_t version0 = version;
         version++;  // a rejected batch leaves the contents as they were; the tier refreshes anyway
         if ((rc = batch_buffers(m))) return rc;
@@ -1543,9 +1704,8 @@ struct rh_store {
                                           dinb[nxt].p, rh_num_blocks(n_max), mcnt.p, r_merge, dsmp[nxt].p,
                                           dsmp2[nxt].p, results.p + 8, r_dcnt, stream));
             if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-            // the batch's rows for the host tier's fold (only while the tier is fresh)
-            if (fmode &&
-                (rc = fold_copies(fmode, skeys.p, sfps.p, sops.p, dheap.p + heap_len * sizeof(rh::DeltaRec), dops.p, m)))
+            // the batch's rows for the host tier's fold and a refresh's log
+            if (want && (rc = fold_copies(skeys.p, sfps.p, sops.p, dheap.p + heap_len * sizeof(rh::DeltaRec), dops.p, m)))
                 return rc;
             // 5. the one round trip
             RH_HIP(hipMemcpyAsync(host, results.p, 96, hipMemcpyDeviceToHost, stream));
@@ -1587,12 +1747,13 @@ struct rh_store {
         dtotal += dcnt;
         rh_fp_add(root_d, &host[8], root_d);  // mod 2^256
         dsums_ok = false;
-        if (fmode) fold_batch(fmode, m);
+        fold_batch(fmode, m, want);
         // the heap also holds records no row points to any more (overwritten or dropped keys)
         const uint64_t thresh_now = std::max<uint64_t>(nb / compact_div, compact_min);
         if (nd > thresh_now || heap_len > thresh_now) {
             if ((rc = compact())) return rc;
         }
+        if ((rc = post_batch())) return rc;
         return next_rc ? next_rc : RH_OK;
     }
     // A batch with repeated keys, after its sort (scratch u32(7): each input row's sorted row; skeys:
@@ -1919,6 +2080,7 @@ struct rh_store {
     }
     void release() {
         (void)hipStreamSynchronize(stream);
+        if (cstream) (void)hipStreamSynchronize(cstream);
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dslot[k].release();
         }
@@ -1935,7 +2097,11 @@ struct rh_store {
         q_in.release(); q_res.release();
         stage_in.release(); stage_out.release(); stage_out2.release(); load_flag.release();
         r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); pr_out.release();
-        tier_keys.release(); tier_prefix.release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release();
+        tsets[0].release(); tsets[1].release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release(); tier_dsmp.release();
+        if (cstream) (void)hipStreamDestroy(cstream);
+        if (rf_ready) (void)hipEventDestroy(rf_ready);
+        if (rf_ev) (void)hipEventDestroy(rf_ev);
+        cstream = nullptr, rf_ready = rf_ev = nullptr, rf_on = false;
         snap.release();
         sbsums.release(); sssums.release(); sbsmp.release(); sbsmp2.release(); sbtab.release(); sbtabp.release();
         stot.release(); snap_words.release(); snap_hdr.release();
@@ -1972,10 +2138,15 @@ static int tier_ready(rh_store *s) {
     const int frc = flush_locked(s);
     if (frc) return frc;
     if (!s->tier_on) return 0;
-    if (s->tier_fresh()) return 1;
     RH_HIP(hipSetDevice(s->device));
-    const int rc = s->tier_refresh();
-    return rc ? rc : 1;
+    int rc;
+    // a stale tier takes a landed copy now (a fresh one takes it at the next write: no log replay
+    // on a question)
+    if (s->rf_on && !s->tier_fresh() && (rc = s->poll_refresh(false))) return rc;
+    if (s->tier_fresh()) return 1;
+    // stale: the device answers; a refresh is under way (or starts here if none is)
+    if (!s->rf_on && (rc = s->start_refresh())) return rc;
+    return 0;
 }
 
 extern "C" {
@@ -2298,6 +2469,19 @@ int rh_store_tier_stats(rh_store *s, uint64_t *base_rows, uint64_t *delta_entrie
     return RH_OK;
 }
 
+int rh_store_tier_sync(rh_store *s) {
+    if (!s) return fail(RH_ERR_ARG, "store is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    int rc;
+    if ((rc = flush_locked(s))) return rc;
+    if (!s->tier_on) return RH_OK;
+    RH_HIP(hipSetDevice(s->device));
+    if (!s->tier_fresh() && !s->rf_on && (rc = s->start_refresh())) return rc;
+    if ((rc = s->settle())) return rc;
+    if (!s->tier_fresh() && (rc = s->start_refresh()) == RH_OK) rc = s->settle();
+    return rc;
+}
+
 int rh_store_reserve(rh_store *s, uint64_t rows, uint64_t batch_rows) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     if (rows >= (1ull << 31) || batch_rows >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows)");
@@ -2324,20 +2508,25 @@ int rh_store_stage(rh_store *s, const rh_columns *h, const uint8_t *ops, size_t 
 int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
     if (!s || enable < 0 || enable > 1) return fail(RH_ERR_ARG, "bad host tier setting");
     std::lock_guard<std::mutex> g(s->mu);
+    RH_HIP(hipSetDevice(s->device));
+    int rc;
+    if ((rc = s->settle())) return rc;
+    const bool was_on = s->tier_on;
     s->tier_on = enable == 1;
     s->tier_round_max = round_max ? round_max : 128;
     if (s->tier_on) {
-        const int rc = s->tier_reserve(s->nb + s->nd + (s->nb + s->nd) / 4);
-        if (rc) return rc;
+        if ((rc = s->tier_reserve(s->nb + s->nd + (s->nb + s->nd) / 4))) return rc;
+        if (!was_on) {  // the first copy, in the background
+            s->tier_version = ~0ull;
+            if ((rc = flush_locked(s)) || (rc = s->start_refresh())) return rc;
+        }
     }
     if (!s->tier_on) {  // give the host memory back
         s->tier_version = ~0ull;
         s->tier.reset();
-        s->tier_keys.release();
-        s->tier_prefix.release();
+        s->tsets[0].release(), s->tsets[1].release();
         s->tier_out = std::vector<uint8_t>();
-        (void)hipSetDevice(s->device);
-        s->tier_dpre.release(), s->tier_spre.release(), s->tier_bpre.release();
+        s->tier_dpre.release(), s->tier_spre.release(), s->tier_bpre.release(), s->tier_dsmp.release();
     }
     return RH_OK;
 }

@@ -49,9 +49,10 @@ struct SmallBatch {
     uint32_t *upos, *usrc, *rlist;
     uint64_t *mcnt;        // out (device): [0] inserts, [1] overwrites, [2] removals, [3] upserts, [4] present
     uint64_t *res;         // out: the result block (SMALL_RES_WORDS words)
-    int fold;              // 0: none; 1: fkeys + frecs (DeltaRecs) + fdrop (drop flags); 2: fkeys + frecs
-                           // (fingerprints) + fdrop (ops) -- the host tier's fold rows, in key order
-    uint8_t *fkeys, *frecs, *fdrop;
+    // the host tier's fold rows, in key order (each nullable): the kept keys, their DeltaRecs and
+    // drop flags (folds against the device's base), their fingerprints and ops (folds against the
+    // tier's own base copy)
+    uint8_t *fkeys, *frecs, *fdrop, *ffps, *fops;
 };
 
 // KL key bytes with the widest aligned word accesses (key rows are KL-aligned; KL a multiple of 4)
@@ -224,16 +225,11 @@ __global__ __launch_bounds__(1024) void k_small_batch(SmallBatch a) {
             dcnt -= ((w[9] & DeltaRec::LIVE) ? 1 : 0) - ((w[9] & DeltaRec::IN_BASE) ? 1 : 0);
         }
         fp_sub(nc, oc, dfp);
-        if (a.fold) {
-            copy_key_words<KL>(a.fkeys + (uint64_t)t * KL, key);
-            if (a.fold == 1) {
-                reinterpret_cast<DeltaRec *>(a.frecs)[t] = r;
-                a.fdrop[t] = drop ? 1 : 0;
-            } else {
-                fp_store(a.frecs + 32ull * t, cur);
-                a.fdrop[t] = isdel ? 1 : 0;
-            }
-        }
+        if (a.fkeys) copy_key_words<KL>(a.fkeys + (uint64_t)t * KL, key);
+        if (a.frecs) reinterpret_cast<DeltaRec *>(a.frecs)[t] = r;
+        if (a.fdrop) a.fdrop[t] = drop ? 1 : 0;
+        if (a.ffps) fp_store(a.ffps + 32ull * t, cur);
+        if (a.fops) a.fops[t] = isdel ? 1 : 0;
     }
     // the merge lists (k_delta_lists): upsert U lands at rank + U - R (U upserts, R run rows replaced
     // before it); the run rows the batch replaces, in order

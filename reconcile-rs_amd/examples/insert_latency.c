@@ -77,6 +77,7 @@ int main(int argc, char **argv) {
     if (tier) {
         uint64_t r0 = 0;
         CHECK(rh_store_rank(s, &keys[nr / 2], &r0));
+        CHECK(rh_store_tier_sync(s)); /* the background copy of the loaded base has landed */
     }
     uint64_t refreshes0 = 0, folds0 = 0;
     CHECK(rh_store_tier_stats(s, NULL, NULL, &refreshes0, &folds0));

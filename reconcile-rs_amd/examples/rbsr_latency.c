@@ -172,8 +172,10 @@ int main(int argc, char **argv) {
         CHECK(rh_store_set_host_tier(b, 1, 0));
     }
     double t0 = now_s();
-    cost_t c = reconcile(a, b, &sc); /* the first one also refreshes the host tier */
+    cost_t c = reconcile(a, b, &sc); /* the first one: the tiers' copies are still in flight */
     const double first = now_s() - t0;
+    CHECK(rh_store_tier_sync(a)); /* then a warm store: the copies have landed */
+    CHECK(rh_store_tier_sync(b));
     double *ts = malloc(sizeof(double) * (size_t)(reps > 0 ? reps : 1));
     double *tw = malloc(sizeof(double) * (size_t)(reps > 0 ? reps : 1));
     double total = 0, wtotal = 0;

@@ -179,6 +179,10 @@ class GpuFingerprintStore:
         A.check(A.lib().rh_store_stats(self._h, C.byref(b), C.byref(d), C.byref(c)), "rh_store_stats")
         return {"base_rows": int(b.value), "delta_rows": int(d.value), "compactions": int(c.value)}
 
+    def tier_sync(self) -> None:
+        """Wait until the host tier is fresh (its background refresh landed): rh_store_tier_sync."""
+        A.check(A.lib().rh_store_tier_sync(self._h), "rh_store_tier_sync")
+
     def batch_stats(self) -> Dict[str, int]:
         """Batches applied by the small-batch path and by the large-batch path (rh_store_batch_stats)."""
         a, b = C.c_uint64(), C.c_uint64()

@@ -26,15 +26,30 @@ struct DevState<K> {
     pending: BTreeMap<K, Option<Vec<u8>>>, // Some(record bytes) = insert / overwrite, None = delete
 }
 
-pub struct HipEncodedMap<K: Ord + Clone + Serialize, V: Serialize> {
-    store: *mut ffi::rh_estore,
+/// The library's encoded store, owned (its one `Drop`: see `StoreHandle` in lib.rs).
+struct EStoreHandle(*mut ffi::rh_estore);
+
+impl Drop for EStoreHandle {
+    fn drop(&mut self) {
+        // SAFETY: the pointer came from rh_estore_create and is destroyed once, here.
+        unsafe { ffi::rh_estore_destroy(self.0) };
+    }
+}
+
+// SAFETY: the C store serialises every call with its own mutex; a handle has no other state.
+unsafe impl Send for EStoreHandle {}
+unsafe impl Sync for EStoreHandle {}
+
+/// `Rsos<K>` for any serde `K` / `V` on an MI355X.  No bounds on the type (as
+/// `FingerprintTreeMap<K, V>`, rsos/src/fingerprint_tree_map.rs:94): `Replica`'s field
+/// `Arc<RwLock<HipEncodedMap<K, Entry<Timestamp, V>>>>` (src/replica.rs:69) is well-formed for
+/// its unbounded `K`, `V`; the methods need `K: Ord + Clone + Serialize, V: Serialize`, which
+/// `lww_register::Key` / `Value` imply (lww-register/src/bounds.rs:21,31).
+pub struct HipEncodedMap<K, V> {
+    store: EStoreHandle,
     entries: SortedBlocks<K, V>,
     dev: Mutex<DevState<K>>,
 }
-
-// SAFETY: the C store serialises calls with its own mutex; the device-side state is behind a Mutex.
-unsafe impl<K: Ord + Clone + Serialize + Send, V: Serialize + Send> Send for HipEncodedMap<K, V> {}
-unsafe impl<K: Ord + Clone + Serialize + Send + Sync, V: Serialize + Sync> Sync for HipEncodedMap<K, V> {}
 
 fn record<K: Serialize, V: Serialize>(k: &K, v: &V) -> Vec<u8> {
     // encode_to_vec fails only for a hand-written Serialize that errors; lift panics then too
@@ -59,12 +74,19 @@ fn pack(records: &[Vec<u8>]) -> (Vec<u8>, Vec<u64>) {
 }
 
 impl<K: Ord + Clone + Serialize, V: Serialize> HipEncodedMap<K, V> {
-    pub fn new(device: i32) -> Self {
+    /// An empty map on the default device (`FingerprintTreeMap::new()`, src/replica/construct.rs:205-206).
+    pub fn new() -> Self {
+        Self::on_device(crate::default_device())
+    }
+
+    /// An empty map on HIP device `device`.
+    pub fn on_device(device: i32) -> Self {
         let mut store = std::ptr::null_mut();
         // SAFETY: valid out-pointer.
         check(unsafe { ffi::rh_estore_create(device, &mut store) }, "rh_estore_create");
+        let store = EStoreHandle(store);
         // SAFETY: store was just created.
-        check(unsafe { ffi::rh_estore_set_host_tier(store, 1) }, "rh_estore_set_host_tier");
+        check(unsafe { ffi::rh_estore_set_host_tier(store.0, 1) }, "rh_estore_set_host_tier");
         HipEncodedMap {
             store,
             entries: SortedBlocks::new(),
@@ -80,7 +102,7 @@ impl<K: Ord + Clone + Serialize, V: Serialize> HipEncodedMap<K, V> {
         let recs: Vec<Vec<u8>> = items.iter().map(|(k, v)| record(k, v)).collect();
         let (bytes, offs) = pack(&recs);
         // SAFETY: buffers outlive the synchronous call.
-        check(unsafe { ffi::rh_estore_load(self.store, bytes.as_ptr(), offs.as_ptr(), items.len()) },
+        check(unsafe { ffi::rh_estore_load(self.store.0, bytes.as_ptr(), offs.as_ptr(), items.len()) },
               "rh_estore_load");
         let keys = items.iter().map(|(k, _)| (k.clone(), ())).collect();
         *self.dev.get_mut().expect("rsos-hip: poisoned") =
@@ -123,7 +145,7 @@ impl<K: Ord + Clone + Serialize, V: Serialize> HipEncodedMap<K, V> {
         let (bytes, offs) = pack(&recs);
         // SAFETY: buffers outlive the synchronous call; positions are sorted (BTreeMap order).
         check(unsafe {
-            ffi::rh_estore_apply(self.store, pos.as_ptr(), kinds.as_ptr(), pos.len(), bytes.as_ptr(), offs.as_ptr(),
+            ffi::rh_estore_apply(self.store.0, pos.as_ptr(), kinds.as_ptr(), pos.len(), bytes.as_ptr(), offs.as_ptr(),
                                  recs.len())
         }, "rh_estore_apply");
         for k in dels {
@@ -143,12 +165,6 @@ impl<K: Ord + Clone + Serialize, V: Serialize> HipEncodedMap<K, V> {
     }
 }
 
-impl<K: Ord + Clone + Serialize, V: Serialize> Drop for HipEncodedMap<K, V> {
-    fn drop(&mut self) {
-        // SAFETY: store came from rh_estore_create and is destroyed once.
-        unsafe { ffi::rh_estore_destroy(self.store) };
-    }
-}
 
 impl<K: Ord + Clone + Serialize, V: Serialize> Rsos<K> for HipEncodedMap<K, V> {
     type Value = V;
@@ -163,7 +179,7 @@ impl<K: Ord + Clone + Serialize, V: Serialize> Rsos<K> for HipEncodedMap<K, V> {
         let hi = (self.bound_rank(range.end_bound(), false) as u64).max(lo); // inverted -> ZERO
         let mut out = ffi::rh_aggregate::default();
         // SAFETY: one range in, one aggregate out.
-        check(unsafe { ffi::rh_estore_aggregates(self.store, &lo, &hi, 1, &mut out) }, "rh_estore_aggregates");
+        check(unsafe { ffi::rh_estore_aggregates(self.store.0, &lo, &hi, 1, &mut out) }, "rh_estore_aggregates");
         Aggregate::new(out.size as usize, Fingerprint(out.fingerprint))
     }
 
@@ -206,7 +222,7 @@ impl<K: Ord + Clone + Serialize, V: Serialize> Rsos<K> for HipEncodedMap<K, V> {
 
 impl<K: Ord + Clone + Serialize, V: Serialize> Default for HipEncodedMap<K, V> {
     fn default() -> Self {
-        HipEncodedMap::new(0)
+        HipEncodedMap::new()
     }
 }
 
@@ -338,13 +354,13 @@ impl<K: Ord + Clone + Serialize, V: Serialize> HipEncodedMap<K, V> {
         self.flush();
         let mut n = 0u64;
         // SAFETY: out-pointer.
-        check(unsafe { ffi::rh_estore_len(self.store, &mut n) }, "rh_estore_len");
+        check(unsafe { ffi::rh_estore_len(self.store.0, &mut n) }, "rh_estore_len");
         assert_eq!(n as usize, self.entries.len(), "rsos-hip: device and host sizes differ");
     }
 }
 
 /// The reference's `rsos::Entry` (public-api/rsos.txt:118-121).
-pub struct Entry<'a, K: Ord + Clone + Serialize, V: Serialize> {
+pub struct Entry<'a, K, V> {
     map: &'a mut HipEncodedMap<K, V>,
     key: K,
 }
@@ -383,7 +399,7 @@ impl<'a, K: Ord + Clone + Serialize, V: Serialize> Entry<'a, K, V> {
 
 impl<K: Ord + Clone + Serialize, V: Serialize> FromIterator<(K, V)> for HipEncodedMap<K, V> {
     fn from_iter<T: IntoIterator<Item = (K, V)>>(iter: T) -> Self {
-        let mut m = HipEncodedMap::new(0);
+        let mut m = HipEncodedMap::new();
         m.load_bulk(iter.into_iter().collect());
         m
     }

@@ -27,8 +27,10 @@
 mod encoded;
 mod ffi;
 mod sorted;
+mod values;
 
 pub use encoded::HipEncodedMap;
+pub use values::{FixedBytes, FixedValue};
 
 use std::ffi::CStr;
 use std::ops::{Bound, RangeBounds};
@@ -85,9 +87,10 @@ pub struct RecordRow {
 }
 
 /// A value type whose canonical encoding the device synthesises from fixed-width columns.
-/// Implement it for `lww_register::Entry<Timestamp, V>` (RECORD_KIND = DATED),
-/// `State<V>` (PROJECTION) or a plain `V` (PLAIN).  `write` must produce exactly the
-/// fields `rsos::encoding` would serialise; the library's tests pin that equivalence.
+/// Implemented in this crate (values.rs) for `lww_register::Entry<Timestamp, V>` (RECORD_KIND =
+/// DATED) and `State<V>` (PROJECTION) over any `V: FixedValue`, and for plain `u32` / `u64` /
+/// `FixedBytes<N>` values (PLAIN).  `write` must produce exactly the fields `rsos::encoding` would
+/// serialise; the library's tests pin that equivalence.
 pub trait GpuRecord: Serialize {
     const VALUE_KIND: i32;
     const VALUE_LEN: u32;
@@ -95,17 +98,44 @@ pub trait GpuRecord: Serialize {
     fn write(&self, row: &mut RecordRow);
 }
 
-/// `Rsos<K>` on an MI355X.
-pub struct HipFingerprintMap<K: GpuKey, V: GpuRecord> {
-    store: *mut ffi::rh_store,
+/// The library's store, owned: the one place its pointer lives and its one `Drop`, so the map
+/// types carry no bounds on their definitions (a generic `Drop` impl must repeat them, E0367) --
+/// `FingerprintTreeMap<K, V>` has none either (rsos/src/fingerprint_tree_map.rs:94), and
+/// `Replica`'s fields name the map with unbounded `K`, `V` (src/replica.rs:68-74).
+pub(crate) struct StoreHandle(pub(crate) *mut ffi::rh_store);
+
+impl StoreHandle {
+    fn create(device: i32, s: &ffi::rh_schema) -> StoreHandle {
+        let mut store = std::ptr::null_mut();
+        // SAFETY: valid schema pointer and out-pointer.
+        check(unsafe { ffi::rh_store_create(device, s, &mut store) }, "rh_store_create");
+        StoreHandle(store)
+    }
+}
+
+impl Drop for StoreHandle {
+    fn drop(&mut self) {
+        // SAFETY: the pointer came from rh_store_create and is destroyed once, here.
+        unsafe { ffi::rh_store_destroy(self.0) };
+    }
+}
+
+// SAFETY: the C store serialises every call with its internal mutex; a handle has no other state.
+unsafe impl Send for StoreHandle {}
+unsafe impl Sync for StoreHandle {}
+
+/// The HIP device a map created by `new()` / `default()` lives on: `RSOS_HIP_DEVICE`, else 0
+/// (`FingerprintTreeMap::new()` takes no arguments, src/replica/construct.rs:205-206).
+pub fn default_device() -> i32 {
+    std::env::var("RSOS_HIP_DEVICE").ok().and_then(|v| v.parse().ok()).unwrap_or(0)
+}
+
+/// `Rsos<K>` on an MI355X.  No bounds on the type: the methods carry them.
+pub struct HipFingerprintMap<K, V> {
+    store: StoreHandle,
     /// rank-ordered host index (owns K and V; select / enumerate borrow from it)
     entries: sorted::SortedBlocks<K, V>,
 }
-
-// SAFETY: the C store serialises all calls with an internal mutex; the host mirror follows
-// Rust's aliasing rules through &self / &mut self.
-unsafe impl<K: GpuKey + Send, V: GpuRecord + Send> Send for HipFingerprintMap<K, V> {}
-unsafe impl<K: GpuKey + Sync, V: GpuRecord + Sync> Sync for HipFingerprintMap<K, V> {}
 
 fn schema<K: GpuKey, V: GpuRecord>() -> ffi::rh_schema {
     ffi::rh_schema {
@@ -171,14 +201,16 @@ impl Batch {
 }
 
 impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
+    /// An empty map on the default device (`FingerprintTreeMap::new()`).
+    pub fn new() -> Self {
+        Self::on_device(default_device())
+    }
+
     /// An empty map on HIP device `device`.
-    pub fn new(device: i32) -> Self {
-        let s = schema::<K, V>();
-        let mut store = std::ptr::null_mut();
-        // SAFETY: valid schema pointer and out-pointer.
-        check(unsafe { ffi::rh_store_create(device, &s, &mut store) }, "rh_store_create");
+    pub fn on_device(device: i32) -> Self {
+        let store = StoreHandle::create(device, &schema::<K, V>());
         // SAFETY: store was just created.
-        check(unsafe { ffi::rh_store_set_host_tier(store, 1, 0) }, "rh_store_set_host_tier");
+        check(unsafe { ffi::rh_store_set_host_tier(store.0, 1, 0) }, "rh_store_set_host_tier");
         HipFingerprintMap { store, entries: sorted::SortedBlocks::new() }
     }
 
@@ -191,7 +223,7 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         let batch = Batch::new(items.iter().map(|(k, v)| (k, Some(v))));
         let cols = batch.columns();
         // SAFETY: the column buffers outlive the synchronous call.
-        check(unsafe { ffi::rh_store_load(self.store, &cols, items.len()) }, "rh_store_load");
+        check(unsafe { ffi::rh_store_load(self.store.0, &cols, items.len()) }, "rh_store_load");
         self.entries = sorted::SortedBlocks::from_sorted(items);
     }
 
@@ -209,7 +241,7 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         let hi: Vec<u64> = ranges.iter().map(|r| r.1 as u64).collect();
         let mut out = vec![ffi::rh_aggregate::default(); ranges.len()];
         // SAFETY: buffers sized r.
-        check(unsafe { ffi::rh_store_aggregates(self.store, lo.as_ptr(), hi.as_ptr(), ranges.len(), out.as_mut_ptr()) },
+        check(unsafe { ffi::rh_store_aggregates(self.store.0, lo.as_ptr(), hi.as_ptr(), ranges.len(), out.as_mut_ptr()) },
               "rh_store_aggregates");
         out.into_iter().map(|a| Aggregate::new(a.size as usize, Fingerprint(a.fingerprint))).collect()
     }
@@ -221,7 +253,7 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         let cols = batch.columns();
         let op = [if value.is_some() { 0u8 } else { 1u8 }];
         // SAFETY: the library copies the row before returning.
-        check(unsafe { ffi::rh_store_stage(self.store, &cols, op.as_ptr(), 1) }, "rh_store_stage");
+        check(unsafe { ffi::rh_store_stage(self.store.0, &cols, op.as_ptr(), 1) }, "rh_store_stage");
     }
 
     fn key_bound(b: Bound<&K>, lower: bool) -> (i32, Vec<u8>) {
@@ -367,13 +399,6 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
     }
 }
 
-impl<K: GpuKey, V: GpuRecord> Drop for HipFingerprintMap<K, V> {
-    fn drop(&mut self) {
-        // SAFETY: store came from rh_store_create and is destroyed once.
-        unsafe { ffi::rh_store_destroy(self.store) };
-    }
-}
-
 impl<K: GpuKey, V: GpuRecord> Rsos<K> for HipFingerprintMap<K, V> {
     type Value = V;
 
@@ -389,7 +414,7 @@ impl<K: GpuKey, V: GpuRecord> Rsos<K> for HipFingerprintMap<K, V> {
         let mut out = ffi::rh_aggregate::default();
         let ptr = |b: &Vec<u8>| if b.is_empty() { std::ptr::null() } else { b.as_ptr() as *const c_void };
         // SAFETY: bound keys are key_len bytes (or NULL when unbounded); out is one aggregate.
-        check(unsafe { ffi::rh_store_aggregate_keys(self.store, lk, ptr(&lb), hk, ptr(&hb), &mut out) },
+        check(unsafe { ffi::rh_store_aggregate_keys(self.store.0, lk, ptr(&lb), hk, ptr(&hb), &mut out) },
               "rh_store_aggregate_keys");
         Aggregate::new(out.size as usize, Fingerprint(out.fingerprint))
     }
@@ -433,7 +458,7 @@ impl<K: GpuKey, V: GpuRecord> Rsos<K> for HipFingerprintMap<K, V> {
 
 impl<K: GpuKey, V: GpuRecord> Default for HipFingerprintMap<K, V> {
     fn default() -> Self {
-        HipFingerprintMap::new(0)
+        HipFingerprintMap::new()
     }
 }
 
@@ -506,7 +531,7 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
             let cols = batch.columns();
             let op = [0u8];
             // SAFETY: the library copies the row before returning.
-            check(unsafe { ffi::rh_store_stage(self.store, &cols, op.as_ptr(), 1) }, "rh_store_stage");
+            check(unsafe { ffi::rh_store_stage(self.store.0, &cols, op.as_ptr(), 1) }, "rh_store_stage");
         }
         r
     }
@@ -560,13 +585,13 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
     pub fn check_invariants(&self) {
         let mut n = 0u64;
         // SAFETY: out-pointer.
-        check(unsafe { ffi::rh_store_len(self.store, &mut n) }, "rh_store_len");
+        check(unsafe { ffi::rh_store_len(self.store.0, &mut n) }, "rh_store_len");
         assert_eq!(n as usize, self.entries.len(), "rsos-hip: device and host sizes differ");
     }
 }
 
 /// The reference's `rsos::Entry` (public-api/rsos.txt:118-121) for the column store.
-pub struct HipEntry<'a, K: GpuKey, V: GpuRecord> {
+pub struct HipEntry<'a, K, V> {
     map: &'a mut HipFingerprintMap<K, V>,
     key: K,
 }
@@ -605,7 +630,7 @@ impl<'a, K: GpuKey, V: GpuRecord> HipEntry<'a, K, V> {
 
 impl<K: GpuKey, V: GpuRecord> FromIterator<(K, V)> for HipFingerprintMap<K, V> {
     fn from_iter<T: IntoIterator<Item = (K, V)>>(iter: T) -> Self {
-        let mut m = HipFingerprintMap::new(0);
+        let mut m = HipFingerprintMap::new();
         m.load_bulk(iter.into_iter().collect());
         m
     }

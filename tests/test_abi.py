@@ -191,3 +191,113 @@ def test_apply_device_many_argument_checks(rsos_hip_lib):
     L = A.lib()
     assert L.rh_store_apply_device_many(None, None, None, None, 0, None, None) == A.ERR_ARG
     assert L.rh_store_apply_device_many(None, None, None, None, 3, None, None) == A.ERR_ARG
+
+
+# ---- the Rust FFI block against the header, signature by signature -------------------------------
+# (the crate cannot be compiled in this image: no cargo / rustc; this is the check a
+# compiler would make at the boundary -- arity, pointer depth and constness, integer width)
+_C_BASE = {"int": "i32", "int32_t": "i32", "unsigned": "u32", "uint32_t": "u32", "uint64_t": "u64",
+           "int64_t": "i64", "size_t": "usize", "uint8_t": "u8", "int8_t": "i8", "char": "i8", "void": "void",
+           "double": "f64", "float": "f32", "uint16_t": "u16", "int16_t": "i16"}
+_R_BASE = {"c_int": "i32", "i32": "i32", "u32": "u32", "u64": "u64", "i64": "i64", "usize": "usize", "u8": "u8",
+           "i8": "i8", "c_char": "i8", "c_void": "void", "f64": "f64", "f32": "f32", "u16": "u16", "i16": "i16",
+           "()": "void"}
+
+
+def _c_type(t: str):
+    """(base, [const-ness of each pointer level's pointee, outermost first]) of a C parameter type"""
+    t = t.replace("*", " * ").split()
+    # split into pointer levels: the tokens before the first '*' are the base (+ its const)
+    levels, cur = [], []
+    for tok in t:
+        if tok == "*":
+            levels.append(cur)
+            cur = []
+        else:
+            cur.append(tok)
+    levels.append(cur)  # trailing qualifiers of the outermost pointer itself (ignored)
+    base_toks = [x for x in levels[0] if x not in ("const", "struct", "unsigned")] or ["unsigned"]
+    if "unsigned" in levels[0] and base_toks == ["int"]:
+        base_toks = ["unsigned"]
+    base = base_toks[-1]
+    base = _C_BASE.get(base, base)
+    # pointee constness per level: level 0's const applies to the innermost pointee
+    consts = ["const" in lv for lv in levels[:-1]]
+    return base, list(reversed(consts))
+
+
+def _c_param(p: str):
+    p = p.strip()
+    arr = re.search(r"\[\s*\d*\s*\]$", p)
+    if arr:  # `const uint64_t a[4]`: a pointer
+        p = p[:arr.start()].strip()
+        p = re.sub(r"\b(\w+)$", r"* \1", p)
+    name = re.search(r"(\w+)$", p).group(1)
+    return _c_type(p[: len(p) - len(name)])
+
+
+def _r_type(t: str):
+    t = t.strip()
+    consts = []
+    while t.startswith("*"):
+        m = re.match(r"\*\s*(const|mut)\s+", t)
+        consts.append(m.group(1) == "const")
+        t = t[m.end():]
+    return _R_BASE.get(t, t), consts
+
+
+def _c_prototypes():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = "\n".join(l for l in text.splitlines() if not l.strip().startswith("#"))
+    text = re.sub(r"typedef struct[^;]*?\{.*?\}\s*\w+\s*;", "", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(rh_\w+)\s*\(([^;{}()]*)\)\s*;", text):
+        ret, name, params = m.group(1), m.group(2), m.group(3).strip()
+        ps = [] if params in ("", "void") else [_c_param(p) for p in params.split(",")]
+        out[name] = (_c_type(ret), ps)
+    return out
+
+
+def _rust_prototypes():
+    ffi = open(os.path.join(ROOT, "reconcile-rs_amd", "rust", "rsos-hip", "src", "ffi.rs")).read()
+    ffi = re.sub(r"//[^\n]*", "", ffi)
+    out = {}
+    for m in re.finditer(r"pub fn (rh_\w+)\s*\(([^)]*)\)\s*(->\s*([^;]+))?;", ffi, flags=re.S):
+        name, params, ret = m.group(1), m.group(2), (m.group(4) or "()").strip()
+        ps = [_r_type(p.split(":", 1)[1]) for p in params.split(",") if p.strip()]
+        out[name] = (_r_type(ret), ps)
+    return out
+
+
+def test_rust_ffi_signatures_match_the_header():
+    """Every extern "C" fn of ffi.rs has its header prototype's arity, and per parameter and return
+    value the same pointer depth, pointee constness at every level and base type width (c_int =
+    int = i32, size_t = usize, char = c_char, void = c_void / ())."""
+    c, r = _c_prototypes(), _rust_prototypes()
+    assert set(c) == set(declared_symbols())
+    assert set(r) == set(c), (set(c) ^ set(r))
+    bad = []
+    for name, (cret, cps) in sorted(c.items()):
+        rret, rps = r[name]
+        if len(cps) != len(rps):
+            bad.append((name, "arity", len(cps), len(rps)))
+            continue
+        if cret != rret:
+            bad.append((name, "return", cret, rret))
+        for i, (cp, rp) in enumerate(zip(cps, rps)):
+            if cp != rp:
+                bad.append((name, "param %d" % i, cp, rp))
+    assert not bad, bad
+
+
+def test_signature_parser_catches_mismatches():
+    """The parser above distinguishes what a compiler would: width, pointer depth, constness."""
+    assert _c_param("const uint8_t *const *dev_ops") == ("u8", [True, True])
+    assert _r_type("*const *const u8") == ("u8", [True, True])
+    assert _c_param("uint64_t *n_new") == ("u64", [False])
+    assert _r_type("*mut u64") == ("u64", [False])
+    assert _c_param("size_t n") == ("usize", []) != _c_param("uint32_t n")
+    assert _c_param("const uint64_t a[4]") == ("u64", [True]) == _r_type("*const u64")
+    assert _c_param("void *stream") == _r_type("*mut c_void")
+    assert _c_param("const void *keys") != _r_type("*mut c_void")

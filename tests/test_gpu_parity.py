@@ -122,7 +122,8 @@ def test_encoded_golden_ragged(gpu, golden):
 # ---- seeded random batches vs the C oracle ---------------------------------------------------
 
 SHAPES = [("u32", "u32"), ("u64", "u64"), ("u64", "bytes64"), ("bytes16", "bytes64"),
-          ("bytes16", "bytes1024"), ("bytes16", "u64"), ("bytes32", "bytes64")]
+          ("bytes16", "bytes1024"), ("bytes16", "u64"), ("bytes32", "bytes64"), ("bytes16", "unit"),
+          ("u64", "unit")]
 
 
 def oracle_records(O, schema, h):
@@ -861,7 +862,8 @@ def test_store_load_refuses_2_pow_31_rows(gpu):
 
 def test_host_tier_equals_device_answers(gpu, oracle_lib):
     """The host tier (rh_store_set_host_tier) against the device path on the same store, before
-    and after batches (the tier refreshes on the first question after a change): ranks of
+    and after batches (a load or a moved buffer refreshes the tier in the background, the device
+    answering meanwhile; batches fold into it): ranks of
     present and absent keys, select, key-range aggregates with every bound kind (inverted ones
     give ZERO), rank-range aggregates, and the root against the oracle FTM's."""
     import torch
@@ -895,7 +897,8 @@ def test_host_tier_equals_device_answers(gpu, oracle_lib):
         hi = lo + rng.integers(0, 70_000, 64)
         assert tier.aggregates_ranks(list(lo), list(hi)) == dev.aggregates_ranks(list(lo), list(hi))
 
-    probe()
+    probe()  # answered by the device or the tier, whichever holds the copy by then
+    tier.tier_sync()
     assert tier.tier_stats()["refreshes"] == 1
     for k in range(3):  # inserts, then overwrites + deletes of existing keys
         b = make_records(s, 20_000, seed=300 + k, random_keys=True)
@@ -933,6 +936,7 @@ def test_host_tier_equals_device_answers(gpu, oracle_lib):
     # again instead of reading the old ones (a use-after-free before)
     tier.reserve(4 * n, 20_000)
     probe()
+    tier.tier_sync()
     assert tier.tier_stats()["refreshes"] == 2
     # small batches (the staged-insert shape): one row, then 1,000 rows
     one = make_records(s, 1, seed=501, random_keys=True)

@@ -24,6 +24,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import socket
@@ -490,6 +491,8 @@ def incremental(args, world, rank, dev, dist):
     torch.cuda.synchronize()
     counts = [0, 0, 0]
     comp0 = st.stats()["compactions"]
+    from rsos_hip import _abi as A
+    A.check(A.lib().rh_debug_batch_timing(1), "rh_debug_batch_timing")  # HIP events around k_lift_search
     t0 = time.perf_counter()
     if args.pipeline:  # the queued batches drained in order by one call, then the root
         for c in st.apply_device_many(batches[args.warmup:args.warmup + args.steps]):
@@ -504,6 +507,9 @@ def incremental(args, world, rank, dev, dist):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ls_us, ls_n = C.c_double(), C.c_uint64()
+    A.check(A.lib().rh_debug_batch_kernel_us(C.byref(ls_us), C.byref(ls_n)), "rh_debug_batch_kernel_us")
+    A.check(A.lib().rh_debug_batch_timing(0), "rh_debug_batch_timing")
     applied = [sum(b["keys"].shape[0] for b in batches[args.warmup:args.warmup + args.steps])]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -567,6 +573,8 @@ def incremental(args, world, rank, dev, dist):
                      "compaction) + the whole map's root after each"),
             "compactions_in_timed_steps": stats["compactions"] - comp0, "delta_rows_at_end": stats["delta_rows"],
             "reserved_rows": reserved, "compaction_divisor": args.compact_div or 6,
+            "roofline": config5_roofline(schema, n, m, args.compact_div or 6, elapsed / args.steps,
+                                         ls_us.value / max(ls_n.value, 1), int(ls_n.value)),
         }
         if args.cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_incremental(schema, m, args.cpu_sample or 10_000_000)
@@ -574,6 +582,57 @@ def incremental(args, world, rank, dev, dist):
     st.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def config5_roofline(schema, n, m, div, step_s, ls_us, launches):
+    """config5's roofline ("config5: algorithmic bytes"): the dominant kernel,
+    k_lift_search (the fused lift + base / delta searches), timed with HIP events on the store's
+    stream over the timed batches (rh_debug_batch_timing), against its algorithmic bytes per
+    launch; and the whole batch's steady-state byte model against ms_per_step.  traffic: the
+    kernel's DRAM bytes per launch from the committed PMC summary (TCC_EA0_RDREQ_DRAM_32B x 32 +
+    the write requests; scripts/pmc_c5.sh, pmc_c5_summary.py)."""
+    rec = schema.key_row + (20 if schema.dated_kind else 0) + schema.value_row  # the record columns read
+    line = 128  # one random key line per search (the tables and sample lines stay in L2)
+    per_key = {"records": rec, "fingerprint_write": 32, "search_results": 2 * (4 + 1), "position": 4,
+               "base_key_line": line, "delta_key_line": line}
+    ls_bytes = m * sum(per_key.values())
+    achieved = ls_bytes / (ls_us * 1e-6) / 1e9 if ls_us > 0 else 0.0
+    # the batch, steady state: the delta run grows from 0 to T = n / div rows between compactions
+    T = max(n // div, 65_536)
+    batches_per_cycle = max(T / m, 1.0)
+    terms = {
+        "sort": m * (schema.key_row * 2 + 4),                       # keys read, sorted keys + positions written
+        "lift_search": ls_bytes,
+        "delta_records": m * (32 + 40 + 1),                         # fingerprints in, DeltaRecs + drop flags out
+        "delta_merge": int((T / 2 + m) * (schema.key_row + 4) * 2),  # the run's (key, slot) rows read + written
+        "compaction": int(((n + T / 2) * (schema.key_row + 32) * 2 + T * (schema.key_row + 4 + 40)) / batches_per_cycle),
+    }
+    batch_bytes = sum(terms.values())
+    batch_gbs = batch_bytes / step_s / 1e9
+    traffic = None
+    p = _profile_any("pmc_config5.json")
+    if p:
+        try:
+            with open(p) as f:
+                k = next(v for name, v in json.load(f)["kernels"].items() if name.startswith("k_lift_search"))
+            traffic = {"bytes_per_launch": int(k["dram_read_bytes"] + k["dram_write_bytes"]),
+                       "source": os.path.relpath(p, ROOT)}
+        except (OSError, ValueError, KeyError, StopIteration):
+            traffic = None
+    return {"bound": "hbm", "kernel": "k_lift_search", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": ls_bytes, "algorithmic_bytes_per_key": per_key,
+            "kernel_avg_us": round(ls_us, 2), "launches_timed": launches,
+            "batch_model": {"algorithmic_bytes_per_batch": batch_bytes, "terms": terms,
+                            "achieved": round(batch_gbs, 1), "frac": round(batch_gbs / HBM_PEAK_GBS, 4),
+                            "delta_threshold_rows": T}}
+
+
+def _profile_any(suffix):
+    """The newest committed profiles/rNN_<suffix>, or None."""
+    import glob
+    ps = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_" + suffix)), reverse=True)
+    return ps[0] if ps else None
 
 
 def _encode_host(h) -> "np.ndarray":

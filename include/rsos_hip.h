@@ -440,6 +440,12 @@ int rh_debug_fail_point(const char *name);
  * Both are 0 until a timed reload has run.                                                  */
 int rh_debug_reload_timing(int on);
 int rh_debug_last_reload_us(double *locate_us, double *lift_us);
+/* on != 0: time every following large batch's fused lift + search launch (k_lift_search, the
+ * batch path's dominant kernel) with HIP events on the store's stream, accumulated over every
+ * store; rh_debug_batch_kernel_us reads the sum (microseconds) and the number of timed launches,
+ * on = 1 also zeroes them.                                                                     */
+int rh_debug_batch_timing(int on);
+int rh_debug_batch_kernel_us(double *lift_search_us, uint64_t *launches);
 
 #ifdef __cplusplus
 }

@@ -34,6 +34,10 @@ struct DevCols {
     // written by the key sort that runs before the lift; rows with dst[i] >= n are not written);
     // block sums are not formed then
     const uint32_t *dst = nullptr;
+    // optional, with dst: dst[i] is an index into dst2, which holds the row (the bucket sort's
+    // two-level positions: each input row's slot in its bucket's stretch, written in input order,
+    // and each slot's sorted row, written in slot order -- both whole-line writes)
+    const uint32_t *dst2 = nullptr;
 };
 
 constexpr int lowbit(int x) { return x & -x; }
@@ -383,7 +387,7 @@ __global__ __launch_bounds__(LIFT_THREADS) void k_lift(DevCols c, uint64_t n, ui
         if (c.dst) {
             // bounded: a bucket the key sort could not order leaves its rows' slots unwritten
             // (the sort flags it and the batch is sorted and lifted again)
-            const uint32_t r = c.dst[i];
+            const uint32_t r = c.dst2 ? c.dst2[c.dst[i]] : c.dst[i];
             if (r < n) store_fp<uint64_t>(fps, r, h);
         } else {
             store_fp(fps + b0 * 32, t, h);

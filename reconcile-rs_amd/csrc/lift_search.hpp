@@ -83,7 +83,7 @@ __global__ __launch_bounds__(LIFT_THREADS) void k_lift_search(DevCols c, uint64_
         const uint8_t *vrow = cb.values + t * (uint32_t)L::VAL_ROW;
         uint32_t h[8];
         lift_record<KK, KL, VK, VL, RK, TAGS>(kw, sw, tomb, vrow, h);
-        const uint32_t r = c.dst[i];
+        const uint32_t r = c.dst2 ? c.dst2[c.dst[i]] : c.dst[i];
         if (r < n) store_fp<uint64_t>(fps, r, h);  // bounded as in k_lift
     } else {
         const SearchJob &j = role == 1 ? jb : jd;

@@ -50,6 +50,12 @@ bool fail_point(const char *name) {
     return true;
 }
 
+// rh_debug_batch_timing: HIP events around every large batch's fused lift + search launch
+std::atomic<int> g_time_batch{0};
+std::mutex g_batch_mu;
+double g_batch_us = 0;
+uint64_t g_batch_n = 0;
+
 #define RH_HIP(expr)                                                                           \
     do {                                                                                       \
         hipError_t e_ = (expr);                                                                \
@@ -116,11 +122,13 @@ int check_cols(const rh_schema &s, const rh_columns *c, size_t n) {
 
 // dst_row (optional, single lift without block sums): record i's fingerprint to row dst_row[i]
 int lift_dispatch(const rh_schema &s, const rh_columns &c, size_t n, uint8_t *fps, uint8_t *bs,
-                  uint8_t *fps2, uint8_t *bs2, bool dual, hipStream_t st, const uint32_t *dst_row = nullptr) {
+                  uint8_t *fps2, uint8_t *bs2, bool dual, hipStream_t st, const uint32_t *dst_row = nullptr,
+                  const uint32_t *dst2 = nullptr) {
     bool supported = false;
     if (dst_row && (bs || dual)) return fail(RH_ERR_STATE, "lift to sorted rows: no block sums (internal error)");
     rh::DevCols dc = to_dev(c);
     dc.dst = dst_row;
+    dc.dst2 = dst2;
     hipError_t e = rh::launch_lift_schema(s.key_kind, (int)s.key_len, s.value_kind, (int)s.value_len,
                                           s.record_kind, c.tags != nullptr, dual, dc, n, fps, bs,
                                           fps2, bs2, st, &supported);
@@ -1544,7 +1552,7 @@ struct rh_store {
         if ((rc = skeys.ensure(m * kl + 64)) || (rc = sfps.ensure(m * 32 + 64)) || (rc = sops.ensure(m + 64)) ||
             (rc = dops.ensure(m + 64)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)) || (rc = results.ensure(12)))
             return rc;
-        (void)scratch.u32(7, m), (void)scratch.u32(9, m), (void)scratch.u32(10, m);
+        (void)scratch.u32(7, m), (void)scratch.u32(9, m), (void)scratch.u32(10, m), (void)scratch.i32(0, m);
         (void)scratch.u8(2, m), (void)scratch.u8(3, m);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         return RH_OK;
@@ -1555,14 +1563,21 @@ struct rh_store {
     // its sorted row of sfps, so the sort gathers no fingerprints.
     // pre: the keys' digit min / max partials are in the pre-minmax slot (queued by the previous
     // batch's k_lift_search, pre_minmax)
+    // The bucket sort's positions come in two levels (store_kernels.hpp sort_batch): scratch u32(7)
+    // holds each input row's slot and sort_s2o each slot's sorted row; the full sort writes the sorted
+    // rows into u32(7) directly (sort_s2o = nullptr).
+    uint32_t *sort_s2o = nullptr;
     int prepare_batch(const rh_columns &c, const uint8_t *ops, size_t m, bool full, bool pre = false) {
         uint32_t *pos = scratch.u32(7, m);
+        const bool two = !full && m <= rh::SORT_BUCKET_MAX;
+        uint32_t *s2o = two ? reinterpret_cast<uint32_t *>(scratch.i32(0, m)) : nullptr;
         const uint32_t npart = (uint32_t)((m + rh::MINMAX_TILE - 1) / rh::MINMAX_TILE);
         const uint64_t *part = pre ? scratch.u64(3, 2ull * npart) : nullptr;
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        sort_s2o = s2o;
         uint32_t *r_flags = reinterpret_cast<uint32_t *>(results.p + 6);
         RH_HIP(kops->sort_batch(static_cast<const uint8_t *>(c.keys), nullptr, ops, m, scratch, skeys.p, nullptr, sops.p,
-                                r_flags, full, stream, pos, part, npart));
+                                r_flags, full, stream, pos, part, npart, s2o));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         return RH_OK;
     }
@@ -1579,6 +1594,7 @@ struct rh_store {
         if (fused_lift_search) {
             rh::DevCols dc = to_dev(c);
             dc.dst = pos;
+            dc.dst2 = sort_s2o;
             rh::NextMinmax nx{};
             if (next && next_m && next_m <= rh::SORT_BUCKET_MAX && pre_minmax) {
                 nx.keys = static_cast<const uint8_t *>(next->keys);
@@ -1587,10 +1603,22 @@ struct rh_store {
                 if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
             }
             bool supported = false;
+            const bool timed = g_time_batch.load() != 0;
+            if (timed) {
+                if (!ls_ev[0]) {
+                    RH_HIP(hipEventCreate(&ls_ev[0]));
+                    RH_HIP(hipEventCreate(&ls_ev[1]));
+                }
+                RH_HIP(hipEventRecord(ls_ev[0], stream));
+            }
             const hipError_t e =
                 rh::launch_lift_search_schema(schema.key_kind, (int)schema.key_len, schema.value_kind, (int)schema.value_len,
                                               schema.record_kind, c.tags != nullptr, dc, m, sfps.p, skeys.p, jb, jd, nx,
                                               stream, &supported);
+            if (timed && supported && e == hipSuccess) {
+                RH_HIP(hipEventRecord(ls_ev[1], stream));
+                ls_pending = true;
+            }
             if (e != hipSuccess) return fail(RH_ERR_HIP, std::string("lift + search launch: ") + hipGetErrorString(e));
             if (supported) {
                 if (pre_minmax) *pre_minmax = nx.keys != nullptr;
@@ -1598,10 +1626,25 @@ struct rh_store {
             }
         }
         int rc;
-        if ((rc = lift_dispatch(schema, c, m, sfps.p, nullptr, nullptr, nullptr, false, stream, pos))) return rc;
+        if ((rc = lift_dispatch(schema, c, m, sfps.p, nullptr, nullptr, nullptr, false, stream, pos, sort_s2o)))
+            return rc;
         RH_HIP(kops->search_sampled(jb.keys, jb.n, jb.smp, jb.smp2, skeys.p, m, jb.rank, jb.present, stream, jb.tb));
         RH_HIP(kops->search_sampled(jd.keys, jd.n, jd.smp, jd.smp2, skeys.p, m, jd.rank, jd.present, stream, jd.tb));
         return RH_OK;
+    }
+    hipEvent_t ls_ev[2] = {nullptr, nullptr};  // rh_debug_batch_timing: around the fused launch
+    bool ls_pending = false;
+    void take_batch_timing() {  // after the batch's wait: the launch's time into the global sum
+        if (!ls_pending) return;
+        ls_pending = false;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, ls_ev[0], ls_ev[1]) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        std::lock_guard<std::mutex> g(g_batch_mu);
+        g_batch_us += 1000.0 * ms;
+        g_batch_n++;
     }
     // A/B switch: RSOS_HIP_PRE_MINMAX=0 = the next batch's sort runs its own min / max pass
     bool pre_minmax_on = !(getenv("RSOS_HIP_PRE_MINMAX") && *getenv("RSOS_HIP_PRE_MINMAX") == '0');
@@ -1722,6 +1765,7 @@ struct rh_store {
                 return rc;
             }
             memcpy(&flags, &host[6], 4);
+            take_batch_timing();
             if (!(flags & 6)) break;  // 2: leading-digit tie, 4: skewed buckets
             if (next_prepared) *next_prepared = false;  // the re-sort overwrites the next batch's step 1
         }
@@ -1733,7 +1777,7 @@ struct rh_store {
         out[2] = host[2];
         if (flags & 1) {
             out[0] = out[1] = out[2] = 0;
-            if (!last_wins) return fail(RH_ERR_ARG, "duplicate key within one batch");
+            if (!last_wins || next) return fail(RH_ERR_ARG, "duplicate key within one batch");
             // nothing was committed: reduce the batch to the last row of each key (the sort's
             // positions and sorted keys are still in place) and apply that
             version = version0;
@@ -1766,7 +1810,7 @@ struct rh_store {
         const uint32_t *pos = scratch.u32(7, m);
         uint32_t *keep = scratch.u32(11, m + 1), *dst = scratch.u32(12, m + 1);
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        RH_HIP(kops->keep_last_rows(skeys.p, pos, m, keep, stream));
+        RH_HIP(kops->keep_last_rows(skeys.p, pos, sort_s2o, m, keep, stream));
         RH_HIP(rh::launch_exclusive_scan_u32(keep, dst, m + 1, scratch, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         try {
@@ -2111,6 +2155,8 @@ struct rh_store {
         dep = nullptr;
         if (res_ev) (void)hipEventDestroy(res_ev);
         res_ev = nullptr;
+        for (auto &e : ls_ev)
+            if (e) (void)hipEventDestroy(e), e = nullptr;
     }
 };
 
@@ -2998,6 +3044,21 @@ int rh_debug_last_reload_us(double *locate_us, double *lift_us) {
     std::lock_guard<std::mutex> g(g_reload_mu);
     *locate_us = g_reload_us[0];
     *lift_us = g_reload_us[1];
+    return RH_OK;
+}
+
+int rh_debug_batch_timing(int on) {
+    std::lock_guard<std::mutex> g(g_batch_mu);
+    g_time_batch.store(on ? 1 : 0);
+    if (on) g_batch_us = 0, g_batch_n = 0;
+    return RH_OK;
+}
+
+int rh_debug_batch_kernel_us(double *lift_search_us, uint64_t *launches) {
+    if (!lift_search_us || !launches) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(g_batch_mu);
+    *lift_search_us = g_batch_us;
+    *launches = g_batch_n;
     return RH_OK;
 }
 

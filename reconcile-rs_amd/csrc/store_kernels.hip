@@ -346,10 +346,12 @@ __device__ __forceinline__ uint64_t digit_of_words(const uint32_t *w) {
 
 // (key, row) pairs into coarse-bucket order: the whole key travels, so the per-bucket sort
 // reads its keys from one contiguous stretch instead of gathering them from the input rows
+// oidx (nullable): each slot's input row (for the ops and a stable order of equal keys); islot
+// (nullable): each input row's slot, in input order (the first level of the two-level positions)
 template <int KK, int KL>
 __global__ __launch_bounds__(CS_WG) void k_cs_scatter(const uint8_t *keys, uint64_t m, const uint64_t *params,
                                                       uint32_t C, const uint32_t *hist, const uint32_t *start,
-                                                      uint8_t *okey, uint32_t *oidx) {
+                                                      uint8_t *okey, uint32_t *oidx, uint32_t *islot) {
     __shared__ uint32_t cur[CS_MAX_C];
     const uint64_t mn = params[0], sh = params[1];
     const uint32_t *h = hist + (uint64_t)blockIdx.x * C;
@@ -372,7 +374,8 @@ __global__ __launch_bounds__(CS_WG) void k_cs_scatter(const uint8_t *keys, uint6
                 const uint64_t d = digit_of_words<KK, KL>(kw[k]);
                 const uint32_t pos = atomicAdd(&cur[(uint32_t)((d - mn) >> sh) >> CS_FINE_BITS], 1u);
                 key_words_store<KL>(okey + (uint64_t)pos * KL, kw[k]);
-                oidx[pos] = (uint32_t)i;
+                if (oidx) oidx[pos] = (uint32_t)i;
+                if (islot) islot[i] = pos;
             }
         }
     };
@@ -384,10 +387,11 @@ __global__ __launch_bounds__(CS_WG) void k_cs_scatter(const uint8_t *keys, uint6
 // rows 256 (K0 + k) + lane, k < 4, of a bucket's sorted order: the key from the bucket's stretch
 // of scattered keys, the op (and, with fps, the fingerprint) from the input row; pos (when given):
 // pos[input row] = its sorted row, for a lift that runs after the sort
+// (s2o: pos[input row] is its slot, written by the scatter; here s2o[slot] = its sorted row)
 template <int KL, int K0>
 __device__ __forceinline__ void cs_gather(const uint16_t *sx, const uint32_t *tx, const uint16_t *tl, uint32_t n,
                                           uint32_t s0, const uint8_t *okey, const uint8_t *fps, const uint8_t *ops,
-                                          uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *pos) {
+                                          uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *pos, uint32_t *s2o) {
     static_assert(KL % 4 == 0, "keys: whole dwords");
     const uint32_t t = threadIdx.x;
     uint32_t kw[4][KL / 4], ov[4], xr[4];
@@ -397,7 +401,7 @@ __device__ __forceinline__ void cs_gather(const uint16_t *sx, const uint32_t *tx
         const uint32_t j = 256 * (K0 + k) + t;
         const uint32_t q = j < n ? sx[j] : 0;  // slot 0 stands in past n (not stored)
         const uint64_t src = tx[q];
-        xr[k] = (uint32_t)src;
+        xr[k] = s2o ? s0 + (uint32_t)tl[q] : (uint32_t)src;
         key_words_load<KL>(okey + (uint64_t)(s0 + tl[q]) * KL, kw[k]);
         if (fps) {
             f0[k] = reinterpret_cast<const uint4 *>(fps + 32 * src)[0];
@@ -416,7 +420,8 @@ __device__ __forceinline__ void cs_gather(const uint16_t *sx, const uint32_t *tx
             reinterpret_cast<uint4 *>(sfps + 32 * o)[0] = a;
             reinterpret_cast<uint4 *>(sfps + 32 * o)[1] = b;
         }
-        if (pos) pos[x] = (uint32_t)o;
+        if (s2o) s2o[x] = (uint32_t)o;  // x: the row's slot
+        else if (pos) pos[x] = (uint32_t)o;
         sops[o] = (uint8_t)op;
     };
     put(0, kw[0], f0[0], f1[0], ov[0], xr[0]);
@@ -430,7 +435,7 @@ template <int KK, int KL>
 __global__ __launch_bounds__(256) void k_cs_sort(const uint8_t *okey, const uint32_t *idx, const uint32_t *start,
                                                  const uint32_t *total, const uint64_t *params, const uint8_t *fps,
                                                  const uint8_t *ops, uint8_t *skeys, uint8_t *sfps, uint8_t *sops,
-                                                 uint32_t *pos, uint32_t *flags) {
+                                                 uint32_t *pos, uint32_t *flags, uint32_t *s2o) {
     constexpr int D = KK == KEY_BYTES ? KL / 8 : 1, PER = CS_CAP / 256;
     static_assert(CS_FINE == 256, "one fine bucket per lane");
     // fine-bucket order: td digit, tx input row, tl index in the bucket's stretch; sx: sorted
@@ -450,7 +455,7 @@ __global__ __launch_bounds__(256) void k_cs_sort(const uint8_t *okey, const uint
     for (int k = 0; k < PER; k++) {
         const uint32_t i = 256 * k + t;
         d[k] = i < n ? key_digit<KK, KL>(bk + (uint64_t)i * KL, 0) : 0;
-        x[k] = i < n ? idx[s0 + i] : 0;
+        x[k] = i < n ? (idx ? idx[s0 + i] : i) : 0;  // without idx: the slot (ties then by slot)
         f[k] = (uint32_t)((d[k] - mn) >> sh) & (CS_FINE - 1);
     }
     fcur[t] = 0;
@@ -508,8 +513,8 @@ __global__ __launch_bounds__(256) void k_cs_sort(const uint8_t *okey, const uint
     __syncthreads();
     // gather key / op (/ fingerprint) of the sorted rows, 4 per lane at a time with all of the
     // group's loads before its stores
-    cs_gather<KL, 0>(sx, tx, tl, n, s0, okey, fps, ops, skeys, sfps, sops, pos);
-    if (n > 4 * 256) cs_gather<KL, 4>(sx, tx, tl, n, s0, okey, fps, ops, skeys, sfps, sops, pos);
+    cs_gather<KL, 0>(sx, tx, tl, n, s0, okey, fps, ops, skeys, sfps, sops, pos, s2o);
+    if (n > 4 * 256) cs_gather<KL, 4>(sx, tx, tl, n, s0, okey, fps, ops, skeys, sfps, sops, pos, s2o);
     if (__ballot(dup) && (t & 63) == 0) atomicOr(flags, 1u);
 }
 
@@ -616,14 +621,15 @@ __global__ void k_dedup_scatter(const uint8_t *keys, const uint8_t *fps, const u
 }
 
 template <int KK, int KL>
-__global__ void k_keep_last(const uint8_t *skeys, const uint32_t *pos, uint64_t m, uint32_t *keep) {
+__global__ void k_keep_last(const uint8_t *skeys, const uint32_t *pos, const uint32_t *s2o, uint64_t m,
+                            uint32_t *keep) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > m) return;
     if (i == m) {
         keep[m] = 0;
         return;
     }
-    const uint64_t j = pos[i];
+    const uint64_t j = s2o ? s2o[pos[i]] : pos[i];
     keep[i] = (j + 1 < m && key_cmp<KK, KL>(skeys + j * KL, skeys + (j + 1) * KL) == 0) ? 0u : 1u;
 }
 
@@ -1489,7 +1495,8 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
                           uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, bool full,
-                          hipStream_t st, uint32_t *pos, const uint64_t *pre_part, uint32_t pre_npart) override {
+                          hipStream_t st, uint32_t *pos, const uint64_t *pre_part, uint32_t pre_npart,
+                          uint32_t *s2o) override {
         hipError_t e;
         if (!fps == !pos) return hipErrorInvalidValue;  // exactly one of: gather fps, emit positions
         uint32_t *perm = s.u32(0, m), *perm2 = s.u32(1, m);
@@ -1507,7 +1514,8 @@ struct KeyOps final : StoreKeyOps {
             return hipSuccess;
         };
         if (!full && m <= CS_MAX_M)
-            return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st, pos, pre_part, pre_npart);
+            return sort_batch_buckets(keys, fps, ops, m, s, skeys, sfps, sops, flags, st, pos, pre_part, pre_npart,
+                                      pos ? s2o : nullptr);
         if ((e = hipMemsetAsync(flags, 0, 4, st))) return e;
         hipLaunchKernelGGL(k_iota, g1(m), dim3(256), 0, st, perm, m);
         // multi-digit keys: the most significant digit alone orders random and spread keys
@@ -1523,7 +1531,7 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t sort_batch_buckets(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m, Scratch &s,
                                   uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags, hipStream_t st,
-                                  uint32_t *pos, const uint64_t *pre_part, uint32_t pre_npart) {
+                                  uint32_t *pos, const uint64_t *pre_part, uint32_t pre_npart, uint32_t *s2o) {
         uint32_t cb = 0;
         while ((1ull << cb) * 1024 < m) cb++;  // ~1,000 keys per coarse bucket
         const uint32_t C = 1u << cb, nwg = (uint32_t)((m + CS_TILE - 1) / CS_TILE), bbits = cb + CS_FINE_BITS;
@@ -1542,10 +1550,13 @@ struct KeyOps final : StoreKeyOps {
                            ticket);
         hipLaunchKernelGGL(k_cs_colscan, dim3((C + 63) / 64), dim3(1024), 0, st, hist, nwg, C, total, ticket, start,
                            flags, mm, npart, bbits, params);
+        // the slots' input rows only where something needs them (the ops, the fingerprints of the
+        // gather mode, a stable order of equal keys: always there when ops are)
+        uint32_t *sidx = (ops || fps || !s2o) ? idx : nullptr;
         hipLaunchKernelGGL((k_cs_scatter<KK, KL>), dim3(nwg), dim3(CS_WG), 0, st, keys, m, params, C, hist, start,
-                           okey, idx);
-        hipLaunchKernelGGL((k_cs_sort<KK, KL>), dim3(C), dim3(256), 0, st, okey, idx, start, total, params, fps, ops,
-                           skeys, sfps, sops, pos, flags);
+                           okey, sidx, s2o ? pos : nullptr);
+        hipLaunchKernelGGL((k_cs_sort<KK, KL>), dim3(C), dim3(256), 0, st, okey, sidx, start, total, params, fps, ops,
+                           skeys, sfps, sops, s2o ? nullptr : pos, flags, s2o);
         return hipGetLastError();
     }
 
@@ -1603,9 +1614,9 @@ struct KeyOps final : StoreKeyOps {
         return hipGetLastError();
     }
 
-    hipError_t keep_last_rows(const uint8_t *skeys, const uint32_t *pos, uint64_t m, uint32_t *keep,
-                              hipStream_t st) override {
-        hipLaunchKernelGGL((k_keep_last<KK, KL>), g1(m + 1), dim3(256), 0, st, skeys, pos, m, keep);
+    hipError_t keep_last_rows(const uint8_t *skeys, const uint32_t *pos, const uint32_t *s2o, uint64_t m,
+                              uint32_t *keep, hipStream_t st) override {
+        hipLaunchKernelGGL((k_keep_last<KK, KL>), g1(m + 1), dim3(256), 0, st, skeys, pos, s2o, m, keep);
         return hipGetLastError();
     }
 
@@ -1784,6 +1795,7 @@ hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch) {
     const uint64_t G = (std::max(plan, batch) + DB_WG - 1) / DB_WG;  // launch_delta_apply / launch_compact partials
     (void)s.u32(13, G * DB_PARTS), (void)s.u32(6, 2 * G), (void)s.u64(7, 4 * G);
     (void)s.u32(9, batch), (void)s.u32(10, batch), (void)s.u8(2, batch), (void)s.u8(3, batch);
+    (void)s.i32(0, batch);  // the bucket sort's slot -> sorted row
     return s.err;
 }
 

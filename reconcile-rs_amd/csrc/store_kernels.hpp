@@ -123,10 +123,16 @@ struct StoreKeyOps {
     // the digit: the order is then not final -- sort again with full = true, the LSD radix over
     // every digit.  *flags |= 1 if two batch keys are equal.  *flags is zeroed first (in stream
     // order) by the sort itself.
+    // s2o (bucket sort with pos only): the positions in two levels -- pos[input row] = its slot in
+    // its bucket's stretch (written by the scatter in input order), s2o[slot] = its sorted row
+    // (written by the bucket sort in slot order): whole-line writes both, where one level is a
+    // 4-byte store per row scattered over the whole batch.  The full sort ignores it (one level).
+    // Without ops, equal keys are ordered by slot rather than input row (they only reject the batch).
     virtual hipError_t sort_batch(const uint8_t *keys, const uint8_t *fps, const uint8_t *ops, uint64_t m,
                                   Scratch &s, uint8_t *skeys, uint8_t *sfps, uint8_t *sops, uint32_t *flags,
                                   bool full, hipStream_t st, uint32_t *pos = nullptr,
-                                  const uint64_t *pre_part = nullptr, uint32_t pre_npart = 0) = 0;
+                                  const uint64_t *pre_part = nullptr, uint32_t pre_npart = 0,
+                                  uint32_t *s2o = nullptr) = 0;
     // lower-bound rank of each query key (and whether it is present)
     virtual hipError_t search(const uint8_t *keys, uint64_t n, const uint8_t *q, uint64_t m, uint32_t *rank,
                               uint8_t *present, hipStream_t st) = 0;
@@ -145,8 +151,8 @@ struct StoreKeyOps {
     virtual hipError_t bounds(const uint8_t *keys, uint64_t n, const uint8_t *lo_key, int lo_kind,
                               const uint8_t *hi_key, int hi_kind, uint64_t *qlo, uint64_t *qhi, hipStream_t st) = 0;
     // keep[i] (i < m) = 1 unless input row i's sorted successor has its key; keep[m] = 0
-    virtual hipError_t keep_last_rows(const uint8_t *skeys, const uint32_t *pos, uint64_t m, uint32_t *keep,
-                                      hipStream_t st) = 0;
+    virtual hipError_t keep_last_rows(const uint8_t *skeys, const uint32_t *pos, const uint32_t *s2o, uint64_t m,
+                                      uint32_t *keep, hipStream_t st) = 0;
     // keys[64 j] leading digits, j < ceil(n / stride): the host tier's sample array
     virtual hipError_t sample_stride(const uint8_t *keys, uint64_t n, uint64_t stride, uint64_t *smp, hipStream_t st) = 0;
     // the key type's Ord on the host (for argument checks)

@@ -127,6 +127,8 @@ SIGNATURES = [
     ("rh_debug_fail_point", C.c_int, [C.c_char_p]),
     ("rh_debug_reload_timing", C.c_int, [C.c_int]),
     ("rh_debug_last_reload_us", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    ("rh_debug_batch_timing", C.c_int, [C.c_int]),
+    ("rh_debug_batch_kernel_us", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
 ]
 
 _lib = None

@@ -198,4 +198,6 @@ extern "C" {
     pub fn rh_debug_fail_point(name: *const c_char) -> c_int;
     pub fn rh_debug_reload_timing(on: c_int) -> c_int;
     pub fn rh_debug_last_reload_us(locate_us: *mut f64, lift_us: *mut f64) -> c_int;
+    pub fn rh_debug_batch_timing(on: c_int) -> c_int;
+    pub fn rh_debug_batch_kernel_us(lift_search_us: *mut f64, launches: *mut u64) -> c_int;
 }

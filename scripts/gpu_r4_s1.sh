@@ -25,7 +25,6 @@ for v in off on; do
   python3 scripts/write_timeline.py $O/wt_$v k_merge_run > $O/write_timeline_$v.txt 2>&1
   tail -30 $O/write_timeline_$v.txt
   rm -rf $O/wt_$v
-  run latency_$v 600 bash -c 'reconcile-rs_amd/examples/rbsr_latency 1000000 1 300 1 1 && reconcile-rs_amd/examples/rbsr_latency 100000000 1 40 1 1 && reconcile-rs_amd/examples/rbsr_latency 100000000 1 40 1 1000'
-  run inserts_$v 300 bash -c 'reconcile-rs_amd/examples/insert_latency 100000 1000000 1 && reconcile-rs_amd/examples/insert_latency 10000000 1000000 1'
+  run latency_$v 600 bash -c 'reconcile-rs_amd/examples/rbsr_latency 1000000 1 300 1 1 && reconcile-rs_amd/examples/rbsr_latency 100000000 1 40 1 1'
 done
 echo "== done"

@@ -1,0 +1,35 @@
+"""The host tier under large write batches (examples/tier_interleave.c): batches the tier's delta
+tree cannot take start a background refresh (csrc/rsos_hip_abi.hip start_refresh: the device
+compacts, a copy stream brings the new base down), the drives in between are answered by the
+device, the next write waits for the copy; batches the tree takes are folded.  Whatever the path,
+every reconciliation between the two replicas (FixedFanOut(16), the reference's
+reconciliation_drive, benches/protocol.rs:455-520) sees the same rounds, ranges, IDLIST ranges and
+enumerated keys as with the tier off -- the device path, itself checked round by round against
+oracle/rbsr.py by tests/test_rbsr_latency.py / tests/test_rbsr.py."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(ROOT, "reconcile-rs_amd", "examples", "tier_interleave")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,n,m", [("u64", 200_000, 80_000), ("c5", 200_000, 80_000), ("u64", 200_000, 2_000),
+                                       ("c5", 300_000, 500)])
+def test_interleaved_drives_equal_device_path(gpu, shape, n, m):
+    out = {}
+    for tier in (0, 1):
+        r = subprocess.run([EX, str(n), str(m), "5", str(tier), shape, "1"], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr
+        out[tier] = json.loads(r.stdout)
+    keys = ("size", "rounds", "ranges", "idlists", "enumerated", "wire_bytes")
+    assert {k: out[0][k] for k in keys} == {k: out[1][k] for k in keys}
+    assert out[1]["size"] == n + 6 * m and out[1]["idlists"] >= 1
+    if m > 65_536:  # past the tier's delta tree (max(2^16, min(n / 8, 2^18)) at these sizes): refreshed
+        assert out[1]["tier_refreshes"] >= 4 and out[1]["tier_folds"] == 0
+    else:  # folded, never copied again
+        assert out[1]["tier_refreshes"] == 0 and out[1]["tier_folds"] == 5  # store a's folds

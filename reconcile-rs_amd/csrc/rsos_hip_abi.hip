@@ -1328,10 +1328,17 @@ struct rh_store {
         const int nxt = 1 - cb;
         int rc;
         if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
-        if ((rc = bkeys[nxt].ensure(m * kl + 64)) || (rc = bfps[nxt].ensure(m * 32 + 64)) ||
-            (rc = sbsums.ensure(rh_num_blocks(m) * 32 + 32)) || (rc = sssums.ensure(rh_num_superblocks(m) * 32 + 32)) ||
-            (rc = sbsmp.ensure(rh_num_blocks(m) + 1)) || (rc = sbsmp2.ensure(rh::sample2_entries(m))) ||
-            (rc = sbtab.ensure((1ull << rh::search_table_bits(m)) + 2)) || (rc = sbtabp.ensure(2)) ||
+        // load_commit swaps the spare set in: it gets at least the active set's capacity, so that
+        // rows reserved by rh_store_reserve stay reserved across a reload (no reallocation, and
+        // no device-draining hipFree, at the next compaction)
+        auto at_least = [](size_t need, size_t cap) { return std::max(need, cap); };
+        if ((rc = bkeys[nxt].ensure(at_least(m * kl + 64, bkeys[cb].cap))) ||
+            (rc = bfps[nxt].ensure(at_least(m * 32 + 64, bfps[cb].cap))) ||
+            (rc = sbsums.ensure(at_least(rh_num_blocks(m) * 32 + 32, bsums.cap))) ||
+            (rc = sssums.ensure(at_least(rh_num_superblocks(m) * 32 + 32, ssums.cap))) ||
+            (rc = sbsmp.ensure(at_least(rh_num_blocks(m) + 1, bsmp.cap))) ||
+            (rc = sbsmp2.ensure(at_least(rh::sample2_entries(m), bsmp2.cap))) ||
+            (rc = sbtab.ensure(at_least((1ull << rh::search_table_bits(m)) + 2, btab.cap))) || (rc = sbtabp.ensure(2)) ||
             (rc = stot.ensure(4)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
         return RH_OK;

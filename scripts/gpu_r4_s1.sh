@@ -16,9 +16,9 @@ run() {  # name, timeout, cmd...
   echo "== $name rc=$rc"; tail -3 "$O/$name.log" | cut -c1-400
   [ $rc -eq 0 ] || exit $rc
 }
-run torch_repro 600 python -u scripts/torch_large_ops_repro.py 100000000
-run pytest_small 600 python -u -m pytest tests/test_small_batch.py -m gpu -x -v --timeout 300 --timeout-method thread
-run pytest_all 1100 python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread
+run torch_repro 240 python -u scripts/torch_large_ops_repro.py 100000000
+run pytest_small 240 python -u -m pytest tests/test_small_batch.py -m gpu -x -v --timeout 300 --timeout-method thread
+run pytest_all 650 python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread
 for v in off on; do
   if [ $v = off ]; then export RSOS_HIP_SMALL_MAX=0; else unset RSOS_HIP_SMALL_MAX; fi
   run write_trace_$v 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/wt_$v -o wt -- reconcile-rs_amd/examples/rbsr_latency 1000000 1 60 1 1

@@ -1671,6 +1671,9 @@ struct rh_store {
         if (next_prepared) *next_prepared = false;
         if (m == 0) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        // keeping the last row of a repeated key needs the sort to order ties by input row, which
+        // the batch sort does only when it carries the rows' indices (it does with ops)
+        if (last_wins && !ops) return fail(RH_ERR_ARG, "last-wins batch without its op column");
         if ((rc = pre_batch())) return rc;
         if (!prepared && !next && m <= small_limit()) {  // the small-batch path: two launches
             bool done = false;

@@ -1158,7 +1158,9 @@ def test_batch_path_variants_agree(gpu, oracle_lib, monkeypatch):
     batch's digit min / max formed by that launch against the sort's own pass
     (RSOS_HIP_PRE_MINMAX=0, read when a store is created), and the merges' precomputed tile bounds
     (k_tile_bounds) against each tile searching its own (RSOS_HIP_TILE_SEARCH=1, read per
-    merge): the same batches -- fresh keys, overwrites, deletes,
+    merge), and the small-batch path (one workgroup + the merge, small_batch.hpp) against the
+    large-batch path for the batches of <= 1,024 rows (RSOS_HIP_SMALL_MAX=0, read when a store is
+    created): the same batches -- 30,000, 700 and 1 rows of fresh keys, overwrites, deletes,
     through apply_device and apply_device_many, across compactions -- leave every store with the
     same counts, fingerprints, ranks and root, and that root equals the oracle's fold of the live
     records' lifts."""
@@ -1180,27 +1182,43 @@ def test_batch_path_variants_agree(gpu, oracle_lib, monkeypatch):
         o[:1_500] = 1
         bs.append(b)
         ops.append(o)
+        # two batches the small path takes: 700 rows (200 overwrites and 60 deletes of resident
+        # keys) and one fresh row
+        b2 = make_records(s, 700, seed=800 + k, random_keys=True)
+        rows = torch.randperm(200_000, device="cuda", generator=g)[:200]
+        b2["keys"][:200] = base["keys"][rows]
+        b2["phys"][:200] = base["phys"][rows] + 5
+        o2 = torch.zeros(700, dtype=torch.uint8, device="cuda")
+        o2[:60] = 1
+        bs += [b2, make_records(s, 1, seed=900 + k, random_keys=True)]
+        ops += [o2, torch.zeros(1, dtype=torch.uint8, device="cuda")]
 
-    def run(unfused, tile_search, many, pre_minmax=True):
+    def run(unfused, tile_search, many, pre_minmax=True, small=True):
         monkeypatch.setenv("RSOS_HIP_UNFUSED", "1" if unfused else "")
         monkeypatch.setenv("RSOS_HIP_TILE_SEARCH", "1" if tile_search else "0")
         monkeypatch.setenv("RSOS_HIP_PRE_MINMAX", "1" if pre_minmax else "0")
+        if small:
+            monkeypatch.delenv("RSOS_HIP_SMALL_MAX", raising=False)
+        else:
+            monkeypatch.setenv("RSOS_HIP_SMALL_MAX", "0")
         st = GpuFingerprintStore(s)
         st.set_compaction(4, 40_000)
         st.load_bulk_device(base)
         counts = st.apply_device_many(bs, ops) if many else [st.apply_device(b, o) for b, o in zip(bs, ops)]
         out = (counts, st.size(), st.aggregate(), st.fingerprints(), st.stats()["compactions"],
-               [st.select(r) for r in range(0, st.size(), 9_973)])
+               [st.select(r) for r in range(0, st.size(), 9_973)], st.batch_stats())
         st.close()
         return out
 
     ref = run(False, False, True)
     assert ref[4] > 0  # compactions happened
     for variant in [(True, False, True), (False, True, True), (True, True, False), (False, False, False),
-                    (False, False, True, False)]:
+                    (False, False, True, False), (False, False, False, True, False)]:
         got = run(*variant)
         assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2] and got[4] == ref[4], variant
         assert np.array_equal(got[3], ref[3]) and got[5] == ref[5], variant
+        if variant[2] is False:  # one call per batch: the 12 small batches took the small path, or none did
+            assert got[6]["small"] == (0 if variant[4:] == (False,) else 12), (variant, got[6])
     # the root against the oracle: Σ lift over the live records (last write wins, deletes removed)
     live = {}
     cols = {c: t.cpu().numpy() for c, t in base.items()}

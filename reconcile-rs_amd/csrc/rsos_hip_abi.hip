@@ -914,11 +914,15 @@ struct rh_store {
     // prefix sums and samples down into the tier's spare page-locked set.  Meanwhile:
     //   - if the tier is still fresh (a tree past its limit), it keeps answering, the batches
     //     applied meanwhile fold into it and are logged for the new copy; the copy is swapped in
-    //     (finish_refresh: the log replayed into a new tree) by the next write or compaction;
+    //     (finish_refresh: the log replayed into a new tree) by the next write;
     //   - if it is stale (a load, a large batch), questions are answered by the device (the delta
-    //     run is empty, so no question compacts), and the next write first waits for the copy.
-    // So no question ever pays the O(n) copy (rsos/src/fingerprint_tree_map/query.rs:25-76 never
-    // does); writes pay the compaction, and a write right behind a refresh waits for its copy.
+    //     run is empty right after the refresh's compaction), and writes go on without waiting:
+    //     logged for the copy, or, too large to log, leaving the tier stale when the copy lands,
+    //     for the next write to refresh again (one refresh per copy time under a stream of large
+    //     batches, never one per batch).
+    // So no question pays the O(n) copy (rsos/src/fingerprint_tree_map/query.rs:25-76 never does)
+    // and no write waits for one; writes pay the compaction.  A wait remains only where a copy's
+    // source would be overwritten: a second compaction during one copy, a load, a reservation.
     uint64_t version = 0;       // bumped by every change of contents (load, batch, failed load)
     uint64_t base_epoch = 0;    // bumped whenever the device's base run changes (load, compaction)
     bool tier_on = false;
@@ -947,7 +951,8 @@ struct rh_store {
     }
     // the refresh in flight (one at a time): its copy into tsets[rf_set] lands at rf_ev on cstream
     bool rf_on = false, refresh_wanted = false;
-    int rf_set = 1;
+    int rf_set = 1, rf_cb = 0;  // rf_cb: the base buffer the copy reads
+    uint64_t stale_questions = 0;  // questions the device answered since the last batch
     uint64_t rf_version = 0, rf_epoch = 0, rf_nb = 0;
     hipStream_t cstream = nullptr;
     hipEvent_t rf_ready = nullptr, rf_ev = nullptr;
@@ -1013,6 +1018,7 @@ struct rh_store {
         rf_on = true;
         refresh_wanted = false;
         rf_set = spare;
+        rf_cb = cb;
         rf_version = rf_log_version = version;
         rf_epoch = base_epoch;
         rf_nb = n;
@@ -1065,20 +1071,24 @@ struct rh_store {
     // Before anything writes what an in-flight copy reads (a compaction, a load, a reservation),
     // or before a batch while the tier is stale: let the copy land and swap it in.
     int settle() { return rf_on ? poll_refresh(true) : RH_OK; }
-    // Before a batch: a stale tier waiting for its copy takes it now (so the batch folds into a
-    // fresh tier); a landed copy is swapped in.
-    int pre_batch() { return poll_refresh(rf_on && !tier_fresh()); }
-    // After a batch (committed, folded, logged): start the refresh the tier needs.  A batch the
-    // tier could not take while a copy is in flight hands over to that copy now (the write waits
-    // for it and replays the log), so a question never replays a long log.
+    // Before a batch: a landed copy is swapped in (its log replayed).  A copy still in flight is
+    // not waited for: the batch is logged for it (or breaks its log, and the tier stays stale).
+    int pre_batch() { return poll_refresh(false); }
+    // After a batch (committed, folded, logged): start the refresh the tier needs, unless one is
+    // in flight -- so under a stream of large batches the refreshes (a compaction and a copy
+    // each) run back to back, one per copy time, not one per batch, and no write waits for one.
     int post_batch() {
-        int rc;
         if (!tier_on) return RH_OK;
-        if (rf_on && !tier_fresh() && (rc = settle())) return rc;
+        stale_questions = 0;
         if (rf_on) return RH_OK;
         if (!tier_fresh() || refresh_wanted || tier.dt.size() > tree_limit()) return start_refresh();
         return RH_OK;
     }
+    // A question to a stale tier with no copy in flight starts one only when that costs the
+    // question nothing (the delta run is empty: no compaction), or after enough questions since
+    // the last batch to pay for the compaction it waits behind -- otherwise the next batch does.
+    static constexpr uint64_t STALE_QUESTIONS = 256;
+    bool question_may_refresh() { return nd == 0 || ++stale_questions >= STALE_QUESTIONS; }
     // How a batch of m rows reaches the tier (decided before the batch, under the lock):
     //   0: it does not (tier off or stale, or the batch is larger than the tree takes: the tier
     //      goes stale and a refresh follows the batch),
@@ -1434,8 +1444,18 @@ struct rh_store {
     }
     int compact() {  // merge the delta run into the base run
         int rc;
-        if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
         if (nd == 0) return RH_OK;
+        // a tier copy in flight reads bkeys[rf_cb]; the merge writes the other base buffer, so one
+        // compaction runs beside the copy (whose log then breaks: later batches' records are
+        // relative to the new base), and a second one, which would write the buffer being copied,
+        // waits for it
+        if (rf_on) {
+            if (1 - cb == rf_cb) {
+                if ((rc = settle())) return rc;
+            } else {
+                rf_log_ok = false;
+            }
+        }
         if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64))) return rc;
         const int nxt = 1 - cb;
         const uint64_t nbk = rh_num_blocks(nb + nd);
@@ -1479,6 +1499,7 @@ struct rh_store {
     // old buffer, and hipFree waits for the whole device.
     int reserve(uint64_t rows, uint64_t batch) {
         int rc;
+        if ((rc = settle())) return rc;   // a tier copy in flight reads the base run it may move
         if ((rc = compact())) return rc;  // the delta run is empty: its buffers hold nothing
         const uint64_t thresh = std::max<uint64_t>(rows / compact_div, compact_min);
         const uint64_t plan = thresh + batch, base = rows + plan;
@@ -2200,8 +2221,8 @@ static int tier_ready(rh_store *s) {
     // on a question)
     if (s->rf_on && !s->tier_fresh() && (rc = s->poll_refresh(false))) return rc;
     if (s->tier_fresh()) return 1;
-    // stale: the device answers; a refresh is under way (or starts here if none is)
-    if (!s->rf_on && (rc = s->start_refresh())) return rc;
+    // stale: the device answers; a refresh is under way (or starts here when that is cheap)
+    if (!s->rf_on && s->question_may_refresh() && (rc = s->start_refresh())) return rc;
     return 0;
 }
 

@@ -15,8 +15,11 @@
  * are timed separately; the JSON line reports their distributions (p50 / p90 / p99 / max), the
  * rounds of the last drive (identical with the tier on or off: tests/test_tier_interleave.py) and
  * the tier's refreshes and folds.  With the tier on, a batch larger than the tier's delta tree
- * takes starts a background refresh; the drive after it is answered by the device while the copy
- * is in flight, and the next write waits for the copy.
+ * takes starts a background refresh; the drives while it is in flight are answered by the device,
+ * and writes go on without waiting for it (one refresh per copy time, never one per batch).
+ * tier_refreshes counts the refreshes started by the timed batches (the last one landed by an
+ * untimed rh_store_tier_sync after the loop); tier_refreshes_landed_in_loop those that landed
+ * inside it.
  */
 #define _POSIX_C_SOURCE 199309L
 #define __HIP_PLATFORM_AMD__ 1
@@ -255,7 +258,11 @@ int main(int argc, char **argv) {
     double wsum = 0, dsum = 0;
     uint64_t ref0 = 0, fold0 = 0, next = 1;
     for (int r = -warm; r < reps; r++) {
-        if (r == 0) CHECK(rh_store_tier_stats(a, NULL, NULL, &ref0, &fold0));
+        if (r == 0) { /* the timed loop starts from settled tiers (untimed) */
+            CHECK(rh_store_tier_sync(a));
+            CHECK(rh_store_tier_sync(b));
+            CHECK(rh_store_tier_stats(a, NULL, NULL, &ref0, &fold0));
+        }
         for (uint64_t j = 0; j < m; j++, next++)
             make_row(n + next, 1, hb.keys + j * KL, hb.vals + j * VL, DATED ? hb.phys + j : NULL,
                      DATED ? hb.logical + j : NULL, DATED ? hb.node + j : NULL);
@@ -279,8 +286,10 @@ int main(int argc, char **argv) {
             wsum += w, dsum += d;
         }
     }
-    uint64_t size = 0, refreshes = 0, folds = 0;
+    uint64_t size = 0, refreshes = 0, folds = 0, loop_refreshes = 0;
     CHECK(rh_store_len(a, &size));
+    CHECK(rh_store_tier_stats(a, NULL, NULL, &loop_refreshes, NULL));
+    CHECK(rh_store_tier_sync(a)); /* the copy the last batch started lands (untimed) */
     CHECK(rh_store_tier_stats(a, NULL, NULL, &refreshes, &folds));
     qsort(tw, (size_t)reps, sizeof(double), cmp_d);
     qsort(td, (size_t)reps, sizeof(double), cmp_d);
@@ -289,12 +298,14 @@ int main(int argc, char **argv) {
            "\"rounds\": %llu, \"ranges\": %llu, \"idlists\": %llu, \"enumerated\": %llu, \"wire_bytes\": %llu, "
            "\"first_drive_us\": %.1f, \"drive_mean_us\": %.1f, \"drive_p50_us\": %.1f, \"drive_p90_us\": %.1f, "
            "\"drive_p99_us\": %.1f, \"drive_max_us\": %.1f, \"write_mean_us\": %.1f, \"write_p50_us\": %.1f, "
-           "\"write_p99_us\": %.1f, \"write_max_us\": %.1f, \"tier_refreshes\": %llu, \"tier_folds\": %llu}\n",
+           "\"write_p99_us\": %.1f, \"write_max_us\": %.1f, \"tier_refreshes\": %llu, \"tier_refreshes_landed_in_loop\": %llu, "
+           "\"tier_folds\": %llu}\n",
            (unsigned long long)n, c5 ? "c5" : "u64", (unsigned long long)m, tier, reps, (unsigned long long)size,
            (unsigned long long)c.rounds, (unsigned long long)c.ranges, (unsigned long long)c.idlists,
            (unsigned long long)c.enumerated, (unsigned long long)c.wire_bytes, first * 1e6, dsum / reps * 1e6,
            PCT(td, 50), PCT(td, 90), PCT(td, 99), td[reps - 1] * 1e6, wsum / reps * 1e6, PCT(tw, 50), PCT(tw, 99),
-           tw[reps - 1] * 1e6, (unsigned long long)(refreshes - ref0), (unsigned long long)(folds - fold0));
+           tw[reps - 1] * 1e6, (unsigned long long)(refreshes - ref0), (unsigned long long)(loop_refreshes - ref0),
+           (unsigned long long)(folds - fold0));
     CHECK(rh_store_destroy(a));
     CHECK(rh_store_destroy(b));
     return 0;

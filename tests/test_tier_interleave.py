@@ -1,7 +1,7 @@
 """The host tier under large write batches (examples/tier_interleave.c): batches the tier's delta
 tree cannot take start a background refresh (csrc/rsos_hip_abi.hip start_refresh: the device
 compacts, a copy stream brings the new base down), the drives in between are answered by the
-device, the next write waits for the copy; batches the tree takes are folded.  Whatever the path,
+device, and writes go on without waiting for the copy; batches the tree takes are folded.  Whatever the path,
 every reconciliation between the two replicas (FixedFanOut(16), the reference's
 reconciliation_drive, benches/protocol.rs:455-520) sees the same rounds, ranges, IDLIST ranges and
 enumerated keys as with the tier off -- the device path, itself checked round by round against
@@ -30,6 +30,6 @@ def test_interleaved_drives_equal_device_path(gpu, shape, n, m):
     assert {k: out[0][k] for k in keys} == {k: out[1][k] for k in keys}
     assert out[1]["size"] == n + 6 * m and out[1]["idlists"] >= 1
     if m > 65_536:  # past the tier's delta tree (max(2^16, min(n / 8, 2^18)) at these sizes): refreshed
-        assert out[1]["tier_refreshes"] >= 4 and out[1]["tier_folds"] == 0
+        assert out[1]["tier_refreshes"] >= 1 and out[1]["tier_folds"] == 0
     else:  # folded, never copied again
         assert out[1]["tier_refreshes"] == 0 and out[1]["tier_folds"] == 5  # store a's folds

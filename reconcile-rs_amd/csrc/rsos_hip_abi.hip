@@ -1030,6 +1030,14 @@ struct rh_store {
     // The copy has landed: the new set becomes the tier's, the logged batches folded into its tree.
     void finish_refresh() {
         rf_on = false;
+        if (!(rf_log_ok && rf_log_version == version) && tier_fresh()) {
+            // the copy cannot be brought up to date but the tier still is (a tree past its limit):
+            // keep the tier, drop the copy, and let the next write start another
+            refresh_wanted = true;
+            rf_log.clear();
+            rf_keys = std::vector<uint8_t>(), rf_recs = std::vector<uint8_t>(), rf_drop = std::vector<uint8_t>();
+            return;
+        }
         tact = rf_set;
         TierSet &S = tsets[tact];
         tier.build((uint32_t)kl, schema.key_kind, rf_nb, S.keys.data(), S.prefix.data(), S.samp.data());

@@ -2601,9 +2601,10 @@ int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
     s->tier_round_max = round_max ? round_max : 128;
     if (s->tier_on) {
         if ((rc = s->tier_reserve(s->nb + s->nd + (s->nb + s->nd) / 4))) return rc;
-        if (!was_on) {  // the first copy, in the background
+        if (!was_on) {  // the first copy, in the background (an empty store's: at its load or first question)
             s->tier_version = ~0ull;
-            if ((rc = flush_locked(s)) || (rc = s->start_refresh())) return rc;
+            if ((rc = flush_locked(s))) return rc;
+            if (s->nb + s->nd > 0 && (rc = s->start_refresh())) return rc;
         }
     }
     if (!s->tier_on) {  // give the host memory back

@@ -565,7 +565,8 @@ struct PinnedVec {
     size_t n = 0, cap = 0;
     // hipHostMallocMapped: the buffer also has a device address (hipHostGetDevicePointer), so a
     // kernel may read it or write it in place; the writes are visible to the host once the
-    // stream has synchronised (the kernel's end-of-dispatch release)
+    // stream has synchronised (the kernel's end-of-dispatch release), or after a system-scope
+    // fence in the kernel (the small batch's sequence word)
     unsigned flags = hipHostMallocMapped | hipHostMallocPortable;
     PinnedVec() = default;
     PinnedVec(const PinnedVec &) = delete;
@@ -595,6 +596,7 @@ struct PinnedVec {
         p[n++] = v;
     }
     size_t size() const { return n; }
+    size_t capacity() const { return cap; }
     bool empty() const { return n == 0; }
     T *data() { return p; }
     T &operator[](size_t i) { return p[i]; }
@@ -866,6 +868,7 @@ struct rh_store {
         a.upos = upos, a.usrc = usrc, a.rlist = rlist;
         a.mcnt = mcnt.p;
         a.res = res;
+        a.seq = ++small_seq;
         a.fkeys = fk, a.frecs = fr, a.fdrop = fd, a.ffps = ff, a.fops = fo;
         bool supported = false;
         hipError_t e = rh::launch_small_batch_schema(schema.key_kind, (int)schema.key_len, schema.value_kind,
@@ -878,7 +881,7 @@ struct rh_store {
         RH_HIP(rh::launch_delta_merge(schema.key_kind, (int)kl, dkeys[cd].p, dslot[cd].p, nd, skeys.p, m, upos, usrc, rlist,
                                       mcnt.p, dkeys[nxt].p, dslot[nxt].p, rh_num_blocks(nd + m), dsmp[nxt].p,
                                       dsmp2[nxt].p, dheap.p, heap_len, stream));
-        if ((rc = sync())) return rc;
+        if ((rc = wait_small(a.seq))) return rc;
         const uint64_t *h = sb_res.data();
         if (h[6] & 1) {  // nothing committed
             version = version0;
@@ -903,7 +906,32 @@ struct rh_store {
         }
         return post_batch();
     }
-    uint64_t small_batches = 0, large_batches = 0;
+    uint64_t small_batches = 0, large_batches = 0, small_seq = 0;
+    // The small path's wait: k_small_batch writes its sequence word into the mapped result block
+    // after every host-visible result (a system-scope fence first), and the host polls it.  The
+    // merge behind it need not have finished -- it writes only device buffers, which every later
+    // command on the stream is ordered after -- so a small batch returns without the merge's time
+    // and the stream's completion signal.  A stream that fails or drains without the word is an error.
+    int wait_small(uint64_t seq) {
+        uint64_t *w = sb_res.data() + 13;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 1;; spin++) {
+            if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return RH_OK;
+            if ((spin & 63) == 0) {
+                const hipError_t e = hipStreamQuery(stream);
+                if (e == hipSuccess) {
+                    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return RH_OK;
+                    return fail(RH_ERR_HIP, "small batch: the stream finished without the result word");
+                }
+                if (e != hipErrorNotReady) return fail(RH_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                    RH_HIP(hipStreamSynchronize(stream));
+                    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return RH_OK;
+                    return fail(RH_ERR_HIP, "small batch: the stream finished without the result word");
+                }
+            }
+        }
+    }
     // ---- the host tier (host_tier.hpp) ---------------------------------------------------------
     // The tier answers from (its copy of a base run) + (its delta tree: every batch since).  It is
     // fresh while tier_version == version.  A batch of up to tree_limit() rows keeps it fresh by
@@ -991,10 +1019,14 @@ struct rh_store {
             return rc;
         const int spare = 1 - tact;
         TierSet &S = tsets[spare];
-        try {  // headroom: a growing map re-pins rarely
-            S.keys.reserve((n + n / 4) * kl + 64);
-            S.prefix.reserve((n + n / 4 + 1) * 4 + 8);
-            S.samp.reserve((n + n / 4) / 64 + 16);
+        try {  // headroom, once the set must grow anyway: a growing map re-pins rarely
+            S.keys.clear(), S.prefix.clear(), S.samp.clear();  // the old contents are not kept
+            if (S.keys.capacity() < n * kl + 64 || S.prefix.capacity() < (n + 1) * 4 + 8 ||
+                S.samp.capacity() < nsmp + 8) {
+                S.keys.reserve((n + n / 4) * kl + 64);
+                S.prefix.reserve((n + n / 4 + 1) * 4 + 8);
+                S.samp.reserve((n + n / 4) / 64 + 16);
+            }
             S.keys.resize(n * kl + 64);
             S.prefix.resize((n + 1) * 4 + 8);
             S.samp.resize(nsmp + 8);
@@ -1404,6 +1436,7 @@ struct rh_store {
         const void *k0 = tsets[tact].keys.p, *p0 = tsets[tact].prefix.p, *s0 = tsets[tact].samp.p;
         try {
             for (TierSet &S : tsets) {
+                S.keys.clear(), S.prefix.clear(), S.samp.clear();  // a move leaves the tier stale: nothing to keep
                 S.keys.reserve(rows * kl + 64);
                 S.prefix.reserve((rows + 1) * 4 + 8);
                 S.samp.reserve(rows / 64 + 16);

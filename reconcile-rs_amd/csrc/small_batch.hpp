@@ -12,12 +12,17 @@
 //      applying the rows in order: Replica::just_insert_bulk, src/replica/write.rs:107-121);
 //      otherwise they are reported (flags bit 1) and the caller commits nothing;
 //   3. every kept row lifted (lift_record, as k_lift) into its sorted slot in LDS, and every kept
-//      key searched in the base and the delta run (search_sampled_one, as k_lift_search);
+//      key searched in the base and the delta run (search_sampled_one, as k_lift_search) -- for a
+//      batch of up to 320 rows by three groups of waves at once (the launch is then 3 x the rows,
+//      rounded to waves): the lift's VALU work and the two searches' chains of dependent loads
+//      overlap instead of following one another in each thread;
 //   4. the batch's DeltaRecs into the record heap and the merge lists, exactly as k_delta_build /
 //      k_delta_parts / k_delta_lists form them (FingerprintTreeMap::insert / remove's signed
 //      deltas, rsos/src/fingerprint_tree_map/mutate.rs:23-154), the counts and totals by block
 //      reductions, the result block and (optionally) the host tier's fold rows written straight to
-//      page-locked host memory mapped into the device's address space -- no copy command.
+//      page-locked host memory mapped into the device's address space -- no copy command; every
+//      thread's writes made visible to the host (a system-scope fence), then the block's sequence
+//      word, which the host polls instead of waiting for the stream.
 // Then the delta merge (k_merge_run<HEAP>) is the second and last launch of the batch.
 #pragma once
 #include "fp_device.hpp"
@@ -32,8 +37,14 @@ __host__ __device__ constexpr uint32_t small_batch_max(int kl) { return kl <= 16
 // result block words (res): [0..2] new / overwritten / deleted rows vs the merged view, [3..5] the
 // merge's inserts / overwrites / removals in the delta run, [6] flags (1: duplicate keys, not
 // merged), [7] the change of the delta run's count total (int64), [8..11] the change of its
-// contribution total (mod 2^256), [12] rows kept
-constexpr int SMALL_RES_WORDS = 13;
+// contribution total (mod 2^256), [12] rows kept, [13] the batch's sequence number, written last
+constexpr int SMALL_RES_WORDS = 14;
+
+// threads of the launch for m rows: three groups of whole waves while they fit one workgroup
+__host__ __device__ constexpr uint32_t small_batch_threads(uint32_t m) {
+    const uint32_t r = ((m + 63) / 64) * 64;
+    return 3 * r <= 1024 ? 3 * r : r;
+}
 
 struct SmallBatch {
     DevCols c;             // the batch's columns (device memory or mapped host memory), input order
@@ -49,6 +60,7 @@ struct SmallBatch {
     uint32_t *upos, *usrc, *rlist;
     uint64_t *mcnt;        // out (device): [0] inserts, [1] overwrites, [2] removals, [3] upserts, [4] present
     uint64_t *res;         // out: the result block (SMALL_RES_WORDS words)
+    uint64_t seq;          // written to res[13] after everything else is visible to the host
     // the host tier's fold rows, in key order (each nullable): the kept keys, their DeltaRecs and
     // drop flags (folds against the device's base), their fingerprints and ops (folds against the
     // tier's own base copy)
@@ -117,6 +129,8 @@ __global__ __launch_bounds__(1024) void k_small_batch(SmallBatch a) {
     __shared__ __attribute__((aligned(16))) uint8_t K[SBM * KL];
     __shared__ __attribute__((aligned(16))) uint32_t F[SBM * 8];
     __shared__ uint16_t sidx[SBM], kidx[SBM], posof[SBM];
+    __shared__ uint32_t srb[SBM], srd[SBM];  // each sorted kept row's base / delta rank
+    __shared__ uint8_t sib[SBM], sid[SBM];   // and whether its key is there
     __shared__ uint32_t wa[16], wb[16];
     __shared__ uint32_t wcnt[16][5];
     __shared__ int32_t wdc[16];
@@ -155,8 +169,13 @@ __global__ __launch_bounds__(1024) void k_small_batch(SmallBatch a) {
     if (real) posof[sidx[t]] = keep ? (uint16_t)jn : (uint16_t)0xFFFF;
     if (keep) kidx[jn] = sidx[t];
     __syncthreads();
+    // 3. with three groups (G threads each): group 0 lifts, group 1 searches the base, group 2 the
+    // delta run; otherwise every thread does all three for its row
+    const uint32_t G = (m + 63) & ~63u;
+    const bool split = NT >= 3 * G;
+    const uint32_t role = split ? t / G : 3u, row = split ? t - role * G : t;
     // 3a. the lift of input row t into its sorted slot (the key from LDS)
-    if (t < m && posof[t] != 0xFFFF) {
+    if ((role == 0 || role == 3) && row < m && posof[row] != 0xFFFF) {
         uint32_t kw[L::KEY_ENC / 4 > 0 ? L::KEY_ENC / 4 : 1];
         uint32_t sw[5];
         load_key<KK, KL, uint32_t>(K, t, kw);
@@ -169,18 +188,29 @@ __global__ __launch_bounds__(1024) void k_small_batch(SmallBatch a) {
 #pragma unroll
         for (int q = 0; q < 8; q++) o[q] = h[q];
     }
-    // 3b. sorted kept row t: where its key is in the base and the delta run
+    // 3b. sorted kept row `row`: where its key is in the base and the delta run
+    if (row < m2 && role != 0) {
+        const uint8_t *key = K + kidx[row] * KL;
+        uint32_t rk = 0, rk2 = 0;
+        uint8_t in = 0, in2 = 0;
+        if (role != 2) {
+            search_sampled_one<KK, KL>(a.jb.keys, a.jb.n, a.jb.smp, a.jb.smp2, a.jb.tb, key, &rk, &in);
+            srb[row] = rk;
+            sib[row] = in;
+            copy_key_words<KL>(a.skeys + (uint64_t)row * KL, key);
+        }
+        if (role != 1) {
+            search_sampled_one<KK, KL>(a.jd.keys, a.jd.n, a.jd.smp, a.jd.smp2, a.jd.tb, key, &rk2, &in2);
+            srd[row] = rk2;
+            sid[row] = in2;
+        }
+    }
+    __syncthreads();  // F, the ranks complete
     const bool act = t < m2;
     const uint32_t src = act ? kidx[t] : 0u;
     const uint8_t *key = K + src * KL;
-    uint32_t rank_b = 0, rank_d = 0;
-    uint8_t in_b = 0, in_d = 0;
-    if (act) {
-        search_sampled_one<KK, KL>(a.jb.keys, a.jb.n, a.jb.smp, a.jb.smp2, a.jb.tb, key, &rank_b, &in_b);
-        search_sampled_one<KK, KL>(a.jd.keys, a.jd.n, a.jd.smp, a.jd.smp2, a.jd.tb, key, &rank_d, &in_d);
-        copy_key_words<KL>(a.skeys + (uint64_t)t * KL, key);
-    }
-    __syncthreads();  // F complete
+    const uint32_t rank_b = act ? srb[t] : 0u, rank_d = act ? srd[t] : 0u;
+    const uint8_t in_b = act ? sib[t] : 0, in_d = act ? sid[t] : 0;
     // 4. the row's DeltaRec (k_delta_build's rule)
     bool c_new = false, c_over = false, c_del = false, c_up = false, c_pr = false;
     int32_t dcnt = 0;
@@ -295,6 +325,10 @@ __global__ __launch_bounds__(1024) void k_small_batch(SmallBatch a) {
         for (int q = 0; q < 4; q++) o[8 + q] = (uint64_t)f[2 * q] | ((uint64_t)f[2 * q + 1] << 32);
         o[12] = m2;
     }
+    // every thread's host-visible writes (the fold rows, the result block) before the sequence word
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(a.res + 13, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace rh

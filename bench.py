@@ -463,8 +463,13 @@ def incremental(args, world, rank, dev, dist):
         if m_over:  # re-stamp distinct existing keys of this shard: an overwrite, the new - old delta (mutate.rs:31-41)
             rows = torch.randperm(n, generator=gen, device=dev)[:m_over]
             mo = min(m_over, b["keys"].shape[0])
-            b["keys"][:mo] = base["keys"][rows[:mo]]
-            b["phys"][:mo] = base["phys"][rows[:mo]] + 1_000_000
+            # the picked resident rows regenerated from their global indices (the generator is
+            # counter-based), not gathered from the 10^8-row columns: torch's gathers of 10^8
+            # output rows return wrong rows on this image (profiles/r04_torch_large_ops_repro.log)
+            old = make_records(schema, mo, seed=42, device=dev, key_space=n * world, indices=rows[:mo] + rank * n)
+            b["keys"][:mo] = old["keys"]
+            b["phys"][:mo] = old["phys"] + 1_000_000
+            del old
         batches.append(b)
     del base
     torch.cuda.synchronize()

@@ -60,7 +60,8 @@ def _row_bytes(seed: int, idx: torch.Tensor, width: int, chunk_words: int = 1 <<
 
 def make_records(schema: RecordSchema, n: int, seed: int = 42, device="cuda",
                  tombstone_fraction: float = 0.0, first_index: int = 0,
-                 random_keys: bool = False, key_space: int = 0) -> Dict[str, torch.Tensor]:
+                 random_keys: bool = False, key_space: int = 0,
+                 indices: torch.Tensor = None) -> Dict[str, torch.Tensor]:
     """Rows [first_index, first_index + n) of a key-sorted set of `key_space` records
     (default first_index + n) whose keys spread evenly over the whole key space: row i's
     first 8 key bytes are the big-endian u64 i * stride + r, r < stride = 2^64 / key_space.
@@ -68,10 +69,18 @@ def make_records(schema: RecordSchema, n: int, seed: int = 42, device="cuda",
     [a, b) of the set is the same rows whether it is generated alone or as part of the whole
     (strong-scaling runs at any GPU count hash the same data set).
     random_keys: uniformly random byte keys instead (unsorted; update batches that land
-    anywhere in an existing key range)."""
+    anywhere in an existing key range).
+    indices: the global row indices to generate (int64, n of them) instead of
+    [first_index, first_index + n) -- rows picked from a set without gathering its columns
+    (bench.py's overwrites of resident keys); key_space must then be given."""
     dev = torch.device(device)
     cols: Dict[str, torch.Tensor] = {}
-    idx = torch.arange(first_index, first_index + n, device=dev, dtype=torch.int64)
+    if indices is not None:
+        if not key_space or indices.shape[0] != n:
+            raise ValueError("indices: n of them, and the set's key_space")
+        idx = indices.to(device=dev, dtype=torch.int64).contiguous()
+    else:
+        idx = torch.arange(first_index, first_index + n, device=dev, dtype=torch.int64)
     sk, sv, st = seed * 4 + 1, seed * 4 + 2, seed * 4 + 3  # key / value / tag streams
     if schema.key_kind == A.KEY_BYTES:
         kl = schema.key_len

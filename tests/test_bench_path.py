@@ -142,3 +142,19 @@ def test_config5_routed_batches_equal_one_store(tmp_path, gpu, world):
         assert got["ranges"][j] == [x - (1 << 64) if x >> 63 else x for x in a.fingerprint.limbs] + [a.size]
     st.close()
     torch.cuda.synchronize()
+
+
+def test_records_by_index_equal_the_rows_of_the_set():
+    """bench.py's overwrites regenerate the picked resident rows from their global indices
+    (make_records(indices=...)) instead of gathering them from the 10^8-row columns: the same bytes
+    as the rows of the whole set, for byte and integer keys (CPU, no GPU needed)."""
+    import torch
+    from rsos_hip import RecordSchema
+    from rsos_hip.synth import make_records
+    for s in (RecordSchema.dated("bytes16", "bytes64"), RecordSchema.plain("u64", "u64")):
+        whole = make_records(s, 50_000, seed=42, device="cpu", first_index=200_000, key_space=400_000)
+        rows = torch.randperm(50_000, generator=torch.Generator().manual_seed(3))[:4_000]
+        picked = make_records(s, 4_000, seed=42, device="cpu", key_space=400_000, indices=rows + 200_000)
+        assert set(picked) == set(whole)
+        for c in whole:
+            assert torch.equal(whole[c][rows], picked[c]), c

@@ -1251,8 +1251,8 @@ def test_full_size_config5_100m(gpu, oracle_lib, n):
     then 18 batches of 1 M rows -- 900 k fresh random keys, 50 k overwrites and 50 k deletes of
     resident keys each -- so the delta run passes the compaction threshold at this size (a
     111 M-row base is merged at least once).  Afterwards, against exactly the records that should be
-    live (assembled and key-sorted on the host with numpy; torch's gathers and sorts of 10^8-row
-    tensors gave wrong rows on this image): the root and size (an independent torch reduction of
+    live (assembled and key-sorted on the host with numpy; torch's gathers with 10^8 output rows
+    return wrong rows on this image: profiles/r04_torch_large_ops_repro.log): the root and size (an independent torch reduction of
     their lifts); the store's whole rank order dumped -- every key and fingerprint, row for row;
     select at 200 ranks; rank of present and absent keys; 20 rank-range and key-range aggregates;
     and the fingerprints at 20 sampled ranks against the oracle's lift of those records

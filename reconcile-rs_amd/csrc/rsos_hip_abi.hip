@@ -1013,36 +1013,38 @@ struct rh_store {
             RH_HIP(hipEventCreateWithFlags(&rf_ready, hipEventDisableTiming));
             RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
         }
-        const uint64_t n = nb, nbk = rh_num_blocks(n), ns = rh_num_superblocks(n), nsmp = (n + 63) / 64;
+        const uint64_t n = nb, nbk = rh_num_blocks(n), ns = rh_num_superblocks(n), nsmp = (n + 63) / 64,
+                       nsmp2 = (n + 4095) / 4096;  // the samples' index (host_tier.hpp samp2)
         if ((rc = tier_dpre.ensure((n + 1) * 32 + 64)) || (rc = tier_spre.ensure((ns + 1) * 32 + 64)) ||
-            (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)) || (rc = tier_dsmp.ensure(nsmp + 8)))
+            (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)) || (rc = tier_dsmp.ensure(nsmp + nsmp2 + 8)))
             return rc;
         const int spare = 1 - tact;
         TierSet &S = tsets[spare];
         try {  // headroom, once the set must grow anyway: a growing map re-pins rarely
             S.keys.clear(), S.prefix.clear(), S.samp.clear();  // the old contents are not kept
             if (S.keys.capacity() < n * kl + 64 || S.prefix.capacity() < (n + 1) * 4 + 8 ||
-                S.samp.capacity() < nsmp + 8) {
+                S.samp.capacity() < nsmp + nsmp2 + 8) {
                 S.keys.reserve((n + n / 4) * kl + 64);
                 S.prefix.reserve((n + n / 4 + 1) * 4 + 8);
-                S.samp.reserve((n + n / 4) / 64 + 16);
+                S.samp.reserve((n + n / 4) / 64 + (n + n / 4) / 4096 + 16);
             }
             S.keys.resize(n * kl + 64);
             S.prefix.resize((n + 1) * 4 + 8);
-            S.samp.resize(nsmp + 8);
+            S.samp.resize(nsmp + nsmp2 + 8);
         } catch (const std::bad_alloc &) {
             return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
         }
         if (n) {
             RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, stream));
             RH_HIP(kops->sample_stride(bkeys[cb].p, n, 64, tier_dsmp.p, stream));
+            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 4096, tier_dsmp.p + nsmp, stream));
         }
         RH_HIP(hipEventRecord(rf_ready, stream));
         RH_HIP(hipStreamWaitEvent(cstream, rf_ready, 0));
         if (n) {
             RH_HIP(hipMemcpyAsync(S.keys.data(), bkeys[cb].p, n * kl, hipMemcpyDeviceToHost, cstream));
             RH_HIP(hipMemcpyAsync(S.prefix.data(), tier_dpre.p, (n + 1) * 32, hipMemcpyDeviceToHost, cstream));
-            RH_HIP(hipMemcpyAsync(S.samp.data(), tier_dsmp.p, nsmp * 8, hipMemcpyDeviceToHost, cstream));
+            RH_HIP(hipMemcpyAsync(S.samp.data(), tier_dsmp.p, (nsmp + nsmp2) * 8, hipMemcpyDeviceToHost, cstream));
         } else {
             memset(S.prefix.data(), 0, 32);
         }
@@ -1072,7 +1074,8 @@ struct rh_store {
         }
         tact = rf_set;
         TierSet &S = tsets[tact];
-        tier.build((uint32_t)kl, schema.key_kind, rf_nb, S.keys.data(), S.prefix.data(), S.samp.data());
+        tier.build((uint32_t)kl, schema.key_kind, rf_nb, S.keys.data(), S.prefix.data(), S.samp.data(),
+                   S.samp.data() + (rf_nb + 63) / 64);
         tier_epoch = rf_epoch;
         tier_refreshes++;
         bool ok = rf_log_ok && rf_log_version == version;
@@ -1439,7 +1442,7 @@ struct rh_store {
                 S.keys.clear(), S.prefix.clear(), S.samp.clear();  // a move leaves the tier stale: nothing to keep
                 S.keys.reserve(rows * kl + 64);
                 S.prefix.reserve((rows + 1) * 4 + 8);
-                S.samp.reserve(rows / 64 + 16);
+                S.samp.reserve(rows / 64 + rows / 4096 + 16);
             }
         } catch (const std::bad_alloc &) {
             tier_version = ~0ull;

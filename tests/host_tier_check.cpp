@@ -145,6 +145,16 @@ int main(int argc, char **argv) {
             const std::string &z = uni[rng() % uni.size()];
             const uint8_t *zk = (const uint8_t *)z.data();
             EXPECT(A.rank(zk) == B.rank(zk), "rank");
+            {  // and against a plain binary search of the flattened model (no samples, no index)
+                uint64_t lo = 0, hi = n;
+                while (lo < hi) {
+                    const uint64_t mid = (lo + hi) / 2;
+                    if (ko.cmp(cur.keys.data() + mid * kl, zk) < 0) lo = mid + 1;
+                    else hi = mid;
+                }
+                EXPECT(B.rank(zk) == lo, "rank vs the model: %llu vs %llu", (unsigned long long)B.rank(zk),
+                       (unsigned long long)lo);
+            }
             const std::string &z2 = uni[rng() % uni.size()];
             const uint8_t *zk2 = (const uint8_t *)z2.data();
             for (int lk = 0; lk < 3; lk++)

@@ -1116,13 +1116,26 @@ struct rh_store {
     int settle() { return rf_on ? poll_refresh(true) : RH_OK; }
     // Before a batch: a landed copy is swapped in (its log replayed).  A copy still in flight is
     // not waited for: the batch is logged for it (or breaks its log, and the tier stays stale).
-    int pre_batch() { return poll_refresh(false); }
+    // RSOS_HIP_TIER_SYNC=1 (read when a store is created): writes keep the tier fresh instead --
+    // a stale tier's copy is waited for here, and a refresh a batch starts is waited for by that
+    // batch (post_batch), so questions are never answered by the device but a write that outgrows
+    // the tree pays the compaction and the whole copy.
+    bool tier_sync_writes = getenv("RSOS_HIP_TIER_SYNC") && atoi(getenv("RSOS_HIP_TIER_SYNC")) == 1;
+    int pre_batch() { return poll_refresh(tier_sync_writes && rf_on && !tier_fresh()); }
     // After a batch (committed, folded, logged): start the refresh the tier needs, unless one is
     // in flight -- so under a stream of large batches the refreshes (a compaction and a copy
     // each) run back to back, one per copy time, not one per batch, and no write waits for one.
     int post_batch() {
         if (!tier_on) return RH_OK;
         stale_questions = 0;
+        int rc;
+        if (tier_sync_writes) {
+            if (rf_on && !tier_fresh() && (rc = settle())) return rc;
+            if (!tier_fresh() && !rf_on) {
+                if ((rc = start_refresh())) return rc;
+                return settle();
+            }
+        }
         if (rf_on) return RH_OK;
         if (!tier_fresh() || refresh_wanted || tier.dt.size() > tree_limit()) return start_refresh();
         return RH_OK;

@@ -23,4 +23,5 @@ run inserts 300 bash -c 'reconcile-rs_amd/examples/insert_latency 100000 1000000
 run interleave_trace 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/it -o it -- reconcile-rs_amd/examples/tier_interleave 100000000 1000000 8 1 c5 1
 python3 scripts/copy_summary.py $O/it > $O/interleave_copies.txt 2>&1; rm -rf $O/it
 run interleave_c5_1m_tier1 400 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 20 1 c5 2
+run interleave_c5_1m_tier1_sync 400 env RSOS_HIP_TIER_SYNC=1 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 20 1 c5 2
 echo "== done"

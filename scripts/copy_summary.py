@@ -24,14 +24,15 @@ def main():
             k[0] += 1
             k[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     copies.sort()
-    big = [c for c in copies if c[2] >= 1 << 20]
+    # the copy trace may carry no byte count: a copy of >= 1 MiB or of >= 1 ms counts as large
+    big = [c for c in copies if c[2] >= 1 << 20 or c[1] - c[0] >= 1_000_000]
     t0 = copies[0][0] if copies else 0
-    print("copies: %d in all, %d of >= 1 MiB" % (len(copies), len(big)))
+    print("copies: %d in all, %d of >= 1 MiB or >= 1 ms" % (len(copies), len(big)))
     for s, e, b, dr in big:
         us = (e - s) / 1e3
         print("  at %10.1f ms  %-14s %10.1f MB  %9.1f us  %6.1f GB/s" % ((s - t0) / 1e6, dr, b / 1e6, us,
                                                                        b / us / 1e3 if us > 0 else 0))
-    small = [c for c in copies if c[2] < 1 << 20]
+    small = [c for c in copies if c not in big]
     if small:
         durs = sorted((e - s) / 1e3 for s, e, _, _ in small)
         print("small copies: %d, median %.1f us, p99 %.1f us, max %.1f us" %

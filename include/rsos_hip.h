@@ -272,15 +272,19 @@ int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
 /* The tier after a batch (host_tier.hpp, host_delta.hpp): the tier holds a copy of the device's
  * base run plus a B+ tree of the signed deltas of every batch since (the device's own DeltaRecs,
  * count and contribution per touched key), so a batch of up to max(2^16, min(base / 8, 2^18)) rows
- * updates it in O(batch log n) -- the reference's O(log n) per insert (mutate.rs:23-88).  A load,
- * a larger batch, or a tree past that size refreshes the copy IN THE BACKGROUND: the device
- * compacts and a copy stream brings the new base down into a second page-locked set; a tier
- * that is still fresh keeps answering meanwhile (the batches applied meanwhile are logged and
- * replayed into the new copy's tree), a stale one hands the questions to the device (its delta
- * run is then empty: no question compacts) -- so no question waits for the O(n) copy.  The next
- * write after a load or a large batch waits for the copy instead.
- * Stats (nullable): base rows and delta entries of a fresh tier (0, 0 when stale), refreshes
- * swapped in and batch folds so far.                                                            */
+ * updates it in O(batch log n) -- the reference's O(log n) per insert (mutate.rs:23-88).  A
+ * larger batch, while the tier's base is still the device's (no compaction since its copy), takes
+ * a copy of the device's delta run instead (its DeltaRecs with prefix sums: O(delta run), not
+ * O(n)); a load, a batch after a compaction or after such a run copy, or a tree past its size
+ * refreshes the base copy: the device compacts and a copy stream brings the new base down into a
+ * second page-locked set.  By default (RSOS_HIP_TIER_SYNC unset or 1) the write or load that
+ * starts a refresh waits for it, so every question is answered from a fresh tier; with
+ * RSOS_HIP_TIER_SYNC=0 writes never wait -- a stale tier hands the questions to the device (its
+ * delta run is then empty: no question compacts) and batches applied during a copy are logged and
+ * replayed into it.  No question waits for an O(n) copy under either policy.
+ * Stats (nullable): base rows and delta entries (tree entries + run-copy entries) of a fresh tier
+ * (0, 0 when stale), copies taken from the device (base refreshes and run copies) and batch folds
+ * so far.                                                                                        */
 int rh_store_tier_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_entries, uint64_t *refreshes,
                         uint64_t *folds);
 /* Wait until the host tier is fresh (a background refresh landed and swapped in, one started if

@@ -48,6 +48,33 @@ struct HostTier {
     std::vector<uint64_t> samp2_own;
     DeltaTree dt;
     static constexpr unsigned SHIFT = 6;
+    // A copy of the device's delta run (the run copy), taken after a batch too large for the
+    // tree: its entries in key order, each the DeltaRec the device keeps for the key (the
+    // contribution cur - base and the count delta live - in_base relative to the base, its flags
+    // and its base rank), with exclusive prefix sums of both, all formed on the device
+    // (rsos_hip_abi.hip tier_run_snapshot).  Base + run copy is the whole map, as the device's
+    // base + delta run is; the tree is empty while a run copy is held (the next small batch
+    // refreshes the base instead).
+    struct Run {
+        uint64_t n = 0;
+        const uint8_t *keys = nullptr;      // n * kl, key order
+        const uint64_t *prefix = nullptr;   // (n + 1) * 4 limbs: Σ contribs of entries [0, i)
+        const int32_t *cntp = nullptr;      // n + 1: Σ count deltas of entries [0, i)
+        const uint8_t *flags = nullptr;     // n: DeltaRec flags (1 in the base, 2 live)
+        const uint32_t *brank = nullptr;    // n: base rows below the key
+        const uint64_t *samp = nullptr, *samp2 = nullptr;  // digits of every 64th / 4096th key
+        uint64_t ns = 0, ns2 = 0;
+    };
+    Run run;
+    bool has_run() const { return run.n != 0; }
+    // hold a run copy (replacing the tree: the run holds every change since the base copy)
+    void set_run(const Run &r) {
+        run = r;
+        run.ns = (r.n + 63) >> SHIFT;
+        run.ns2 = (run.ns + 63) >> SHIFT;
+        dt.clear();
+        n = (uint64_t)((int64_t)nb + (r.n ? r.cntp[r.n] : 0));
+    }
 
     uint64_t digit(const uint8_t *k) const { return ko.digit(k); }
     int cmp(const uint8_t *a, const uint8_t *b) const { return ko.cmp(a, b); }
@@ -63,6 +90,7 @@ struct HostTier {
         dt.set_order(ko);
         samp_own.clear();
         samp2_own.clear();
+        run = Run{};
         samp = samp2 = nullptr;
         ns = ns2 = 0;
         if (!keys) return;  // the encoded store keeps its keys on the host side of the ABI
@@ -85,13 +113,31 @@ struct HostTier {
     }
     // the first sample >= d (> d with upper), through the index: samp[64 (i - 1)] < d (<= d) and
     // samp[64 i] >= d (> d) bound a window of 63 samples
-    uint64_t samp_bound(uint64_t d, bool upper, uint64_t from = 0) const {
+    static uint64_t samp_bound(const uint64_t *samp, uint64_t ns, const uint64_t *samp2, uint64_t ns2, uint64_t d,
+                               bool upper, uint64_t from = 0) {
         const uint64_t i = upper ? std::upper_bound(samp2, samp2 + ns2, d) - samp2
                                  : std::lower_bound(samp2, samp2 + ns2, d) - samp2;
         const uint64_t lo = std::max<uint64_t>(from, i ? ((i - 1) << SHIFT) + 1 : 0);
         const uint64_t hi = std::min<uint64_t>(ns, i << SHIFT);
         if (lo >= hi) return lo;  // the window is empty: the bound is its start
         return upper ? std::upper_bound(samp + lo, samp + hi, d) - samp : std::lower_bound(samp + lo, samp + hi, d) - samp;
+    }
+    // keys below `key` among n sorted keys with those samples: the samples narrow it to one window
+    // of 64 keys (or the run of keys sharing its digit), then a binary search
+    uint64_t sampled_lb(const uint8_t *ks, uint64_t nk, const uint64_t *sp, uint64_t nsp, const uint64_t *sp2,
+                        uint64_t nsp2, const uint8_t *key) const {
+        if (nk == 0) return 0;
+        const uint64_t d = digit(key);
+        const uint64_t jl = samp_bound(sp, nsp, sp2, nsp2, d, false);
+        const uint64_t jh = samp_bound(sp, nsp, sp2, nsp2, d, true, jl);
+        uint64_t lo = jl ? ((jl - 1) << SHIFT) + 1 : 0;     // keys[64 (jl - 1)] < key
+        uint64_t hi = std::min<uint64_t>(nk, jh << SHIFT);  // keys[64 jh] > key
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (cmp(ks + mid * kl, key) < 0) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
     }
     // forget everything (tier off)
     void reset() {
@@ -124,6 +170,7 @@ struct HostTier {
     // m sorted, distinct rows into the delta tree; drop[j]: remove row j's key.  A batch large
     // against the tree is one merge pass over the whole tree instead of m walks.
     void fold(const DeltaTree::Rec *rows, const uint8_t *drop, size_t m) {
+        if (has_run()) return;  // the caller refreshes instead (fold_mode is 0 with a run copy)
         if (m > 256 && m * 16 > dt.size()) {
             dt.merge_rebuild(rows, drop, m);
         } else {
@@ -136,33 +183,31 @@ struct HostTier {
     }
 
     // base rows with key < z
-    uint64_t rank_b(const uint8_t *key) const {
-        if (nb == 0) return 0;
-        const uint64_t d = digit(key);
-        const uint64_t jl = samp_bound(d, false);
-        const uint64_t jh = samp_bound(d, true, jl);
-        uint64_t lo = jl ? ((jl - 1) << SHIFT) + 1 : 0;  // keys[64 (jl - 1)] < key
-        uint64_t hi = std::min<uint64_t>(nb, jh << SHIFT);  // keys[64 jh] > key
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (cmp(keys + mid * kl, key) < 0) lo = mid + 1;
-            else hi = mid;
-        }
-        return lo;
+    uint64_t rank_b(const uint8_t *key) const { return sampled_lb(keys, nb, samp, ns, samp2, ns2, key); }
+    // run entries with key < z
+    uint64_t rank_run(const uint8_t *key) const {
+        return sampled_lb(run.keys, run.n, run.samp, run.ns, run.samp2, run.ns2, key);
     }
 
     // A place in the merged key order: r live keys below it, b base rows below it, d delta entries
     // below it; k = the live key at rank r (set by at(), r < n).
+    // With a run copy: j run entries below it (the tree is then empty, d = 0).
     struct Cur {
         uint64_t r = 0, b = 0, d = 0;
         const uint8_t *k = nullptr;
+        uint64_t j = 0;
     };
-    Cur begin() const { return Cur{0, 0, 0, nullptr}; }
-    Cur end() const { return Cur{n, nb, dt.size(), nullptr}; }
+    Cur begin() const { return Cur{0, 0, 0, nullptr, 0}; }
+    Cur end() const { return Cur{n, nb, dt.size(), nullptr, run.n}; }
     // keys < z
     Cur lt(const uint8_t *z) const {
         Cur c;
         c.b = rank_b(z);
+        if (has_run()) {  // live keys below z = base rows below z + Σ count deltas of run entries below z
+            c.j = rank_run(z);
+            c.r = (uint64_t)((int64_t)c.b + run.cntp[c.j]);
+            return c;
+        }
         if (plain()) {
             c.r = c.b;
             return c;
@@ -177,6 +222,12 @@ struct HostTier {
         Cur c;
         c.b = rank_b(z);
         if (c.b < nb && cmp(keys + c.b * kl, z) == 0) c.b++;
+        if (has_run()) {
+            c.j = rank_run(z);
+            if (c.j < run.n && cmp(run.keys + c.j * kl, z) == 0) c.j++;
+            c.r = (uint64_t)((int64_t)c.b + run.cntp[c.j]);
+            return c;
+        }
         if (plain()) {
             c.r = c.b;
             return c;
@@ -189,7 +240,8 @@ struct HostTier {
     // select: the place of the r-th live key (r <= n; r == n is end())
     Cur at(uint64_t r) const {
         if (r >= n) return end();
-        if (plain()) return Cur{r, r, 0, keys + r * kl};
+        if (has_run()) return at_run(r);
+        if (plain()) return Cur{r, r, 0, keys + r * kl, 0};
         // F(b) = live keys <= base key b, non-decreasing in b; find the smallest b with F(b) > r.
         // |F(b) - b| <= delta entries + 1 brackets the search.
         const uint64_t nd = dt.size();
@@ -209,7 +261,7 @@ struct HostTier {
             DeltaTree::Pos p;
             const uint64_t f = F(b, &p);
             const bool live = !p.found || p.flive;
-            if (live && f - 1 == r) return Cur{r, b, p.idx, keys + b * kl};
+            if (live && f - 1 == r) return Cur{r, b, p.idx, keys + b * kl, 0};
         }
         // the r-th live key is an inserted delta key between base keys b - 1 and b: every delta
         // entry in that gap is one (a key not in the base is in the delta run only while live)
@@ -220,11 +272,35 @@ struct HostTier {
             d0 = q.idx + (q.found ? 1 : 0);
         }
         const uint64_t d = d0 + (r - fprev);
-        return Cur{r, b, d, dt.key_at(d)};
+        return Cur{r, b, d, dt.key_at(d), 0};
+    }
+    // select over base + run copy: G(j) = live keys <= run key j = brank + cntp + live, non-
+    // decreasing; the first entry with G(j) > r is the r-th live key itself, or the r-th live key
+    // is an untouched base row between entries j - 1 and j (those rows are consecutive)
+    bool run_live(uint64_t j) const { return run.flags[j] & 2; }
+    bool run_in_base(uint64_t j) const { return run.flags[j] & 1; }
+    uint64_t run_below(uint64_t j) const { return (uint64_t)((int64_t)run.brank[j] + run.cntp[j]); }
+    Cur at_run(uint64_t r) const {
+        uint64_t lo = 0, hi = run.n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (run_below(mid) + (run_live(mid) ? 1 : 0) > r) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint64_t j = lo;
+        if (j < run.n && run_below(j) == r && run_live(j)) return Cur{r, run.brank[j], 0, run.keys + j * kl, j};
+        const uint64_t gprev = j ? run_below(j - 1) + (run_live(j - 1) ? 1 : 0) : 0;
+        const uint64_t b0 = j ? run.brank[j - 1] + (run_in_base(j - 1) ? 1 : 0) : 0;
+        const uint64_t b = b0 + (r - gprev);
+        return Cur{r, b, 0, keys + b * kl, j};
     }
     // Σ fingerprints of the live keys below c
     void pre(const Cur &c, uint64_t out[4]) const {
         memcpy(out, prefix + 4 * c.b, 32);
+        if (has_run()) {
+            fp4_add(out, run.prefix + 4 * c.j);
+            return;
+        }
         if (!plain() && c.d) {
             uint64_t t[4];
             dt.fp_prefix(c.d, t);
@@ -250,7 +326,7 @@ struct HostTier {
     void agg(uint64_t lo, uint64_t hi, rh_aggregate *o) const {
         if (hi > n) hi = n;
         if (lo > hi) lo = hi;
-        if (plain()) {
+        if (plain() && !has_run()) {
             uint64_t a[4];
             memcpy(a, prefix + 4 * hi, 32);
             fp4_sub(a, prefix + 4 * lo);
@@ -269,6 +345,24 @@ struct HostTier {
     // the keys of ranks [lo, hi) (hi <= n), in order
     void copy_keys(uint64_t lo, uint64_t hi, uint8_t *out) const {
         if (hi <= lo) return;
+        if (has_run()) {  // base rows and run entries merged: an entry replaces its base row
+            const Cur c = at(lo);
+            uint64_t b = c.b, j = c.j;
+            for (uint64_t r = lo; r < hi;) {
+                if (j < run.n && b >= run.brank[j]) {
+                    if (run_in_base(j)) b++;
+                    if (run_live(j)) {
+                        memcpy(out, run.keys + j * kl, kl);
+                        out += kl, r++;
+                    }
+                    j++;
+                } else {
+                    memcpy(out, keys + b * kl, kl);
+                    out += kl, r++, b++;
+                }
+            }
+            return;
+        }
         if (plain()) {
             memcpy(out, keys + lo * kl, (hi - lo) * kl);
             return;

@@ -833,6 +833,7 @@ struct rh_store {
         if (m == 0 || m > small_limit()) return RH_OK;
         if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         if ((rc = pre_batch())) return rc;
+        snap_ok = run_copy_allowed(m);
         int fmode = fold_mode(m);
         bool want = fold_rows_wanted(fmode);
         if (want && !fold_room(m)) fmode = 0, want = false, rf_log_ok = false;  // the tier goes stale
@@ -1134,6 +1135,12 @@ struct rh_store {
         int rc;
         if (tier_sync_writes) {
             if (rf_on && !tier_fresh() && (rc = settle())) return rc;
+            const bool snap = snap_ok;
+            snap_ok = false;
+            // a large batch into a tier whose base is still the device's: copy the delta run
+            // (unless it has grown past a quarter of the base: then the base is refreshed)
+            if (snap && !tier_fresh() && !rf_on && tier_epoch == base_epoch && nd <= tier.nb / 4 + (1u << 16))
+                return tier_run_snapshot();
             if (!tier_fresh() && !rf_on) {
                 if ((rc = start_refresh())) return rc;
                 return settle();
@@ -1148,6 +1155,91 @@ struct rh_store {
     // the last batch to pay for the compaction it waits behind -- otherwise the next batch does.
     static constexpr uint64_t STALE_QUESTIONS = 256;
     bool question_may_refresh() { return nd == 0 || ++stale_questions >= STALE_QUESTIONS; }
+    // ---- the tier's run copy (host_tier.hpp HostTier::Run) --------------------------------------
+    // With writes keeping the tier fresh, a batch too large for the tree would cost a compaction
+    // and a copy of the whole base (~0.1 s per 10^8 rows).  While the tier's base is still the
+    // device's (no compaction since its copy), the device's delta run is exactly every change
+    // since: its DeltaRecs, as columns with prefix sums, are copied down instead -- O(delta run),
+    // <= n / compact_div rows -- and the tier answers from base + run copy.  The next small batch
+    // (or a compaction, or a run copy past a quarter of the base) refreshes the base instead.
+    DevBuf<uint8_t> trun_c, trun_fl, trun_bs, trun_ss, trun_spre, trun_bpre, trun_pre;
+    DevBuf<uint32_t> trun_cnt, trun_cntp, trun_br;
+    DevBuf<uint64_t> trun_smp;
+    PinnedVec<uint8_t> trh_keys, trh_fl;
+    PinnedVec<uint64_t> trh_pre, trh_smp;
+    PinnedVec<uint32_t> trh_cntp, trh_br;
+    uint64_t tier_runs = 0;
+    bool snap_ok = false;  // set before a batch: a run copy may replace the refresh it causes
+    bool run_copy_allowed(size_t m) const {
+        return tier_sync_writes && tier_fresh() && tier_epoch == base_epoch && m > tree_limit();
+    }
+    int tier_run_snapshot() {
+        int rc;
+        const uint64_t n1 = nd;
+        if (n1 == 0) {  // nothing since the base copy: the base alone is the map
+            tier.set_run(rh::HostTier::Run{});
+            tier_version = version;
+            return RH_OK;
+        }
+        const uint64_t nbk = rh_num_blocks(n1), nsb = rh_num_superblocks(n1), ns = (n1 + 63) / 64,
+                       ns2 = (n1 + 4095) / 4096;
+        if ((rc = trun_c.ensure(n1 * 32 + 64)) || (rc = trun_cnt.ensure(n1 + 16)) || (rc = trun_fl.ensure(n1 + 16)) ||
+            (rc = trun_br.ensure(n1 + 16)) || (rc = trun_bs.ensure(nbk * 32 + 32)) || (rc = trun_ss.ensure(nsb * 32 + 32)) ||
+            (rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64)) ||
+            (rc = trun_pre.ensure((n1 + 1) * 32 + 64)) || (rc = trun_cntp.ensure(n1 + 16)) ||
+            (rc = trun_smp.ensure(ns + ns2 + 8)))
+            return rc;
+        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
+        RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
+        RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
+        RH_HIP(rh::launch_prefix(trun_c.p, n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, trun_pre.p, stream));
+        RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
+        try {
+            auto fit = [](auto &v, size_t want) {  // headroom: the run grows batch by batch
+                if (v.capacity() < want) {
+                    v.clear();
+                    v.reserve(want + want / 2);
+                }
+                v.resize(want);
+            };
+            fit(trh_keys, n1 * kl + 64);
+            fit(trh_pre, (n1 + 1) * 4 + 8);
+            fit(trh_cntp, n1 + 16);
+            fit(trh_fl, n1 + 16);
+            fit(trh_br, n1 + 16);
+            fit(trh_smp, ns + ns2 + 8);
+        } catch (const std::bad_alloc &) {
+            tier_version = ~0ull;
+            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+        }
+        RH_HIP(hipMemcpyAsync(trh_keys.data(), dkeys[cd].p, n1 * kl, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(trh_pre.data(), trun_pre.p, (n1 + 1) * 32, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(trh_cntp.data(), trun_cntp.p, (n1 + 1) * 4, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(trh_fl.data(), trun_fl.p, n1, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(trh_br.data(), trun_br.p, n1 * 4, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(trh_smp.data(), trun_smp.p, (ns + ns2) * 8, hipMemcpyDeviceToHost, stream));
+        if ((rc = sync())) {
+            tier_version = ~0ull;
+            return rc;
+        }
+        rh::HostTier::Run r;
+        r.n = n1;
+        r.keys = trh_keys.data();
+        r.prefix = trh_pre.data();
+        r.cntp = reinterpret_cast<const int32_t *>(trh_cntp.data());
+        r.flags = trh_fl.data();
+        r.brank = trh_br.data();
+        r.samp = trh_smp.data();
+        r.samp2 = trh_smp.data() + ns;
+        tier.set_run(r);
+        tier_version = version;
+        tier_runs++;
+        tier_refreshes++;  // a copy from the device, as a refresh is (rh_store_tier_stats)
+        return RH_OK;
+    }
     // How a batch of m rows reaches the tier (decided before the batch, under the lock):
     //   0: it does not (tier off or stale, or the batch is larger than the tree takes: the tier
     //      goes stale and a refresh follows the batch),
@@ -1155,7 +1247,7 @@ struct rh_store {
     //   2: from the batch's sorted fingerprints and ops, the deltas formed against the tier's own
     //      base on the host (the device compacted since the tier's copy was taken).
     int fold_mode(size_t m) const {
-        if (!tier_fresh() || m > tree_limit()) return 0;
+        if (!tier_fresh() || m > tree_limit() || tier.has_run()) return 0;  // a run copy takes no folds
         return tier_epoch == base_epoch ? 1 : 2;
     }
     // whether the batch's rows must come down at all (a fold, or a refresh in flight to log for)
@@ -1763,6 +1855,7 @@ struct rh_store {
             if ((rc = apply_small(c, ops, m, last_wins, out, &done))) return rc;
             if (done) return RH_OK;
         }
+        snap_ok = run_copy_allowed(m);
         int fmode = fold_mode(m);  // how this batch reaches a fresh host tier
         bool want = fold_rows_wanted(fmode);
         if (want && !fold_room(m)) fmode = 0, want = false, rf_log_ok = false;  // the tier goes stale
@@ -2602,7 +2695,7 @@ int rh_store_tier_stats(rh_store *s, uint64_t *base_rows, uint64_t *delta_entrie
     if (rc) return rc;
     const bool fresh = s->tier_fresh();
     if (base_rows) *base_rows = fresh ? s->tier.nb : 0;
-    if (delta_entries) *delta_entries = fresh ? s->tier.dt.size() : 0;
+    if (delta_entries) *delta_entries = fresh ? s->tier.dt.size() + s->tier.run.n : 0;
     if (refreshes) *refreshes = s->tier_refreshes;
     if (folds) *folds = s->tier_folds;
     return RH_OK;

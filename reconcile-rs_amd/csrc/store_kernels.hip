@@ -1714,6 +1714,33 @@ hipError_t launch_delta_merge(int kk, int kl, const uint8_t *dkeys, const uint32
                                nbk, osmp, osmp2, st, heap, (uint32_t)heap_base, nullptr);
 }
 
+// The host tier's run copy (host_tier.hpp HostTier::Run): delta row i's DeltaRec, read through its
+// slot, as columns -- the contribution (32 B), the count delta live - in_base (cnt[n] = 0 closes
+// the array for the exclusive scan that follows), the flags and the base rank
+__global__ void k_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n, uint8_t *contrib, uint32_t *cnt,
+                           uint8_t *flags, uint32_t *brank) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {
+        cnt[n] = 0;
+        return;
+    }
+    const DeltaRec *r = reinterpret_cast<const DeltaRec *>(heap) + slot[i];
+    const uint4 *c = reinterpret_cast<const uint4 *>(r->contrib);
+    reinterpret_cast<uint4 *>(contrib + 32 * i)[0] = c[0];
+    reinterpret_cast<uint4 *>(contrib + 32 * i)[1] = c[1];
+    const uint32_t f = r->flags;
+    cnt[i] = (uint32_t)(((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0));
+    flags[i] = (uint8_t)f;
+    brank[i] = r->brank;
+}
+
+hipError_t launch_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n, uint8_t *contrib, uint32_t *cnt,
+                           uint8_t *flags, uint32_t *brank, hipStream_t st) {
+    hipLaunchKernelGGL(k_tier_run, g1(n + 1), dim3(256), 0, st, slot, heap, n, contrib, cnt, flags, brank);
+    return hipGetLastError();
+}
+
 hipError_t launch_compact_rows(const uint8_t *src, uint32_t row_bytes, const uint32_t *keep, const uint32_t *dst,
                                uint64_t m, uint8_t *out, hipStream_t st) {
     if (m == 0 || row_bytes == 0 || !src) return hipSuccess;

@@ -231,6 +231,9 @@ hipError_t launch_delta_merge(int kk, int kl, const uint8_t *dkeys, const uint32
 hipError_t launch_compact_rows(const uint8_t *src, uint32_t row_bytes, const uint32_t *keep, const uint32_t *dst,
                                uint64_t m, uint8_t *out, hipStream_t st);
 hipError_t launch_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, Scratch &s, hipStream_t st);
+// the delta run's DeltaRecs as the host tier's run-copy columns (k_tier_run); cnt has n + 1 entries
+hipError_t launch_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n, uint8_t *contrib, uint32_t *cnt,
+                           uint8_t *flags, uint32_t *brank, hipStream_t st);
 // pre-size the scratch slots a compaction of up to `plan` delta rows and a batch of `batch` rows use
 hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch);
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);

@@ -197,8 +197,9 @@ class GpuFingerprintStore:
         A.check(A.lib().rh_store_stage(self._h, C.byref(c), _np_ptr(ops_a), len(ops_a)), "rh_store_stage")
 
     def tier_stats(self) -> Dict[str, int]:
-        """The host tier's bookkeeping (rh_store_tier_stats): rows of its base copy and entries of
-        its delta tree while fresh, full refreshes (base copies) and batch folds so far."""
+        """The host tier's bookkeeping (rh_store_tier_stats): rows of its base copy and its delta
+        entries (tree + run copy) while fresh, copies taken from the device (base refreshes and run
+        copies) and batch folds so far."""
         b, d, r, f = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
         A.check(A.lib().rh_store_tier_stats(self._h, C.byref(b), C.byref(d), C.byref(r), C.byref(f)),
                 "rh_store_tier_stats")

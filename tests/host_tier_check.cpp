@@ -102,6 +102,71 @@ int main(int argc, char **argv) {
     flatten(base);
     HostTier A;
     A.build(kl, kk, model.size(), base.keys.data(), base.prefix.data());
+    // A run copy (HostTier::Run): every key whose state differs from A's base copy, with the
+    // device's DeltaRec rule (contrib = cur - base, count delta = live - in_base) and prefix sums
+    struct RunArrays {
+        std::vector<uint8_t> keys, flags;
+        std::vector<uint64_t> prefix, samp, samp2;
+        std::vector<int32_t> cntp;
+        std::vector<uint32_t> brank;
+    } run;
+    auto take_run = [&]() {
+        run = RunArrays{};
+        const uint64_t nbase = A.nb;
+        auto base_key = [&](uint64_t i) { return std::string((const char *)base.keys.data() + i * kl, kl); };
+        auto base_fp = [&](uint64_t i, uint64_t out[4]) {
+            memcpy(out, &base.prefix[4 * (i + 1)], 32);
+            rh::fp4_sub(out, &base.prefix[4 * i]);
+        };
+        uint64_t acc[4] = {0, 0, 0, 0};
+        int32_t cacc = 0;
+        run.prefix.assign(4, 0);
+        run.cntp.push_back(0);
+        auto emit = [&](const std::string &k, uint64_t br, bool inb, bool live, const uint64_t *cur, const uint64_t *bfp) {
+            uint64_t c[4] = {0, 0, 0, 0};
+            if (live) memcpy(c, cur, 32);
+            if (inb) rh::fp4_sub(c, bfp);
+            run.keys.insert(run.keys.end(), k.begin(), k.end());
+            run.flags.push_back((uint8_t)((inb ? 1 : 0) | (live ? 2 : 0)));
+            run.brank.push_back((uint32_t)br);
+            rh::fp4_add(acc, c);
+            run.prefix.insert(run.prefix.end(), acc, acc + 4);
+            cacc += (live ? 1 : 0) - (inb ? 1 : 0);
+            run.cntp.push_back(cacc);
+        };
+        uint64_t i = 0;
+        auto it = model.begin();
+        while (i < nbase || it != model.end()) {
+            const int c = i >= nbase ? 1 : it == model.end() ? -1 : ko.cmp(base.keys.data() + i * kl, (const uint8_t *)it->first.data());
+            uint64_t bfp[4];
+            if (c < 0) {  // a base key the model no longer holds: deleted
+                base_fp(i, bfp);
+                emit(base_key(i), i, true, false, nullptr, bfp);
+                i++;
+            } else if (c > 0) {  // inserted
+                emit(it->first, i, false, true, it->second.w, nullptr);
+                ++it;
+            } else {  // in both: an entry only if the fingerprint changed
+                base_fp(i, bfp);
+                if (memcmp(bfp, it->second.w, 32)) emit(it->first, i, true, true, it->second.w, bfp);
+                i++, ++it;
+            }
+        }
+        const uint64_t nr = run.flags.size();
+        for (uint64_t j = 0; j < nr; j += 64) run.samp.push_back(ko.digit(run.keys.data() + j * kl));
+        for (uint64_t j = 0; j < nr; j += 4096) run.samp2.push_back(ko.digit(run.keys.data() + j * kl));
+        run.keys.resize(run.keys.size() + 64);
+        HostTier::Run r;
+        r.n = nr;
+        r.keys = run.keys.data();
+        r.prefix = run.prefix.data();
+        r.cntp = run.cntp.data();
+        r.flags = run.flags.data();
+        r.brank = run.brank.data();
+        r.samp = run.samp.data();
+        r.samp2 = run.samp2.data();
+        A.set_run(r);
+    };
 
     uint64_t checked = 0;
     for (uint64_t it = 0; it < batches; it++) {
@@ -117,6 +182,13 @@ int main(int argc, char **argv) {
         std::vector<DeltaTree::Rec> rows(bk.size());
         std::vector<uint8_t> drop(bk.size());
         std::vector<Fp> fps(bk.size());
+        // every 4th batch is "too large for the tree": A takes a run copy of the whole change since
+        // its base copy instead of folding; the batch after it refreshes A's base (as the store does)
+        const bool snap = it % 4 == 2, after_snap = A.has_run();
+        if (after_snap) {
+            flatten(base);
+            A.build(kl, kk, model.size(), base.keys.data(), base.prefix.data());
+        }
         for (size_t j = 0; j < bk.size(); j++) {
             const bool del = rng() % 10 < 3;
             fps[j] = rand_fp();
@@ -124,7 +196,8 @@ int main(int argc, char **argv) {
             if (del) model.erase(bk[j]);
             else model[bk[j]] = fps[j];
         }
-        A.fold(rows.data(), drop.data(), rows.size());
+        if (snap) take_run();
+        else A.fold(rows.data(), drop.data(), rows.size());
 
         flatten(cur);
         HostTier B;
@@ -210,7 +283,8 @@ int main(int argc, char **argv) {
         }
         if (failures) break;
     }
-    printf("{\"ok\": %s, \"checked\": %llu, \"delta_entries\": %llu, \"size\": %llu}\n", failures ? "false" : "true",
-           (unsigned long long)checked, (unsigned long long)A.dt.size(), (unsigned long long)A.n);
+    printf("{\"ok\": %s, \"checked\": %llu, \"delta_entries\": %llu, \"run_entries\": %llu, \"size\": %llu}\n",
+           failures ? "false" : "true", (unsigned long long)checked, (unsigned long long)A.dt.size(),
+           (unsigned long long)A.run.n, (unsigned long long)A.n);
     return failures ? 1 : 0;
 }

@@ -1359,3 +1359,97 @@ def test_full_size_config5_100m(gpu, oracle_lib, n):
     want = O.Records(sc, h["keys"], h["values"], h["phys"], h["logical"], h["node"], None).lift()
     assert np.array_equal(ef[pick], want)
     st.close()
+
+
+@pytest.mark.gpu
+def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
+    """Batches too large for the tier's tree (RSOS_HIP_TIER_TREE=2000 here, read at store creation)
+    take a copy of the device's delta run instead of a refresh of the whole base
+    (rsos_hip_abi.hip tier_run_snapshot, host_tier.hpp HostTier::Run): inserts, overwrites and
+    deletes of base keys, deletes of keys a previous batch inserted, re-inserts.  After each, the
+    tier -- base copy + run copy -- answers ranks of present and absent keys, select at every kind
+    of rank, key-bound aggregates of every bound kind, rank-range aggregates and whole protocol
+    rounds exactly as the device does; a small batch after a run copy, and a large one after a
+    compaction, refresh the base instead."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    from rsos_hip.synth import make_records, to_host
+    monkeypatch.setenv("RSOS_HIP_TIER_TREE", "2000")
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 200_000
+    base = make_records(s, n, seed=31)
+    dev, tier = GpuFingerprintStore(s, host_tier=False), GpuFingerprintStore(s, host_tier=True)
+    for st in (dev, tier):
+        st.load_bulk_device(base)
+    rng = np.random.default_rng(9)
+    keys_h = to_host(base)["keys"]
+    seen = [keys_h]
+
+    def probe():
+        assert tier.size() == dev.size() and tier.aggregate() == dev.aggregate()
+        pool = np.concatenate(seen)
+        ks = [pool[i].tobytes() for i in rng.integers(0, len(pool), 300)] + [rng.bytes(16) for _ in range(100)]
+        ks += [b"\x00" * 16, b"\xff" * 16]
+        karr = np.frombuffer(b"".join(ks), np.uint8).reshape(-1, 16)
+        assert np.array_equal(tier.ranks(karr), dev.ranks(karr))
+        size = tier.size()
+        for r in [0, 1, size - 1] + list(rng.integers(0, size, 200)):
+            assert tier.select(int(r)) == dev.select(int(r))
+        for _ in range(150):
+            a, b = ks[rng.integers(len(ks))], ks[rng.integers(len(ks))]
+            sk, ek = ["included", "excluded"][rng.integers(2)], ["included", "excluded"][rng.integers(2)]
+            rg = KeyRange(a if rng.random() > 0.1 else None, b if rng.random() > 0.1 else None, sk, ek)
+            assert tier.aggregate(rg) == dev.aggregate(rg)
+        lo = rng.integers(0, size, 64)
+        hi = lo + rng.integers(0, 30_000, 64)
+        assert tier.aggregates_ranks(list(lo), list(hi)) == dev.aggregates_ranks(list(lo), list(hi))
+        lo0 = int(rng.integers(0, size - 3000))
+        a0, b0 = tier.select(lo0), tier.select(lo0 + 3000)
+        assert list(tier.enumerate(KeyRange(a0, b0))) == list(dev.enumerate(KeyRange(a0, b0)))  # rh_store_keys
+
+    def both(b, ops=None):
+        assert tier.apply_device(b, ops) == dev.apply_device(b, ops)
+
+    def large(seed, over=0):
+        b = make_records(s, 6_000, seed=seed, random_keys=True)
+        ops = torch.zeros(6_000, dtype=torch.uint8, device="cuda")
+        if over:  # overwrite and delete resident keys, delete keys an earlier batch inserted
+            rows = torch.from_numpy(rng.choice(n, 2 * over, replace=False)).cuda()
+            b["keys"][:2 * over] = base["keys"][rows]
+            b["phys"][:2 * over] = base["phys"][rows] + 7
+            ops[over:2 * over] = 1
+            prev = torch.from_numpy(seen[-1][:over].copy()).cuda()
+            b["keys"][2 * over:3 * over] = prev
+            ops[2 * over:3 * over] = 1
+        seen.append(to_host(b)["keys"])
+        return b, ops
+
+    probe()
+    r0 = tier.tier_stats()["refreshes"]
+    b, o = large(600)
+    both(b, o)
+    st = tier.tier_stats()
+    assert st["refreshes"] == r0 + 1 and st["delta_entries"] == dev.stats()["delta_rows"] and st["base_rows"] == n
+    probe()
+    b, o = large(601, over=800)  # a second run copy over the first's keys
+    both(b, o)
+    assert tier.tier_stats()["delta_entries"] == dev.stats()["delta_rows"]
+    probe()
+    small = make_records(s, 100, seed=602, random_keys=True)
+    both(small)  # after a run copy: the base is refreshed (the device compacts)
+    st = tier.tier_stats()
+    assert st["delta_entries"] == 0 and st["base_rows"] == tier.size()
+    probe()
+    b, o = large(603, over=500)
+    both(b, o)
+    assert tier.tier_stats()["delta_entries"] == dev.stats()["delta_rows"] > 0
+    probe()
+    for st_ in (dev, tier):
+        st_.compact()
+    b, o = large(604, over=300)  # after a compaction the run would not match the tier's base
+    both(b, o)
+    assert tier.tier_stats()["delta_entries"] == 0
+    probe()
+    dev.close()
+    tier.close()

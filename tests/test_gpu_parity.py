@@ -1384,7 +1384,7 @@ def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
         st.load_bulk_device(base)
     rng = np.random.default_rng(9)
     keys_h = to_host(base)["keys"]
-    seen = [keys_h]
+    seen, fresh = [keys_h], []
 
     def probe():
         assert tier.size() == dev.size() and tier.aggregate() == dev.aggregate()
@@ -1419,10 +1419,12 @@ def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
             b["keys"][:2 * over] = base["keys"][rows]
             b["phys"][:2 * over] = base["phys"][rows] + 7
             ops[over:2 * over] = 1
-            prev = torch.from_numpy(seen[-1][:over].copy()).cuda()
+            prev = torch.from_numpy(fresh[-1][:over].copy()).cuda()  # keys the last large batch inserted
             b["keys"][2 * over:3 * over] = prev
             ops[2 * over:3 * over] = 1
-        seen.append(to_host(b)["keys"])
+        kh = to_host(b)["keys"]
+        seen.append(kh)
+        fresh.append(kh[3 * over:])
         return b, ops
 
     probe()

@@ -1352,7 +1352,7 @@ struct rh_store {
             return rc;
         if (nb) {
             if (!have_samples) RH_HIP(kops->sample(bkeys[cb].p, nb, bsmp.p, bsmp2.p, stream));
-            if ((rc = btab.ensure((1ull << rh::search_table_bits(nb)) + 2)) || (rc = btabp.ensure(2))) return rc;
+            if ((rc = btab.ensure((1ull << rh::search_table_bits(nb)) + 2)) || (rc = btabp.ensure(3))) return rc;
             RH_HIP(rh::launch_search_table(bsmp2.p, nb, btab.p, btabp.p, stream));
             if (!have_block_sums) RH_HIP(rh::launch_reduce(bfps[cb].p, nb, bsums.p, stream));
             RH_HIP(rh::launch_reduce(bsums.p, nbk, ssums.p, stream));
@@ -1499,7 +1499,7 @@ struct rh_store {
             (rc = sssums.ensure(at_least(rh_num_superblocks(m) * 32 + 32, ssums.cap))) ||
             (rc = sbsmp.ensure(at_least(rh_num_blocks(m) + 1, bsmp.cap))) ||
             (rc = sbsmp2.ensure(at_least(rh::sample2_entries(m), bsmp2.cap))) ||
-            (rc = sbtab.ensure(at_least((1ull << rh::search_table_bits(m)) + 2, btab.cap))) || (rc = sbtabp.ensure(2)) ||
+            (rc = sbtab.ensure(at_least((1ull << rh::search_table_bits(m)) + 2, btab.cap))) || (rc = sbtabp.ensure(3)) ||
             (rc = stot.ensure(4)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
         return RH_OK;
@@ -1674,8 +1674,8 @@ struct rh_store {
         }
         if ((rc = bsums.ensure(rh_num_blocks(base) * 32 + 32)) || (rc = ssums.ensure(rh_num_superblocks(base) * 32 + 32)) ||
             (rc = bsmp.ensure(rh_num_blocks(base) + 1)) || (rc = bsmp2.ensure(rh::sample2_entries(base))) ||
-            (rc = btab.ensure((1ull << rh::search_table_bits(base)) + 2)) || (rc = btabp.ensure(2)) ||
-            (rc = dtab.ensure((1ull << rh::search_table_bits(plan, false)) + 2)) || (rc = dtabp.ensure(2)) ||
+            (rc = btab.ensure((1ull << rh::search_table_bits(base)) + 2)) || (rc = btabp.ensure(3)) ||
+            (rc = dtab.ensure((1ull << rh::search_table_bits(plan, false)) + 2)) || (rc = dtabp.ensure(3)) ||
             (rc = dsmp[0].ensure(rh_num_blocks(plan) + 1)) || (rc = dsmp[1].ensure(rh_num_blocks(plan) + 1)) ||
             (rc = dsmp2[0].ensure(rh::sample2_entries(plan))) || (rc = dsmp2[1].ensure(rh::sample2_entries(plan))) ||
             (rc = cfps.ensure(plan * 32 + 64)) ||
@@ -1913,7 +1913,7 @@ struct rh_store {
             // table is built here, where the run's row count is known on the host
             rh::SearchTable dt{};
             if (nd >= DTAB_MIN) {
-                if ((rc = dtab.ensure((1ull << rh::search_table_bits(nd, false)) + 2)) || (rc = dtabp.ensure(2))) return rc;
+                if ((rc = dtab.ensure((1ull << rh::search_table_bits(nd, false)) + 2)) || (rc = dtabp.ensure(3))) return rc;
                 if (full == 0) RH_HIP(rh::launch_search_table(dsmp2[cd].p, nd, dtab.p, dtabp.p, stream, false));
                 dt = rh::SearchTable{dtab.p, dtabp.p, rh::search_table_bits(nd, false)};
             }

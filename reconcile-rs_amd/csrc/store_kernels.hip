@@ -19,6 +19,7 @@
 // batch's DeltaRecs, merge them into the delta run (O(m + nD), one pass that also writes the
 // run's sums); when the delta run passes nB / 8 it is merged into the base the same way
 // (O(nB)) -- amortised, and on demand before rank / select.
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -563,8 +564,12 @@ __device__ __forceinline__ void table_params(const uint64_t *smp2, uint64_t ns2,
 }
 
 // built from the samples in one pass: sample s opens buckets (h(s - 1), h(s)] (h(-1) = -1), and
-// the last sample closes the rest; bucket h's value is the first sample at or above it
-__global__ void k_search_table(const uint64_t *smp2, uint64_t ns2, uint32_t bits, uint32_t *tab, uint64_t *par) {
+// the last sample closes the rest; bucket h's value is the first sample at or above it.  A gap of
+// more than 256 buckets (keys bunched in a corner of their digit range: one thread would write
+// millions of entries -- 10 ms for a 2^24-entry table) is left to k_search_table_gaps, told by
+// par[2] = gen (this build's number)
+__global__ void k_search_table(const uint64_t *smp2, uint64_t ns2, uint32_t bits, uint32_t *tab, uint64_t *par,
+                               uint64_t gen) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = 1ull << bits;
     if (s > ns2) return;
     uint64_t dmin;
@@ -580,7 +585,30 @@ __global__ void k_search_table(const uint64_t *smp2, uint64_t ns2, uint32_t bits
         return v < nt ? v : nt - 1;
     };
     const uint64_t lo = s == 0 ? 0 : h(s - 1) + 1, hi = s == ns2 ? nt : h(s);
+    if (hi >= lo && hi - lo >= 256) {
+        par[2] = gen;
+        return;
+    }
     for (uint64_t b = lo; b <= hi && b <= nt; b++) tab[b] = (uint32_t)s;
+}
+
+// after a build with a long gap: every bucket's value by a binary search of the samples (the
+// buckets of one gap all follow the same path, so it stays in cache); otherwise nothing
+__global__ void k_search_table_gaps(const uint64_t *smp2, uint64_t ns2, uint32_t bits, uint32_t *tab,
+                                    const uint64_t *par, uint64_t gen) {
+    if (par[2] != gen) return;
+    const uint64_t nt = 1ull << bits, dmin = par[0];
+    const uint32_t sh = (uint32_t)par[1];
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= nt; b += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = ns2;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            const uint64_t v = (smp2[mid] - dmin) >> sh;
+            if ((v < nt ? v : nt - 1) >= b) hi = mid;
+            else lo = mid + 1;
+        }
+        tab[b] = (uint32_t)lo;
+    }
 }
 
 template <int KK, int KL>
@@ -1811,7 +1839,12 @@ hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, 
     const uint64_t ns2 = (n + SMP2_STRIDE - 1) / SMP2_STRIDE;
     if (ns2 == 0) return hipSuccess;
     const uint32_t bits = search_table_bits(n, base);
-    hipLaunchKernelGGL(k_search_table, g1(ns2 + 1), dim3(256), 0, st, smp2, ns2, bits, tab, par);
+    static std::atomic<uint64_t> builds{0};
+    const uint64_t gen = ++builds;
+    hipLaunchKernelGGL(k_search_table, g1(ns2 + 1), dim3(256), 0, st, smp2, ns2, bits, tab, par, gen);
+    const uint64_t nt = 1ull << bits;
+    hipLaunchKernelGGL(k_search_table_gaps, dim3((uint32_t)std::min<uint64_t>((nt + 1 + 255) / 256, 2048)), dim3(256), 0,
+                       st, smp2, ns2, bits, tab, (const uint64_t *)par, gen);
     return hipGetLastError();
 }
 

@@ -1456,3 +1456,41 @@ def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
     probe()
     dev.close()
     tier.close()
+
+
+@pytest.mark.gpu
+def test_search_table_with_bunched_keys(gpu):
+    """Keys bunched in one corner of their digit range (the leading 8 bytes below 2^40), then a
+    batch of uniformly random keys: the search tables' buckets are almost all one long gap
+    (k_search_table leaves it to k_search_table_gaps).  Ranks of present and absent keys, selects
+    and the key dump equal numpy's sort of the same set, before and after a compaction."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.synth import make_records
+    s = RecordSchema.plain("bytes16", "u64")
+    n = 300_000
+    rng = np.random.default_rng(17)
+    hi8 = np.sort(rng.choice(1 << 40, n, replace=False)).astype(">u8")
+    keys = np.zeros((n, 16), np.uint8)
+    keys[:, :8] = hi8.view(np.uint8).reshape(n, 8)
+    keys[:, 8:] = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+    base = {"keys": torch.from_numpy(keys).cuda(), "values": torch.from_numpy(rng.integers(0, 256, (n, 8), dtype=np.uint8)).cuda()}
+    st = GpuFingerprintStore(s, host_tier=False)
+    st.load_bulk_device(base)
+    b = make_records(s, 50_000, seed=5, random_keys=True)
+    st.apply_device(b)
+    allk = np.concatenate([keys, b["keys"].cpu().numpy()])
+    srt = allk[np.lexsort(allk.T[::-1])]
+    view = srt.view("S16").ravel()
+
+    def check():
+        probes = np.concatenate([allk[rng.integers(0, len(allk), 2000)], rng.integers(0, 256, (2000, 16), dtype=np.uint8)])
+        want = np.searchsorted(view, probes.view("S16").ravel(), side="left")
+        assert np.array_equal(st.ranks(probes).astype(np.int64), want)
+        for r in rng.integers(0, len(srt), 100):
+            assert st.select(int(r)) == srt[r].tobytes()
+
+    check()
+    st.compact()
+    check()
+    st.close()

@@ -69,6 +69,7 @@ static uint64_t splitmix64(uint64_t i) {
 }
 
 static size_t KL, VL;
+static uint64_t STRIDE = 1;
 static int DATED;
 
 /* a round's segments, owned by the driver (copied out of the store's buffers) */
@@ -162,8 +163,9 @@ static void make_row(uint64_t i, int fresh, uint8_t *key, uint8_t *val, uint64_t
     if (KL == 8) {
         const uint64_t k = fresh ? splitmix64(i ^ 0x5bd1e995ull) : i;
         memcpy(key, &k, 8);
-    } else {  /* big-endian (i << 20 | r) then 8 bytes of noise: sorted by i, memcmp order */
-        const uint64_t h = fresh ? splitmix64(i ^ 0x5bd1e995ull) : (i << 20) | (splitmix64(i) >> 44);
+    } else {  /* big-endian (i * stride + r), r < stride = 2^64 / n, then 8 bytes of noise: sorted by i,
+                 spread over the whole key space as config5's keys are (rsos_hip/synth.py) */
+        const uint64_t h = fresh ? splitmix64(i ^ 0x5bd1e995ull) : i * STRIDE + splitmix64(i) % STRIDE;
         for (int b = 0; b < 8; b++) key[b] = (uint8_t)(h >> (56 - 8 * b));
         const uint64_t l = splitmix64(i + 77);
         memcpy(key + 8, &l, 8);
@@ -216,6 +218,7 @@ int main(int argc, char **argv) {
     const int reps = atoi(argv[3]), tier = atoi(argv[4]), warm = argc > 6 ? atoi(argv[6]) : 2;
     const int c5 = strcmp(argv[5], "c5") == 0;
     KL = c5 ? 16 : 8;
+    STRIDE = n > 1 ? UINT64_MAX / n : 1;
     VL = c5 ? 64 : 8;
     DATED = c5;
     const rh_schema sc = c5 ? (rh_schema){RH_KEY_BYTES, 16, RH_VAL_BYTES, 64, RH_REC_DATED, 0}

@@ -16,7 +16,7 @@ run() {  # name, timeout, cmd...
   echo "== $name rc=$rc"; tail -2 "$O/$name.log" | cut -c1-900
   [ $rc -eq 0 ] || exit $rc
 }
-run pytest_tier 600 python -u -m pytest tests/test_gpu_parity.py -k "host_tier or run_copy or variants or write_round or staged or keys_checked" tests/test_small_batch.py tests/test_tier_interleave.py tests/test_insert_latency.py tests/test_rbsr_latency.py -m gpu -v --timeout 300 --timeout-method thread
+run pytest_tier 600 python -u -m pytest tests/test_gpu_parity.py -k "host_tier or run_copy or variants or write_round or staged or keys_checked or bunched" tests/test_small_batch.py tests/test_tier_interleave.py tests/test_insert_latency.py tests/test_rbsr_latency.py -m gpu -v --timeout 300 --timeout-method thread
 run interleave_default 400 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 20 1 c5 2
 run interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 20 1 c5 2
 run interleave_tier0 400 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 20 0 c5 2

@@ -1,8 +1,7 @@
 #!/bin/bash
 # Round 4, third GPU session: config5 after the two-level sort positions -- bench lines (20 and 40
 # batches) with the roofline, a kernel-stats trace and the three PMC passes of scripts/pmc_c5.sh,
-# summarised into r04_pmc_config5.json; then the default line, the tier interleave under both
-# refresh policies, the 1-row write -> round cycle at 10^8 and smoke.  Stops at the first failing step.
+# summarised into r04_pmc_config5.json; then the default line and smoke.  Stops at the first failing step.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -25,8 +24,5 @@ cp "$S" $O/config5_kernel_stats.csv
 run pmc_summary 60 python3 scripts/pmc_c5_summary.py gpurun_out $O/config5_kernel_stats.csv $O/r04_pmc_config5.json
 rm -rf $O/c5stats
 run default 300 python3 bench.py
-run interleave_sync 400 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 20 1 c5 2
-run interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 20 1 c5 2
-run latency 300 reconcile-rs_amd/examples/rbsr_latency 100000000 1 200 1 1
 run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 echo "== done"

@@ -63,6 +63,8 @@ struct HostTier {
         const uint8_t *flags = nullptr;     // n: DeltaRec flags (1 in the base, 2 live)
         const uint32_t *brank = nullptr;    // n: base rows below the key
         const uint64_t *samp = nullptr, *samp2 = nullptr;  // digits of every 64th / 4096th key
+        // G(64 k) = live keys <= entry 64 k (brank + cntp + live), k < ns: select's index (nullable)
+        const uint64_t *gsamp = nullptr;
         uint64_t ns = 0, ns2 = 0;
     };
     Run run;
@@ -282,6 +284,11 @@ struct HostTier {
     uint64_t run_below(uint64_t j) const { return (uint64_t)((int64_t)run.brank[j] + run.cntp[j]); }
     Cur at_run(uint64_t r) const {
         uint64_t lo = 0, hi = run.n;
+        if (run.gsamp) {  // the first sampled entry with G > r bounds a window of 64 entries
+            const uint64_t k = std::upper_bound(run.gsamp, run.gsamp + run.ns, r) - run.gsamp;
+            lo = k ? ((k - 1) << SHIFT) + 1 : 0;  // G(64 (k - 1)) <= r
+            hi = std::min<uint64_t>(run.n, k << SHIFT);  // G(64 k) > r (or the end)
+        }
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
             if (run_below(mid) + (run_live(mid) ? 1 : 0) > r) hi = mid;

@@ -1164,9 +1164,9 @@ struct rh_store {
     // (or a compaction, or a run copy past a quarter of the base) refreshes the base instead.
     DevBuf<uint8_t> trun_c, trun_fl, trun_bs, trun_ss, trun_spre, trun_bpre, trun_pre;
     DevBuf<uint32_t> trun_cnt, trun_cntp, trun_br;
-    DevBuf<uint64_t> trun_smp;
+    DevBuf<uint64_t> trun_smp, trun_gs;
     PinnedVec<uint8_t> trh_keys, trh_fl;
-    PinnedVec<uint64_t> trh_pre, trh_smp;
+    PinnedVec<uint64_t> trh_pre, trh_smp, trh_gs;
     PinnedVec<uint32_t> trh_cntp, trh_br;
     uint64_t tier_runs = 0;
     bool snap_ok = false;  // set before a batch: a run copy may replace the refresh it causes
@@ -1187,7 +1187,7 @@ struct rh_store {
             (rc = trun_br.ensure(n1 + 16)) || (rc = trun_bs.ensure(nbk * 32 + 32)) || (rc = trun_ss.ensure(nsb * 32 + 32)) ||
             (rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64)) ||
             (rc = trun_pre.ensure((n1 + 1) * 32 + 64)) || (rc = trun_cntp.ensure(n1 + 16)) ||
-            (rc = trun_smp.ensure(ns + ns2 + 8)))
+            (rc = trun_smp.ensure(ns + ns2 + 8)) || (rc = trun_gs.ensure(ns + 8)))
             return rc;
         RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
         RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
@@ -1197,6 +1197,7 @@ struct rh_store {
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
+        RH_HIP(rh::launch_tier_gsamp(trun_br.p, trun_cntp.p, trun_fl.p, n1, trun_gs.p, stream));
         try {
             auto fit = [](auto &v, size_t want) {  // headroom: the run grows batch by batch
                 if (v.capacity() < want) {
@@ -1211,6 +1212,7 @@ struct rh_store {
             fit(trh_fl, n1 + 16);
             fit(trh_br, n1 + 16);
             fit(trh_smp, ns + ns2 + 8);
+            fit(trh_gs, ns + 8);
         } catch (const std::bad_alloc &) {
             tier_version = ~0ull;
             return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
@@ -1221,6 +1223,7 @@ struct rh_store {
         RH_HIP(hipMemcpyAsync(trh_fl.data(), trun_fl.p, n1, hipMemcpyDeviceToHost, stream));
         RH_HIP(hipMemcpyAsync(trh_br.data(), trun_br.p, n1 * 4, hipMemcpyDeviceToHost, stream));
         RH_HIP(hipMemcpyAsync(trh_smp.data(), trun_smp.p, (ns + ns2) * 8, hipMemcpyDeviceToHost, stream));
+        RH_HIP(hipMemcpyAsync(trh_gs.data(), trun_gs.p, ns * 8, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) {
             tier_version = ~0ull;
             return rc;
@@ -1234,6 +1237,7 @@ struct rh_store {
         r.brank = trh_br.data();
         r.samp = trh_smp.data();
         r.samp2 = trh_smp.data() + ns;
+        r.gsamp = trh_gs.data();
         tier.set_run(r);
         tier_version = version;
         tier_runs++;

@@ -1769,6 +1769,21 @@ hipError_t launch_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n
     return hipGetLastError();
 }
 
+// select's index over the run copy: G(64 k) = live keys <= entry 64 k = brank + count prefix + live
+__global__ void k_tier_gsamp(const uint32_t *brank, const uint32_t *cntp, const uint8_t *flags, uint64_t n,
+                             uint64_t *gsamp) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, j = k * 64;
+    if (j >= n) return;
+    gsamp[k] = (uint64_t)((int64_t)brank[j] + (int32_t)cntp[j] + ((flags[j] & DeltaRec::LIVE) ? 1 : 0));
+}
+
+hipError_t launch_tier_gsamp(const uint32_t *brank, const uint32_t *cntp, const uint8_t *flags, uint64_t n,
+                             uint64_t *gsamp, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tier_gsamp, g1((n + 63) / 64), dim3(256), 0, st, brank, cntp, flags, n, gsamp);
+    return hipGetLastError();
+}
+
 hipError_t launch_compact_rows(const uint8_t *src, uint32_t row_bytes, const uint32_t *keep, const uint32_t *dst,
                                uint64_t m, uint8_t *out, hipStream_t st) {
     if (m == 0 || row_bytes == 0 || !src) return hipSuccess;

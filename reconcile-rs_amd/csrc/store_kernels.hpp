@@ -234,6 +234,9 @@ hipError_t launch_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t
 // the delta run's DeltaRecs as the host tier's run-copy columns (k_tier_run); cnt has n + 1 entries
 hipError_t launch_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n, uint8_t *contrib, uint32_t *cnt,
                            uint8_t *flags, uint32_t *brank, hipStream_t st);
+// and select's index over it: entry 64 k's live keys at or below it (k_tier_gsamp)
+hipError_t launch_tier_gsamp(const uint32_t *brank, const uint32_t *cntp, const uint8_t *flags, uint64_t n,
+                             uint64_t *gsamp, hipStream_t st);
 // pre-size the scratch slots a compaction of up to `plan` delta rows and a batch of `batch` rows use
 hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch);
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);

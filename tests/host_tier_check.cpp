@@ -106,11 +106,11 @@ int main(int argc, char **argv) {
     // device's DeltaRec rule (contrib = cur - base, count delta = live - in_base) and prefix sums
     struct RunArrays {
         std::vector<uint8_t> keys, flags;
-        std::vector<uint64_t> prefix, samp, samp2;
+        std::vector<uint64_t> prefix, samp, samp2, gsamp;
         std::vector<int32_t> cntp;
         std::vector<uint32_t> brank;
     } run;
-    auto take_run = [&]() {
+    auto take_run = [&](bool with_index) {
         run = RunArrays{};
         const uint64_t nbase = A.nb;
         auto base_key = [&](uint64_t i) { return std::string((const char *)base.keys.data() + i * kl, kl); };
@@ -155,6 +155,8 @@ int main(int argc, char **argv) {
         const uint64_t nr = run.flags.size();
         for (uint64_t j = 0; j < nr; j += 64) run.samp.push_back(ko.digit(run.keys.data() + j * kl));
         for (uint64_t j = 0; j < nr; j += 4096) run.samp2.push_back(ko.digit(run.keys.data() + j * kl));
+        for (uint64_t j = 0; j < nr; j += 64)  // select's index, as the device forms it
+            run.gsamp.push_back((uint64_t)((int64_t)run.brank[j] + run.cntp[j] + ((run.flags[j] & 2) ? 1 : 0)));
         run.keys.resize(run.keys.size() + 64);
         HostTier::Run r;
         r.n = nr;
@@ -165,6 +167,7 @@ int main(int argc, char **argv) {
         r.brank = run.brank.data();
         r.samp = run.samp.data();
         r.samp2 = run.samp2.data();
+        r.gsamp = with_index ? run.gsamp.data() : nullptr;  // with and without select's index
         A.set_run(r);
     };
 
@@ -196,7 +199,7 @@ int main(int argc, char **argv) {
             if (del) model.erase(bk[j]);
             else model[bk[j]] = fps[j];
         }
-        if (snap) take_run();
+        if (snap) take_run(it % 8 != 2);
         else A.fold(rows.data(), drop.data(), rows.size());
 
         flatten(cur);

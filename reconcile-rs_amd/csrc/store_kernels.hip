@@ -1858,7 +1858,8 @@ hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, 
     const uint64_t gen = ++builds;
     hipLaunchKernelGGL(k_search_table, g1(ns2 + 1), dim3(256), 0, st, smp2, ns2, bits, tab, par, gen);
     const uint64_t nt = 1ull << bits;
-    hipLaunchKernelGGL(k_search_table_gaps, dim3((uint32_t)std::min<uint64_t>((nt + 1 + 255) / 256, 2048)), dim3(256), 0,
+    // a small grid: without a long gap (the usual case) it only reads par[2] and exits (~1 us)
+    hipLaunchKernelGGL(k_search_table_gaps, dim3((uint32_t)std::min<uint64_t>((nt + 1 + 255) / 256, 128)), dim3(256), 0,
                        st, smp2, ns2, bits, tab, (const uint64_t *)par, gen);
     return hipGetLastError();
 }

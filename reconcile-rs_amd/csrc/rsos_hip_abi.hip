@@ -2756,6 +2756,9 @@ int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
             s->tier_version = ~0ull;
             if ((rc = flush_locked(s))) return rc;
             if (s->nb + s->nd > 0 && (rc = s->start_refresh())) return rc;
+            // with writes keeping the tier fresh, enabling it waits for its first copy too: no
+            // question after this call is answered by the device
+            if (s->tier_sync_writes && (rc = s->settle())) return rc;
         }
     }
     if (!s->tier_on) {  // give the host memory back

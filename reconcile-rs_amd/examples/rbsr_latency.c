@@ -172,7 +172,7 @@ int main(int argc, char **argv) {
         CHECK(rh_store_set_host_tier(b, 1, 0));
     }
     double t0 = now_s();
-    cost_t c = reconcile(a, b, &sc); /* the first one: the tiers' copies are still in flight */
+    cost_t c = reconcile(a, b, &sc); /* the first one (RSOS_HIP_TIER_SYNC=0: the tiers' copies may be in flight) */
     const double first = now_s() - t0;
     CHECK(rh_store_tier_sync(a)); /* then a warm store: the copies have landed */
     CHECK(rh_store_tier_sync(b));

@@ -17,13 +17,17 @@ EX = os.path.join(ROOT, "reconcile-rs_amd", "examples", "tier_interleave")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape,n,m", [("u64", 200_000, 80_000), ("c5", 200_000, 80_000), ("u64", 200_000, 2_000),
-                                       ("c5", 300_000, 500)])
-def test_interleaved_drives_equal_device_path(gpu, shape, n, m):
+@pytest.mark.parametrize("shape,n,m,policy", [("u64", 200_000, 80_000, "1"), ("c5", 200_000, 80_000, "1"),
+                                              ("u64", 200_000, 80_000, "0"), ("c5", 200_000, 80_000, "0"),
+                                              ("u64", 200_000, 2_000, "1"), ("c5", 300_000, 500, "1")])
+def test_interleaved_drives_equal_device_path(gpu, shape, n, m, policy):
+    """policy: RSOS_HIP_TIER_SYNC -- 1 (the default: writes keep the tier fresh; batches past the
+    tree take run copies) or 0 (writes never wait; the device answers while a copy is in flight)."""
     out = {}
+    env = dict(os.environ, RSOS_HIP_TIER_SYNC=policy)
     for tier in (0, 1):
         r = subprocess.run([EX, str(n), str(m), "5", str(tier), shape, "1"], capture_output=True, text=True,
-                           timeout=300)
+                           timeout=300, env=env)
         assert r.returncode == 0, r.stderr
         out[tier] = json.loads(r.stdout)
     keys = ("size", "rounds", "ranges", "idlists", "enumerated", "wire_bytes")

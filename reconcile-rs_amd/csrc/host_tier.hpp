@@ -52,9 +52,9 @@ struct HostTier {
     // tree: its entries in key order, each the DeltaRec the device keeps for the key (the
     // contribution cur - base and the count delta live - in_base relative to the base, its flags
     // and its base rank), with exclusive prefix sums of both, all formed on the device
-    // (rsos_hip_abi.hip tier_run_snapshot).  Base + run copy is the whole map, as the device's
-    // base + delta run is; the tree is empty while a run copy is held (the next small batch
-    // refreshes the base instead).
+    // (rsos_hip_abi.hip tier_run_snapshot).  Base + run copy (the *view*) is the whole map, as the
+    // device's base + delta run is; later small batches fold into the tree as deltas against the
+    // view (entry_vs_base), and the next run copy absorbs them.
     struct Run {
         uint64_t n = 0;
         const uint8_t *keys = nullptr;      // n * kl, key order
@@ -75,8 +75,9 @@ struct HostTier {
         run.ns = (r.n + 63) >> SHIFT;
         run.ns2 = (run.ns + 63) >> SHIFT;
         dt.clear();
-        n = (uint64_t)((int64_t)nb + (r.n ? r.cntp[r.n] : 0));
+        nv = n = (uint64_t)((int64_t)nb + (r.n ? r.cntp[r.n] : 0));
     }
+    uint64_t nv = 0;  // live keys of the view (base + run copy)
 
     uint64_t digit(const uint8_t *k) const { return ko.digit(k); }
     int cmp(const uint8_t *a, const uint8_t *b) const { return ko.cmp(a, b); }
@@ -86,7 +87,7 @@ struct HostTier {
                const uint64_t *smp = nullptr, const uint64_t *smp2 = nullptr) {
         ko = KeyOrder{key_len, key_kind};
         kl = key_len;
-        nb = n = rows;
+        nb = n = nv = rows;
         keys = k;
         prefix = p;
         dt.set_order(ko);
@@ -149,30 +150,47 @@ struct HostTier {
         segs = std::vector<Seg>();
     }
     bool plain() const { return dt.size() == 0; }
-    // One batch row's entry formed against this tier's own base: the rule of k_delta_build
-    // (store_kernels.hip) -- an upsert is (cur - base, 1 - in_base, live), a delete of a base key
-    // (-base, -1, dead), a delete of any other key drops the key's entry (returns true).
-    // cur == nullptr: a delete.
-    bool entry_vs_base(const uint8_t *key, const uint64_t *cur, DeltaTree::Rec *r) const {
+    // Whether the view holds key, and its fingerprint (the run's entry if it has one, else the base)
+    bool view_find(const uint8_t *key, uint64_t fp[4]) const {
+        if (has_run()) {
+            const uint64_t j = rank_run(key);
+            if (j < run.n && cmp(run.keys + j * kl, key) == 0) {
+                if (!run_live(j)) return false;
+                memcpy(fp, run.prefix + 4 * (j + 1), 32);  // contrib = cur - base
+                fp4_sub(fp, run.prefix + 4 * j);
+                if (run_in_base(j)) {
+                    fp4_add(fp, prefix + 4 * (run.brank[j] + 1));
+                    fp4_sub(fp, prefix + 4 * run.brank[j]);
+                }
+                return true;
+            }
+        }
         const uint64_t b = rank_b(key);
-        const bool in_b = b < nb && cmp(keys + b * kl, key) == 0;
+        if (b < nb && cmp(keys + b * kl, key) == 0) {
+            memcpy(fp, prefix + 4 * (b + 1), 32);
+            fp4_sub(fp, prefix + 4 * b);
+            return true;
+        }
+        return false;
+    }
+    // One batch row's entry formed against this tier's own view (its base, and its run copy when
+    // held): the rule of k_delta_build (store_kernels.hip) -- an upsert is (cur - view, 1 - in_view,
+    // live), a delete of a view key (-view, -1, dead), a delete of any other key drops the key's
+    // entry (returns true).  cur == nullptr: a delete.
+    bool entry_vs_base(const uint8_t *key, const uint64_t *cur, DeltaTree::Rec *r) const {
+        uint64_t v[4] = {0, 0, 0, 0};
+        const bool in_v = view_find(key, v);
         r->key = key;
         if (cur) memcpy(r->fp, cur, 32);
         else memset(r->fp, 0, 32);
-        if (in_b) {
-            uint64_t base[4];
-            memcpy(base, prefix + 4 * (b + 1), 32);
-            fp4_sub(base, prefix + 4 * b);
-            fp4_sub(r->fp, base);
-        }
-        r->cnt = (int8_t)((cur ? 1 : 0) - (in_b ? 1 : 0));
+        if (in_v) fp4_sub(r->fp, v);
+        r->cnt = (int8_t)((cur ? 1 : 0) - (in_v ? 1 : 0));
         r->live = cur != nullptr;
-        return !cur && !in_b;
+        return !cur && !in_v;
     }
     // m sorted, distinct rows into the delta tree; drop[j]: remove row j's key.  A batch large
     // against the tree is one merge pass over the whole tree instead of m walks.
     void fold(const DeltaTree::Rec *rows, const uint8_t *drop, size_t m) {
-        if (has_run()) return;  // the caller refreshes instead (fold_mode is 0 with a run copy)
         if (m > 256 && m * 16 > dt.size()) {
             dt.merge_rebuild(rows, drop, m);
         } else {
@@ -181,7 +199,7 @@ struct HostTier {
                 else dt.upsert(rows[j]);
             }
         }
-        n = (uint64_t)((int64_t)nb + dt.cnt_total());
+        n = (uint64_t)((int64_t)nv + dt.cnt_total());
     }
 
     // base rows with key < z
@@ -191,9 +209,76 @@ struct HostTier {
         return sampled_lb(run.keys, run.n, run.samp, run.ns, run.samp2, run.ns2, key);
     }
 
-    // A place in the merged key order: r live keys below it, b base rows below it, d delta entries
-    // below it; k = the live key at rank r (set by at(), r < n).
-    // With a run copy: j run entries below it (the tree is then empty, d = 0).
+    // ---- the view: the base copy, merged with the run copy when one is held ----------------------
+    // A place in it: b base rows and j run entries below; the live view keys below are then
+    // b + Σ count deltas of those run entries.
+    bool run_live(uint64_t j) const { return run.flags[j] & 2; }
+    bool run_in_base(uint64_t j) const { return run.flags[j] & 1; }
+    uint64_t run_below(uint64_t j) const { return (uint64_t)((int64_t)run.brank[j] + run.cntp[j]); }
+    uint64_t view_rank(uint64_t b, uint64_t j) const {
+        return has_run() ? (uint64_t)((int64_t)b + run.cntp[j]) : b;
+    }
+    // view keys < z (le: <= z)
+    void view_lt(const uint8_t *z, bool le, uint64_t &b, uint64_t &j) const {
+        b = rank_b(z);
+        if (le && b < nb && cmp(keys + b * kl, z) == 0) b++;
+        j = 0;
+        if (has_run()) {
+            j = rank_run(z);
+            if (le && j < run.n && cmp(run.keys + j * kl, z) == 0) j++;
+        }
+    }
+    // the view key of rank v < nv, with its place.  G(j) = live view keys <= run entry j = brank +
+    // cntp + live, non-decreasing; the first entry with G(j) > v is that key itself, or the key is
+    // an untouched base row between entries j - 1 and j (those rows are consecutive)
+    const uint8_t *view_at(uint64_t v, uint64_t &b, uint64_t &j) const {
+        if (!has_run()) {
+            b = v, j = 0;
+            return keys + v * kl;
+        }
+        uint64_t lo = 0, hi = run.n;
+        if (run.gsamp) {  // the first sampled entry with G > v bounds a window of 64 entries
+            const uint64_t k = std::upper_bound(run.gsamp, run.gsamp + run.ns, v) - run.gsamp;
+            lo = k ? ((k - 1) << SHIFT) + 1 : 0;         // G(64 (k - 1)) <= v
+            hi = std::min<uint64_t>(run.n, k << SHIFT);  // G(64 k) > v (or the end)
+        }
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (run_below(mid) + (run_live(mid) ? 1 : 0) > v) hi = mid;
+            else lo = mid + 1;
+        }
+        j = lo;
+        if (j < run.n && run_below(j) == v && run_live(j)) {
+            b = run.brank[j];
+            return run.keys + j * kl;
+        }
+        const uint64_t gprev = j ? run_below(j - 1) + (run_live(j - 1) ? 1 : 0) : 0;
+        const uint64_t b0 = j ? run.brank[j - 1] + (run_in_base(j - 1) ? 1 : 0) : 0;
+        b = b0 + (v - gprev);
+        return keys + b * kl;
+    }
+    // in-order walk of the view from a place: the next live key (nullptr at the end) and a step
+    // past it.  A run entry comes before base row b when b >= its base rank; one in the base
+    // replaces that row, a dead one is skipped.
+    const uint8_t *view_peek(uint64_t &b, uint64_t &j) const {
+        while (j < run.n && b >= run.brank[j] && !run_live(j)) {
+            if (run_in_base(j)) b++;
+            j++;
+        }
+        if (j < run.n && b >= run.brank[j]) return run.keys + j * kl;
+        return b < nb ? keys + b * kl : nullptr;
+    }
+    void view_step(uint64_t &b, uint64_t &j) const {
+        if (j < run.n && b >= run.brank[j]) {
+            if (run_in_base(j)) b++;
+            j++;
+        } else {
+            b++;
+        }
+    }
+
+    // A place in the merged key order (the view + the tree): r live keys below it; b, j its place
+    // in the view; d tree entries below it; k = the live key at rank r (set by at(), r < n).
     struct Cur {
         uint64_t r = 0, b = 0, d = 0;
         const uint8_t *k = nullptr;
@@ -201,113 +286,74 @@ struct HostTier {
     };
     Cur begin() const { return Cur{0, 0, 0, nullptr, 0}; }
     Cur end() const { return Cur{n, nb, dt.size(), nullptr, run.n}; }
-    // keys < z
-    Cur lt(const uint8_t *z) const {
+    // keys < z (le: keys <= z)
+    Cur place(const uint8_t *z, bool le) const {
         Cur c;
-        c.b = rank_b(z);
-        if (has_run()) {  // live keys below z = base rows below z + Σ count deltas of run entries below z
-            c.j = rank_run(z);
-            c.r = (uint64_t)((int64_t)c.b + run.cntp[c.j]);
-            return c;
-        }
-        if (plain()) {
-            c.r = c.b;
-            return c;
-        }
+        view_lt(z, le, c.b, c.j);
+        c.r = view_rank(c.b, c.j);
+        if (plain()) return c;
         const DeltaTree::Pos p = dt.lt(z);
-        c.d = p.idx;
-        c.r = (uint64_t)((int64_t)c.b + p.cnt);
+        c.d = p.idx + (le && p.found ? 1 : 0);
+        c.r = (uint64_t)((int64_t)c.r + p.cnt + (le && p.found ? p.fcnt : 0));
         return c;
     }
-    // keys <= z
-    Cur le(const uint8_t *z) const {
-        Cur c;
-        c.b = rank_b(z);
-        if (c.b < nb && cmp(keys + c.b * kl, z) == 0) c.b++;
-        if (has_run()) {
-            c.j = rank_run(z);
-            if (c.j < run.n && cmp(run.keys + c.j * kl, z) == 0) c.j++;
-            c.r = (uint64_t)((int64_t)c.b + run.cntp[c.j]);
-            return c;
-        }
-        if (plain()) {
-            c.r = c.b;
-            return c;
-        }
-        const DeltaTree::Pos p = dt.lt(z);
-        c.d = p.idx + (p.found ? 1 : 0);
-        c.r = (uint64_t)((int64_t)c.b + p.cnt + (p.found ? p.fcnt : 0));
-        return c;
-    }
+    Cur lt(const uint8_t *z) const { return place(z, false); }
+    Cur le(const uint8_t *z) const { return place(z, true); }
     // select: the place of the r-th live key (r <= n; r == n is end())
     Cur at(uint64_t r) const {
         if (r >= n) return end();
-        if (has_run()) return at_run(r);
-        if (plain()) return Cur{r, r, 0, keys + r * kl, 0};
-        // F(b) = live keys <= base key b, non-decreasing in b; find the smallest b with F(b) > r.
-        // |F(b) - b| <= delta entries + 1 brackets the search.
-        const uint64_t nd = dt.size();
-        uint64_t lo = r > nd ? r - nd : 0, hi = std::min<uint64_t>(nb, r + nd + 1);
-        auto F = [&](uint64_t b, DeltaTree::Pos *pp) {
-            const DeltaTree::Pos p = dt.lt(keys + b * kl);
+        Cur c;
+        if (plain()) {
+            c.k = view_at(r, c.b, c.j);
+            c.r = r;
+            return c;
+        }
+        // F(v) = live keys <= view key v, non-decreasing in v; find the smallest v with F(v) > r.
+        // |F(v) - v| <= tree entries + 1 brackets the search.
+        const uint64_t nt = dt.size();
+        uint64_t lo = r > nt ? r - nt : 0, hi = std::min<uint64_t>(nv, r + nt + 1);
+        auto F = [&](uint64_t v, DeltaTree::Pos *pp, Cur *vc) {
+            uint64_t b, j;
+            const uint8_t *k = view_at(v, b, j);
+            const DeltaTree::Pos p = dt.lt(k);
             if (pp) *pp = p;
-            return (uint64_t)((int64_t)b + 1 + p.cnt + (p.found ? p.fcnt : 0));
+            if (vc) vc->b = b, vc->j = j, vc->k = k;
+            return (uint64_t)((int64_t)v + 1 + p.cnt + (p.found ? p.fcnt : 0));
         };
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
-            if (F(mid, nullptr) > r) hi = mid;
+            if (F(mid, nullptr, nullptr) > r) hi = mid;
             else lo = mid + 1;
         }
-        const uint64_t b = lo;
-        if (b < nb) {
+        const uint64_t v = lo;
+        if (v < nv) {
             DeltaTree::Pos p;
-            const uint64_t f = F(b, &p);
+            const uint64_t f = F(v, &p, &c);
             const bool live = !p.found || p.flive;
-            if (live && f - 1 == r) return Cur{r, b, p.idx, keys + b * kl, 0};
+            if (live && f - 1 == r) {
+                c.r = r;
+                c.d = p.idx;
+                return c;
+            }
         }
-        // the r-th live key is an inserted delta key between base keys b - 1 and b: every delta
-        // entry in that gap is one (a key not in the base is in the delta run only while live)
+        // the r-th live key is an inserted tree key between view keys v - 1 and v: every tree
+        // entry in that gap is one (a key not in the view is in the tree only while live)
         uint64_t fprev = 0, d0 = 0;
-        if (b > 0) {
+        if (v > 0) {
             DeltaTree::Pos q;
-            fprev = F(b - 1, &q);
+            fprev = F(v - 1, &q, nullptr);
             d0 = q.idx + (q.found ? 1 : 0);
         }
         const uint64_t d = d0 + (r - fprev);
-        return Cur{r, b, d, dt.key_at(d), 0};
-    }
-    // select over base + run copy: G(j) = live keys <= run key j = brank + cntp + live, non-
-    // decreasing; the first entry with G(j) > r is the r-th live key itself, or the r-th live key
-    // is an untouched base row between entries j - 1 and j (those rows are consecutive)
-    bool run_live(uint64_t j) const { return run.flags[j] & 2; }
-    bool run_in_base(uint64_t j) const { return run.flags[j] & 1; }
-    uint64_t run_below(uint64_t j) const { return (uint64_t)((int64_t)run.brank[j] + run.cntp[j]); }
-    Cur at_run(uint64_t r) const {
-        uint64_t lo = 0, hi = run.n;
-        if (run.gsamp) {  // the first sampled entry with G > r bounds a window of 64 entries
-            const uint64_t k = std::upper_bound(run.gsamp, run.gsamp + run.ns, r) - run.gsamp;
-            lo = k ? ((k - 1) << SHIFT) + 1 : 0;  // G(64 (k - 1)) <= r
-            hi = std::min<uint64_t>(run.n, k << SHIFT);  // G(64 k) > r (or the end)
-        }
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (run_below(mid) + (run_live(mid) ? 1 : 0) > r) hi = mid;
-            else lo = mid + 1;
-        }
-        const uint64_t j = lo;
-        if (j < run.n && run_below(j) == r && run_live(j)) return Cur{r, run.brank[j], 0, run.keys + j * kl, j};
-        const uint64_t gprev = j ? run_below(j - 1) + (run_live(j - 1) ? 1 : 0) : 0;
-        const uint64_t b0 = j ? run.brank[j - 1] + (run_in_base(j - 1) ? 1 : 0) : 0;
-        const uint64_t b = b0 + (r - gprev);
-        return Cur{r, b, 0, keys + b * kl, j};
+        const uint8_t *k = dt.key_at(d);
+        view_lt(k, false, c.b, c.j);
+        c.r = r, c.d = d, c.k = k;
+        return c;
     }
     // Σ fingerprints of the live keys below c
     void pre(const Cur &c, uint64_t out[4]) const {
         memcpy(out, prefix + 4 * c.b, 32);
-        if (has_run()) {
-            fp4_add(out, run.prefix + 4 * c.j);
-            return;
-        }
+        if (has_run()) fp4_add(out, run.prefix + 4 * c.j);
         if (!plain() && c.d) {
             uint64_t t[4];
             dt.fp_prefix(c.d, t);
@@ -352,42 +398,26 @@ struct HostTier {
     // the keys of ranks [lo, hi) (hi <= n), in order
     void copy_keys(uint64_t lo, uint64_t hi, uint8_t *out) const {
         if (hi <= lo) return;
-        if (has_run()) {  // base rows and run entries merged: an entry replaces its base row
-            const Cur c = at(lo);
-            uint64_t b = c.b, j = c.j;
-            for (uint64_t r = lo; r < hi;) {
-                if (j < run.n && b >= run.brank[j]) {
-                    if (run_in_base(j)) b++;
-                    if (run_live(j)) {
-                        memcpy(out, run.keys + j * kl, kl);
-                        out += kl, r++;
-                    }
-                    j++;
-                } else {
-                    memcpy(out, keys + b * kl, kl);
-                    out += kl, r++, b++;
-                }
-            }
-            return;
-        }
-        if (plain()) {
+        if (plain() && !has_run()) {
             memcpy(out, keys + lo * kl, (hi - lo) * kl);
             return;
         }
         const Cur c = at(lo);
-        uint64_t b = c.b;
+        uint64_t b = c.b, j = c.j;
         DeltaTree::Iter it = dt.iter(c.d);
         for (uint64_t r = lo; r < hi;) {
-            const int s = !it.l ? -1 : b >= nb ? 1 : cmp(keys + b * kl, it.key());
-            if (s < 0) {  // a base key the delta run does not touch
-                memcpy(out, keys + b * kl, kl);
-                out += kl, r++, b++;
+            const uint8_t *vk = view_peek(b, j);
+            const int s = !it.l ? -1 : !vk ? 1 : cmp(vk, it.key());
+            if (s < 0) {  // a view key the tree does not touch
+                memcpy(out, vk, kl);
+                out += kl, r++;
+                view_step(b, j);
             } else {
                 if (it.live()) {  // inserted (s > 0) or overwritten (s == 0)
                     memcpy(out, it.key(), kl);
                     out += kl, r++;
                 }
-                if (s == 0) b++;
+                if (s == 0) view_step(b, j);
                 it.advance();
             }
         }

@@ -1137,14 +1137,15 @@ struct rh_store {
             if (rf_on && !tier_fresh() && (rc = settle())) return rc;
             const bool snap = snap_ok;
             snap_ok = false;
-            // a large batch into a tier whose base is still the device's: copy the delta run
-            // (unless it has grown past a quarter of the base: then the base is refreshed)
-            if (snap && !tier_fresh() && !rf_on && tier_epoch == base_epoch && nd <= tier.nb / 4 + (1u << 16))
-                return tier_run_snapshot();
+            // a copy of the delta run serves while the tier's base is still the device's and the
+            // run is at most a quarter of the base (past that the base is refreshed)
+            const bool run_ok = !rf_on && tier_epoch == base_epoch && nd <= tier.nb / 4 + (1u << 16);
+            if (snap && !tier_fresh() && run_ok) return tier_run_snapshot();  // a batch too large to fold
             if (!tier_fresh() && !rf_on) {
                 if ((rc = start_refresh())) return rc;
                 return settle();
             }
+            if (tier_fresh() && tier.dt.size() > tree_limit() && run_ok) return tier_run_snapshot();  // the tree full
         }
         if (rf_on) return RH_OK;
         if (!tier_fresh() || refresh_wanted || tier.dt.size() > tree_limit()) return start_refresh();
@@ -1170,8 +1171,12 @@ struct rh_store {
     PinnedVec<uint32_t> trh_cntp, trh_br;
     uint64_t tier_runs = 0;
     bool snap_ok = false;  // set before a batch: a run copy may replace the refresh it causes
+    // with a run copy held, batches fold into the tree as deltas against base + run (mode 2: a
+    // host search of the run per row); one larger than this takes a new run copy instead
+    static constexpr size_t RUN_FOLD_MAX = 4096;
     bool run_copy_allowed(size_t m) const {
-        return tier_sync_writes && tier_fresh() && tier_epoch == base_epoch && m > tree_limit();
+        return tier_sync_writes && tier_fresh() && tier_epoch == base_epoch &&
+               (m > tree_limit() || (tier.has_run() && m > RUN_FOLD_MAX));
     }
     int tier_run_snapshot() {
         int rc;
@@ -1251,7 +1256,8 @@ struct rh_store {
     //   2: from the batch's sorted fingerprints and ops, the deltas formed against the tier's own
     //      base on the host (the device compacted since the tier's copy was taken).
     int fold_mode(size_t m) const {
-        if (!tier_fresh() || m > tree_limit() || tier.has_run()) return 0;  // a run copy takes no folds
+        if (!tier_fresh() || m > tree_limit()) return 0;
+        if (tier.has_run()) return m <= RUN_FOLD_MAX ? 2 : 0;  // deltas against base + run copy
         return tier_epoch == base_epoch ? 1 : 2;
     }
     // whether the batch's rows must come down at all (a fold, or a refresh in flight to log for)

@@ -186,9 +186,10 @@ int main(int argc, char **argv) {
         std::vector<uint8_t> drop(bk.size());
         std::vector<Fp> fps(bk.size());
         // every 4th batch is "too large for the tree": A takes a run copy of the whole change since
-        // its base copy instead of folding; the batch after it refreshes A's base (as the store does)
-        const bool snap = it % 4 == 2, after_snap = A.has_run();
-        if (after_snap) {
+        // its base copy instead of folding, and later batches fold into a tree over base + run;
+        // every 11th refreshes A's base (a compaction and a copy, as the store does)
+        const bool snap = it % 4 == 2;
+        if (it % 11 == 10) {
             flatten(base);
             A.build(kl, kk, model.size(), base.keys.data(), base.prefix.data());
         }

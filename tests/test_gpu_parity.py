@@ -1367,10 +1367,11 @@ def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
     take a copy of the device's delta run instead of a refresh of the whole base
     (rsos_hip_abi.hip tier_run_snapshot, host_tier.hpp HostTier::Run): inserts, overwrites and
     deletes of base keys, deletes of keys a previous batch inserted, re-inserts.  After each, the
-    tier -- base copy + run copy -- answers ranks of present and absent keys, select at every kind
-    of rank, key-bound aggregates of every bound kind, rank-range aggregates and whole protocol
-    rounds exactly as the device does; a small batch after a run copy, and a large one after a
-    compaction, refresh the base instead."""
+    tier -- base copy + run copy, and the tree of the small batches folded over them -- answers
+    ranks of present and absent keys, select at every kind of rank, key-bound aggregates of every
+    bound kind, rank-range aggregates and key dumps exactly as the device does; small batches
+    after a run copy fold into the tree (no copy), a large batch after a compaction refreshes the
+    base instead."""
     import torch
     from rsos_hip import GpuFingerprintStore, RecordSchema
     from rsos_hip.store import KeyRange
@@ -1439,10 +1440,17 @@ def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
     both(b, o)
     assert tier.tier_stats()["delta_entries"] == tier.stats()["delta_rows"]
     probe()
+    st0 = tier.tier_stats()
     small = make_records(s, 100, seed=602, random_keys=True)
-    both(small)  # after a run copy: the base is refreshed (the device compacts)
+    both(small)  # after a run copy: folded into the tree over base + run copy (no copy)
+    ov = {c: t[:300].clone() for c, t in base.items()}  # overwrites of base rows the run holds or not
+    ov["values"] ^= 0x21
+    dl = torch.ones(300, dtype=torch.uint8, device="cuda")
+    both({c: t[300:600].clone() for c, t in base.items()}, dl)  # deletes of base rows
+    both(ov)
+    both({c: t[:50].clone() for c, t in b.items()}, torch.ones(50, dtype=torch.uint8, device="cuda"))  # run keys deleted
     st = tier.tier_stats()
-    assert st["delta_entries"] == 0 and st["base_rows"] == tier.size()
+    assert st["refreshes"] == st0["refreshes"] and st["folds"] == st0["folds"] + 4
     probe()
     b, o = large(603, over=500)
     both(b, o)

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r4s5
+O=gpurun_out/${R4_OUT:-r4s5}
 mkdir -p $O
 run() {  # name, timeout, cmd...
   local name=$1 t=$2; shift 2

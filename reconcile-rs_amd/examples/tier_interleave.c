@@ -2,7 +2,7 @@
  * tier_interleave.c -- large write batches interleaved with small reconciliations, through the C ABI:
  * the host tier's background refresh under the load that forces it.
  *
- *   tier_interleave <n> <batch_rows> <reps> <host_tier 0|1> <shape u64|c5> [warmup]
+ *   tier_interleave <n> <batch_rows> <reps> <host_tier 0|1> <shape u64|c5> [warmup] [small]
  *
  * Two replicas of n records (shape u64: FingerprintTreeMap<u64, u64>, keys 0..n-1 as the
  * reference's protocol bench builds them, benches/protocol.rs:198-232; shape c5: config5's 16-byte
@@ -19,7 +19,10 @@
  * and writes go on without waiting for it (one refresh per copy time, never one per batch).
  * tier_refreshes counts the refreshes started by the timed batches (the last one landed by an
  * untimed rh_store_tier_sync after the loop); tier_refreshes_landed_in_loop those that landed
- * inside it.
+ * inside it.  small > 0: after each large batch and its drive, `small` cycles of one row staged
+ * into both replicas (rh_store_stage, the Rsos::insert path) and a drive -- the small writes that
+ * follow a large merge (with the tier on they fold over the run copy the large batch took); their
+ * distributions are reported as small_write_* / small_drive_*.
  */
 #define _POSIX_C_SOURCE 199309L
 #define __HIP_PLATFORM_AMD__ 1
@@ -211,11 +214,12 @@ static rh_columns view(const host_cols_t *c) {
 
 int main(int argc, char **argv) {
     if (argc < 6) {
-        fprintf(stderr, "usage: tier_interleave <n> <batch_rows> <reps> <host_tier 0|1> <u64|c5> [warmup]\n");
+        fprintf(stderr, "usage: tier_interleave <n> <batch_rows> <reps> <host_tier 0|1> <u64|c5> [warmup] [small]\n");
         return 1;
     }
     const uint64_t n = strtoull(argv[1], NULL, 10), m = strtoull(argv[2], NULL, 10);
     const int reps = atoi(argv[3]), tier = atoi(argv[4]), warm = argc > 6 ? atoi(argv[6]) : 2;
+    const int small = argc > 7 ? atoi(argv[7]) : 0;
     const int c5 = strcmp(argv[5], "c5") == 0;
     KL = c5 ? 16 : 8;
     STRIDE = n > 1 ? UINT64_MAX / n : 1;
@@ -260,6 +264,12 @@ int main(int argc, char **argv) {
     double *tw = malloc(sizeof(double) * (size_t)(reps + 1)), *td = malloc(sizeof(double) * (size_t)(reps + 1));
     double wsum = 0, dsum = 0;
     uint64_t ref0 = 0, fold0 = 0, next = 1;
+    const size_t nsm = (size_t)reps * (size_t)small + 1;
+    double *sw = malloc(sizeof(double) * nsm), *sd = malloc(sizeof(double) * nsm);
+    size_t ns_done = 0;
+    host_cols_t one;
+    alloc_cols(&one, 1);
+    const uint8_t op0 = 0;
     for (int r = -warm; r < reps; r++) {
         if (r == 0) { /* the timed loop starts from settled tiers (untimed) */
             CHECK(rh_store_tier_sync(a));
@@ -288,6 +298,22 @@ int main(int argc, char **argv) {
             tw[r] = w, td[r] = d;
             wsum += w, dsum += d;
         }
+        for (int k = 0; r >= 0 && k < small; k++) {  /* one staged row into both, then a drive */
+            make_row(n + next, 1, one.keys, one.vals, DATED ? one.phys : NULL, DATED ? one.logical : NULL,
+                     DATED ? one.node : NULL);
+            next++;
+            const rh_columns oc = view(&one);
+            uint64_t la = 0, lb = 0;
+            t0 = now_s();
+            CHECK(rh_store_stage(a, &oc, &op0, 1));
+            CHECK(rh_store_stage(b, &oc, &op0, 1));
+            CHECK(rh_store_len(a, &la)); /* each store applies its staged row on its next question */
+            CHECK(rh_store_len(b, &lb));
+            sw[ns_done] = now_s() - t0;
+            t0 = now_s();
+            c = reconcile(a, b, &sc);
+            sd[ns_done++] = now_s() - t0;
+        }
     }
     uint64_t size = 0, refreshes = 0, folds = 0, loop_refreshes = 0;
     CHECK(rh_store_len(a, &size));
@@ -296,19 +322,25 @@ int main(int argc, char **argv) {
     CHECK(rh_store_tier_stats(a, NULL, NULL, &refreshes, &folds));
     qsort(tw, (size_t)reps, sizeof(double), cmp_d);
     qsort(td, (size_t)reps, sizeof(double), cmp_d);
+    qsort(sw, ns_done, sizeof(double), cmp_d);
+    qsort(sd, ns_done, sizeof(double), cmp_d);
+#define SPCT(x, p) (ns_done ? (x)[(size_t)(((ns_done - 1) * (p)) / 100)] * 1e6 : 0.0)
 #define PCT(x, p) ((x)[(size_t)(((reps - 1) * (p)) / 100)] * 1e6)
     printf("{\"n\": %llu, \"shape\": \"%s\", \"batch_rows\": %llu, \"host_tier\": %d, \"reps\": %d, \"size\": %llu, "
            "\"rounds\": %llu, \"ranges\": %llu, \"idlists\": %llu, \"enumerated\": %llu, \"wire_bytes\": %llu, "
            "\"first_drive_us\": %.1f, \"drive_mean_us\": %.1f, \"drive_p50_us\": %.1f, \"drive_p90_us\": %.1f, "
            "\"drive_p99_us\": %.1f, \"drive_max_us\": %.1f, \"write_mean_us\": %.1f, \"write_p50_us\": %.1f, "
            "\"write_p99_us\": %.1f, \"write_max_us\": %.1f, \"tier_refreshes\": %llu, \"tier_refreshes_landed_in_loop\": %llu, "
-           "\"tier_folds\": %llu}\n",
+           "\"tier_folds\": %llu, \"small_cycles\": %llu, \"small_write_p50_us\": %.1f, \"small_write_p99_us\": %.1f, "
+           "\"small_write_max_us\": %.1f, \"small_drive_p50_us\": %.1f, \"small_drive_p99_us\": %.1f, "
+           "\"small_drive_max_us\": %.1f}\n",
            (unsigned long long)n, c5 ? "c5" : "u64", (unsigned long long)m, tier, reps, (unsigned long long)size,
            (unsigned long long)c.rounds, (unsigned long long)c.ranges, (unsigned long long)c.idlists,
            (unsigned long long)c.enumerated, (unsigned long long)c.wire_bytes, first * 1e6, dsum / reps * 1e6,
            PCT(td, 50), PCT(td, 90), PCT(td, 99), td[reps - 1] * 1e6, wsum / reps * 1e6, PCT(tw, 50), PCT(tw, 99),
            tw[reps - 1] * 1e6, (unsigned long long)(refreshes - ref0), (unsigned long long)(loop_refreshes - ref0),
-           (unsigned long long)(folds - fold0));
+           (unsigned long long)(folds - fold0), (unsigned long long)ns_done, SPCT(sw, 50), SPCT(sw, 99),
+           ns_done ? sw[ns_done - 1] * 1e6 : 0.0, SPCT(sd, 50), SPCT(sd, 99), ns_done ? sd[ns_done - 1] * 1e6 : 0.0);
     CHECK(rh_store_destroy(a));
     CHECK(rh_store_destroy(b));
     return 0;

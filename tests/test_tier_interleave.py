@@ -37,3 +37,22 @@ def test_interleaved_drives_equal_device_path(gpu, shape, n, m, policy):
         assert out[1]["tier_refreshes"] >= 1 and out[1]["tier_folds"] == 0
     else:  # folded, never copied again
         assert out[1]["tier_refreshes"] == 0 and out[1]["tier_folds"] == 5  # store a's folds
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["u64", "c5"])
+def test_small_writes_after_large_batches(gpu, shape):
+    """After each large batch (a run copy under the default policy) three single rows staged into
+    both replicas, each followed by a reconciliation: the rows fold into the tier's tree over base +
+    run copy (no copy), and every reconciliation sees what the device path sees."""
+    n, m, small = 200_000, 80_000, 3
+    out = {}
+    for tier in (0, 1):
+        r = subprocess.run([EX, str(n), str(m), "4", str(tier), shape, "1", str(small)], capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out[tier] = json.loads(r.stdout)
+    keys = ("size", "rounds", "ranges", "idlists", "enumerated", "wire_bytes")
+    assert {k: out[0][k] for k in keys} == {k: out[1][k] for k in keys}
+    assert out[1]["size"] == n + 5 * m + 4 * small and out[1]["small_cycles"] == 4 * small
+    assert out[1]["tier_folds"] == 4 * small  # store a's: every staged row folded, none copied

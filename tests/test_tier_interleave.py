@@ -45,7 +45,9 @@ def test_small_writes_after_large_batches(gpu, shape):
     """After each large batch (a run copy under the default policy) three single rows staged into
     both replicas, each followed by a reconciliation: the rows fold into the tier's tree over base +
     run copy (no copy), and every reconciliation sees what the device path sees."""
-    n, m, small = 200_000, 80_000, 3
+    # 130 k rows: past the tree (max(2^16, min(n / 8, 2^18)) = 125 k) -> a run copy, and past the
+    # compaction threshold (n / 6) every second batch -> a base refresh: both paths, then folds
+    n, m, small = 1_000_000, 130_000, 3
     out = {}
     for tier in (0, 1):
         r = subprocess.run([EX, str(n), str(m), "4", str(tier), shape, "1", str(small)], capture_output=True,

@@ -114,6 +114,12 @@ struct HostTier {
             samp2 = samp2_own.data();
         }
     }
+    // a window's cache lines requested at once (at 10^8 rows the windows are cold: the binary search
+    // in them would otherwise wait for each line in turn)
+    static void prefetch_span(const void *p, size_t bytes) {
+        const char *c = static_cast<const char *>(p);
+        for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch(c + o);
+    }
     // the first sample >= d (> d with upper), through the index: samp[64 (i - 1)] < d (<= d) and
     // samp[64 i] >= d (> d) bound a window of 63 samples
     static uint64_t samp_bound(const uint64_t *samp, uint64_t ns, const uint64_t *samp2, uint64_t ns2, uint64_t d,
@@ -123,6 +129,7 @@ struct HostTier {
         const uint64_t lo = std::max<uint64_t>(from, i ? ((i - 1) << SHIFT) + 1 : 0);
         const uint64_t hi = std::min<uint64_t>(ns, i << SHIFT);
         if (lo >= hi) return lo;  // the window is empty: the bound is its start
+        prefetch_span(samp + lo, (hi - lo) * 8);
         return upper ? std::upper_bound(samp + lo, samp + hi, d) - samp : std::lower_bound(samp + lo, samp + hi, d) - samp;
     }
     // keys below `key` among n sorted keys with those samples: the samples narrow it to one window
@@ -135,6 +142,7 @@ struct HostTier {
         const uint64_t jh = samp_bound(sp, nsp, sp2, nsp2, d, true, jl);
         uint64_t lo = jl ? ((jl - 1) << SHIFT) + 1 : 0;     // keys[64 (jl - 1)] < key
         uint64_t hi = std::min<uint64_t>(nk, jh << SHIFT);  // keys[64 jh] > key
+        if (hi - lo <= 64) prefetch_span(ks + lo * kl, (hi - lo) * kl);
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
             if (cmp(ks + mid * kl, key) < 0) lo = mid + 1;

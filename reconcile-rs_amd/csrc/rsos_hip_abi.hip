@@ -1699,7 +1699,11 @@ struct rh_store {
         if ((rc = tier_reserve(rows))) return rc;
         // bsums / ssums / samples may have moved: derive them again from the kept fingerprints
         if ((rc = resum_base())) return rc;
-        return sync();
+        if ((rc = sync())) return rc;
+        // a tier whose page-locked sets moved is stale: with writes keeping it fresh, the
+        // reservation (a setup call) copies it again now, not the next question's device path
+        if (tier_on && tier_sync_writes && !tier_fresh() && !rf_on && (rc = start_refresh())) return rc;
+        return tier_sync_writes ? settle() : RH_OK;
     }
     hipEvent_t res_ev = nullptr;  // apply_device_many: the result copy of the batch in flight
     int sync_event(hipEvent_t ev) {  // sync() for one event: poll ~1 ms, then block

@@ -16,5 +16,6 @@ run() {  # name, timeout, cmd...
 }
 run pytest_tier 500 python -u -m pytest tests/test_tier_interleave.py tests/test_gpu_parity.py -k "interleave or small_writes or run_copy or host_tier" -m gpu -v --timeout 300 --timeout-method thread
 run interleave_small 500 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 12 1 c5 2 3
+run latency 200 reconcile-rs_amd/examples/rbsr_latency 100000000 1 200 1 1
 run interleave_small_tier0 500 reconcile-rs_amd/examples/tier_interleave 100000000 1000000 12 0 c5 2 3
 echo "== done"

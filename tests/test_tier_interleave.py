@@ -45,16 +45,19 @@ def test_small_writes_after_large_batches(gpu, shape):
     """After each large batch (a run copy under the default policy) three single rows staged into
     both replicas, each followed by a reconciliation: the rows fold into the tier's tree over base +
     run copy (no copy), and every reconciliation sees what the device path sees."""
-    # 130 k rows: past the tree (max(2^16, min(n / 8, 2^18)) = 125 k) -> a run copy, and past the
-    # compaction threshold (n / 6) every second batch -> a base refresh: both paths, then folds
+    # 130 k rows: past the tree (RSOS_HIP_TIER_TREE=50000 here, as the map grows past n / 8) -> a
+    # run copy, and past the compaction threshold (n / 6) every second batch -> a base refresh:
+    # both paths, then folds
     n, m, small = 1_000_000, 130_000, 3
     out = {}
+    env = dict(os.environ, RSOS_HIP_TIER_TREE="50000")
     for tier in (0, 1):
         r = subprocess.run([EX, str(n), str(m), "4", str(tier), shape, "1", str(small)], capture_output=True,
-                           text=True, timeout=300)
+                           text=True, timeout=300, env=env)
         assert r.returncode == 0, r.stderr
         out[tier] = json.loads(r.stdout)
     keys = ("size", "rounds", "ranges", "idlists", "enumerated", "wire_bytes")
     assert {k: out[0][k] for k in keys} == {k: out[1][k] for k in keys}
     assert out[1]["size"] == n + 5 * m + 4 * small and out[1]["small_cycles"] == 4 * small
-    assert out[1]["tier_folds"] == 4 * small  # store a's: every staged row folded, none copied
+    assert out[1]["tier_folds"] == 4 * small  # store a's: every staged row folded, no large batch
+    assert out[1]["tier_refreshes"] >= 4  # every large batch: a run copy or a base refresh

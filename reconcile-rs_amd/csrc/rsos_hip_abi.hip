@@ -1129,7 +1129,18 @@ struct rh_store {
     // After a batch (committed, folded, logged): start the refresh the tier needs, unless one is
     // in flight -- so under a stream of large batches the refreshes (a compaction and a copy
     // each) run back to back, one per copy time, not one per batch, and no write waits for one.
+    // The batch has committed by now: a tier that cannot be brought up to date for want of host
+    // memory is left stale (questions go to the device; the next write tries again) -- reporting
+    // it would make the caller think the batch failed.  Device errors still propagate.
     int post_batch() {
+        const int rc = post_batch_tier();
+        if (rc == RH_ERR_OOM) {
+            tier_version = ~0ull;
+            return RH_OK;
+        }
+        return rc;
+    }
+    int post_batch_tier() {
         if (!tier_on) return RH_OK;
         stale_questions = 0;
         int rc;

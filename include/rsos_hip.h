@@ -433,7 +433,9 @@ int rh_estore_set_host_tier(rh_estore *store, int enable);
 /* ---- testing ---------------------------------------------------------------------------
  * Make the named internal failure point fail once (RH_ERR_OOM) on the calling thread; NULL or
  * "" clears it.  Points: "snapshot.load_begin" (the projection store's half of a reload),
- * "snapshot.load_finish" (the dated store's).  For tests of error paths only.              */
+ * "snapshot.load_finish" (the dated store's), "tier.run_copy" (the host tier's copy of the delta
+ * run after a large batch: the batch still succeeds, the tier goes stale).  For tests of error
+ * paths only.                                                                                */
 int rh_debug_fail_point(const char *name);
 
 /* ---- measurement -----------------------------------------------------------------------

@@ -1191,6 +1191,7 @@ struct rh_store {
     }
     int tier_run_snapshot() {
         int rc;
+        if (fail_point("tier.run_copy")) return fail(RH_ERR_OOM, "injected failure (tier run copy)");
         const uint64_t n1 = nd;
         if (n1 == 0) {  // nothing since the base copy: the base alone is the map
             tier.set_run(rh::HostTier::Run{});

@@ -1462,6 +1462,18 @@ def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
     both(b, o)
     assert tier.tier_stats()["delta_entries"] == 0
     probe()
+    # a run copy that fails for want of host memory: the batch still commits, the tier goes stale
+    # (the device answers), and the next write brings it back
+    from rsos_hip import _abi as A
+    b, o = large(605, over=200)
+    A.lib().rh_debug_fail_point(b"tier.run_copy")
+    both(b, o)
+    A.lib().rh_debug_fail_point(b"")
+    assert tier.tier_stats()["base_rows"] == 0  # stale
+    probe()
+    both(make_records(s, 10, seed=606, random_keys=True))
+    assert tier.tier_stats()["base_rows"] > 0
+    probe()
     dev.close()
     tier.close()
 

@@ -1579,6 +1579,32 @@ struct rh_store {
             return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
         }
         if (tsets[tact].keys.p != k0 || tsets[tact].prefix.p != p0 || tsets[tact].samp.p != s0) tier_version = ~0ull;
+        // the run copy's page-locked columns, for the largest run the policy copies (a quarter of
+        // the base): pinned here, with the base's, not by the write whose run first outgrows them
+        if (tier_sync_writes) {
+            const uint64_t rr = rows / 4 + (1u << 16);
+            const void *before[7] = {trh_keys.p, trh_pre.p, trh_cntp.p, trh_fl.p, trh_br.p, trh_smp.p, trh_gs.p};
+            try {
+                auto room = [](auto &v, size_t want) {
+                    if (v.capacity() < want) {
+                        v.clear();
+                        v.reserve(want);
+                    }
+                };
+                room(trh_keys, rr * kl + 64);
+                room(trh_pre, (rr + 1) * 4 + 8);
+                room(trh_cntp, rr + 16);
+                room(trh_fl, rr + 16);
+                room(trh_br, rr + 16);
+                room(trh_smp, rr / 64 + rr / 4096 + 16);
+                room(trh_gs, rr / 64 + 16);
+            } catch (const std::bad_alloc &) {
+                tier_version = ~0ull;
+                return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+            }
+            const void *after[7] = {trh_keys.p, trh_pre.p, trh_cntp.p, trh_fl.p, trh_br.p, trh_smp.p, trh_gs.p};
+            if (tier.has_run() && memcmp(before, after, sizeof before)) tier_version = ~0ull;  // a held run moved
+        }
         return RH_OK;
     }
     int load_finish(size_t m, bool last_wins) {

@@ -290,6 +290,12 @@ int rh_store_tier_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_en
 /* Wait until the host tier is fresh (a background refresh landed and swapped in, one started if
  * none was under way): a warm store for benchmarks and tests.  No-op with the tier off.          */
 int rh_store_tier_sync(rh_store *store);
+/* The refresh policy of one store (its default: RSOS_HIP_TIER_SYNC when the store was created,
+ * else 1).  keep_fresh = 1: a write, load or reservation that needs the tier copied again waits
+ * for the copy, so every question is answered on the host; 0: writes never wait for a copy, and
+ * questions go to the device while one is in flight.  Takes effect from the next write; a copy in
+ * flight is waited for first.                                                                  */
+int rh_store_set_tier_policy(rh_store *store, int keep_fresh);
 
 /* Staged single-record updates: Rsos::insert / delete one record at a time (mutate.rs:23-154)
  * without one device round trip each.  rh_store_stage appends m host rows (columns as for

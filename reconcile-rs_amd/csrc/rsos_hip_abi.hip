@@ -2766,6 +2766,16 @@ int rh_store_tier_sync(rh_store *s) {
     return rc;
 }
 
+int rh_store_set_tier_policy(rh_store *s, int keep_fresh) {
+    if (!s || keep_fresh < 0 || keep_fresh > 1) return fail(RH_ERR_ARG, "bad tier policy");
+    std::lock_guard<std::mutex> g(s->mu);
+    RH_HIP(hipSetDevice(s->device));
+    int rc;
+    if ((rc = s->settle())) return rc;
+    s->tier_sync_writes = keep_fresh == 1;
+    return RH_OK;
+}
+
 int rh_store_reserve(rh_store *s, uint64_t rows, uint64_t batch_rows) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
     if (rows >= (1ull << 31) || batch_rows >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows)");

@@ -107,6 +107,7 @@ SIGNATURES = [
     ("rh_store_tier_stats", C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64)]),
     ("rh_store_tier_sync", C.c_int, [P]),
+    ("rh_store_set_tier_policy", C.c_int, [P, C.c_int]),
     ("rh_snapshot_header", C.c_int, [VP, SZ, C.POINTER(C.c_uint64)]),
     ("rh_snapshot_decode_device", C.c_int, [C.POINTER(Schema), C.c_int, VP, SZ, C.POINTER(Columns), SZ,
                                             C.POINTER(SnapshotInfo), VP]),

@@ -183,6 +183,11 @@ class GpuFingerprintStore:
         """Wait until the host tier is fresh (its background refresh landed): rh_store_tier_sync."""
         A.check(A.lib().rh_store_tier_sync(self._h), "rh_store_tier_sync")
 
+    def set_tier_policy(self, keep_fresh: bool) -> None:
+        """Whether writes keep the host tier fresh (wait for the copies they cause; the default)
+        or never wait (questions go to the device meanwhile): rh_store_set_tier_policy."""
+        A.check(A.lib().rh_store_set_tier_policy(self._h, 1 if keep_fresh else 0), "rh_store_set_tier_policy")
+
     def batch_stats(self) -> Dict[str, int]:
         """Batches applied by the small-batch path and by the large-batch path (rh_store_batch_stats)."""
         a, b = C.c_uint64(), C.c_uint64()

@@ -164,6 +164,7 @@ extern "C" {
     pub fn rh_store_tier_stats(store: *mut rh_store, base_rows: *mut u64, delta_entries: *mut u64,
                                refreshes: *mut u64, folds: *mut u64) -> c_int;
     pub fn rh_store_tier_sync(store: *mut rh_store) -> c_int;
+    pub fn rh_store_set_tier_policy(store: *mut rh_store, keep_fresh: c_int) -> c_int;
     pub fn rh_store_set_compaction(store: *mut rh_store, divisor: u64, min_rows: u64) -> c_int;
     pub fn rh_store_reserve(store: *mut rh_store, rows: u64, batch_rows: u64) -> c_int;
     pub fn rh_store_stats(store: *mut rh_store, base_rows: *mut u64, delta_rows: *mut u64,

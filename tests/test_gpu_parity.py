@@ -1514,3 +1514,40 @@ def test_search_table_with_bunched_keys(gpu):
     st.compact()
     check()
     st.close()
+
+
+@pytest.mark.gpu
+def test_tier_policy_switch(gpu):
+    """rh_store_set_tier_policy: with writes never waiting, a batch past the tier's tree returns at
+    once and questions may go to the device while the copy is in flight; switched back, the next
+    such batch leaves the tier fresh (base copy or run copy).  Answers equal the device path's
+    either way."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.synth import make_records, to_host
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 100_000
+    base = make_records(s, n, seed=41)
+    dev, tier = GpuFingerprintStore(s, host_tier=False), GpuFingerprintStore(s, host_tier=True)
+    for st in (dev, tier):
+        st.load_bulk_device(base)
+    rng = np.random.default_rng(3)
+    pool = to_host(base)["keys"]
+
+    def same():
+        ks = np.concatenate([pool[rng.integers(0, n, 300)], rng.integers(0, 256, (100, 16), dtype=np.uint8)])
+        assert np.array_equal(tier.ranks(ks), dev.ranks(ks))
+        assert tier.aggregate() == dev.aggregate()
+        for r in rng.integers(0, dev.size(), 50):
+            assert tier.select(int(r)) == dev.select(int(r))
+
+    tier.set_tier_policy(False)
+    b = make_records(s, 70_000, seed=42, random_keys=True)
+    assert tier.apply_device(b) == dev.apply_device(b)
+    same()
+    tier.set_tier_policy(True)
+    b = make_records(s, 70_000, seed=43, random_keys=True)
+    assert tier.apply_device(b) == dev.apply_device(b)
+    assert tier.tier_stats()["base_rows"] > 0  # fresh right after the write
+    same()
+    dev.close()
+    tier.close()

@@ -34,7 +34,7 @@ pub use values::{FixedBytes, FixedValue};
 
 use std::ffi::CStr;
 use std::ops::{Bound, RangeBounds};
-use std::os::raw::c_void;
+use std::os::raw::{c_int, c_void};
 
 use rsos::{Aggregate, Fingerprint, Rsos};
 use serde::Serialize;
@@ -212,6 +212,15 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         // SAFETY: store was just created.
         check(unsafe { ffi::rh_store_set_host_tier(store.0, 1, 0) }, "rh_store_set_host_tier");
         HipFingerprintMap { store, entries: sorted::SortedBlocks::new() }
+    }
+
+    /// Whether a write that outgrows the host tier's delta tree waits for the tier's copy
+    /// (`true`, the default: every later read is answered from host memory) or returns at once
+    /// (`false`: reads go to the device until the copy lands) -- `rh_store_set_tier_policy`.
+    pub fn set_tier_policy(&self, keep_fresh: bool) {
+        // SAFETY: the handle is live for &self.
+        check(unsafe { ffi::rh_store_set_tier_policy(self.store.0, keep_fresh as c_int) },
+              "rh_store_set_tier_policy");
     }
 
     /// Bulk fill (FromIterator / ReplicatedMap::load_bulk): sort, de-duplicate keeping the

@@ -568,6 +568,8 @@ struct PinnedVec {
     // stream has synchronised (the kernel's end-of-dispatch release), or after a system-scope
     // fence in the kernel (the small batch's sequence word)
     unsigned flags = hipHostMallocMapped | hipHostMallocPortable;
+    void *dptr = nullptr;          // the device address of p, once looked up (store.dev_ptr)
+    const void *dptr_of = nullptr;  // ... and the allocation it belongs to
     PinnedVec() = default;
     PinnedVec(const PinnedVec &) = delete;
     PinnedVec &operator=(const PinnedVec &) = delete;
@@ -576,6 +578,7 @@ struct PinnedVec {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         n = cap = 0;
+        dptr = nullptr;
     }
     void reserve(size_t want) {
         if (want <= cap) return;
@@ -587,6 +590,7 @@ struct PinnedVec {
         if (p) (void)hipHostFree(p);
         p = q;
         cap = c;
+        dptr = nullptr;  // a new allocation: its device address is looked up again
     }
     void resize(size_t m) { reserve(m); n = m; }
     void assign(size_t m, uint8_t byte) { resize(m); memset(p, byte, m * sizeof(T)); }
@@ -754,15 +758,21 @@ struct rh_store {
     }
     PinnedVec<uint8_t> sb_in;    // a small host batch, packed (the device reads it in place)
     PinnedVec<uint64_t> sb_res;  // the small path's result block (written by the device in place)
+    // the device address of a mapped page-locked buffer: looked up once per allocation (the
+    // buffer keeps it until it moves), not once per batch
     template <class T>
-    int dev_ptr(T *host, T **dev) {  // the device address of mapped page-locked memory
-        void *d = nullptr;
-        const hipError_t e = hipHostGetDevicePointer(&d, host, 0);
-        if (e != hipSuccess || !d) {
-            (void)hipGetLastError();
-            return fail(RH_ERR_HIP, "page-locked buffer has no device address");
+    int dev_ptr(PinnedVec<T> &v, T **dev) {
+        if (!v.dptr || v.dptr_of != v.p) {
+            void *d = nullptr;
+            const hipError_t e = hipHostGetDevicePointer(&d, v.p, 0);
+            if (e != hipSuccess || !d) {
+                (void)hipGetLastError();
+                return fail(RH_ERR_HIP, "page-locked buffer has no device address");
+            }
+            v.dptr = d;
+            v.dptr_of = v.p;
         }
-        *dev = static_cast<T *>(d);
+        *dev = static_cast<T *>(v.dptr);
         return RH_OK;
     }
     int pack_small(const rh_columns &h, const uint8_t *ops, size_t m, rh_columns *d, const uint8_t **dops) {
@@ -793,7 +803,7 @@ struct rh_store {
         if (tags) put(o_tg, h.tags, m);
         put(o_op, ops, m);
         uint8_t *db;
-        int rc = dev_ptr(b, &db);
+        int rc = dev_ptr(sb_in, &db);
         if (rc) return rc;
         *d = rh_columns{db, dated ? reinterpret_cast<const uint64_t *>(db + o_ph) : nullptr,
                         dated ? reinterpret_cast<const uint32_t *>(db + o_lg) : nullptr,
@@ -847,10 +857,9 @@ struct rh_store {
         } catch (const std::bad_alloc &) {
             return fail(RH_ERR_OOM, "small batch: page-locked allocation failed");
         }
-        if ((rc = dev_ptr(sb_res.data(), &res))) return rc;
-        if (want && ((rc = dev_ptr(fold_keys.data(), &fk)) || (rc = dev_ptr(fold_recs.data(), &fr)) ||
-                     (rc = dev_ptr(fold_ops.data(), &fd)) || (rc = dev_ptr(fold_fps.data(), &ff)) ||
-                     (rc = dev_ptr(fold_sops.data(), &fo))))
+        if ((rc = dev_ptr(sb_res, &res))) return rc;
+        if (want && ((rc = dev_ptr(fold_keys, &fk)) || (rc = dev_ptr(fold_recs, &fr)) || (rc = dev_ptr(fold_ops, &fd)) ||
+                     (rc = dev_ptr(fold_fps, &ff)) || (rc = dev_ptr(fold_sops, &fo))))
             return rc;
         const int nxt = 1 - cd;
         rh::SmallBatch a{};

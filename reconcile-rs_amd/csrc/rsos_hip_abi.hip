@@ -2286,16 +2286,14 @@ struct rh_store {
                 if (p.src) memcpy(stage_in.data() + p.off, p.src, p.bytes);
             if (zero_copy) {
                 pr_out.resize(worst);
-                void *di = nullptr, *dout = nullptr;
+                uint8_t *di = nullptr, *dout = nullptr;
                 // both buffers are allocated mapped; if the runtime still gives no device address,
-                // take the copy path below instead
-                if (hipHostGetDevicePointer(&di, stage_in.data(), 0) != hipSuccess || !di ||
-                    hipHostGetDevicePointer(&dout, pr_out.data(), 0) != hipSuccess || !dout) {
-                    (void)hipGetLastError();
+                // take the copy path below instead (dev_ptr looks each one up once per allocation)
+                if (dev_ptr(stage_in, &di) || dev_ptr(pr_out, &dout)) {
                     zero_copy = false;
                 } else {
-                    in_p = static_cast<const uint8_t *>(di);
-                    out_p = static_cast<uint8_t *>(dout);
+                    in_p = di;
+                    out_p = dout;
                 }
             }
             if (!zero_copy) {

@@ -2300,8 +2300,20 @@ struct rh_store {
                 RH_HIP(hipMemcpyAsync(r_in.p, stage_in.data(), in_bytes, hipMemcpyHostToDevice, stream));
             }
         } else {
-            for (const auto &p : parts)  // keys of an all-unbounded side may be NULL (never read)
-                if (p.src) RH_HIP(hipMemcpyAsync(r_in.p + p.off, p.src, p.bytes, hipMemcpyHostToDevice, stream));
+            // the peer store's children, handed over in place (round_layout), already sit in this
+            // input layout whenever a row of keys is a whole number of 16-byte units: one copy
+            const uint8_t *base = reinterpret_cast<const uint8_t *>(in.start_kinds);
+            const bool contiguous = base && in.end_kinds && in.start_keys && in.end_keys && in.aggregates &&
+                                    reinterpret_cast<const uint8_t *>(in.end_kinds) == base + o_ek &&
+                                    static_cast<const uint8_t *>(in.start_keys) == base + o_sk &&
+                                    static_cast<const uint8_t *>(in.end_keys) == base + o_ekeys &&
+                                    reinterpret_cast<const uint8_t *>(in.aggregates) == base + o_rem;
+            if (contiguous) {
+                RH_HIP(hipMemcpyAsync(r_in.p, base, in_bytes, hipMemcpyHostToDevice, stream));
+            } else {
+                for (const auto &p : parts)  // keys of an all-unbounded side may be NULL (never read)
+                    if (p.src) RH_HIP(hipMemcpyAsync(r_in.p + p.off, p.src, p.bytes, hipMemcpyHostToDevice, stream));
+            }
         }
         const uint8_t *d_sk = in_p, *d_ek = in_p + o_ek, *d_skeys = in_p + o_sk, *d_ekeys = in_p + o_ekeys;
         const uint64_t *d_rem = reinterpret_cast<const uint64_t *>(in_p + o_rem);

@@ -444,11 +444,10 @@ __device__ __forceinline__ void acc_span_lane(Acc &a, const uint8_t *src, uint64
     }
 }
 
-// Σ over rank range [lo, hi) (already clamped) by one wave; lane 0 writes the rh_aggregate
-// {u64 fp[4]; u64 size} at o
-__device__ __forceinline__ void wave_range_agg(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
-                                               const uint8_t *ssums, uint64_t lo, uint64_t hi, uint32_t lane,
-                                               uint64_t *o) {
+// Σ over rank range [lo, hi) (already clamped) by one wave, as four 64-bit limbs (lane 0's are the sum)
+__device__ __forceinline__ void wave_range_fp(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
+                                              const uint8_t *ssums, uint64_t lo, uint64_t hi, uint32_t lane,
+                                              uint64_t fp[4]) {
     Acc a;
     acc_zero(a);
     const uint64_t B = 256;
@@ -468,13 +467,25 @@ __device__ __forceinline__ void wave_range_agg(const uint8_t *fps, uint32_t stri
         }
     }
     acc_wave_reduce(a);
+    uint32_t f[8];
+    acc_normalise(a, f);
+    fp[0] = (uint64_t)f[0] | ((uint64_t)f[1] << 32);
+    fp[1] = (uint64_t)f[2] | ((uint64_t)f[3] << 32);
+    fp[2] = (uint64_t)f[4] | ((uint64_t)f[5] << 32);
+    fp[3] = (uint64_t)f[6] | ((uint64_t)f[7] << 32);
+}
+
+// the same; lane 0 writes the rh_aggregate {u64 fp[4]; u64 size} at o
+__device__ __forceinline__ void wave_range_agg(const uint8_t *fps, uint32_t stride, const uint8_t *bsums,
+                                               const uint8_t *ssums, uint64_t lo, uint64_t hi, uint32_t lane,
+                                               uint64_t *o) {
+    uint64_t fp[4];
+    wave_range_fp(fps, stride, bsums, ssums, lo, hi, lane, fp);
     if (lane == 0) {
-        uint32_t f[8];
-        acc_normalise(a, f);
-        o[0] = (uint64_t)f[0] | ((uint64_t)f[1] << 32);
-        o[1] = (uint64_t)f[2] | ((uint64_t)f[3] << 32);
-        o[2] = (uint64_t)f[4] | ((uint64_t)f[5] << 32);
-        o[3] = (uint64_t)f[6] | ((uint64_t)f[7] << 32);
+        o[0] = fp[0];
+        o[1] = fp[1];
+        o[2] = fp[2];
+        o[3] = fp[3];
         o[4] = hi - lo;
     }
 }
@@ -628,6 +639,191 @@ __global__ __launch_bounds__(256) void k_round_emit(const uint64_t *hdr, uint64_
     for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nc; c += nw) {
         const uint64_t j = round_owner(g.choff, r, c);
         round_emit_child(c, j, c - g.choff[j], L, kl, lane, in, g, out);
+    }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < r; j += nw * 64)
+        if (g.nen[j]) round_emit_enum(j, g.enoff[j], L, kl, in, g, out);
+}
+
+// ---- rounds over base + delta run (RoundRun, internal.hpp) ----
+__device__ __forceinline__ void fp_add256(uint64_t a[4], const uint64_t *b) {
+    uint64_t c = 0;
+    for (int i = 0; i < 4; i++) {
+        const uint64_t s = a[i] + b[i], t = s + c;
+        c = (uint64_t)(s < a[i]) | (uint64_t)(t < s);
+        a[i] = t;
+    }
+}
+__device__ __forceinline__ bool run_live(const RoundRun &R, uint64_t j) { return R.flags[j] & 2; }
+__device__ __forceinline__ bool run_in_base(const RoundRun &R, uint64_t j) { return R.flags[j] & 1; }
+// live view keys <= run entry j (non-decreasing in j)
+__device__ __forceinline__ int64_t run_g(const RoundRun &R, uint64_t j) {
+    return (int64_t)R.brank[j] + R.cntp[j] + (run_live(R, j) ? 1 : 0);
+}
+struct ViewPlace {
+    uint64_t b, j;
+    const uint8_t *key;
+};
+// select: the view key of rank v < nv and its place (host_tier.hpp HostTier::view_at): the first
+// entry with G(j) > v is that key itself, or the key is an untouched base row between entries
+// j - 1 and j.  Every lane computes the same (uniform loads).
+__device__ __forceinline__ ViewPlace view_at(const RoundRun &R, const uint8_t *bkeys, uint32_t kl, uint64_t v) {
+    const uint64_t ns = (R.n + 63) >> 6;
+    uint64_t a = 0, z = ns;
+    while (a < z) {  // the first sampled entry with G > v bounds a window of 64 entries
+        const uint64_t mid = (a + z) >> 1;
+        if ((uint64_t)R.gsamp[mid] > v) z = mid;
+        else a = mid + 1;
+    }
+    uint64_t lo = a ? ((a - 1) << 6) + 1 : 0, hi = a << 6 < R.n ? a << 6 : R.n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)run_g(R, mid) > v) hi = mid;
+        else lo = mid + 1;
+    }
+    const uint64_t j = lo;
+    if (j < R.n && run_live(R, j) && (uint64_t)((int64_t)R.brank[j] + R.cntp[j]) == v)
+        return ViewPlace{R.brank[j], j, R.keys + j * kl};
+    const uint64_t gprev = j ? (uint64_t)run_g(R, j - 1) : 0;
+    const uint64_t b0 = j ? R.brank[j - 1] + (run_in_base(R, j - 1) ? 1 : 0) : 0;
+    const uint64_t b = b0 + (v - gprev);
+    return ViewPlace{b, j, bkeys + b * kl};
+}
+// Σ of the live view keys between two places (lane 0's limbs)
+__device__ __forceinline__ void view_range_fp(const RoundIn &in, const RoundRun &R, uint64_t b0, uint64_t j0,
+                                              uint64_t b1, uint64_t j1, uint32_t lane, uint64_t fp[4]) {
+    uint64_t d[4];
+    wave_range_fp(in.fps, 32, in.bsums, in.ssums, b0, b1, lane, fp);
+    wave_range_fp(R.contrib, 32, R.bsums, R.ssums, j0, j1, lane, d);
+    fp_add256(fp, d);
+}
+
+// Every segment's view rank range [l, h), its places and its aggregate (ZERO when inverted), one
+// wave each.  The bound keys' ranks are rank_x[ia * j] / rank_x[ib * j + off] (a round: starts then
+// ends; the two-call path: interleaved)
+__global__ __launch_bounds__(256) void k_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk,
+                                                     const uint8_t *ek, RoundIn in, RoundRun R, uint64_t r,
+                                                     uint32_t ia, uint32_t ib, uint64_t off, uint64_t *lo_out,
+                                                     uint64_t *hi_out, uint64_t *agg_out, uint64_t *place) {
+    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (j >= r) return;  // uniform per wave
+    const uint64_t qs = ia * j, qe = ib * j + off;
+    const uint64_t bs = sk[j] ? rank_b[qs] : 0, js = sk[j] ? rank_j[qs] : 0;
+    const uint64_t be = ek[j] ? rank_b[qe] : R.nb, je = ek[j] ? rank_j[qe] : R.n;
+    const uint64_t l = (uint64_t)((int64_t)bs + R.cntp[js]), h = (uint64_t)((int64_t)be + R.cntp[je]);
+    uint64_t fp[4] = {0, 0, 0, 0};
+    if (h > l) view_range_fp(in, R, bs, js, be, je, lane, fp);  // uniform; an inverted range is ZERO
+    if (lane == 0) {
+        lo_out[j] = l;
+        hi_out[j] = h;
+        if (place) {
+            place[4 * j] = bs;
+            place[4 * j + 1] = js;
+            place[4 * j + 2] = be;
+            place[4 * j + 3] = je;
+        }
+        uint64_t *o = agg_out + 5 * j;
+        o[0] = fp[0];
+        o[1] = fp[1];
+        o[2] = fp[2];
+        o[3] = fp[3];
+        o[4] = h > l ? h - l : 0;
+    }
+}
+
+// Rank-range aggregates over the view ([lo, hi) clamped as k_range_query_wave clamps), one wave each
+__global__ __launch_bounds__(256) void k_range_query_view(RoundIn in, RoundRun R, uint32_t kl, uint64_t nv,
+                                                          const uint64_t *qlo, const uint64_t *qhi, uint64_t q,
+                                                          uint64_t *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (j >= q) return;  // uniform per wave
+    uint64_t lo = qlo[j], hi = qhi[j];
+    if (hi > nv) hi = nv;
+    if (lo > hi) lo = hi;
+    uint64_t fp[4] = {0, 0, 0, 0};
+    if (hi > lo) {
+        const ViewPlace a = view_at(R, in.bkeys, kl, lo);
+        const ViewPlace z = hi < nv ? view_at(R, in.bkeys, kl, hi) : ViewPlace{R.nb, R.n, nullptr};
+        view_range_fp(in, R, a.b, a.j, z.b, z.j, lane, fp);
+    }
+    if (lane == 0) {
+        uint64_t *o = out + 5 * j;
+        o[0] = fp[0];
+        o[1] = fp[1];
+        o[2] = fp[2];
+        o[3] = fp[3];
+        o[4] = hi - lo;
+    }
+}
+
+// The view keys of the given ranks (each < nv), one thread each
+__global__ void k_select_view(RoundRun R, const uint8_t *bkeys, uint32_t kl, const uint64_t *ranks, uint64_t first,
+                              uint64_t m, uint8_t *out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    const ViewPlace p = view_at(R, bkeys, kl, ranks ? ranks[t] : first + t);
+    for (uint32_t w = 0; w < kl / 4; w++)
+        reinterpret_cast<uint32_t *>(out + t * kl)[w] = reinterpret_cast<const uint32_t *>(p.key)[w];
+}
+
+// child c (k-th of segment j) over the view: round_emit_child with the cut keys selected from
+// base + run and the sums taken between places
+__device__ __forceinline__ void round_emit_child_view(uint64_t c, uint64_t j, uint64_t k, const RoundLayout &L,
+                                                      uint32_t kl, uint32_t lane, const RoundIn &in,
+                                                      const RoundRun &R, const RoundSegs &g, const uint64_t *place,
+                                                      uint8_t *out) {
+    uint8_t skd = in.sk[j], ekd = in.ek[j];
+    const uint8_t *skey = skd ? in.skeys + j * kl : nullptr, *ekey = ekd ? in.ekeys + j * kl : nullptr;
+    uint64_t *agg = reinterpret_cast<uint64_t *>(out + L.caggs) + 5 * c;
+    const uint64_t ncuts = g.nch[j] - 1;
+    if (g.kind[j] == 1 || ncuts == 0) {
+        if (lane < 5) agg[lane] = g.kind[j] == 1 ? 0ull : g.loc[5 * j + lane];
+    } else {
+        const uint64_t st = g.stride[j], s0 = g.si[j];
+        const uint64_t lo = s0 + k * st, hi = k == ncuts ? g.ei[j] : s0 + (k + 1) * st;
+        ViewPlace a{place[4 * j], place[4 * j + 1], nullptr}, z{place[4 * j + 2], place[4 * j + 3], nullptr};
+        if (k) {
+            a = view_at(R, in.bkeys, kl, lo);
+            skd = 1, skey = a.key;
+        }
+        if (k != ncuts) {
+            z = view_at(R, in.bkeys, kl, hi);
+            ekd = 1, ekey = z.key;
+        }
+        uint64_t fp[4];
+        view_range_fp(in, R, a.b, a.j, z.b, z.j, lane, fp);
+        if (lane == 0) {
+            agg[0] = fp[0];
+            agg[1] = fp[1];
+            agg[2] = fp[2];
+            agg[3] = fp[3];
+            agg[4] = hi - lo;
+        }
+    }
+    if (lane == 0) {
+        out[L.csk + c] = skd;
+        out[L.cek + c] = ekd;
+    }
+    if (lane < kl / 4) {
+        reinterpret_cast<uint32_t *>(out + L.cskeys + c * kl)[lane] =
+            skey ? reinterpret_cast<const uint32_t *>(skey)[lane] : 0u;
+        reinterpret_cast<uint32_t *>(out + L.cekeys + c * kl)[lane] =
+            ekey ? reinterpret_cast<const uint32_t *>(ekey)[lane] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_round_emit_view(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl,
+                                                         RoundIn in, RoundRun R, RoundSegs g, const uint64_t *place,
+                                                         uint8_t *out) {
+    const uint64_t nc = hdr[3], ne = hdr[1];
+    if (nc > cap) return;  // the host grows the buffer and launches again
+    const RoundLayout L = round_layout(nc, ne, kl);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nc; c += nw) {
+        const uint64_t j = round_owner(g.choff, r, c);
+        round_emit_child_view(c, j, c - g.choff[j], L, kl, lane, in, R, g, place, out);
     }
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < r; j += nw * 64)
         if (g.nen[j]) round_emit_enum(j, g.enoff[j], L, kl, in, g, out);
@@ -1031,6 +1227,50 @@ hipError_t launch_round_bounds(const uint32_t *rank, const RoundIn &in, const Ro
                                hipStream_t st) {
     if (r == 0) return hipSuccess;
     hipLaunchKernelGGL(k_round_bounds, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, rank, in, g, r, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const RoundIn &in,
+                                    const RoundRun &run, const RoundSegs &g, uint64_t *place, uint64_t r,
+                                    hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bounds_view, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, rank_b, rank_j, in.sk, in.ek, in,
+                       run, r, 1u, 1u, r, g.lo, g.hi, g.loc, place);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk, const uint8_t *ek,
+                               const RoundIn &in, const RoundRun &run, uint64_t r, uint64_t *lo, uint64_t *hi,
+                               uint64_t *aggs, hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bounds_view, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, rank_b, rank_j, sk, ek, in, run,
+                       r, 2u, 2u, (uint64_t)1, lo, hi, aggs, (uint64_t *)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_range_query_view(const RoundIn &in, const RoundRun &run, uint32_t kl, uint64_t nv,
+                                   const uint64_t *lo, const uint64_t *hi, uint64_t q, uint64_t *out, hipStream_t st) {
+    if (q == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_range_query_view, dim3((uint32_t)((q + 3) / 4)), dim3(256), 0, st, in, run, kl, nv, lo, hi, q,
+                       out);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_view(const RoundRun &run, const uint8_t *bkeys, uint32_t kl, const uint64_t *ranks,
+                              uint64_t first, uint64_t m, uint8_t *out, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_select_view, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, st, run, bkeys, kl, ranks, first,
+                       m, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_emit_view(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl, const RoundIn &in,
+                                  const RoundRun &run, const RoundSegs &g, const uint64_t *place, uint8_t *out,
+                                  hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    const uint64_t wgs = std::min<uint64_t>(std::max<uint64_t>((cap + 3) / 4, (r + 255) / 256), 4096);
+    hipLaunchKernelGGL(k_round_emit_view, dim3((uint32_t)wgs), dim3(256), 0, st, hdr, cap, r, kl, in, run, g, place,
+                       out);
     return hipGetLastError();
 }
 

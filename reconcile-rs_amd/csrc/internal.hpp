@@ -74,6 +74,41 @@ struct RoundIn {
     const uint64_t *remote;
     const uint8_t *bkeys, *fps, *bsums, *ssums;
 };
+// A round over the base + the delta run as they stand (no compaction first): the run's entries in
+// key order as columns (k_tier_run, the host tier's run copy) -- the contributions (cur - base)
+// with their block and super-block sums, the exclusive prefix sums of the count deltas
+// (live - in_base), the DeltaRec flags, the base ranks and G(64 k) = live keys <= entry 64 k.  A
+// place in the view is (b base rows, j run entries) below it: view rank b + cntp[j]; the sum
+// between two places is Σ base[b0, b1) + Σ contrib[j0, j1).
+struct RoundRun {
+    uint64_t n = 0;
+    const uint8_t *keys = nullptr;
+    const uint8_t *contrib = nullptr, *bsums = nullptr, *ssums = nullptr;
+    const int32_t *cntp = nullptr;
+    const uint8_t *flags = nullptr;
+    const uint32_t *brank = nullptr;
+    const uint64_t *gsamp = nullptr;
+    uint64_t nb = 0;
+};
+// every segment's view rank range, its places (place[4 j ..]: start b, start j, end b, end j)
+// and local aggregate, from the bound keys' base ranks (rank_b) and run ranks (rank_j)
+hipError_t launch_round_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const RoundIn &in,
+                                    const RoundRun &run, const RoundSegs &g, uint64_t *place, uint64_t r,
+                                    hipStream_t st);
+// the two-call path's step 1 over the view: bound keys interleaved (row 2 j start, 2 j + 1 end)
+hipError_t launch_resolve_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk, const uint8_t *ek,
+                               const RoundIn &in, const RoundRun &run, uint64_t r, uint64_t *lo, uint64_t *hi,
+                               uint64_t *aggs, hipStream_t st);
+// rank-range aggregates over the view (in: only bkeys, fps, bsums, ssums are read)
+hipError_t launch_range_query_view(const RoundIn &in, const RoundRun &run, uint32_t kl, uint64_t nv,
+                                   const uint64_t *lo, const uint64_t *hi, uint64_t q, uint64_t *out, hipStream_t st);
+// select over the view: the keys of ranks[t] (ranks NULL: first + t), each < nv
+hipError_t launch_select_view(const RoundRun &run, const uint8_t *bkeys, uint32_t kl, const uint64_t *ranks,
+                              uint64_t first, uint64_t m, uint8_t *out, hipStream_t st);
+// k_round_emit over the view: cut keys by select over base + run, children's sums over both
+hipError_t launch_round_emit_view(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl, const RoundIn &in,
+                                  const RoundRun &run, const RoundSegs &g, const uint64_t *place, uint8_t *out,
+                                  hipStream_t st);
 // large rounds: decisions (g.lo / g.hi / g.loc filled) -> hdr (zeroed by the caller) gets the
 // outcome counts; after the offsets are scanned, children and enumerations into `out`
 // (round_layout(hdr children, hdr enumerated, kl)), nothing when the children outnumber cap

@@ -1198,6 +1198,31 @@ struct rh_store {
         return tier_sync_writes && tier_fresh() && tier_epoch == base_epoch &&
                (m > tree_limit() || (tier.has_run() && m > RUN_FOLD_MAX));
     }
+    // The delta run as columns (k_tier_run: contributions with their block and super-block sums,
+    // the count deltas' exclusive prefix sums, flags, base ranks, select's index G(64 k)), formed
+    // on the device once per version of the contents: device reads over base + run use them in
+    // place (rh::RoundRun), the run copy adds the contributions' prefix sums and takes them down.
+    // trun_ver: the version they hold.
+    uint64_t trun_ver = ~0ull;
+    int run_columns() {
+        int rc;
+        const uint64_t n1 = nd;
+        if (trun_ver == version && trun_gs.p) return RH_OK;
+        trun_ver = ~0ull;
+        const uint64_t nbk = rh_num_blocks(n1), nsb = rh_num_superblocks(n1), ns = (n1 + 63) / 64;
+        if ((rc = trun_c.ensure(n1 * 32 + 64)) || (rc = trun_cnt.ensure(n1 + 16)) || (rc = trun_fl.ensure(n1 + 16)) ||
+            (rc = trun_br.ensure(n1 + 16)) || (rc = trun_bs.ensure(nbk * 32 + 32)) || (rc = trun_ss.ensure(nsb * 32 + 32)) ||
+            (rc = trun_cntp.ensure(n1 + 16)) || (rc = trun_gs.ensure(ns + 8)))
+            return rc;
+        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
+        RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
+        RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
+        RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
+        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        RH_HIP(rh::launch_tier_gsamp(trun_br.p, trun_cntp.p, trun_fl.p, n1, trun_gs.p, stream));
+        trun_ver = version;
+        return RH_OK;
+    }
     int tier_run_snapshot() {
         int rc;
         if (fail_point("tier.run_copy")) return fail(RH_ERR_OOM, "injected failure (tier run copy)");
@@ -1207,23 +1232,16 @@ struct rh_store {
             tier_version = version;
             return RH_OK;
         }
-        const uint64_t nbk = rh_num_blocks(n1), nsb = rh_num_superblocks(n1), ns = (n1 + 63) / 64,
-                       ns2 = (n1 + 4095) / 4096;
-        if ((rc = trun_c.ensure(n1 * 32 + 64)) || (rc = trun_cnt.ensure(n1 + 16)) || (rc = trun_fl.ensure(n1 + 16)) ||
-            (rc = trun_br.ensure(n1 + 16)) || (rc = trun_bs.ensure(nbk * 32 + 32)) || (rc = trun_ss.ensure(nsb * 32 + 32)) ||
+        const uint64_t ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096, nbk = rh_num_blocks(n1),
+                       nsb = rh_num_superblocks(n1);
+        if ((rc = run_columns()) || (rc = trun_smp.ensure(ns + ns2 + 8)) ||
             (rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64)) ||
-            (rc = trun_pre.ensure((n1 + 1) * 32 + 64)) || (rc = trun_cntp.ensure(n1 + 16)) ||
-            (rc = trun_smp.ensure(ns + ns2 + 8)) || (rc = trun_gs.ensure(ns + 8)))
+            (rc = trun_pre.ensure((n1 + 1) * 32 + 64)))
             return rc;
-        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
-        RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
-        RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
+        // the host walks prefix sums (HostTier::Run::prefix); the device kernels sum blocks instead
         RH_HIP(rh::launch_prefix(trun_c.p, n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, trun_pre.p, stream));
-        RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
-        if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
-        RH_HIP(rh::launch_tier_gsamp(trun_br.p, trun_cntp.p, trun_fl.p, n1, trun_gs.p, stream));
         try {
             auto fit = [](auto &v, size_t want) {  // headroom: the run grows batch by batch
                 if (v.capacity() < want) {
@@ -2096,15 +2114,56 @@ struct rh_store {
         if (!c.values && kept) RH_HIP(hipMemsetAsync(lastcols.values.p, 0, kept * vr, stream));
         return apply_device(lastcols.view(schema), lastops.p, kept, out);
     }
+    // Reads while a delta run is pending go to base + run as they stand (no O(n) compaction on a
+    // read): the run's columns (run_columns) and the base run, as the device kernels take them
+    int view_of(rh::RoundRun *run, rh::RoundIn *in) {
+        int rc;
+        if ((rc = run_columns())) return rc;
+        *run = rh::RoundRun{nd,
+                            dkeys[cd].p,
+                            trun_c.p,
+                            trun_bs.p,
+                            trun_ss.p,
+                            reinterpret_cast<const int32_t *>(trun_cntp.p),
+                            trun_fl.p,
+                            trun_br.p,
+                            trun_gs.p,
+                            nb};
+        *in = rh::RoundIn{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p};
+        return RH_OK;
+    }
+    // the run ranks of m keys (lower bounds among the delta run's keys)
+    hipError_t search_run(const uint8_t *keys, size_t m, uint32_t *out) {
+        return kops->search_sampled(dkeys[cd].p, nd, dsmp[cd].p, dsmp2[cd].p, keys, m, out, nullptr, stream,
+                                    rh::SearchTable{});
+    }
+    static constexpr uint64_t KEYS_VIEW_MAX = 1ull << 22;  // larger key dumps compact, then copy
+    // the keys of ranks [lo, hi) over base + run (hi - lo <= KEYS_VIEW_MAX)
+    int keys_view(uint64_t lo, uint64_t hi, void *host_out) {
+        int rc;
+        rh::RoundRun run;
+        rh::RoundIn din;
+        if ((rc = view_of(&run, &din)) || (rc = q_keys.ensure((hi - lo) * kl + 64))) return rc;
+        RH_HIP(rh::launch_select_view(run, bkeys[cb].p, (uint32_t)kl, nullptr, lo, hi - lo, q_keys.p, stream));
+        RH_HIP(hipMemcpyAsync(host_out, q_keys.p, (hi - lo) * kl, hipMemcpyDeviceToHost, stream));
+        return sync();
+    }
     int query(const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {  // rank ranges
         int rc;
         if (r == 0) return RH_OK;
-        if ((rc = compact())) return rc;
         if ((rc = q_lo.ensure(r)) || (rc = q_hi.ensure(r)) || (rc = q_out.ensure(r))) return rc;
         RH_HIP(hipMemcpyAsync(q_lo.p, lo, r * 8, hipMemcpyHostToDevice, stream));
         RH_HIP(hipMemcpyAsync(q_hi.p, hi, r * 8, hipMemcpyHostToDevice, stream));
-        RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, r,
-                                      reinterpret_cast<uint64_t *>(q_out.p), stream));
+        if (nd) {  // over base + run: select the bounds, sum between their places
+            rh::RoundRun run;
+            rh::RoundIn din;
+            if ((rc = view_of(&run, &din))) return rc;
+            RH_HIP(rh::launch_range_query_view(din, run, (uint32_t)kl, size(), q_lo.p, q_hi.p, r,
+                                               reinterpret_cast<uint64_t *>(q_out.p), stream));
+        } else {
+            RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, q_lo.p, q_hi.p, r,
+                                          reinterpret_cast<uint64_t *>(q_out.p), stream));
+        }
         RH_HIP(hipMemcpyAsync(out, q_out.p, r * sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
         return sync();
     }
@@ -2164,9 +2223,9 @@ struct rh_store {
     int resolve_staged(size_t r, const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys,
                        const uint64_t **lo, const uint64_t **hi, const rh_aggregate **aggs) {
         int rc;
-        if ((rc = compact())) return rc;
         const size_t kb = pad8(2 * r * kl), in_bytes = kb + pad8(2 * r), out_bytes = 16 * r + r * sizeof(rh_aggregate);
-        if ((rc = q_in.ensure(in_bytes + 64)) || (rc = q_res.ensure(out_bytes + 64)) || (rc = q_rank.ensure(2 * r)))
+        if ((rc = q_in.ensure(in_bytes + 64)) || (rc = q_res.ensure(out_bytes + 64)) || (rc = q_rank.ensure(2 * r)) ||
+            (nd && (rc = q_drank.ensure(2 * r))))
             return rc;
         stage_in.resize(in_bytes);
         stage_out.resize(out_bytes);
@@ -2183,9 +2242,18 @@ struct rh_store {
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, q_in.p, 2 * r, q_rank.p, nullptr, stream,
                                         base_table()));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
-        RH_HIP(rh::launch_resolve_bounds(q_rank.p, q_in.p + kb, q_in.p + kb + r, r, nb, d_lo, d_hi, stream));
-        // an inverted segment (hi < lo) is clamped to the empty range: ZERO
-        RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, d_lo, d_hi, r, d_agg, stream));
+        if (nd) {  // ranks in the run as well; view ranks and sums over base + run
+            rh::RoundRun run;
+            rh::RoundIn din;
+            if ((rc = view_of(&run, &din))) return rc;
+            RH_HIP(search_run(q_in.p, 2 * r, q_drank.p));
+            RH_HIP(rh::launch_resolve_view(q_rank.p, q_drank.p, q_in.p + kb, q_in.p + kb + r, din, run, r, d_lo, d_hi,
+                                           d_agg, stream));
+        } else {
+            RH_HIP(rh::launch_resolve_bounds(q_rank.p, q_in.p + kb, q_in.p + kb + r, r, nb, d_lo, d_hi, stream));
+            // an inverted segment (hi < lo) is clamped to the empty range: ZERO
+            RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, d_lo, d_hi, r, d_agg, stream));
+        }
         RH_HIP(hipMemcpyAsync(stage_out.data(), q_res.p, out_bytes, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
         *lo = reinterpret_cast<const uint64_t *>(stage_out.data());
@@ -2209,9 +2277,9 @@ struct rh_store {
     int split_staged(size_t m, const uint64_t *sel, size_t q, const uint64_t *lo, const uint64_t *hi,
                      const uint8_t **keys, const rh_aggregate **aggs) {
         int rc;
-        if ((rc = compact())) return rc;
+        const uint64_t nv = size();
         for (size_t i = 0; i < m; i++)
-            if (sel[i] >= nb) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+            if (sel[i] >= nv) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
         const size_t in_bytes = 8 * (m + 2 * q), kb = pad8(m * kl), out_bytes = kb + q * sizeof(rh_aggregate);
         if ((rc = q_in.ensure(in_bytes + 64)) || (rc = q_res.ensure(out_bytes + 64))) return rc;
         stage_in.resize(in_bytes);
@@ -2222,10 +2290,19 @@ struct rh_store {
         memcpy(h + m + q, hi, q * 8);
         RH_HIP(hipMemcpyAsync(q_in.p, h, in_bytes, hipMemcpyHostToDevice, stream));
         const uint64_t *d_sel = reinterpret_cast<const uint64_t *>(q_in.p), *d_lo = d_sel + m, *d_hi = d_lo + q;
-        if (m) RH_HIP(rh::launch_gather_keys(bkeys[cb].p, (uint32_t)kl, d_sel, m, q_res.p, stream));
-        if (q)
-            RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, d_lo, d_hi, q,
-                                          reinterpret_cast<uint64_t *>(q_res.p + kb), stream));
+        if (nd) {  // select and sums over base + run
+            rh::RoundRun run;
+            rh::RoundIn din;
+            if ((rc = view_of(&run, &din))) return rc;
+            RH_HIP(rh::launch_select_view(run, bkeys[cb].p, (uint32_t)kl, d_sel, 0, m, q_res.p, stream));
+            RH_HIP(rh::launch_range_query_view(din, run, (uint32_t)kl, nv, d_lo, d_hi, q,
+                                               reinterpret_cast<uint64_t *>(q_res.p + kb), stream));
+        } else {
+            if (m) RH_HIP(rh::launch_gather_keys(bkeys[cb].p, (uint32_t)kl, d_sel, m, q_res.p, stream));
+            if (q)
+                RH_HIP(rh::launch_range_query(bfps[cb].p, bsums.p, ssums.p, nb, d_lo, d_hi, q,
+                                              reinterpret_cast<uint64_t *>(q_res.p + kb), stream));
+        }
         RH_HIP(hipMemcpyAsync(stage_out2.data(), q_res.p, out_bytes, hipMemcpyDeviceToHost, stream));
         if ((rc = sync())) return rc;
         *keys = stage_out2.data();
@@ -2260,16 +2337,24 @@ struct rh_store {
         *ch = rh_segments{};
         *en = rh_segments{};
         if (r == 0) return RH_OK;
-        if ((rc = compact())) return rc;
-        const uint64_t n = nb;                     // compacted: the base run is the whole store
+        // a pending delta run stays where it is: the round reads base + run through the run's
+        // columns (no O(n) compaction on a read)
+        const bool view = nd != 0;
+        rh::RoundRun run{};
+        if (view) {
+            rh::RoundIn unused;
+            if ((rc = view_of(&run, &unused))) return rc;
+        }
+        const uint64_t n = size();                 // live keys of base + run
         const uint64_t b = param < 2 ? 2 : param;  // FanOut::new
         // device input: start kinds, end kinds, start keys then end keys (searched as one run of
         // 2r queries), remote aggregates
         const size_t o_ek = pad16(r), o_sk = o_ek + pad16(r), o_ekeys = o_sk + r * kl,
                      o_rem = pad16(o_ekeys + r * kl), in_bytes = o_rem + r * sizeof(rh_aggregate);
         uint64_t cap = r * std::min<uint64_t>(b, 16);
-        if ((rc = r_in.ensure(in_bytes + 64)) || (rc = r_kind.ensure(r)) || (rc = r_seg.ensure(14 * r)) ||
-            (rc = q_rank.ensure(2 * r)) || (rc = r_out.ensure(rh::round_layout(cap, r, kl).end)))
+        if ((rc = r_in.ensure(in_bytes + 64)) || (rc = r_kind.ensure(r)) || (rc = r_seg.ensure(18 * r)) ||
+            (rc = q_rank.ensure(2 * r)) || (view && (rc = q_drank.ensure(2 * r))) ||
+            (rc = r_out.ensure(rh::round_layout(cap, r, kl).end)))
             return rc;
         const struct { const void *src; size_t off, bytes; } parts[5] = {
             {in.start_kinds, 0, r}, {in.end_kinds, o_ek, r}, {in.start_keys, o_sk, r * kl},
@@ -2277,7 +2362,7 @@ struct rh_store {
         // tiny rounds read their segments from, and write the round into, page-locked host memory
         // (mapped into the device's address space): no copy command either way
         const size_t worst = rh::round_layout(cap, r, kl).end;
-        bool zero_copy = r <= rh::round_tiny_max() && in_bytes <= kRoundSmall && worst <= kRoundSmall;
+        bool zero_copy = !view && r <= rh::round_tiny_max() && in_bytes <= kRoundSmall && worst <= kRoundSmall;
         const uint8_t *in_p = r_in.p;
         uint8_t *out_p = r_out.p;
         if (in_bytes <= kRoundSmall) {
@@ -2318,28 +2403,36 @@ struct rh_store {
         const uint8_t *d_sk = in_p, *d_ek = in_p + o_ek, *d_skeys = in_p + o_sk, *d_ekeys = in_p + o_ekeys;
         const uint64_t *d_rem = reinterpret_cast<const uint64_t *>(in_p + o_rem);
         uint64_t *lo = r_seg.p, *hi = lo + r, *loc = hi + r, *st = loc + 5 * r, *si = st + r, *ei = si + r,
-                 *nch = ei + r, *choff = nch + r, *nen = choff + r, *enoff = nen + r;
+                 *nch = ei + r, *choff = nch + r, *nen = choff + r, *enoff = nen + r, *place = enoff + r;
         const rh::RoundSegs g{r_kind.p, lo, hi, loc, st, si, ei, nch, choff, nen, enoff};
         const rh::RoundIn din{d_sk, d_ek, d_skeys, d_ekeys, d_rem, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p};
         uint64_t *hdr = reinterpret_cast<uint64_t *>(r_out.p);
         const int sq = policy == RH_POLICY_SQRT_FAN_OUT;
-        if (n)
-            RH_HIP(kops->search_sampled(bkeys[cb].p, n, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
+        if (nb)
+            RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
                                         base_table()));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
-        if (r <= rh::round_tiny_max()) {
+        auto emit = [&](uint64_t c) {
+            return view ? rh::launch_round_emit_view(hdr, c, r, (uint32_t)kl, din, run, g, place, r_out.p, stream)
+                        : rh::launch_round_emit(hdr, c, r, (uint32_t)kl, din, g, r_out.p, stream);
+        };
+        if (view) {  // the bound keys' ranks in the run as well; places and sums over both
+            RH_HIP(search_run(d_skeys, 2 * r, q_drank.p));
+            RH_HIP(rh::launch_round_bounds_view(q_rank.p, q_drank.p, din, run, g, place, r, stream));
+        }
+        if (!view && r <= rh::round_tiny_max()) {
             RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, out_p, stream));
         } else if (r <= rh::round_small_max()) {
-            RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
+            if (!view) RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
             RH_HIP(rh::launch_round_plan_scan(din, g, r, n, sq, b, r_out.p, stream));
-            RH_HIP(rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
+            RH_HIP(emit(cap));
         } else {
-            RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
+            if (!view) RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
             RH_HIP(hipMemsetAsync(hdr, 0, 64, stream));
             RH_HIP(rh::launch_round_plan(g, d_rem, r, n, sq, b, hdr, stream));
             RH_HIP(rh::launch_exclusive_scan_u64(nch, choff, r, scratch, stream));
             RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
-            RH_HIP(rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
+            RH_HIP(emit(cap));
         }
         uint64_t h[5];
         if (zero_copy) {
@@ -2365,7 +2458,7 @@ struct rh_store {
             pr_out.resize(L.end);
             hdr = reinterpret_cast<uint64_t *>(r_out.p);
             RH_HIP(hipMemcpyAsync(hdr, pr_out.data(), 64, hipMemcpyHostToDevice, stream));
-            RH_HIP(rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
+            RH_HIP(emit(cap));
         }
         if (regrow || worst > kRoundSmall) {
             pr_out.resize(L.end);
@@ -2571,6 +2664,7 @@ int rh_store_keys(rh_store *s, uint64_t lo, uint64_t hi, void *host_out) {
         return RH_OK;
     }
     RH_HIP(hipSetDevice(s->device));
+    if (s->nd && hi - lo <= rh_store::KEYS_VIEW_MAX) return s->keys_view(lo, hi, host_out);
     if ((rc = s->compact())) return rc;
     RH_HIP(hipMemcpyAsync(host_out, s->bkeys[s->cb].p + lo * s->kl, (hi - lo) * s->kl, hipMemcpyDeviceToHost,
                           s->stream));

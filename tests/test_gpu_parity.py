@@ -7,6 +7,8 @@ tests/timestamp_wire_format.rs:105-121), fold-of-lift oracles
 (tests/proptest_fingerprint_tree_map/btreemap_oracle.rs:132-162,
 rsos/src/fingerprint_tree_map/tests/aggregate.rs:59-78), duplicate delivery (:195-231).
 """
+import types
+
 import numpy as np
 import pytest
 
@@ -720,10 +722,40 @@ def test_store_lsm_policies_agree(gpu, oracle_lib):
         assert (lazy.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
         assert (eager.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
         assert (res.ranks(probes.view(np.uint8).reshape(-1, 8)) == want).all()
-    # a rank-order query compacts the lazy store; afterwards both agree row for row
+        # rank-order reads over base + delta run as they stand (select over both, no compaction):
+        # select, key dumps, rank-range aggregates (inverted and beyond-the-end ones too) and the
+        # two-call round's steps
+        nl = len(ks)
+        sel = sorted({0, nl - 1} | {int(x) for x in rng.integers(0, nl, 40)})
+        lo_r, hi_r = rng.integers(0, nl + 3, 40), rng.integers(0, nl + 3, 40)
+
+        def want_agg(a, b):
+            b = min(int(b), nl)
+            a = min(int(a), b)
+            return b - a, (pref[b] - pref[a]) % M256
+        ka, kb = sorted(int(x) for x in rng.integers(0, 2**40, 2))
+        segs = [types.SimpleNamespace(start=ka, end=kb), types.SimpleNamespace(start=kb, end=ka),
+                types.SimpleNamespace(start=None, end=ka), types.SimpleNamespace(start=kb, end=None)]
+        for st in (lazy, res):
+            assert [st.select(r) for r in sel[:8]] == [int(ks[r]) for r in sel[:8]]
+            got = st.aggregates_ranks(lo_r, hi_r)
+            assert [(g.size, g.fingerprint.to_int()) for g in got] == [want_agg(a, b) for a, b in zip(lo_r, hi_r)]
+            ra, rb = int(np.searchsorted(ks, ka)), int(np.searchsorted(ks, kb))
+            assert [k for k, _ in st.enumerate(KeyRange(ka, kb))] == [int(k) for k in ks[ra:rb]]
+            keys_out, aggs = st.split_segments(sel, lo_r, hi_r)
+            assert keys_out == [int(ks[r]) for r in sel]
+            assert [(g.size, g.fingerprint.to_int()) for g in aggs] == [want_agg(a, b) for a, b in zip(lo_r, hi_r)]
+            lo, hi, la = st.resolve_segments(segs)
+            assert list(lo) == [ra, rb, 0, rb] and list(hi) == [rb, ra, ra, nl]
+            assert [(g.size, g.fingerprint.to_int()) for g in la] == \
+                [want_agg(ra, rb), (0, 0), want_agg(0, ra), want_agg(rb, nl)]
+        assert lazy.stats()["delta_rows"] > 0 and lazy.stats()["compactions"] == 0
+    # the reads left the lazy store's delta run in place; the fingerprint dump compacts it, and
+    # afterwards the stores agree row for row
     assert lazy.select(100) == int(ks[100])
-    assert lazy.stats()["delta_rows"] == 0
+    assert lazy.stats()["delta_rows"] > 0
     assert np.array_equal(lazy.fingerprints(), eager.fingerprints())
+    assert lazy.stats()["delta_rows"] == 0
     assert np.array_equal(res.fingerprints(), eager.fingerprints())
     lazy.close()
     eager.close()

@@ -249,6 +249,66 @@ def _dated_sets(seed, n_common, n_a, n_b, n_mod):
     return keys, cols(a_idx), cols(b_idx, bump=mod), a_idx[n_common:], b_idx[n_common:], sorted(mod)
 
 
+def _cat(*cols):
+    return {k: np.concatenate([c[k] for c in cols]) for k in cols[0]}
+
+
+def _rows(cols, sel):
+    return {k: v[sel] for k, v in cols.items()}
+
+
+def _store_via_delta(schema, c, seed):
+    """A GPU store holding exactly c's records with its delta run pending: a different base
+    (withheld rows, extra rows, stale versions), then two batches -- the withheld rows inserted,
+    the extra rows deleted, the stale rows overwritten, and keys inserted by the first batch and
+    deleted by the second.  Rounds must read base + run without compacting it."""
+    from rsos_hip import GpuFingerprintStore
+    rng = np.random.default_rng(seed)
+    n = len(c["keys"])
+    idx = rng.permutation(n)
+    nw, no = max(n // 40, 4), max(n // 60, 4)
+    w, o = np.sort(idx[:nw]), np.sort(idx[nw:nw + no])
+    have = {k.tobytes() for k in c["keys"]}
+    fresh = []
+    while len(fresh) < 2 * nw:
+        k = rng.integers(0, 256, 16, dtype=np.uint8)
+        if k.tobytes() not in have:
+            have.add(k.tobytes())
+            fresh.append(k)
+    fresh = np.array(fresh)
+
+    def fresh_cols(ks):
+        m = len(ks)
+        return {"keys": ks, "values": rng.integers(0, 256, (m, 64), dtype=np.uint8),
+                "phys": np.full(m, 1_600_000_000_000, np.uint64), "logical": np.zeros(m, np.uint32),
+                "node": np.ones(m, np.uint64), "tags": np.zeros(m, np.uint8)}
+    keep = np.ones(n, bool)
+    keep[w] = False
+    base = _rows(c, keep)
+    stale = {k: v.copy() for k, v in c.items()}
+    stale["values"][o] ^= 0x5A
+    stale["phys"][o] -= 5
+    kept_idx = np.flatnonzero(keep)
+    base["values"], base["phys"] = stale["values"][kept_idx], stale["phys"][kept_idx]
+    xs, ys = fresh_cols(fresh[:nw]), fresh_cols(fresh[nw:])  # X: in the base; Y: batch 1 only
+    base = _cat(base, xs)
+    order = sorted(range(len(base["keys"])), key=lambda i: base["keys"][i].tobytes())
+    base = _rows(base, np.array(order))
+    st = GpuFingerprintStore(schema)
+    st.load_bulk(base)
+    hw, ho, hx = nw // 2, no // 2, nw // 2
+    b1 = _cat(_rows(c, w[:hw]), _rows(c, o[:ho]), _rows(xs, slice(0, hx)), ys)
+    ops1 = np.concatenate([np.zeros(hw + ho, np.uint8), np.ones(hx, np.uint8), np.zeros(nw, np.uint8)])
+    b2 = _cat(_rows(c, w[hw:]), _rows(c, o[ho:]), _rows(xs, slice(hx, None)), ys)
+    ops2 = np.concatenate([np.zeros(nw - hw + no - ho, np.uint8), np.ones(nw - hx, np.uint8),
+                           np.ones(nw, np.uint8)])
+    st.apply(b1, ops1)
+    st.apply(b2, ops2)
+    s = st.stats()
+    assert s["delta_rows"] > 0 and s["compactions"] == 0 and st.size() == n
+    return st
+
+
 def _gpu_and_oracle(schema, c):
     from rsos_hip import GpuFingerprintStore
     st = GpuFingerprintStore(schema)
@@ -297,7 +357,8 @@ def test_gpu_reconciliation_rounds_match_oracle(gpu, oracle_lib, policy, native)
 @pytest.mark.gpu
 def test_gpu_round_edge_segments(gpu, oracle_lib):
     """Inverted, empty, beyond-the-end and unbounded segments, u64 keys, an empty store, and a
-    store with a pending delta run (the round compacts it first: one snapshot)."""
+    store with a pending delta run (the one-call round reads base + run as they stand; the
+    two-call path compacts first)."""
     from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
     rng = np.random.default_rng(9)
     keys = np.unique(rng.integers(0, 2**40, 5000, dtype=np.uint64))
@@ -306,7 +367,8 @@ def test_gpu_round_edge_segments(gpu, oracle_lib):
     schema = RecordSchema.plain("u64", "u64")
     st = GpuFingerprintStore(schema)
     st.load_bulk({"keys": keys[:-100].view(np.uint8).reshape(-1, 8), "values": vals[:-100].view(np.uint8).reshape(-1, 8)})
-    # the last 100 records arrive as a batch: they sit in the delta run until the round compacts
+    # the last 100 records arrive as a batch: they sit in the delta run (the one-call round reads
+    # it in place, the two-call path compacts it)
     st.apply({"keys": keys[-100:].view(np.uint8).reshape(-1, 8), "values": vals[-100:].view(np.uint8).reshape(-1, 8)},
              np.zeros(100, np.uint8))
     recs = O.Records(O.Schema(O.KEY_U64, 8, O.VAL_U64, 8, O.REC_PLAIN, 0), keys.view(np.uint8).reshape(n, 8),
@@ -529,3 +591,64 @@ def test_gpu_native_round_large_batches(gpu, policy):
     assert widest > 4000 and k > 3
     ga.close()
     gb.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["fixed16", "sqrt", "fixed2"])
+def test_gpu_rounds_over_pending_delta_run_match_oracle(gpu, oracle_lib, policy):
+    """Both replicas reach their contents through batches that stay in the delta run (inserts,
+    deletes of base keys, overwrites, a key inserted then deleted): the one-call device round reads
+    base + run in place (select over both, sums over both) and must equal the literal driver over
+    the final contents round by round -- without compacting either store."""
+    from rsos_hip import RecordSchema, rbsr as R
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(11, 20_000, 60, 45, 30)
+    ga, gb = _store_via_delta(schema, ca, 1), _store_via_delta(schema, cb, 2)
+    _, oa = _gpu_and_oracle(schema, ca)
+    _, ob = _gpu_and_oracle(schema, cb)
+    pol, decide = {"fixed16": (R.FixedFanOut(16), OR.fixed_fan_out(16)), "sqrt": (R.SqrtFanOut(), OR.sqrt_fan_out),
+                   "fixed2": (R.FixedFanOut(2), OR.fixed_fan_out(2))}[policy]
+    want = reconcile(oa, ob, lambda v, act, ch, en: OR.protocol_round(v, decide, act, ch, en), OR.initial_ranges)
+    got = reconcile(ga, gb, lambda v, act, ch, en: _outcome(R.protocol_round_with_policy(v, pol, act, ch, en)),
+                    R.initial_ranges)
+    assert len(got[0]) == len(want[0]) > 2
+    for (gc, ge, go), (wc, we, wo) in zip(got[0], want[0]):
+        assert go == wo and ge == we and gc == wc
+    for g in (ga, gb):
+        s = g.stats()
+        assert s["delta_rows"] > 0 and s["compactions"] == 0
+        g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["fixed16", "sqrt"])
+def test_gpu_large_rounds_over_pending_delta_run(gpu, policy):
+    """Rounds of thousands of segments over a replica whose delta run is pending equal the same
+    rounds over a freshly loaded replica with the same contents (the base-only path, tested above
+    against the literal driver), round by round, and leave the delta run in place."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(23, 200_000, 1000, 1000, 1000)
+    va = _store_via_delta(schema, ca, 3)
+    fa = GpuFingerprintStore(schema)
+    fa.load_bulk(ca)
+    gb = GpuFingerprintStore(schema)
+    gb.load_bulk(cb)
+    pol = {"fixed16": R.FixedFanOut(16), "sqrt": R.SqrtFanOut()}[policy]
+    active, k, widest = R.initial_segments(gb), 0, 0
+    while len(active):
+        if k % 2 == 0:
+            widest = max(widest, len(active))
+            ch, en, o = R.protocol_round_segments(va, pol, active)
+            wch, wen, wo = R.protocol_round_segments(fa, pol, active)
+            assert _outcome(o) == _outcome(wo)
+            assert _norm(ch.items(schema)) == _norm(wch.items(schema))
+            assert [en.bounds(schema, i) for i in range(en.n)] == [wen.bounds(schema, i) for i in range(wen.n)]
+        else:
+            ch, en, o = R.protocol_round_segments(gb, pol, active)
+        active, k = ch, k + 1
+    assert widest > 1024 and k > 3
+    s = va.stats()
+    assert s["delta_rows"] > 0 and s["compactions"] == 0
+    for g in (va, fa, gb):
+        g.close()

@@ -2362,7 +2362,7 @@ struct rh_store {
         // tiny rounds read their segments from, and write the round into, page-locked host memory
         // (mapped into the device's address space): no copy command either way
         const size_t worst = rh::round_layout(cap, r, kl).end;
-        bool zero_copy = !view && r <= rh::round_tiny_max() && in_bytes <= kRoundSmall && worst <= kRoundSmall;
+        bool zero_copy = r <= rh::round_tiny_max() && in_bytes <= kRoundSmall && worst <= kRoundSmall;
         const uint8_t *in_p = r_in.p;
         uint8_t *out_p = r_out.p;
         if (in_bytes <= kRoundSmall) {
@@ -2412,9 +2412,10 @@ struct rh_store {
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
                                         base_table()));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
-        auto emit = [&](uint64_t c) {
-            return view ? rh::launch_round_emit_view(hdr, c, r, (uint32_t)kl, din, run, g, place, r_out.p, stream)
-                        : rh::launch_round_emit(hdr, c, r, (uint32_t)kl, din, g, r_out.p, stream);
+        // emit reads the header `hd` that the plan wrote and writes the round into `o`
+        auto emit = [&](uint64_t c, const uint64_t *hd, uint8_t *o) {
+            return view ? rh::launch_round_emit_view(hd, c, r, (uint32_t)kl, din, run, g, place, o, stream)
+                        : rh::launch_round_emit(hd, c, r, (uint32_t)kl, din, g, o, stream);
         };
         if (view) {  // the bound keys' ranks in the run as well; places and sums over both
             RH_HIP(search_run(d_skeys, 2 * r, q_drank.p));
@@ -2423,16 +2424,17 @@ struct rh_store {
         if (!view && r <= rh::round_tiny_max()) {
             RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, out_p, stream));
         } else if (r <= rh::round_small_max()) {
+            // (a tiny round over base + run: straight into the mapped output, header first)
             if (!view) RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
-            RH_HIP(rh::launch_round_plan_scan(din, g, r, n, sq, b, r_out.p, stream));
-            RH_HIP(emit(cap));
+            RH_HIP(rh::launch_round_plan_scan(din, g, r, n, sq, b, out_p, stream));
+            RH_HIP(emit(cap, reinterpret_cast<const uint64_t *>(out_p), out_p));
         } else {
             if (!view) RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
             RH_HIP(hipMemsetAsync(hdr, 0, 64, stream));
             RH_HIP(rh::launch_round_plan(g, d_rem, r, n, sq, b, hdr, stream));
             RH_HIP(rh::launch_exclusive_scan_u64(nch, choff, r, scratch, stream));
             RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
-            RH_HIP(emit(cap));
+            RH_HIP(emit(cap, hdr, r_out.p));
         }
         uint64_t h[5];
         if (zero_copy) {
@@ -2458,7 +2460,7 @@ struct rh_store {
             pr_out.resize(L.end);
             hdr = reinterpret_cast<uint64_t *>(r_out.p);
             RH_HIP(hipMemcpyAsync(hdr, pr_out.data(), 64, hipMemcpyHostToDevice, stream));
-            RH_HIP(emit(cap));
+            RH_HIP(emit(cap, hdr, r_out.p));
         }
         if (regrow || worst > kRoundSmall) {
             pr_out.resize(L.end);

@@ -279,9 +279,9 @@ int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
  * refreshes the base copy: the device compacts and a copy stream brings the new base down into a
  * second page-locked set.  By default (RSOS_HIP_TIER_SYNC unset or 1) the write or load that
  * starts a refresh waits for it, so every question is answered from a fresh tier; with
- * RSOS_HIP_TIER_SYNC=0 writes never wait -- a stale tier hands the questions to the device (its
- * delta run is then empty: no question compacts) and batches applied during a copy are logged and
- * replayed into it.  No question waits for an O(n) copy under either policy.
+ * RSOS_HIP_TIER_SYNC=0 writes never wait -- a stale tier hands the questions to the device (which
+ * reads base + delta run in place: no question compacts) and batches applied during a copy are
+ * logged and replayed into it.  No question waits for an O(n) copy under either policy.
  * Stats (nullable): base rows and delta entries (tree entries + run-copy entries) of a fresh tier
  * (0, 0 when stale), copies taken from the device (base refreshes and run copies) and batch folds
  * so far.                                                                                        */
@@ -329,8 +329,10 @@ int rh_store_apply_device_many(rh_store *store, const rh_columns *dev_cols, cons
 
 /* LSM maintenance.  A batch merges into a sorted signed-delta run (O(batch + delta)); the delta
  * run merges into the base run when it exceeds max(base / divisor, min_rows) rows (default
- * 6, 65536), and before rank-order queries (select, rank-range aggregates, key / fingerprint
- * dumps).  Results never depend on the policy, only timings do.                            */
+ * 6, 65536), and before a fingerprint dump or a key dump of more than 2^22 rows.  Every other
+ * read -- rank / select / keys, aggregates by rank or by key, resolve / split and protocol rounds --
+ * reads base + delta run in place (select over both through the run's count prefix), so no read
+ * pays an O(n) merge.  Results never depend on the policy, only timings do.               */
 int rh_store_compact(rh_store *store);
 int rh_store_set_compaction(rh_store *store, uint64_t divisor, uint64_t min_rows);
 /* Capacity for `rows` resident rows fed batches of up to `batch_rows` rows (the device-side

@@ -993,7 +993,7 @@ struct rh_store {
     uint64_t stale_questions = 0;  // questions the device answered since the last batch
     uint64_t rf_version = 0, rf_epoch = 0, rf_nb = 0;
     hipStream_t cstream = nullptr;
-    hipEvent_t rf_ready = nullptr, rf_ev = nullptr;
+    hipEvent_t rf_ready = nullptr, rf_ev = nullptr, rf_kdone = nullptr;
     // the batches applied while the copy is in flight, as mode-1 rows against its base (which is
     // the device's base until the next compaction, and no compaction runs while a copy is in
     // flight): replayed into the new copy's tree when it is swapped in
@@ -1022,6 +1022,7 @@ struct rh_store {
             RH_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
             RH_HIP(hipEventCreateWithFlags(&rf_ready, hipEventDisableTiming));
             RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
+            RH_HIP(hipEventCreateWithFlags(&rf_kdone, hipEventDisableTiming));
         }
         const uint64_t n = nb, nbk = rh_num_blocks(n), ns = rh_num_superblocks(n), nsmp = (n + 63) / 64,
                        nsmp2 = (n + 4095) / 4096;  // the samples' index (host_tier.hpp samp2)
@@ -1044,13 +1045,18 @@ struct rh_store {
         } catch (const std::bad_alloc &) {
             return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
         }
-        if (n) {
-            RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, stream));
-            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 64, tier_dsmp.p, stream));
-            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 4096, tier_dsmp.p + nsmp, stream));
-        }
+        // the prefix scan and the samples run on the copy stream too, behind the compaction: the
+        // store's own stream goes on at once (a question answered by the device meanwhile is not
+        // queued behind ~1-2 ms of scans at 10^8 rows); the next compaction, which rewrites the
+        // base's block sums they read, waits for them (rf_kdone)
         RH_HIP(hipEventRecord(rf_ready, stream));
         RH_HIP(hipStreamWaitEvent(cstream, rf_ready, 0));
+        if (n) {
+            RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, cstream));
+            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 64, tier_dsmp.p, cstream));
+            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 4096, tier_dsmp.p + nsmp, cstream));
+        }
+        RH_HIP(hipEventRecord(rf_kdone, cstream));
         if (n) {
             RH_HIP(hipMemcpyAsync(S.keys.data(), bkeys[cb].p, n * kl, hipMemcpyDeviceToHost, cstream));
             RH_HIP(hipMemcpyAsync(S.prefix.data(), tier_dpre.p, (n + 1) * 32, hipMemcpyDeviceToHost, cstream));
@@ -1683,6 +1689,8 @@ struct rh_store {
                 if ((rc = settle())) return rc;
             } else {
                 rf_log_ok = false;
+                // the merge rewrites the base's block sums, which the copy's prefix scan reads
+                RH_HIP(hipStreamWaitEvent(stream, rf_kdone, 0));
             }
         }
         if ((rc = cfps.ensure(nd * 32 + 64)) || (rc = cops.ensure(nd + 64))) return rc;
@@ -2497,7 +2505,8 @@ struct rh_store {
         if (cstream) (void)hipStreamDestroy(cstream);
         if (rf_ready) (void)hipEventDestroy(rf_ready);
         if (rf_ev) (void)hipEventDestroy(rf_ev);
-        cstream = nullptr, rf_ready = rf_ev = nullptr, rf_on = false;
+        if (rf_kdone) (void)hipEventDestroy(rf_kdone);
+        cstream = nullptr, rf_ready = rf_ev = rf_kdone = nullptr, rf_on = false;
         snap.release();
         sbsums.release(); sssums.release(); sbsmp.release(); sbsmp2.release(); sbtab.release(); sbtabp.release();
         stot.release(); snap_words.release(); snap_hdr.release();

@@ -697,16 +697,14 @@ __device__ __forceinline__ void view_range_fp(const RoundIn &in, const RoundRun 
     fp_add256(fp, d);
 }
 
-// Every segment's view rank range [l, h), its places and its aggregate (ZERO when inverted), one
-// wave each.  The bound keys' ranks are rank_x[ia * j] / rank_x[ib * j + off] (a round: starts then
+// Segment j's view rank range [l, h), its places and its aggregate (ZERO when inverted), by one
+// wave.  The bound keys' ranks are rank_x[ia * j] / rank_x[ib * j + off] (a round: starts then
 // ends; the two-call path: interleaved)
-__global__ __launch_bounds__(256) void k_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk,
-                                                     const uint8_t *ek, RoundIn in, RoundRun R, uint64_t r,
-                                                     uint32_t ia, uint32_t ib, uint64_t off, uint64_t *lo_out,
-                                                     uint64_t *hi_out, uint64_t *agg_out, uint64_t *place) {
-    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63;
-    if (j >= r) return;  // uniform per wave
+__device__ __forceinline__ void bounds_view_one(uint64_t j, uint32_t lane, const uint32_t *rank_b,
+                                                const uint32_t *rank_j, const uint8_t *sk, const uint8_t *ek,
+                                                const RoundIn &in, const RoundRun &R, uint32_t ia, uint32_t ib,
+                                                uint64_t off, uint64_t *lo_out, uint64_t *hi_out, uint64_t *agg_out,
+                                                uint64_t *place) {
     const uint64_t qs = ia * j, qe = ib * j + off;
     const uint64_t bs = sk[j] ? rank_b[qs] : 0, js = sk[j] ? rank_j[qs] : 0;
     const uint64_t be = ek[j] ? rank_b[qe] : R.nb, je = ek[j] ? rank_j[qe] : R.n;
@@ -729,6 +727,16 @@ __global__ __launch_bounds__(256) void k_bounds_view(const uint32_t *rank_b, con
         o[3] = fp[3];
         o[4] = h > l ? h - l : 0;
     }
+}
+
+// every segment's bounds over the view, one wave each
+__global__ __launch_bounds__(256) void k_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk,
+                                                     const uint8_t *ek, RoundIn in, RoundRun R, uint64_t r,
+                                                     uint32_t ia, uint32_t ib, uint64_t off, uint64_t *lo_out,
+                                                     uint64_t *hi_out, uint64_t *agg_out, uint64_t *place) {
+    const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= r) return;  // uniform per wave
+    bounds_view_one(j, threadIdx.x & 63, rank_b, rank_j, sk, ek, in, R, ia, ib, off, lo_out, hi_out, agg_out, place);
 }
 
 // Rank-range aggregates over the view ([lo, hi) clamped as k_range_query_wave clamps), one wave each
@@ -926,6 +934,55 @@ __global__ __launch_bounds__(1024) void k_round_small(const uint32_t *rank, Roun
     for (uint64_t c = w; c < nc; c += 16) {
         const uint64_t j = round_owner(g.choff, r, c);
         round_emit_child(c, j, c - g.choff[j], L, kl, lane, in, g, out);
+    }
+}
+// A tiny round over base + delta run in one launch after the two searches: k_round_small's
+// shape with the view's bounds (bounds_view_one) and children (round_emit_child_view)
+__global__ __launch_bounds__(1024) void k_round_small_view(const uint32_t *rank_b, const uint32_t *rank_j, RoundIn in,
+                                                           RoundRun R, RoundSegs g, uint64_t *place, uint64_t r,
+                                                           uint64_t n, int sqrt_policy, uint64_t b, uint64_t cap,
+                                                           uint32_t kl, uint8_t *out) {
+    __shared__ uint64_t wsum[2][16], tot[2];
+    __shared__ unsigned long long cnt[5];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t < 5) cnt[t] = 0;
+    const bool mine = t < r;
+    for (uint64_t j = w; j < r; j += 16)
+        bounds_view_one(j, lane, rank_b, rank_j, in.sk, in.ek, in, R, 1u, 1u, r, g.lo, g.hi, g.loc, place);
+    __syncthreads();
+    RoundSeg d{3, 0, 0, 0, 0, 0};
+    if (mine) {
+        d = round_decide(g.lo[t], g.hi[t], g.loc + 5 * t, in.remote + 5 * t, n, sqrt_policy, b);
+        g.kind[t] = (uint8_t)d.kind;
+        g.stride[t] = d.stride;
+        g.si[t] = d.si;
+        g.ei[t] = d.ei;
+        g.nch[t] = d.children;
+        g.nen[t] = d.enums;
+        atomicAdd(&cnt[d.kind == 3 ? 4 : d.kind], 1ull);
+    }
+    const uint64_t co = block_exclusive_scan(d.children, wsum[0], &tot[0]);
+    const uint64_t eo = block_exclusive_scan(d.enums, wsum[1], &tot[1]);
+    const uint64_t nc = tot[0], ne = tot[1];
+    if (mine) {
+        g.choff[t] = co;
+        g.enoff[t] = eo;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t *hdr = reinterpret_cast<uint64_t *>(out);
+        hdr[0] = cnt[0];
+        hdr[1] = ne;
+        hdr[2] = cnt[2];
+        hdr[3] = nc;
+        hdr[4] = cnt[4];
+    }
+    if (nc > cap) return;  // uniform
+    const RoundLayout L = round_layout(nc, ne, kl);
+    if (mine && d.enums) round_emit_enum(t, eo, L, kl, in, g, out);
+    for (uint64_t c = w; c < nc; c += 16) {
+        const uint64_t j = round_owner(g.choff, r, c);
+        round_emit_child_view(c, j, c - g.choff[j], L, kl, lane, in, R, g, place, out);
     }
 }
 __global__ __launch_bounds__(1024) void k_round_plan_scan(RoundIn in, RoundSegs g, uint64_t r, uint64_t n,
@@ -1289,6 +1346,16 @@ hipError_t launch_round_small(const uint32_t *rank, const RoundIn &in, const Rou
     if (r == 0 || r > ROUND_TINY) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_round_small, dim3(1), dim3(ROUND_SMALL), 0, st, rank, in, g, r, n, sqrt_policy, b, cap, kl,
                        out);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_small_view(const uint32_t *rank_b, const uint32_t *rank_j, const RoundIn &in,
+                                   const RoundRun &run, const RoundSegs &g, uint64_t *place, uint64_t r, uint64_t n,
+                                   int sqrt_policy, uint64_t b, uint64_t cap, uint32_t kl, uint8_t *out,
+                                   hipStream_t st) {
+    if (r == 0 || r > ROUND_TINY) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_round_small_view, dim3(1), dim3(ROUND_SMALL), 0, st, rank_b, rank_j, in, run, g, place, r, n,
+                       sqrt_policy, b, cap, kl, out);
     return hipGetLastError();
 }
 

@@ -95,6 +95,11 @@ struct RoundRun {
 hipError_t launch_round_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const RoundIn &in,
                                     const RoundRun &run, const RoundSegs &g, uint64_t *place, uint64_t r,
                                     hipStream_t st);
+// a tiny round (r <= round_tiny_max()) over the view in one launch after the two searches
+hipError_t launch_round_small_view(const uint32_t *rank_b, const uint32_t *rank_j, const RoundIn &in,
+                                   const RoundRun &run, const RoundSegs &g, uint64_t *place, uint64_t r, uint64_t n,
+                                   int sqrt_policy, uint64_t b, uint64_t cap, uint32_t kl, uint8_t *out,
+                                   hipStream_t st);
 // the two-call path's step 1 over the view: bound keys interleaved (row 2 j start, 2 j + 1 end)
 hipError_t launch_resolve_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk, const uint8_t *ek,
                                const RoundIn &in, const RoundRun &run, uint64_t r, uint64_t *lo, uint64_t *hi,

@@ -2425,19 +2425,20 @@ struct rh_store {
             return view ? rh::launch_round_emit_view(hd, c, r, (uint32_t)kl, din, run, g, place, o, stream)
                         : rh::launch_round_emit(hd, c, r, (uint32_t)kl, din, g, o, stream);
         };
-        if (view) {  // the bound keys' ranks in the run as well; places and sums over both
-            RH_HIP(search_run(d_skeys, 2 * r, q_drank.p));
-            RH_HIP(rh::launch_round_bounds_view(q_rank.p, q_drank.p, din, run, g, place, r, stream));
-        }
-        if (!view && r <= rh::round_tiny_max()) {
-            RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, out_p, stream));
+        if (view) RH_HIP(search_run(d_skeys, 2 * r, q_drank.p));  // the bound keys' ranks in the run too
+        if (r <= rh::round_tiny_max()) {
+            if (view)
+                RH_HIP(rh::launch_round_small_view(q_rank.p, q_drank.p, din, run, g, place, r, n, sq, b, cap,
+                                                   (uint32_t)kl, out_p, stream));
+            else RH_HIP(rh::launch_round_small(q_rank.p, din, g, r, n, sq, b, cap, (uint32_t)kl, out_p, stream));
         } else if (r <= rh::round_small_max()) {
-            // (a tiny round over base + run: straight into the mapped output, header first)
-            if (!view) RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
+            if (view) RH_HIP(rh::launch_round_bounds_view(q_rank.p, q_drank.p, din, run, g, place, r, stream));
+            else RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
             RH_HIP(rh::launch_round_plan_scan(din, g, r, n, sq, b, out_p, stream));
             RH_HIP(emit(cap, reinterpret_cast<const uint64_t *>(out_p), out_p));
         } else {
-            if (!view) RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
+            if (view) RH_HIP(rh::launch_round_bounds_view(q_rank.p, q_drank.p, din, run, g, place, r, stream));
+            else RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
             RH_HIP(hipMemsetAsync(hdr, 0, 64, stream));
             RH_HIP(rh::launch_round_plan(g, d_rem, r, n, sq, b, hdr, stream));
             RH_HIP(rh::launch_exclusive_scan_u64(nch, choff, r, scratch, stream));

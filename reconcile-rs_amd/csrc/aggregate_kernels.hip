@@ -837,6 +837,22 @@ __global__ __launch_bounds__(256) void k_round_emit_view(const uint64_t *hdr, ui
         if (g.nen[j]) round_emit_enum(j, g.enoff[j], L, kl, in, g, out);
 }
 
+// A round's output out of device memory into mapped page-locked memory, exactly round_layout's
+// bytes (the header says how many) -- no header round trip to the host first.  Children beyond
+// cap: the header alone (the host grows the buffer and emits again).  16-byte stores, whole lines
+// per wave.
+__global__ __launch_bounds__(256) void k_round_copy_out(const uint64_t *hdr, uint64_t cap, uint32_t kl,
+                                                        const uint8_t *src, uint8_t *dst, uint64_t max_bytes) {
+    const uint64_t nc = hdr[3], ne = hdr[1];
+    uint64_t end = nc > cap ? 64 : round_layout(nc, ne, kl).end;
+    if (end > max_bytes) end = max_bytes;
+    const uint64_t n16 = end / 16;
+    const uint4 *s = reinterpret_cast<const uint4 *>(src);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+        d[i] = s[i];
+}
+
 // Every segment's raw rank range and local aggregate, one wave each
 __global__ __launch_bounds__(256) void k_round_bounds(const uint32_t *rank, RoundIn in, RoundSegs g, uint64_t r,
                                                       uint64_t n) {
@@ -1328,6 +1344,13 @@ hipError_t launch_round_emit_view(const uint64_t *hdr, uint64_t cap, uint64_t r,
     const uint64_t wgs = std::min<uint64_t>(std::max<uint64_t>((cap + 3) / 4, (r + 255) / 256), 4096);
     hipLaunchKernelGGL(k_round_emit_view, dim3((uint32_t)wgs), dim3(256), 0, st, hdr, cap, r, kl, in, run, g, place,
                        out);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_copy_out(const uint64_t *hdr, uint64_t cap, uint32_t kl, const uint8_t *src, uint8_t *dst,
+                                 uint64_t worst, hipStream_t st) {
+    const uint64_t wgs = std::min<uint64_t>(std::max<uint64_t>(worst / 16 / 256, 1), 1024);
+    hipLaunchKernelGGL(k_round_copy_out, dim3((uint32_t)wgs), dim3(256), 0, st, hdr, cap, kl, src, dst, worst);
     return hipGetLastError();
 }
 

@@ -121,6 +121,10 @@ hipError_t launch_round_plan(const RoundSegs &g, const uint64_t *remote, uint64_
                              uint64_t b, uint64_t *hdr, hipStream_t st);
 hipError_t launch_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl, const RoundIn &in,
                              const RoundSegs &g, uint8_t *out, hipStream_t st);
+// the round (round_layout bytes, per the header at hdr; the header alone when the children
+// outnumber cap) from src into dst, mapped page-locked memory of at least `worst` bytes
+hipError_t launch_round_copy_out(const uint64_t *hdr, uint64_t cap, uint32_t kl, const uint8_t *src, uint8_t *dst,
+                                 uint64_t worst, hipStream_t st);
 // every segment's raw rank range (from the searched bound ranks) and local aggregate
 hipError_t launch_round_bounds(const uint32_t *rank, const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n,
                                hipStream_t st);

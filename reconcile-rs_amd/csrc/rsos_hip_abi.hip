@@ -2337,6 +2337,8 @@ struct rh_store {
     DevBuf<uint64_t> r_seg;
     PinnedVec<uint8_t> pr_out;
     static constexpr size_t kRoundSmall = 256 << 10;  // below this, one speculative copy each way
+    static constexpr size_t kDirectMax = 256ull << 20;  // mapped output sized for the worst case up to this
+    int round_copyout = getenv("RSOS_HIP_ROUND_COPYOUT") ? atoi(getenv("RSOS_HIP_ROUND_COPYOUT")) : 2;
     int protocol_round(int policy, uint64_t param, const rh_segments &in, rh_segments *ch, rh_segments *en,
                        rh_round_outcome *oc) {
         int rc;
@@ -2420,6 +2422,19 @@ struct rh_store {
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
                                         base_table()));
         else RH_HIP(hipMemsetAsync(q_rank.p, 0, 2 * r * 4, stream));
+        // a larger round reaches the host through mapped memory sized for the worst case, with one
+        // wait and no header round trip first: emitted there directly, the header copied after it
+        // by a kernel (RSOS_HIP_ROUND_COPYOUT=2, the default), or emitted into device memory and
+        // copied out whole by that kernel (1); 0: a header copy, then the round's bytes.  Writes
+        // over PCIe from the emit itself overlap its sums: 2.515-2.551 ms per reconciliation
+        // against 2.61-2.62 (1) and 2.64-2.65 (0) (profiles/r04_s18_rbsr_copyout_ab.jsonl)
+        bool direct = false;
+        uint8_t *dout = nullptr;
+        if (!zero_copy && worst > kRoundSmall && worst <= kDirectMax && round_copyout) {
+            pr_out.resize(worst);
+            direct = !dev_ptr(pr_out, &dout);
+        }
+        uint8_t *eo = direct && round_copyout == 2 ? dout : r_out.p;  // where emit writes
         // emit reads the header `hd` that the plan wrote and writes the round into `o`
         auto emit = [&](uint64_t c, const uint64_t *hd, uint8_t *o) {
             return view ? rh::launch_round_emit_view(hd, c, r, (uint32_t)kl, din, run, g, place, o, stream)
@@ -2435,7 +2450,7 @@ struct rh_store {
             if (view) RH_HIP(rh::launch_round_bounds_view(q_rank.p, q_drank.p, din, run, g, place, r, stream));
             else RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
             RH_HIP(rh::launch_round_plan_scan(din, g, r, n, sq, b, out_p, stream));
-            RH_HIP(emit(cap, reinterpret_cast<const uint64_t *>(out_p), out_p));
+            RH_HIP(emit(cap, reinterpret_cast<const uint64_t *>(out_p), zero_copy ? out_p : eo));
         } else {
             if (view) RH_HIP(rh::launch_round_bounds_view(q_rank.p, q_drank.p, din, run, g, place, r, stream));
             else RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
@@ -2443,10 +2458,13 @@ struct rh_store {
             RH_HIP(rh::launch_round_plan(g, d_rem, r, n, sq, b, hdr, stream));
             RH_HIP(rh::launch_exclusive_scan_u64(nch, choff, r, scratch, stream));
             RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
-            RH_HIP(emit(cap, hdr, r_out.p));
+            RH_HIP(emit(cap, hdr, eo));
         }
         uint64_t h[5];
-        if (zero_copy) {
+        if (direct)  // the round (or, emitted in place, its header alone)
+            RH_HIP(rh::launch_round_copy_out(hdr, cap, (uint32_t)kl, r_out.p, dout, round_copyout == 2 ? 64 : worst,
+                                             stream));
+        if (zero_copy || direct) {
             if ((rc = sync())) return rc;
             memcpy(h, pr_out.data(), sizeof h);
         } else if (worst <= kRoundSmall) {
@@ -2471,7 +2489,7 @@ struct rh_store {
             RH_HIP(hipMemcpyAsync(hdr, pr_out.data(), 64, hipMemcpyHostToDevice, stream));
             RH_HIP(emit(cap, hdr, r_out.p));
         }
-        if (regrow || worst > kRoundSmall) {
+        if (regrow || (worst > kRoundSmall && !direct)) {
             pr_out.resize(L.end);
             RH_HIP(hipMemcpyAsync(pr_out.data() + 64, r_out.p + 64, L.end - 64, hipMemcpyDeviceToHost, stream));
             if ((rc = sync())) return rc;

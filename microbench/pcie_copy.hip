@@ -1,5 +1,5 @@
 // pcie_copy.hip -- host <-> device copy rates of round-sized buffers (1-8 MiB) by page-locked
-// allocation flags, and the rate of a kernel that writes mapped host memory in whole lines: what a
+// allocation flags, and the rates of a kernel that writes / reads mapped host memory in whole lines: what a
 // large protocol round's input / output copies could cost.
 //   hipcc -O3 --offload-arch=gfx950 microbench/pcie_copy.hip -o /tmp/pcie_copy && /tmp/pcie_copy
 #include <hip/hip_runtime.h>
@@ -59,10 +59,25 @@ int main() {
                     if (ms < best_k) best_k = ms;
                 }
             }
+            float best_r = 1e9;
+            if (f > 0) {  // a kernel reading mapped host memory into device memory (the reverse)
+                uint8_t *hd;
+                CK(hipHostGetDevicePointer((void **)&hd, h, 0));
+                for (int rep = 0; rep < 20; rep++) {
+                    float ms;
+                    CK(hipEventRecord(a, st));
+                    hipLaunchKernelGGL(k_write_lines, dim3(1024), dim3(256), 0, st, (uint4 *)d, (const uint4 *)hd, n / 16);
+                    CK(hipEventRecord(b, st));
+                    CK(hipEventSynchronize(b));
+                    CK(hipEventElapsedTime(&ms, a, b));
+                    if (ms < best_r) best_r = ms;
+                }
+            }
             printf("{\"alloc\": \"%s\", \"bytes\": %zu, \"d2h_us\": %.1f, \"d2h_GBs\": %.1f, \"h2d_us\": %.1f, \"h2d_GBs\": %.1f, "
-                   "\"kernel_write_us\": %.1f, \"kernel_write_GBs\": %.1f}\n",
+                   "\"kernel_write_us\": %.1f, \"kernel_write_GBs\": %.1f, \"kernel_read_us\": %.1f, \"kernel_read_GBs\": %.1f}\n",
                    names[f], n, best_d2h * 1e3, n / (best_d2h * 1e6), best_h2d * 1e3, n / (best_h2d * 1e6),
-                   f ? best_k * 1e3 : 0.0, f ? n / (best_k * 1e6) : 0.0);
+                   f ? best_k * 1e3 : 0.0, f ? n / (best_k * 1e6) : 0.0, f ? best_r * 1e3 : 0.0,
+                   f ? n / (best_r * 1e6) : 0.0);
         }
         CK(hipHostFree(h));
     }

@@ -576,7 +576,7 @@ def test_gpu_native_round_large_batches(gpu, policy):
     ga, _ = _gpu_and_oracle(schema, ca)
     gb, _ = _gpu_and_oracle(schema, cb)
     pol = {"fixed16": R.FixedFanOut(16), "sqrt": R.SqrtFanOut()}[policy]
-    active, sides, k, widest = R.initial_segments(ga), [gb, ga], 0, 0
+    active, sides, k, widest, log = R.initial_segments(ga), [gb, ga], 0, 0, []
     while len(active):
         side = sides[k % 2]
         widest = max(widest, len(active))
@@ -587,8 +587,17 @@ def test_gpu_native_round_large_batches(gpu, policy):
         assert _outcome(o) == _outcome(wo)
         assert _norm(ch.items(schema)) == _norm(want_ch)
         assert [en.bounds(schema, i) for i in range(en.n)] == want_en
+        log.append((_outcome(o), _norm(want_ch), want_en))
         active, k = ch, k + 1
     assert widest > 4000 and k > 3
+    # the same rounds handed over in place (each store's output arrays, in mapped page-locked
+    # memory, are the peer's next input: read in by a kernel, not copied)
+    active, k = R.initial_segments(ga), 0
+    while len(active):
+        active, en, o = R.protocol_round_segments(sides[k % 2], pol, active, copy=False)
+        assert (_outcome(o), _norm(active.items(schema)), [en.bounds(schema, i) for i in range(en.n)]) == log[k]
+        k += 1
+    assert k == len(log)
     ga.close()
     gb.close()
 

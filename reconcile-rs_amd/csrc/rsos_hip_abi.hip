@@ -2328,11 +2328,13 @@ struct rh_store {
         return RH_OK;
     }
     // A whole protocol round (protocol_round_with_policy, protocol.rs:212-317) for the policies
-    // that decide on the span alone, in one device round trip: the segments go up in one copy
-    // (or one per array when large), the bounds' ranks, local aggregates, decisions, children
-    // (cut keys and aggregates) and enumerations are formed on the device (k_round_*), and the
-    // round comes back in one copy of round_layout() -- the header first when the worst-case
-    // layout is large, so the copy is exact.
+    // that decide on the span alone, in one device round trip, over the base run and any pending
+    // delta run (k_round_*_view: no compaction): the bounds' ranks, local aggregates, decisions,
+    // children (cut keys and aggregates) and enumerations are formed on the device, in
+    // round_layout().  Tiny rounds read their segments from and write the round into mapped
+    // page-locked memory (no copy command); larger ones go up in one copy (a peer's round handed
+    // over in place) and are emitted straight into mapped memory sized for the worst case (up to
+    // kDirectMax; past it, the header comes down first so the copy is exact).
     DevBuf<uint8_t> r_in, r_kind, r_out;
     DevBuf<uint64_t> r_seg;
     PinnedVec<uint8_t> pr_out;

@@ -21,4 +21,7 @@ run interleave_off 400 reconcile-rs_amd/examples/tier_interleave 100000000 10000
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- reconcile-rs_amd/examples/tier_interleave 100000000 1000000 4 0 c5 1 3 > $O/prof.log 2>&1 || exit $?
 python3 scripts/copy_summary.py $O/prof > $O/interleave_off_kernel_stats.txt 2>&1 || true
 rm -rf $O/prof/*/*_kernel_trace.csv 2>/dev/null
+RSOS_HIP_TIER_SYNC=0 timeout -k 10 400 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d $O/hip -o hip -- reconcile-rs_amd/examples/tier_interleave 100000000 1000000 12 1 c5 2 3 > $O/nowait_trace.log 2>&1 || exit $?
+python3 scripts/long_calls.py $O/hip > $O/nowait_long_calls.txt 2>&1 || true
+rm -rf $O/hip
 echo "== done"

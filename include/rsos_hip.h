@@ -438,6 +438,59 @@ int rh_estore_aggregates(rh_estore *store, const uint64_t *lo, const uint64_t *h
 int rh_estore_fingerprints(rh_estore *store, uint64_t lo, uint64_t hi, uint8_t *host_out);
 int rh_estore_set_host_tier(rh_estore *store, int enable);
 
+/* ---- the sharded store: one map over several GPUs ------------------------------------------
+ * The north_star's key-range shards inside one replica (a replica is one process
+ * holding one map, src/replica.rs:68-74): rh_sstore is n column stores, shard s on devices[s]
+ * (a device may repeat), shard s holding the keys in [split[s - 1], split[s]).  Same schema rules,
+ * same answers, same errors as one rh_store holding the whole map -- the Rsos<K> surface
+ * (rsos/src/rsos_trait.rs:39-90) and the protocol round (rbsr/src/protocol.rs:212-317).  Every
+ * question is decomposed over the shards with no device-to-device traffic (ranks and aggregates
+ * add over a key-range partition, aggregate.rs:79-89; select goes to the shard holding its rank;
+ * a round's segments inside one shard's range are that shard's own round, a segment straddling a
+ * boundary is resolved from its two boundary shards and cut on the host), and the shards are
+ * driven concurrently by one host thread each.  Every call is synchronous and takes the map's
+ * lock: each answer is one snapshot of every shard (rbsr/src/rsos_view.rs:36).
+ * Splitters: until the first load the key space is cut evenly (u32 / u64 keys at multiples of
+ * 2^32 / n and 2^64 / n, byte keys by their leading 8 bytes), so single inserts spread over the
+ * shards; a load cuts its rows at equal counts (shard s gets rows [n_rows * s / n, n_rows * (s + 1) / n)).
+ * apply: a batch with a repeated key is rejected (RH_ERR_ARG) before any shard changes.
+ * Round outputs belong to the sharded store (valid until its next call), as rh_store_protocol_round's.
+ * reserve: each shard reserves rows / n (+ 1/8) resident rows and batches of batch_rows.        */
+typedef struct rh_sstore rh_sstore;
+int rh_sstore_create(const int *devices, int n, const rh_schema *schema, rh_sstore **out);
+int rh_sstore_destroy(rh_sstore *store);
+int rh_sstore_shard_count(rh_sstore *store);
+/* shard i's store (borrowed: stats, tier stats; destroyed with the sharded store)            */
+int rh_sstore_shard(rh_sstore *store, int i, rh_store **out);
+/* the n - 1 splitters (key_len bytes each); set_splitters only while the map is empty
+ * (RH_ERR_STATE otherwise), non-decreasing                                                    */
+int rh_sstore_splitters(rh_sstore *store, void *out);
+int rh_sstore_set_splitters(rh_sstore *store, const void *keys);
+int rh_sstore_load(rh_sstore *store, const rh_columns *host_cols, size_t n);
+int rh_sstore_stage(rh_sstore *store, const rh_columns *host_cols, const uint8_t *ops, size_t m);
+int rh_sstore_apply(rh_sstore *store, const rh_columns *host_cols, const uint8_t *ops, size_t n, uint64_t *n_new,
+                    uint64_t *n_overwritten, uint64_t *n_deleted);
+int rh_sstore_len(rh_sstore *store, uint64_t *out);
+int rh_sstore_aggregates(rh_sstore *store, const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out);
+int rh_sstore_aggregate_keys(rh_sstore *store, int lo_kind, const void *lo_key, int hi_kind, const void *hi_key,
+                             rh_aggregate *out);
+int rh_sstore_rank(rh_sstore *store, const void *key, uint64_t *out);
+int rh_sstore_ranks(rh_sstore *store, const void *keys, size_t m, uint64_t *out);
+int rh_sstore_select(rh_sstore *store, uint64_t r, void *key_out);
+int rh_sstore_keys(rh_sstore *store, uint64_t lo, uint64_t hi, void *host_out);
+int rh_sstore_fingerprints(rh_sstore *store, uint64_t lo, uint64_t hi, uint8_t *host_out);
+int rh_sstore_resolve_segments(rh_sstore *store, size_t r, const uint8_t *start_kinds, const void *start_keys,
+                               const uint8_t *end_kinds, const void *end_keys, uint64_t *raw_start,
+                               uint64_t *raw_end, rh_aggregate *local);
+int rh_sstore_split_segments(rh_sstore *store, size_t m, const uint64_t *select_ranks, void *keys_out, size_t q,
+                             const uint64_t *lo, const uint64_t *hi, rh_aggregate *out);
+int rh_sstore_protocol_round(rh_sstore *store, int policy, uint64_t fan_out, const rh_segments *active,
+                             rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome);
+int rh_sstore_set_host_tier(rh_sstore *store, int enable, uint64_t round_max);
+int rh_sstore_set_tier_policy(rh_sstore *store, int keep_fresh);
+int rh_sstore_reserve(rh_sstore *store, uint64_t rows, uint64_t batch_rows);
+int rh_sstore_compact(rh_sstore *store);
+
 /* ---- testing ---------------------------------------------------------------------------
  * Make the named internal failure point fail once (RH_ERR_OOM) on the calling thread; NULL or
  * "" clears it.  Points: "snapshot.load_begin" (the projection store's half of a reload),

@@ -27,6 +27,7 @@
 #include "../../include/rsos_hip.h"
 #include "host_delta.hpp"
 #include "internal.hpp"
+#include "round_decide.hpp"
 
 namespace rh {
 
@@ -432,11 +433,8 @@ struct HostTier {
     }
 
     // ---- one protocol round (protocol_round_with_policy, rbsr/src/protocol.rs:212-317) ------------
-    // The same decisions as the device path (round_decide, aggregate_kernels.hip) and the same output
-    // layout (round_layout): SKIP on equal aggregates, the shared cutoffs (policy/cutoffs.rs), the
-    // policy's stride (FixedFanOut ceil(span / b), SqrtFanOut (span as f32).sqrt()), a non-progressing
-    // SPLIT turned IDLIST (:263-272), an IDLIST with a non-empty remote side bounced back as one child
-    // with the ZERO aggregate, a SPLIT's children cut at every stride-th rank (:288-313).
+    // The same decisions as the device path (round_decide, aggregate_kernels.hip; on the host
+    // decide_segment, round_decide.hpp) and the same output layout (round_layout).
     struct Seg {
         int kind;  // 0 skip, 1 IDLIST, 2 SPLIT, 3 dropped
         uint64_t stride, children, enums;
@@ -455,31 +453,8 @@ struct HostTier {
             Seg &g = segs[j];
             g = Seg{3, 0, 0, 0, sk[j] ? lt(skeys + j * kl) : begin(), ek[j] ? lt(ekeys + j * kl) : end(), {}};
             agg(g.cs, g.ce, &g.loc);
-            const rh_aggregate &R = in.aggregates[j];
-            if (g.ce.r >= g.cs.r) {
-                const uint64_t span = g.loc.size, rem = R.size;
-                uint64_t st = 0;
-                int k;
-                if (span == rem && !memcmp(g.loc.fingerprint, R.fingerprint, 32)) k = 0;
-                else if (rem == 0) k = 1;
-                else if (span == 0) k = 2, st = 1;
-                else if (span == 1 && rem == 1) k = 1;
-                else if (span == 1) k = 2, st = 1;
-                else {
-                    k = 2;
-                    st = sqrt_policy ? (uint64_t)std::sqrt((float)span) : (span + b - 1) / b;
-                    if (st == 0) st = 1;  // SplitStride::per_child
-                }
-                if (k == 2 && span > 1 && st >= span) k = 1;
-                g.kind = k;
-                g.stride = st;
-                if (k == 1) {
-                    g.enums = 1;
-                    g.children = rem != 0;
-                } else if (k == 2) {
-                    g.children = (g.ce.r > g.cs.r ? (g.ce.r - g.cs.r - 1) / st : 0) + 1;
-                }
-            }
+            const SegDecision d = decide_segment(g.cs.r, g.ce.r, g.loc, in.aggregates[j], sqrt_policy, b);
+            g.kind = d.kind, g.stride = d.stride, g.children = d.children, g.enums = d.enums;
             cnt[g.kind == 3 ? 4 : g.kind]++;
             nc += g.children;
             ne += g.enums;

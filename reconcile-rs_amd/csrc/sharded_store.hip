@@ -1,0 +1,1097 @@
+// sharded_store.hip -- rh_sstore: one replica's map over several GPUs (include/rsos_hip.h).
+//
+// The north_star shards records by key range across the GPUs of one node.  A
+// replica is one process holding one map (Inner<K, V>, /root/reference/src/replica.rs:68-74), so
+// the in-process form of that partitioning is a list of column stores (rh_store), one per device,
+// each owning a contiguous key range: shard s holds the keys in [split[s - 1], split[s]).  Every
+// question of the Rsos<K> surface (rsos/src/rsos_trait.rs:39-90) and of a protocol round
+// (rbsr/src/protocol.rs:212-317) decomposes over that partition with no device-to-device traffic:
+//   - size, rank(z): sums -- rank(z) = (rows of the shards below z's) + rank in z's shard;
+//   - aggregate(range): Aggregate's Add (rsos/src/aggregate.rs:79-89) of the shards' parts: the
+//     shards wholly inside the range give their cached roots, at most two boundary shards are asked;
+//   - select(r): the shard whose rank interval holds r;
+//   - insert / delete: each row routed to its key's shard by the splitters;
+//   - a protocol round: a run of segments inside one shard's key range is that shard's own round
+//     (a segment's decisions, cut ranks and children depend on ranks only through differences
+//     inside the segment, so the shard answers exactly what the whole map would); a segment that
+//     straddles a boundary (at most one per boundary per round, the segments being key-ordered) is
+//     resolved from its two boundary shards, decided on the host (round_decide.hpp) and cut by
+//     selects and rank-range aggregates routed to the shards that hold them.
+// Shards are driven concurrently by host threads (one per shard; each store has its own stream and
+// lock), so per-shard device work overlaps.  Only the public rh_store_* entry points are used.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/rsos_hip.h"
+#include "internal.hpp"
+#include "round_decide.hpp"
+
+namespace rh {
+int set_error(int code, const std::string &msg);  // rsos_hip_abi.hip: the calling thread's rh_last_error
+}
+
+namespace {
+
+// Runs one task per shard concurrently: the first on the calling thread, the others on the shards'
+// own worker threads (which spin briefly, then sleep, between calls: a host-tier question is
+// microseconds, a device one tens of microseconds).
+class ShardPool {
+  public:
+    explicit ShardPool(int n) : slots_(n) {
+        for (int i = 1; i < n; i++) slots_[i].th = std::thread([this, i] { loop(i); });
+    }
+    ~ShardPool() {
+        for (size_t i = 1; i < slots_.size(); i++) {
+            Slot &w = slots_[i];
+            {
+                std::lock_guard<std::mutex> g(w.mu);
+                w.quit = true;
+                w.state.store(1, std::memory_order_release);
+            }
+            w.cv.notify_one();
+            w.th.join();
+        }
+    }
+    // fn(s) for every shard s in `idx` (distinct, ascending); returns when all have finished
+    void run(const std::vector<int> &idx, const std::function<void(int)> &fn) {
+        if (idx.empty()) return;
+        if (idx.size() == 1) {
+            fn(idx[0]);
+            return;
+        }
+        for (size_t k = 1; k < idx.size(); k++) {
+            Slot &w = slots_[idx[k]];
+            {
+                std::lock_guard<std::mutex> g(w.mu);
+                w.fn = &fn;
+                w.state.store(1, std::memory_order_release);
+            }
+            w.cv.notify_one();
+        }
+        fn(idx[0]);
+        for (size_t k = 1; k < idx.size(); k++) {
+            Slot &w = slots_[idx[k]];
+            wait_for(w, 2);
+            w.state.store(0, std::memory_order_relaxed);
+        }
+    }
+
+  private:
+    struct Slot {
+        std::thread th;
+        std::mutex mu;
+        std::condition_variable cv;
+        std::atomic<int> state{0};  // 0 idle, 1 task posted, 2 done
+        const std::function<void(int)> *fn = nullptr;
+        bool quit = false;
+    };
+    std::vector<Slot> slots_;
+    static void wait_for(Slot &w, int want) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (w.state.load(std::memory_order_acquire) != want) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
+                std::unique_lock<std::mutex> g(w.mu);
+                w.cv.wait(g, [&] { return w.state.load(std::memory_order_acquire) == want; });
+                return;
+            }
+        }
+    }
+    void loop(int i) {
+        Slot &w = slots_[i];
+        for (;;) {
+            wait_for(w, 1);
+            if (w.quit) return;
+            (*w.fn)(i);
+            {
+                std::lock_guard<std::mutex> g(w.mu);
+                w.state.store(2, std::memory_order_release);
+            }
+            w.cv.notify_all();
+        }
+    }
+};
+
+int fail(int code, const std::string &msg) { return rh::set_error(code, msg); }
+
+// a shard call's status, with its message (rh_last_error is per thread)
+struct Status {
+    int rc = RH_OK;
+    std::string msg;
+    void take(int r) {
+        if (r != RH_OK && rc == RH_OK) {
+            rc = r;
+            const char *m = rh_last_error();
+            msg = m ? m : "";
+        }
+    }
+};
+
+int key_row(const rh_schema &s) {
+    switch (s.key_kind) {
+    case RH_KEY_UNIT: return 0;
+    case RH_KEY_U32: return 4;
+    case RH_KEY_U64: return 8;
+    default: return (int)s.key_len;
+    }
+}
+int value_row(const rh_schema &s) {
+    switch (s.value_kind) {
+    case RH_VAL_UNIT: return 0;
+    case RH_VAL_U32: return 4;
+    case RH_VAL_U64: return 8;
+    default: return (int)s.value_len;
+    }
+}
+
+const rh_aggregate kZero{{0, 0, 0, 0}, 0};
+void agg_add(rh_aggregate &a, const rh_aggregate &b) {
+    rh_fp_add(a.fingerprint, b.fingerprint, a.fingerprint);
+    a.size += b.size;
+}
+
+}  // namespace
+
+struct rh_sstore {
+    rh_schema schema{};
+    int G = 0;
+    size_t kl = 0;
+    std::vector<rh_store *> shards;
+    std::vector<uint8_t> split;     // G - 1 keys: shard s holds [split[s - 1], split[s])
+    std::vector<uint64_t> sizes;    // rows per shard (valid while sizes_ok)
+    std::vector<uint64_t> off;      // G + 1 prefix sums of sizes
+    bool sizes_ok = false;
+    std::vector<uint8_t> dirty;     // shard has staged rows not yet applied
+    std::mutex mu;                  // one call at a time: every answer is one snapshot of every shard
+    ShardPool *pool = nullptr;
+    std::vector<uint8_t> round_out;  // the last round's output, round_layout()
+
+    // ---- key order (the key type's Ord: numeric for u32 / u64 keys stored LE, bytewise else) ----
+    int cmp(const uint8_t *a, const uint8_t *b) const {
+        if (schema.key_kind == RH_KEY_U32 || schema.key_kind == RH_KEY_U64) {
+            uint64_t x = 0, y = 0;
+            memcpy(&x, a, kl);
+            memcpy(&y, b, kl);
+            return (x > y) - (x < y);
+        }
+        return kl ? memcmp(a, b, kl) : 0;
+    }
+    const uint8_t *splitter(int j) const { return split.data() + (size_t)j * kl; }
+    // the shard holding key z: the number of splitters <= z (bisect_right)
+    int owner(const uint8_t *z) const {
+        int lo = 0, hi = G - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) / 2;
+            if (cmp(splitter(mid), z) <= 0) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    }
+    // the last shard that can hold a key below z: the number of splitters < z (bisect_left)
+    int owner_below(const uint8_t *z) const {
+        int lo = 0, hi = G - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) / 2;
+            if (cmp(splitter(mid), z) < 0) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    }
+    // Until the first load, the key space is cut evenly: u32 / u64 keys at multiples of 2^32 / G
+    // and 2^64 / G, byte keys by their leading 8 bytes read big-endian (their order), so that a map
+    // filled by single inserts (just_insert_bulk, src/replica/write.rs:107-121) spreads over the
+    // shards; a load re-cuts at equal counts.
+    void even_splitters() {
+        split.assign((size_t)(G - 1) * kl, 0);
+        for (int j = 1; j < G; j++) {
+            const unsigned __int128 v = ((unsigned __int128)1 << 64) * (unsigned)j / (unsigned)G;
+            uint8_t *k = split.data() + (size_t)(j - 1) * kl;
+            if (schema.key_kind == RH_KEY_U32) {
+                const uint32_t x = (uint32_t)(v >> 32);
+                memcpy(k, &x, 4);
+            } else if (schema.key_kind == RH_KEY_U64) {
+                const uint64_t x = (uint64_t)v;
+                memcpy(k, &x, 8);
+            } else {
+                for (size_t b = 0; b < kl && b < 8; b++) k[b] = (uint8_t)((uint64_t)v >> (56 - 8 * b));
+            }
+        }
+    }
+
+    // ---- sizes (every read flushes the shards' staged rows first, concurrently) ----------------
+    Status flush() {
+        Status st;
+        if (sizes_ok) return st;
+        std::vector<uint64_t> got(G, 0);
+        std::vector<Status> ss(G);
+        std::vector<int> busy, idle;
+        for (int s = 0; s < G; s++) (dirty[s] ? busy : idle).push_back(s);
+        auto len = [&](int s) { ss[s].take(rh_store_len(shards[s], &got[s])); };
+        pool->run(busy, len);
+        for (int s : idle) len(s);
+        for (int s = 0; s < G; s++)
+            if (ss[s].rc) {
+                st.rc = ss[s].rc;
+                st.msg = ss[s].msg;
+                return st;
+            }
+        sizes = got;
+        off.assign(G + 1, 0);
+        for (int s = 0; s < G; s++) off[s + 1] = off[s] + sizes[s];
+        std::fill(dirty.begin(), dirty.end(), 0);
+        sizes_ok = true;
+        return st;
+    }
+    uint64_t total() const { return off[G]; }
+    // the shard holding global rank r (< total()): the last shard whose first rank is <= r
+    int shard_of_rank(uint64_t r) const {
+        return (int)(std::upper_bound(off.begin() + 1, off.begin() + G, r) - (off.begin() + 1));
+    }
+    // run fn over shards concurrently and collect the first error (with its message)
+    int each(const std::vector<int> &idx, const std::function<int(int)> &fn) {
+        std::vector<Status> ss(G);
+        pool->run(idx, [&](int s) {
+            try {
+                ss[s].take(fn(s));
+            } catch (const std::bad_alloc &) {
+                ss[s].rc = RH_ERR_OOM;
+                ss[s].msg = "sharded store: host allocation failed";
+            }
+        });
+        for (int s : idx)
+            if (ss[s].rc) return fail(ss[s].rc, ss[s].msg);
+        return RH_OK;
+    }
+    std::vector<int> all() const {
+        std::vector<int> v(G);
+        for (int s = 0; s < G; s++) v[s] = s;
+        return v;
+    }
+
+    // ---- rows routed to their shards ---------------------------------------------------------
+    // per-shard copies of m host rows: rows[s] lists the input rows shard s takes, in input order
+    struct Part {
+        std::vector<uint8_t> keys, vals, tags, ops;
+        std::vector<uint64_t> phys, node;
+        std::vector<uint32_t> logical;
+        size_t m = 0;
+        rh_columns cols() const {
+            auto p = [](const auto &v) { return v.empty() ? nullptr : v.data(); };
+            return rh_columns{p(keys), reinterpret_cast<const uint64_t *>(p(phys)),
+                              reinterpret_cast<const uint32_t *>(p(logical)),
+                              reinterpret_cast<const uint64_t *>(p(node)), p(tags), p(vals)};
+        }
+    };
+    void route(const uint8_t *keys, size_t m, std::vector<std::vector<uint32_t>> &rows) const {
+        rows.assign(G, {});
+        for (size_t i = 0; i < m; i++) rows[owner(keys + i * kl)].push_back((uint32_t)i);
+    }
+    void gather(const rh_columns &h, const uint8_t *ops, const std::vector<uint32_t> &rows, Part &p) const {
+        const size_t m = rows.size(), vr = value_row(schema);
+        const bool dated = schema.record_kind == RH_REC_DATED;
+        p.m = m;
+        auto pick = [&](auto &dst, const auto *src, size_t w) {
+            using T = std::remove_cv_t<std::remove_pointer_t<decltype(src)>>;
+            if (!src) return;
+            dst.resize(m * w);
+            for (size_t i = 0; i < m; i++) memcpy(&dst[i * w], reinterpret_cast<const T *>(src) + (size_t)rows[i] * w, w * sizeof(T));
+        };
+        pick(p.keys, static_cast<const uint8_t *>(h.keys), kl);
+        pick(p.vals, static_cast<const uint8_t *>(h.values), vr);
+        if (schema.record_kind != RH_REC_PLAIN) pick(p.tags, h.tags, 1);
+        if (dated) {
+            pick(p.phys, h.phys, 1);
+            pick(p.node, h.node, 1);
+            pick(p.logical, h.logical, 1);
+        }
+        pick(p.ops, ops, 1);
+    }
+    // whether m key rows hold a repeated key (strictly increasing input answers in one pass)
+    bool has_duplicates(const uint8_t *keys, size_t m) const {
+        bool sorted = true;
+        for (size_t i = 1; i < m && sorted; i++) sorted = cmp(keys + (i - 1) * kl, keys + i * kl) < 0;
+        if (sorted) return false;
+        std::vector<uint32_t> ix(m);
+        for (size_t i = 0; i < m; i++) ix[i] = (uint32_t)i;
+        std::sort(ix.begin(), ix.end(), [&](uint32_t a, uint32_t b) { return cmp(keys + a * kl, keys + b * kl) < 0; });
+        for (size_t i = 1; i < m; i++)
+            if (cmp(keys + ix[i - 1] * kl, keys + ix[i] * kl) == 0) return true;
+        return false;
+    }
+
+    // ---- rank-range pieces ------------------------------------------------------------------
+    // the part of global rank range [lo, hi) in shard s, as shard-local ranks (empty: l == h)
+    void piece(int s, uint64_t lo, uint64_t hi, uint64_t *l, uint64_t *h) const {
+        const uint64_t a = std::clamp(lo, off[s], off[s + 1]), b = std::clamp(hi, off[s], off[s + 1]);
+        *l = a - off[s];
+        *h = std::max(a, b) - off[s];
+    }
+    // aggregates of q global rank ranges (clamped; inverted = ZERO), and m selects, in one call per
+    // shard holding any of them (rh_store_split_segments)
+    int split_ranks(size_t m, const uint64_t *sel, uint8_t *keys_out, size_t q, const uint64_t *lo,
+                    const uint64_t *hi, rh_aggregate *out) {
+        struct Job {
+            std::vector<uint64_t> sel, lo, hi;
+            std::vector<size_t> sel_at, agg_at;
+            std::vector<uint8_t> keys;
+            std::vector<rh_aggregate> aggs;
+        };
+        std::vector<Job> jobs(G);
+        const uint64_t n = total();
+        for (size_t i = 0; i < m; i++) {
+            if (sel[i] >= n) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+            const int s = shard_of_rank(sel[i]);
+            jobs[s].sel.push_back(sel[i] - off[s]);
+            jobs[s].sel_at.push_back(i);
+        }
+        for (size_t j = 0; j < q; j++) {
+            out[j] = kZero;
+            const uint64_t h = std::min(hi[j], n), l = std::min(lo[j], h);
+            if (l == h) continue;
+            for (int s = shard_of_rank(l); s < G && off[s] < h; s++) {
+                uint64_t a, b;
+                piece(s, l, h, &a, &b);
+                if (a == b) continue;
+                jobs[s].lo.push_back(a);
+                jobs[s].hi.push_back(b);
+                jobs[s].agg_at.push_back(j);
+            }
+        }
+        std::vector<int> idx;
+        for (int s = 0; s < G; s++)
+            if (!jobs[s].sel.empty() || !jobs[s].lo.empty()) idx.push_back(s);
+        int rc = each(idx, [&](int s) -> int {
+            Job &J = jobs[s];
+            J.keys.resize(J.sel.size() * kl + 1);
+            J.aggs.resize(J.lo.size() + 1);
+            return rh_store_split_segments(shards[s], J.sel.size(), J.sel.data(), J.keys.data(), J.lo.size(),
+                                           J.lo.data(), J.hi.data(), J.aggs.data());
+        });
+        if (rc) return rc;
+        for (int s : idx) {
+            const Job &J = jobs[s];
+            for (size_t i = 0; i < J.sel.size(); i++) memcpy(keys_out + J.sel_at[i] * kl, J.keys.data() + i * kl, kl);
+            for (size_t i = 0; i < J.lo.size(); i++) agg_add(out[J.agg_at[i]], J.aggs[i]);
+        }
+        return RH_OK;
+    }
+
+    // ---- segments resolved over the shards ----------------------------------------------------
+    // Segment j's keys lie in shards [a_j, b_j]: a_j holds its start bound (0 when unbounded), b_j
+    // the keys just below its end bound (G - 1 when unbounded).  Its raw ranks come from those two
+    // shards alone; its local aggregate adds the roots of the shards between them.  a_j > b_j is an
+    // empty or inverted segment: its ranks still come from a_j and b_j, its aggregate is ZERO.
+    void span(const uint8_t sk, const uint8_t *skey, const uint8_t ek, const uint8_t *ekey, int *a, int *b) const {
+        *a = sk ? owner(skey) : 0;
+        *b = ek ? owner_below(ekey) : G - 1;
+    }
+    int resolve_list(const std::vector<size_t> &J, const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek,
+                     const uint8_t *ekeys, uint64_t *raw_lo, uint64_t *raw_hi, rh_aggregate *local) {
+        struct Job {
+            std::vector<uint8_t> sk, ek, skeys, ekeys;
+            std::vector<size_t> at;
+            std::vector<uint8_t> side;  // 1: the start side, 2: the end side, 3: both
+            std::vector<uint64_t> lo, hi;
+            std::vector<rh_aggregate> aggs;
+        };
+        std::vector<Job> jobs(G);
+        std::vector<int> A(J.size()), B(J.size());
+        auto add = [&](int s, size_t t, int side) {
+            const size_t j = J[t];
+            Job &q = jobs[s];
+            const bool st = side & 1, en = side & 2;
+            q.sk.push_back(st ? sk[j] : 0);
+            q.ek.push_back(en ? ek[j] : 0);
+            const size_t o = q.skeys.size();
+            q.skeys.resize(o + kl, 0);
+            q.ekeys.resize(o + kl, 0);
+            if (st && sk[j]) memcpy(q.skeys.data() + o, skeys + j * kl, kl);
+            if (en && ek[j]) memcpy(q.ekeys.data() + o, ekeys + j * kl, kl);
+            q.at.push_back(t);
+            q.side.push_back((uint8_t)side);
+        };
+        for (size_t t = 0; t < J.size(); t++) {
+            const size_t j = J[t];
+            span(sk[j], sk[j] ? skeys + j * kl : nullptr, ek[j], ek[j] ? ekeys + j * kl : nullptr, &A[t], &B[t]);
+            if (A[t] == B[t]) add(A[t], t, 3);
+            else add(A[t], t, 1), add(B[t], t, 2);
+        }
+        std::vector<int> idx;
+        for (int s = 0; s < G; s++)
+            if (!jobs[s].at.empty()) idx.push_back(s);
+        int rc = each(idx, [&](int s) -> int {
+            Job &q = jobs[s];
+            const size_t r = q.at.size();
+            q.lo.resize(r), q.hi.resize(r), q.aggs.resize(r);
+            return rh_store_resolve_segments(shards[s], r, q.sk.data(), q.skeys.data(), q.ek.data(), q.ekeys.data(),
+                                             q.lo.data(), q.hi.data(), q.aggs.data());
+        });
+        if (rc) return rc;
+        // the roots of the shards between a segment's two boundary shards
+        std::vector<rh_aggregate> roots;
+        for (size_t t = 0; t < J.size(); t++) {
+            local[t] = kZero;
+            if (B[t] > A[t] + 1 && roots.empty()) {
+                roots.assign(G, kZero);
+                for (int s = 0; s < G; s++)
+                    if ((rc = rh_store_aggregate_keys(shards[s], 0, nullptr, 0, nullptr, &roots[s]))) return rc;
+            }
+        }
+        for (int s : idx) {
+            const Job &q = jobs[s];
+            for (size_t i = 0; i < q.at.size(); i++) {
+                const size_t t = q.at[i];
+                if (q.side[i] & 1) raw_lo[t] = off[s] + q.lo[i];
+                if (q.side[i] & 2) raw_hi[t] = off[s] + q.hi[i];
+                if (A[t] <= B[t]) agg_add(local[t], q.aggs[i]);
+            }
+        }
+        for (size_t t = 0; t < J.size(); t++)
+            for (int s = A[t] + 1; s < B[t]; s++) agg_add(local[t], roots[s]);
+        return RH_OK;
+    }
+
+    // ---- a protocol round --------------------------------------------------------------------
+    // One piece of the round's output: the children and enumerations of a run of segments.
+    struct Out {
+        std::vector<uint8_t> csk, cek, cskeys, cekeys, esk, eek, eskeys, eekeys;
+        std::vector<rh_aggregate> caggs;
+        uint64_t cnt[5] = {0, 0, 0, 0, 0};  // skipped, enumerated, split, children, dropped
+        void child(uint8_t s, const uint8_t *sk, uint8_t e, const uint8_t *ek, const rh_aggregate &a, size_t kl) {
+            csk.push_back(s), cek.push_back(e);
+            put(cskeys, s ? sk : nullptr, kl), put(cekeys, e ? ek : nullptr, kl);
+            caggs.push_back(a);
+        }
+        void enumeration(uint8_t s, const uint8_t *sk, uint8_t e, const uint8_t *ek, size_t kl) {
+            esk.push_back(s), eek.push_back(e);
+            put(eskeys, s ? sk : nullptr, kl), put(eekeys, e ? ek : nullptr, kl);
+        }
+        static void put(std::vector<uint8_t> &v, const uint8_t *k, size_t kl) {
+            const size_t o = v.size();
+            v.resize(o + kl, 0);
+            if (k) memcpy(v.data() + o, k, kl);
+        }
+        // a shard's round, copied out of the shard's buffers (valid until its next call)
+        void take(const rh_segments &c, const rh_segments &e, const rh_round_outcome &o, size_t kl) {
+            auto app = [](std::vector<uint8_t> &v, const void *p, size_t bytes) {
+                if (bytes) v.insert(v.end(), static_cast<const uint8_t *>(p), static_cast<const uint8_t *>(p) + bytes);
+            };
+            app(csk, c.start_kinds, c.n), app(cek, c.end_kinds, c.n);
+            app(cskeys, c.start_keys, c.n * kl), app(cekeys, c.end_keys, c.n * kl);
+            if (c.n) caggs.insert(caggs.end(), c.aggregates, c.aggregates + c.n);
+            app(esk, e.start_kinds, e.n), app(eek, e.end_kinds, e.n);
+            app(eskeys, e.start_keys, e.n * kl), app(eekeys, e.end_keys, e.n * kl);
+            cnt[0] += o.skipped, cnt[1] += o.enumerated, cnt[2] += o.split, cnt[3] += o.children,
+                cnt[4] += o.dropped_malformed;
+        }
+    };
+    struct Run {
+        int shard;  // -1: segments that straddle shard boundaries
+        size_t j0, j1;
+    };
+    int protocol_round(int policy, uint64_t fan_out, const rh_segments &in, rh_segments *ch, rh_segments *en,
+                       rh_round_outcome *oc) {
+        const size_t r = in.n;
+        const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
+        const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
+        const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
+        // maximal runs of consecutive segments with one owning shard
+        std::vector<Run> runs;
+        for (size_t j = 0; j < r; j++) {
+            int a, b;
+            span(sk[j], sk[j] ? skeys + j * kl : nullptr, ek[j], ek[j] ? ekeys + j * kl : nullptr, &a, &b);
+            const int s = a == b ? a : -1;
+            if (!runs.empty() && runs.back().shard == s && runs.back().j1 == j) runs.back().j1 = j + 1;
+            else runs.push_back(Run{s, j, j + 1});
+        }
+        std::vector<Out> outs(runs.size());
+        // the runs inside one shard: that shard's own round, the shards concurrently
+        std::vector<std::vector<size_t>> mine(G);
+        std::vector<size_t> cross;
+        for (size_t k = 0; k < runs.size(); k++) {
+            if (runs[k].shard >= 0) mine[runs[k].shard].push_back(k);
+            else
+                for (size_t j = runs[k].j0; j < runs[k].j1; j++) cross.push_back(j);
+        }
+        std::vector<int> idx;
+        for (int s = 0; s < G; s++)
+            if (!mine[s].empty()) idx.push_back(s);
+        int rc = each(idx, [&](int s) -> int {
+            for (size_t k : mine[s]) {
+                const Run &R = runs[k];
+                const size_t j = R.j0;
+                const rh_segments sub{const_cast<uint8_t *>(sk + j), skeys ? const_cast<uint8_t *>(skeys + j * kl) : nullptr,
+                                      const_cast<uint8_t *>(ek + j), ekeys ? const_cast<uint8_t *>(ekeys + j * kl) : nullptr,
+                                      in.aggregates + j, R.j1 - R.j0, R.j1 - R.j0};
+                rh_segments c{}, e{};
+                rh_round_outcome o{};
+                const int q = rh_store_protocol_round(shards[s], policy, fan_out, &sub, &c, &e, &o);
+                if (q) return q;
+                outs[k].take(c, e, o, kl);
+            }
+            return RH_OK;
+        });
+        if (rc) return rc;
+        if (!cross.empty() && (rc = cross_round(policy, fan_out, in, runs, cross, outs))) return rc;
+        // the pieces in segment order, in round_layout()
+        uint64_t nc = 0, ne = 0, cnt[5] = {0, 0, 0, 0, 0};
+        for (const Out &o : outs) {
+            nc += o.csk.size(), ne += o.esk.size();
+            for (int i = 0; i < 5; i++) cnt[i] += o.cnt[i];
+        }
+        const rh::RoundLayout L = rh::round_layout(nc, ne, kl);
+        round_out.assign(L.end, 0);
+        uint8_t *o = round_out.data();
+        uint64_t c = 0, e = 0;
+        for (const Out &p : outs) {
+            const size_t pc = p.csk.size(), pe = p.esk.size();
+            if (pc) {
+                memcpy(o + L.csk + c, p.csk.data(), pc);
+                memcpy(o + L.cek + c, p.cek.data(), pc);
+                memcpy(o + L.cskeys + c * kl, p.cskeys.data(), pc * kl);
+                memcpy(o + L.cekeys + c * kl, p.cekeys.data(), pc * kl);
+                memcpy(o + L.caggs + c * sizeof(rh_aggregate), p.caggs.data(), pc * sizeof(rh_aggregate));
+            }
+            if (pe) {
+                memcpy(o + L.esk + e, p.esk.data(), pe);
+                memcpy(o + L.eek + e, p.eek.data(), pe);
+                memcpy(o + L.eskeys + e * kl, p.eskeys.data(), pe * kl);
+                memcpy(o + L.eekeys + e * kl, p.eekeys.data(), pe * kl);
+            }
+            c += pc, e += pe;
+        }
+        const uint64_t h[5] = {cnt[0], cnt[1], cnt[2], cnt[3], cnt[4]};
+        memcpy(o, h, sizeof h);
+        if (oc) *oc = rh_round_outcome{h[0], h[1], h[2], h[3], h[4]};
+        *ch = rh_segments{o + L.csk, o + L.cskeys, o + L.cek, o + L.cekeys, reinterpret_cast<rh_aggregate *>(o + L.caggs),
+                          (size_t)nc, (size_t)nc};
+        *en = rh_segments{o + L.esk, o + L.eskeys, o + L.eek, o + L.eekeys, nullptr, (size_t)ne, (size_t)ne};
+        return RH_OK;
+    }
+    // The segments that straddle a shard boundary: resolved from their boundary shards, decided on
+    // the host (decide_segment), their SPLIT cuts selected and their children summed over the
+    // shards holding them -- one call per shard for each of the two steps.
+    int cross_round(int policy, uint64_t fan_out, const rh_segments &in, const std::vector<Run> &runs,
+                    const std::vector<size_t> &J, std::vector<Out> &outs) {
+        const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
+        const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
+        const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
+        static const uint8_t zkey[64] = {0};
+        const uint8_t *skp = skeys ? skeys : zkey, *ekp = ekeys ? ekeys : zkey;
+        const size_t nj = J.size();
+        std::vector<uint64_t> lo(nj), hi(nj);
+        std::vector<rh_aggregate> loc(nj);
+        int rc = resolve_list(J, sk, skp, ek, ekp, lo.data(), hi.data(), loc.data());
+        if (rc) return rc;
+        const int sq = policy == RH_POLICY_SQRT_FAN_OUT;
+        const uint64_t b = fan_out < 2 ? 2 : fan_out;
+        std::vector<rh::SegDecision> d(nj);
+        std::vector<uint64_t> sel, clo, chi;
+        std::vector<size_t> first_sel(nj), first_child(nj);
+        for (size_t t = 0; t < nj; t++) {
+            d[t] = rh::decide_segment(lo[t], hi[t], loc[t], in.aggregates[J[t]], sq, b);
+            first_sel[t] = sel.size(), first_child[t] = clo.size();
+            if (d[t].kind != 2 || d[t].children < 2) continue;
+            const uint64_t ncuts = d[t].children - 1;
+            uint64_t x = lo[t];
+            for (uint64_t k = 0; k <= ncuts; k++) {
+                const uint64_t y = k == ncuts ? hi[t] : lo[t] + (k + 1) * d[t].stride;
+                if (k != ncuts) sel.push_back(y);
+                clo.push_back(x), chi.push_back(y);
+                x = y;
+            }
+        }
+        std::vector<uint8_t> cut(sel.size() * kl + 1);
+        std::vector<rh_aggregate> caggs(clo.size() + 1);
+        if ((!sel.empty() || !clo.empty()) &&
+            (rc = split_ranks(sel.size(), sel.data(), cut.data(), clo.size(), clo.data(), chi.data(), caggs.data())))
+            return rc;
+        // each straddling segment's output goes to its run's piece, in segment order
+        size_t t = 0;
+        for (size_t k = 0; k < runs.size() && t < nj; k++) {
+            if (runs[k].shard >= 0) continue;
+            Out &o = outs[k];
+            for (size_t j = runs[k].j0; j < runs[k].j1; j++, t++) {
+                const rh::SegDecision &g = d[t];
+                const uint8_t *s0 = sk[j] ? skp + j * kl : nullptr, *e0 = ek[j] ? ekp + j * kl : nullptr;
+                o.cnt[g.kind == 3 ? 4 : g.kind]++;
+                if (g.kind == 1) {
+                    o.enumeration(sk[j], s0, ek[j], e0, kl);
+                    if (g.children) o.child(sk[j], s0, ek[j], e0, kZero, kl);
+                } else if (g.kind == 2) {
+                    if (g.children < 2) {
+                        o.child(sk[j], s0, ek[j], e0, loc[t], kl);
+                    } else {
+                        const uint64_t ncuts = g.children - 1;
+                        const uint8_t *prev = nullptr;
+                        for (uint64_t c = 0; c <= ncuts; c++) {
+                            const uint8_t *key = c < ncuts ? cut.data() + (first_sel[t] + c) * kl : nullptr;
+                            o.child(c ? 1 : sk[j], c ? prev : s0, c != ncuts ? 1 : ek[j], c != ncuts ? key : e0,
+                                    caggs[first_child[t] + c], kl);
+                            prev = key;
+                        }
+                    }
+                }
+                o.cnt[3] += g.children;
+            }
+        }
+        return RH_OK;
+    }
+};
+
+namespace {
+
+int lock_sizes(rh_sstore *s, std::unique_lock<std::mutex> &g) {
+    g = std::unique_lock<std::mutex>(s->mu);
+    Status st = s->flush();
+    return st.rc ? fail(st.rc, st.msg) : RH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rh_sstore_create(const int *devices, int n, const rh_schema *schema, rh_sstore **out) {
+    if (!devices || n < 1 || n > 64 || !schema || !out) return fail(RH_ERR_ARG, "sstore: bad arguments");
+    rh_sstore *s = new (std::nothrow) rh_sstore();
+    if (!s) return fail(RH_ERR_OOM, "sstore: host allocation failed");
+    s->schema = *schema;
+    s->G = n;
+    s->kl = (size_t)key_row(*schema);
+    s->shards.assign(n, nullptr);
+    for (int i = 0; i < n; i++) {
+        const int rc = rh_store_create(devices[i], schema, &s->shards[i]);
+        if (rc) {
+            const std::string msg = rh_last_error();
+            for (rh_store *t : s->shards) rh_store_destroy(t);
+            delete s;
+            return fail(rc, msg);
+        }
+    }
+    s->sizes.assign(n, 0);
+    s->off.assign(n + 1, 0);
+    s->sizes_ok = true;
+    s->dirty.assign(n, 0);
+    s->even_splitters();
+    try {
+        s->pool = new ShardPool(n);
+    } catch (...) {
+        for (rh_store *t : s->shards) rh_store_destroy(t);
+        delete s;
+        return fail(RH_ERR_OOM, "sstore: cannot start the shard threads");
+    }
+    *out = s;
+    return RH_OK;
+}
+
+int rh_sstore_destroy(rh_sstore *s) {
+    if (!s) return RH_OK;
+    delete s->pool;
+    for (rh_store *t : s->shards) rh_store_destroy(t);
+    delete s;
+    return RH_OK;
+}
+
+int rh_sstore_shard_count(rh_sstore *s) { return s ? s->G : fail(RH_ERR_ARG, "sstore is NULL"); }
+
+int rh_sstore_shard(rh_sstore *s, int i, rh_store **out) {
+    if (!s || !out || i < 0 || i >= s->G) return fail(RH_ERR_ARG, "sstore: bad shard index");
+    *out = s->shards[i];
+    return RH_OK;
+}
+
+int rh_sstore_splitters(rh_sstore *s, void *out) {
+    if (!s || (s->G > 1 && !out)) return fail(RH_ERR_ARG, "NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    if (s->G > 1) memcpy(out, s->split.data(), s->split.size());
+    return RH_OK;
+}
+
+int rh_sstore_set_splitters(rh_sstore *s, const void *keys) {
+    if (!s || (s->G > 1 && !keys)) return fail(RH_ERR_ARG, "NULL");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    if (s->total() != 0) return fail(RH_ERR_STATE, "sstore: splitters can only be set on an empty map");
+    const uint8_t *k = static_cast<const uint8_t *>(keys);
+    for (int j = 1; j + 1 < s->G; j++)
+        if (s->cmp(k + (j - 1) * s->kl, k + j * s->kl) > 0) return fail(RH_ERR_ARG, "sstore: splitters must not decrease");
+    if (s->G > 1) s->split.assign(k, k + (size_t)(s->G - 1) * s->kl);
+    return RH_OK;
+}
+
+int rh_sstore_load(rh_sstore *s, const rh_columns *h, size_t n) {
+    if (!s || !h) return fail(RH_ERR_ARG, "NULL");
+    if (n && s->kl && !h->keys) return fail(RH_ERR_ARG, "keys column is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const int G = s->G;
+    const size_t kl = s->kl, vr = value_row(s->schema);
+    const uint8_t *keys = static_cast<const uint8_t *>(h->keys);
+    std::vector<uint64_t> cut(G + 1);
+    for (int j = 0; j <= G; j++) cut[j] = (uint64_t)((unsigned __int128)n * (unsigned)j / (unsigned)G);
+    // the keys must be strictly increasing across the cuts too (each shard checks its own rows)
+    bool ok = true;
+    for (int j = 1; j < G && ok; j++)
+        if (cut[j] > 0 && cut[j] < n) ok = s->cmp(keys + (cut[j] - 1) * kl, keys + cut[j] * kl) < 0;
+    auto part = [&](int j) {
+        const uint64_t a = cut[j];
+        const bool dated = s->schema.record_kind == RH_REC_DATED;
+        auto at = [&](const void *p, size_t w) -> const void * {
+            return p ? static_cast<const uint8_t *>(p) + a * w : nullptr;
+        };
+        return rh_columns{at(h->keys, kl), static_cast<const uint64_t *>(dated ? at(h->phys, 8) : nullptr),
+                          static_cast<const uint32_t *>(dated ? at(h->logical, 4) : nullptr),
+                          static_cast<const uint64_t *>(dated ? at(h->node, 8) : nullptr),
+                          static_cast<const uint8_t *>(at(h->tags, 1)), at(h->values, vr)};
+    };
+    int rc = RH_OK;
+    s->sizes_ok = false;
+    std::fill(s->dirty.begin(), s->dirty.end(), 0);
+    if (!ok) {
+        rc = fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
+    } else {
+        rc = s->each(s->all(), [&](int j) -> int {
+            const rh_columns c = part(j);
+            return rh_store_load(s->shards[j], &c, cut[j + 1] - cut[j]);
+        });
+    }
+    if (rc) {  // the map is left empty, as a single store is after a failed load
+        const std::string msg = rh_last_error();
+        const rh_columns none{};
+        for (int j = 0; j < G; j++) (void)rh_store_load(s->shards[j], &none, 0);
+        s->even_splitters();
+        s->sizes.assign(G, 0), s->off.assign(G + 1, 0), s->sizes_ok = true;
+        return fail(rc, msg);
+    }
+    if (n) {
+        s->split.resize((size_t)(G - 1) * kl);
+        for (int j = 1; j < G; j++) memcpy(s->split.data() + (j - 1) * kl, keys + cut[j] * kl, kl);
+    } else {
+        s->even_splitters();
+    }
+    for (int j = 0; j < G; j++) s->sizes[j] = cut[j + 1] - cut[j];
+    for (int j = 0; j <= G; j++) s->off[j] = cut[j];
+    s->sizes_ok = true;
+    return RH_OK;
+}
+
+int rh_sstore_stage(rh_sstore *s, const rh_columns *h, const uint8_t *ops, size_t m) {
+    if (!s || !h || (m && !ops)) return fail(RH_ERR_ARG, "NULL");
+    if (m == 0) return RH_OK;
+    if (s->kl && !h->keys) return fail(RH_ERR_ARG, "keys column is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const uint8_t *keys = static_cast<const uint8_t *>(h->keys);
+    for (size_t i = 0; i < m; i++)
+        if (ops[i] > 1) return fail(RH_ERR_ARG, "op must be 0 (insert) or 1 (delete)");
+    int rc;
+    if (m == 1 || s->G == 1) {  // the Rsos::insert path: one row, no copies
+        const int t = s->G == 1 ? 0 : s->owner(keys);
+        if ((rc = rh_store_stage(s->shards[t], h, ops, m))) return rc;
+        s->dirty[t] = 1;
+        s->sizes_ok = false;
+        return RH_OK;
+    }
+    try {
+        std::vector<std::vector<uint32_t>> rows;
+        s->route(keys, m, rows);
+        for (int t = 0; t < s->G; t++) {
+            if (rows[t].empty()) continue;
+            rh_sstore::Part p;
+            s->gather(*h, ops, rows[t], p);
+            const rh_columns c = p.cols();
+            if ((rc = rh_store_stage(s->shards[t], &c, p.ops.data(), p.m))) return rc;
+            s->dirty[t] = 1;
+            s->sizes_ok = false;
+        }
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "stage: host allocation failed");
+    }
+    return RH_OK;
+}
+
+int rh_sstore_apply(rh_sstore *s, const rh_columns *h, const uint8_t *ops, size_t m, uint64_t *n_new, uint64_t *n_over,
+                    uint64_t *n_del) {
+    if (!s || !h || (m && !ops)) return fail(RH_ERR_ARG, "NULL");
+    if (m && s->kl && !h->keys) return fail(RH_ERR_ARG, "keys column is NULL");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);  // staged rows first: they were staged before this batch
+    if (rc) return rc;
+    uint64_t c[64][3] = {};
+    try {
+        std::vector<std::vector<uint32_t>> rows;
+        s->route(static_cast<const uint8_t *>(h->keys), m, rows);
+        std::vector<rh_sstore::Part> parts(s->G);
+        std::vector<int> idx;
+        for (int t = 0; t < s->G; t++)
+            if (!rows[t].empty()) idx.push_back(t);
+        std::vector<uint8_t> dup(s->G, 0);
+        // every shard's rows gathered and checked first: a batch with a repeated key changes no shard
+        if ((rc = s->each(idx, [&](int t) -> int {
+                 s->gather(*h, ops, rows[t], parts[t]);
+                 dup[t] = s->has_duplicates(parts[t].keys.data(), parts[t].m);
+                 return RH_OK;
+             })))
+            return rc;
+        for (int t : idx)
+            if (dup[t]) return fail(RH_ERR_ARG, "duplicate key within one batch");
+        s->sizes_ok = false;
+        rc = s->each(idx, [&](int t) -> int {
+            const rh_columns cols = parts[t].cols();
+            return rh_store_apply(s->shards[t], &cols, parts[t].ops.data(), parts[t].m, &c[t][0], &c[t][1], &c[t][2]);
+        });
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "apply: host allocation failed");
+    }
+    uint64_t tot[3] = {0, 0, 0};
+    for (int t = 0; t < s->G; t++)
+        for (int i = 0; i < 3; i++) tot[i] += c[t][i];
+    if (n_new) *n_new = tot[0];
+    if (n_over) *n_over = tot[1];
+    if (n_del) *n_del = tot[2];
+    return rc;
+}
+
+int rh_sstore_len(rh_sstore *s, uint64_t *out) {
+    if (!s || !out) return fail(RH_ERR_ARG, "NULL");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    *out = s->total();
+    return RH_OK;
+}
+
+int rh_sstore_aggregates(rh_sstore *s, const uint64_t *lo, const uint64_t *hi, size_t r, rh_aggregate *out) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    if (r && (!lo || !hi || !out)) return fail(RH_ERR_ARG, "NULL buffer");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    try {
+        return s->split_ranks(0, nullptr, nullptr, r, lo, hi, out);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "aggregates: host allocation failed");
+    }
+}
+
+int rh_sstore_aggregate_keys(rh_sstore *s, int lo_kind, const void *lo_key, int hi_kind, const void *hi_key,
+                             rh_aggregate *out) {
+    if (!s || !out) return fail(RH_ERR_ARG, "NULL");
+    if (lo_kind < 0 || lo_kind > 2 || hi_kind < 0 || hi_kind > 2) return fail(RH_ERR_ARG, "bad bound kind");
+    if ((lo_kind && !lo_key) || (hi_kind && !hi_key)) return fail(RH_ERR_ARG, "bound key is NULL");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    const uint8_t *lk = static_cast<const uint8_t *>(lo_key), *hk = static_cast<const uint8_t *>(hi_key);
+    // the shards the range can touch: from the one holding its lower bound to the one holding the
+    // keys just below its upper bound (Included(k) reaches k's own shard)
+    const int a = lo_kind ? s->owner(lk) : 0;
+    const int b = !hi_kind ? s->G - 1 : hi_kind == 1 ? s->owner(hk) : s->owner_below(hk);
+    *out = kZero;
+    if (a > b) return RH_OK;  // an inverted or empty range: ZERO (rbsr/src/protocol.rs:230-232)
+    std::vector<rh_aggregate> part(s->G, kZero);
+    std::vector<int> edge{a};
+    if (b != a) edge.push_back(b);
+    rc = s->each(edge, [&](int t) -> int {
+        return rh_store_aggregate_keys(s->shards[t], t == a ? lo_kind : 0, lo_key, t == b ? hi_kind : 0, hi_key, &part[t]);
+    });
+    if (rc) return rc;
+    for (int t = a + 1; t < b; t++)
+        if ((rc = rh_store_aggregate_keys(s->shards[t], 0, nullptr, 0, nullptr, &part[t]))) return rc;
+    for (int t = a; t <= b; t++) agg_add(*out, part[t]);
+    return RH_OK;
+}
+
+int rh_sstore_ranks(rh_sstore *s, const void *keys, size_t m, uint64_t *out) {
+    if (!s || (m && (!keys || !out))) return fail(RH_ERR_ARG, "NULL");
+    if (m == 0) return RH_OK;
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    const uint8_t *k = static_cast<const uint8_t *>(keys);
+    if (m == 1) {
+        const int t = s->owner(k);
+        uint64_t r = 0;
+        if ((rc = rh_store_rank(s->shards[t], k, &r))) return rc;
+        *out = s->off[t] + r;
+        return RH_OK;
+    }
+    try {
+        std::vector<std::vector<uint32_t>> rows;
+        s->route(k, m, rows);
+        std::vector<std::vector<uint8_t>> qk(s->G);
+        std::vector<std::vector<uint64_t>> qr(s->G);
+        std::vector<int> idx;
+        for (int t = 0; t < s->G; t++)
+            if (!rows[t].empty()) idx.push_back(t);
+        rc = s->each(idx, [&](int t) -> int {
+            qk[t].resize(rows[t].size() * s->kl + 1);
+            for (size_t i = 0; i < rows[t].size(); i++) memcpy(&qk[t][i * s->kl], k + rows[t][i] * s->kl, s->kl);
+            qr[t].resize(rows[t].size());
+            return rh_store_ranks(s->shards[t], qk[t].data(), rows[t].size(), qr[t].data());
+        });
+        if (rc) return rc;
+        for (int t : idx)
+            for (size_t i = 0; i < rows[t].size(); i++) out[rows[t][i]] = s->off[t] + qr[t][i];
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "ranks: host allocation failed");
+    }
+    return RH_OK;
+}
+
+int rh_sstore_rank(rh_sstore *s, const void *key, uint64_t *out) { return rh_sstore_ranks(s, key, 1, out); }
+
+int rh_sstore_keys(rh_sstore *s, uint64_t lo, uint64_t hi, void *host_out) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    if (lo > hi || hi > s->total()) return fail(RH_ERR_ARG, "bad rank range");
+    if (hi == lo) return RH_OK;
+    if (!host_out) return fail(RH_ERR_ARG, "host_out NULL");
+    std::vector<int> idx;
+    for (int t = 0; t < s->G; t++)
+        if (s->off[t] < hi && s->off[t + 1] > lo) idx.push_back(t);
+    return s->each(idx, [&](int t) -> int {
+        uint64_t a, b;
+        s->piece(t, lo, hi, &a, &b);
+        return rh_store_keys(s->shards[t], a, b, static_cast<uint8_t *>(host_out) + (s->off[t] + a - lo) * s->kl);
+    });
+}
+
+int rh_sstore_select(rh_sstore *s, uint64_t r, void *key_out) {
+    if (!s || !key_out) return fail(RH_ERR_ARG, "NULL");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    if (r >= s->total()) return fail(RH_ERR_ARG, "select: rank out of range (r >= size)");
+    const int t = s->shard_of_rank(r);
+    return rh_store_select(s->shards[t], r - s->off[t], key_out);
+}
+
+int rh_sstore_fingerprints(rh_sstore *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    if (lo > hi || hi > s->total()) return fail(RH_ERR_ARG, "bad rank range");
+    if (hi == lo) return RH_OK;
+    if (!host_out) return fail(RH_ERR_ARG, "host_out NULL");
+    std::vector<int> idx;
+    for (int t = 0; t < s->G; t++)
+        if (s->off[t] < hi && s->off[t + 1] > lo) idx.push_back(t);
+    return s->each(idx, [&](int t) -> int {
+        uint64_t a, b;
+        s->piece(t, lo, hi, &a, &b);
+        return rh_store_fingerprints(s->shards[t], a, b, host_out + (s->off[t] + a - lo) * 32);
+    });
+}
+
+int rh_sstore_resolve_segments(rh_sstore *s, size_t r, const uint8_t *start_kinds, const void *start_keys,
+                               const uint8_t *end_kinds, const void *end_keys, uint64_t *raw_start, uint64_t *raw_end,
+                               rh_aggregate *local) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    if (r == 0) return RH_OK;
+    if (!start_kinds || !end_kinds || !raw_start || !raw_end || !local) return fail(RH_ERR_ARG, "NULL buffer");
+    for (size_t j = 0; j < r; j++) {
+        if (start_kinds[j] > 1 || end_kinds[j] > 1)
+            return fail(RH_ERR_ARG, "segment bound kind must be 0 (Unbounded) or 1 (Included / Excluded)");
+        if ((start_kinds[j] && !start_keys) || (end_kinds[j] && !end_keys)) return fail(RH_ERR_ARG, "bound key is NULL");
+    }
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    try {
+        std::vector<uint8_t> zero(r * s->kl + 1, 0);
+        const uint8_t *sk = start_keys ? static_cast<const uint8_t *>(start_keys) : zero.data();
+        const uint8_t *ek = end_keys ? static_cast<const uint8_t *>(end_keys) : zero.data();
+        std::vector<size_t> J(r);
+        for (size_t j = 0; j < r; j++) J[j] = j;
+        return s->resolve_list(J, start_kinds, sk, end_kinds, ek, raw_start, raw_end, local);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "resolve: host allocation failed");
+    }
+}
+
+int rh_sstore_split_segments(rh_sstore *s, size_t m, const uint64_t *select_ranks, void *keys_out, size_t q,
+                             const uint64_t *lo, const uint64_t *hi, rh_aggregate *out) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    if ((m && (!select_ranks || !keys_out)) || (q && (!lo || !hi || !out))) return fail(RH_ERR_ARG, "NULL buffer");
+    if (m == 0 && q == 0) return RH_OK;
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    try {
+        return s->split_ranks(m, select_ranks, static_cast<uint8_t *>(keys_out), q, lo, hi, out);
+    } catch (const std::bad_alloc &) {
+        return fail(RH_ERR_OOM, "split: host allocation failed");
+    }
+}
+
+int rh_sstore_protocol_round(rh_sstore *s, int policy, uint64_t fan_out, const rh_segments *active,
+                             rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome) {
+    if (!s || !active || !children || !enumerations) return fail(RH_ERR_ARG, "NULL");
+    if (policy != RH_POLICY_FIXED_FAN_OUT && policy != RH_POLICY_SQRT_FAN_OUT) return fail(RH_ERR_ARG, "unknown policy");
+    const size_t r = active->n;
+    if (r && (!active->start_kinds || !active->end_kinds || !active->aggregates))
+        return fail(RH_ERR_ARG, "active segments: NULL buffer");
+    for (size_t j = 0; j < r; j++) {
+        if (active->start_kinds[j] > 1 || active->end_kinds[j] > 1)
+            return fail(RH_ERR_ARG, "segment bound kind must be 0 (Unbounded) or 1 (Included / Excluded)");
+        if ((active->start_kinds[j] && !active->start_keys) || (active->end_kinds[j] && !active->end_keys))
+            return fail(RH_ERR_ARG, "bound key is NULL");
+    }
+    *children = rh_segments{};
+    *enumerations = rh_segments{};
+    if (outcome) *outcome = rh_round_outcome{};
+    if (r == 0) return RH_OK;
+    std::unique_lock<std::mutex> g;
+    int rc = lock_sizes(s, g);
+    if (rc) return rc;
+    try {
+        rc = s->protocol_round(policy, fan_out, *active, children, enumerations, outcome);
+    } catch (const std::bad_alloc &) {
+        rc = fail(RH_ERR_OOM, "protocol round: host allocation failed");
+    }
+    if (rc) {
+        *children = rh_segments{};
+        *enumerations = rh_segments{};
+        if (outcome) *outcome = rh_round_outcome{};
+    }
+    return rc;
+}
+
+int rh_sstore_set_host_tier(rh_sstore *s, int enable, uint64_t round_max) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    return s->each(s->all(), [&](int t) -> int { return rh_store_set_host_tier(s->shards[t], enable, round_max); });
+}
+
+int rh_sstore_set_tier_policy(rh_sstore *s, int keep_fresh) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    return s->each(s->all(), [&](int t) -> int { return rh_store_set_tier_policy(s->shards[t], keep_fresh); });
+}
+
+int rh_sstore_reserve(rh_sstore *s, uint64_t rows, uint64_t batch_rows) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    const uint64_t per = (rows + s->G - 1) / s->G;
+    return s->each(s->all(), [&](int t) -> int { return rh_store_reserve(s->shards[t], per + per / 8, batch_rows); });
+}
+
+int rh_sstore_compact(rh_sstore *s) {
+    if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
+    std::lock_guard<std::mutex> g(s->mu);
+    s->sizes_ok = false;
+    return s->each(s->all(), [&](int t) -> int { return rh_store_compact(s->shards[t]); });
+}
+
+}  // extern "C"

@@ -125,6 +125,32 @@ SIGNATURES = [
     ("rh_estore_aggregates", C.c_int, [P, U64P, U64P, SZ, P]),
     ("rh_estore_fingerprints", C.c_int, [P, C.c_uint64, C.c_uint64, U8P]),
     ("rh_estore_set_host_tier", C.c_int, [P, C.c_int]),
+    ("rh_sstore_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(Schema), C.POINTER(C.c_void_p)]),
+    ("rh_sstore_destroy", C.c_int, [P]),
+    ("rh_sstore_shard_count", C.c_int, [P]),
+    ("rh_sstore_shard", C.c_int, [P, C.c_int, C.POINTER(C.c_void_p)]),
+    ("rh_sstore_splitters", C.c_int, [P, VP]),
+    ("rh_sstore_set_splitters", C.c_int, [P, VP]),
+    ("rh_sstore_load", C.c_int, [P, C.POINTER(Columns), SZ]),
+    ("rh_sstore_stage", C.c_int, [P, C.POINTER(Columns), U8P, SZ]),
+    ("rh_sstore_apply", C.c_int, [P, C.POINTER(Columns), U8P, SZ, C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("rh_sstore_len", C.c_int, [P, C.POINTER(C.c_uint64)]),
+    ("rh_sstore_aggregates", C.c_int, [P, U64P, U64P, SZ, P]),
+    ("rh_sstore_aggregate_keys", C.c_int, [P, C.c_int, VP, C.c_int, VP, C.POINTER(Aggregate)]),
+    ("rh_sstore_rank", C.c_int, [P, VP, C.POINTER(C.c_uint64)]),
+    ("rh_sstore_ranks", C.c_int, [P, VP, SZ, U64P]),
+    ("rh_sstore_select", C.c_int, [P, C.c_uint64, VP]),
+    ("rh_sstore_keys", C.c_int, [P, C.c_uint64, C.c_uint64, VP]),
+    ("rh_sstore_fingerprints", C.c_int, [P, C.c_uint64, C.c_uint64, U8P]),
+    ("rh_sstore_resolve_segments", C.c_int, [P, SZ, U8P, VP, U8P, VP, U64P, U64P, P]),
+    ("rh_sstore_split_segments", C.c_int, [P, SZ, U64P, VP, SZ, U64P, U64P, P]),
+    ("rh_sstore_protocol_round", C.c_int, [P, C.c_int, C.c_uint64, C.POINTER(Segments), C.POINTER(Segments),
+                                           C.POINTER(Segments), C.POINTER(RoundOutcome)]),
+    ("rh_sstore_set_host_tier", C.c_int, [P, C.c_int, C.c_uint64]),
+    ("rh_sstore_set_tier_policy", C.c_int, [P, C.c_int]),
+    ("rh_sstore_reserve", C.c_int, [P, C.c_uint64, C.c_uint64]),
+    ("rh_sstore_compact", C.c_int, [P]),
     ("rh_debug_fail_point", C.c_int, [C.c_char_p]),
     ("rh_debug_reload_timing", C.c_int, [C.c_int]),
     ("rh_debug_last_reload_us", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),

@@ -258,8 +258,8 @@ def protocol_round_segments(store, policy, active: Segments,
         raise TypeError("protocol_round_segments runs FixedFanOut / SqrtFanOut; use protocol_round_with_policy")
     kl = store.schema.key_row
     a, cc, ec, oc = active.c(), A.Segments(), A.Segments(), A.RoundOutcome()
-    A.check(A.lib().rh_store_protocol_round(store._h, kind, b, C.byref(a), C.byref(cc), C.byref(ec), C.byref(oc)),
-            "rh_store_protocol_round")
+    A.check(store._f("protocol_round")(store._h, kind, b, C.byref(a), C.byref(cc), C.byref(ec), C.byref(oc)),
+            store._P + "protocol_round")
     return (_wrap(cc, kl, copy, True), _wrap(ec, kl, copy, False),
             RoundOutcome(int(oc.skipped), int(oc.enumerated), int(oc.split), int(oc.children),
                          int(oc.dropped_malformed)))

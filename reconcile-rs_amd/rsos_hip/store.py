@@ -61,6 +61,11 @@ DEFAULT_HOST_TIER = False
 
 
 class GpuFingerprintStore:
+    _P = "rh_store_"  # the entry points' prefix (the sharded store's are rh_sstore_*)
+
+    def _f(self, name: str):
+        return getattr(A.lib(), self._P + name)
+
     def __init__(self, schema: RecordSchema, device: int = 0, host_tier: Optional[bool] = None):
         self.schema = schema
         self._s = schema.c()
@@ -72,7 +77,7 @@ class GpuFingerprintStore:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            A.lib().rh_store_destroy(self._h)
+            self._f("destroy")(self._h)
             self._h = None
 
     def __del__(self):
@@ -111,14 +116,14 @@ class GpuFingerprintStore:
         """Replace the contents with records sorted by key, without duplicates."""
         c, held = self._columns(cols)
         n = len(held["keys"]) if "keys" in held else len(held["values"])
-        A.check(A.lib().rh_store_load(self._h, C.byref(c), n), "rh_store_load")
+        A.check(self._f("load")(self._h, C.byref(c), n), "rh_store_load")
 
     def load_bulk_device(self, cols) -> None:
         """load_bulk from device (torch) columns already resident in HBM."""
         from .device import _check_cols, _columns
         n = _check_cols(self.schema, cols)
         c = _columns(cols)
-        A.check(A.lib().rh_store_load_device(self._h, C.byref(c), n, _torch_stream()), "rh_store_load_device")
+        A.check(self._f("load_device")(self._h, C.byref(c), n, _torch_stream()), "rh_store_load_device")
 
     def apply_device(self, cols, ops=None) -> Tuple[int, int, int]:
         """apply() with device (torch) columns / ops; returns (new, overwritten, deleted)."""
@@ -128,7 +133,7 @@ class GpuFingerprintStore:
             raise ValueError("ops must be m device bytes")
         c = _columns(cols)
         a, b, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        A.check(A.lib().rh_store_apply_device(self._h, C.byref(c), None if ops is None else ops.data_ptr(), m,
+        A.check(self._f("apply_device")(self._h, C.byref(c), None if ops is None else ops.data_ptr(), m,
                                               C.byref(a), C.byref(b), C.byref(d), _torch_stream()),
                 "rh_store_apply_device")
         return int(a.value), int(b.value), int(d.value)
@@ -152,46 +157,46 @@ class GpuFingerprintStore:
                 raise ValueError("ops must be m device bytes")
             optr[i] = None if o is None else o.data_ptr()
         out = (C.c_uint64 * (3 * max(k, 1)))()
-        A.check(A.lib().rh_store_apply_device_many(self._h, cols, None if ops is None else optr, ns, k, out,
+        A.check(self._f("apply_device_many")(self._h, cols, None if ops is None else optr, ns, k, out,
                                                    _torch_stream()), "rh_store_apply_device_many")
         return [(int(out[3 * i]), int(out[3 * i + 1]), int(out[3 * i + 2])) for i in range(k)]
 
     def compact(self) -> None:
-        A.check(A.lib().rh_store_compact(self._h), "rh_store_compact")
+        A.check(self._f("compact")(self._h), "rh_store_compact")
 
     def set_host_tier(self, enable: bool = True, round_max: int = 0) -> None:
         """Answer rank / select / aggregate and protocol rounds of at most `round_max` segments
         (0: the default, 128) from a host copy of the keys and fingerprint prefix sums plus a tree
         of every later batch's signed deltas (rh_store_set_host_tier): a batch updates it in
         O(batch log n); the base is copied again only after a load or a delta grown past base / 8."""
-        A.check(A.lib().rh_store_set_host_tier(self._h, 1 if enable else 0, round_max), "rh_store_set_host_tier")
+        A.check(self._f("set_host_tier")(self._h, 1 if enable else 0, round_max), "rh_store_set_host_tier")
 
     def set_compaction(self, divisor: int, min_rows: int) -> None:
-        A.check(A.lib().rh_store_set_compaction(self._h, divisor, min_rows), "rh_store_set_compaction")
+        A.check(self._f("set_compaction")(self._h, divisor, min_rows), "rh_store_set_compaction")
 
     def reserve(self, rows: int, batch_rows: int) -> None:
         """Size every device buffer for `rows` resident rows and batches of up to `batch_rows`
         (compacts first; contents unchanged), so later batches never reallocate."""
-        A.check(A.lib().rh_store_reserve(self._h, rows, batch_rows), "rh_store_reserve")
+        A.check(self._f("reserve")(self._h, rows, batch_rows), "rh_store_reserve")
 
     def stats(self) -> Dict[str, int]:
         b, d, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        A.check(A.lib().rh_store_stats(self._h, C.byref(b), C.byref(d), C.byref(c)), "rh_store_stats")
+        A.check(self._f("stats")(self._h, C.byref(b), C.byref(d), C.byref(c)), "rh_store_stats")
         return {"base_rows": int(b.value), "delta_rows": int(d.value), "compactions": int(c.value)}
 
     def tier_sync(self) -> None:
         """Wait until the host tier is fresh (its background refresh landed): rh_store_tier_sync."""
-        A.check(A.lib().rh_store_tier_sync(self._h), "rh_store_tier_sync")
+        A.check(self._f("tier_sync")(self._h), "rh_store_tier_sync")
 
     def set_tier_policy(self, keep_fresh: bool) -> None:
         """Whether writes keep the host tier fresh (wait for the copies they cause; the default)
         or never wait (questions go to the device meanwhile): rh_store_set_tier_policy."""
-        A.check(A.lib().rh_store_set_tier_policy(self._h, 1 if keep_fresh else 0), "rh_store_set_tier_policy")
+        A.check(self._f("set_tier_policy")(self._h, 1 if keep_fresh else 0), "rh_store_set_tier_policy")
 
     def batch_stats(self) -> Dict[str, int]:
         """Batches applied by the small-batch path and by the large-batch path (rh_store_batch_stats)."""
         a, b = C.c_uint64(), C.c_uint64()
-        A.check(A.lib().rh_store_batch_stats(self._h, C.byref(a), C.byref(b)), "rh_store_batch_stats")
+        A.check(self._f("batch_stats")(self._h, C.byref(a), C.byref(b)), "rh_store_batch_stats")
         return {"small": int(a.value), "large": int(b.value)}
 
     def stage(self, cols: Dict[str, np.ndarray], ops: np.ndarray) -> None:
@@ -199,14 +204,14 @@ class GpuFingerprintStore:
         store; a key staged more than once keeps its last operation."""
         c, held = self._columns(cols)
         ops_a = np.ascontiguousarray(ops, dtype=np.uint8)
-        A.check(A.lib().rh_store_stage(self._h, C.byref(c), _np_ptr(ops_a), len(ops_a)), "rh_store_stage")
+        A.check(self._f("stage")(self._h, C.byref(c), _np_ptr(ops_a), len(ops_a)), "rh_store_stage")
 
     def tier_stats(self) -> Dict[str, int]:
         """The host tier's bookkeeping (rh_store_tier_stats): rows of its base copy and its delta
         entries (tree + run copy) while fresh, copies taken from the device (base refreshes and run
         copies) and batch folds so far."""
         b, d, r, f = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
-        A.check(A.lib().rh_store_tier_stats(self._h, C.byref(b), C.byref(d), C.byref(r), C.byref(f)),
+        A.check(self._f("tier_stats")(self._h, C.byref(b), C.byref(d), C.byref(r), C.byref(f)),
                 "rh_store_tier_stats")
         return {"base_rows": int(b.value), "delta_entries": int(d.value), "refreshes": int(r.value),
                 "folds": int(f.value)}
@@ -214,7 +219,7 @@ class GpuFingerprintStore:
     # ---- Rsos<K> -------------------------------------------------------------------------
     def size(self) -> int:
         out = C.c_uint64()
-        A.check(A.lib().rh_store_len(self._h, C.byref(out)), "rh_store_len")
+        A.check(self._f("len")(self._h, C.byref(out)), "rh_store_len")
         return int(out.value)
 
     __len__ = size
@@ -224,14 +229,15 @@ class GpuFingerprintStore:
         lo = None if rng.start is None else C.create_string_buffer(self._key_bytes(rng.start))
         hi = None if rng.end is None else C.create_string_buffer(self._key_bytes(rng.end))
         out = A.Aggregate()
-        A.check(A.lib().rh_store_aggregate_keys(self._h, KeyRange._K[rng.start_kind], lo,
+        A.check(self._f("aggregate_keys")(self._h, KeyRange._K[rng.start_kind], lo,
                                                 KeyRange._K[rng.end_kind], hi, C.byref(out)),
                 "rh_store_aggregate_keys")
         return Aggregate.from_c(out)
 
     def aggregate_ranks(self, lo: int, hi: int) -> Aggregate:
         out = A.Aggregate()
-        A.check(A.lib().rh_store_aggregate(self._h, lo, hi, C.byref(out)), "rh_store_aggregate")
+        A.check(self._f("aggregates")(self._h, _np_ptr(np.array([lo], np.uint64)), _np_ptr(np.array([hi], np.uint64)), 1, C.byref(out)),
+                self._P + "aggregates")
         return Aggregate.from_c(out)
 
     def aggregates_ranks(self, lo: Sequence[int], hi: Sequence[int]):
@@ -239,13 +245,13 @@ class GpuFingerprintStore:
         hi_a = np.ascontiguousarray(hi, dtype=np.uint64)
         r = len(lo_a)
         out = (A.Aggregate * max(r, 1))()
-        A.check(A.lib().rh_store_aggregates(self._h, _np_ptr(lo_a), _np_ptr(hi_a), r, out),
+        A.check(self._f("aggregates")(self._h, _np_ptr(lo_a), _np_ptr(hi_a), r, out),
                 "rh_store_aggregates")
         return [Aggregate.from_c(out[j]) for j in range(r)]
 
     def rank(self, z: Key) -> int:
         out = C.c_uint64()
-        A.check(A.lib().rh_store_rank(self._h, C.create_string_buffer(self._key_bytes(z)), C.byref(out)),
+        A.check(self._f("rank")(self._h, C.create_string_buffer(self._key_bytes(z)), C.byref(out)),
                 "rh_store_rank")
         return int(out.value)
 
@@ -253,7 +259,7 @@ class GpuFingerprintStore:
         if r < 0 or r >= self.size():
             raise IndexError("select: r >= size()")
         buf = C.create_string_buffer(max(self.schema.key_row, 1))
-        A.check(A.lib().rh_store_select(self._h, r, buf), "rh_store_select")
+        A.check(self._f("select")(self._h, r, buf), "rh_store_select")
         return self._key_out(buf.raw[: self.schema.key_row])
 
     def enumerate(self, rng: Optional[KeyRange] = None) -> Iterator[Tuple[Key, int]]:
@@ -270,7 +276,7 @@ class GpuFingerprintStore:
             return
         kl = self.schema.key_row
         buf = np.zeros((hi - lo) * kl, np.uint8)
-        A.check(A.lib().rh_store_keys(self._h, lo, hi, _np_ptr(buf)), "rh_store_keys")
+        A.check(self._f("keys")(self._h, lo, hi, _np_ptr(buf)), "rh_store_keys")
         for r in range(lo, hi):
             yield self._key_out(buf[(r - lo) * kl:(r - lo + 1) * kl].tobytes()), r
 
@@ -278,13 +284,13 @@ class GpuFingerprintStore:
         """Rank of each of m keys (rows of key_len bytes) in one device search."""
         k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, self.schema.key_row)
         out = np.zeros(k.shape[0], np.uint64)
-        A.check(A.lib().rh_store_ranks(self._h, _np_ptr(k), k.shape[0], _np_ptr(out)), "rh_store_ranks")
+        A.check(self._f("ranks")(self._h, _np_ptr(k), k.shape[0], _np_ptr(out)), "rh_store_ranks")
         return out
 
     def fingerprints(self, lo: int = 0, hi: Optional[int] = None) -> np.ndarray:
         hi = self.size() if hi is None else hi
         out = np.zeros((max(hi - lo, 0), 32), np.uint8)
-        A.check(A.lib().rh_store_fingerprints(self._h, lo, hi, _np_ptr(out) if hi > lo else None),
+        A.check(self._f("fingerprints")(self._h, lo, hi, _np_ptr(out) if hi > lo else None),
                 "rh_store_fingerprints")
         return out
 
@@ -305,7 +311,7 @@ class GpuFingerprintStore:
                 ekeys[j] = np.frombuffer(self._key_bytes(seg.end), np.uint8)
         lo, hi = np.zeros(max(r, 1), np.uint64), np.zeros(max(r, 1), np.uint64)
         out = (A.Aggregate * max(r, 1))()
-        A.check(A.lib().rh_store_resolve_segments(self._h, r, _np_ptr(sk), _np_ptr(skeys), _np_ptr(ek),
+        A.check(self._f("resolve_segments")(self._h, r, _np_ptr(sk), _np_ptr(skeys), _np_ptr(ek),
                                                   _np_ptr(ekeys), _np_ptr(lo), _np_ptr(hi), out),
                 "rh_store_resolve_segments")
         return lo[:r], hi[:r], [Aggregate.from_c(out[j]) for j in range(r)]
@@ -320,7 +326,7 @@ class GpuFingerprintStore:
         m, q = len(sel), len(lo_a)
         keys = np.zeros((max(m, 1), kl), np.uint8)
         out = (A.Aggregate * max(q, 1))()
-        A.check(A.lib().rh_store_split_segments(self._h, m, _np_ptr(sel), _np_ptr(keys), q, _np_ptr(lo_a),
+        A.check(self._f("split_segments")(self._h, m, _np_ptr(sel), _np_ptr(keys), q, _np_ptr(lo_a),
                                                 _np_ptr(hi_a), out), "rh_store_split_segments")
         return [self._key_out(keys[i].tobytes()) for i in range(m)], [Aggregate.from_c(out[j]) for j in range(q)]
 
@@ -329,7 +335,7 @@ class GpuFingerprintStore:
         c, held = self._columns(cols)
         ops_a = np.ascontiguousarray(ops, dtype=np.uint8)
         a, b, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        A.check(A.lib().rh_store_apply(self._h, C.byref(c), _np_ptr(ops_a), len(ops_a), C.byref(a), C.byref(b),
+        A.check(self._f("apply")(self._h, C.byref(c), _np_ptr(ops_a), len(ops_a), C.byref(a), C.byref(b),
                                        C.byref(d)), "rh_store_apply")
         return int(a.value), int(b.value), int(d.value)
 

@@ -4,6 +4,9 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
+pub const RH_ABI_VERSION: c_int = 1;
+pub const RH_BLOCK: usize = 256;
+pub const RH_SUPER: usize = 65536;
 pub const RH_OK: c_int = 0;
 pub const RH_KEY_UNIT: i32 = 0;
 pub const RH_KEY_U32: i32 = 1;
@@ -53,6 +56,11 @@ pub struct rh_store {
 
 #[repr(C)]
 pub struct rh_estore {
+    _private: [u8; 0],
+}
+
+#[repr(C)]
+pub struct rh_sstore {
     _private: [u8; 0],
 }
 
@@ -196,6 +204,38 @@ extern "C" {
                                 out: *mut rh_aggregate) -> c_int;
     pub fn rh_estore_fingerprints(store: *mut rh_estore, lo: u64, hi: u64, host_out: *mut u8) -> c_int;
     pub fn rh_estore_set_host_tier(store: *mut rh_estore, enable: c_int) -> c_int;
+    pub fn rh_sstore_create(devices: *const c_int, n: c_int, schema: *const rh_schema, out: *mut *mut rh_sstore) -> c_int;
+    pub fn rh_sstore_destroy(store: *mut rh_sstore) -> c_int;
+    pub fn rh_sstore_shard_count(store: *mut rh_sstore) -> c_int;
+    pub fn rh_sstore_shard(store: *mut rh_sstore, i: c_int, out: *mut *mut rh_store) -> c_int;
+    pub fn rh_sstore_splitters(store: *mut rh_sstore, out: *mut c_void) -> c_int;
+    pub fn rh_sstore_set_splitters(store: *mut rh_sstore, keys: *const c_void) -> c_int;
+    pub fn rh_sstore_load(store: *mut rh_sstore, cols: *const rh_columns, n: usize) -> c_int;
+    pub fn rh_sstore_stage(store: *mut rh_sstore, cols: *const rh_columns, ops: *const u8, m: usize) -> c_int;
+    pub fn rh_sstore_apply(store: *mut rh_sstore, cols: *const rh_columns, ops: *const u8, n: usize,
+                           n_new: *mut u64, n_over: *mut u64, n_del: *mut u64) -> c_int;
+    pub fn rh_sstore_len(store: *mut rh_sstore, out: *mut u64) -> c_int;
+    pub fn rh_sstore_aggregates(store: *mut rh_sstore, lo: *const u64, hi: *const u64, r: usize,
+                                out: *mut rh_aggregate) -> c_int;
+    pub fn rh_sstore_aggregate_keys(store: *mut rh_sstore, lo_kind: c_int, lo_key: *const c_void, hi_kind: c_int,
+                                    hi_key: *const c_void, out: *mut rh_aggregate) -> c_int;
+    pub fn rh_sstore_rank(store: *mut rh_sstore, key: *const c_void, out: *mut u64) -> c_int;
+    pub fn rh_sstore_ranks(store: *mut rh_sstore, keys: *const c_void, m: usize, out: *mut u64) -> c_int;
+    pub fn rh_sstore_select(store: *mut rh_sstore, r: u64, key_out: *mut c_void) -> c_int;
+    pub fn rh_sstore_keys(store: *mut rh_sstore, lo: u64, hi: u64, host_out: *mut c_void) -> c_int;
+    pub fn rh_sstore_fingerprints(store: *mut rh_sstore, lo: u64, hi: u64, host_out: *mut u8) -> c_int;
+    pub fn rh_sstore_resolve_segments(store: *mut rh_sstore, r: usize, start_kinds: *const u8,
+                                      start_keys: *const c_void, end_kinds: *const u8, end_keys: *const c_void,
+                                      raw_start: *mut u64, raw_end: *mut u64, local: *mut rh_aggregate) -> c_int;
+    pub fn rh_sstore_split_segments(store: *mut rh_sstore, m: usize, select_ranks: *const u64, keys_out: *mut c_void,
+                                    q: usize, lo: *const u64, hi: *const u64, out: *mut rh_aggregate) -> c_int;
+    pub fn rh_sstore_protocol_round(store: *mut rh_sstore, policy: c_int, fan_out: u64, active: *const rh_segments,
+                                    children: *mut rh_segments, enumerations: *mut rh_segments,
+                                    outcome: *mut rh_round_outcome) -> c_int;
+    pub fn rh_sstore_set_host_tier(store: *mut rh_sstore, enable: c_int, round_max: u64) -> c_int;
+    pub fn rh_sstore_set_tier_policy(store: *mut rh_sstore, keep_fresh: c_int) -> c_int;
+    pub fn rh_sstore_reserve(store: *mut rh_sstore, rows: u64, batch_rows: u64) -> c_int;
+    pub fn rh_sstore_compact(store: *mut rh_sstore) -> c_int;
     pub fn rh_debug_fail_point(name: *const c_char) -> c_int;
     pub fn rh_debug_reload_timing(on: c_int) -> c_int;
     pub fn rh_debug_last_reload_us(locate_us: *mut f64, lift_us: *mut f64) -> c_int;

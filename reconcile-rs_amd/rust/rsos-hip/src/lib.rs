@@ -26,10 +26,14 @@
 
 mod encoded;
 mod ffi;
+mod round;
+mod sharded;
 mod sorted;
 mod values;
 
 pub use encoded::HipEncodedMap;
+pub use round::RoundPolicy;
+pub use sharded::HipShardedMap;
 pub use values::{FixedBytes, FixedValue};
 
 use std::ffi::CStr;
@@ -53,27 +57,33 @@ pub trait GpuKey: Ord + Clone + Serialize {
     const LEN: u32;
     /// The key column bytes: LE integer for u32 / u64, the raw bytes for `[u8; N]`.
     fn column_bytes(&self) -> Vec<u8>;
+    /// The key of `LEN` column bytes (the inverse of `column_bytes`: keys the library returns).
+    fn from_column_bytes(b: &[u8]) -> Self;
 }
 
 impl GpuKey for u32 {
     const KIND: i32 = ffi::RH_KEY_U32;
     const LEN: u32 = 4;
     fn column_bytes(&self) -> Vec<u8> { self.to_le_bytes().to_vec() }
+    fn from_column_bytes(b: &[u8]) -> Self { u32::from_le_bytes(b.try_into().expect("4 key bytes")) }
 }
 impl GpuKey for u64 {
     const KIND: i32 = ffi::RH_KEY_U64;
     const LEN: u32 = 8;
     fn column_bytes(&self) -> Vec<u8> { self.to_le_bytes().to_vec() }
+    fn from_column_bytes(b: &[u8]) -> Self { u64::from_le_bytes(b.try_into().expect("8 key bytes")) }
 }
 impl GpuKey for [u8; 16] {
     const KIND: i32 = ffi::RH_KEY_BYTES;
     const LEN: u32 = 16;
     fn column_bytes(&self) -> Vec<u8> { self.to_vec() }
+    fn from_column_bytes(b: &[u8]) -> Self { b.try_into().expect("16 key bytes") }
 }
 impl GpuKey for [u8; 32] {
     const KIND: i32 = ffi::RH_KEY_BYTES;
     const LEN: u32 = 32;
     fn column_bytes(&self) -> Vec<u8> { self.to_vec() }
+    fn from_column_bytes(b: &[u8]) -> Self { b.try_into().expect("32 key bytes") }
 }
 
 /// One record's device columns (what the kernels read to synthesise the canonical encoding).
@@ -135,6 +145,8 @@ pub struct HipFingerprintMap<K, V> {
     store: StoreHandle,
     /// rank-ordered host index (owns K and V; select / enumerate borrow from it)
     entries: sorted::SortedBlocks<K, V>,
+    /// held while a round's outputs (the library's buffers) are read
+    round_mu: std::sync::Mutex<()>,
 }
 
 fn schema<K: GpuKey, V: GpuRecord>() -> ffi::rh_schema {
@@ -211,7 +223,7 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         let store = StoreHandle::create(device, &schema::<K, V>());
         // SAFETY: store was just created.
         check(unsafe { ffi::rh_store_set_host_tier(store.0, 1, 0) }, "rh_store_set_host_tier");
-        HipFingerprintMap { store, entries: sorted::SortedBlocks::new() }
+        HipFingerprintMap { store, entries: sorted::SortedBlocks::new(), round_mu: std::sync::Mutex::new(()) }
     }
 
     /// Whether a write that outgrows the host tier's delta tree waits for the tier's copy
@@ -287,20 +299,32 @@ pub struct RoundCounts {
     pub dropped_malformed: usize,
 }
 
-fn start_key<K: Clone>(b: Bound<&K>) -> Option<K> {
-    match b {
-        Bound::Included(k) | Bound::Excluded(k) => Some(k.clone()),
-        Bound::Unbounded => None,
-    }
-}
-
 impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
-    /// One `rbsr` protocol round under `FixedFanOut(fan_out)` with the store's questions
-    /// batched (`protocol_round_with_policy`, rbsr/src/protocol.rs:212-317; cutoffs
-    /// policy/cutoffs.rs; stride `ceil(span / b)`, fixed_fan_out.rs).  Ranks and `select` come
-    /// from the host mirror; every segment's local aggregate is one device call, and every SPLIT
-    /// child's aggregate a second one -- two device round trips per round instead of one per
-    /// question.  Outputs are appended in the reference's order.
+    /// One `rbsr` protocol round (`protocol_round_with_policy`, rbsr/src/protocol.rs:212-317) answered
+    /// by the library in one call (`rh_store_protocol_round`): from the host tier for rounds of up
+    /// to 128 segments, else in one device round trip.  Outputs are appended in the reference's
+    /// order; any other `RefinementPolicy` goes through `rbsr::protocol_round_with_policy` on the
+    /// `Rsos<K>` surface.
+    pub fn protocol_round(
+        &self,
+        policy: RoundPolicy,
+        active: Vec<rbsr::RangeAggregate<K>>,
+        child_ranges: &mut Vec<rbsr::RangeAggregate<K>>,
+        enumeration_ranges: &mut Vec<rbsr::EnumerationRange<K>>,
+    ) -> RoundCounts {
+        let _g = self.round_mu.lock().unwrap_or_else(|e| e.into_inner());
+        let store = self.store.0;
+        // SAFETY: the handle is live for &self; run_round passes valid segment buffers.
+        round::run_round(
+            |p, b, a, c, e, o| unsafe { ffi::rh_store_protocol_round(store, p, b, a, c, e, o) },
+            policy,
+            active,
+            child_ranges,
+            enumeration_ranges,
+        )
+    }
+
+    /// `protocol_round` under `FixedFanOut(fan_out)` (16 = `protocol_round`'s default).
     pub fn protocol_round_fixed(
         &self,
         fan_out: usize,
@@ -308,103 +332,7 @@ impl<K: GpuKey, V: GpuRecord> HipFingerprintMap<K, V> {
         child_ranges: &mut Vec<rbsr::RangeAggregate<K>>,
         enumeration_ranges: &mut Vec<rbsr::EnumerationRange<K>>,
     ) -> RoundCounts {
-        let b = fan_out.max(2); // FanOut::new
-        let size = self.entries.len();
-        let mut counts = RoundCounts::default();
-        // step 1: raw ranks of both bounds (BoundedRange::parse), then all local aggregates
-        let raw: Vec<(usize, usize)> = active
-            .iter()
-            .map(|s| (self.bound_rank(s.start_bound(), true), self.bound_rank(s.end_bound(), false)))
-            .collect();
-        let clamped: Vec<(usize, usize)> = raw.iter().map(|&(l, h)| (l, h.max(l))).collect(); // inverted -> ZERO
-        let local = self.aggregates_by_rank(&clamped);
-        // the decisions, in segment order; SPLIT children planned as rank ranges
-        enum Plan {
-            Drop,
-            Skip,
-            Enumerate,
-            Split { cuts: Vec<usize>, first: usize },
-        }
-        let mut plans = Vec::with_capacity(active.len());
-        let mut child_spans: Vec<(usize, usize)> = Vec::new();
-        for (j, seg) in active.iter().enumerate() {
-            let (lo, hi) = raw[j];
-            if hi < lo {
-                counts.dropped_malformed += 1;
-                plans.push(Plan::Drop);
-                continue;
-            }
-            let (si, ei) = (lo.min(size), hi.min(size));
-            let (mine, theirs) = (&local[j], seg.aggregate());
-            let (span, remote) = (mine.size(), theirs.size());
-            let mut stride = 0usize;
-            let mut enumerate = false;
-            let skip = mine == theirs;
-            if !skip {
-                if remote == 0 || (span == 1 && remote == 1) {
-                    enumerate = true;
-                } else if span <= 1 {
-                    stride = 1;
-                } else {
-                    stride = span.div_ceil(b).max(1);
-                    if stride >= span {
-                        enumerate = true; // a non-progressing SPLIT becomes an IDLIST (:263-272)
-                    }
-                }
-            }
-            if skip {
-                counts.skipped += 1;
-                plans.push(Plan::Skip);
-            } else if enumerate {
-                counts.enumerated += 1;
-                if remote != 0 {
-                    counts.children += 1;
-                }
-                plans.push(Plan::Enumerate);
-            } else {
-                counts.split += 1;
-                let cuts: Vec<usize> = (1..).map(|k| si + k * stride).take_while(|&c| c < ei).collect();
-                let first = child_spans.len();
-                if !cuts.is_empty() {
-                    let mut cur = si;
-                    for &c in &cuts {
-                        child_spans.push((cur, c));
-                        cur = c;
-                    }
-                    child_spans.push((cur, ei));
-                }
-                counts.children += cuts.len() + 1;
-                plans.push(Plan::Split { cuts, first });
-            }
-        }
-        // step 2: every child's aggregate in one device call
-        let child_aggs = if child_spans.is_empty() { Vec::new() } else { self.aggregates_by_rank(&child_spans) };
-        for ((seg, plan), mine) in active.into_iter().zip(plans).zip(local) {
-            let (start, end) = (start_key(seg.start_bound()), start_key(seg.end_bound()));
-            match plan {
-                Plan::Drop | Plan::Skip => {}
-                Plan::Enumerate => {
-                    if seg.aggregate().size() != 0 {
-                        child_ranges.push(rbsr::RangeAggregate::new(start.clone(), end.clone(), Aggregate::ZERO));
-                    }
-                    enumeration_ranges.push((seg.start_bound().cloned(), seg.end_bound().cloned()));
-                }
-                Plan::Split { cuts, first } => {
-                    if cuts.is_empty() {
-                        child_ranges.push(rbsr::RangeAggregate::new(start, end, mine)); // the parent itself
-                        continue;
-                    }
-                    let mut cur = start;
-                    for (i, &c) in cuts.iter().enumerate() {
-                        let key = self.entries.at(c).0.clone(); // select(c)
-                        child_ranges.push(rbsr::RangeAggregate::new(cur, Some(key.clone()), child_aggs[first + i]));
-                        cur = Some(key);
-                    }
-                    child_ranges.push(rbsr::RangeAggregate::new(cur, end, child_aggs[first + cuts.len()]));
-                }
-            }
-        }
-        counts
+        self.protocol_round(RoundPolicy::FixedFanOut(fan_out), active, child_ranges, enumeration_ranges)
     }
 }
 

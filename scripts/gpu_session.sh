@@ -1,0 +1,107 @@
+#!/bin/bash
+# One GPU session on a gpurun box: named steps, run in order, each under its own time limit;
+# the session stops at the first step that fails (a fault, a time limit or a wrong answer: nothing
+# more runs on the GPU in that call).  Output goes to gpurun_out/<tag>/<step>.log.
+#
+#   scripts/gpu_session.sh <tag> <step> [<step> ...]
+#
+# Steps (env: RECORDS for the profile steps, PYTEST_K for pytest_k, N for the latency steps):
+#   pytest            every GPU test
+#   pytest_k          the GPU tests matching $PYTEST_K
+#   smoke             __graft_entry__.smoke()
+#   default config5 config5_40 rbsr snapshot encoded config2 config3
+#                     one bench.py line each (the default is configs[3] at N = 1)
+#   prof_config4      rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE and VALU passes of the
+#                     default line at $RECORDS (100 M unless set), summarised into <tag>_*.json
+#   prof_config5      kernel stats + the per-dispatch DRAM byte passes of config5
+#   prof_rbsr         kernel stats of the rbsr line
+#   latency_tier latency_off
+#                     the 1-row write -> d = 1 reconciliation cycle at $N rows (rbsr_latency),
+#                     host tier on / off
+#   trace_latency_off the same, tier off, under a kernel trace (kernel summary + timeline)
+#   interleave_sync interleave_nowait interleave_off
+#                     1 M-row batches into both replicas at 10^8 between d = 1 drives (tier_interleave)
+#   trace_interleave  the default-policy interleave under a kernel + memory-copy trace
+#   sstore            the sharded store's client (examples/sstore_client) on device 0
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:?usage: gpu_session.sh <tag> <step>...}
+shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+RECORDS=${RECORDS:-100000000}
+N=${N:-100000000}
+EX=reconcile-rs_amd/examples
+
+run() {  # name, seconds, command...
+    local name=$1 t=$2
+    shift 2
+    echo "== $name"
+    timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 2 "$O/$name.log" | cut -c1-900
+    [ $rc -eq 0 ] || exit $rc
+}
+
+PMC_B="python3 bench.py --config config4 --records $RECORDS --steps 10 --warmup 3 --cpu-baseline 0 --check 0 --e2e 0"
+
+for step in "$@"; do
+    case $step in
+    pytest) run pytest 900 python -u -m pytest tests -m gpu -q -rf --maxfail=3 --timeout 300 --timeout-method thread ;;
+    pytest_k) run pytest_k 700 python -u -m pytest tests -m gpu -k "${PYTEST_K:?}" -q -rf --maxfail=3 --timeout 300 --timeout-method thread ;;
+    smoke) run smoke 200 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    default) run default 300 python3 bench.py ;;
+    config5) run config5 300 python3 bench.py --config config5 ;;
+    config5_40) run config5_40 300 python3 bench.py --config config5 --steps 40 ;;
+    rbsr) run rbsr 300 python3 bench.py --config rbsr ;;
+    snapshot) run snapshot 300 python3 bench.py --config snapshot ;;
+    encoded) run encoded 300 python3 bench.py --config encoded ;;
+    config2) run config2 300 python3 bench.py --config config2 ;;
+    config3) run config3 300 python3 bench.py --config config3 ;;
+    prof_config4)
+        R=$RECORDS
+        run stats_c4_$R 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c4_$R" -o run -- $PMC_B
+        run fetch_c4_$R 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_lift --output-format csv -d "$O/fetch_c4_$R" -o run -- $PMC_B
+        run write_c4_$R 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_lift --output-format csv -d "$O/write_c4_$R" -o run -- $PMC_B
+        run valu_c4_$R 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex k_lift --output-format csv -d "$O/valu_c4_$R" -o run -- $PMC_B
+        python3 scripts/pmc_traffic.py "$O/fetch_c4_$R/run_counter_collection.csv" "$O/write_c4_$R/run_counter_collection.csv" config4 "$R" "$O/${TAG}_traffic_config4_$R.json" || exit 1
+        python3 scripts/pmc_valu.py "$O/valu_c4_$R/run_counter_collection.csv" "$O/stats_c4_$R/run_kernel_stats.csv" config4 "$R" "$O/${TAG}_valu_config4_$R.json" || exit 1
+        cp "$O/stats_c4_$R/run_kernel_stats.csv" "$O/${TAG}_config4_${R}_kernel_stats.csv"
+        rm -f "$O"/*_c4_$R/*_kernel_trace.csv "$O"/*_c4_$R/*_counter_collection.csv
+        ;;
+    prof_config5)
+        run stats_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c5" -o run -- python3 bench.py --config config5 --cpu-baseline 0
+        cp "$O/stats_c5/run_kernel_stats.csv" "$O/${TAG}_config5_kernel_stats.csv"
+        rm -f "$O"/stats_c5/*_kernel_trace.csv
+        run pmc_c5 600 bash scripts/pmc_c5.sh
+        python3 scripts/pmc_c5_summary.py gpurun_out "$O/${TAG}_config5_kernel_stats.csv" "$O/${TAG}_pmc_config5.json" || exit 1
+        rm -f gpurun_out/pmc_c5_*/*_counter_collection.csv
+        ;;
+    prof_rbsr)
+        run stats_rbsr 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_rbsr" -o run -- python3 bench.py --config rbsr --cpu-baseline 0
+        cp "$O/stats_rbsr/run_kernel_stats.csv" "$O/${TAG}_rbsr_kernel_stats.csv"
+        rm -f "$O"/stats_rbsr/*_kernel_trace.csv
+        ;;
+    latency_tier) run latency_tier 300 $EX/rbsr_latency "$N" 1 200 1 1 ;;
+    latency_off) run latency_off 300 $EX/rbsr_latency "$N" 1 40 0 1 ;;
+    trace_latency_off)
+        run trace_latency_off 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trlat" -o tr -- $EX/rbsr_latency "$N" 1 10 0 1
+        python3 scripts/write_timeline.py "$O/trlat" k_round > "$O/${TAG}_latency_off_timeline.txt" 2>&1 || true
+        cp "$O"/trlat/tr_kernel_stats.csv "$O/${TAG}_latency_off_kernel_stats.csv" 2>/dev/null || true
+        rm -rf "$O/trlat"
+        ;;
+    interleave_sync) run interleave_sync 400 $EX/tier_interleave 100000000 1000000 20 1 c5 2 ;;
+    interleave_nowait) run interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 $EX/tier_interleave 100000000 1000000 12 1 c5 2 3 ;;
+    interleave_off) run interleave_off 400 $EX/tier_interleave 100000000 1000000 12 0 c5 2 3 ;;
+    trace_interleave)
+        run trace_interleave 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trint" -o tr -- $EX/tier_interleave 100000000 1000000 6 1 c5 1
+        python3 scripts/copy_summary.py "$O/trint" > "$O/${TAG}_interleave_trace_summary.txt" 2>&1 || true
+        rm -rf "$O/trint"
+        ;;
+    sstore) run sstore 300 $EX/sstore_client 4 2000000 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "== done"

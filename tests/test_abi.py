@@ -155,35 +155,6 @@ def test_host_tensors_are_rejected(rsos_hip_lib):
         lift_records(s, cols)
 
 
-@pytest.mark.parametrize("kind,key", [("u32", "u32"), ("u64", "u64"), ("b16", "bytes16"), ("b32", "bytes32")])
-def test_sharded_routing_is_bisect_right(kind, key):
-    """ShardedStore.apply routes a batch with one np.searchsorted over the load-time splitters;
-    it must equal bisect_right on the keys' Ord (numeric for integers, memcmp for byte arrays,
-    including rows with trailing zero bytes and rows equal to a splitter)."""
-    import bisect
-    from rsos_hip import RecordSchema
-    from rsos_hip.sharded import ShardedStore
-    from rsos_hip.store import GpuFingerprintStore
-    schema = RecordSchema.plain(key, "u64")
-    kl = schema.key_row
-    probe = GpuFingerprintStore.__new__(GpuFingerprintStore)  # key conversion only: no device
-    probe.schema = schema
-    sh = ShardedStore.__new__(ShardedStore)
-    sh.schema, sh.shards = schema, [probe]
-    rng = np.random.default_rng(5)
-    rows = rng.integers(0, 256, (4000, kl), dtype=np.uint8)
-    rows[::7, kl // 2:] = 0  # trailing zero bytes
-    rows[::11, 0] = rows[0, 0]  # shared leading byte
-    keys = [probe._key_out(r.tobytes()) for r in rows]
-    sh.splitters = sorted(keys[j] for j in (3, 500, 1200, 2500, 3999))
-    rows[1] = rows[500]  # a key equal to a splitter goes to the shard it starts
-    keys[1] = keys[500]
-    want = [bisect.bisect_right(sh.splitters, k) for k in keys]
-    assert sh._owners(rows).tolist() == want
-    sh.splitters = []
-    assert sh._owners(rows).tolist() == [0] * len(rows)
-
-
 def test_apply_device_many_argument_checks(rsos_hip_lib):
     """rh_store_apply_device_many refuses a NULL store, and NULL column / size arrays for k > 0,
     before touching a device."""
@@ -301,3 +272,110 @@ def test_signature_parser_catches_mismatches():
     assert _c_param("const uint64_t a[4]") == ("u64", [True]) == _r_type("*const u64")
     assert _c_param("void *stream") == _r_type("*mut c_void")
     assert _c_param("const void *keys") != _r_type("*mut c_void")
+
+
+# ---- the Rust FFI block against the header, data layout and constants ---------------------------
+def _c_structs(text=None):
+    """{name: [(field, base, pointer depth, pointee constness per level, array length)]} of every
+    `typedef struct name { ... } name;` in the header"""
+    text = re.sub(r"/\*.*?\*/", "", text if text is not None else open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"typedef struct (\w+)\s*\{(.*?)\}\s*(\w+)\s*;", text, flags=re.S):
+        fields = []
+        for decl in m.group(2).split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            typ, names = re.match(r"(.*?)(\**\s*\w+(?:\s*\[\s*\d+\s*\])?(?:\s*,\s*\**\s*\w+(?:\s*\[\s*\d+\s*\])?)*)$",
+                                  decl, flags=re.S).groups()
+            for nm in names.split(","):
+                nm = nm.strip()
+                stars = nm.count("*")
+                nm = nm.replace("*", "").strip()
+                arr = re.search(r"\[\s*(\d+)\s*\]", nm)
+                n_arr = int(arr.group(1)) if arr else 0
+                nm = re.sub(r"\[.*\]", "", nm).strip()
+                base, consts = _c_type(typ + " " + "*" * stars)
+                fields.append((nm, base, len(consts), consts, n_arr))
+        out[m.group(3)] = fields
+    return out
+
+
+def _rust_structs(ffi=None):
+    ffi = ffi if ffi is not None else open(os.path.join(ROOT, "reconcile-rs_amd", "rust", "rsos-hip", "src", "ffi.rs")).read()
+    ffi = re.sub(r"//[^\n]*", "", ffi)
+    out = {}
+    for m in re.finditer(r"#\[repr\(C\)\]\s*(?:#\[derive\([^)]*\)\]\s*)?pub struct (\w+)\s*\{(.*?)\}", ffi, flags=re.S):
+        fields = []
+        for decl in m.group(2).split(","):
+            decl = decl.strip()
+            if not decl or decl.startswith("_private"):
+                continue
+            nm, ty = [x.strip() for x in re.sub(r"^pub\s+", "", decl).split(":", 1)]
+            arr = re.match(r"\[(.*);\s*(\d+)\]$", ty)
+            n_arr = int(arr.group(2)) if arr else 0
+            base, consts = _r_type(arr.group(1) if arr else ty)
+            fields.append((nm, base, len(consts), consts, n_arr))
+        out[m.group(1)] = fields
+    return out
+
+
+def _c_consts(text=None):
+    text = re.sub(r"/\*.*?\*/", "", text if text is not None else open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"typedef enum \w+\s*\{(.*?)\}", text, flags=re.S):
+        for item in m.group(1).split(","):
+            kv = re.match(r"\s*(RH_\w+)\s*=\s*(-?\d+)", item)
+            if kv:
+                out[kv.group(1)] = int(kv.group(2))
+    for m in re.finditer(r"#define (RH_\w+) (-?\d+)", text):
+        out[m.group(1)] = int(m.group(2))
+    return out
+
+
+def _rust_consts(ffi=None):
+    ffi = ffi if ffi is not None else open(os.path.join(ROOT, "reconcile-rs_amd", "rust", "rsos-hip", "src", "ffi.rs")).read()
+    return {m.group(1): int(m.group(2)) for m in re.finditer(r"pub const (RH_\w+):\s*\w+\s*=\s*(-?\d+)\s*;", ffi)}
+
+
+def _layout_mismatches(ffi=None):
+    c, r = _c_structs(), _rust_structs(ffi)
+    bad = []
+    for name, fields in c.items():
+        if name not in r:
+            bad.append((name, "missing in ffi.rs"))
+        elif r[name] != fields:
+            bad.append((name, fields, r[name]))
+    cc, rc = _c_consts(), _rust_consts(ffi)
+    for k, v in cc.items():
+        if rc.get(k) != v:
+            bad.append((k, v, rc.get(k)))
+    for k in rc:
+        if k not in cc:
+            bad.append((k, "not in the header"))
+    return bad
+
+
+def test_rust_ffi_layout_and_constants_match_the_header():
+    """Every `typedef struct` of the header has a #[repr(C)] twin in ffi.rs with the same fields in
+    the same order (name, base type width, pointer depth, pointee constness, array length), and every
+    enumerator / #define of the header is a `pub const` of ffi.rs with the same value (and no other)."""
+    c = _c_structs()
+    assert {"rh_schema", "rh_columns", "rh_aggregate", "rh_snapshot_info", "rh_segments", "rh_round_outcome"} <= set(c)
+    assert c["rh_aggregate"] == [("fingerprint", "u64", 0, [], 4), ("size", "u64", 0, [], 0)]
+    assert len(_c_consts()) >= 25
+    assert _layout_mismatches() == []
+
+
+def test_layout_check_catches_a_swapped_field_and_a_wrong_constant():
+    """The check above fails on the mistakes it exists for: two fields swapped, a field's width
+    changed, a pointer's constness flipped, a renumbered constant."""
+    ffi = open(os.path.join(ROOT, "reconcile-rs_amd", "rust", "rsos-hip", "src", "ffi.rs")).read()
+    swapped = ffi.replace("    pub fingerprint: [u64; 4],\n    pub size: u64,", "    pub size: u64,\n    pub fingerprint: [u64; 4],")
+    assert swapped != ffi and _layout_mismatches(swapped)
+    narrowed = ffi.replace("    pub key_len: u32,", "    pub key_len: u64,")
+    assert narrowed != ffi and _layout_mismatches(narrowed)
+    mutable = ffi.replace("    pub phys: *const u64,", "    pub phys: *mut u64,")
+    assert mutable != ffi and _layout_mismatches(mutable)
+    renumbered = ffi.replace("pub const RH_REC_DATED: i32 = 1;", "pub const RH_REC_DATED: i32 = 2;")
+    assert renumbered != ffi and _layout_mismatches(renumbered)

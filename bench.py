@@ -937,12 +937,19 @@ def reconcile(args, world, rank, dev, dist):
     del cols, batch
     pol = R.FixedFanOut(16)
 
+    kl = schema.key_row
+    pcie = {"in": 0, "out": 0}
+
     def run():
         active, k, segs, enum = R.initial_segments(a), 0, 0, 0
+        pcie["in"] = pcie["out"] = 0
         while len(active):
             segs += len(active)
+            r = len(active)
             active, en, _ = R.protocol_round_segments((b, a)[k % 2], pol, active, copy=False)
             enum += len(en)
+            pcie["in"] += round_in_bytes(r, kl)
+            pcie["out"] += round_out_bytes(len(active), len(en), kl)
             k += 1
         return k, segs, enum
 
@@ -978,6 +985,7 @@ def reconcile(args, world, rank, dev, dist):
             "step": "initial_ranges + protocol rounds (rh_store_protocol_round, one device round trip each) "
                     "until no segment is left",
         }
+        line["roofline"] = rbsr_roofline(pcie["in"], pcie["out"], elapsed / args.steps, rounds)
         if cpu_line:
             line["cpu_baseline"] = cpu_line
         print(json.dumps(line), flush=True)
@@ -985,6 +993,51 @@ def reconcile(args, world, rank, dev, dist):
     b.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _pad16(x):
+    return (x + 15) // 16 * 16
+
+
+def round_in_bytes(r, kl):
+    """A round's segments as the device reads them (rsos_hip_abi.hip protocol_round): start / end
+    kinds, start then end keys, the peer's aggregates -- one copy up, or read in place when tiny."""
+    return _pad16(_pad16(r) + _pad16(r) + 2 * r * kl) + 40 * r
+
+
+def round_out_bytes(nc, ne, kl):
+    """A round's output in round_layout() (internal.hpp): the 64-byte header, the children's kinds,
+    keys and aggregates, the enumerations' kinds and keys -- written by the emit kernel into mapped
+    page-locked memory (or copied down when small)."""
+    return 64 + 2 * _pad16(nc) + 2 * _pad16(nc * kl) + _pad16(40 * nc) + 2 * _pad16(ne) + 2 * _pad16(ne * kl)
+
+
+def rbsr_roofline(in_bytes, out_bytes, step_s, rounds):
+    """The rbsr line's bound: a reconciliation moves its rounds' inputs up and
+    outputs down over PCIe, one device round trip per round.  achieved = those bytes per
+    reconciliation / its time, against the link's measured ceiling -- a kernel's 16-byte stores
+    into mapped page-locked memory, the fastest form measured (microbench/pcie_copy.hip,
+    profiles/r04_pcie_copy.jsonl); model_ms = the inputs at the measured copy rate plus the
+    outputs at the mapped-store rate, the time the bytes alone would take."""
+    w_gbs, h2d_gbs, src = 54.6, 21.7, None
+    p = os.path.join(ROOT, "profiles", "r04_pcie_copy.jsonl")
+    try:
+        rows = [json.loads(x) for x in open(p) if x.strip()]
+        big = max(r["bytes"] for r in rows)
+        w_gbs = max(r["kernel_write_GBs"] for r in rows if r["bytes"] == big)
+        h2d_gbs = max(r["h2d_GBs"] for r in rows if r["bytes"] == big)
+        src = os.path.relpath(p, ROOT)
+    except (OSError, ValueError, KeyError):
+        pass
+    total = in_bytes + out_bytes
+    achieved = total / step_s / 1e9 if step_s > 0 else 0.0
+    model_s = in_bytes / (h2d_gbs * 1e9) + out_bytes / (w_gbs * 1e9)
+    return {"bound": "pcie", "achieved": round(achieved, 2), "peak": w_gbs, "unit": "GB/s",
+            "frac": round(achieved / w_gbs, 4), "traffic": None,
+            "bytes_per_reconciliation": {"in": in_bytes, "out": out_bytes},
+            "peak_h2d_copy_GBs": h2d_gbs, "model_ms": round(model_s * 1e3, 3),
+            "model_frac_of_step": round(model_s / step_s, 4) if step_s > 0 else None,
+            "round_trips": rounds, "source": src}
 
 
 def cpu_baseline_reconcile(schema, cols, rows, m):

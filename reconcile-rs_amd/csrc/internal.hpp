@@ -29,6 +29,9 @@ hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_
 // (ceil(n/65536) + 1 entries), bpre (ceil(n/256) + 1 entries), 32 B each
 hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre,
                          uint8_t *bpre, uint8_t *out, hipStream_t st);
+// launch_prefix's first two levels only: bpre[k] = Σ block sums [0, k), k in [0, ceil(n / 256)]
+hipError_t launch_block_prefix(uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre, uint8_t *bpre,
+                               hipStream_t st);
 // Rank-addressed merge: out row r of segment k (start[k] <= r < start[k + 1]) is row
 // (src[k] & ~2^63) + r - start[k] of `newf` if src[k] has bit 63 set, else of `old`
 hipError_t launch_seg_copy(const uint8_t *old, const uint8_t *newf, const uint64_t *start, const uint64_t *src,
@@ -73,6 +76,9 @@ struct RoundIn {
     const uint8_t *sk, *ek, *skeys, *ekeys;
     const uint64_t *remote;
     const uint8_t *bkeys, *fps, *bsums, *ssums;
+    // nullable: the base's exclusive prefix over its block sums (launch_block_prefix), which makes
+    // any range sum the head and tail rows plus one difference (wave_range_fp_pre)
+    const uint8_t *bpre = nullptr;
 };
 // A round over the base + the delta run as they stand (no compaction first): the run's entries in
 // key order as columns (k_tier_run, the host tier's run copy) -- the contributions (cur - base)
@@ -89,6 +95,7 @@ struct RoundRun {
     const uint32_t *brank = nullptr;
     const uint64_t *gsamp = nullptr;
     uint64_t nb = 0;
+    const uint8_t *bpre = nullptr;  // nullable: the contributions' block prefix (as RoundIn::bpre)
 };
 // every segment's view rank range, its places (place[4 j ..]: start b, start j, end b, end j)
 // and local aggregate, from the bound keys' base ranks (rank_b) and run ranks (rank_j)

@@ -571,6 +571,9 @@ struct PinnedVec {
     void *dptr = nullptr;          // the device address of p, once looked up (store.dev_ptr)
     const void *dptr_of = nullptr;  // ... and the allocation it belongs to
     PinnedVec() = default;
+    // extra allocation flags: hipHostMallocCoherent for a buffer the host polls while a kernel
+    // writes it (a sequence word stored last), so the poll never depends on HIP_HOST_COHERENT
+    explicit PinnedVec(unsigned extra) : flags(hipHostMallocMapped | hipHostMallocPortable | extra) {}
     PinnedVec(const PinnedVec &) = delete;
     PinnedVec &operator=(const PinnedVec &) = delete;
     ~PinnedVec() { release(); }
@@ -757,7 +760,7 @@ struct rh_store {
         return std::min<uint64_t>(small_env, rh::small_batch_max((int)kl));
     }
     PinnedVec<uint8_t> sb_in;    // a small host batch, packed (the device reads it in place)
-    PinnedVec<uint64_t> sb_res;  // the small path's result block (written by the device in place)
+    PinnedVec<uint64_t> sb_res{hipHostMallocCoherent};  // the small path's result block (written by the device in place)
     // the device address of a mapped page-locked buffer: looked up once per allocation (the
     // buffer keeps it until it moves), not once per batch
     template <class T>
@@ -922,8 +925,9 @@ struct rh_store {
     // merge behind it need not have finished -- it writes only device buffers, which every later
     // command on the stream is ordered after -- so a small batch returns without the merge's time
     // and the stream's completion signal.  A stream that fails or drains without the word is an error.
-    int wait_small(uint64_t seq) {
-        uint64_t *w = sb_res.data() + 13;
+    int wait_small(uint64_t seq) { return wait_word(sb_res.data() + 13, seq); }
+    // Poll a word a kernel stores last (after a system-scope fence) into mapped page-locked memory
+    int wait_word(const uint64_t *w, uint64_t seq) {
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 1;; spin++) {
             if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return RH_OK;
@@ -931,13 +935,13 @@ struct rh_store {
                 const hipError_t e = hipStreamQuery(stream);
                 if (e == hipSuccess) {
                     if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return RH_OK;
-                    return fail(RH_ERR_HIP, "small batch: the stream finished without the result word");
+                    return fail(RH_ERR_HIP, "the stream finished without the kernel's result word");
                 }
                 if (e != hipErrorNotReady) return fail(RH_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
                 if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
                     RH_HIP(hipStreamSynchronize(stream));
                     if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return RH_OK;
-                    return fail(RH_ERR_HIP, "small batch: the stream finished without the result word");
+                    return fail(RH_ERR_HIP, "the stream finished without the kernel's result word");
                 }
             }
         }
@@ -1006,7 +1010,9 @@ struct rh_store {
     uint64_t rf_log_version = 0;
     // a batch's rows as the folds read them, in key order: keys, the device's DeltaRecs and drop
     // flags (against the device's base), the fingerprints and ops (against the tier's own base)
-    PinnedVec<uint8_t> fold_keys, fold_recs, fold_ops, fold_fps, fold_sops;
+    // (coherent: the small path writes them in place before the sequence word the host polls)
+    PinnedVec<uint8_t> fold_keys{hipHostMallocCoherent}, fold_recs{hipHostMallocCoherent},
+        fold_ops{hipHostMallocCoherent}, fold_fps{hipHostMallocCoherent}, fold_sops{hipHostMallocCoherent};
     bool tier_fresh() const { return tier_on && tier_version == version; }
     // Start a refresh of the host tier: compact, the prefix sums and samples on the device, and
     // their copy down on the copy stream into the spare set.  Returns at once (no wait).
@@ -1223,6 +1229,8 @@ struct rh_store {
         RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
         RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
         RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
+        if ((rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64))) return rc;
+        RH_HIP(rh::launch_block_prefix(n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, stream));
         RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         RH_HIP(rh::launch_tier_gsamp(trun_br.p, trun_cntp.p, trun_fl.p, n1, trun_gs.p, stream));
@@ -2127,6 +2135,7 @@ struct rh_store {
     int view_of(rh::RoundRun *run, rh::RoundIn *in) {
         int rc;
         if ((rc = run_columns())) return rc;
+        if ((rc = ensure_base_prefix())) return rc;
         *run = rh::RoundRun{nd,
                             dkeys[cd].p,
                             trun_c.p,
@@ -2136,8 +2145,24 @@ struct rh_store {
                             trun_fl.p,
                             trun_br.p,
                             trun_gs.p,
-                            nb};
-        *in = rh::RoundIn{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p};
+                            nb,
+                            trun_bpre.p};
+        *in = rh::RoundIn{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
+        return RH_OK;
+    }
+    // The base run's exclusive block prefix (bpre_b[k] = Σ block sums [0, k)), formed once per base
+    // (after a load or a compaction; ~n / 256 entries) on the first question that sums over it on
+    // the device: any range sum is then its head and tail rows plus one difference (view_range_fp)
+    DevBuf<uint8_t> bpre_b, spre_b;
+    uint64_t bpre_epoch = ~0ull;
+    int ensure_base_prefix() {
+        int rc;
+        if (bpre_epoch == base_epoch && bpre_b.p) return RH_OK;
+        const uint64_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
+        if ((rc = bpre_b.ensure((nbk + 1) * 32 + 64)) || (rc = spre_b.ensure((ns + 1) * 32 + 64))) return rc;
+        if (nb) RH_HIP(rh::launch_block_prefix(nb, bsums.p, ssums.p, spre_b.p, bpre_b.p, stream));
+        else RH_HIP(hipMemsetAsync(bpre_b.p, 0, 32, stream));
+        bpre_epoch = base_epoch;
         return RH_OK;
     }
     // the run ranks of m keys (lower bounds among the delta run's keys)
@@ -2182,6 +2207,12 @@ struct rh_store {
             out->size = size();
             return RH_OK;
         }
+        if (query_fused) {
+            uint8_t k2[64] = {0};
+            if (lo_kind) memcpy(k2, lo_key, kl);
+            if (hi_kind) memcpy(k2 + kl, hi_key, kl);
+            return query_tiny(2, k2, 2 * kl, 1, lo_kind, hi_kind, out, sizeof(rh_aggregate));
+        }
         if ((rc = q_keys.ensure(2 * kl + 64)) || (rc = q_lo.ensure(1)) || (rc = q_hi.ensure(1)) ||
             (rc = q_dlo.ensure(1)) || (rc = q_dhi.ensure(1)) || (rc = q_out.ensure(1)) || (rc = q_bout.ensure(1)) ||
             (rc = q_dout.ensure(1)))
@@ -2204,8 +2235,47 @@ struct rh_store {
         RH_HIP(hipMemcpyAsync(out, q_out.p, sizeof(rh_aggregate), hipMemcpyDeviceToHost, stream));
         return sync();
     }
+    // ---- the small questions in one launch (round_tiny.hpp k_query_tiny) ----------------------
+    // ranks of up to QUERY_TINY keys, selects of up to QUERY_TINY ranks, one key-range aggregate,
+    // over base + delta run as they stand: the input and the answer in mapped page-locked memory,
+    // the host polling the sequence word the kernel stores last.  A/B: RSOS_HIP_QUERY_FUSED=0.
+    PinnedVec<uint8_t> qt_buf{hipHostMallocCoherent};
+    uint64_t qt_seq = 0;
+    int query_fused = getenv("RSOS_HIP_QUERY_FUSED") ? atoi(getenv("RSOS_HIP_QUERY_FUSED")) : 1;
+    int query_tiny(int mode, const void *in, size_t in_bytes, uint64_t m, int lo_kind, int hi_kind, void *out,
+                   size_t out_bytes) {
+        int rc;
+        rh::RoundRun run{};
+        if (nd) {
+            rh::RoundIn unused;
+            if ((rc = view_of(&run, &unused))) return rc;
+        }
+        run.nb = nb;
+        constexpr size_t o_out = 4096, o_seq = 8192;  // inputs: at most QUERY_TINY 32-byte keys
+        try {
+            qt_buf.resize(o_seq + 64);
+        } catch (const std::bad_alloc &) {
+            return fail(RH_ERR_OOM, "query: page-locked allocation failed");
+        }
+        uint8_t *d;
+        if ((rc = dev_ptr(qt_buf, &d))) return rc;
+        memcpy(qt_buf.data(), in, in_bytes);
+        rh::QueryTiny q{};
+        q.mode = mode, q.in = d, q.m = m, q.lo_kind = lo_kind, q.hi_kind = hi_kind;
+        if ((rc = ensure_base_prefix())) return rc;
+        q.base = rh::RoundIn{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
+        q.run = run;
+        q.bsmp = bsmp.p, q.bsmp2 = bsmp2.p, q.btab = (!bsmp2.p || nb == 0) ? rh::SearchTable{} : base_table();
+        q.dsmp = nd ? dsmp[cd].p : nullptr, q.dsmp2 = nd ? dsmp2[cd].p : nullptr;
+        q.out = d + o_out, q.seq_word = reinterpret_cast<uint64_t *>(d + o_seq), q.seq = ++qt_seq;
+        RH_HIP(kops->query_tiny(q, stream));
+        if ((rc = wait_word(reinterpret_cast<const uint64_t *>(qt_buf.data() + o_seq), q.seq))) return rc;
+        memcpy(out, qt_buf.data() + o_out, out_bytes);
+        return RH_OK;
+    }
     int ranks(const void *keys, size_t m, uint64_t *out) {
         int rc;
+        if (query_fused && m <= rh::QUERY_TINY) return query_tiny(0, keys, m * kl, m, 0, 0, out, m * 8);
         if ((rc = q_keys.ensure(m * kl + 64)) || (rc = q_rank.ensure(m)) || (rc = q_drank.ensure(m)) ||
             (rc = q_merged.ensure(m)))
             return rc;
@@ -2337,7 +2407,7 @@ struct rh_store {
     // kDirectMax; past it, the header comes down first so the copy is exact).
     DevBuf<uint8_t> r_in, r_kind, r_out;
     DevBuf<uint64_t> r_seg;
-    PinnedVec<uint8_t> pr_out;
+    PinnedVec<uint8_t> pr_out{hipHostMallocCoherent};  // a round's output (polled: round_tiny's sequence word)
     static constexpr size_t kRoundSmall = 256 << 10;  // below this, one speculative copy each way
     static constexpr size_t kDirectMax = 256ull << 20;  // mapped output sized for the worst case up to this
     int round_copyout = getenv("RSOS_HIP_ROUND_COPYOUT") ? atoi(getenv("RSOS_HIP_ROUND_COPYOUT")) : 2;
@@ -2417,9 +2487,28 @@ struct rh_store {
         uint64_t *lo = r_seg.p, *hi = lo + r, *loc = hi + r, *st = loc + 5 * r, *si = st + r, *ei = si + r,
                  *nch = ei + r, *choff = nch + r, *nen = choff + r, *enoff = nen + r, *place = enoff + r;
         const rh::RoundSegs g{r_kind.p, lo, hi, loc, st, si, ei, nch, choff, nen, enoff};
-        const rh::RoundIn din{d_sk, d_ek, d_skeys, d_ekeys, d_rem, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p};
+        if ((rc = ensure_base_prefix())) return rc;
+        const rh::RoundIn din{d_sk, d_ek, d_skeys, d_ekeys, d_rem, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
         uint64_t *hdr = reinterpret_cast<uint64_t *>(r_out.p);
         const int sq = policy == RH_POLICY_SQRT_FAN_OUT;
+        uint64_t h[5];
+        if (zero_copy && round_fused) {
+            // a tiny round whole in one launch (round_tiny.hpp): the bound keys' searches in both
+            // runs, the bounds, decisions and emission, the per-segment arrays in LDS; the host
+            // waits for the sequence word the kernel stores last into the mapped output
+            rh::RoundTiny t{};
+            t.in = din;
+            t.run = run;
+            t.run.nb = nb;
+            t.bsmp = bsmp.p, t.bsmp2 = bsmp2.p, t.btab = (!bsmp2.p || nb == 0) ? rh::SearchTable{} : base_table();
+            t.dsmp = view ? dsmp[cd].p : nullptr, t.dsmp2 = view ? dsmp2[cd].p : nullptr;
+            t.g = g, t.gplace = place, t.r = r, t.n = n, t.sqrt_policy = sq, t.b = b, t.cap = cap, t.out = out_p;
+            t.seq = ++round_seq;
+            RH_HIP(kops->round_tiny(t, stream));
+            if ((rc = wait_word(reinterpret_cast<const uint64_t *>(pr_out.data()) + 7, t.seq))) return rc;
+            memcpy(h, pr_out.data(), sizeof h);
+            return round_finish(h, cap, r, view, din, run, g, place, false, ch, en, oc);
+        }
         if (nb)
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
                                         base_table()));
@@ -2462,7 +2551,6 @@ struct rh_store {
             RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
             RH_HIP(emit(cap, hdr, eo));
         }
-        uint64_t h[5];
         if (direct)  // the round (or, emitted in place, its header alone)
             RH_HIP(rh::launch_round_copy_out(hdr, cap, (uint32_t)kl, r_out.p, dout, round_copyout == 2 ? 64 : worst,
                                              stream));
@@ -2480,6 +2568,15 @@ struct rh_store {
             if ((rc = sync())) return rc;
             memcpy(h, pr_out.data(), sizeof h);
         }
+        return round_finish(h, cap, r, view, din, run, g, place, worst > kRoundSmall && !direct, ch, en, oc);
+    }
+    // the round's header is in h (and pr_out): emit again if its children outnumber cap (a wide
+    // fan-out; the per-segment arrays are in g / place), copy the rest down if it is still on the
+    // device, and point the outputs at pr_out
+    int round_finish(const uint64_t h[5], uint64_t cap, size_t r, bool view, const rh::RoundIn &din,
+                     const rh::RoundRun &run, const rh::RoundSegs &g, const uint64_t *place, bool copy_rest,
+                     rh_segments *ch, rh_segments *en, rh_round_outcome *oc) {
+        int rc;
         const uint64_t nc = h[3], ne = h[1];
         const rh::RoundLayout L = rh::round_layout(nc, ne, kl);
         const bool regrow = nc > cap;
@@ -2487,11 +2584,12 @@ struct rh_store {
             cap = nc;
             if ((rc = r_out.ensure(L.end))) return rc;  // r_out may have moved: restore its header
             pr_out.resize(L.end);
-            hdr = reinterpret_cast<uint64_t *>(r_out.p);
+            uint64_t *hdr = reinterpret_cast<uint64_t *>(r_out.p);
             RH_HIP(hipMemcpyAsync(hdr, pr_out.data(), 64, hipMemcpyHostToDevice, stream));
-            RH_HIP(emit(cap, hdr, r_out.p));
+            RH_HIP(view ? rh::launch_round_emit_view(hdr, cap, r, (uint32_t)kl, din, run, g, place, r_out.p, stream)
+                        : rh::launch_round_emit(hdr, cap, r, (uint32_t)kl, din, g, r_out.p, stream));
         }
-        if (regrow || (worst > kRoundSmall && !direct)) {
+        if (regrow || copy_rest) {
             pr_out.resize(L.end);
             RH_HIP(hipMemcpyAsync(pr_out.data() + 64, r_out.p + 64, L.end - 64, hipMemcpyDeviceToHost, stream));
             if ((rc = sync())) return rc;
@@ -2503,6 +2601,9 @@ struct rh_store {
         *en = rh_segments{o + L.esk, o + L.eskeys, o + L.eek, o + L.eekeys, nullptr, (size_t)ne, (size_t)ne};
         return RH_OK;
     }
+    // A/B switch: RSOS_HIP_ROUND_FUSED=0 keeps tiny rounds on the two searches + k_round_small(_view)
+    int round_fused = getenv("RSOS_HIP_ROUND_FUSED") ? atoi(getenv("RSOS_HIP_ROUND_FUSED")) : 1;
+    uint64_t round_seq = 0;
     void release() {
         (void)hipStreamSynchronize(stream);
         if (cstream) (void)hipStreamSynchronize(cstream);
@@ -2529,6 +2630,7 @@ struct rh_store {
         if (rf_kdone) (void)hipEventDestroy(rf_kdone);
         cstream = nullptr, rf_ready = rf_ev = rf_kdone = nullptr, rf_on = false;
         snap.release();
+        bpre_b.release(); spre_b.release();
         sbsums.release(); sssums.release(); sbsmp.release(); sbsmp2.release(); sbtab.release(); sbtabp.release();
         stot.release(); snap_words.release(); snap_hdr.release();
         scratch.release();
@@ -2696,6 +2798,11 @@ int rh_store_keys(rh_store *s, uint64_t lo, uint64_t hi, void *host_out) {
         return RH_OK;
     }
     RH_HIP(hipSetDevice(s->device));
+    if (s->query_fused && hi - lo <= rh::QUERY_TINY) {  // select and short dumps: one launch
+        uint64_t rk[rh::QUERY_TINY];
+        for (uint64_t i = lo; i < hi; i++) rk[i - lo] = i;
+        return s->query_tiny(1, rk, (hi - lo) * 8, hi - lo, 0, 0, host_out, (hi - lo) * s->kl);
+    }
     if (s->nd && hi - lo <= rh_store::KEYS_VIEW_MAX) return s->keys_view(lo, hi, host_out);
     if ((rc = s->compact())) return rc;
     RH_HIP(hipMemcpyAsync(host_out, s->bkeys[s->cb].p + lo * s->kl, (hi - lo) * s->kl, hipMemcpyDeviceToHost,

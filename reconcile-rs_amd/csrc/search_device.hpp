@@ -98,4 +98,63 @@ __device__ __forceinline__ void search_sampled_one(const uint8_t *keys, uint64_t
     if (present) *present = (lo < end && key_cmp<KK, KL>(keys + lo * KL, key) == 0) ? 1 : 0;
 }
 
+// ---- the same searches by a group of W lanes (W = 16 or 64), for latency-bound questions -------
+// A group's W lanes probe W evenly spaced rows of the window at once, so a window of w rows takes
+// ceil(log_W w) dependent loads instead of log2 w (a tiny round's or a single rank's critical path).
+// The bits of a wave-wide ballot that belong to the calling group (its W lanes, aligned)
+template <int W>
+__device__ __forceinline__ uint64_t group_ballot(bool p) {
+    const uint64_t b = __ballot(p);
+    if constexpr (W == 64) return b;
+    else return (b >> (threadIdx.x & 63 & ~(W - 1))) & ((1ull << W) - 1);
+}
+
+// lower bound of q in keys[lo, n) given that it lies in [lo, hi] and (hi == n or keys[hi] >= q);
+// *present: keys[rank] == q.  Every lane of the group returns the same; gl = the lane's index in it.
+template <int KK, int KL, int W>
+__device__ __forceinline__ uint64_t lower_bound_group(const uint8_t *keys, uint64_t n, uint64_t lo, uint64_t hi,
+                                                      const uint8_t *q, uint32_t gl, bool *present) {
+    while (hi - lo + 1 > W) {
+        const uint64_t step = (hi - lo + W - 1) / W;
+        const uint64_t p = lo + gl * step;
+        const bool less = p < hi && key_cmp<KK, KL>(keys + p * KL, q) < 0;
+        const uint32_t c = __popcll(group_ballot<W>(less));  // the probes below q: a prefix
+        if (c == 0) {
+            hi = lo;
+            break;
+        }
+        const uint64_t pc = lo + (c - 1) * step;
+        lo = pc + 1;
+        hi = pc + step < hi ? pc + step : hi;
+    }
+    const uint64_t p = lo + gl;
+    const bool valid = p <= hi && p < n;
+    const int c = valid ? key_cmp<KK, KL>(keys + p * KL, q) : 1;
+    const uint64_t lt = group_ballot<W>(valid && c < 0), eq = group_ballot<W>(valid && c == 0);
+    const uint32_t r = __popcll(lt);
+    *present = (eq >> r) & 1;
+    return lo + r;
+}
+
+// search_sampled_one by a group: the table's window (base runs), else the whole run
+template <int KK, int KL, int W>
+__device__ __forceinline__ void search_group(const uint8_t *keys, uint64_t n, SearchTable tb, const uint8_t *key,
+                                             uint32_t gl, uint32_t *rank, uint8_t *present) {
+    uint64_t lo = 0, hi = n;
+    if (tb.tab && n) {
+        const uint64_t d = key_digit<KK, KL>(key, 0);
+        const uint64_t dmin = tb.par[0], sh = tb.par[1], nt = 1ull << tb.bits;
+        uint64_t h = d < dmin ? 0 : (d - dmin) >> sh;
+        h = h < nt ? h : nt - 1;
+        const uint64_t a0 = tb.tab[h], a1 = tb.tab[h + 1];
+        lo = a0 ? (a0 - 1) * SMP2_STRIDE : 0;
+        hi = a1 * SMP2_STRIDE < n ? a1 * SMP2_STRIDE : n;  // n, or a sampled row whose digit is above d
+        lo = lo < hi ? lo : hi;
+    }
+    bool pr = false;
+    const uint64_t r = n ? lower_bound_group<KK, KL, W>(keys, n, lo, hi, key, gl, &pr) : 0;
+    *rank = (uint32_t)r;
+    if (present) *present = pr ? 1 : 0;
+}
+
 }  // namespace rh

@@ -30,6 +30,7 @@
 #include "store_kernels.hpp"
 #include "search_device.hpp"
 #include "fp_device.hpp"
+#include "round_tiny.hpp"
 
 namespace rh {
 
@@ -1652,6 +1653,18 @@ struct KeyOps final : StoreKeyOps {
         const uint64_t ns = (n + stride - 1) / stride;
         if (ns == 0) return hipSuccess;
         hipLaunchKernelGGL((k_sample<KK, KL>), g1(ns), dim3(256), 0, st, keys, n, stride, smp);
+        return hipGetLastError();
+    }
+
+    hipError_t query_tiny(const QueryTiny &a, hipStream_t st) override {
+        if (a.m > QUERY_TINY || (a.mode == 2 && a.m != 1)) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_query_tiny<KK, KL>), dim3(1), dim3(1024), 0, st, a);
+        return hipGetLastError();
+    }
+
+    hipError_t round_tiny(const RoundTiny &a, hipStream_t st) override {
+        if (a.r == 0 || a.r > ROUND_TINY) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_round_tiny<KK, KL>), dim3(1), dim3(1024), 0, st, a);
         return hipGetLastError();
     }
 

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <vector>
 
+#include "internal.hpp"
 #include "lift_kernels.hpp"
 
 namespace rh {
@@ -110,6 +111,43 @@ constexpr uint64_t SORT_BUCKET_MAX = 2ull << 20;
 constexpr uint64_t MINMAX_TILE = 2048;
 
 // Key-type-specialised device operations of the store.
+// A tiny protocol round in one launch (round_tiny.hpp k_round_tiny): the segments, the base and
+// delta runs with their search samples, where the round goes
+struct RoundTiny {
+    RoundIn in;  // sk, ek, skeys (start keys then end keys), remote: mapped input; bkeys, fps, sums: the base
+    RoundRun run;  // run.n == 0: no delta run (run.nb = the base rows either way)
+    const uint64_t *bsmp, *bsmp2;  // the base run's search samples and table
+    SearchTable btab;
+    const uint64_t *dsmp, *dsmp2;  // the delta run's (its keys: run.keys)
+    RoundSegs g;                   // global copies of the per-segment arrays, written only when the
+    uint64_t *gplace;              // children outnumber cap (the host then emits again from them)
+    uint64_t r, n;                 // segments; live keys of base + run
+    int sqrt_policy;
+    uint64_t b, cap;
+    uint8_t *out;                  // round_layout (mapped page-locked)
+    uint64_t seq;                  // stored to out word 7 last
+};
+
+// The small questions in one launch (round_tiny.hpp k_query_tiny), over the base run and any delta
+// run (as columns, RoundRun; run.n == 0: none): mode 0, the ranks of m <= QUERY_TINY keys; mode 1,
+// the keys of m <= QUERY_TINY ranks (select); mode 2, one key-range aggregate.  Input and output
+// in mapped page-locked memory, a sequence word stored last.
+constexpr uint32_t QUERY_TINY = 64;
+struct QueryTiny {
+    int mode;
+    const uint8_t *in;   // mode 0: m keys; 1: m u64 ranks (each < the view's size); 2: lo key, hi key
+    uint64_t m;
+    int lo_kind, hi_kind;  // mode 2: 0 unbounded, 1 included, 2 excluded (std::ops::Bound)
+    RoundIn base;          // bkeys, fps, bsums, ssums
+    RoundRun run;
+    const uint64_t *bsmp, *bsmp2;
+    SearchTable btab;
+    const uint64_t *dsmp, *dsmp2;
+    uint8_t *out;          // mode 0: m u64; 1: m keys; 2: one rh_aggregate
+    uint64_t *seq_word;
+    uint64_t seq;
+};
+
 struct StoreKeyOps {
     virtual ~StoreKeyOps() = default;
     // sort a batch by key (stable) and gather keys / fingerprints / ops into key order; with
@@ -157,6 +195,10 @@ struct StoreKeyOps {
     virtual hipError_t sample_stride(const uint8_t *keys, uint64_t n, uint64_t stride, uint64_t *smp, hipStream_t st) = 0;
     // the key type's Ord on the host (for argument checks)
     virtual int compare_keys_host(const uint8_t *a, const uint8_t *b) const = 0;
+    // a whole tiny round (a.r <= ROUND_TINY segments) in one launch of one workgroup
+    virtual hipError_t round_tiny(const RoundTiny &a, hipStream_t st) = 0;
+    // ranks, selects or a key-range aggregate (QueryTiny) in one launch of one workgroup
+    virtual hipError_t query_tiny(const QueryTiny &a, hipStream_t st) = 0;
 };
 
 // Σ count deltas of delta rows [0, i] = sblk[i / 65536] (exclusive super-block prefix)

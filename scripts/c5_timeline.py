@@ -1,4 +1,4 @@
-"""Per-batch kernel timeline of a config5 kernel trace (scripts/gpu_c5_trace.sh):
+"""Per-batch kernel timeline of a config5 kernel trace (scripts/gpu_session.sh):
 python scripts/c5_timeline.py gpurun_out/c5t/c5_kernel_trace.csv [batch ...]"""
 import csv
 import sys

@@ -1,6 +1,6 @@
 """Large copies and kernel totals from a rocprofv3 kernel + memory-copy trace (csv): every copy of at
 least 1 MiB with its duration and rate, the gaps in them, and the kernels' time by name -- to see
-what the host tier's background refresh costs beside the store's own work (scripts/gpu_r4_*.sh).
+what the host tier's background refresh costs beside the store's own work (scripts/gpu_session.sh).
 
   python scripts/copy_summary.py <dir with *_kernel_trace.csv and *_memory_copy_trace.csv>"""
 import collections

@@ -23,6 +23,9 @@
 #                     1 M-row batches into both replicas at 10^8 between d = 1 drives (tier_interleave)
 #   trace_interleave  the default-policy interleave under a kernel + memory-copy trace
 #   sstore            the sharded store's client (examples/sstore_client) on device 0
+#   rccl1             every workload under torch.distributed.run with one rank (the nccl = RCCL
+#                     process group, its gathers and barriers)
+#   inserts           10^6 staged single inserts into 10^5 and 10^7 resident rows (insert_latency)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -101,6 +104,18 @@ for step in "$@"; do
         rm -rf "$O/trint"
         ;;
     sstore) run sstore 300 $EX/sstore_client 4 2000000 ;;
+    rccl1)
+        for cfg in config4 config2 config5 snapshot rbsr; do
+            extra=""
+            [ "$cfg" = config5 ] && extra="--records 20000000"
+            run rccl1_$cfg 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+                --master-port 29517 bench.py --gpus 1 --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 $extra
+        done
+        ;;
+    inserts)
+        run inserts_1e5 300 $EX/insert_latency 100000 1000000 1
+        run inserts_1e7 300 $EX/insert_latency 10000000 1000000 1
+        ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -1,6 +1,6 @@
 """The longest HIP API calls, kernels and copies of a rocprofv3 trace (csv), in time order: where a
 host thread waited (hipEventSynchronize, hipStreamSynchronize, hipHostMalloc, ...) and what the
-device ran meanwhile (scripts/gpu_r4_s13.sh).
+device ran meanwhile (scripts/gpu_session.sh).
 
   python scripts/long_calls.py <dir with *_hip_api_trace.csv [*_kernel_trace.csv]> [min_us]"""
 import csv

@@ -1,4 +1,4 @@
-"""Kernel timeline of one snapshot reload from a kernel trace (scripts/gpu_r3_snap.sh):
+"""Kernel timeline of one snapshot reload from a kernel trace (scripts/gpu_session.sh):
 python scripts/snap_timeline.py <kernel_trace.csv> [reload index, default: the second to last]
 A reload starts at k_snap_walk; kernels of both stores' streams are listed in start order."""
 import csv

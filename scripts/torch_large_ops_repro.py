@@ -1,7 +1,7 @@
 """Repro attempt for DESIGN.md's round-3 claim that torch gathers and sorts of 10^8-row tensors
 returned wrong rows on this image (commit 29d67a0).
 
-Every op the round-3 debugging scripts (scripts/dbg_c5_100m.py) and bench.py's config5 path use on
+Every op the round-3 debugging scripts (since removed) and bench.py's config5 path use on
 10^8-row tensors is run on the GPU and checked against numpy on the host, on the same data:
   - torch.randperm(n, device="cuda", generator=...): a permutation of 0..n-1;
   - row gathers of a (n, 16) uint8 tensor by an int64 index (t[idx], index_select), and of its

@@ -1,5 +1,5 @@
 """Device timeline of single-row writes from a rocprofv3 kernel + memory-copy trace
-(scripts/gpu_r4_*.sh): every kernel and copy between two consecutive occurrences of a marker kernel,
+(scripts/gpu_session.sh): every kernel and copy between two consecutive occurrences of a marker kernel,
 with the idle gap before each and the span per write.
 
   python scripts/write_timeline.py <dir with *_kernel_trace.csv and *_memory_copy_trace.csv> <marker> [k ...]

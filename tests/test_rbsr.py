@@ -603,12 +603,17 @@ def test_gpu_native_round_large_batches(gpu, policy):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", ["fused", "unfused"])
 @pytest.mark.parametrize("policy", ["fixed16", "sqrt", "fixed2"])
-def test_gpu_rounds_over_pending_delta_run_match_oracle(gpu, oracle_lib, policy):
+def test_gpu_rounds_over_pending_delta_run_match_oracle(gpu, oracle_lib, policy, fused, monkeypatch):
     """Both replicas reach their contents through batches that stay in the delta run (inserts,
     deletes of base keys, overwrites, a key inserted then deleted): the one-call device round reads
     base + run in place (select over both, sums over both) and must equal the literal driver over
-    the final contents round by round -- without compacting either store."""
+    the final contents round by round -- without compacting either store.  fused: tiny rounds in
+    one launch (round_tiny.hpp k_round_tiny, the default); unfused: RSOS_HIP_ROUND_FUSED=0, the two
+    searches and k_round_small_view."""
+    monkeypatch.setenv("RSOS_HIP_ROUND_FUSED", "1" if fused == "fused" else "0")
+    monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused == "fused" else "0")
     from rsos_hip import RecordSchema, rbsr as R
     schema = RecordSchema.dated("bytes16", "bytes64")
     keys, ca, cb, only_a, only_b, mod = _dated_sets(11, 20_000, 60, 45, 30)
@@ -660,4 +665,59 @@ def test_gpu_large_rounds_over_pending_delta_run(gpu, policy):
     s = va.stats()
     assert s["delta_rows"] > 0 and s["compactions"] == 0
     for g in (va, fa, gb):
+        g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", ["fused", "unfused"])
+def test_tiny_questions_over_pending_delta_run(gpu, oracle_lib, fused, monkeypatch):
+    """The small questions a device answers when the host tier is off or stale -- rank, ranks of up
+    to 64 keys, select and dumps of up to 64 keys, an aggregate over a key range with every bound
+    kind -- in one launch each (round_tiny.hpp k_query_tiny) over a store whose delta run is pending,
+    against a freshly loaded store with the same contents and the oracle FTM; with
+    RSOS_HIP_QUERY_FUSED=0 the same questions take the multi-launch paths."""
+    monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused == "fused" else "0")
+    from rsos_hip import GpuFingerprintStore, RecordSchema, _abi as A
+    from rsos_hip.store import KeyRange
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(29, 20_000, 80, 10, 10)
+    va = _store_via_delta(schema, ca, 5)
+    monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "0")
+    fa = GpuFingerprintStore(schema)  # the base-only, multi-launch reference
+    fa.load_bulk(ca)
+    _, ov = _gpu_and_oracle(schema, ca)
+    ftm = ov.t
+    rng = np.random.default_rng(3)
+    n = fa.size()
+    assert va.size() == n
+    present = [bytes(k) for k in ca["keys"][rng.integers(0, n, 120)]]
+    absent = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(120)]
+    probes = present + absent + [b"\x00" * 16, b"\xff" * 16]
+    for z in probes:
+        assert va.rank(z) == fa.rank(z) == ftm.rank(z)
+    for m in (1, 64, 65):
+        pk = np.frombuffer(b"".join(probes[:m]), np.uint8).reshape(m, 16)
+        assert (va.ranks(pk) == fa.ranks(pk)).all()
+    for r in [0, n - 1] + [int(x) for x in rng.integers(0, n, 60)]:
+        assert va.select(r) == fa.select(r)
+    for lo, cnt in ((0, 64), (n - 64, 64), (n // 2, 65), (7, 1)):
+        k1, k2 = np.zeros(cnt * 16, np.uint8), np.zeros(cnt * 16, np.uint8)
+        A.check(A.lib().rh_store_keys(va._h, lo, lo + cnt, k1.ctypes.data), "keys")
+        A.check(A.lib().rh_store_keys(fa._h, lo, lo + cnt, k2.ctypes.data), "keys")
+        assert (k1 == k2).all()
+    kinds = ["unbounded", "included", "excluded"]
+    for i in range(120):
+        a, b = sorted((probes[int(rng.integers(len(probes)))], probes[int(rng.integers(len(probes)))]))
+        if i % 7 == 0:
+            a, b = b, a  # inverted: ZERO
+        lk, hk = kinds[i % 3], kinds[(i // 3) % 3]
+        rg = KeyRange(None if lk == "unbounded" else a, None if hk == "unbounded" else b, lk, hk)
+        got = va.aggregate(rg)
+        assert got == fa.aggregate(rg), (i, lk, hk)
+        if lk == "included" and hk == "excluded" and a <= b:  # the oracle FTM's own range form
+            fp, size = ftm.aggregate(a, b)
+            assert got.size == size and list(got.fingerprint.limbs) == [int(x) for x in fp]
+    s = va.stats()
+    assert s["delta_rows"] > 0 and s["compactions"] == 0
+    for g in (va, fa):
         g.close()

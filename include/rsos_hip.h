@@ -284,7 +284,13 @@ int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
  * logged and replayed into it.  No question waits for an O(n) copy under either policy.
  * Stats (nullable): base rows and delta entries (tree entries + run-copy entries) of a fresh tier
  * (0, 0 when stale), copies taken from the device (base refreshes and run copies) and batch folds
- * so far.                                                                                        */
+ * so far.
+ * Page-locked host memory: enabling the tier (or a reservation) pins (key_len + 32) B per row plus
+ * 8 B per 64 rows for the set the tier reads, with 25% headroom; the first refresh after that pins a
+ * second set of the same size, which later refreshes alternate with (a failure to pin leaves the
+ * tier stale and is never the write's error); the delta run's copy takes ~(key_len + 41) B per
+ * delta row (up to a quarter of the rows).  At 10^8 rows of 16-byte keys: 6 GB, then 12 GB, plus
+ * up to 1.4 GB.                                                                                  */
 int rh_store_tier_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_entries, uint64_t *refreshes,
                         uint64_t *folds);
 /* Wait until the host tier is fresh (a background refresh landed and swapped in, one started if
@@ -495,8 +501,10 @@ int rh_sstore_compact(rh_sstore *store);
  * Make the named internal failure point fail once (RH_ERR_OOM) on the calling thread; NULL or
  * "" clears it.  Points: "snapshot.load_begin" (the projection store's half of a reload),
  * "snapshot.load_finish" (the dated store's), "tier.run_copy" (the host tier's copy of the delta
- * run after a large batch: the batch still succeeds, the tier goes stale).  For tests of error
- * paths only.                                                                                */
+ * run after a large batch: the batch still succeeds, the tier goes stale), "small_batch.merge"
+ * (the next small batch's delta merge is reported failed when the store is next entered: that call
+ * and every later one return RH_ERR_HIP naming it, until a load replaces the contents).  For tests
+ * of error paths only.                                                                       */
 int rh_debug_fail_point(const char *name);
 
 /* ---- measurement -----------------------------------------------------------------------

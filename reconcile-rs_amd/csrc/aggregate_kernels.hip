@@ -1030,6 +1030,30 @@ hipError_t launch_round_emit_view(const uint64_t *hdr, uint64_t cap, uint64_t r,
     return hipGetLastError();
 }
 
+// every job's 16-byte units by the whole grid (the tails of jobs not a multiple of 16 bytes by
+// single bytes); src and dst 16-byte aligned (device buffers and page-locked allocations are)
+__global__ __launch_bounds__(256) void k_copy_to_host(CopyJobs j) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < j.n; k++) {
+        const uint64_t n16 = j.bytes[k] / 16;
+        const uint4 *s = reinterpret_cast<const uint4 *>(j.src[k]);
+        uint4 *d = reinterpret_cast<uint4 *>(j.dst[k]);
+        for (uint64_t i = tid; i < n16; i += nt) d[i] = s[i];
+        for (uint64_t i = n16 * 16 + tid; i < j.bytes[k]; i += nt) j.dst[k][i] = j.src[k][i];
+    }
+}
+
+hipError_t launch_copy_to_host(const CopyJobs &jobs, hipStream_t st) {
+    uint64_t tot = 0;
+    for (int k = 0; k < jobs.n; k++) tot += jobs.bytes[k];
+    if (tot == 0) return hipSuccess;
+    // one workgroup per CU at most: enough stores in flight for the link, and CUs left for the
+    // store's own kernels while a background refresh copies
+    const uint64_t wgs = std::min<uint64_t>(256, (tot / 16 + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_copy_to_host, dim3((uint32_t)wgs), dim3(256), 0, st, jobs);
+    return hipGetLastError();
+}
+
 hipError_t launch_round_copy_out(const uint64_t *hdr, uint64_t cap, uint32_t kl, const uint8_t *src, uint8_t *dst,
                                  uint64_t worst, hipStream_t st) {
     const uint64_t wgs = std::min<uint64_t>(std::max<uint64_t>(worst / 16 / 256, 1), 1024);

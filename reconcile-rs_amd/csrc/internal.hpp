@@ -130,6 +130,16 @@ hipError_t launch_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint
                              const RoundSegs &g, uint8_t *out, hipStream_t st);
 // the round (round_layout bytes, per the header at hdr; the header alone when the children
 // outnumber cap) from src into dst, mapped page-locked memory of at least `worst` bytes
+// Device -> host copies as a kernel's 16-byte stores into mapped page-locked memory (dst: the
+// mapped buffers' device addresses): ~52 GB/s over PCIe, where the copy engine moves ~30 GB/s
+// (microbench/pcie_copy.hip, profiles/r04_pcie_copy.jsonl).  Up to 8 (src, dst, bytes) jobs.
+struct CopyJobs {
+    const uint8_t *src[8];
+    uint8_t *dst[8];
+    uint64_t bytes[8];
+    int n;
+};
+hipError_t launch_copy_to_host(const CopyJobs &jobs, hipStream_t st);
 hipError_t launch_round_copy_out(const uint64_t *hdr, uint64_t cap, uint32_t kl, const uint8_t *src, uint8_t *dst,
                                  uint64_t worst, hipStream_t st);
 // every segment's raw rank range (from the searched bound ranks) and local aggregate

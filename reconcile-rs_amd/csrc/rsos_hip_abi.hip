@@ -610,6 +610,28 @@ struct PinnedVec {
     const T &operator[](size_t i) const { return p[i]; }
 };
 
+// a PinnedVec's device address, type-erased (the copy list of rh_store::copy_down)
+struct PinnedAny {
+    void **dptr;
+    const void **dptr_of;
+    void *p;
+    template <class T>
+    PinnedAny(PinnedVec<T> &v) : dptr(&v.dptr), dptr_of(&v.dptr_of), p(v.p) {}
+    int lookup(uint8_t **dev) const {  // 0 on success
+        if (!*dptr || *dptr_of != p) {
+            void *d = nullptr;
+            if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+                (void)hipGetLastError();
+                return 1;
+            }
+            *dptr = d;
+            *dptr_of = p;
+        }
+        *dev = static_cast<uint8_t *>(*dptr);
+        return 0;
+    }
+};
+
 struct rh_store {
     int device = 0;
     rh_schema schema{};
@@ -724,7 +746,33 @@ struct rh_store {
     // src/replica/write.rs:107-121).  A batch of up to small_batch_max rows takes the one-workgroup
     // path (apply_small, reading the rows from page-locked host memory); larger ones go up in one
     // copy per column.  No host sort, no per-row host work.
+    // A small batch commits on the host once k_small_batch's sequence word lands; the delta merge
+    // behind it may still run.  Its completion is checked (an event) when the store is next
+    // entered: a merge that failed leaves the host's bookkeeping ahead of the device, so the store
+    // refuses every call with that error -- attributed to the batch -- until a load replaces the
+    // contents.  Fail point "small_batch.merge" reports the next small batch's merge as failed.
+    hipEvent_t small_ev = nullptr;
+    bool small_pending = false, small_fault = false;
+    std::string sticky;
+    int health() {
+        if (!sticky.empty()) return fail(RH_ERR_HIP, sticky);
+        if (!small_pending) return RH_OK;
+        const hipError_t e = small_fault ? hipErrorLaunchFailure : hipEventQuery(small_ev);
+        if (e == hipErrorNotReady) return RH_OK;
+        small_pending = false;
+        if (e == hipSuccess) return RH_OK;
+        small_fault = false;
+        (void)hipGetLastError();
+        sticky = std::string("a committed small batch's delta merge failed (") + hipGetErrorString(e) +
+                 "): the store is inconsistent until its next load";
+        return fail(RH_ERR_HIP, sticky);
+    }
+    void health_reset() {  // a load replaces the contents
+        sticky.clear();
+        small_pending = small_fault = false;
+    }
     int flush() {
+        if (int rc = health()) return rc;
         if (!pend.n) return RH_OK;
         const size_t m = pend.n;
         const bool dated = schema.record_kind == RH_REC_DATED;
@@ -894,6 +942,10 @@ struct rh_store {
         RH_HIP(rh::launch_delta_merge(schema.key_kind, (int)kl, dkeys[cd].p, dslot[cd].p, nd, skeys.p, m, upos, usrc, rlist,
                                       mcnt.p, dkeys[nxt].p, dslot[nxt].p, rh_num_blocks(nd + m), dsmp[nxt].p,
                                       dsmp2[nxt].p, dheap.p, heap_len, stream));
+        if (!small_ev) RH_HIP(hipEventCreateWithFlags(&small_ev, hipEventDisableTiming));
+        RH_HIP(hipEventRecord(small_ev, stream));
+        small_pending = true;
+        if (fail_point("small_batch.merge")) small_fault = true;
         if ((rc = wait_small(a.seq))) return rc;
         const uint64_t *h = sb_res.data();
         if (h[6] & 1) {  // nothing committed
@@ -1014,6 +1066,33 @@ struct rh_store {
     PinnedVec<uint8_t> fold_keys{hipHostMallocCoherent}, fold_recs{hipHostMallocCoherent},
         fold_ops{hipHostMallocCoherent}, fold_fps{hipHostMallocCoherent}, fold_sops{hipHostMallocCoherent};
     bool tier_fresh() const { return tier_on && tier_version == version; }
+    // Device -> host copies into the tier's page-locked (mapped) buffers: one kernel whose 16-byte
+    // stores cross PCIe at ~52 GB/s (launch_copy_to_host), where copy commands move ~30 GB/s
+    // (profiles/r05_s1_interleave_trace_summary.txt); RSOS_HIP_COPY_KERNEL=0 keeps the copy commands.
+    struct Down {
+        void *host;
+        PinnedAny pin;
+        const void *dev;
+        size_t bytes;
+    };
+    int copy_kernel = getenv("RSOS_HIP_COPY_KERNEL") ? atoi(getenv("RSOS_HIP_COPY_KERNEL")) : 1;
+    int copy_down(const Down *d, int n, hipStream_t st) {
+        rh::CopyJobs j{};
+        bool kernel = copy_kernel != 0;
+        for (int k = 0; k < n && kernel; k++) {
+            uint8_t *dp = nullptr;
+            if (d[k].pin.lookup(&dp)) kernel = false;
+            j.src[k] = static_cast<const uint8_t *>(d[k].dev), j.dst[k] = dp, j.bytes[k] = d[k].bytes;
+        }
+        if (kernel) {
+            j.n = n;
+            RH_HIP(rh::launch_copy_to_host(j, st));
+            return RH_OK;
+        }
+        for (int k = 0; k < n; k++)
+            if (d[k].bytes) RH_HIP(hipMemcpyAsync(d[k].host, d[k].dev, d[k].bytes, hipMemcpyDeviceToHost, st));
+        return RH_OK;
+    }
     // Start a refresh of the host tier: compact, the prefix sums and samples on the device, and
     // their copy down on the copy stream into the spare set.  Returns at once (no wait).
     int start_refresh() {
@@ -1049,7 +1128,7 @@ struct rh_store {
             S.prefix.resize((n + 1) * 4 + 8);
             S.samp.resize(nsmp + nsmp2 + 8);
         } catch (const std::bad_alloc &) {
-            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+            return tier_oom();
         }
         // the prefix scan and the samples run on the copy stream too, behind the compaction: the
         // store's own stream goes on at once (a question answered by the device meanwhile is not
@@ -1064,9 +1143,10 @@ struct rh_store {
         }
         RH_HIP(hipEventRecord(rf_kdone, cstream));
         if (n) {
-            RH_HIP(hipMemcpyAsync(S.keys.data(), bkeys[cb].p, n * kl, hipMemcpyDeviceToHost, cstream));
-            RH_HIP(hipMemcpyAsync(S.prefix.data(), tier_dpre.p, (n + 1) * 32, hipMemcpyDeviceToHost, cstream));
-            RH_HIP(hipMemcpyAsync(S.samp.data(), tier_dsmp.p, (nsmp + nsmp2) * 8, hipMemcpyDeviceToHost, cstream));
+            const Down d[3] = {{S.keys.data(), S.keys, bkeys[cb].p, n * kl},
+                               {S.prefix.data(), S.prefix, tier_dpre.p, (n + 1) * 32},
+                               {S.samp.data(), S.samp, tier_dsmp.p, (nsmp + nsmp2) * 8}};
+            if ((rc = copy_down(d, 3, cstream))) return rc;
         } else {
             memset(S.prefix.data(), 0, 32);
         }
@@ -1154,9 +1234,24 @@ struct rh_store {
     // memory is left stale (questions go to the device; the next write tries again) -- reporting
     // it would make the caller think the batch failed.  Device errors still propagate.
     int post_batch() {
+        tier_host_oom = false;
         const int rc = post_batch_tier();
-        if (rc == RH_ERR_OOM) {
+        return tier_stale_on_host_oom(rc);
+    }
+    // A failure to pin host memory for the tier leaves the tier stale (questions go to the device;
+    // the next write tries again) and is not the caller's error: the write or load has committed.
+    // Device allocation failures (e.g. the compaction a refresh starts) still propagate.
+    bool tier_host_oom = false;
+    int tier_oom(const char *what = "host tier: page-locked allocation failed") {
+        tier_host_oom = true;
+        tier_version = ~0ull;
+        return fail(RH_ERR_OOM, what);
+    }
+    int tier_stale_on_host_oom(int rc) {
+        if (rc == RH_ERR_OOM && tier_host_oom) {
+            tier_host_oom = false;
             tier_version = ~0ull;
+            g_err.clear();  // reported as success: no stale message for the caller to read
             return RH_OK;
         }
         return rc;
@@ -1239,7 +1334,7 @@ struct rh_store {
     }
     int tier_run_snapshot() {
         int rc;
-        if (fail_point("tier.run_copy")) return fail(RH_ERR_OOM, "injected failure (tier run copy)");
+        if (fail_point("tier.run_copy")) return tier_oom("injected failure (tier run copy)");
         const uint64_t n1 = nd;
         if (n1 == 0) {  // nothing since the base copy: the base alone is the map
             tier.set_run(rh::HostTier::Run{});
@@ -1273,15 +1368,18 @@ struct rh_store {
             fit(trh_gs, ns + 8);
         } catch (const std::bad_alloc &) {
             tier_version = ~0ull;
-            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+            return tier_oom();
         }
-        RH_HIP(hipMemcpyAsync(trh_keys.data(), dkeys[cd].p, n1 * kl, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(trh_pre.data(), trun_pre.p, (n1 + 1) * 32, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(trh_cntp.data(), trun_cntp.p, (n1 + 1) * 4, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(trh_fl.data(), trun_fl.p, n1, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(trh_br.data(), trun_br.p, n1 * 4, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(trh_smp.data(), trun_smp.p, (ns + ns2) * 8, hipMemcpyDeviceToHost, stream));
-        RH_HIP(hipMemcpyAsync(trh_gs.data(), trun_gs.p, ns * 8, hipMemcpyDeviceToHost, stream));
+        {
+            const Down d[7] = {{trh_keys.data(), trh_keys, dkeys[cd].p, n1 * kl},
+                               {trh_pre.data(), trh_pre, trun_pre.p, (n1 + 1) * 32},
+                               {trh_cntp.data(), trh_cntp, trun_cntp.p, (n1 + 1) * 4},
+                               {trh_fl.data(), trh_fl, trun_fl.p, n1},
+                               {trh_br.data(), trh_br, trun_br.p, n1 * 4},
+                               {trh_smp.data(), trh_smp, trun_smp.p, (ns + ns2) * 8},
+                               {trh_gs.data(), trh_gs, trun_gs.p, ns * 8}};
+            if ((rc = copy_down(d, 7, stream))) return rc;
+        }
         if ((rc = sync())) {
             tier_version = ~0ull;
             return rc;
@@ -1513,6 +1611,7 @@ struct rh_store {
         // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
+        health_reset();
         version++;
         base_epoch++;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
@@ -1582,6 +1681,7 @@ struct rh_store {
     // the target becomes the base run (host state only: load_finish then takes the root and
     // checks the order flag)
     void load_commit(size_t m) {
+        health_reset();
         auto swap_buf = [](auto &x, auto &y) {
             std::swap(x.p, y.p);
             std::swap(x.cap, y.cap);
@@ -1608,16 +1708,18 @@ struct rh_store {
     int tier_reserve(uint64_t rows) {
         if (!tier_on) return RH_OK;
         const void *k0 = tsets[tact].keys.p, *p0 = tsets[tact].prefix.p, *s0 = tsets[tact].samp.p;
+        // the set the tier reads now; the spare set is pinned by the first refresh that copies into
+        // it (start_refresh: a failure there leaves the tier stale, never fails the caller), so
+        // enabling the tier or reserving pins (key_len + 32) B per row, not twice that
         try {
-            for (TierSet &S : tsets) {
-                S.keys.clear(), S.prefix.clear(), S.samp.clear();  // a move leaves the tier stale: nothing to keep
-                S.keys.reserve(rows * kl + 64);
-                S.prefix.reserve((rows + 1) * 4 + 8);
-                S.samp.reserve(rows / 64 + rows / 4096 + 16);
-            }
+            TierSet &S = tsets[tact];
+            S.keys.clear(), S.prefix.clear(), S.samp.clear();  // a move leaves the tier stale: nothing to keep
+            S.keys.reserve(rows * kl + 64);
+            S.prefix.reserve((rows + 1) * 4 + 8);
+            S.samp.reserve(rows / 64 + rows / 4096 + 16);
         } catch (const std::bad_alloc &) {
             tier_version = ~0ull;
-            return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+            return tier_oom();
         }
         if (tsets[tact].keys.p != k0 || tsets[tact].prefix.p != p0 || tsets[tact].samp.p != s0) tier_version = ~0ull;
         // the run copy's page-locked columns, for the largest run the policy copies (a quarter of
@@ -1641,7 +1743,7 @@ struct rh_store {
                 room(trh_gs, rr / 64 + 16);
             } catch (const std::bad_alloc &) {
                 tier_version = ~0ull;
-                return fail(RH_ERR_OOM, "host tier: page-locked allocation failed");
+                return tier_oom();
             }
             const void *after[7] = {trh_keys.p, trh_pre.p, trh_cntp.p, trh_fl.p, trh_br.p, trh_smp.p, trh_gs.p};
             if (tier.has_run() && memcmp(before, after, sizeof before)) tier_version = ~0ull;  // a held run moved
@@ -1650,10 +1752,12 @@ struct rh_store {
     }
     int load_finish(size_t m, bool last_wins) {
         int rc = load_finish_rows(m, last_wins);
-        if (!rc) rc = tier_reserve(nb + nb / 4);
+        if (rc) return rc;
+        tier_host_oom = false;
+        rc = tier_reserve(nb + nb / 4);
         if (!rc) rc = start_refresh();  // the tier copies the new base in the background
         if (!rc && tier_sync_writes) rc = settle();  // ... and, with writes keeping it fresh, the load waits
-        return rc;
+        return tier_stale_on_host_oom(rc);
     }
     int load_finish_rows(size_t m, bool last_wins) {
         int rc;
@@ -1777,13 +1881,16 @@ struct rh_store {
             return rc;
         RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        if ((rc = tier_reserve(rows))) return rc;
+        tier_host_oom = false;
+        // the tier's page-locked room: a failure leaves the tier stale, not the device reservation failed
+        if ((rc = tier_stale_on_host_oom(tier_reserve(rows)))) return rc;
         // bsums / ssums / samples may have moved: derive them again from the kept fingerprints
         if ((rc = resum_base())) return rc;
         if ((rc = sync())) return rc;
         // a tier whose page-locked sets moved is stale: with writes keeping it fresh, the
         // reservation (a setup call) copies it again now, not the next question's device path
-        if (tier_on && tier_sync_writes && !tier_fresh() && !rf_on && (rc = start_refresh())) return rc;
+        if (tier_on && tier_sync_writes && !tier_fresh() && !rf_on && (rc = tier_stale_on_host_oom(start_refresh())))
+            return rc;
         return tier_sync_writes ? settle() : RH_OK;
     }
     hipEvent_t res_ev = nullptr;  // apply_device_many: the result copy of the batch in flight
@@ -2639,6 +2746,8 @@ struct rh_store {
         dep = nullptr;
         if (res_ev) (void)hipEventDestroy(res_ev);
         res_ev = nullptr;
+        if (small_ev) (void)hipEventDestroy(small_ev);
+        small_ev = nullptr;
         for (auto &e : ls_ev)
             if (e) (void)hipEventDestroy(e), e = nullptr;
     }
@@ -2657,6 +2766,7 @@ struct rh_store {
     } while (0)
 
 static int flush_locked(rh_store *s) {
+    if (int rc = s->health()) return rc;
     if (!s->pend.n) return RH_OK;
     RH_HIP(hipSetDevice(s->device));
     return s->flush();

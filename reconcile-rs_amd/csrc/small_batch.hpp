@@ -31,8 +31,15 @@
 
 namespace rh {
 
-// the largest batch the one-workgroup path takes (LDS: keys + sorted fingerprints <= 48 KiB)
+// the largest batch the one-workgroup path takes.  LDS per workgroup (k_small_batch's arrays):
+// SBM * (KL + 32 + 3 * 2 + 2 * 4 + 2) bytes + ~1.5 KiB of reductions -- 67 KB for 16-byte keys
+// (1,024 rows), 42 KB for 32-byte keys (512 rows): within gfx950's 160 KiB per workgroup, not
+// within the 64 KiB of earlier CDNA parts (checked per instantiation below, small_batch_lds)
 __host__ __device__ constexpr uint32_t small_batch_max(int kl) { return kl <= 16 ? 1024u : 512u; }
+__host__ __device__ constexpr uint32_t small_batch_lds(int kl) {
+    return small_batch_max(kl) * (uint32_t)(kl + 32 + 3 * 2 + 2 * 4 + 2) + 16 * 4 * 2 + 16 * 5 * 4 + 16 * 4 + 16 * 8 * 8;
+}
+constexpr uint32_t LDS_BYTES_GFX950 = 160u * 1024u;
 
 // result block words (res): [0..2] new / overwritten / deleted rows vs the merged view, [3..5] the
 // merge's inserts / overwrites / removals in the delta run, [6] flags (1: duplicate keys, not
@@ -126,6 +133,7 @@ template <int KK, int KL, int VK, int VL, int RK, bool TAGS>
 __global__ __launch_bounds__(1024) void k_small_batch(SmallBatch a) {
     using L = Layout<KK, KL, VK, VL, RK>;
     constexpr uint32_t SBM = small_batch_max(KL);
+    static_assert(small_batch_lds(KL) <= LDS_BYTES_GFX950, "k_small_batch's LDS exceeds a gfx950 workgroup's 160 KiB");
     __shared__ __attribute__((aligned(16))) uint8_t K[SBM * KL];
     __shared__ __attribute__((aligned(16))) uint32_t F[SBM * 8];
     __shared__ uint16_t sidx[SBM], kidx[SBM], posof[SBM];

@@ -197,3 +197,38 @@ def test_staged_large_batch_keeps_last_operation(gpu, oracle_lib, monkeypatch):
     assert np.array_equal(st.fingerprints(), np.stack([np.frombuffer(model.d[k], np.uint8) for k in keys]))
     assert st.batch_stats()["large"] >= 3
     st.close()
+
+
+@pytest.mark.gpu
+def test_failed_small_merge_is_reported_and_sticks_until_a_load(gpu, oracle_lib):
+    """A small batch commits on the host once its first kernel's result word lands, with the delta
+    merge still queued behind it.  If that merge fails, the next call on the store reports it
+    (RH_ERR_HIP, naming the small batch's merge), and so does every call after it -- the host's
+    bookkeeping is ahead of the device -- until a load replaces the contents (fail point
+    "small_batch.merge" stands in for the device fault)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, _abi as A
+    sch = RecordSchema.plain("u64", "u64")
+    rng = np.random.default_rng(9)
+    st = GpuFingerprintStore(sch)
+    cols = _gen(rng, sch, 2000, False)
+    order = np.argsort(cols["keys"].copy().view("<u8").ravel())
+    cols = {c: v[order] for c, v in cols.items()}
+    _, first = np.unique(cols["keys"], axis=0, return_index=True)
+    cols = {c: v[np.sort(first)] for c, v in cols.items()}
+    st.load_bulk(cols)
+    n0 = st.size()
+    one = _gen(rng, sch, 1, False)
+    A.check(A.lib().rh_debug_fail_point(b"small_batch.merge"), "fail point")
+    st.apply(one, np.zeros(1, np.uint8))  # commits: the merge's failure is not known yet
+    for _ in range(2):
+        with pytest.raises(A.RsosHipError) as e:
+            st.size()
+        assert e.value.code == A.ERR_HIP and "small batch's delta merge failed" in str(e.value)
+    with pytest.raises(A.RsosHipError):
+        st.aggregate()
+    st.load_bulk(cols)  # a load replaces the contents: the store works again
+    assert st.size() == n0
+    st.apply(one, np.zeros(1, np.uint8))
+    assert st.size() == n0 + 1
+    assert st.batch_stats()["small"] >= 2
+    st.close()

@@ -303,31 +303,30 @@ __device__ __forceinline__ void neg256(uint32_t f[8]) {  // two's complement mod
         f[k] = s;
     }
 }
+// up to 256 rows [lo, hi) into a: every lane's four loads issued before any is added
+__device__ __forceinline__ void acc_rows256(Acc &a, const uint8_t *fps, uint64_t lo, uint64_t hi, uint32_t lane) {
+    uint32_t f[4][8];
+    bool v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t i = lo + lane + 64 * k;
+        v[k] = i < hi;
+        if (v[k]) load_fp(fps, i, f[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (v[k]) acc_add_fp(a, f[k]);
+}
 __device__ __forceinline__ void acc_range_pre(Acc &a, const uint8_t *fps, const uint8_t *bpre, uint64_t lo, uint64_t hi,
                                               uint32_t lane) {
     const uint64_t B = 256, b1 = (lo + B - 1) / B, b2 = hi / B;
     const uint64_t h1 = hi < b1 * B ? hi : b1 * B;          // head rows [lo, h1)
     const uint64_t t0 = b2 * B > h1 ? b2 * B : h1;          // tail rows [t0, hi)
-    uint32_t f[8][8];
-    bool v[8];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint64_t i = lo + lane + 64 * k;
-        v[k] = i < h1;
-        if (v[k]) load_fp(fps, i, f[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint64_t i = t0 + lane + 64 * k;
-        v[4 + k] = i < hi;
-        if (v[4 + k]) load_fp(fps, i, f[4 + k]);
-    }
     uint32_t p[8];
     const bool pv = b1 < b2 && lane < 2;  // lane 0: bpre[b2], lane 1: -bpre[b1]
     if (pv) load_fp(bpre, lane == 0 ? b2 : b1, p);
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-        if (v[k]) acc_add_fp(a, f[k]);
+    acc_rows256(a, fps, lo, h1, lane);
+    acc_rows256(a, fps, t0, hi, lane);
     if (pv) {
         if (lane == 1) neg256(p);
         acc_add_fp(a, p);

@@ -1,9 +1,10 @@
 // round_tiny.hpp -- a tiny rbsr protocol round (r <= ROUND_TINY segments) in ONE launch, over the
 // base run and any pending delta run (protocol_round_with_policy, rbsr/src/protocol.rs:212-317).
 //
-// One workgroup of 16 waves: the segments come in from mapped page-locked memory into LDS (one
+// One workgroup of 8 waves: the segments come in from mapped page-locked memory into LDS (one
 // PCIe round trip, every thread loading a word); the 2r bound keys are searched in the base run
-// (wave 0: table, then one line of keys, search_device.hpp) and in the delta run (wave 1) at once;
+// (a 16-lane group per key: table, then W-way probes of the window, search_device.hpp) and in the
+// delta run at once;
 // a wave per segment forms its view rank range, places and local sum (view_range_fp); one thread
 // decides the <= 16 segments and scans their children / enumeration counts; then a wave per child
 // cuts it (select over base + run, view_at) and sums it, and the round is written in round_layout()
@@ -19,8 +20,10 @@
 namespace rh {
 
 
+// 512 lanes (8 waves): 1,024 would cap a lane at 128 VGPRs and spill the emission's state to scratch
+constexpr uint32_t ROUND_TINY_THREADS = 512;
 template <int KK, int KL>
-__global__ __launch_bounds__(1024) void k_round_tiny(RoundTiny a) {
+__global__ __launch_bounds__(ROUND_TINY_THREADS) void k_round_tiny(RoundTiny a) {
     constexpr uint32_t RT = ROUND_TINY;
     __shared__ __align__(16) uint8_t keys[2 * RT * KL];
     __shared__ uint8_t sk[RT], ek[RT], kind[RT];
@@ -31,6 +34,11 @@ __global__ __launch_bounds__(1024) void k_round_tiny(RoundTiny a) {
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t r = (uint32_t)a.r;
     const RoundRun &R = a.run;
+    // phase clocks (the 100 MHz real-time counter, a read; stored by a vector store) when asked
+    auto clock = [&](int k) {
+        if (a.dbg && t == 0) a.dbg[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    clock(0);
     // the segments into LDS: kinds, bound keys (4-byte words), the peer's aggregates
     {
         const uint32_t nk = 2 * r * KL / 4;
@@ -40,13 +48,15 @@ __global__ __launch_bounds__(1024) void k_round_tiny(RoundTiny a) {
         for (uint32_t i = t; i < 5 * r; i += blockDim.x) rem[i] = a.in.remote[i];
     }
     __syncthreads();
+    clock(1);
     // the bound keys' lower bounds, a 16-lane group each (search_group: W-way probes), all at once:
     // groups 0..31 in the base run, 32..63 in the delta run; row q < r is segment q's start, row
     // r + j segment j's end; an unbounded side is not searched
     {
-        const uint32_t grp = t >> 4, gl = t & 15, q = grp & 31;
-        const bool in_run = grp >= 32;
-        if (q < 2 * r) {  // uniform per group
+        const uint32_t grp = t >> 4, gl = t & 15, ngrp = ROUND_TINY_THREADS / 16;
+        for (uint32_t job = grp; job < 4 * r; job += ngrp) {  // uniform per group
+            const bool in_run = job >= 2 * r;
+            const uint32_t q = in_run ? job - 2 * r : job;
             const bool bounded = q < r ? sk[q] : ek[q - r];
             uint32_t rank = 0;
             if (bounded && !in_run) search_group<KK, KL, 16>(a.in.bkeys, R.nb, a.btab, keys + q * KL, gl, &rank, nullptr);
@@ -55,8 +65,10 @@ __global__ __launch_bounds__(1024) void k_round_tiny(RoundTiny a) {
         }
     }
     __syncthreads();
+    clock(2);
     // segment j's view rank range, places and local sum (a wave each)
-    for (uint32_t j = w; j < r; j += 16) {
+    constexpr uint32_t NW = ROUND_TINY_THREADS / 64;
+    for (uint32_t j = w; j < r; j += NW) {
         const uint64_t bs = sk[j] ? rb[j] : 0, js = sk[j] ? rj[j] : 0;
         const uint64_t be = ek[j] ? rb[r + j] : R.nb, je = ek[j] ? rj[r + j] : R.n;
         const int64_t cs = R.n ? R.cntp[js] : 0, ce = R.n ? R.cntp[je] : 0;
@@ -71,20 +83,21 @@ __global__ __launch_bounds__(1024) void k_round_tiny(RoundTiny a) {
         }
     }
     __syncthreads();
+    clock(3);
     // the decisions, offsets and header: one thread, <= 16 segments
     if (t == 0) {
-        uint64_t cnt[5] = {0, 0, 0, 0, 0}, nc = 0, ne = 0;
+        uint64_t skipped = 0, split = 0, dropped = 0, nc = 0, ne = 0;  // (no indexed local array: scratch)
         for (uint32_t j = 0; j < r; j++) {
             const RoundSeg d = round_decide(lo[j], hi[j], loc + 5 * j, rem + 5 * j, a.n, a.sqrt_policy, a.b);
             kind[j] = (uint8_t)d.kind, stride[j] = d.stride, si[j] = d.si, ei[j] = d.ei;
             nch[j] = d.children, nen[j] = d.enums;
             choff[j] = nc, enoff[j] = ne;
             nc += d.children, ne += d.enums;
-            cnt[d.kind == 3 ? 4 : d.kind]++;
+            skipped += d.kind == 0, split += d.kind == 2, dropped += d.kind == 3;
         }
         tot[0] = nc, tot[1] = ne;
         uint64_t *hdr = reinterpret_cast<uint64_t *>(a.out);
-        hdr[0] = cnt[0], hdr[1] = ne, hdr[2] = cnt[2], hdr[3] = nc, hdr[4] = cnt[4];
+        hdr[0] = skipped, hdr[1] = ne, hdr[2] = split, hdr[3] = nc, hdr[4] = dropped;
         if (nc > a.cap) {  // the host emits again from global copies of the arrays
             for (uint32_t j = 0; j < r; j++) {
                 a.g.kind[j] = kind[j], a.g.lo[j] = lo[j], a.g.hi[j] = hi[j], a.g.stride[j] = stride[j];
@@ -96,6 +109,7 @@ __global__ __launch_bounds__(1024) void k_round_tiny(RoundTiny a) {
         }
     }
     __syncthreads();
+    clock(4);
     const uint64_t nc = tot[0], ne = tot[1];
     if (nc <= a.cap) {  // uniform
         const RoundLayout L = round_layout(nc, ne, KL);
@@ -104,15 +118,18 @@ __global__ __launch_bounds__(1024) void k_round_tiny(RoundTiny a) {
         il.sk = sk, il.ek = ek, il.skeys = keys, il.ekeys = keys + r * KL;
         const RoundSegs gl{kind, lo, hi, loc, stride, si, ei, nch, choff, nen, enoff};
         if (t < r && nen[t]) round_emit_enum(t, enoff[t], L, KL, il, gl, a.out);
-        for (uint64_t c = w; c < nc; c += 16) {
+        for (uint64_t c = w; c < nc; c += NW) {
             uint32_t j = 0;
             while (j + 1 < r && choff[j + 1] <= c) j++;  // the segment that owns child c
             round_emit_child_view(c, j, c - choff[j], L, KL, lane, il, R, gl, place, a.out);
         }
     }
+    __syncthreads();
+    clock(5);
     // every thread's host-visible writes before the sequence word
     __threadfence_system();
     __syncthreads();
+    clock(6);
     if (t == 0) __hip_atomic_store(reinterpret_cast<uint64_t *>(a.out) + 7, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

@@ -1076,9 +1076,11 @@ struct rh_store {
         size_t bytes;
     };
     int copy_kernel = getenv("RSOS_HIP_COPY_KERNEL") ? atoi(getenv("RSOS_HIP_COPY_KERNEL")) : 1;
-    int copy_down(const Down *d, int n, hipStream_t st) {
+    // kernel = false: copy commands (a background copy under "writes never wait": a copy kernel
+    // would hold CUs beside the batches and questions that run meanwhile)
+    int copy_down(const Down *d, int n, hipStream_t st, bool kernel_ok = true) {
         rh::CopyJobs j{};
-        bool kernel = copy_kernel != 0;
+        bool kernel = copy_kernel != 0 && kernel_ok;
         for (int k = 0; k < n && kernel; k++) {
             uint8_t *dp = nullptr;
             if (d[k].pin.lookup(&dp)) kernel = false;
@@ -1146,7 +1148,9 @@ struct rh_store {
             const Down d[3] = {{S.keys.data(), S.keys, bkeys[cb].p, n * kl},
                                {S.prefix.data(), S.prefix, tier_dpre.p, (n + 1) * 32},
                                {S.samp.data(), S.samp, tier_dsmp.p, (nsmp + nsmp2) * 8}};
-            if ((rc = copy_down(d, 3, cstream))) return rc;
+            // by kernel stores when the write or load that starts the refresh waits for it (the
+            // default policy); by the copy engines when it runs behind the store's own work
+            if ((rc = copy_down(d, 3, cstream, tier_sync_writes))) return rc;
         } else {
             memset(S.prefix.data(), 0, 32);
         }
@@ -2611,9 +2615,19 @@ struct rh_store {
             t.dsmp = view ? dsmp[cd].p : nullptr, t.dsmp2 = view ? dsmp2[cd].p : nullptr;
             t.g = g, t.gplace = place, t.r = r, t.n = n, t.sqrt_policy = sq, t.b = b, t.cap = cap, t.out = out_p;
             t.seq = ++round_seq;
+            if (round_dbg) {
+                if ((rc = dbg_clk.ensure(8))) return rc;
+                t.dbg = dbg_clk.p;
+            }
             RH_HIP(kops->round_tiny(t, stream));
             if ((rc = wait_word(reinterpret_cast<const uint64_t *>(pr_out.data()) + 7, t.seq))) return rc;
             memcpy(h, pr_out.data(), sizeof h);
+            if (round_dbg) {  // phase times of this round (10 ns ticks), summed until the store is destroyed
+                uint64_t c[8];
+                RH_HIP(hipMemcpy(c, dbg_clk.p, sizeof c, hipMemcpyDeviceToHost));
+                for (int k = 0; k < 6; k++) dbg_sum[k] += (double)(c[k + 1] - c[k]) * 0.01;
+                dbg_rounds++;
+            }
             return round_finish(h, cap, r, view, din, run, g, place, false, ch, en, oc);
         }
         if (nb)
@@ -2711,7 +2725,18 @@ struct rh_store {
     // A/B switch: RSOS_HIP_ROUND_FUSED=0 keeps tiny rounds on the two searches + k_round_small(_view)
     int round_fused = getenv("RSOS_HIP_ROUND_FUSED") ? atoi(getenv("RSOS_HIP_ROUND_FUSED")) : 1;
     uint64_t round_seq = 0;
+    // RSOS_HIP_ROUND_DBG=1: k_round_tiny's phase clocks, averaged to stderr when the store is destroyed
+    int round_dbg = getenv("RSOS_HIP_ROUND_DBG") ? atoi(getenv("RSOS_HIP_ROUND_DBG")) : 0;
+    DevBuf<uint64_t> dbg_clk;
+    double dbg_sum[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t dbg_rounds = 0;
     void release() {
+        if (round_dbg && dbg_rounds)
+            fprintf(stderr,
+                    "{\"k_round_tiny_phases_us\": {\"rounds\": %llu, \"input\": %.2f, \"searches\": %.2f, "
+                    "\"bounds\": %.2f, \"decide\": %.2f, \"emit\": %.2f, \"fence\": %.2f}}\n",
+                    (unsigned long long)dbg_rounds, dbg_sum[0] / dbg_rounds, dbg_sum[1] / dbg_rounds,
+                    dbg_sum[2] / dbg_rounds, dbg_sum[3] / dbg_rounds, dbg_sum[4] / dbg_rounds, dbg_sum[5] / dbg_rounds);
         (void)hipStreamSynchronize(stream);
         if (cstream) (void)hipStreamSynchronize(cstream);
         for (int k = 0; k < 2; k++) {
@@ -2737,7 +2762,7 @@ struct rh_store {
         if (rf_kdone) (void)hipEventDestroy(rf_kdone);
         cstream = nullptr, rf_ready = rf_ev = rf_kdone = nullptr, rf_on = false;
         snap.release();
-        bpre_b.release(); spre_b.release();
+        bpre_b.release(); spre_b.release(); dbg_clk.release();
         sbsums.release(); sssums.release(); sbsmp.release(); sbsmp2.release(); sbtab.release(); sbtabp.release();
         stot.release(); snap_words.release(); snap_hdr.release();
         scratch.release();

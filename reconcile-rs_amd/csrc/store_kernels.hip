@@ -1664,7 +1664,7 @@ struct KeyOps final : StoreKeyOps {
 
     hipError_t round_tiny(const RoundTiny &a, hipStream_t st) override {
         if (a.r == 0 || a.r > ROUND_TINY) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_round_tiny<KK, KL>), dim3(1), dim3(1024), 0, st, a);
+        hipLaunchKernelGGL((k_round_tiny<KK, KL>), dim3(1), dim3(ROUND_TINY_THREADS), 0, st, a);
         return hipGetLastError();
     }
 

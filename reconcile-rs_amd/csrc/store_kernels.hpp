@@ -126,6 +126,7 @@ struct RoundTiny {
     uint64_t b, cap;
     uint8_t *out;                  // round_layout (mapped page-locked)
     uint64_t seq;                  // stored to out word 7 last
+    uint64_t *dbg;                 // nullable: per-phase real-time clocks (RSOS_HIP_ROUND_DBG)
 };
 
 // The small questions in one launch (round_tiny.hpp k_query_tiny), over the base run and any delta

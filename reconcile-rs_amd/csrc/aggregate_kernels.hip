@@ -638,7 +638,7 @@ __global__ __launch_bounds__(1024) void k_round_small_view(const uint32_t *rank_
     if (t < 5) cnt[t] = 0;
     const bool mine = t < r;
     for (uint64_t j = w; j < r; j += 16)
-        bounds_view_one(j, lane, rank_b, rank_j, in.sk, in.ek, in, R, 1u, 1u, r, g.lo, g.hi, g.loc, place);
+        bounds_view_one<false>(j, lane, rank_b, rank_j, in.sk, in.ek, in, R, 1u, 1u, r, g.lo, g.hi, g.loc, place);
     __syncthreads();
     RoundSeg d{3, 0, 0, 0, 0, 0};
     if (mine) {
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(1024) void k_round_small_view(const uint32_t *rank_
     if (mine && d.enums) round_emit_enum(t, eo, L, kl, in, g, out);
     for (uint64_t c = w; c < nc; c += 16) {
         const uint64_t j = round_owner(g.choff, r, c);
-        round_emit_child_view(c, j, c - g.choff[j], L, kl, lane, in, R, g, place, out);
+        round_emit_child_view<false>(c, j, c - g.choff[j], L, kl, lane, in, R, g, place, out);
     }
 }
 __global__ __launch_bounds__(1024) void k_round_plan_scan(RoundIn in, RoundSegs g, uint64_t r, uint64_t n,

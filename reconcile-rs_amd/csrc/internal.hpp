@@ -79,6 +79,9 @@ struct RoundIn {
     // nullable: the base's exclusive prefix over its block sums (launch_block_prefix), which makes
     // any range sum the head and tail rows plus one difference (wave_range_fp_pre)
     const uint8_t *bpre = nullptr;
+    // nullable: the base's exclusive prefix over its rows (pre[i] = Σ fps [0, i), n + 1 entries):
+    // any range sum is one difference, two loads a lane can take alone (pre_range_fp)
+    const uint8_t *pre = nullptr;
 };
 // A round over the base + the delta run as they stand (no compaction first): the run's entries in
 // key order as columns (k_tier_run, the host tier's run copy) -- the contributions (cur - base)
@@ -96,6 +99,7 @@ struct RoundRun {
     const uint64_t *gsamp = nullptr;
     uint64_t nb = 0;
     const uint8_t *bpre = nullptr;  // nullable: the contributions' block prefix (as RoundIn::bpre)
+    const uint8_t *pre = nullptr;   // nullable: the contributions' row prefix (as RoundIn::pre)
 };
 // every segment's view rank range, its places (place[4 j ..]: start b, start j, end b, end j)
 // and local aggregate, from the bound keys' base ranks (rank_b) and run ranks (rank_j)

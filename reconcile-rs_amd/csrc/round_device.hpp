@@ -288,13 +288,8 @@ __device__ __forceinline__ ViewPlace view_at_group(const RoundRun &R, const uint
     const uint64_t b = b0 + (v - gprev);
     return ViewPlace{b, j, bkeys + b * kl};
 }
-// Σ of the live view keys between two places (lane 0's limbs)
-// Σ over rank range [lo, hi) of a run with a global exclusive block prefix (bpre[k] = Σ block sums
-// [0, k)): the head rows up to the first whole block and the tail rows after the last (fewer than
-// 256 each, every lane's four + four loads issued before any is added) plus bpre[b2] - bpre[b1]
-// for the whole blocks between -- two dependent rounds of loads whatever the range's length, where
-// wave_range_fp walks head and tail blocks and super-blocks lane by lane.  Accumulates into a.
-__device__ __forceinline__ void neg256(uint32_t f[8]) {  // two's complement mod 2^256
+// two's complement mod 2^256 (a fingerprint subtracted by adding it)
+__device__ __forceinline__ void neg256(uint32_t f[8]) {
     uint32_t c = 1;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -303,47 +298,157 @@ __device__ __forceinline__ void neg256(uint32_t f[8]) {  // two's complement mod
         f[k] = s;
     }
 }
-// up to 256 rows [lo, hi) into a: every lane's four loads issued before any is added
-__device__ __forceinline__ void acc_rows256(Acc &a, const uint8_t *fps, uint64_t lo, uint64_t hi, uint32_t lane) {
-    uint32_t f[4][8];
+// One part's (base or run) range [lo, hi) of n rows as at most two signed pieces, each <= 128
+// rows and at most one bpre entry: a short range is its rows; a longer one is P(hi) - P(lo), P(x) =
+// Σ rows [0, x) taken from the nearer block edge -- bpre[x/256] + rows [256(x/256), x) or
+// bpre[x/256 + 1] - rows [x, 256(x/256 + 1)) (bpre's last entry is the total, so the last partial
+// block's edge is n).  k < 0: no bpre entry.
+struct PrePiece {
+    uint64_t a, b;
+    int64_t k;
+    bool neg_rows, neg_pre;
+};
+__device__ __forceinline__ PrePiece pre_end(uint64_t x, uint64_t n, bool neg) {
+    const uint64_t k = x >> 8, off = x & 255;
+    if (off <= 128) return PrePiece{x - off, x, (int64_t)k, neg, neg};
+    const uint64_t e = ((k + 1) << 8) < n ? (k + 1) << 8 : n;
+    return PrePiece{x, e, (int64_t)k + 1, !neg, neg};
+}
+__device__ __forceinline__ void pre_pieces(uint64_t lo, uint64_t hi, uint64_t n, PrePiece &p, PrePiece &q) {
+    const PrePiece none{0, 0, -1, false, false};
+    if (hi <= lo) p = q = none;
+    else if (hi - lo <= 128) p = PrePiece{lo, hi, -1, false, false}, q = none;
+    else p = pre_end(hi, n, false), q = pre_end(lo, n, true);
+}
+__device__ __forceinline__ void piece_load(const uint8_t *fps, const PrePiece &p, uint32_t lane, uint32_t f0[8],
+                                           uint32_t f1[8], bool &v0, bool &v1) {
+    const uint64_t i0 = p.a + lane, i1 = i0 + 64;
+    v0 = i0 < p.b;
+    v1 = i1 < p.b;
+    if (v0) load_fp(fps, i0, f0);
+    if (v1) load_fp(fps, i1, f1);
+}
+__device__ __forceinline__ void acc_signed(Acc &a, uint32_t f[8], bool v, bool neg) {
+    if (!v) return;
+    if (neg) neg256(f);
+    acc_add_fp(a, f);
+}
+
+// (a - b) mod 2^256, as 8 x u32
+__device__ __forceinline__ void sub256(uint32_t a[8], const uint32_t b[8]) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t x = a[k], d = x - b[k], e = d - br;
+        br = (x < b[k] || d < br) ? 1u : 0u;
+        a[k] = e;
+    }
+}
+// the row prefixes' difference between two places by one lane: Σ base [b0, b1) + Σ run [j0, j1)
+// = pre_b[b1] - pre_b[b0] + pre_r[j1] - pre_r[j0] (four independent 32-B loads, one round of
+// latency; the lanes of a wave that ask the same places share the loads)
+__device__ __forceinline__ bool has_row_prefix(const RoundIn &in, const RoundRun &R) {
+    return in.pre && (R.n == 0 || R.pre);
+}
+__device__ __forceinline__ void pre_range_fp(const RoundIn &in, const RoundRun &R, uint64_t b0, uint64_t j0,
+                                             uint64_t b1, uint64_t j1, uint64_t fp[4]) {
+    uint32_t x[8], y[8], u[8], v[8];
+    const bool br = b1 > b0, rr = j1 > j0;
+    if (br) load_fp(in.pre, b1, x), load_fp(in.pre, b0, y);
+    if (rr) load_fp(R.pre, j1, u), load_fp(R.pre, j0, v);
+    uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (br) {
+        sub256(x, y);
+#pragma unroll
+        for (int k = 0; k < 8; k++) s[k] = x[k];
+    }
+    if (rr) {
+        sub256(u, v);
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint64_t t = (uint64_t)s[k] + u[k] + c;
+            s[k] = (uint32_t)t;
+            c = (uint32_t)(t >> 32);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) fp[q] = (uint64_t)s[2 * q] | ((uint64_t)s[2 * q + 1] << 32);
+}
+
+// two pieces of one part into a: four row loads per lane and two prefix entries (lanes 0, 1)
+// issued before any is added
+__device__ __forceinline__ void acc_pieces2(Acc &a, const uint8_t *fps, const uint8_t *bpre, const PrePiece &p0,
+                                            const PrePiece &p1, uint32_t lane) {
+    uint32_t f[4][8], pf[8];
     bool v[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint64_t i = lo + lane + 64 * k;
-        v[k] = i < hi;
-        if (v[k]) load_fp(fps, i, f[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (v[k]) acc_add_fp(a, f[k]);
+    piece_load(fps, p0, lane, f[0], f[1], v[0], v[1]);
+    piece_load(fps, p1, lane, f[2], f[3], v[2], v[3]);
+    const PrePiece &pq = lane == 0 ? p0 : p1;
+    const bool pv = lane < 2 && pq.k >= 0;
+    if (pv) load_fp(bpre, (uint64_t)pq.k, pf);
+    acc_signed(a, f[0], v[0], p0.neg_rows);
+    acc_signed(a, f[1], v[1], p0.neg_rows);
+    acc_signed(a, f[2], v[2], p1.neg_rows);
+    acc_signed(a, f[3], v[3], p1.neg_rows);
+    acc_signed(a, pf, pv, pq.neg_pre);
 }
-__device__ __forceinline__ void acc_range_pre(Acc &a, const uint8_t *fps, const uint8_t *bpre, uint64_t lo, uint64_t hi,
-                                              uint32_t lane) {
-    const uint64_t B = 256, b1 = (lo + B - 1) / B, b2 = hi / B;
-    const uint64_t h1 = hi < b1 * B ? hi : b1 * B;          // head rows [lo, h1)
-    const uint64_t t0 = b2 * B > h1 ? b2 * B : h1;          // tail rows [t0, hi)
-    uint32_t p[8];
-    const bool pv = b1 < b2 && lane < 2;  // lane 0: bpre[b2], lane 1: -bpre[b1]
-    if (pv) load_fp(bpre, lane == 0 ? b2 : b1, p);
-    acc_rows256(a, fps, lo, h1, lane);
-    acc_rows256(a, fps, t0, hi, lane);
-    if (pv) {
-        if (lane == 1) neg256(p);
-        acc_add_fp(a, p);
-    }
-}
+
+// Σ of the live view keys between two places (lane 0's limbs): base rows [b0, b1) plus run
+// contributions [j0, j1).  With both block prefixes present every load of the four pieces (eight
+// per lane, and four prefix entries on lanes 0-3) is issued before any is added: one round of
+// memory latency whatever the ranges' lengths.  With the row prefixes, their difference
+// (pre_range_fp).  Wide = false (a 1,024-lane workgroup, 128 VGPRs a
+// lane): the base's pieces, then the run's -- two rounds, no scratch.
+template <bool Wide = true>
 __device__ __forceinline__ void view_range_fp(const RoundIn &in, const RoundRun &R, uint64_t b0, uint64_t j0,
                                               uint64_t b1, uint64_t j1, uint32_t lane, uint64_t fp[4]) {
-    if (in.bpre && (R.n == 0 || R.bpre)) {  // both parts by prefix differences, one reduction
+    if (has_row_prefix(in, R)) {  // every lane the same sum (the loads are shared)
+        pre_range_fp(in, R, b0, j0, b1, j1, fp);
+        return;
+    }
+    if (in.bpre && (R.n == 0 || R.bpre)) {
+        PrePiece p0, p1, p2, p3;
+        pre_pieces(b0, b1, R.nb, p0, p1);
+        pre_pieces(j0, j1, R.n, p2, p3);
+        if (!Wide) {
+            Acc a;
+            acc_zero(a);
+            acc_pieces2(a, in.fps, in.bpre, p0, p1, lane);
+            if (j1 > j0) acc_pieces2(a, R.contrib, R.bpre, p2, p3, lane);  // uniform
+            acc_wave_reduce(a);
+            uint32_t g[8];
+            acc_normalise(a, g);
+#pragma unroll
+            for (int q = 0; q < 4; q++) fp[q] = (uint64_t)g[2 * q] | ((uint64_t)g[2 * q + 1] << 32);
+            return;
+        }
+        uint32_t f[8][8], pf[8];
+        bool v[8];
+        piece_load(in.fps, p0, lane, f[0], f[1], v[0], v[1]);
+        piece_load(in.fps, p1, lane, f[2], f[3], v[2], v[3]);
+        piece_load(R.contrib, p2, lane, f[4], f[5], v[4], v[5]);
+        piece_load(R.contrib, p3, lane, f[6], f[7], v[6], v[7]);
+        // lane q < 4: piece q's prefix entry
+        const PrePiece &pq = lane == 0 ? p0 : lane == 1 ? p1 : lane == 2 ? p2 : p3;
+        const bool pv = lane < 4 && pq.k >= 0;
+        if (pv) load_fp(lane < 2 ? in.bpre : R.bpre, (uint64_t)pq.k, pf);
         Acc a;
         acc_zero(a);
-        if (b1 > b0) acc_range_pre(a, in.fps, in.bpre, b0, b1, lane);
-        if (j1 > j0) acc_range_pre(a, R.contrib, R.bpre, j0, j1, lane);
+        acc_signed(a, f[0], v[0], p0.neg_rows);
+        acc_signed(a, f[1], v[1], p0.neg_rows);
+        acc_signed(a, f[2], v[2], p1.neg_rows);
+        acc_signed(a, f[3], v[3], p1.neg_rows);
+        acc_signed(a, f[4], v[4], p2.neg_rows);
+        acc_signed(a, f[5], v[5], p2.neg_rows);
+        acc_signed(a, f[6], v[6], p3.neg_rows);
+        acc_signed(a, f[7], v[7], p3.neg_rows);
+        acc_signed(a, pf, pv, pq.neg_pre);
         acc_wave_reduce(a);
-        uint32_t f[8];
-        acc_normalise(a, f);
+        uint32_t g[8];
+        acc_normalise(a, g);
 #pragma unroll
-        for (int q = 0; q < 4; q++) fp[q] = (uint64_t)f[2 * q] | ((uint64_t)f[2 * q + 1] << 32);
+        for (int q = 0; q < 4; q++) fp[q] = (uint64_t)g[2 * q] | ((uint64_t)g[2 * q + 1] << 32);
         return;
     }
     uint64_t d[4];
@@ -355,6 +460,7 @@ __device__ __forceinline__ void view_range_fp(const RoundIn &in, const RoundRun 
 // Segment j's view rank range [l, h), its places and its aggregate (ZERO when inverted), by one
 // wave.  The bound keys' ranks are rank_x[ia * j] / rank_x[ib * j + off] (a round: starts then
 // ends; the two-call path: interleaved)
+template <bool Wide = true>
 __device__ __forceinline__ void bounds_view_one(uint64_t j, uint32_t lane, const uint32_t *rank_b,
                                                 const uint32_t *rank_j, const uint8_t *sk, const uint8_t *ek,
                                                 const RoundIn &in, const RoundRun &R, uint32_t ia, uint32_t ib,
@@ -365,7 +471,7 @@ __device__ __forceinline__ void bounds_view_one(uint64_t j, uint32_t lane, const
     const uint64_t be = ek[j] ? rank_b[qe] : R.nb, je = ek[j] ? rank_j[qe] : R.n;
     const uint64_t l = (uint64_t)((int64_t)bs + R.cntp[js]), h = (uint64_t)((int64_t)be + R.cntp[je]);
     uint64_t fp[4] = {0, 0, 0, 0};
-    if (h > l) view_range_fp(in, R, bs, js, be, je, lane, fp);  // uniform; an inverted range is ZERO
+    if (h > l) view_range_fp<Wide>(in, R, bs, js, be, je, lane, fp);  // uniform; an inverted range is ZERO
     if (lane == 0) {
         lo_out[j] = l;
         hi_out[j] = h;
@@ -386,6 +492,7 @@ __device__ __forceinline__ void bounds_view_one(uint64_t j, uint32_t lane, const
 
 // child c (k-th of segment j) over the view: round_emit_child with the cut keys selected from
 // base + run and the sums taken between places
+template <bool Wide = true>
 __device__ __forceinline__ void round_emit_child_view(uint64_t c, uint64_t j, uint64_t k, const RoundLayout &L,
                                                       uint32_t kl, uint32_t lane, const RoundIn &in,
                                                       const RoundRun &R, const RoundSegs &g, const uint64_t *place,
@@ -409,7 +516,7 @@ __device__ __forceinline__ void round_emit_child_view(uint64_t c, uint64_t j, ui
             ekd = 1, ekey = z.key;
         }
         uint64_t fp[4];
-        view_range_fp(in, R, a.b, a.j, z.b, z.j, lane, fp);
+        view_range_fp<Wide>(in, R, a.b, a.j, z.b, z.j, lane, fp);
         if (lane == 0) {
             agg[0] = fp[0];
             agg[1] = fp[1];

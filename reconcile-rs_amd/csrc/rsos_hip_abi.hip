@@ -1328,8 +1328,11 @@ struct rh_store {
         RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
         RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
         RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
-        if ((rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64))) return rc;
-        RH_HIP(rh::launch_block_prefix(n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, stream));
+        if ((rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64)) ||
+            (rc = trun_pre.ensure((n1 + 1) * 32 + 64)))
+            return rc;
+        // block and row prefixes: a range sum over the run is then one difference (pre_range_fp)
+        RH_HIP(rh::launch_prefix(trun_c.p, n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, trun_pre.p, stream));
         RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         RH_HIP(rh::launch_tier_gsamp(trun_br.p, trun_cntp.p, trun_fl.p, n1, trun_gs.p, stream));
@@ -1347,12 +1350,8 @@ struct rh_store {
         }
         const uint64_t ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096, nbk = rh_num_blocks(n1),
                        nsb = rh_num_superblocks(n1);
-        if ((rc = run_columns()) || (rc = trun_smp.ensure(ns + ns2 + 8)) ||
-            (rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64)) ||
-            (rc = trun_pre.ensure((n1 + 1) * 32 + 64)))
-            return rc;
-        // the host walks prefix sums (HostTier::Run::prefix); the device kernels sum blocks instead
-        RH_HIP(rh::launch_prefix(trun_c.p, n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, trun_pre.p, stream));
+        // run_columns formed the contributions' row prefix: the host walks it (HostTier::Run::prefix)
+        if ((rc = run_columns()) || (rc = trun_smp.ensure(ns + ns2 + 8))) return rc;
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
         try {
@@ -2257,24 +2256,51 @@ struct rh_store {
                             trun_br.p,
                             trun_gs.p,
                             nb,
-                            trun_bpre.p};
-        *in = rh::RoundIn{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
+                            trun_bpre.p,
+                            trun_pre.p};
+        *in = base_in();
         return RH_OK;
     }
-    // The base run's exclusive block prefix (bpre_b[k] = Σ block sums [0, k)), formed once per base
-    // (after a load or a compaction; ~n / 256 entries) on the first question that sums over it on
-    // the device: any range sum is then its head and tail rows plus one difference (view_range_fp)
-    DevBuf<uint8_t> bpre_b, spre_b;
+    // The base run's exclusive prefixes, formed once per base (after a load or a compaction) on the
+    // first question that sums over it on the device: over its block sums (bpre_b[k] = Σ blocks
+    // [0, k), ~n / 256 entries: any range sum is head and tail rows plus one difference) and, when
+    // the device has the room (32 B a row: 3.2 GB at 10^8 rows), over its rows (pre_b[i] = Σ fps
+    // [0, i): any range sum is one difference, two loads).  RSOS_HIP_ROW_PREFIX=0: block prefix only.
+    DevBuf<uint8_t> bpre_b, spre_b, pre_b;
     uint64_t bpre_epoch = ~0ull;
+    bool pre_b_ok = false;
+    int row_prefix = getenv("RSOS_HIP_ROW_PREFIX") ? atoi(getenv("RSOS_HIP_ROW_PREFIX")) : 1;
     int ensure_base_prefix() {
         int rc;
         if (bpre_epoch == base_epoch && bpre_b.p) return RH_OK;
         const uint64_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
         if ((rc = bpre_b.ensure((nbk + 1) * 32 + 64)) || (rc = spre_b.ensure((ns + 1) * 32 + 64))) return rc;
-        if (nb) RH_HIP(rh::launch_block_prefix(nb, bsums.p, ssums.p, spre_b.p, bpre_b.p, stream));
-        else RH_HIP(hipMemsetAsync(bpre_b.p, 0, 32, stream));
+        pre_b_ok = false;
+        const size_t need = (nb + 1) * 32 + 64;
+        if (row_prefix && nb && pre_b.cap < need) {  // room for it, with 1 GiB to spare, or go without
+            size_t free_b = 0, total_b = 0;
+            pre_b.release();
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > need + (1ull << 30)) {
+                const std::string keep = g_err;  // a refused allocation is not the caller's error
+                if (pre_b.ensure(need) != RH_OK) g_err = keep;
+            }
+        }
+        if (row_prefix && nb && pre_b.cap >= need) {
+            RH_HIP(rh::launch_prefix(bfps[cb].p, nb, bsums.p, ssums.p, spre_b.p, bpre_b.p, pre_b.p, stream));
+            pre_b_ok = true;
+        } else if (nb) {
+            RH_HIP(rh::launch_block_prefix(nb, bsums.p, ssums.p, spre_b.p, bpre_b.p, stream));
+        } else {
+            RH_HIP(hipMemsetAsync(bpre_b.p, 0, 32, stream));
+        }
         bpre_epoch = base_epoch;
         return RH_OK;
+    }
+    // the base run as the round and query kernels read it (no segments)
+    rh::RoundIn base_in() const {
+        rh::RoundIn b{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
+        b.pre = pre_b_ok ? pre_b.p : nullptr;
+        return b;
     }
     // the run ranks of m keys (lower bounds among the delta run's keys)
     hipError_t search_run(const uint8_t *keys, size_t m, uint32_t *out) {
@@ -2362,7 +2388,7 @@ struct rh_store {
             if ((rc = view_of(&run, &unused))) return rc;
         }
         run.nb = nb;
-        constexpr size_t o_out = 4096, o_seq = 8192;  // inputs: at most QUERY_TINY 32-byte keys
+        constexpr size_t o_out = 0, o_seq = 4096;  // output: at most QUERY_TINY 32-byte keys
         try {
             qt_buf.resize(o_seq + 64);
         } catch (const std::bad_alloc &) {
@@ -2370,11 +2396,12 @@ struct rh_store {
         }
         uint8_t *d;
         if ((rc = dev_ptr(qt_buf, &d))) return rc;
-        memcpy(qt_buf.data(), in, in_bytes);
         rh::QueryTiny q{};
-        q.mode = mode, q.in = d, q.m = m, q.lo_kind = lo_kind, q.hi_kind = hi_kind;
+        if (in_bytes > sizeof q.in) return fail(RH_ERR_ARG, "query: question larger than the tiny query's");
+        memcpy(q.in, in, in_bytes);
+        q.mode = mode, q.m = m, q.lo_kind = lo_kind, q.hi_kind = hi_kind;
         if ((rc = ensure_base_prefix())) return rc;
-        q.base = rh::RoundIn{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
+        q.base = base_in();
         q.run = run;
         q.bsmp = bsmp.p, q.bsmp2 = bsmp2.p, q.btab = (!bsmp2.p || nb == 0) ? rh::SearchTable{} : base_table();
         q.dsmp = nd ? dsmp[cd].p : nullptr, q.dsmp2 = nd ? dsmp2[cd].p : nullptr;
@@ -2526,6 +2553,7 @@ struct rh_store {
                        rh_round_outcome *oc) {
         int rc;
         const size_t r = in.n;
+        const double h0 = round_dbg ? now_us() : 0;
         if (oc) *oc = rh_round_outcome{};
         *ch = rh_segments{};
         *en = rh_segments{};
@@ -2538,6 +2566,7 @@ struct rh_store {
             rh::RoundIn unused;
             if ((rc = view_of(&run, &unused))) return rc;
         }
+        const double hv = round_dbg ? now_us() : 0;
         const uint64_t n = size();                 // live keys of base + run
         const uint64_t b = param < 2 ? 2 : param;  // FanOut::new
         // device input: start kinds, end kinds, start keys then end keys (searched as one run of
@@ -2593,21 +2622,27 @@ struct rh_store {
                     if (p.src) RH_HIP(hipMemcpyAsync(r_in.p + p.off, p.src, p.bytes, hipMemcpyHostToDevice, stream));
             }
         }
+        const double hs = round_dbg ? now_us() : 0;
         const uint8_t *d_sk = in_p, *d_ek = in_p + o_ek, *d_skeys = in_p + o_sk, *d_ekeys = in_p + o_ekeys;
         const uint64_t *d_rem = reinterpret_cast<const uint64_t *>(in_p + o_rem);
         uint64_t *lo = r_seg.p, *hi = lo + r, *loc = hi + r, *st = loc + 5 * r, *si = st + r, *ei = si + r,
                  *nch = ei + r, *choff = nch + r, *nen = choff + r, *enoff = nen + r, *place = enoff + r;
         const rh::RoundSegs g{r_kind.p, lo, hi, loc, st, si, ei, nch, choff, nen, enoff};
         if ((rc = ensure_base_prefix())) return rc;
-        const rh::RoundIn din{d_sk, d_ek, d_skeys, d_ekeys, d_rem, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
+        rh::RoundIn din = base_in();
+        din.sk = d_sk, din.ek = d_ek, din.skeys = d_skeys, din.ekeys = d_ekeys, din.remote = d_rem;
         uint64_t *hdr = reinterpret_cast<uint64_t *>(r_out.p);
         const int sq = policy == RH_POLICY_SQRT_FAN_OUT;
         uint64_t h[5];
-        if (zero_copy && round_fused) {
+        if (zero_copy && round_fused && kl <= rh::ROUND_TINY_KL && r <= rh::ROUND_TINY_SEGS) {
             // a tiny round whole in one launch (round_tiny.hpp): the bound keys' searches in both
             // runs, the bounds, decisions and emission, the per-segment arrays in LDS; the host
             // waits for the sequence word the kernel stores last into the mapped output
             rh::RoundTiny t{};
+            memcpy(t.isk, stage_in.data(), r);
+            memcpy(t.iek, stage_in.data() + o_ek, r);
+            memcpy(t.ikeys, stage_in.data() + o_sk, 2 * r * kl);  // start keys then end keys
+            memcpy(t.irem, stage_in.data() + o_rem, r * sizeof(rh_aggregate));
             t.in = din;
             t.run = run;
             t.run.nb = nb;
@@ -2619,16 +2654,26 @@ struct rh_store {
                 if ((rc = dbg_clk.ensure(8))) return rc;
                 t.dbg = dbg_clk.p;
             }
+            const double h1 = round_dbg ? now_us() : 0;
             RH_HIP(kops->round_tiny(t, stream));
+            const double h2 = round_dbg ? now_us() : 0;
             if ((rc = wait_word(reinterpret_cast<const uint64_t *>(pr_out.data()) + 7, t.seq))) return rc;
+            const double h3 = round_dbg ? now_us() : 0;
             memcpy(h, pr_out.data(), sizeof h);
+            rc = round_finish(h, cap, r, view, din, run, g, place, false, ch, en, oc);
             if (round_dbg) {  // phase times of this round (10 ns ticks), summed until the store is destroyed
+                const double h4 = now_us();
                 uint64_t c[8];
                 RH_HIP(hipMemcpy(c, dbg_clk.p, sizeof c, hipMemcpyDeviceToHost));
                 for (int k = 0; k < 6; k++) dbg_sum[k] += (double)(c[k + 1] - c[k]) * 0.01;
+                dbg_host[0] += h1 - h0, dbg_host[1] += h2 - h1, dbg_host[2] += h3 - h2, dbg_host[3] += h4 - h3;
+                dbg_prep[0] += hv - h0, dbg_prep[1] += hs - hv, dbg_prep[2] += h1 - hs;
+                if (h0 - dbg_last < 100) dbg_host[4] += h0 - dbg_last, dbg_host_n++;  // the caller's own time
+                                                                                        // between rounds of a drive
+                dbg_last = now_us();
                 dbg_rounds++;
             }
-            return round_finish(h, cap, r, view, din, run, g, place, false, ch, en, oc);
+            return rc;
         }
         if (nb)
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
@@ -2729,7 +2774,13 @@ struct rh_store {
     int round_dbg = getenv("RSOS_HIP_ROUND_DBG") ? atoi(getenv("RSOS_HIP_ROUND_DBG")) : 0;
     DevBuf<uint64_t> dbg_clk;
     double dbg_sum[6] = {0, 0, 0, 0, 0, 0};
+    double dbg_host[5] = {0, 0, 0, 0, 0}, dbg_last = 0;  // host: prep, launch, wait, finish, caller
+    uint64_t dbg_host_n = 0;
+    double dbg_prep[3] = {0, 0, 0};  // prep: the view, the staging, the launch record
     uint64_t dbg_rounds = 0;
+    static double now_us() {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
     void release() {
         if (round_dbg && dbg_rounds)
             fprintf(stderr,
@@ -2737,6 +2788,13 @@ struct rh_store {
                     "\"bounds\": %.2f, \"decide\": %.2f, \"emit\": %.2f, \"fence\": %.2f}}\n",
                     (unsigned long long)dbg_rounds, dbg_sum[0] / dbg_rounds, dbg_sum[1] / dbg_rounds,
                     dbg_sum[2] / dbg_rounds, dbg_sum[3] / dbg_rounds, dbg_sum[4] / dbg_rounds, dbg_sum[5] / dbg_rounds);
+        if (round_dbg && dbg_rounds > 1)
+            fprintf(stderr,
+                    "{\"round_host_us\": {\"prep\": %.2f, \"launch\": %.2f, \"wait\": %.2f, \"finish\": %.2f, "
+                    "\"caller_between_rounds\": %.2f, \"prep_view\": %.2f, \"prep_stage\": %.2f, \"prep_args\": %.2f}}\n",
+                    dbg_host[0] / dbg_rounds, dbg_host[1] / dbg_rounds, dbg_host[2] / dbg_rounds, dbg_host[3] / dbg_rounds,
+                    dbg_host_n ? dbg_host[4] / dbg_host_n : 0.0, dbg_prep[0] / dbg_rounds, dbg_prep[1] / dbg_rounds,
+                    dbg_prep[2] / dbg_rounds);
         (void)hipStreamSynchronize(stream);
         if (cstream) (void)hipStreamSynchronize(cstream);
         for (int k = 0; k < 2; k++) {
@@ -2762,7 +2820,7 @@ struct rh_store {
         if (rf_kdone) (void)hipEventDestroy(rf_kdone);
         cstream = nullptr, rf_ready = rf_ev = rf_kdone = nullptr, rf_on = false;
         snap.release();
-        bpre_b.release(); spre_b.release(); dbg_clk.release();
+        bpre_b.release(); spre_b.release(); pre_b.release(); pre_b_ok = false; dbg_clk.release();
         sbsums.release(); sssums.release(); sbsmp.release(); sbsmp2.release(); sbtab.release(); sbtabp.release();
         stot.release(); snap_words.release(); snap_hdr.release();
         scratch.release();

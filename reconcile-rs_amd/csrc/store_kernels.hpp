@@ -113,8 +113,14 @@ constexpr uint64_t MINMAX_TILE = 2048;
 // Key-type-specialised device operations of the store.
 // A tiny protocol round in one launch (round_tiny.hpp k_round_tiny): the segments, the base and
 // delta runs with their search samples, where the round goes
+constexpr uint32_t ROUND_TINY_SEGS = 16, ROUND_TINY_KL = 32;  // = ROUND_TINY; the widest key
 struct RoundTiny {
-    RoundIn in;  // sk, ek, skeys (start keys then end keys), remote: mapped input; bkeys, fps, sums: the base
+    // the segments, inline in the kernel's arguments: the kernel reads them where the runtime put
+    // them (in device memory), not over PCIe from page-locked memory -- 2.9 us a round as mapped input
+    uint64_t irem[5 * ROUND_TINY_SEGS];               // the peer's aggregates
+    uint8_t ikeys[2 * ROUND_TINY_SEGS * ROUND_TINY_KL];  // start keys, then end keys (kl bytes each)
+    uint8_t isk[ROUND_TINY_SEGS], iek[ROUND_TINY_SEGS];
+    RoundIn in;  // sk, ek, skeys, ekeys, remote: the mapped copy (unread); bkeys, fps, sums: the base
     RoundRun run;  // run.n == 0: no delta run (run.nb = the base rows either way)
     const uint64_t *bsmp, *bsmp2;  // the base run's search samples and table
     SearchTable btab;
@@ -131,12 +137,14 @@ struct RoundTiny {
 
 // The small questions in one launch (round_tiny.hpp k_query_tiny), over the base run and any delta
 // run (as columns, RoundRun; run.n == 0: none): mode 0, the ranks of m <= QUERY_TINY keys; mode 1,
-// the keys of m <= QUERY_TINY ranks (select); mode 2, one key-range aggregate.  Input and output
-// in mapped page-locked memory, a sequence word stored last.
+// the keys of m <= QUERY_TINY ranks (select); mode 2, one key-range aggregate.  The question in
+// the kernel's arguments, the answer in mapped page-locked memory with a sequence word stored last.
 constexpr uint32_t QUERY_TINY = 64;
 struct QueryTiny {
+    // the question, inline in the kernel's arguments (as RoundTiny's segments): mode 0, m keys;
+    // 1, m u64 ranks (each < the view's size); 2, lo key, hi key
+    uint64_t in[QUERY_TINY * ROUND_TINY_KL / 8];
     int mode;
-    const uint8_t *in;   // mode 0: m keys; 1: m u64 ranks (each < the view's size); 2: lo key, hi key
     uint64_t m;
     int lo_kind, hi_kind;  // mode 2: 0 unbounded, 1 included, 2 excluded (std::ops::Bound)
     RoundIn base;          // bkeys, fps, bsums, ssums

@@ -123,11 +123,15 @@ static cost_t reconcile(rh_store *a, rh_store *b, const rh_schema *sc) {
         const uint8_t *esk = en.start_kinds, *eek = en.end_kinds;
         const uint64_t *eskey = (const uint64_t *)en.start_keys, *eekey = (const uint64_t *)en.end_keys;
         for (size_t j = 0; j < en.n; j++) {
-            uint64_t lo = 0, hi = 0, size = 0;
+            uint64_t lo = 0, hi = 0, size = 0, q[2], rk[2];
+            size_t nq = 0;
             CHECK(rh_store_len(resp, &size));
-            if (esk[j]) CHECK(rh_store_rank(resp, &eskey[j], &lo));
             hi = size;
-            if (eek[j]) CHECK(rh_store_rank(resp, &eekey[j], &hi));
+            if (esk[j]) q[nq++] = eskey[j];
+            if (eek[j]) q[nq++] = eekey[j];
+            if (nq) CHECK(rh_store_ranks(resp, q, nq, rk)); /* both bounds' ranks in one question */
+            if (esk[j]) lo = rk[0];
+            if (eek[j]) hi = rk[nq - 1];
             if (hi > lo) {
                 if (hi - lo > enum_cap) {
                     enum_cap = 2 * (hi - lo);

@@ -20,6 +20,7 @@
 #                     host tier on / off
 #   trace_latency_off the same, tier off, under a kernel trace (kernel summary + timeline)
 #   latency_phases    the same, tier off, with k_round_tiny's phase clocks (RSOS_HIP_ROUND_DBG=1)
+#   launch            examples/launch_latency: one waited-for small launch, 16 B and ~2.4 KB arguments
 #   interleave_sync interleave_nowait interleave_off
 #                     1 M-row batches into both replicas at 10^8 between d = 1 drives (tier_interleave)
 #   trace_interleave  the default-policy interleave under a kernel + memory-copy trace
@@ -91,6 +92,7 @@ for step in "$@"; do
     latency_tier) run latency_tier 300 $EX/rbsr_latency "$N" 1 200 1 1 ;;
     latency_off) run latency_off 300 $EX/rbsr_latency "$N" 1 40 0 1 ;;
     latency_phases) run latency_phases 300 env RSOS_HIP_ROUND_DBG=1 $EX/rbsr_latency "$N" 1 40 0 1 ;;
+    launch) run launch 120 $EX/launch_latency 2000 ;;
     trace_latency_off)
         run trace_latency_off 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trlat" -o tr -- $EX/rbsr_latency "$N" 1 10 0 1
         python3 scripts/write_timeline.py "$O/trlat" k_round > "$O/${TAG}_latency_off_timeline.txt" 2>&1 || true

@@ -603,7 +603,7 @@ def test_gpu_native_round_large_batches(gpu, policy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fused", ["fused", "unfused"])
+@pytest.mark.parametrize("fused", ["fused", "fused_block", "unfused", "unfused_block"])
 @pytest.mark.parametrize("policy", ["fixed16", "sqrt", "fixed2"])
 def test_gpu_rounds_over_pending_delta_run_match_oracle(gpu, oracle_lib, policy, fused, monkeypatch):
     """Both replicas reach their contents through batches that stay in the delta run (inserts,
@@ -611,9 +611,11 @@ def test_gpu_rounds_over_pending_delta_run_match_oracle(gpu, oracle_lib, policy,
     base + run in place (select over both, sums over both) and must equal the literal driver over
     the final contents round by round -- without compacting either store.  fused: tiny rounds in
     one launch (round_tiny.hpp k_round_tiny, the default); unfused: RSOS_HIP_ROUND_FUSED=0, the two
-    searches and k_round_small_view."""
-    monkeypatch.setenv("RSOS_HIP_ROUND_FUSED", "1" if fused == "fused" else "0")
-    monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused == "fused" else "0")
+    searches and k_round_small_view.  *_block: RSOS_HIP_ROW_PREFIX=0, sums from the block prefixes
+    (head and tail rows plus a difference) instead of the row prefixes' one difference."""
+    monkeypatch.setenv("RSOS_HIP_ROUND_FUSED", "1" if fused.startswith("fused") else "0")
+    monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused.startswith("fused") else "0")
+    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "0" if fused.endswith("_block") else "1")
     from rsos_hip import RecordSchema, rbsr as R
     schema = RecordSchema.dated("bytes16", "bytes64")
     keys, ca, cb, only_a, only_b, mod = _dated_sets(11, 20_000, 60, 45, 30)
@@ -669,14 +671,16 @@ def test_gpu_large_rounds_over_pending_delta_run(gpu, policy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fused", ["fused", "unfused"])
+@pytest.mark.parametrize("fused", ["fused", "fused_block", "unfused"])
 def test_tiny_questions_over_pending_delta_run(gpu, oracle_lib, fused, monkeypatch):
     """The small questions a device answers when the host tier is off or stale -- rank, ranks of up
     to 64 keys, select and dumps of up to 64 keys, an aggregate over a key range with every bound
     kind -- in one launch each (round_tiny.hpp k_query_tiny) over a store whose delta run is pending,
     against a freshly loaded store with the same contents and the oracle FTM; with
-    RSOS_HIP_QUERY_FUSED=0 the same questions take the multi-launch paths."""
-    monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused == "fused" else "0")
+    RSOS_HIP_QUERY_FUSED=0 the same questions take the multi-launch paths; fused_block: without the
+    row prefixes (RSOS_HIP_ROW_PREFIX=0)."""
+    monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused.startswith("fused") else "0")
+    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "0" if fused.endswith("_block") else "1")
     from rsos_hip import GpuFingerprintStore, RecordSchema, _abi as A
     from rsos_hip.store import KeyRange
     schema = RecordSchema.dated("bytes16", "bytes64")

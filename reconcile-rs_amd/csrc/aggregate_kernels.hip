@@ -764,41 +764,49 @@ __device__ __forceinline__ uint64_t shfl_up_u64(uint64_t x, int d) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// grid-stride over the 256-entry chunks: a grid of one workgroup per chunk (launch_prefix), or at
+// most PREFIX_WGS workgroups (launch_row_prefix: a row prefix formed beside the store's questions,
+// ensure_base_prefix, leaves the CUs' slots to their one-workgroup kernels)
+constexpr uint32_t PREFIX_WGS = 1024;
 __global__ __launch_bounds__(256) void k_prefix256(const uint8_t *in, uint64_t n, const uint8_t *base,
                                                    uint8_t *out) {
     __shared__ uint64_t wtot[4][8];
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (i < n) load_fp(in, i, f);
-    Acc a;
+    const uint64_t nch = n / 256 + 1;
+    for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+        __syncthreads();  // the previous chunk's wtot reads are done
+        const uint64_t i = ch * 256 + threadIdx.x;
+        const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (i < n) load_fp(in, i, f);
+        Acc a;
 #pragma unroll
-    for (int q = 0; q < 8; q++) a.l[q] = f[q];
+        for (int q = 0; q < 8; q++) a.l[q] = f[q];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
+        for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint64_t y = shfl_up_u64(a.l[q], d);
+                if (lane >= (uint32_t)d) a.l[q] += y;
+            }
+        }
+        if (lane == 63) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) wtot[w][q] = a.l[q];
+        }
+        __syncthreads();
+        uint32_t bf[8];
+        load_fp(base, ch, bf);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            const uint64_t y = shfl_up_u64(a.l[q], d);
-            if (lane >= (uint32_t)d) a.l[q] += y;
+            uint64_t v = a.l[q] - f[q] + bf[q];  // inclusive -> exclusive, + the chunk's base
+            for (uint32_t k = 0; k < w; k++) v += wtot[k][q];
+            a.l[q] = v;
         }
-    }
-    if (lane == 63) {
-#pragma unroll
-        for (int q = 0; q < 8; q++) wtot[w][q] = a.l[q];
-    }
-    __syncthreads();
-    uint32_t bf[8];
-    load_fp(base, blockIdx.x, bf);
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-        uint64_t v = a.l[q] - f[q] + bf[q];  // inclusive -> exclusive, + the chunk's base
-        for (uint32_t k = 0; k < w; k++) v += wtot[k][q];
-        a.l[q] = v;
-    }
-    if (i <= n) {
-        uint32_t o[8];
-        acc_normalise(a, o);
-        store_sum(out, i, o);
+        if (i <= n) {
+            uint32_t o[8];
+            acc_normalise(a, o);
+            store_sum(out, i, o);
+        }
     }
 }
 
@@ -886,13 +894,20 @@ hipError_t launch_seg_copy(const uint8_t *old, const uint8_t *newf, const uint64
 }
 
 hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre,
-                         uint8_t *bpre, uint8_t *out, hipStream_t st) {
+                         uint8_t *bpre, uint8_t *out, hipStream_t st, uint32_t max_wgs) {
     const uint64_t nbk = (n + 255) / 256, ns = (nbk + 255) / 256;
     hipLaunchKernelGGL(k_prefix_top, dim3(1), dim3(256), 0, st, ssums, ns, spre);
     hipLaunchKernelGGL(k_prefix256, dim3((uint32_t)(nbk / 256 + 1)), dim3(256), 0, st, bsums, nbk,
                        (const uint8_t *)spre, bpre);
-    hipLaunchKernelGGL(k_prefix256, dim3((uint32_t)(n / 256 + 1)), dim3(256), 0, st, fps, n, (const uint8_t *)bpre,
+    const uint64_t g = max_wgs ? std::min<uint64_t>(n / 256 + 1, max_wgs) : n / 256 + 1;
+    hipLaunchKernelGGL(k_prefix256, dim3((uint32_t)g), dim3(256), 0, st, fps, n, (const uint8_t *)bpre,
                        out);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bpre, uint8_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_prefix256, dim3((uint32_t)std::min<uint64_t>(n / 256 + 1, PREFIX_WGS)), dim3(256), 0, st, fps, n,
+                       bpre, out);
     return hipGetLastError();
 }
 

@@ -26,9 +26,12 @@ hipError_t launch_reduce(const uint8_t *in, uint64_t n_in, uint8_t *out, hipStre
 hipError_t launch_total(const uint8_t *in, uint64_t n, uint64_t *out, hipStream_t st);
 // Exclusive prefix sums of n fingerprints: out[i] = Σ fps[0..i) for i in [0, n] (n + 1 entries),
 // from the run's block sums (ceil(n/256)) and super-block sums (ceil(n/65536)); scratch: spre
-// (ceil(n/65536) + 1 entries), bpre (ceil(n/256) + 1 entries), 32 B each
+// (ceil(n/65536) + 1 entries), bpre (ceil(n/256) + 1 entries), 32 B each.  max_wgs > 0: the row
+// level on at most that many workgroups (grid-stride), for a scan beside latency-bound work
 hipError_t launch_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre,
-                         uint8_t *bpre, uint8_t *out, hipStream_t st);
+                         uint8_t *bpre, uint8_t *out, hipStream_t st, uint32_t max_wgs = 0);
+// launch_prefix's last level only: out[i] = Σ fps [0, i) for i in [0, n], from bpre
+hipError_t launch_row_prefix(const uint8_t *fps, uint64_t n, const uint8_t *bpre, uint8_t *out, hipStream_t st);
 // launch_prefix's first two levels only: bpre[k] = Σ block sums [0, k), k in [0, ceil(n / 256)]
 hipError_t launch_block_prefix(uint64_t n, const uint8_t *bsums, const uint8_t *ssums, uint8_t *spre, uint8_t *bpre,
                                hipStream_t st);

@@ -50,6 +50,45 @@ bool fail_point(const char *name) {
     return true;
 }
 
+// Foreground and background streams.  A question's kernels are one small workgroup each and
+// latency-bound; the work a store does behind them (the host tier's refresh copies and prefix
+// scans, the base's row prefix) launches grids of up to ~400 K workgroups that would fill every
+// CU's slots and starve them (a 2.3 ms tiny round beside a refresh's 100 M-row prefix scan).  So
+// background kernels run on streams with a CU mask without the last RSOS_HIP_BG_RESERVE (default
+// 32) compute units, which stay free for the questions: with 32 (mask bits 224-255, CUs on every
+// XCD) a no-wait drive beside a refresh took 0.38 ms against 2.5 ms unmasked; 8 (bits 248-255) did
+// not help (profiles/r05_s19_nowait_ab.jsonl).  The store's own stream asks for the device's highest
+// priority (RSOS_HIP_FORE_PRIORITY=0: not), which measured no difference on its own.  Either falls
+// back to a plain stream where the runtime refuses it.  Copies stay on plain streams.
+static hipError_t create_fore_stream(hipStream_t *st) {
+    static const int prio = getenv("RSOS_HIP_FORE_PRIORITY") ? atoi(getenv("RSOS_HIP_FORE_PRIORITY")) : 1;
+    int least = 0, greatest = 0;
+    if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least &&
+        hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest) == hipSuccess)
+        return hipSuccess;
+    (void)hipGetLastError();
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+static hipError_t create_back_stream(hipStream_t *st, int device) {
+    static const int reserve = getenv("RSOS_HIP_BG_RESERVE") ? atoi(getenv("RSOS_HIP_BG_RESERVE")) : 32;
+    int ncu = 0;
+    if (reserve > 0 && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        ncu > 4 * reserve) {
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu - reserve; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+        const hipError_t e = hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+        if (getenv("RSOS_HIP_STREAM_DBG")) {
+            std::vector<uint32_t> got(mask.size(), 0u);
+            if (e == hipSuccess) (void)hipExtStreamGetCUMask(*st, (uint32_t)got.size(), got.data());
+            fprintf(stderr, "{\"back_stream\": {\"cus\": %d, \"reserve\": %d, \"created\": %d, \"mask_last_word\": \"%08x\"}}\n",
+                    ncu, reserve, e == hipSuccess, got.empty() ? 0u : got.back());
+        }
+        if (e == hipSuccess) return hipSuccess;
+    }
+    (void)hipGetLastError();
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
 // rh_debug_batch_timing: HIP events around every large batch's fused lift + search launch
 std::atomic<int> g_time_batch{0};
 std::mutex g_batch_mu;
@@ -1048,7 +1087,10 @@ struct rh_store {
     int rf_set = 1, rf_cb = 0;  // rf_cb: the base buffer the copy reads
     uint64_t stale_questions = 0;  // questions the device answered since the last batch
     uint64_t rf_version = 0, rf_epoch = 0, rf_nb = 0;
-    hipStream_t cstream = nullptr;
+    hipStream_t cstream = nullptr, kstream = nullptr;  // the refresh's copies; its kernels
+    // the workgroups of a refresh's row prefix scan that runs beside the store's questions
+    // (RSOS_HIP_TIER_SYNC=0; 0: one per 256 rows)
+    uint32_t bg_prefix_wgs = getenv("RSOS_HIP_BG_PREFIX_WGS") ? (uint32_t)atoi(getenv("RSOS_HIP_BG_PREFIX_WGS")) : 0;
     hipEvent_t rf_ready = nullptr, rf_ev = nullptr, rf_kdone = nullptr;
     // the batches applied while the copy is in flight, as mode-1 rows against its base (which is
     // the device's base until the next compaction, and no compaction runs while a copy is in
@@ -1106,7 +1148,11 @@ struct rh_store {
         }
         if ((rc = compact())) return rc;
         if (!cstream) {
+            // the copies on a plain stream (the copy engines); the scans and samples, and kernel
+            // copies, on a CU-masked one (create_back_stream): a copy issued on a CU-masked stream
+            // held the next write's uploads behind it (write p50 7 -> 100 ms, 10^8 rows)
             RH_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+            RH_HIP(create_back_stream(&kstream, device));
             RH_HIP(hipEventCreateWithFlags(&rf_ready, hipEventDisableTiming));
             RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
             RH_HIP(hipEventCreateWithFlags(&rf_kdone, hipEventDisableTiming));
@@ -1137,24 +1183,27 @@ struct rh_store {
         // queued behind ~1-2 ms of scans at 10^8 rows); the next compaction, which rewrites the
         // base's block sums they read, waits for them (rf_kdone)
         RH_HIP(hipEventRecord(rf_ready, stream));
-        RH_HIP(hipStreamWaitEvent(cstream, rf_ready, 0));
+        RH_HIP(hipStreamWaitEvent(kstream, rf_ready, 0));
         if (n) {
-            RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, cstream));
-            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 64, tier_dsmp.p, cstream));
-            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 4096, tier_dsmp.p + nsmp, cstream));
+            RH_HIP(rh::launch_prefix(bfps[cb].p, n, bsums.p, ssums.p, tier_spre.p, tier_bpre.p, tier_dpre.p, kstream,
+                                     tier_sync_writes ? 0u : bg_prefix_wgs));
+            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 64, tier_dsmp.p, kstream));
+            RH_HIP(kops->sample_stride(bkeys[cb].p, n, 4096, tier_dsmp.p + nsmp, kstream));
         }
-        RH_HIP(hipEventRecord(rf_kdone, cstream));
+        RH_HIP(hipEventRecord(rf_kdone, kstream));
+        // by kernel stores (on kstream) when the write or load that starts the refresh waits for it
+        // (the default policy); by the copy engines (on cstream) when it runs behind the store's work
+        hipStream_t down = tier_sync_writes ? kstream : cstream;
+        if (down == cstream) RH_HIP(hipStreamWaitEvent(cstream, rf_kdone, 0));
         if (n) {
             const Down d[3] = {{S.keys.data(), S.keys, bkeys[cb].p, n * kl},
                                {S.prefix.data(), S.prefix, tier_dpre.p, (n + 1) * 32},
                                {S.samp.data(), S.samp, tier_dsmp.p, (nsmp + nsmp2) * 8}};
-            // by kernel stores when the write or load that starts the refresh waits for it (the
-            // default policy); by the copy engines when it runs behind the store's own work
-            if ((rc = copy_down(d, 3, cstream, tier_sync_writes))) return rc;
+            if ((rc = copy_down(d, 3, down, tier_sync_writes))) return rc;
         } else {
             memset(S.prefix.data(), 0, 32);
         }
-        RH_HIP(hipEventRecord(rf_ev, cstream));
+        RH_HIP(hipEventRecord(rf_ev, down));
         rf_on = true;
         refresh_wanted = false;
         rf_set = spare;
@@ -1315,6 +1364,8 @@ struct rh_store {
     // place (rh::RoundRun), the run copy adds the contributions' prefix sums and takes them down.
     // trun_ver: the version they hold.
     uint64_t trun_ver = ~0ull;
+    // A/B switch: RSOS_HIP_RUNCOL_FUSED=0 forms a short run's columns in the eight launches too
+    int run_cols_fused = getenv("RSOS_HIP_RUNCOL_FUSED") ? atoi(getenv("RSOS_HIP_RUNCOL_FUSED")) : 1;
     int run_columns() {
         int rc;
         const uint64_t n1 = nd;
@@ -1325,12 +1376,19 @@ struct rh_store {
             (rc = trun_br.ensure(n1 + 16)) || (rc = trun_bs.ensure(nbk * 32 + 32)) || (rc = trun_ss.ensure(nsb * 32 + 32)) ||
             (rc = trun_cntp.ensure(n1 + 16)) || (rc = trun_gs.ensure(ns + 8)))
             return rc;
-        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
-        RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
-        RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
         if ((rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64)) ||
             (rc = trun_pre.ensure((n1 + 1) * 32 + 64)))
             return rc;
+        if (n1 <= rh::RUNCOL_SMALL && run_cols_fused) {  // a short run: every column in one launch
+            const rh::RunCols o{trun_c.p,  trun_cnt.p,  trun_fl.p,   trun_br.p,   trun_pre.p, trun_bs.p,
+                                trun_ss.p, trun_spre.p, trun_bpre.p, trun_cntp.p, trun_gs.p};
+            RH_HIP(rh::launch_run_columns_small(dslot[cd].p, dheap.p, n1, o, stream));
+            trun_ver = version;
+            return RH_OK;
+        }
+        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
+        RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
+        RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
         // block and row prefixes: a range sum over the run is then one difference (pre_range_fp)
         RH_HIP(rh::launch_prefix(trun_c.p, n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, trun_pre.p, stream));
         RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
@@ -1611,6 +1669,7 @@ struct rh_store {
     // block sums the caller then writes into bkeys[cb], bfps[cb] and bsums
     int load_prep(size_t m) {
         int rc;
+        if ((rc = drain_prefix_build())) return rc;  // it reads bfps[cb], rewritten here
         // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
@@ -1653,6 +1712,7 @@ struct rh_store {
         if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
         const int nxt = 1 - cb;
         int rc;
+        if ((rc = drain_prefix_build())) return rc;  // one from two bases ago may read bfps[nxt]
         if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
         // load_commit swaps the spare set in: it gets at least the active set's capacity, so that
         // rows reserved by rh_store_reserve stay reserved across a reload (no reallocation, and
@@ -1795,6 +1855,7 @@ struct rh_store {
     int compact() {  // merge the delta run into the base run
         int rc;
         if (nd == 0) return RH_OK;
+        if ((rc = drain_prefix_build())) return rc;  // one from two bases ago may read bfps[1 - cb]
         // a tier copy in flight reads bkeys[rf_cb]; the merge writes the other base buffer, so one
         // compaction runs beside the copy (whose log then breaks: later batches' records are
         // relative to the new base), and a second one, which would write the buffer being copied,
@@ -2263,43 +2324,88 @@ struct rh_store {
     }
     // The base run's exclusive prefixes, formed once per base (after a load or a compaction) on the
     // first question that sums over it on the device: over its block sums (bpre_b[k] = Σ blocks
-    // [0, k), ~n / 256 entries: any range sum is head and tail rows plus one difference) and, when
-    // the device has the room (32 B a row: 3.2 GB at 10^8 rows), over its rows (pre_b[i] = Σ fps
-    // [0, i): any range sum is one difference, two loads).  RSOS_HIP_ROW_PREFIX=0: block prefix only.
+    // [0, k), ~n / 256 entries, on the store's stream: any range sum is head and tail rows plus one
+    // difference) and, when the device has the room (32 B a row: 3.2 GB at 10^8 rows), over its
+    // rows (pre_b[i] = Σ fps [0, i): any range sum is one difference, two loads).  The row prefix
+    // reads and writes 64 B a row (~1.2 ms at 10^8 rows), so it is formed only once the base has
+    // served max(16, n / 2^20) device questions, beside them on a stream of its own (pstream), and
+    // used from the first question after it has landed (pre_ev); until then the block prefix
+    // serves.  A base that changes every few questions (large batches with compactions between
+    // drives) never forms it.  RSOS_HIP_ROW_PREFIX=0: block prefix only;
+    // 2: the row prefix in order on the store's stream, used from the first question (tests).
     DevBuf<uint8_t> bpre_b, spre_b, pre_b;
-    uint64_t bpre_epoch = ~0ull;
-    bool pre_b_ok = false;
+    uint64_t bpre_epoch = ~0ull, pre_epoch = ~0ull;
+    bool pre_b_ok = false, pre_pending = false;
+    hipStream_t pstream = nullptr;
+    hipEvent_t pre_ev = nullptr, pre_base_ev = nullptr;
     int row_prefix = getenv("RSOS_HIP_ROW_PREFIX") ? atoi(getenv("RSOS_HIP_ROW_PREFIX")) : 1;
+    // before anything rewrites a base buffer or pre_b: the build in flight reads them (host wait;
+    // the build is long done in the common case)
+    int drain_prefix_build() {
+        if (!pre_pending) return RH_OK;
+        RH_HIP(hipEventSynchronize(pre_ev));
+        pre_pending = false;
+        pre_b_ok = pre_epoch == base_epoch;
+        return RH_OK;
+    }
+    uint64_t epoch_questions = 0;  // device questions over the current base so far
     int ensure_base_prefix() {
         int rc;
-        if (bpre_epoch == base_epoch && bpre_b.p) return RH_OK;
-        const uint64_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
-        if ((rc = bpre_b.ensure((nbk + 1) * 32 + 64)) || (rc = spre_b.ensure((ns + 1) * 32 + 64))) return rc;
-        pre_b_ok = false;
-        const size_t need = (nb + 1) * 32 + 64;
-        if (row_prefix && nb && pre_b.cap < need) {  // room for it, with 1 GiB to spare, or go without
-            size_t free_b = 0, total_b = 0;
-            pre_b.release();
-            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > need + (1ull << 30)) {
-                const std::string keep = g_err;  // a refused allocation is not the caller's error
-                if (pre_b.ensure(need) != RH_OK) g_err = keep;
+        if (bpre_epoch != base_epoch || !bpre_b.p) {
+            const uint64_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
+            if (pre_pending) RH_HIP(hipStreamWaitEvent(stream, pre_ev, 0));  // it reads bpre_b
+            if ((rc = bpre_b.ensure((nbk + 1) * 32 + 64)) || (rc = spre_b.ensure((ns + 1) * 32 + 64))) return rc;
+            pre_b_ok = false;
+            if (nb) RH_HIP(rh::launch_block_prefix(nb, bsums.p, ssums.p, spre_b.p, bpre_b.p, stream));
+            else RH_HIP(hipMemsetAsync(bpre_b.p, 0, 32, stream));
+            bpre_epoch = base_epoch;
+            epoch_questions = 0;
+            // pre_b sized like the base buffer, allocated at a base's first question (a large
+            // hipMalloc is tens of ms: not inside a later drive), reallocated only when the base
+            // buffer was (no extra device-draining hipFree)
+            if (row_prefix && nb && pre_b.cap < (nb + 1) * 32 + 64) {
+                const size_t need = (std::max<size_t>(nb, bfps[cb].cap / 32) + 1) * 32 + 64;
+                if ((rc = drain_prefix_build())) return rc;
+                pre_b.release();
+                size_t free_b = 0, total_b = 0;  // room for it, with 1 GiB to spare, or go without
+                if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= need + (1ull << 30)) {
+                    const std::string keep = g_err;  // a refused allocation is not the caller's error
+                    if (pre_b.ensure(need) != RH_OK) g_err = keep;
+                }
+            }
+            if (row_prefix == 1 && pre_b.p && !pstream) {  // its stream too (a queue: milliseconds)
+                RH_HIP(create_back_stream(&pstream, device));
+                RH_HIP(hipEventCreateWithFlags(&pre_ev, hipEventDisableTiming));
+                RH_HIP(hipEventCreateWithFlags(&pre_base_ev, hipEventDisableTiming));
             }
         }
-        if (row_prefix && nb && pre_b.cap >= need) {
-            RH_HIP(rh::launch_prefix(bfps[cb].p, nb, bsums.p, ssums.p, spre_b.p, bpre_b.p, pre_b.p, stream));
+        // the row prefix once the base has served enough questions to pay for it: ~1.2 ms at 10^8
+        // rows against a few us saved a question; a base rewritten every drive never forms it
+        const uint64_t want_q = std::max<uint64_t>(16, nb >> 20);
+        if (!row_prefix || !nb || pre_epoch == base_epoch || (row_prefix != 2 && ++epoch_questions < want_q))
+            return RH_OK;
+        pre_epoch = base_epoch;  // tried once per base
+        if (pre_b.cap < (nb + 1) * 32 + 64 || (row_prefix != 2 && !pstream)) return RH_OK;  // no room for it
+        if (row_prefix == 2) {  // in order on the store's stream, used at once (the tests' switch)
+            RH_HIP(rh::launch_row_prefix(bfps[cb].p, nb, bpre_b.p, pre_b.p, stream));
             pre_b_ok = true;
-        } else if (nb) {
-            RH_HIP(rh::launch_block_prefix(nb, bsums.p, ssums.p, spre_b.p, bpre_b.p, stream));
-        } else {
-            RH_HIP(hipMemsetAsync(bpre_b.p, 0, 32, stream));
+            return RH_OK;
         }
-        bpre_epoch = base_epoch;
+        RH_HIP(hipEventRecord(pre_base_ev, stream));  // the base and its block prefix are in place
+        RH_HIP(hipStreamWaitEvent(pstream, pre_base_ev, 0));
+        RH_HIP(rh::launch_row_prefix(bfps[cb].p, nb, bpre_b.p, pre_b.p, pstream));
+        RH_HIP(hipEventRecord(pre_ev, pstream));
+        pre_pending = true;
         return RH_OK;
     }
     // the base run as the round and query kernels read it (no segments)
-    rh::RoundIn base_in() const {
+    rh::RoundIn base_in() {
         rh::RoundIn b{nullptr, nullptr, nullptr, nullptr, nullptr, bkeys[cb].p, bfps[cb].p, bsums.p, ssums.p, bpre_b.p};
-        b.pre = pre_b_ok ? pre_b.p : nullptr;
+        if (pre_pending && hipEventQuery(pre_ev) == hipSuccess) {  // the row prefix has landed
+            pre_pending = false;
+            pre_b_ok = pre_epoch == base_epoch;
+        }
+        b.pre = pre_b_ok && pre_epoch == base_epoch ? pre_b.p : nullptr;
         return b;
     }
     // the run ranks of m keys (lower bounds among the delta run's keys)
@@ -2650,7 +2756,7 @@ struct rh_store {
             t.dsmp = view ? dsmp[cd].p : nullptr, t.dsmp2 = view ? dsmp2[cd].p : nullptr;
             t.g = g, t.gplace = place, t.r = r, t.n = n, t.sqrt_policy = sq, t.b = b, t.cap = cap, t.out = out_p;
             t.seq = ++round_seq;
-            if (round_dbg) {
+            if (round_dbg == 1) {  // 2: the host's times only (no copy of the clocks after each round)
                 if ((rc = dbg_clk.ensure(8))) return rc;
                 t.dbg = dbg_clk.p;
             }
@@ -2663,9 +2769,11 @@ struct rh_store {
             rc = round_finish(h, cap, r, view, din, run, g, place, false, ch, en, oc);
             if (round_dbg) {  // phase times of this round (10 ns ticks), summed until the store is destroyed
                 const double h4 = now_us();
-                uint64_t c[8];
-                RH_HIP(hipMemcpy(c, dbg_clk.p, sizeof c, hipMemcpyDeviceToHost));
-                for (int k = 0; k < 6; k++) dbg_sum[k] += (double)(c[k + 1] - c[k]) * 0.01;
+                if (round_dbg == 1) {
+                    uint64_t c[8];
+                    RH_HIP(hipMemcpy(c, dbg_clk.p, sizeof c, hipMemcpyDeviceToHost));
+                    for (int k = 0; k < 6; k++) dbg_sum[k] += (double)(c[k + 1] - c[k]) * 0.01;
+                }
                 dbg_host[0] += h1 - h0, dbg_host[1] += h2 - h1, dbg_host[2] += h3 - h2, dbg_host[3] += h4 - h3;
                 dbg_prep[0] += hv - h0, dbg_prep[1] += hs - hv, dbg_prep[2] += h1 - hs;
                 if (h0 - dbg_last < 100) dbg_host[4] += h0 - dbg_last, dbg_host_n++;  // the caller's own time
@@ -2770,7 +2878,8 @@ struct rh_store {
     // A/B switch: RSOS_HIP_ROUND_FUSED=0 keeps tiny rounds on the two searches + k_round_small(_view)
     int round_fused = getenv("RSOS_HIP_ROUND_FUSED") ? atoi(getenv("RSOS_HIP_ROUND_FUSED")) : 1;
     uint64_t round_seq = 0;
-    // RSOS_HIP_ROUND_DBG=1: k_round_tiny's phase clocks, averaged to stderr when the store is destroyed
+    // RSOS_HIP_ROUND_DBG=1: k_round_tiny's phase clocks and the host's times per round, averaged to
+    // stderr when the store is destroyed; 2: the host's times only (no clock copy per round)
     int round_dbg = getenv("RSOS_HIP_ROUND_DBG") ? atoi(getenv("RSOS_HIP_ROUND_DBG")) : 0;
     DevBuf<uint64_t> dbg_clk;
     double dbg_sum[6] = {0, 0, 0, 0, 0, 0};
@@ -2782,7 +2891,7 @@ struct rh_store {
         return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
     }
     void release() {
-        if (round_dbg && dbg_rounds)
+        if (round_dbg == 1 && dbg_rounds)
             fprintf(stderr,
                     "{\"k_round_tiny_phases_us\": {\"rounds\": %llu, \"input\": %.2f, \"searches\": %.2f, "
                     "\"bounds\": %.2f, \"decide\": %.2f, \"emit\": %.2f, \"fence\": %.2f}}\n",
@@ -2797,6 +2906,7 @@ struct rh_store {
                     dbg_prep[2] / dbg_rounds);
         (void)hipStreamSynchronize(stream);
         if (cstream) (void)hipStreamSynchronize(cstream);
+        if (kstream) (void)hipStreamSynchronize(kstream);
         for (int k = 0; k < 2; k++) {
             bkeys[k].release(); bfps[k].release(); dkeys[k].release(); dslot[k].release();
         }
@@ -2815,12 +2925,21 @@ struct rh_store {
         r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); pr_out.release();
         tsets[0].release(); tsets[1].release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release(); tier_dsmp.release();
         if (cstream) (void)hipStreamDestroy(cstream);
+        if (kstream) (void)hipStreamDestroy(kstream);
         if (rf_ready) (void)hipEventDestroy(rf_ready);
         if (rf_ev) (void)hipEventDestroy(rf_ev);
         if (rf_kdone) (void)hipEventDestroy(rf_kdone);
-        cstream = nullptr, rf_ready = rf_ev = rf_kdone = nullptr, rf_on = false;
+        cstream = kstream = nullptr, rf_ready = rf_ev = rf_kdone = nullptr, rf_on = false;
         snap.release();
-        bpre_b.release(); spre_b.release(); pre_b.release(); pre_b_ok = false; dbg_clk.release();
+        if (pstream) {
+            (void)hipStreamSynchronize(pstream);
+            (void)hipStreamDestroy(pstream);
+            (void)hipEventDestroy(pre_ev);
+            (void)hipEventDestroy(pre_base_ev);
+            pstream = nullptr, pre_ev = pre_base_ev = nullptr;
+        }
+        pre_pending = pre_b_ok = false;
+        bpre_b.release(); spre_b.release(); pre_b.release(); dbg_clk.release();
         sbsums.release(); sssums.release(); sbsmp.release(); sbsmp2.release(); sbtab.release(); sbtabp.release();
         stot.release(); snap_words.release(); snap_hdr.release();
         scratch.release();
@@ -2888,7 +3007,7 @@ int rh_store_create(int device, const rh_schema *schema, rh_store **out) {
     s->schema = *schema;
     s->kops = kops;
     s->kl = key_row(*schema);
-    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    hipError_t e = create_fore_stream(&s->stream);
     if (e != hipSuccess) {
         delete s;
         return fail(RH_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));

@@ -1797,6 +1797,121 @@ hipError_t launch_tier_gsamp(const uint32_t *brank, const uint32_t *cntp, const 
     return hipGetLastError();
 }
 
+// The delta run's columns for a short run in one launch of one workgroup (1,024 lanes, four
+// consecutive entries each): the entries as k_tier_run reads them; one workgroup scan gives the
+// contributions' row prefix and the count deltas' prefix; then the block sums and block /
+// super-block prefixes are differences and entries of the row prefix, and G(64 k) as
+// k_tier_gsamp.  A run of one batch's few rows (a 1-row write before a question) paid ~70 us of
+// host launches and in-stream gaps for the eight kernels this replaces.
+constexpr uint32_t RUNCOL_THREADS = 1024, RUNCOL_PER = 4;
+static_assert(RUNCOL_SMALL < (uint64_t)RUNCOL_THREADS * RUNCOL_PER, "k_run_columns_small: n + 1 entries");
+__global__ __launch_bounds__(RUNCOL_THREADS) void k_run_columns_small(const uint32_t *slot, const uint8_t *heap,
+                                                                       uint64_t n, RunCols o) {
+    __shared__ uint64_t wacc[RUNCOL_THREADS / 64][8];
+    __shared__ int32_t wcnt[RUNCOL_THREADS / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int32_t c[RUNCOL_PER];
+    Acc s;
+    acc_zero(s);
+    int32_t cs = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < RUNCOL_PER; q++) {
+        const uint64_t i = (uint64_t)t * RUNCOL_PER + q;
+        c[q] = 0;
+        if (i < n) {
+            const DeltaRec *r = reinterpret_cast<const DeltaRec *>(heap) + slot[i];
+            const uint4 *cp = reinterpret_cast<const uint4 *>(r->contrib);
+            const uint4 a = cp[0], b = cp[1];
+            const uint32_t f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            reinterpret_cast<uint4 *>(o.contrib + 32 * i)[0] = a;
+            reinterpret_cast<uint4 *>(o.contrib + 32 * i)[1] = b;
+            const uint32_t fl = r->flags;
+            c[q] = ((fl & DeltaRec::LIVE) ? 1 : 0) - ((fl & DeltaRec::IN_BASE) ? 1 : 0);
+            o.cnt[i] = (uint32_t)c[q];
+            o.flags[i] = (uint8_t)fl;
+            o.brank[i] = r->brank;
+            acc_add_fp(s, f);
+            cs += c[q];
+        } else if (i == n) {
+            o.cnt[n] = 0;
+        }
+    }
+    // inclusive scans of the lanes' sums in the wave, then across the waves
+    Acc inc = s;
+    int32_t ic = cs;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint64_t y = __shfl_up((unsigned long long)inc.l[k], d);
+            if (lane >= (uint32_t)d) inc.l[k] += y;
+        }
+        const int32_t y = __shfl_up(ic, d);
+        if (lane >= (uint32_t)d) ic += y;
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) wacc[w][k] = inc.l[k];
+        wcnt[w] = ic;
+    }
+    __syncthreads();
+    Acc e;
+    int32_t ec = ic - cs;
+#pragma unroll
+    for (int k = 0; k < 8; k++) e.l[k] = inc.l[k] - s.l[k];
+    for (uint32_t v = 0; v < w; v++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) e.l[k] += wacc[v][k];
+        ec += wcnt[v];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < RUNCOL_PER; q++) {
+        const uint64_t i = (uint64_t)t * RUNCOL_PER + q;
+        if (i <= n) {
+            uint32_t g[8];
+            acc_normalise(e, g);
+            store_sum(o.pre, i, g);
+            o.cntp[i] = (uint32_t)ec;
+        }
+        if (i < n) {  // this lane's own contribution, written above (read back: no registers held over the scan)
+            uint32_t f[8];
+            load_fp(o.contrib, i, f);
+            acc_add_fp(e, f), ec += c[q];
+        }
+    }
+    __syncthreads();  // the row prefix is written (the workgroup's own global stores)
+    const uint64_t nbk = (n + 255) / 256;
+    for (uint64_t k = t; k <= nbk; k += RUNCOL_THREADS) {
+        const uint64_t lo = k * 256 < n ? k * 256 : n, hi = (k + 1) * 256 < n ? (k + 1) * 256 : n;
+        uint32_t a[8], b[8];
+        load_fp(o.pre, lo, b);
+        store_sum(o.bpre, k, b);  // bpre[nbk] = pre[n], the total
+        if (k < nbk) {
+            load_fp(o.pre, hi, a);
+            sub256(a, b);
+            store_sum(o.bsums, k, a);
+        }
+    }
+    if (t == 0) {  // one super-block (n < 65536): its sum and prefix
+        uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot[8];
+        load_fp(o.pre, n, tot);
+        if (n) store_sum(o.ssums, 0, tot);
+        store_sum(o.spre, 0, z);
+        store_sum(o.spre, 1, tot);
+    }
+    for (uint64_t k = t; k * 64 < n; k += RUNCOL_THREADS) {
+        const uint64_t j = k * 64;
+        o.gsamp[k] = (uint64_t)((int64_t)o.brank[j] + (int32_t)o.cntp[j] + ((o.flags[j] & DeltaRec::LIVE) ? 1 : 0));
+    }
+}
+
+hipError_t launch_run_columns_small(const uint32_t *slot, const uint8_t *heap, uint64_t n, const RunCols &o,
+                                    hipStream_t st) {
+    if (n == 0 || n > RUNCOL_SMALL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_run_columns_small, dim3(1), dim3(RUNCOL_THREADS), 0, st, slot, heap, n, o);
+    return hipGetLastError();
+}
+
 hipError_t launch_compact_rows(const uint8_t *src, uint32_t row_bytes, const uint32_t *keep, const uint32_t *dst,
                                uint64_t m, uint8_t *out, hipStream_t st) {
     if (m == 0 || row_bytes == 0 || !src) return hipSuccess;

@@ -288,6 +288,21 @@ hipError_t launch_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n
 // and select's index over it: entry 64 k's live keys at or below it (k_tier_gsamp)
 hipError_t launch_tier_gsamp(const uint32_t *brank, const uint32_t *cntp, const uint8_t *flags, uint64_t n,
                              uint64_t *gsamp, hipStream_t st);
+// All the run's columns at once for a short run (n <= RUNCOL_SMALL), one launch of one workgroup
+// (k_run_columns_small): what launch_tier_run, two launch_reduce, launch_prefix, the count scan and
+// launch_tier_gsamp form in eight launches
+struct RunCols {
+    uint8_t *contrib;
+    uint32_t *cnt;
+    uint8_t *flags;
+    uint32_t *brank;
+    uint8_t *pre, *bsums, *ssums, *spre, *bpre;  // row prefix (n + 1), block / super-block sums and prefixes
+    uint32_t *cntp;                              // the count deltas' exclusive prefix (n + 1)
+    uint64_t *gsamp;
+};
+constexpr uint64_t RUNCOL_SMALL = 4095;
+hipError_t launch_run_columns_small(const uint32_t *slot, const uint8_t *heap, uint64_t n, const RunCols &o,
+                                    hipStream_t st);
 // pre-size the scratch slots a compaction of up to `plan` delta rows and a batch of `batch` rows use
 hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch);
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);

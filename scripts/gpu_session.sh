@@ -20,10 +20,14 @@
 #                     host tier on / off
 #   trace_latency_off the same, tier off, under a kernel trace (kernel summary + timeline)
 #   latency_phases    the same, tier off, with k_round_tiny's phase clocks (RSOS_HIP_ROUND_DBG=1)
+#   latency_host      the same with the host's times per round only (RSOS_HIP_ROUND_DBG=2)
 #   launch            examples/launch_latency: one waited-for small launch, 16 B and ~2.4 KB arguments
 #   interleave_sync interleave_nowait interleave_off
 #                     1 M-row batches into both replicas at 10^8 between d = 1 drives (tier_interleave)
 #   trace_interleave  the default-policy interleave under a kernel + memory-copy trace
+#   trace_interleave_nowait  the same with RSOS_HIP_TIER_SYNC=0
+#   interleave_nowait_ab     interleave_nowait with the foreground stream priority / background CU
+#                     mask each on and off (RSOS_HIP_FORE_PRIORITY, RSOS_HIP_BG_RESERVE)
 #   sstore            the sharded store's client (examples/sstore_client) on device 0
 #   rccl1             every workload under torch.distributed.run with one rank (the nccl = RCCL
 #                     process group, its gathers and barriers)
@@ -93,6 +97,7 @@ for step in "$@"; do
     latency_off) run latency_off 300 $EX/rbsr_latency "$N" 1 40 0 1 ;;
     latency_phases) run latency_phases 300 env RSOS_HIP_ROUND_DBG=1 $EX/rbsr_latency "$N" 1 40 0 1 ;;
     launch) run launch 120 $EX/launch_latency 2000 ;;
+    latency_host) run latency_host 300 env RSOS_HIP_ROUND_DBG=2 $EX/rbsr_latency "$N" 1 40 0 1 ;;
     trace_latency_off)
         run trace_latency_off 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trlat" -o tr -- $EX/rbsr_latency "$N" 1 10 0 1
         python3 scripts/write_timeline.py "$O/trlat" k_round > "$O/${TAG}_latency_off_timeline.txt" 2>&1 || true
@@ -101,7 +106,20 @@ for step in "$@"; do
         ;;
     interleave_sync) run interleave_sync 400 $EX/tier_interleave 100000000 1000000 20 1 c5 2 ;;
     interleave_nowait) run interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 $EX/tier_interleave 100000000 1000000 12 1 c5 2 3 ;;
+    interleave_nowait_ab)  # the foreground priority and background CU mask, each on and off
+        run nowait_p0r0 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_FORE_PRIORITY=0 RSOS_HIP_BG_RESERVE=0 RSOS_HIP_STREAM_DBG=1 $EX/tier_interleave 100000000 1000000 8 1 c5 2 &&
+        run nowait_p1r0 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_FORE_PRIORITY=1 RSOS_HIP_BG_RESERVE=0 RSOS_HIP_STREAM_DBG=1 $EX/tier_interleave 100000000 1000000 8 1 c5 2 &&
+        run nowait_p0r8 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_FORE_PRIORITY=0 RSOS_HIP_BG_RESERVE=8 RSOS_HIP_STREAM_DBG=1 $EX/tier_interleave 100000000 1000000 8 1 c5 2 &&
+        run nowait_p0r32 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_FORE_PRIORITY=0 RSOS_HIP_BG_RESERVE=32 RSOS_HIP_STREAM_DBG=1 $EX/tier_interleave 100000000 1000000 8 1 c5 2 ;;
+    interleave_nowait_wgs)  # the refresh's background prefix scan on all / 1024 / 256 workgroups
+        run nowait_w0 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_BG_PREFIX_WGS=0 $EX/tier_interleave 100000000 1000000 12 1 c5 2 &&
+        run nowait_w1024 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_BG_PREFIX_WGS=1024 $EX/tier_interleave 100000000 1000000 12 1 c5 2 &&
+        run nowait_w256 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_BG_PREFIX_WGS=256 $EX/tier_interleave 100000000 1000000 12 1 c5 2 ;;
     interleave_off) run interleave_off 400 $EX/tier_interleave 100000000 1000000 12 0 c5 2 3 ;;
+    trace_interleave_nowait)
+        run trace_interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trinw" -o tr -- $EX/tier_interleave 100000000 1000000 6 1 c5 1
+        python3 scripts/copy_summary.py "$O/trinw" > "$O/${TAG}_interleave_nowait_trace_summary.txt" 2>&1 || true
+        python3 scripts/write_timeline.py "$O/trinw" k_cs_minmax > "$O/${TAG}_interleave_nowait_timeline.txt" 2>&1 || true ;;
     trace_interleave)
         run trace_interleave 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trint" -o tr -- $EX/tier_interleave 100000000 1000000 6 1 c5 1
         python3 scripts/copy_summary.py "$O/trint" > "$O/${TAG}_interleave_trace_summary.txt" 2>&1 || true

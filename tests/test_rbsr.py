@@ -611,11 +611,14 @@ def test_gpu_rounds_over_pending_delta_run_match_oracle(gpu, oracle_lib, policy,
     base + run in place (select over both, sums over both) and must equal the literal driver over
     the final contents round by round -- without compacting either store.  fused: tiny rounds in
     one launch (round_tiny.hpp k_round_tiny, the default); unfused: RSOS_HIP_ROUND_FUSED=0, the two
-    searches and k_round_small_view.  *_block: RSOS_HIP_ROW_PREFIX=0, sums from the block prefixes
-    (head and tail rows plus a difference) instead of the row prefixes' one difference."""
+    searches and k_round_small_view, with the run's columns from the eight launches
+    (RSOS_HIP_RUNCOL_FUSED=0) rather than k_run_columns_small.  *_block: RSOS_HIP_ROW_PREFIX=0, sums
+    from the block prefixes (head and tail rows plus a difference) instead of the row prefixes' one
+    difference (formed in order, RSOS_HIP_ROW_PREFIX=2, so that every question reads them)."""
     monkeypatch.setenv("RSOS_HIP_ROUND_FUSED", "1" if fused.startswith("fused") else "0")
     monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused.startswith("fused") else "0")
-    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "0" if fused.endswith("_block") else "1")
+    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "0" if fused.endswith("_block") else "2")
+    monkeypatch.setenv("RSOS_HIP_RUNCOL_FUSED", "1" if fused.startswith("fused") else "0")
     from rsos_hip import RecordSchema, rbsr as R
     schema = RecordSchema.dated("bytes16", "bytes64")
     keys, ca, cb, only_a, only_b, mod = _dated_sets(11, 20_000, 60, 45, 30)
@@ -680,7 +683,8 @@ def test_tiny_questions_over_pending_delta_run(gpu, oracle_lib, fused, monkeypat
     RSOS_HIP_QUERY_FUSED=0 the same questions take the multi-launch paths; fused_block: without the
     row prefixes (RSOS_HIP_ROW_PREFIX=0)."""
     monkeypatch.setenv("RSOS_HIP_QUERY_FUSED", "1" if fused.startswith("fused") else "0")
-    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "0" if fused.endswith("_block") else "1")
+    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "0" if fused.endswith("_block") else "2")
+    monkeypatch.setenv("RSOS_HIP_RUNCOL_FUSED", "1" if fused.startswith("fused") else "0")
     from rsos_hip import GpuFingerprintStore, RecordSchema, _abi as A
     from rsos_hip.store import KeyRange
     schema = RecordSchema.dated("bytes16", "bytes64")

@@ -1089,8 +1089,9 @@ struct rh_store {
     uint64_t rf_version = 0, rf_epoch = 0, rf_nb = 0;
     hipStream_t cstream = nullptr, kstream = nullptr;  // the refresh's copies; its kernels
     // the workgroups of a refresh's row prefix scan that runs beside the store's questions
-    // (RSOS_HIP_TIER_SYNC=0; 0: one per 256 rows)
-    uint32_t bg_prefix_wgs = getenv("RSOS_HIP_BG_PREFIX_WGS") ? (uint32_t)atoi(getenv("RSOS_HIP_BG_PREFIX_WGS")) : 0;
+    // (RSOS_HIP_TIER_SYNC=0; 0: one per 256 rows).  At 10^8 rows, 1,024: no-wait drive p50 0.94 ms,
+    // write p50 8.1 ms; all: 1.03 / 7.4; 256: 0.78 / 12.3 (profiles/r05_s22_nowait_wgs.jsonl)
+    uint32_t bg_prefix_wgs = getenv("RSOS_HIP_BG_PREFIX_WGS") ? (uint32_t)atoi(getenv("RSOS_HIP_BG_PREFIX_WGS")) : 1024;
     hipEvent_t rf_ready = nullptr, rf_ev = nullptr, rf_kdone = nullptr;
     // the batches applied while the copy is in flight, as mode-1 rows against its base (which is
     // the device's base until the next compaction, and no compaction runs while a copy is in
@@ -1676,6 +1677,7 @@ struct rh_store {
         health_reset();
         version++;
         base_epoch++;
+        base_loaded = true;
         if ((rc = bkeys[cb].ensure(m * kl + 64)) || (rc = bfps[cb].ensure(m * 32 + 64)) || (rc = flag.ensure(4)) ||
             (rc = counts.ensure(4)))
             return rc;
@@ -1758,6 +1760,7 @@ struct rh_store {
         swap_buf(btabp, sbtabp);
         version++;
         base_epoch++;
+        base_loaded = true;
         nd = 0;
         heap_len = 0;
         dtotal = 0;
@@ -1894,6 +1897,7 @@ struct rh_store {
         RH_HIP(hipMemcpyAsync(c, mcnt.p, 24, hipMemcpyDeviceToHost, stream));
         const uint64_t want = size(), nb_old = nb;
         base_epoch++;  // same contents, a new base: the tier's copy stays valid, not the device's deltas
+        base_loaded = false;
         cb = nxt;
         nb = want;
         nd = 0;
@@ -2327,8 +2331,9 @@ struct rh_store {
     // [0, k), ~n / 256 entries, on the store's stream: any range sum is head and tail rows plus one
     // difference) and, when the device has the room (32 B a row: 3.2 GB at 10^8 rows), over its
     // rows (pre_b[i] = Σ fps [0, i): any range sum is one difference, two loads).  The row prefix
-    // reads and writes 64 B a row (~1.2 ms at 10^8 rows), so it is formed only once the base has
-    // served max(16, n / 2^20) device questions, beside them on a stream of its own (pstream), and
+    // reads and writes 64 B a row (~1.2 ms at 10^8 rows), so it is formed at a loaded base's first
+    // question, or once a compacted base has served max(16, n / 2^20) device questions, beside them
+    // on a stream of its own (pstream), and
     // used from the first question after it has landed (pre_ev); until then the block prefix
     // serves.  A base that changes every few questions (large batches with compactions between
     // drives) never forms it.  RSOS_HIP_ROW_PREFIX=0: block prefix only;
@@ -2349,6 +2354,7 @@ struct rh_store {
         return RH_OK;
     }
     uint64_t epoch_questions = 0;  // device questions over the current base so far
+    bool base_loaded = true;       // the current base came from a load (false: a compaction)
     int ensure_base_prefix() {
         int rc;
         if (bpre_epoch != base_epoch || !bpre_b.p) {
@@ -2381,8 +2387,9 @@ struct rh_store {
         }
         // the row prefix once the base has served enough questions to pay for it: ~1.2 ms at 10^8
         // rows against a few us saved a question; a base rewritten every drive never forms it
-        const uint64_t want_q = std::max<uint64_t>(16, nb >> 20);
-        if (!row_prefix || !nb || pre_epoch == base_epoch || (row_prefix != 2 && ++epoch_questions < want_q))
+        // (a loaded base is formed at its first question: loads are rare, compactions are not)
+        const uint64_t want_q = base_loaded ? 0 : std::max<uint64_t>(16, nb >> 20);
+        if (!row_prefix || !nb || pre_epoch == base_epoch || (row_prefix != 2 && ++epoch_questions <= want_q))
             return RH_OK;
         pre_epoch = base_epoch;  // tried once per base
         if (pre_b.cap < (nb + 1) * 32 + 64 || (row_prefix != 2 && !pstream)) return RH_OK;  // no room for it

@@ -181,7 +181,14 @@ void rh_fp_sub(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
  * Realises Rsos<K> (rsos/src/rsos_trait.rs:39-90) for u32 / u64 / 8-, 16-, 32-byte keys:
  *   size -> rh_store_len, aggregate -> rh_store_aggregate[s|_keys], rank -> rh_store_rank[s],
  *   select -> rh_store_select, insert / delete -> rh_store_apply[_device].
- * Every call drains the store's stream before returning.                                   */
+ * Every call drains the store's stream before returning.
+ * Device memory: keys + 32 B fingerprint per base row, block sums, search samples and tables,
+ * the delta run (a 40 B record per changed key), and -- for questions over the device -- a row
+ * prefix of the base, 32 B per row (3.2 GB at 10^8 rows), allocated at a base's first device
+ * question only while 1 GiB stays free (RSOS_HIP_ROW_PREFIX=0: none; sums then take a block prefix
+ * and the head / tail rows).  Streams: the store's own at the device's highest priority;
+ * background kernels (the host tier's refresh scans, the row prefix) on streams whose CU mask
+ * leaves the last RSOS_HIP_BG_RESERVE (default 32) compute units to the questions' kernels.     */
 typedef struct rh_store rh_store;
 
 int rh_store_create(int device, const rh_schema *schema, rh_store **out);

@@ -729,3 +729,67 @@ def test_tiny_questions_over_pending_delta_run(gpu, oracle_lib, fused, monkeypat
     assert s["delta_rows"] > 0 and s["compactions"] == 0
     for g in (va, fa):
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("run_rows", [1, 255, 256, 4094, 4095, 4096, 9000])
+def test_run_columns_at_the_one_launch_limit(gpu, oracle_lib, run_rows, monkeypatch):
+    """A delta run of run_rows entries on a base whose size is no multiple of 256: its columns
+    from k_run_columns_small (up to RUNCOL_SMALL = 4,095 entries; the eight-launch path above it)
+    against the eight launches (RSOS_HIP_RUNCOL_FUSED=0), each with the row prefixes formed in
+    order and without them, and against a store loaded with the final contents: ranks, selects,
+    key-range aggregates and a whole reconciliation round by round."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    from rsos_hip.store import KeyRange
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    rng = np.random.default_rng(run_rows)
+    n = 20_011
+    keys = np.unique(rng.integers(0, 256, (n + run_rows + 64, 16), dtype=np.uint8), axis=0)[:n + run_rows]
+    rng.shuffle(keys)
+    tot = len(keys)
+    cols = {"keys": keys, "values": rng.integers(0, 256, (tot, 64), dtype=np.uint8),
+            "phys": (1_700_000_000_000 + np.arange(tot)).astype(np.uint64), "logical": np.zeros(tot, np.uint32),
+            "node": np.ones(tot, np.uint64), "tags": np.zeros(tot, np.uint8)}
+
+    def part(idx):
+        idx = np.array(sorted(idx, key=lambda i: keys[i].tobytes()))
+        return {k: v[idx].copy() for k, v in cols.items()}
+    base, batch, final = part(range(n)), part(range(n, tot)), part(range(tot))
+    stores = {}
+    for fusedc in ("1", "0"):
+        for rowp in ("2", "0"):
+            monkeypatch.setenv("RSOS_HIP_RUNCOL_FUSED", fusedc)
+            monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", rowp)
+            st = GpuFingerprintStore(schema)
+            st.load_bulk(base)
+            st.apply(batch, np.zeros(len(batch["keys"]), np.uint8))
+            assert st.stats()["delta_rows"] == run_rows
+            stores[(fusedc, rowp)] = st
+    ref = GpuFingerprintStore(schema)
+    ref.load_bulk(final)
+    probes = [bytes(k) for k in final["keys"][rng.integers(0, tot, 80)]] + \
+        [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(40)]
+    kinds = ["unbounded", "included", "excluded"]
+    for st in stores.values():
+        assert st.size() == ref.size() == tot
+        assert st.aggregate() == ref.aggregate()
+        for z in probes[:40]:
+            assert st.rank(z) == ref.rank(z)
+        for r in [0, tot - 1] + [int(x) for x in rng.integers(0, tot, 30)]:
+            assert st.select(r) == ref.select(r)
+        for i in range(60):
+            a, b = sorted((probes[int(rng.integers(len(probes)))], probes[int(rng.integers(len(probes)))]))
+            rg = KeyRange(a, b, kinds[i % 3] if i % 3 else "included", kinds[(i // 3) % 3] if (i // 3) % 3 else "excluded")
+            assert st.aggregate(rg) == ref.aggregate(rg), i
+    peer = GpuFingerprintStore(schema)
+    peer.load_bulk(part([i for i in range(tot) if i % 97]))
+    want = reconcile(ref, peer, lambda v, act, ch, en: _outcome(R.protocol_round_with_policy(v, R.FixedFanOut(16), act, ch, en)),
+                     R.initial_ranges)
+    for st in stores.values():
+        got = reconcile(st, peer, lambda v, act, ch, en: _outcome(R.protocol_round_with_policy(v, R.FixedFanOut(16), act, ch, en)),
+                        R.initial_ranges)
+        assert got[0] == want[0]
+        assert st.stats()["compactions"] == 0
+        st.close()
+    ref.close()
+    peer.close()

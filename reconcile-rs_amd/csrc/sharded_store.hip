@@ -95,10 +95,15 @@ class ShardPool {
         bool quit = false;
     };
     std::vector<Slot> slots_;
+    // spin this long before sleeping (RSOS_HIP_SSTORE_SPIN_US, default 50)
+    static int64_t spin_us() {
+        static const int64_t us = getenv("RSOS_HIP_SSTORE_SPIN_US") ? atoll(getenv("RSOS_HIP_SSTORE_SPIN_US")) : 50;
+        return us;
+    }
     static void wait_for(Slot &w, int want) {
         const auto t0 = std::chrono::steady_clock::now();
         while (w.state.load(std::memory_order_acquire) != want) {
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us())) {
                 std::unique_lock<std::mutex> g(w.mu);
                 w.cv.wait(g, [&] { return w.state.load(std::memory_order_acquire) == want; });
                 return;

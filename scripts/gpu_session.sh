@@ -21,6 +21,7 @@
 #   trace_latency_off the same, tier off, under a kernel trace (kernel summary + timeline)
 #   latency_phases    the same, tier off, with k_round_tiny's phase clocks (RSOS_HIP_ROUND_DBG=1)
 #   latency_host      the same with the host's times per round only (RSOS_HIP_ROUND_DBG=2)
+#   sstore_ab         sstore_client with RSOS_HIP_SSTORE_SPIN_US 50 / 300 / 2000, d 1 / 100, tier on / off
 #   launch            examples/launch_latency: one waited-for small launch, 16 B and ~2.4 KB arguments
 #   interleave_sync interleave_nowait interleave_off
 #                     1 M-row batches into both replicas at 10^8 between d = 1 drives (tier_interleave)
@@ -126,6 +127,14 @@ for step in "$@"; do
         rm -rf "$O/trint"
         ;;
     sstore) run sstore 300 $EX/sstore_client 4 2000000 ;;
+    sstore_ab)  # the shard threads' spin before sleeping, d = 1 and 100, tier on and off
+        for sp in 50 300 2000; do
+            for d in 1 100; do
+                for t in 1 0; do
+                    run sstore_s${sp}_d${d}_t${t} 120 env RSOS_HIP_SSTORE_SPIN_US=$sp $EX/sstore_client 4 2000000 $d $t 10 || exit 1
+                done
+            done
+        done ;;
     rccl1)
         for cfg in config4 config2 config5 snapshot rbsr; do
             extra=""

@@ -456,6 +456,69 @@ __global__ __launch_bounds__(256) void k_round_plan(RoundSegs g, const uint64_t 
     if (threadIdx.x < 5 && cnt[threadIdx.x]) atomicAdd((unsigned long long *)&hdr[threadIdx.x], cnt[threadIdx.x]);
 }
 
+// ---- the large round's plan in three launches (a memset, k_round_plan and two library scans
+// were six): decisions and per-256-segment counts; one workgroup scans the parts and writes the
+// header; each segment's child / enumeration offsets ---------------------------------------------
+__global__ __launch_bounds__(256) void k_round_plan_part(RoundSegs g, const uint64_t *remote, uint64_t r, uint64_t n,
+                                                         int sqrt_policy, uint64_t b, uint64_t *part) {
+    __shared__ unsigned long long cnt[5];  // skipped, enumerated (= enumerations), split, children, dropped
+    if (threadIdx.x < 5) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < r) {
+        const RoundSeg d = round_decide(g.lo[j], g.hi[j], g.loc + 5 * j, remote + 5 * j, n, sqrt_policy, b);
+        g.kind[j] = (uint8_t)d.kind;
+        g.stride[j] = d.stride;
+        g.si[j] = d.si;
+        g.ei[j] = d.ei;
+        g.nch[j] = d.children;
+        g.nen[j] = d.enums;
+        atomicAdd(&cnt[d.kind == 3 ? 4 : d.kind], 1ull);
+        if (d.children) atomicAdd(&cnt[3], (unsigned long long)d.children);
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) part[5 * (uint64_t)blockIdx.x + threadIdx.x] = cnt[threadIdx.x];
+}
+__global__ __launch_bounds__(1024) void k_round_plan_scan_parts(uint64_t *part, uint64_t np, uint64_t *hdr) {
+    __shared__ uint64_t wsum[2][16], tot[2], carry[2];
+    __shared__ unsigned long long other[3];  // skipped, split, dropped
+    const uint32_t t = threadIdx.x;
+    if (t < 2) carry[t] = 0;
+    if (t < 3) other[t] = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < np; base += blockDim.x) {  // uniform
+        const uint64_t i = base + t;
+        const bool in = i < np;
+        const uint64_t c = in ? part[5 * i + 3] : 0, e = in ? part[5 * i + 1] : 0;
+        if (in) {
+            atomicAdd(&other[0], (unsigned long long)part[5 * i]);
+            atomicAdd(&other[1], (unsigned long long)part[5 * i + 2]);
+            atomicAdd(&other[2], (unsigned long long)part[5 * i + 4]);
+        }
+        const uint64_t co = block_exclusive_scan(c, wsum[0], &tot[0]);
+        const uint64_t eo = block_exclusive_scan(e, wsum[1], &tot[1]);
+        if (in) part[5 * i + 3] = carry[0] + co, part[5 * i + 1] = carry[1] + eo;  // the part's offsets
+        __syncthreads();
+        if (t == 0) carry[0] += tot[0], carry[1] += tot[1];
+        __syncthreads();
+    }
+    if (t == 0) {
+        hdr[0] = other[0], hdr[1] = carry[1], hdr[2] = other[1], hdr[3] = carry[0], hdr[4] = other[2];
+        hdr[5] = hdr[6] = hdr[7] = 0;
+    }
+}
+__global__ __launch_bounds__(256) void k_round_plan_apply(RoundSegs g, uint64_t r, const uint64_t *part) {
+    __shared__ uint64_t wsum[2][4], tot[2];
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t c = j < r ? g.nch[j] : 0, e = j < r ? g.nen[j] : 0;
+    const uint64_t co = block_exclusive_scan(c, wsum[0], &tot[0]);
+    const uint64_t eo = block_exclusive_scan(e, wsum[1], &tot[1]);
+    if (j < r) {
+        g.choff[j] = part[5 * (uint64_t)blockIdx.x + 3] + co;
+        g.enoff[j] = part[5 * (uint64_t)blockIdx.x + 1] + eo;
+    }
+}
+
 // Every child, one wave each, grid-stride (the count is known on the device only), then the
 // enumerations, one thread each
 __global__ __launch_bounds__(256) void k_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl,
@@ -474,6 +537,95 @@ __global__ __launch_bounds__(256) void k_round_emit(const uint64_t *hdr, uint64_
 }
 
 
+
+// ---- base-only rounds with the base's row prefix (RoundIn::pre): every sum is one difference, so
+// a thread per segment and a thread per child do what a wave each did (the wave's head / tail rows
+// and block sums, then a 64-lane reduction, for a range of a few rows) ---------------------------
+__device__ __forceinline__ void base_pre_agg(const uint8_t *pre, uint64_t lo, uint64_t hi, uint64_t *o) {
+    uint32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8];
+    if (hi > lo) {
+        load_fp(pre, hi, a);
+        load_fp(pre, lo, b);
+        sub256(a, b);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) o[q] = (uint64_t)a[2 * q] | ((uint64_t)a[2 * q + 1] << 32);
+    o[4] = hi > lo ? hi - lo : 0;
+}
+
+// every segment's raw rank range and local aggregate, a thread each
+__global__ __launch_bounds__(256) void k_round_bounds_pre(const uint32_t *rank, RoundIn in, RoundSegs g, uint64_t r,
+                                                          uint64_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= r) return;
+    const uint64_t l = in.sk[j] ? (uint64_t)rank[j] : 0ull, h = in.ek[j] ? (uint64_t)rank[r + j] : n;
+    g.lo[j] = l;
+    g.hi[j] = h;
+    uint64_t hi = h < n ? h : n, lo = l;
+    if (lo > hi) lo = hi;
+    uint64_t o[5];
+    base_pre_agg(in.pre, lo, hi, o);
+    uint64_t *d = g.loc + 5 * j;
+#pragma unroll
+    for (int q = 0; q < 5; q++) d[q] = o[q];
+}
+
+// every child a thread (its segment by binary search of the child offsets), 256 consecutive
+// children a workgroup per pass: staged in LDS, then stored with consecutive lanes on consecutive
+// words -- each wave instruction a whole run of lines into the mapped output (a thread storing its
+// own child's words, 16-40 B apart lane to lane, took 810 us for a round's 10 MB against the
+// wave-per-child kernel's 417); then the enumerations, a thread each
+constexpr uint32_t EMIT_CH = 256, EMIT_KW = 8;  // children per pass; key words (kl <= 32)
+__global__ __launch_bounds__(EMIT_CH) void k_round_emit_pre(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl,
+                                                             RoundIn in, RoundSegs g, uint8_t *out) {
+    __shared__ __align__(16) uint8_t s_sk[EMIT_CH], s_ek[EMIT_CH];
+    __shared__ __align__(16) uint32_t s_key[2][EMIT_CH * EMIT_KW];
+    __shared__ __align__(16) uint64_t s_agg[EMIT_CH * 5];
+    const uint64_t nc = hdr[3], ne = hdr[1];
+    if (nc > cap) return;  // the host grows the buffer and launches again
+    const RoundLayout L = round_layout(nc, ne, kl);
+    const uint32_t t = threadIdx.x, kw = kl / 4;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * EMIT_CH; c0 < nc; c0 += (uint64_t)gridDim.x * EMIT_CH) {  // uniform
+        const uint64_t c = c0 + t;
+        if (c < nc) {
+            const uint64_t j = round_owner(g.choff, r, c), k = c - g.choff[j];
+            uint8_t skd = in.sk[j], ekd = in.ek[j];
+            const uint8_t *skey = skd ? in.skeys + j * kl : nullptr, *ekey = ekd ? in.ekeys + j * kl : nullptr;
+            uint64_t o[5];
+            const uint64_t ncuts = g.nch[j] - 1;
+            const uint8_t kind = g.kind[j];
+            if (kind == 1 || ncuts == 0) {
+#pragma unroll
+                for (int q = 0; q < 5; q++) o[q] = kind == 1 ? 0ull : g.loc[5 * j + q];
+            } else {
+                const uint64_t st = g.stride[j], s0 = g.si[j];
+                const uint64_t lo = s0 + k * st, hi = k == ncuts ? g.ei[j] : s0 + (k + 1) * st;
+                if (k) skd = 1, skey = in.bkeys + lo * kl;
+                if (k != ncuts) ekd = 1, ekey = in.bkeys + hi * kl;
+                base_pre_agg(in.pre, lo, hi, o);
+            }
+#pragma unroll
+            for (int q = 0; q < 5; q++) s_agg[5 * t + q] = o[q];
+            s_sk[t] = skd, s_ek[t] = ekd;
+            for (uint32_t w = 0; w < kw; w++) {
+                s_key[0][t * kw + w] = skey ? reinterpret_cast<const uint32_t *>(skey)[w] : 0u;
+                s_key[1][t * kw + w] = ekey ? reinterpret_cast<const uint32_t *>(ekey)[w] : 0u;
+            }
+        }
+        __syncthreads();
+        const uint32_t m = nc - c0 < EMIT_CH ? (uint32_t)(nc - c0) : EMIT_CH;
+        for (uint32_t i = t; i < m; i += EMIT_CH) out[L.csk + c0 + i] = s_sk[i], out[L.cek + c0 + i] = s_ek[i];
+        uint32_t *os = reinterpret_cast<uint32_t *>(out + L.cskeys + c0 * kl);
+        uint32_t *oe = reinterpret_cast<uint32_t *>(out + L.cekeys + c0 * kl);
+        for (uint32_t i = t; i < m * kw; i += EMIT_CH) os[i] = s_key[0][i], oe[i] = s_key[1][i];
+        uint64_t *oa = reinterpret_cast<uint64_t *>(out + L.caggs) + 5 * c0;
+        for (uint32_t i = t; i < 5 * m; i += EMIT_CH) oa[i] = s_agg[i];
+        __syncthreads();  // the next pass overwrites the staging
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + t; j < r; j += stride)
+        if (g.nen[j]) round_emit_enum(j, g.enoff[j], L, kl, in, g, out);
+}
 
 // every segment's bounds over the view, one wave each
 __global__ __launch_bounds__(256) void k_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk,
@@ -978,6 +1130,16 @@ hipError_t launch_range_query(const uint8_t *fps, const uint8_t *bsums, const ui
     return hipGetLastError();
 }
 
+hipError_t launch_round_plan3(const RoundSegs &g, const uint64_t *remote, uint64_t r, uint64_t n, int sqrt_policy,
+                              uint64_t b, uint64_t *part, uint64_t *hdr, hipStream_t st) {
+    if (r == 0) return hipSuccess;
+    const uint64_t np = (r + 255) / 256;
+    hipLaunchKernelGGL(k_round_plan_part, dim3((uint32_t)np), dim3(256), 0, st, g, remote, r, n, sqrt_policy, b, part);
+    hipLaunchKernelGGL(k_round_plan_scan_parts, dim3(1), dim3(1024), 0, st, part, np, hdr);
+    hipLaunchKernelGGL(k_round_plan_apply, dim3((uint32_t)np), dim3(256), 0, st, g, r, (const uint64_t *)part);
+    return hipGetLastError();
+}
+
 hipError_t launch_round_plan(const RoundSegs &g, const uint64_t *remote, uint64_t r, uint64_t n, int sqrt_policy,
                              uint64_t b, uint64_t *hdr, hipStream_t st) {
     if (r == 0) return hipSuccess;
@@ -989,6 +1151,11 @@ hipError_t launch_round_plan(const RoundSegs &g, const uint64_t *remote, uint64_
 hipError_t launch_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl, const RoundIn &in,
                              const RoundSegs &g, uint8_t *out, hipStream_t st) {
     if (r == 0) return hipSuccess;
+    if (in.pre && kl <= 4 * EMIT_KW) {  // a thread per child
+        const uint64_t w = std::min<uint64_t>(std::max<uint64_t>((cap + EMIT_CH - 1) / EMIT_CH, (r + 255) / 256), 8192);
+        hipLaunchKernelGGL(k_round_emit_pre, dim3((uint32_t)w), dim3(EMIT_CH), 0, st, hdr, cap, r, kl, in, g, out);
+        return hipGetLastError();
+    }
     const uint64_t wgs = std::min<uint64_t>(std::max<uint64_t>((cap + 3) / 4, (r + 255) / 256), 4096);
     hipLaunchKernelGGL(k_round_emit, dim3((uint32_t)wgs), dim3(256), 0, st, hdr, cap, r, kl, in, g, out);
     return hipGetLastError();
@@ -997,6 +1164,10 @@ hipError_t launch_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint
 hipError_t launch_round_bounds(const uint32_t *rank, const RoundIn &in, const RoundSegs &g, uint64_t r, uint64_t n,
                                hipStream_t st) {
     if (r == 0) return hipSuccess;
+    if (in.pre) {  // a thread per segment
+        hipLaunchKernelGGL(k_round_bounds_pre, dim3((uint32_t)((r + 255) / 256)), dim3(256), 0, st, rank, in, g, r, n);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_round_bounds, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, rank, in, g, r, n);
     return hipGetLastError();
 }

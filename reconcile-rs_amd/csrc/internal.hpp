@@ -131,6 +131,10 @@ hipError_t launch_round_emit_view(const uint64_t *hdr, uint64_t cap, uint64_t r,
 // large rounds: decisions (g.lo / g.hi / g.loc filled) -> hdr (zeroed by the caller) gets the
 // outcome counts; after the offsets are scanned, children and enumerations into `out`
 // (round_layout(hdr children, hdr enumerated, kl)), nothing when the children outnumber cap
+// the plan, the child / enumeration offsets and the header in three launches (part: 5 u64 per 256
+// segments)
+hipError_t launch_round_plan3(const RoundSegs &g, const uint64_t *remote, uint64_t r, uint64_t n, int sqrt_policy,
+                              uint64_t b, uint64_t *part, uint64_t *hdr, hipStream_t st);
 hipError_t launch_round_plan(const RoundSegs &g, const uint64_t *remote, uint64_t r, uint64_t n, int sqrt_policy,
                              uint64_t b, uint64_t *hdr, hipStream_t st);
 hipError_t launch_round_emit(const uint64_t *hdr, uint64_t cap, uint64_t r, uint32_t kl, const RoundIn &in,

@@ -2657,7 +2657,9 @@ struct rh_store {
     // over in place) and are emitted straight into mapped memory sized for the worst case (up to
     // kDirectMax; past it, the header comes down first so the copy is exact).
     DevBuf<uint8_t> r_in, r_kind, r_out;
-    DevBuf<uint64_t> r_seg;
+    DevBuf<uint64_t> r_seg, r_part;
+    // A/B switch: RSOS_HIP_ROUND_PLAN3=0 plans a large round with k_round_plan and library scans
+    int plan3 = getenv("RSOS_HIP_ROUND_PLAN3") ? atoi(getenv("RSOS_HIP_ROUND_PLAN3")) : 1;
     PinnedVec<uint8_t> pr_out{hipHostMallocCoherent};  // a round's output (polled: round_tiny's sequence word)
     static constexpr size_t kRoundSmall = 256 << 10;  // below this, one speculative copy each way
     static constexpr size_t kDirectMax = 256ull << 20;  // mapped output sized for the worst case up to this
@@ -2790,6 +2792,7 @@ struct rh_store {
             }
             return rc;
         }
+        const double l0 = round_dbg ? now_us() : 0;
         if (nb)
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
                                         base_table()));
@@ -2826,18 +2829,36 @@ struct rh_store {
         } else {
             if (view) RH_HIP(rh::launch_round_bounds_view(q_rank.p, q_drank.p, din, run, g, place, r, stream));
             else RH_HIP(rh::launch_round_bounds(q_rank.p, din, g, r, n, stream));
-            RH_HIP(hipMemsetAsync(hdr, 0, 64, stream));
-            RH_HIP(rh::launch_round_plan(g, d_rem, r, n, sq, b, hdr, stream));
-            RH_HIP(rh::launch_exclusive_scan_u64(nch, choff, r, scratch, stream));
-            RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
+            const double lb = round_dbg ? now_us() : 0;
+            if (plan3) {  // three launches
+                if ((rc = r_part.ensure(5 * ((r + 255) / 256) + 8))) return rc;
+                RH_HIP(rh::launch_round_plan3(g, d_rem, r, n, sq, b, r_part.p, hdr, stream));
+            } else {
+                RH_HIP(hipMemsetAsync(hdr, 0, 64, stream));
+                RH_HIP(rh::launch_round_plan(g, d_rem, r, n, sq, b, hdr, stream));
+            }
+            const double lc = round_dbg ? now_us() : 0;
+            if (!plan3) {
+                RH_HIP(rh::launch_exclusive_scan_u64(nch, choff, r, scratch, stream));
+                RH_HIP(rh::launch_exclusive_scan_u64(nen, enoff, r, scratch, stream));
+            }
+            const double ld = round_dbg ? now_us() : 0;
             RH_HIP(emit(cap, hdr, eo));
+            if (round_dbg) dbg_large_l[0] += lb - l0, dbg_large_l[1] += lc - lb, dbg_large_l[2] += ld - lc, dbg_large_l[3] += now_us() - ld;
         }
         if (direct)  // the round (or, emitted in place, its header alone)
             RH_HIP(rh::launch_round_copy_out(hdr, cap, (uint32_t)kl, r_out.p, dout, round_copyout == 2 ? 64 : worst,
                                              stream));
+        const double l1 = round_dbg ? now_us() : 0;
         if (zero_copy || direct) {
             if ((rc = sync())) return rc;
             memcpy(h, pr_out.data(), sizeof h);
+            if (round_dbg && r > 1024) {  // the large rounds' host times: prep, launches, wait
+                const double l2 = now_us();
+                dbg_large[0] += l0 - h0, dbg_large[1] += l1 - l0, dbg_large[2] += l2 - l1;
+                if (dbg_large_last > 0 && h0 - dbg_large_last < 5000) dbg_large[3] += h0 - dbg_large_last;
+                dbg_large_n++;
+            }
         } else if (worst <= kRoundSmall) {
             pr_out.resize(worst);
             RH_HIP(hipMemcpyAsync(pr_out.data(), r_out.p, worst, hipMemcpyDeviceToHost, stream));
@@ -2849,7 +2870,9 @@ struct rh_store {
             if ((rc = sync())) return rc;
             memcpy(h, pr_out.data(), sizeof h);
         }
-        return round_finish(h, cap, r, view, din, run, g, place, worst > kRoundSmall && !direct, ch, en, oc);
+        rc = round_finish(h, cap, r, view, din, run, g, place, worst > kRoundSmall && !direct, ch, en, oc);
+        if (round_dbg) dbg_large_last = now_us();
+        return rc;
     }
     // the round's header is in h (and pr_out): emit again if its children outnumber cap (a wide
     // fan-out; the per-segment arrays are in g / place), copy the rest down if it is still on the
@@ -2893,6 +2916,9 @@ struct rh_store {
     double dbg_host[5] = {0, 0, 0, 0, 0}, dbg_last = 0;  // host: prep, launch, wait, finish, caller
     uint64_t dbg_host_n = 0;
     double dbg_prep[3] = {0, 0, 0};  // prep: the view, the staging, the launch record
+    double dbg_large[4] = {0, 0, 0, 0}, dbg_large_last = 0;  // rounds of > 1,024 segments
+    double dbg_large_l[4] = {0, 0, 0, 0};  // their launches: searches + bounds, plan, scans, emit
+    uint64_t dbg_large_n = 0;
     uint64_t dbg_rounds = 0;
     static double now_us() {
         return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -2904,6 +2930,14 @@ struct rh_store {
                     "\"bounds\": %.2f, \"decide\": %.2f, \"emit\": %.2f, \"fence\": %.2f}}\n",
                     (unsigned long long)dbg_rounds, dbg_sum[0] / dbg_rounds, dbg_sum[1] / dbg_rounds,
                     dbg_sum[2] / dbg_rounds, dbg_sum[3] / dbg_rounds, dbg_sum[4] / dbg_rounds, dbg_sum[5] / dbg_rounds);
+        if (round_dbg && dbg_large_n)
+            fprintf(stderr,
+                    "{\"large_round_host_us\": {\"rounds\": %llu, \"prep\": %.2f, \"launches\": %.2f, \"wait\": %.2f, "
+                    "\"caller_between_rounds\": %.2f, \"searches_bounds\": %.2f, \"plan\": %.2f, \"scans\": %.2f, "
+                    "\"emit\": %.2f}}\n",
+                    (unsigned long long)dbg_large_n, dbg_large[0] / dbg_large_n, dbg_large[1] / dbg_large_n,
+                    dbg_large[2] / dbg_large_n, dbg_large[3] / dbg_large_n, dbg_large_l[0] / dbg_large_n,
+                    dbg_large_l[1] / dbg_large_n, dbg_large_l[2] / dbg_large_n, dbg_large_l[3] / dbg_large_n);
         if (round_dbg && dbg_rounds > 1)
             fprintf(stderr,
                     "{\"round_host_us\": {\"prep\": %.2f, \"launch\": %.2f, \"wait\": %.2f, \"finish\": %.2f, "
@@ -2929,7 +2963,7 @@ struct rh_store {
         q_out.release(); q_bout.release(); q_dout.release(); q_keys.release(); q_rank.release(); q_drank.release();
         q_in.release(); q_res.release();
         stage_in.release(); stage_out.release(); stage_out2.release(); load_flag.release();
-        r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); pr_out.release();
+        r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); r_part.release(); pr_out.release();
         tsets[0].release(); tsets[1].release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release(); tier_dsmp.release();
         if (cstream) (void)hipStreamDestroy(cstream);
         if (kstream) (void)hipStreamDestroy(kstream);

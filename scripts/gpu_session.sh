@@ -22,6 +22,8 @@
 #   latency_phases    the same, tier off, with k_round_tiny's phase clocks (RSOS_HIP_ROUND_DBG=1)
 #   latency_host      the same with the host's times per round only (RSOS_HIP_ROUND_DBG=2)
 #   sstore_ab         sstore_client with RSOS_HIP_SSTORE_SPIN_US 50 / 300 / 2000, d 1 / 100, tier on / off
+#   trace_rbsr        the rbsr line under a kernel + memory-copy trace, its round timeline
+#   rbsr_host         the rbsr line with the host's times per large round (RSOS_HIP_ROUND_DBG=2)
 #   launch            examples/launch_latency: one waited-for small launch, 16 B and ~2.4 KB arguments
 #   interleave_sync interleave_nowait interleave_off
 #                     1 M-row batches into both replicas at 10^8 between d = 1 drives (tier_interleave)
@@ -66,6 +68,12 @@ for step in "$@"; do
     config5) run config5 300 python3 bench.py --config config5 ;;
     config5_40) run config5_40 300 python3 bench.py --config config5 --steps 40 ;;
     rbsr) run rbsr 300 python3 bench.py --config rbsr ;;
+    trace_rbsr)
+        run trace_rbsr 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trrb" -o tr -- python3 bench.py --config rbsr --cpu-baseline 0 --steps 5 --warmup 2
+        python3 scripts/write_timeline.py "$O/trrb" k_round_bounds > "$O/${TAG}_rbsr_round_timeline.txt" 2>&1 || true
+        cp "$O"/trrb/tr_kernel_stats.csv "$O/${TAG}_rbsr_kernel_stats.csv" 2>/dev/null || true
+        rm -f "$O"/trrb/*_trace.csv ;;
+    rbsr_host) run rbsr_host 300 env RSOS_HIP_ROUND_DBG=2 python3 bench.py --config rbsr --cpu-baseline 0 ;;
     snapshot) run snapshot 300 python3 bench.py --config snapshot ;;
     encoded) run encoded 300 python3 bench.py --config encoded ;;
     config2) run config2 300 python3 bench.py --config config2 ;;

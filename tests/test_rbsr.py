@@ -319,9 +319,14 @@ def _gpu_and_oracle(schema, c):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rowp", ["row_prefix", "block_prefix"])
 @pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("policy", ["fixed16", "sqrt", "fixed2"])
-def test_gpu_reconciliation_rounds_match_oracle(gpu, oracle_lib, policy, native):
+def test_gpu_reconciliation_rounds_match_oracle(gpu, oracle_lib, policy, native, rowp, monkeypatch):
+    """Base-only stores; row_prefix: the base's row prefix formed in order (RSOS_HIP_ROW_PREFIX=2),
+    so every round's sums are its differences (k_round_bounds_pre / k_round_emit_pre, the tiny
+    rounds' lane sums); block_prefix: none (the wave-per-range kernels)."""
+    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "2" if rowp == "row_prefix" else "0")
     from rsos_hip import RecordSchema, rbsr as R
     schema = RecordSchema.dated("bytes16", "bytes64")
     keys, ca, cb, only_a, only_b, mod = _dated_sets(7, 20_000, 60, 45, 30)
@@ -793,3 +798,43 @@ def test_run_columns_at_the_one_launch_limit(gpu, oracle_lib, run_rows, monkeypa
         st.close()
     ref.close()
     peer.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["fixed16", "sqrt"])
+def test_gpu_large_base_rounds_row_prefix_equal_block_prefix(gpu, policy, monkeypatch):
+    """Rounds of thousands of segments over a base-only replica: with the base's row prefix
+    (RSOS_HIP_ROW_PREFIX=2: a thread per segment and per child, k_round_bounds_pre /
+    k_round_emit_pre) equal the wave-per-range kernels without it (RSOS_HIP_ROW_PREFIX=0), whose
+    rounds the tests above hold to the literal driver -- round by round, children with their bounds
+    and sums, enumerations and outcomes.  The first plans a large round in three launches
+    (k_round_plan_part / _scan_parts / _apply), the second with k_round_plan and library scans
+    (RSOS_HIP_ROUND_PLAN3=0)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(31, 200_000, 1500, 1000, 1000)
+    st = {}
+    for rowp in ("2", "0"):
+        monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", rowp)
+        monkeypatch.setenv("RSOS_HIP_ROUND_PLAN3", "1" if rowp == "2" else "0")
+        s = GpuFingerprintStore(schema)
+        s.load_bulk(ca)
+        st[rowp] = s
+    gb = GpuFingerprintStore(schema)
+    gb.load_bulk(cb)
+    pol = {"fixed16": R.FixedFanOut(16), "sqrt": R.SqrtFanOut()}[policy]
+    active, k, widest = R.initial_segments(gb), 0, 0
+    while len(active):
+        if k % 2 == 0:
+            widest = max(widest, len(active))
+            ch, en, o = R.protocol_round_segments(st["2"], pol, active)
+            wch, wen, wo = R.protocol_round_segments(st["0"], pol, active)
+            assert _outcome(o) == _outcome(wo)
+            assert _norm(ch.items(schema)) == _norm(wch.items(schema))
+            assert [en.bounds(schema, i) for i in range(en.n)] == [wen.bounds(schema, i) for i in range(wen.n)]
+        else:
+            ch, en, o = R.protocol_round_segments(gb, pol, active)
+        active, k = ch, k + 1
+    assert widest > 1024 and k > 3
+    for g in (*st.values(), gb):
+        g.close()

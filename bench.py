@@ -946,7 +946,7 @@ def reconcile(args, world, rank, dev, dist):
         while len(active):
             segs += len(active)
             r = len(active)
-            active, en, _ = R.protocol_round_segments((b, a)[k % 2], pol, active, copy=False)
+            active, en, _ = R.protocol_round_segments((b, a)[k % 2], pol, active, raw=True)
             enum += len(en)
             pcie["in"] += round_in_bytes(r, kl)
             pcie["out"] += round_out_bytes(len(active), len(en), kl)

@@ -245,11 +245,28 @@ def _wrap(cs: A.Segments, key_len: int, copy: bool, with_aggs: bool) -> "Segment
     return seg
 
 
-def protocol_round_segments(store, policy, active: Segments,
-                            copy: bool = True) -> Tuple[Segments, Segments, RoundOutcome]:
+class RawSegments:
+    """A round's output as the library returned it (its rh_segments, pointing into the answering
+    store's own buffers, valid until that store's next call): handed to the peer store's round as
+    it is, as a C or Rust caller hands the children over -- no numpy views either way."""
+    __slots__ = ("cs",)
+
+    def __init__(self, cs: A.Segments):
+        self.cs = cs
+
+    def __len__(self) -> int:
+        return int(self.cs.n)
+
+    def c(self) -> A.Segments:
+        return self.cs
+
+
+def protocol_round_segments(store, policy, active,
+                            copy: bool = True, raw: bool = False) -> Tuple[Segments, Segments, RoundOutcome]:
     """One round of FixedFanOut / SqrtFanOut inside the library: (children, enumerations, outcome).
     copy=False returns views of the store's own output arrays, valid until the store's next call
-    (enough to hand the children to the peer store's round)."""
+    (enough to hand the children to the peer store's round); raw=True returns them as RawSegments
+    (no views at all).  `active`: Segments or RawSegments."""
     if isinstance(policy, FixedFanOut):
         kind, b = A.POLICY_FIXED_FAN_OUT, policy.fan_out
     elif isinstance(policy, SqrtFanOut):
@@ -260,6 +277,10 @@ def protocol_round_segments(store, policy, active: Segments,
     a, cc, ec, oc = active.c(), A.Segments(), A.Segments(), A.RoundOutcome()
     A.check(store._f("protocol_round")(store._h, kind, b, C.byref(a), C.byref(cc), C.byref(ec), C.byref(oc)),
             store._P + "protocol_round")
+    if raw:
+        return (RawSegments(cc), RawSegments(ec),
+                RoundOutcome(int(oc.skipped), int(oc.enumerated), int(oc.split), int(oc.children),
+                             int(oc.dropped_malformed)))
     return (_wrap(cc, kl, copy, True), _wrap(ec, kl, copy, False),
             RoundOutcome(int(oc.skipped), int(oc.enumerated), int(oc.split), int(oc.children),
                          int(oc.dropped_malformed)))

@@ -838,3 +838,30 @@ def test_gpu_large_base_rounds_row_prefix_equal_block_prefix(gpu, policy, monkey
     assert widest > 1024 and k > 3
     for g in (*st.values(), gb):
         g.close()
+
+
+@pytest.mark.gpu
+def test_raw_round_handoff_equals_views(gpu):
+    """protocol_round_segments(raw=True) hands a round's output to the peer as the library returned
+    it (RawSegments, bench.py's rbsr loop): the same rounds, outcomes and enumeration counts as
+    copied Segments."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    schema = RecordSchema.dated("bytes16", "bytes64")
+    keys, ca, cb, only_a, only_b, mod = _dated_sets(37, 50_000, 400, 300, 300)
+    a, b = GpuFingerprintStore(schema), GpuFingerprintStore(schema)
+    a.load_bulk(ca)
+    b.load_bulk(cb)
+    pol = R.FixedFanOut(16)
+
+    def run(raw):
+        active, k, log = R.initial_segments(a), 0, []
+        while len(active):
+            kw = {"raw": True} if raw else {"copy": True}
+            active, en, o = R.protocol_round_segments((b, a)[k % 2], pol, active, **kw)
+            log.append((_outcome(o), len(active), len(en)))
+            k += 1
+        return log
+    got, want = run(True), run(False)
+    assert got == want and len(got) > 3
+    a.close()
+    b.close()

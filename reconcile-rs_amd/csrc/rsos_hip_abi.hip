@@ -2664,6 +2664,7 @@ struct rh_store {
     static constexpr size_t kRoundSmall = 256 << 10;  // below this, one speculative copy each way
     static constexpr size_t kDirectMax = 256ull << 20;  // mapped output sized for the worst case up to this
     int round_copyout = getenv("RSOS_HIP_ROUND_COPYOUT") ? atoi(getenv("RSOS_HIP_ROUND_COPYOUT")) : 2;
+    int round_copyin = getenv("RSOS_HIP_ROUND_COPYIN") ? atoi(getenv("RSOS_HIP_ROUND_COPYIN")) : 0;
     int protocol_round(int policy, uint64_t param, const rh_segments &in, rh_segments *ch, rh_segments *en,
                        rh_round_outcome *oc) {
         int rc;
@@ -2730,7 +2731,16 @@ struct rh_store {
                                     static_cast<const uint8_t *>(in.start_keys) == base + o_sk &&
                                     static_cast<const uint8_t *>(in.end_keys) == base + o_ekeys &&
                                     reinterpret_cast<const uint8_t *>(in.aggregates) == base + o_rem;
-            if (contiguous) {
+            // the peer's round, read in place by a kernel (RSOS_HIP_ROUND_COPYIN=1): 206-219 against
+            // the copy engine's 213-214 M segments/s, no gain (profiles/r05_rbsr_copyin_ab.jsonl)
+            void *dsrc = nullptr;
+            if (contiguous && round_copyin && hipHostGetDevicePointer(&dsrc, const_cast<uint8_t *>(base), 0) == hipSuccess &&
+                dsrc) {
+                rh::CopyJobs j{};
+                j.src[0] = static_cast<const uint8_t *>(dsrc), j.dst[0] = r_in.p, j.bytes[0] = in_bytes, j.n = 1;
+                RH_HIP(rh::launch_copy_to_host(j, stream));
+            } else if (contiguous) {
+                (void)hipGetLastError();
                 RH_HIP(hipMemcpyAsync(r_in.p, base, in_bytes, hipMemcpyHostToDevice, stream));
             } else {
                 for (const auto &p : parts)  // keys of an all-unbounded side may be NULL (never read)

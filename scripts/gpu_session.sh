@@ -73,6 +73,11 @@ for step in "$@"; do
         python3 scripts/write_timeline.py "$O/trrb" k_round_bounds > "$O/${TAG}_rbsr_round_timeline.txt" 2>&1 || true
         cp "$O"/trrb/tr_kernel_stats.csv "$O/${TAG}_rbsr_kernel_stats.csv" 2>/dev/null || true
         rm -f "$O"/trrb/*_trace.csv ;;
+    rbsr_copyin_ab)  # a large round's input: copy engine / kernel reading the peer's mapped output
+        run rbsr_copyin0 300 env RSOS_HIP_ROUND_COPYIN=0 python3 bench.py --config rbsr --cpu-baseline 0 &&
+        run rbsr_copyin1 300 env RSOS_HIP_ROUND_COPYIN=1 python3 bench.py --config rbsr --cpu-baseline 0 &&
+        run rbsr_copyin0b 300 env RSOS_HIP_ROUND_COPYIN=0 python3 bench.py --config rbsr --cpu-baseline 0 &&
+        run rbsr_copyin1b 300 env RSOS_HIP_ROUND_COPYIN=1 python3 bench.py --config rbsr --cpu-baseline 0 ;;
     rbsr_host) run rbsr_host 300 env RSOS_HIP_ROUND_DBG=2 python3 bench.py --config rbsr --cpu-baseline 0 ;;
     snapshot) run snapshot 300 python3 bench.py --config snapshot ;;
     encoded) run encoded 300 python3 bench.py --config encoded ;;

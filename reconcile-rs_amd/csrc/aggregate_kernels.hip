@@ -627,6 +627,84 @@ __global__ __launch_bounds__(EMIT_CH) void k_round_emit_pre(const uint64_t *hdr,
         if (g.nen[j]) round_emit_enum(j, g.enoff[j], L, kl, in, g, out);
 }
 
+// ---- the same over base + delta run when both row prefixes are there (has_row_prefix): a thread
+// per segment, a thread per child (its cut places by view_at, its sum their prefixes' difference)
+__global__ __launch_bounds__(256) void k_bounds_view_pre(const uint32_t *rank_b, const uint32_t *rank_j,
+                                                         const uint8_t *sk, const uint8_t *ek, RoundIn in, RoundRun R,
+                                                         uint64_t r, uint32_t ia, uint32_t ib, uint64_t off,
+                                                         uint64_t *lo_out, uint64_t *hi_out, uint64_t *agg_out,
+                                                         uint64_t *place) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= r) return;
+    const uint64_t qs = ia * j, qe = ib * j + off;
+    const uint64_t bs = sk[j] ? rank_b[qs] : 0, js = sk[j] ? rank_j[qs] : 0;
+    const uint64_t be = ek[j] ? rank_b[qe] : R.nb, je = ek[j] ? rank_j[qe] : R.n;
+    const int64_t cs = R.n ? R.cntp[js] : 0, ce = R.n ? R.cntp[je] : 0;
+    const uint64_t l = (uint64_t)((int64_t)bs + cs), h = (uint64_t)((int64_t)be + ce);
+    uint64_t fp[4] = {0, 0, 0, 0};
+    if (h > l) pre_range_fp(in, R, bs, js, be, je, fp);  // an inverted range is ZERO
+    lo_out[j] = l;
+    hi_out[j] = h;
+    if (place) place[4 * j] = bs, place[4 * j + 1] = js, place[4 * j + 2] = be, place[4 * j + 3] = je;
+    uint64_t *o = agg_out + 5 * j;
+    o[0] = fp[0], o[1] = fp[1], o[2] = fp[2], o[3] = fp[3];
+    o[4] = h > l ? h - l : 0;
+}
+__global__ __launch_bounds__(EMIT_CH) void k_round_emit_view_pre(const uint64_t *hdr, uint64_t cap, uint64_t r,
+                                                                  uint32_t kl, RoundIn in, RoundRun R, RoundSegs g,
+                                                                  const uint64_t *place, uint8_t *out) {
+    __shared__ __align__(16) uint8_t s_sk[EMIT_CH], s_ek[EMIT_CH];
+    __shared__ __align__(16) uint32_t s_key[2][EMIT_CH * EMIT_KW];
+    __shared__ __align__(16) uint64_t s_agg[EMIT_CH * 5];
+    const uint64_t nc = hdr[3], ne = hdr[1];
+    if (nc > cap) return;  // the host grows the buffer and launches again
+    const RoundLayout L = round_layout(nc, ne, kl);
+    const uint32_t t = threadIdx.x, kw = kl / 4;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * EMIT_CH; c0 < nc; c0 += (uint64_t)gridDim.x * EMIT_CH) {  // uniform
+        const uint64_t c = c0 + t;
+        if (c < nc) {
+            const uint64_t j = round_owner(g.choff, r, c), k = c - g.choff[j];
+            uint8_t skd = in.sk[j], ekd = in.ek[j];
+            const uint8_t *skey = skd ? in.skeys + j * kl : nullptr, *ekey = ekd ? in.ekeys + j * kl : nullptr;
+            uint64_t o[5];
+            const uint64_t ncuts = g.nch[j] - 1;
+            const uint8_t kind = g.kind[j];
+            if (kind == 1 || ncuts == 0) {
+#pragma unroll
+                for (int q = 0; q < 5; q++) o[q] = kind == 1 ? 0ull : g.loc[5 * j + q];
+            } else {
+                const uint64_t st = g.stride[j], s0 = g.si[j];
+                const uint64_t lo = s0 + k * st, hi = k == ncuts ? g.ei[j] : s0 + (k + 1) * st;
+                ViewPlace a{place[4 * j], place[4 * j + 1], nullptr}, z{place[4 * j + 2], place[4 * j + 3], nullptr};
+                if (k) a = view_at(R, in.bkeys, kl, lo), skd = 1, skey = a.key;
+                if (k != ncuts) z = view_at(R, in.bkeys, kl, hi), ekd = 1, ekey = z.key;
+                uint64_t fp[4];
+                pre_range_fp(in, R, a.b, a.j, z.b, z.j, fp);
+                o[0] = fp[0], o[1] = fp[1], o[2] = fp[2], o[3] = fp[3], o[4] = hi - lo;
+            }
+#pragma unroll
+            for (int q = 0; q < 5; q++) s_agg[5 * t + q] = o[q];
+            s_sk[t] = skd, s_ek[t] = ekd;
+            for (uint32_t w = 0; w < kw; w++) {
+                s_key[0][t * kw + w] = skey ? reinterpret_cast<const uint32_t *>(skey)[w] : 0u;
+                s_key[1][t * kw + w] = ekey ? reinterpret_cast<const uint32_t *>(ekey)[w] : 0u;
+            }
+        }
+        __syncthreads();
+        const uint32_t m = nc - c0 < EMIT_CH ? (uint32_t)(nc - c0) : EMIT_CH;
+        for (uint32_t i = t; i < m; i += EMIT_CH) out[L.csk + c0 + i] = s_sk[i], out[L.cek + c0 + i] = s_ek[i];
+        uint32_t *os = reinterpret_cast<uint32_t *>(out + L.cskeys + c0 * kl);
+        uint32_t *oe = reinterpret_cast<uint32_t *>(out + L.cekeys + c0 * kl);
+        for (uint32_t i = t; i < m * kw; i += EMIT_CH) os[i] = s_key[0][i], oe[i] = s_key[1][i];
+        uint64_t *oa = reinterpret_cast<uint64_t *>(out + L.caggs) + 5 * c0;
+        for (uint32_t i = t; i < 5 * m; i += EMIT_CH) oa[i] = s_agg[i];
+        __syncthreads();
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + t; j < r; j += stride)
+        if (g.nen[j]) round_emit_enum(j, g.enoff[j], L, kl, in, g, out);
+}
+
 // every segment's bounds over the view, one wave each
 __global__ __launch_bounds__(256) void k_bounds_view(const uint32_t *rank_b, const uint32_t *rank_j, const uint8_t *sk,
                                                      const uint8_t *ek, RoundIn in, RoundRun R, uint64_t r,
@@ -1176,6 +1254,11 @@ hipError_t launch_round_bounds_view(const uint32_t *rank_b, const uint32_t *rank
                                     const RoundRun &run, const RoundSegs &g, uint64_t *place, uint64_t r,
                                     hipStream_t st) {
     if (r == 0) return hipSuccess;
+    if (in.pre && (run.n == 0 || run.pre)) {  // a thread per segment
+        hipLaunchKernelGGL(k_bounds_view_pre, dim3((uint32_t)((r + 255) / 256)), dim3(256), 0, st, rank_b, rank_j, in.sk,
+                           in.ek, in, run, r, 1u, 1u, r, g.lo, g.hi, g.loc, place);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_bounds_view, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, rank_b, rank_j, in.sk, in.ek, in,
                        run, r, 1u, 1u, r, g.lo, g.hi, g.loc, place);
     return hipGetLastError();
@@ -1185,6 +1268,11 @@ hipError_t launch_resolve_view(const uint32_t *rank_b, const uint32_t *rank_j, c
                                const RoundIn &in, const RoundRun &run, uint64_t r, uint64_t *lo, uint64_t *hi,
                                uint64_t *aggs, hipStream_t st) {
     if (r == 0) return hipSuccess;
+    if (in.pre && (run.n == 0 || run.pre)) {  // a thread per segment
+        hipLaunchKernelGGL(k_bounds_view_pre, dim3((uint32_t)((r + 255) / 256)), dim3(256), 0, st, rank_b, rank_j, sk, ek,
+                           in, run, r, 2u, 2u, (uint64_t)1, lo, hi, aggs, (uint64_t *)nullptr);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_bounds_view, dim3((uint32_t)((r + 3) / 4)), dim3(256), 0, st, rank_b, rank_j, sk, ek, in, run,
                        r, 2u, 2u, (uint64_t)1, lo, hi, aggs, (uint64_t *)nullptr);
     return hipGetLastError();
@@ -1210,6 +1298,12 @@ hipError_t launch_round_emit_view(const uint64_t *hdr, uint64_t cap, uint64_t r,
                                   const RoundRun &run, const RoundSegs &g, const uint64_t *place, uint8_t *out,
                                   hipStream_t st) {
     if (r == 0) return hipSuccess;
+    if (in.pre && (run.n == 0 || run.pre) && kl <= 4 * EMIT_KW) {  // a thread per child
+        const uint64_t w = std::min<uint64_t>(std::max<uint64_t>((cap + EMIT_CH - 1) / EMIT_CH, (r + 255) / 256), 8192);
+        hipLaunchKernelGGL(k_round_emit_view_pre, dim3((uint32_t)w), dim3(EMIT_CH), 0, st, hdr, cap, r, kl, in, run, g,
+                           place, out);
+        return hipGetLastError();
+    }
     const uint64_t wgs = std::min<uint64_t>(std::max<uint64_t>((cap + 3) / 4, (r + 255) / 256), 4096);
     hipLaunchKernelGGL(k_round_emit_view, dim3((uint32_t)wgs), dim3(256), 0, st, hdr, cap, r, kl, in, run, g, place,
                        out);

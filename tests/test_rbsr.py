@@ -645,11 +645,15 @@ def test_gpu_rounds_over_pending_delta_run_match_oracle(gpu, oracle_lib, policy,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rowp", ["row_prefix", "block_prefix"])
 @pytest.mark.parametrize("policy", ["fixed16", "sqrt"])
-def test_gpu_large_rounds_over_pending_delta_run(gpu, policy):
+def test_gpu_large_rounds_over_pending_delta_run(gpu, policy, rowp, monkeypatch):
     """Rounds of thousands of segments over a replica whose delta run is pending equal the same
     rounds over a freshly loaded replica with the same contents (the base-only path, tested above
-    against the literal driver), round by round, and leave the delta run in place."""
+    against the literal driver), round by round, and leave the delta run in place.  row_prefix:
+    both replicas with their row prefixes formed in order (a thread per segment and per child,
+    k_bounds_view_pre / k_round_emit_view_pre); block_prefix: without (a wave each)."""
+    monkeypatch.setenv("RSOS_HIP_ROW_PREFIX", "2" if rowp == "row_prefix" else "0")
     from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
     schema = RecordSchema.dated("bytes16", "bytes64")
     keys, ca, cb, only_a, only_b, mod = _dated_sets(23, 200_000, 1000, 1000, 1000)

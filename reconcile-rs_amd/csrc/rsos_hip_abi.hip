@@ -1364,7 +1364,16 @@ struct rh_store {
     // on the device once per version of the contents: device reads over base + run use them in
     // place (rh::RoundRun), the run copy adds the contributions' prefix sums and takes them down.
     // trun_ver: the version they hold.
-    uint64_t trun_ver = ~0ull;
+    uint64_t trun_ver = ~0ull, trun_pre_ver = ~0ull;  // the version trun_pre holds
+    // the run's row prefix (run_columns forms it for a short run; a long run's on demand)
+    int run_row_prefix() {
+        int rc;
+        if ((rc = run_columns())) return rc;
+        if (trun_pre_ver == version) return RH_OK;
+        RH_HIP(rh::launch_row_prefix(trun_c.p, nd, trun_bpre.p, trun_pre.p, stream));
+        trun_pre_ver = version;
+        return RH_OK;
+    }
     // A/B switch: RSOS_HIP_RUNCOL_FUSED=0 forms a short run's columns in the eight launches too
     int run_cols_fused = getenv("RSOS_HIP_RUNCOL_FUSED") ? atoi(getenv("RSOS_HIP_RUNCOL_FUSED")) : 1;
     int run_columns() {
@@ -1384,14 +1393,16 @@ struct rh_store {
             const rh::RunCols o{trun_c.p,  trun_cnt.p,  trun_fl.p,   trun_br.p,   trun_pre.p, trun_bs.p,
                                 trun_ss.p, trun_spre.p, trun_bpre.p, trun_cntp.p, trun_gs.p};
             RH_HIP(rh::launch_run_columns_small(dslot[cd].p, dheap.p, n1, o, stream));
-            trun_ver = version;
+            trun_ver = trun_pre_ver = version;
             return RH_OK;
         }
-        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream));
-        RH_HIP(rh::launch_reduce(trun_c.p, n1, trun_bs.p, stream));
+        // a long run: the columns with their block sums in one pass, the block prefix; its row prefix
+        // (another read and write of 32 B an entry: ~0.1 ms at 10^7 entries, more than the rounds
+        // of one reconciliation save with it) only for the tier's run copy (run_row_prefix)
+        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream,
+                                   trun_bs.p));
         RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
-        // block and row prefixes: a range sum over the run is then one difference (pre_range_fp)
-        RH_HIP(rh::launch_prefix(trun_c.p, n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, trun_pre.p, stream));
+        RH_HIP(rh::launch_block_prefix(n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, stream));
         RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         RH_HIP(rh::launch_tier_gsamp(trun_br.p, trun_cntp.p, trun_fl.p, n1, trun_gs.p, stream));
@@ -1409,8 +1420,8 @@ struct rh_store {
         }
         const uint64_t ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096, nbk = rh_num_blocks(n1),
                        nsb = rh_num_superblocks(n1);
-        // run_columns formed the contributions' row prefix: the host walks it (HostTier::Run::prefix)
-        if ((rc = run_columns()) || (rc = trun_smp.ensure(ns + ns2 + 8))) return rc;
+        // the contributions' row prefix: the host walks it (HostTier::Run::prefix)
+        if ((rc = run_row_prefix()) || (rc = trun_smp.ensure(ns + ns2 + 8))) return rc;
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
         try {
@@ -2322,7 +2333,7 @@ struct rh_store {
                             trun_gs.p,
                             nb,
                             trun_bpre.p,
-                            trun_pre.p};
+                            trun_pre_ver == version ? trun_pre.p : nullptr};
         *in = base_in();
         return RH_OK;
     }

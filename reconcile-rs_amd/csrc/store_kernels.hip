@@ -1758,27 +1758,37 @@ hipError_t launch_delta_merge(int kk, int kl, const uint8_t *dkeys, const uint32
 // The host tier's run copy (host_tier.hpp HostTier::Run): delta row i's DeltaRec, read through its
 // slot, as columns -- the contribution (32 B), the count delta live - in_base (cnt[n] = 0 closes
 // the array for the exclusive scan that follows), the flags and the base rank
-__global__ void k_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n, uint8_t *contrib, uint32_t *cnt,
-                           uint8_t *flags, uint32_t *brank) {
+// One workgroup per 256-entry block: with bsums, the block's contribution sum too (the pass a
+// k_reduce over the written contributions took).
+__global__ __launch_bounds__(256) void k_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n,
+                                                  uint8_t *contrib, uint32_t *cnt, uint8_t *flags, uint32_t *brank,
+                                                  uint8_t *bsums) {
+    __shared__ SumTile tile;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n) {
+        const DeltaRec *r = reinterpret_cast<const DeltaRec *>(heap) + slot[i];
+        const uint4 *c = reinterpret_cast<const uint4 *>(r->contrib);
+        const uint4 a = c[0], b = c[1];
+        reinterpret_cast<uint4 *>(contrib + 32 * i)[0] = a;
+        reinterpret_cast<uint4 *>(contrib + 32 * i)[1] = b;
+        h[0] = a.x, h[1] = a.y, h[2] = a.z, h[3] = a.w, h[4] = b.x, h[5] = b.y, h[6] = b.z, h[7] = b.w;
+        const uint32_t f = r->flags;
+        cnt[i] = (uint32_t)(((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0));
+        flags[i] = (uint8_t)f;
+        brank[i] = r->brank;
+    } else if (i == n) {
         cnt[n] = 0;
-        return;
     }
-    const DeltaRec *r = reinterpret_cast<const DeltaRec *>(heap) + slot[i];
-    const uint4 *c = reinterpret_cast<const uint4 *>(r->contrib);
-    reinterpret_cast<uint4 *>(contrib + 32 * i)[0] = c[0];
-    reinterpret_cast<uint4 *>(contrib + 32 * i)[1] = c[1];
-    const uint32_t f = r->flags;
-    cnt[i] = (uint32_t)(((f & DeltaRec::LIVE) ? 1 : 0) - ((f & DeltaRec::IN_BASE) ? 1 : 0));
-    flags[i] = (uint8_t)f;
-    brank[i] = r->brank;
+    if (!bsums || (uint64_t)blockIdx.x * 256 >= n) return;  // uniform
+    uint32_t sum[8];
+    block_sum_fps256(h, tile, sum);  // lanes past the end hold zero
+    if (threadIdx.x == 0) store_sum(bsums, blockIdx.x, sum);
 }
 
 hipError_t launch_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n, uint8_t *contrib, uint32_t *cnt,
-                           uint8_t *flags, uint32_t *brank, hipStream_t st) {
-    hipLaunchKernelGGL(k_tier_run, g1(n + 1), dim3(256), 0, st, slot, heap, n, contrib, cnt, flags, brank);
+                           uint8_t *flags, uint32_t *brank, hipStream_t st, uint8_t *bsums) {
+    hipLaunchKernelGGL(k_tier_run, g1(n + 1), dim3(256), 0, st, slot, heap, n, contrib, cnt, flags, brank, bsums);
     return hipGetLastError();
 }
 

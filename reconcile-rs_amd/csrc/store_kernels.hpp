@@ -283,8 +283,9 @@ hipError_t launch_compact_rows(const uint8_t *src, uint32_t row_bytes, const uin
                                uint64_t m, uint8_t *out, hipStream_t st);
 hipError_t launch_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, Scratch &s, hipStream_t st);
 // the delta run's DeltaRecs as the host tier's run-copy columns (k_tier_run); cnt has n + 1 entries
+// (bsums: the 256-entry blocks' contribution sums too, nullable)
 hipError_t launch_tier_run(const uint32_t *slot, const uint8_t *heap, uint64_t n, uint8_t *contrib, uint32_t *cnt,
-                           uint8_t *flags, uint32_t *brank, hipStream_t st);
+                           uint8_t *flags, uint32_t *brank, hipStream_t st, uint8_t *bsums = nullptr);
 // and select's index over it: entry 64 k's live keys at or below it (k_tier_gsamp)
 hipError_t launch_tier_gsamp(const uint32_t *brank, const uint32_t *cntp, const uint8_t *flags, uint64_t n,
                              uint64_t *gsamp, hipStream_t st);

@@ -29,6 +29,7 @@
 #                     1 M-row batches into both replicas at 10^8 between d = 1 drives (tier_interleave)
 #   trace_interleave  the default-policy interleave under a kernel + memory-copy trace
 #   trace_interleave_nowait  the same with RSOS_HIP_TIER_SYNC=0
+#   trace_interleave_off     the same with the tier off
 #   interleave_nowait_ab     interleave_nowait with the foreground stream priority / background CU
 #                     mask each on and off (RSOS_HIP_FORE_PRIORITY, RSOS_HIP_BG_RESERVE)
 #   sstore            the sharded store's client (examples/sstore_client) on device 0
@@ -134,6 +135,10 @@ for step in "$@"; do
         run trace_interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trinw" -o tr -- $EX/tier_interleave 100000000 1000000 6 1 c5 1
         python3 scripts/copy_summary.py "$O/trinw" > "$O/${TAG}_interleave_nowait_trace_summary.txt" 2>&1 || true
         python3 scripts/write_timeline.py "$O/trinw" k_cs_minmax > "$O/${TAG}_interleave_nowait_timeline.txt" 2>&1 || true ;;
+    trace_interleave_off)
+        run trace_interleave_off 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trio" -o tr -- $EX/tier_interleave 100000000 1000000 6 0 c5 1
+        python3 scripts/write_timeline.py "$O/trio" k_cs_minmax > "$O/${TAG}_interleave_off_timeline.txt" 2>&1 || true
+        rm -f "$O"/trio/*_trace.csv ;;
     trace_interleave)
         run trace_interleave 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trint" -o tr -- $EX/tier_interleave 100000000 1000000 6 1 c5 1
         python3 scripts/copy_summary.py "$O/trint" > "$O/${TAG}_interleave_trace_summary.txt" 2>&1 || true

@@ -30,6 +30,7 @@
 #   trace_interleave  the default-policy interleave under a kernel + memory-copy trace
 #   trace_interleave_nowait  the same with RSOS_HIP_TIER_SYNC=0
 #   trace_interleave_off     the same with the tier off
+#   trace_config5     config5 (40 batches) under a kernel trace, four batches' timelines
 #   interleave_nowait_ab     interleave_nowait with the foreground stream priority / background CU
 #                     mask each on and off (RSOS_HIP_FORE_PRIORITY, RSOS_HIP_BG_RESERVE)
 #   sstore            the sharded store's client (examples/sstore_client) on device 0
@@ -135,6 +136,11 @@ for step in "$@"; do
         run trace_interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trinw" -o tr -- $EX/tier_interleave 100000000 1000000 6 1 c5 1
         python3 scripts/copy_summary.py "$O/trinw" > "$O/${TAG}_interleave_nowait_trace_summary.txt" 2>&1 || true
         python3 scripts/write_timeline.py "$O/trinw" k_cs_minmax > "$O/${TAG}_interleave_nowait_timeline.txt" 2>&1 || true ;;
+    trace_config5)
+        run trace_config5 300 rocprofv3 --kernel-trace --output-format csv -d "$O/c5t" -o c5 -- python3 bench.py --config config5 --steps 40 --cpu-baseline 0
+        f=$(find "$O/c5t" -name 'c5_kernel_trace.csv' | head -n 1)
+        python3 scripts/c5_timeline.py "$f" 20 21 35 36 > "$O/${TAG}_config5_timeline.txt" 2>&1 || true
+        rm -f "$f" ;;
     trace_interleave_off)
         run trace_interleave_off 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trio" -o tr -- $EX/tier_interleave 100000000 1000000 6 0 c5 1
         python3 scripts/write_timeline.py "$O/trio" k_cs_minmax > "$O/${TAG}_interleave_off_timeline.txt" 2>&1 || true

@@ -161,6 +161,110 @@ struct HostTier {
         }
         return lo;
     }
+    // ---- the same searches for many keys at once: each phase's cache lines are requested for every
+    // key before any is read, so the keys' dependent misses overlap (a round's 2r bounds at 10^8 rows
+    // were ~4 dependent DRAM misses each, one key after another) -----------------------------------
+    struct SampWin {
+        uint64_t d, ll, lh, ul, uh;  // the digit, the lower and upper bounds' sample windows
+    };
+    static SampWin samp_windows(const uint64_t *samp, uint64_t ns, const uint64_t *samp2, uint64_t ns2, uint64_t d) {
+        const uint64_t i = std::lower_bound(samp2, samp2 + ns2, d) - samp2;
+        const uint64_t iu = std::upper_bound(samp2, samp2 + ns2, d) - samp2;
+        SampWin w{d, i ? ((i - 1) << SHIFT) + 1 : 0, std::min<uint64_t>(ns, i << SHIFT),
+                  iu ? ((iu - 1) << SHIFT) + 1 : 0, std::min<uint64_t>(ns, iu << SHIFT)};
+        if (w.lh > w.ll) prefetch_span(samp + w.ll, (w.lh - w.ll) * 8);
+        if (w.uh > w.ul && w.ul != w.ll) prefetch_span(samp + w.ul, (w.uh - w.ul) * 8);
+        return w;
+    }
+    // sampled_lb's key window [lo, hi) from the windows (its lines requested)
+    void key_window(const uint8_t *ks, uint64_t nk, const uint64_t *samp, const SampWin &w, uint64_t *lo,
+                    uint64_t *hi) const {
+        const uint64_t jl = w.ll >= w.lh ? w.ll : std::lower_bound(samp + w.ll, samp + w.lh, w.d) - samp;
+        const uint64_t ul = std::max<uint64_t>(jl, w.ul);
+        const uint64_t jh = ul >= w.uh ? ul : std::upper_bound(samp + ul, samp + w.uh, w.d) - samp;
+        *lo = jl ? ((jl - 1) << SHIFT) + 1 : 0;
+        *hi = std::min<uint64_t>(nk, jh << SHIFT);
+        if (*hi - *lo <= 64) prefetch_span(ks + *lo * kl, (*hi - *lo) * kl);
+    }
+    uint64_t key_search(const uint8_t *ks, uint64_t lo, uint64_t hi, const uint8_t *key) const {
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (cmp(ks + mid * kl, key) < 0) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    }
+    // view_lt(z[k], false) for m keys: b[k], j[k] (no tree)
+    std::vector<SampWin> bw_, rw_;
+    std::vector<uint64_t> blo_, bhi_, rlo_, rhi_;
+    void view_lt_batch(const uint8_t *const *z, size_t m, uint64_t *b, uint64_t *j) {
+        bw_.resize(m), rw_.resize(m), blo_.resize(m), bhi_.resize(m), rlo_.resize(m), rhi_.resize(m);
+        const bool run_on = has_run();
+        for (size_t k = 0; k < m; k++) {
+            const uint64_t d = digit(z[k]);
+            if (nb) bw_[k] = samp_windows(samp, ns, samp2, ns2, d);
+            if (run_on) rw_[k] = samp_windows(run.samp, run.ns, run.samp2, run.ns2, d);
+        }
+        for (size_t k = 0; k < m; k++) {
+            if (nb) key_window(keys, nb, samp, bw_[k], &blo_[k], &bhi_[k]);
+            if (run_on) key_window(run.keys, run.n, run.samp, rw_[k], &rlo_[k], &rhi_[k]);
+        }
+        for (size_t k = 0; k < m; k++) {
+            b[k] = nb ? key_search(keys, blo_[k], bhi_[k], z[k]) : 0;
+            j[k] = run_on ? key_search(run.keys, rlo_[k], rhi_[k], z[k]) : 0;
+        }
+    }
+    // view_at for m ranks (each < nv): their places and keys
+    std::vector<uint64_t> alo_, ahi_;
+    void view_at_batch(const uint64_t *v, size_t m, uint64_t *b, uint64_t *j, const uint8_t **key) {
+        if (!has_run() || !run.gsamp) {
+            for (size_t k = 0; k < m; k++) key[k] = view_at(v[k], b[k], j[k]);
+            return;
+        }
+        alo_.resize(m), ahi_.resize(m);
+        for (size_t k = 0; k < m; k++) {  // the first sampled entry with G > v: its window's entries requested
+            uint64_t q;
+            if (!gsamp2_own.empty()) {
+                const uint64_t *g2 = gsamp2_own.data();
+                const uint64_t i = std::upper_bound(g2, g2 + gsamp2_own.size(), v[k]) - g2;
+                const uint64_t l2 = i ? ((i - 1) << SHIFT) + 1 : 0, h2 = std::min<uint64_t>(run.ns, i << SHIFT);
+                q = l2 >= h2 ? h2 : std::upper_bound(run.gsamp + l2, run.gsamp + h2, v[k]) - run.gsamp;
+            } else {
+                q = std::upper_bound(run.gsamp, run.gsamp + run.ns, v[k]) - run.gsamp;
+            }
+            alo_[k] = q ? ((q - 1) << SHIFT) + 1 : 0;
+            ahi_[k] = std::min<uint64_t>(run.n, q << SHIFT);
+            const uint64_t lo = alo_[k] ? alo_[k] - 1 : 0, cnt = ahi_[k] - lo + 1;
+            prefetch_span(run.brank + lo, cnt * 4);
+            prefetch_span(run.cntp + lo, cnt * 4);
+            prefetch_span(run.flags + lo, cnt);
+        }
+        for (size_t k = 0; k < m; k++) {
+            uint64_t lo = alo_[k], hi = ahi_[k];
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (run_below(mid) + (run_live(mid) ? 1 : 0) > v[k]) hi = mid;
+                else lo = mid + 1;
+            }
+            j[k] = lo;
+            if (lo < run.n && run_below(lo) == v[k] && run_live(lo)) {
+                b[k] = run.brank[lo];
+                key[k] = run.keys + lo * kl;
+            } else {
+                const uint64_t gprev = lo ? run_below(lo - 1) + (run_live(lo - 1) ? 1 : 0) : 0;
+                const uint64_t b0 = lo ? run.brank[lo - 1] + (run_in_base(lo - 1) ? 1 : 0) : 0;
+                b[k] = b0 + (v[k] - gprev);
+                key[k] = keys + b[k] * kl;
+            }
+            __builtin_prefetch(key[k]);
+        }
+    }
+    // the prefix sums' lines of places (b, j), requested
+    void prefetch_pre(uint64_t b, uint64_t j) const {
+        __builtin_prefetch(prefix + 4 * b);
+        if (has_run()) __builtin_prefetch(run.prefix + 4 * j);
+    }
+
     // forget everything (tier off)
     void reset() {
         build(0, RH_KEY_BYTES, 0, nullptr, nullptr);
@@ -462,7 +566,12 @@ struct HostTier {
         rh_aggregate loc;
     };
     std::vector<Seg> segs;
+    bool batch = true;  // rounds over base + run copy with the batched searches (false: key by key)
+    std::vector<const uint8_t *> bq_;
+    std::vector<uint64_t> bb_, bj_, cut_r_, cut_b_, cut_j_;
+    std::vector<const uint8_t *> cut_k_;
     void round(int sqrt_policy, uint64_t b, const rh_segments &in, std::vector<uint8_t> &out, uint64_t hdr[5]) {
+        if (batch && plain() && keys && in.n > 1) return round_batched(sqrt_policy, b, in, out, hdr);
         const size_t r = in.n;
         const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
         const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
@@ -517,6 +626,97 @@ struct HostTier {
                 Cur lo = g.cs;
                 for (uint64_t k = 0; k <= ncuts; k++) {
                     const Cur hi = k == ncuts ? g.ce : at(g.cs.r + (k + 1) * g.stride);
+                    rh_aggregate a;
+                    agg(lo, hi, &a);
+                    child(k ? 1 : sk[j], k ? lo.k : s0, k != ncuts ? 1 : ek[j], k != ncuts ? hi.k : e0, a);
+                    lo = hi;
+                }
+            }
+        }
+    }
+    // round() with no tree: the segments' bounds, their sums and the SPLIT cuts each as one batch
+    // of searches (view_lt_batch, view_at_batch), the prefix lines requested before they are read.
+    // The same answers as the key-by-key path (tests/host_tier_check.cpp compares the two).
+    void round_batched(int sqrt_policy, uint64_t b, const rh_segments &in, std::vector<uint8_t> &out, uint64_t hdr[5]) {
+        const size_t r = in.n;
+        const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
+        const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
+        const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
+        segs.resize(r);
+        bq_.clear();
+        for (size_t j = 0; j < r; j++) {
+            if (sk[j]) bq_.push_back(skeys + j * kl);
+            if (ek[j]) bq_.push_back(ekeys + j * kl);
+        }
+        const size_t q = bq_.size();
+        bb_.resize(q), bj_.resize(q);
+        view_lt_batch(bq_.data(), q, bb_.data(), bj_.data());
+        for (size_t k = 0; k < q; k++) prefetch_pre(bb_[k], bj_[k]);
+        uint64_t nc = 0, ne = 0, cnt[5] = {0, 0, 0, 0, 0};
+        size_t qi = 0;
+        cut_r_.clear();
+        for (size_t j = 0; j < r; j++) {
+            Seg &g = segs[j];
+            Cur cs = begin(), ce = end();
+            if (sk[j]) cs.b = bb_[qi], cs.j = bj_[qi], cs.r = view_rank(cs.b, cs.j), cs.d = 0, qi++;
+            if (ek[j]) ce.b = bb_[qi], ce.j = bj_[qi], ce.r = view_rank(ce.b, ce.j), ce.d = 0, qi++;
+            g = Seg{3, 0, 0, 0, cs, ce, {}};
+            agg(g.cs, g.ce, &g.loc);
+            const SegDecision d = decide_segment(g.cs.r, g.ce.r, g.loc, in.aggregates[j], sqrt_policy, b);
+            g.kind = d.kind, g.stride = d.stride, g.children = d.children, g.enums = d.enums;
+            cnt[g.kind == 3 ? 4 : g.kind]++;
+            nc += g.children;
+            ne += g.enums;
+            if (g.kind == 2 && g.children > 1)
+                for (uint64_t k = 0; k + 1 < g.children; k++) cut_r_.push_back(g.cs.r + (k + 1) * g.stride);
+        }
+        const size_t nq = cut_r_.size();
+        cut_b_.resize(nq), cut_j_.resize(nq), cut_k_.resize(nq);
+        view_at_batch(cut_r_.data(), nq, cut_b_.data(), cut_j_.data(), cut_k_.data());
+        for (size_t k = 0; k < nq; k++) prefetch_pre(cut_b_[k], cut_j_[k]);
+        hdr[0] = cnt[0], hdr[1] = ne, hdr[2] = cnt[2], hdr[3] = nc, hdr[4] = cnt[4];
+        const RoundLayout L = round_layout(nc, ne, kl);
+        out.resize(L.end);
+        uint8_t *o = out.data();
+        memcpy(o, hdr, 40);
+        uint64_t c = 0, e = 0;
+        auto put_key = [&](uint64_t off, const uint8_t *k) {
+            if (k) memcpy(o + off, k, kl);
+            else memset(o + off, 0, kl);
+        };
+        auto child = [&](uint8_t skd, const uint8_t *skey, uint8_t ekd, const uint8_t *ekey, const rh_aggregate &a) {
+            o[L.csk + c] = skd;
+            o[L.cek + c] = ekd;
+            put_key(L.cskeys + c * kl, skd ? skey : nullptr);
+            put_key(L.cekeys + c * kl, ekd ? ekey : nullptr);
+            memcpy(o + L.caggs + 40 * c, &a, 40);
+            c++;
+        };
+        const rh_aggregate zero{{0, 0, 0, 0}, 0};
+        size_t ci = 0;
+        for (size_t j = 0; j < r; j++) {
+            const Seg &g = segs[j];
+            const uint8_t *s0 = sk[j] ? skeys + j * kl : nullptr, *e0 = ek[j] ? ekeys + j * kl : nullptr;
+            if (g.kind == 1) {
+                o[L.esk + e] = sk[j];
+                o[L.eek + e] = ek[j];
+                put_key(L.eskeys + e * kl, s0);
+                put_key(L.eekeys + e * kl, e0);
+                e++;
+                if (g.children) child(sk[j], s0, ek[j], e0, zero);
+            } else if (g.kind == 2) {
+                const uint64_t ncuts = g.children - 1;
+                if (ncuts == 0) {
+                    child(sk[j], s0, ek[j], e0, g.loc);
+                    continue;
+                }
+                Cur lo = g.cs;
+                for (uint64_t k = 0; k <= ncuts; k++) {
+                    Cur hi = g.ce;
+                    if (k != ncuts) {
+                        hi.r = cut_r_[ci], hi.b = cut_b_[ci], hi.j = cut_j_[ci], hi.k = cut_k_[ci], hi.d = 0;
+                        ci++;
+                    }
                     rh_aggregate a;
                     agg(lo, hi, &a);
                     child(k ? 1 : sk[j], k ? lo.k : s0, k != ncuts ? 1 : ek[j], k != ncuts ? hi.k : e0, a);

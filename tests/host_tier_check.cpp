@@ -283,6 +283,18 @@ int main(int argc, char **argv) {
             A.round(policy, 16, in, oa, ha);
             B.round(policy, 16, in, ob, hb);
             EXPECT(oa == ob && !memcmp(ha, hb, sizeof ha), "round policy %d (%zu segments)", policy, r);
+            // the batched searches (HostTier::round_batched, taken with no tree) against key by key
+            for (HostTier *T : {&A, &B}) {
+                std::vector<uint8_t> o1, o2;
+                uint64_t h1[5], h2[5];
+                T->batch = true;
+                T->round(policy, 16, in, o1, h1);
+                T->batch = false;
+                T->round(policy, 16, in, o2, h2);
+                T->batch = true;
+                EXPECT(o1 == o2 && !memcmp(h1, h2, sizeof h1), "batched round policy %d (%zu segments, %s)", policy, r,
+                       T == &A ? "folded" : "rebuilt");
+            }
             checked++;
         }
         if (failures) break;

@@ -570,8 +570,9 @@ struct HostTier {
     std::vector<const uint8_t *> bq_;
     std::vector<uint64_t> bb_, bj_, cut_r_, cut_b_, cut_j_;
     std::vector<const uint8_t *> cut_k_;
+    std::vector<Cur> cuts_;
     void round(int sqrt_policy, uint64_t b, const rh_segments &in, std::vector<uint8_t> &out, uint64_t hdr[5]) {
-        if (batch && plain() && keys && in.n > 1) return round_batched(sqrt_policy, b, in, out, hdr);
+        if (batch && keys && in.n > 1) return round_batched(sqrt_policy, b, in, out, hdr);
         const size_t r = in.n;
         const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
         const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
@@ -634,9 +635,10 @@ struct HostTier {
             }
         }
     }
-    // round() with no tree: the segments' bounds, their sums and the SPLIT cuts each as one batch
-    // of searches (view_lt_batch, view_at_batch), the prefix lines requested before they are read.
-    // The same answers as the key-by-key path (tests/host_tier_check.cpp compares the two).
+    // round() with the segments' bounds, their sums and (with no tree) the SPLIT cuts each as one
+    // batch of searches (view_lt_batch, view_at_batch), the prefix lines requested before they are
+    // read; a tree adds its own (cached) search per bound and keeps select key by key.  The same
+    // answers as the key-by-key path (tests/host_tier_check.cpp compares the two).
     void round_batched(int sqrt_policy, uint64_t b, const rh_segments &in, std::vector<uint8_t> &out, uint64_t hdr[5]) {
         const size_t r = in.n;
         const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
@@ -655,11 +657,20 @@ struct HostTier {
         uint64_t nc = 0, ne = 0, cnt[5] = {0, 0, 0, 0, 0};
         size_t qi = 0;
         cut_r_.clear();
+        const bool tree = !plain();
+        auto bound_place = [&](Cur &c) {  // lt(key) from its view place (+ the tree's entries below it)
+            c.r = view_rank(c.b, c.j), c.d = 0, c.k = nullptr;
+            if (tree) {
+                const DeltaTree::Pos p = dt.lt(bq_[qi]);
+                c.d = p.idx;
+                c.r = (uint64_t)((int64_t)c.r + p.cnt);
+            }
+        };
         for (size_t j = 0; j < r; j++) {
             Seg &g = segs[j];
             Cur cs = begin(), ce = end();
-            if (sk[j]) cs.b = bb_[qi], cs.j = bj_[qi], cs.r = view_rank(cs.b, cs.j), cs.d = 0, qi++;
-            if (ek[j]) ce.b = bb_[qi], ce.j = bj_[qi], ce.r = view_rank(ce.b, ce.j), ce.d = 0, qi++;
+            if (sk[j]) cs.b = bb_[qi], cs.j = bj_[qi], bound_place(cs), qi++;
+            if (ek[j]) ce.b = bb_[qi], ce.j = bj_[qi], bound_place(ce), qi++;
             g = Seg{3, 0, 0, 0, cs, ce, {}};
             agg(g.cs, g.ce, &g.loc);
             const SegDecision d = decide_segment(g.cs.r, g.ce.r, g.loc, in.aggregates[j], sqrt_policy, b);
@@ -671,9 +682,17 @@ struct HostTier {
                 for (uint64_t k = 0; k + 1 < g.children; k++) cut_r_.push_back(g.cs.r + (k + 1) * g.stride);
         }
         const size_t nq = cut_r_.size();
-        cut_b_.resize(nq), cut_j_.resize(nq), cut_k_.resize(nq);
-        view_at_batch(cut_r_.data(), nq, cut_b_.data(), cut_j_.data(), cut_k_.data());
-        for (size_t k = 0; k < nq; k++) prefetch_pre(cut_b_[k], cut_j_[k]);
+        cuts_.resize(nq);
+        if (!tree) {
+            cut_b_.resize(nq), cut_j_.resize(nq), cut_k_.resize(nq);
+            view_at_batch(cut_r_.data(), nq, cut_b_.data(), cut_j_.data(), cut_k_.data());
+            for (size_t k = 0; k < nq; k++) {
+                cuts_[k] = Cur{cut_r_[k], cut_b_[k], 0, cut_k_[k], cut_j_[k]};
+                prefetch_pre(cut_b_[k], cut_j_[k]);
+            }
+        } else {
+            for (size_t k = 0; k < nq; k++) cuts_[k] = at(cut_r_[k]);
+        }
         hdr[0] = cnt[0], hdr[1] = ne, hdr[2] = cnt[2], hdr[3] = nc, hdr[4] = cnt[4];
         const RoundLayout L = round_layout(nc, ne, kl);
         out.resize(L.end);
@@ -712,11 +731,7 @@ struct HostTier {
                 }
                 Cur lo = g.cs;
                 for (uint64_t k = 0; k <= ncuts; k++) {
-                    Cur hi = g.ce;
-                    if (k != ncuts) {
-                        hi.r = cut_r_[ci], hi.b = cut_b_[ci], hi.j = cut_j_[ci], hi.k = cut_k_[ci], hi.d = 0;
-                        ci++;
-                    }
+                    const Cur hi = k == ncuts ? g.ce : cuts_[ci++];
                     rh_aggregate a;
                     agg(lo, hi, &a);
                     child(k ? 1 : sk[j], k ? lo.k : s0, k != ncuts ? 1 : ek[j], k != ncuts ? hi.k : e0, a);

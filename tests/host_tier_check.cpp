@@ -283,7 +283,7 @@ int main(int argc, char **argv) {
             A.round(policy, 16, in, oa, ha);
             B.round(policy, 16, in, ob, hb);
             EXPECT(oa == ob && !memcmp(ha, hb, sizeof ha), "round policy %d (%zu segments)", policy, r);
-            // the batched searches (HostTier::round_batched, taken with no tree) against key by key
+            // the batched searches (HostTier::round_batched; A holds a tree, B none) against key by key
             for (HostTier *T : {&A, &B}) {
                 std::vector<uint8_t> o1, o2;
                 uint64_t h1[5], h2[5];

@@ -188,6 +188,10 @@ struct DevBuf {
     // realloc per batch cost ~0.6 ms of idle GPU per config5 batch.
     int ensure(size_t n) {
         if (n <= cap && p) return RH_OK;
+        static const bool dbg = getenv("RSOS_HIP_ALLOC_DBG") != nullptr;  // every reallocation, to stderr
+        if (dbg && p)
+            fprintf(stderr, "rsos_hip: DevBuf<%zu B> %p grows %zu -> %zu elements (caller %p)\n", sizeof(T), (void *)this,
+                    cap, n, __builtin_return_address(0));
         if (p) (void)hipFree(p);
         p = nullptr;
         const size_t grown = cap + cap / 2;
@@ -1158,11 +1162,15 @@ struct rh_store {
             RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
             RH_HIP(hipEventCreateWithFlags(&rf_kdone, hipEventDisableTiming));
         }
-        const uint64_t n = nb, nbk = rh_num_blocks(n), ns = rh_num_superblocks(n), nsmp = (n + 63) / 64,
-                       nsmp2 = (n + 4095) / 4096;  // the samples' index (host_tier.hpp samp2)
-        if ((rc = tier_dpre.ensure((n + 1) * 32 + 64)) || (rc = tier_spre.ensure((ns + 1) * 32 + 64)) ||
-            (rc = tier_bpre.ensure((nbk + 1) * 32 + 64)) || (rc = tier_dsmp.ensure(nsmp + nsmp2 + 8)))
-            return rc;
+        const uint64_t n = nb, nsmp = (n + 63) / 64, nsmp2 = (n + 4095) / 4096;  // samp2: host_tier.hpp
+        {  // sized for the base buffer's capacity: a base grown by compactions reallocates nothing
+           // here (a hipFree waits for every copy in flight, the other store's too)
+            const uint64_t c = std::max<uint64_t>(n, base_cap_rows()), cbk = rh_num_blocks(c),
+                           cs = rh_num_superblocks(c);
+            if ((rc = tier_dpre.ensure((c + 1) * 32 + 64)) || (rc = tier_spre.ensure((cs + 1) * 32 + 64)) ||
+                (rc = tier_bpre.ensure((cbk + 1) * 32 + 64)) || (rc = tier_dsmp.ensure((c + 63) / 64 + (c + 4095) / 4096 + 8)))
+                return rc;
+        }
         const int spare = 1 - tact;
         TierSet &S = tsets[spare];
         try {  // headroom, once the set must grow anyway: a growing map re-pins rarely
@@ -1381,14 +1389,22 @@ struct rh_store {
         const uint64_t n1 = nd;
         if (trun_ver == version && trun_gs.p) return RH_OK;
         trun_ver = ~0ull;
-        const uint64_t nbk = rh_num_blocks(n1), nsb = rh_num_superblocks(n1), ns = (n1 + 63) / 64;
-        if ((rc = trun_c.ensure(n1 * 32 + 64)) || (rc = trun_cnt.ensure(n1 + 16)) || (rc = trun_fl.ensure(n1 + 16)) ||
-            (rc = trun_br.ensure(n1 + 16)) || (rc = trun_bs.ensure(nbk * 32 + 32)) || (rc = trun_ss.ensure(nsb * 32 + 32)) ||
-            (rc = trun_cntp.ensure(n1 + 16)) || (rc = trun_gs.ensure(ns + 8)))
-            return rc;
-        if ((rc = trun_spre.ensure((nsb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((nbk + 1) * 32 + 64)) ||
-            (rc = trun_pre.ensure((n1 + 1) * 32 + 64)))
-            return rc;
+        // sized for the longest run the delta run's buffers are planned for (compaction threshold +
+        // a batch), not this one: a run growing batch by batch would otherwise reallocate here, and
+        // the hipFree waits for everything in flight -- a background refresh copy included (no-wait
+        // drives of 40-175 ms, profiles/r05f_interleave.jsonl)
+        const uint64_t nc = std::max<uint64_t>(n1, dslot[cd].cap > 16 ? dslot[cd].cap - 16 : 0);
+        const uint64_t nbk = rh_num_blocks(n1);
+        {
+            const uint64_t cbk = rh_num_blocks(nc), csb = rh_num_superblocks(nc), cs = (nc + 63) / 64;
+            if ((rc = trun_c.ensure(nc * 32 + 64)) || (rc = trun_cnt.ensure(nc + 16)) || (rc = trun_fl.ensure(nc + 16)) ||
+                (rc = trun_br.ensure(nc + 16)) || (rc = trun_bs.ensure(cbk * 32 + 32)) ||
+                (rc = trun_ss.ensure(csb * 32 + 32)) || (rc = trun_cntp.ensure(nc + 16)) || (rc = trun_gs.ensure(cs + 8)))
+                return rc;
+            if ((rc = trun_spre.ensure((csb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((cbk + 1) * 32 + 64)) ||
+                (rc = trun_pre.ensure((nc + 1) * 32 + 64)))
+                return rc;
+        }
         if (n1 <= rh::RUNCOL_SMALL && run_cols_fused) {  // a short run: every column in one launch
             const rh::RunCols o{trun_c.p,  trun_cnt.p,  trun_fl.p,   trun_br.p,   trun_pre.p, trun_bs.p,
                                 trun_ss.p, trun_spre.p, trun_bpre.p, trun_cntp.p, trun_gs.p};
@@ -1958,7 +1974,7 @@ struct rh_store {
             (rc = dheap.ensure(plan * sizeof(rh::DeltaRec) + 64)) || (rc = dops.ensure(batch + 64)) ||
             (rc = mcnt.ensure(8)) || (rc = results.ensure(12)) || (rc = flag.ensure(4)) || (rc = counts.ensure(4)))
             return rc;
-        RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch));
+        RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch, base));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         tier_host_oom = false;
         // the tier's page-locked room: a failure leaves the tier stale, not the device reservation failed
@@ -2366,10 +2382,16 @@ struct rh_store {
     }
     uint64_t epoch_questions = 0;  // device questions over the current base so far
     bool base_loaded = true;       // the current base came from a load (false: a compaction)
+    // the rows either base buffer holds (a compaction switches between them; they grow separately)
+    uint64_t base_cap_rows() const { return std::max(bfps[0].cap, bfps[1].cap) / 32; }
     int ensure_base_prefix() {
         int rc;
         if (bpre_epoch != base_epoch || !bpre_b.p) {
-            const uint64_t nbk = rh_num_blocks(nb), ns = rh_num_superblocks(nb);
+            // sized for the base buffer's capacity (a reserved store's base grows by compactions
+            // without reallocating; a hipFree here would wait for a tier copy in flight: no-wait
+            // drives of ~175 ms, profiles/r05_nowait_long_calls.txt)
+            const uint64_t cap_rows = std::max<uint64_t>(nb, base_cap_rows());
+            const uint64_t nbk = rh_num_blocks(cap_rows), ns = rh_num_superblocks(cap_rows);
             if (pre_pending) RH_HIP(hipStreamWaitEvent(stream, pre_ev, 0));  // it reads bpre_b
             if ((rc = bpre_b.ensure((nbk + 1) * 32 + 64)) || (rc = spre_b.ensure((ns + 1) * 32 + 64))) return rc;
             pre_b_ok = false;
@@ -2381,7 +2403,7 @@ struct rh_store {
             // hipMalloc is tens of ms: not inside a later drive), reallocated only when the base
             // buffer was (no extra device-draining hipFree)
             if (row_prefix && nb && pre_b.cap < (nb + 1) * 32 + 64) {
-                const size_t need = (std::max<size_t>(nb, bfps[cb].cap / 32) + 1) * 32 + 64;
+                const size_t need = (std::max<size_t>(nb, base_cap_rows()) + 1) * 32 + 64;
                 if ((rc = drain_prefix_build())) return rc;
                 pre_b.release();
                 size_t free_b = 0, total_b = 0;  // room for it, with 1 GiB to spare, or go without

@@ -2002,7 +2002,7 @@ hipError_t launch_search_table(const uint64_t *smp2, uint64_t n, uint32_t *tab, 
     return hipGetLastError();
 }
 
-hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch) {
+hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch, uint64_t base_rows) {
     // the slots the compaction (plan rows) and a batch (batch rows) take
     (void)s.u32(3, plan + 1), (void)s.u32(4, plan + 1), (void)s.u32(5, plan + 1);
     (void)s.u32(14, plan), (void)s.u8(4, plan);
@@ -2010,6 +2010,9 @@ hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch) {
     (void)s.u32(13, G * DB_PARTS), (void)s.u32(6, 2 * G), (void)s.u64(7, 4 * G);
     (void)s.u32(9, batch), (void)s.u32(10, batch), (void)s.u8(2, batch), (void)s.u8(3, batch);
     (void)s.i32(0, batch);  // the bucket sort's slot -> sorted row
+    // merge_tile_bounds' tiles over a compaction's output (the base grows with every compaction:
+    // a slot grown then frees the old one, and hipFree waits for every copy in flight)
+    (void)s.u32(8, (std::max(base_rows, plan) + MT - 1) / MT + 1);
     return s.err;
 }
 

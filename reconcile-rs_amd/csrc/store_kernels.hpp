@@ -305,7 +305,8 @@ constexpr uint64_t RUNCOL_SMALL = 4095;
 hipError_t launch_run_columns_small(const uint32_t *slot, const uint8_t *heap, uint64_t n, const RunCols &o,
                                     hipStream_t st);
 // pre-size the scratch slots a compaction of up to `plan` delta rows and a batch of `batch` rows use
-hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch);
+// base_rows: the largest base a compaction writes (its merge tiles' bounds)
+hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch, uint64_t base_rows = 0);
 hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, Scratch &s, hipStream_t st);
 
 // nullptr if the store does not support this key type

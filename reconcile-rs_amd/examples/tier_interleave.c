@@ -288,15 +288,23 @@ int main(int argc, char **argv) {
         }
         HCHECK(hipDeviceSynchronize());
         t0 = now_s();
+        const double tws = t0;
         CHECK(rh_store_apply_device(a, &dc, NULL, m, NULL, NULL, NULL, NULL));
         CHECK(rh_store_apply_device(b, &dc, NULL, m, NULL, NULL, NULL, NULL));
         const double w = now_s() - t0;
         t0 = now_s();
+        const double tds = t0;
         c = reconcile(a, b, &sc);
         const double d = now_s() - t0;
         if (r >= 0) {
             tw[r] = w, td[r] = d;
             wsum += w, dsum += d;
+            if (getenv("TIER_INTERLEAVE_CYCLES")) {  /* one line per cycle (stderr) */
+                uint64_t rf = 0, fo = 0;
+                CHECK(rh_store_tier_stats(a, NULL, NULL, &rf, &fo));
+                fprintf(stderr, "cycle %d: write %.1f us, drive %.1f us, refreshes %llu, folds %llu (write at %.3f ms, drive at %.3f ms, monotonic)\n",
+                        r, w * 1e6, d * 1e6, (unsigned long long)rf, (unsigned long long)fo, tws * 1e3, tds * 1e3);
+            }
         }
         for (int k = 0; r >= 0 && k < small; k++) {  /* one staged row into both, then a drive */
             make_row(n + next, 1, one.keys, one.vals, DATED ? one.phys : NULL, DATED ? one.logical : NULL,

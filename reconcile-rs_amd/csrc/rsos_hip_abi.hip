@@ -1142,6 +1142,17 @@ struct rh_store {
             if (d[k].bytes) RH_HIP(hipMemcpyAsync(d[k].host, d[k].dev, d[k].bytes, hipMemcpyDeviceToHost, st));
         return RH_OK;
     }
+    // A refresh's device buffers, sized for the base buffers' capacity (reserve() calls it too): a
+    // base grown by compactions reallocates nothing here -- a hipFree waits for every copy in
+    // flight, the other store's too (no-wait drives of 40-175 ms before, profiles/r05_nowait_cycles.txt)
+    int refresh_room() {
+        int rc;
+        const uint64_t c = std::max<uint64_t>(nb, base_cap_rows()), cbk = rh_num_blocks(c), cs = rh_num_superblocks(c);
+        if ((rc = tier_dpre.ensure((c + 1) * 32 + 64)) || (rc = tier_spre.ensure((cs + 1) * 32 + 64)) ||
+            (rc = tier_bpre.ensure((cbk + 1) * 32 + 64)) || (rc = tier_dsmp.ensure((c + 63) / 64 + (c + 4095) / 4096 + 8)))
+            return rc;
+        return RH_OK;
+    }
     // Start a refresh of the host tier: compact, the prefix sums and samples on the device, and
     // their copy down on the copy stream into the spare set.  Returns at once (no wait).
     int start_refresh() {
@@ -1163,14 +1174,7 @@ struct rh_store {
             RH_HIP(hipEventCreateWithFlags(&rf_kdone, hipEventDisableTiming));
         }
         const uint64_t n = nb, nsmp = (n + 63) / 64, nsmp2 = (n + 4095) / 4096;  // samp2: host_tier.hpp
-        {  // sized for the base buffer's capacity: a base grown by compactions reallocates nothing
-           // here (a hipFree waits for every copy in flight, the other store's too)
-            const uint64_t c = std::max<uint64_t>(n, base_cap_rows()), cbk = rh_num_blocks(c),
-                           cs = rh_num_superblocks(c);
-            if ((rc = tier_dpre.ensure((c + 1) * 32 + 64)) || (rc = tier_spre.ensure((cs + 1) * 32 + 64)) ||
-                (rc = tier_bpre.ensure((cbk + 1) * 32 + 64)) || (rc = tier_dsmp.ensure((c + 63) / 64 + (c + 4095) / 4096 + 8)))
-                return rc;
-        }
+        if ((rc = refresh_room())) return rc;
         const int spare = 1 - tact;
         TierSet &S = tsets[spare];
         try {  // headroom, once the set must grow anyway: a growing map re-pins rarely
@@ -1437,7 +1441,9 @@ struct rh_store {
         const uint64_t ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096, nbk = rh_num_blocks(n1),
                        nsb = rh_num_superblocks(n1);
         // the contributions' row prefix: the host walks it (HostTier::Run::prefix)
-        if ((rc = run_row_prefix()) || (rc = trun_smp.ensure(ns + ns2 + 8))) return rc;
+        // (sized like run_columns' buffers: for the longest run planned)
+        const uint64_t nc = std::max<uint64_t>(n1, dslot[cd].cap > 16 ? dslot[cd].cap - 16 : 0);
+        if ((rc = run_row_prefix()) || (rc = trun_smp.ensure((nc + 63) / 64 + (nc + 4095) / 4096 + 8))) return rc;
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
         try {
@@ -1976,6 +1982,7 @@ struct rh_store {
             return rc;
         RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch, base));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
+        if (tier_on && (rc = refresh_room())) return rc;
         tier_host_oom = false;
         // the tier's page-locked room: a failure leaves the tier stale, not the device reservation failed
         if ((rc = tier_stale_on_host_oom(tier_reserve(rows)))) return rc;

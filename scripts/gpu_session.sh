@@ -139,6 +139,8 @@ for step in "$@"; do
     nowait_cycles)  # per-cycle write / drive times, and the HIP calls of the same run
         run nowait_cycles 400 env RSOS_HIP_TIER_SYNC=0 TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d "$O/nwc" -o tr -- $EX/tier_interleave 100000000 1000000 12 1 c5 2 3
         python3 scripts/long_calls.py "$O/nwc" 5000 > "$O/${TAG}_nowait_long_calls.txt" 2>&1 || true ;;
+    sync_cycles) run sync_cycles 400 env TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 $EX/tier_interleave 100000000 1000000 20 1 c5 2 ;;
+    off_cycles) run off_cycles 400 env TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 $EX/tier_interleave 100000000 1000000 12 0 c5 2 3 ;;
     trace_config5)
         run trace_config5 300 rocprofv3 --kernel-trace --output-format csv -d "$O/c5t" -o c5 -- python3 bench.py --config config5 --steps 40 --cpu-baseline 0
         f=$(find "$O/c5t" -name 'c5_kernel_trace.csv' | head -n 1)

@@ -1163,16 +1163,7 @@ struct rh_store {
             return RH_OK;
         }
         if ((rc = compact())) return rc;
-        if (!cstream) {
-            // the copies on a plain stream (the copy engines); the scans and samples, and kernel
-            // copies, on a CU-masked one (create_back_stream): a copy issued on a CU-masked stream
-            // held the next write's uploads behind it (write p50 7 -> 100 ms, 10^8 rows)
-            RH_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-            RH_HIP(create_back_stream(&kstream, device));
-            RH_HIP(hipEventCreateWithFlags(&rf_ready, hipEventDisableTiming));
-            RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
-            RH_HIP(hipEventCreateWithFlags(&rf_kdone, hipEventDisableTiming));
-        }
+        if ((rc = refresh_streams())) return rc;
         const uint64_t n = nb, nsmp = (n + 63) / 64, nsmp2 = (n + 4095) / 4096;  // samp2: host_tier.hpp
         if ((rc = refresh_room())) return rc;
         const int spare = 1 - tact;
@@ -1232,6 +1223,19 @@ struct rh_store {
     // The copy has landed: the new set becomes the tier's, the logged batches folded into its tree.
     void finish_refresh() {
         rf_on = false;
+        if (rf_run) {  // a run copy: the tier takes it if nothing was written since it started
+            rf_run = false;
+            if (rf_version == version && rf_epoch == tier_epoch) {
+                ract = 1 - ract;
+                tier.set_run(trh[ract].run(rf_run_n));
+                tier_version = version;
+                tier_runs++;
+                tier_refreshes++;
+            } else {
+                refresh_wanted = true;
+            }
+            return;
+        }
         if (!(rf_log_ok && rf_log_version == version) && tier_fresh()) {
             // the copy cannot be brought up to date but the tier still is (a tree past its limit):
             // keep the tier, drop the copy, and let the next write start another
@@ -1341,7 +1345,7 @@ struct rh_store {
             if (tier_fresh() && tier.dt.size() > tree_limit() && run_ok) return tier_run_snapshot();  // the tree full
         }
         if (rf_on) return RH_OK;
-        if (!tier_fresh() || refresh_wanted || tier.dt.size() > tree_limit()) return start_refresh();
+        if (!tier_fresh() || refresh_wanted || tier.dt.size() > tree_limit()) return refresh_now();
         return RH_OK;
     }
     // A question to a stale tier with no copy in flight starts one only when that costs the
@@ -1359,9 +1363,42 @@ struct rh_store {
     DevBuf<uint8_t> trun_c, trun_fl, trun_bs, trun_ss, trun_spre, trun_bpre, trun_pre;
     DevBuf<uint32_t> trun_cnt, trun_cntp, trun_br;
     DevBuf<uint64_t> trun_smp, trun_gs;
-    PinnedVec<uint8_t> trh_keys, trh_fl;
-    PinnedVec<uint64_t> trh_pre, trh_smp, trh_gs;
-    PinnedVec<uint32_t> trh_cntp, trh_br;
+    struct RunHost {  // a run copy's page-locked columns
+        PinnedVec<uint8_t> keys, fl;
+        PinnedVec<uint64_t> pre, smp, gs;
+        PinnedVec<uint32_t> cntp, br;
+        void release() { keys.release(), fl.release(), pre.release(), smp.release(), gs.release(), cntp.release(), br.release(); }
+        // room for a run of n1 entries (headroom: the run grows batch by batch)
+        void fit(uint64_t n1, uint32_t kl) {
+            auto f = [](auto &v, size_t want) {
+                if (v.capacity() < want) {
+                    v.clear();
+                    v.reserve(want + want / 2);
+                }
+                v.resize(want);
+            };
+            const uint64_t ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096;
+            f(keys, n1 * kl + 64), f(pre, (n1 + 1) * 4 + 8), f(cntp, n1 + 16), f(fl, n1 + 16), f(br, n1 + 16);
+            f(smp, ns + ns2 + 8), f(gs, ns + 8);
+        }
+        rh::HostTier::Run run(uint64_t n1) {
+            rh::HostTier::Run r;
+            r.n = n1;
+            r.keys = keys.data();
+            r.prefix = pre.data();
+            r.cntp = reinterpret_cast<const int32_t *>(cntp.data());
+            r.flags = fl.data();
+            r.brank = br.data();
+            r.samp = smp.data();
+            r.samp2 = smp.data() + (n1 + 63) / 64;
+            r.gsamp = gs.data();
+            return r;
+        }
+    };
+    // trh[ract]: the run copy the tier reads; trh[1 - ract]: the one a no-wait run refresh fills
+    RunHost trh[2];
+    int ract = 0;
+    DevBuf<uint8_t> trun_keys;  // the run's keys staged for a no-wait run copy (batches rewrite dkeys)
     uint64_t tier_runs = 0;
     bool snap_ok = false;  // set before a batch: a run copy may replace the refresh it causes
     // with a run copy held, batches fold into the tree as deltas against base + run (mode 2: a
@@ -1382,6 +1419,7 @@ struct rh_store {
         int rc;
         if ((rc = run_columns())) return rc;
         if (trun_pre_ver == version) return RH_OK;
+        if ((rc = guard_run_copy())) return rc;
         RH_HIP(rh::launch_row_prefix(trun_c.p, nd, trun_bpre.p, trun_pre.p, stream));
         trun_pre_ver = version;
         return RH_OK;
@@ -1392,6 +1430,7 @@ struct rh_store {
         int rc;
         const uint64_t n1 = nd;
         if (trun_ver == version && trun_gs.p) return RH_OK;
+        if ((rc = guard_run_copy())) return rc;  // a no-wait run copy may still read the columns
         trun_ver = ~0ull;
         // sized for the longest run the delta run's buffers are planned for (compaction threshold +
         // a batch), not this one: a run growing batch by batch would otherwise reallocate here, and
@@ -1438,63 +1477,108 @@ struct rh_store {
             tier_version = version;
             return RH_OK;
         }
-        const uint64_t ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096, nbk = rh_num_blocks(n1),
-                       nsb = rh_num_superblocks(n1);
+        const uint64_t ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096;
         // the contributions' row prefix: the host walks it (HostTier::Run::prefix)
-        // (sized like run_columns' buffers: for the longest run planned)
+        // (the samples sized like run_columns' buffers: for the longest run planned)
         const uint64_t nc = std::max<uint64_t>(n1, dslot[cd].cap > 16 ? dslot[cd].cap - 16 : 0);
         if ((rc = run_row_prefix()) || (rc = trun_smp.ensure((nc + 63) / 64 + (nc + 4095) / 4096 + 8))) return rc;
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
         RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
+        RunHost &H = trh[ract];  // rewritten in place: the writer holds the lock, no question reads it
         try {
-            auto fit = [](auto &v, size_t want) {  // headroom: the run grows batch by batch
-                if (v.capacity() < want) {
-                    v.clear();
-                    v.reserve(want + want / 2);
-                }
-                v.resize(want);
-            };
-            fit(trh_keys, n1 * kl + 64);
-            fit(trh_pre, (n1 + 1) * 4 + 8);
-            fit(trh_cntp, n1 + 16);
-            fit(trh_fl, n1 + 16);
-            fit(trh_br, n1 + 16);
-            fit(trh_smp, ns + ns2 + 8);
-            fit(trh_gs, ns + 8);
+            H.fit(n1, (uint32_t)kl);
         } catch (const std::bad_alloc &) {
             tier_version = ~0ull;
             return tier_oom();
         }
         {
-            const Down d[7] = {{trh_keys.data(), trh_keys, dkeys[cd].p, n1 * kl},
-                               {trh_pre.data(), trh_pre, trun_pre.p, (n1 + 1) * 32},
-                               {trh_cntp.data(), trh_cntp, trun_cntp.p, (n1 + 1) * 4},
-                               {trh_fl.data(), trh_fl, trun_fl.p, n1},
-                               {trh_br.data(), trh_br, trun_br.p, n1 * 4},
-                               {trh_smp.data(), trh_smp, trun_smp.p, (ns + ns2) * 8},
-                               {trh_gs.data(), trh_gs, trun_gs.p, ns * 8}};
+            const Down d[7] = {{H.keys.data(), H.keys, dkeys[cd].p, n1 * kl},
+                               {H.pre.data(), H.pre, trun_pre.p, (n1 + 1) * 32},
+                               {H.cntp.data(), H.cntp, trun_cntp.p, (n1 + 1) * 4},
+                               {H.fl.data(), H.fl, trun_fl.p, n1},
+                               {H.br.data(), H.br, trun_br.p, n1 * 4},
+                               {H.smp.data(), H.smp, trun_smp.p, (ns + ns2) * 8},
+                               {H.gs.data(), H.gs, trun_gs.p, ns * 8}};
             if ((rc = copy_down(d, 7, stream))) return rc;
         }
         if ((rc = sync())) {
             tier_version = ~0ull;
             return rc;
         }
-        rh::HostTier::Run r;
-        r.n = n1;
-        r.keys = trh_keys.data();
-        r.prefix = trh_pre.data();
-        r.cntp = reinterpret_cast<const int32_t *>(trh_cntp.data());
-        r.flags = trh_fl.data();
-        r.brank = trh_br.data();
-        r.samp = trh_smp.data();
-        r.samp2 = trh_smp.data() + ns;
-        r.gsamp = trh_gs.data();
-        tier.set_run(r);
+        tier.set_run(H.run(n1));
         tier_version = version;
         tier_runs++;
         tier_refreshes++;  // a copy from the device, as a refresh is (rh_store_tier_stats)
         return RH_OK;
     }
+    // ---- the no-wait run refresh ----------------------------------------------------------------
+    // With writes never waiting (RSOS_HIP_TIER_SYNC=0) and the tier's base still the device's, a
+    // stale tier is refreshed by a copy of the delta run alone -- O(run), no compaction (a base
+    // refresh compacts first: ~3 ms per 10^8-row store) -- into the spare run set on the copy
+    // engines.  It lands only if nothing was written meanwhile (it is never replayed: the next
+    // write takes another).  The copy reads the run's columns (trun_*) and its staged keys;
+    // whatever would rewrite them first waits for it on the device (guard_run_copy).
+    bool rf_run = false;  // the refresh in flight is a run copy
+    uint64_t rf_run_n = 0;
+    bool run_refresh_ok() const {
+        return tier_on && !tier_sync_writes && !rf_on && tier_epoch == base_epoch && nd > 0 &&
+               nd <= tier.nb / 4 + (1u << 16);
+    }
+    int guard_run_copy() {
+        if (rf_on && rf_run) RH_HIP(hipStreamWaitEvent(stream, rf_ev, 0));
+        return RH_OK;
+    }
+    int refresh_streams() {
+        if (cstream) return RH_OK;
+        // the copies on a plain stream (the copy engines); the scans and samples, and kernel
+        // copies, on a CU-masked one (create_back_stream): a copy issued on a CU-masked stream
+        // held the next write's uploads behind it (write p50 7 -> 100 ms, 10^8 rows)
+        RH_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+        RH_HIP(create_back_stream(&kstream, device));
+        RH_HIP(hipEventCreateWithFlags(&rf_ready, hipEventDisableTiming));
+        RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
+        RH_HIP(hipEventCreateWithFlags(&rf_kdone, hipEventDisableTiming));
+        return RH_OK;
+    }
+    int start_run_refresh() {
+        int rc;
+        if ((rc = refresh_streams())) return rc;
+        const uint64_t n1 = nd, ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096;
+        const uint64_t nc = std::max<uint64_t>(n1, dslot[cd].cap > 16 ? dslot[cd].cap - 16 : 0);
+        if ((rc = run_row_prefix()) || (rc = trun_smp.ensure((nc + 63) / 64 + (nc + 4095) / 4096 + 8)) ||
+            (rc = trun_keys.ensure(nc * kl + 64)))
+            return rc;
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
+        RH_HIP(hipMemcpyAsync(trun_keys.p, dkeys[cd].p, n1 * kl, hipMemcpyDeviceToDevice, stream));
+        RunHost &H = trh[1 - ract];
+        try {
+            H.fit(n1, (uint32_t)kl);
+        } catch (const std::bad_alloc &) {
+            return tier_oom();
+        }
+        RH_HIP(hipEventRecord(rf_ready, stream));
+        RH_HIP(hipStreamWaitEvent(cstream, rf_ready, 0));
+        const Down d[7] = {{H.keys.data(), H.keys, trun_keys.p, n1 * kl},
+                           {H.pre.data(), H.pre, trun_pre.p, (n1 + 1) * 32},
+                           {H.cntp.data(), H.cntp, trun_cntp.p, (n1 + 1) * 4},
+                           {H.fl.data(), H.fl, trun_fl.p, n1},
+                           {H.br.data(), H.br, trun_br.p, n1 * 4},
+                           {H.smp.data(), H.smp, trun_smp.p, (ns + ns2) * 8},
+                           {H.gs.data(), H.gs, trun_gs.p, ns * 8}};
+        if ((rc = copy_down(d, 7, cstream, false))) return rc;
+        RH_HIP(hipEventRecord(rf_ev, cstream));
+        rf_on = rf_run = true;
+        refresh_wanted = false;
+        rf_version = version;
+        rf_epoch = base_epoch;
+        rf_run_n = n1;
+        rf_log.clear();
+        rf_log_ok = false;
+        return RH_OK;
+    }
+    // the refresh a stale tier takes: a run copy when that is enough, else the base's
+    int refresh_now() { return run_refresh_ok() ? start_run_refresh() : start_refresh(); }
     // How a batch of m rows reaches the tier (decided before the batch, under the lock):
     //   0: it does not (tier off or stale, or the batch is larger than the tree takes: the tier
     //      goes stale and a refresh follows the batch),
@@ -1546,7 +1630,7 @@ struct rh_store {
     std::vector<rh::DeltaTree::Rec> fold_rows;
     std::vector<uint8_t> fold_drop;
     void fold_batch(int mode, size_t m, bool copied) {
-        if (rf_on) {  // the log for the copy in flight (mode-1 rows against its base)
+        if (rf_on && !rf_run) {  // the log for the copy in flight (mode-1 rows against its base)
             if (!copied || rf_keys.size() / kl + m > 2 * tree_limit()) {
                 rf_log_ok = false;
             } else if (rf_log_ok) {
@@ -1820,12 +1904,16 @@ struct rh_store {
             tier_version = ~0ull;
             return tier_oom();
         }
-        if (tsets[tact].keys.p != k0 || tsets[tact].prefix.p != p0 || tsets[tact].samp.p != s0) tier_version = ~0ull;
+        // a base copy that moved is gone: the next refresh copies the base again (not a run copy)
+        if (tsets[tact].keys.p != k0 || tsets[tact].prefix.p != p0 || tsets[tact].samp.p != s0)
+            tier_version = ~0ull, tier_epoch = ~0ull;
         // the run copy's page-locked columns, for the largest run the policy copies (a quarter of
         // the base): pinned here, with the base's, not by the write whose run first outgrows them
-        if (tier_sync_writes) {
+        // (both sets under "writes never wait": the spare is filled while the tier reads the other)
+        {
             const uint64_t rr = rows / 4 + (1u << 16);
-            const void *before[7] = {trh_keys.p, trh_pre.p, trh_cntp.p, trh_fl.p, trh_br.p, trh_smp.p, trh_gs.p};
+            RunHost &H = trh[ract];
+            const void *before[7] = {H.keys.p, H.pre.p, H.cntp.p, H.fl.p, H.br.p, H.smp.p, H.gs.p};
             try {
                 auto room = [](auto &v, size_t want) {
                     if (v.capacity() < want) {
@@ -1833,18 +1921,21 @@ struct rh_store {
                         v.reserve(want);
                     }
                 };
-                room(trh_keys, rr * kl + 64);
-                room(trh_pre, (rr + 1) * 4 + 8);
-                room(trh_cntp, rr + 16);
-                room(trh_fl, rr + 16);
-                room(trh_br, rr + 16);
-                room(trh_smp, rr / 64 + rr / 4096 + 16);
-                room(trh_gs, rr / 64 + 16);
+                for (int k = 0; k < (tier_sync_writes ? 1 : 2); k++) {
+                    RunHost &R = trh[k == 0 ? ract : 1 - ract];
+                    room(R.keys, rr * kl + 64);
+                    room(R.pre, (rr + 1) * 4 + 8);
+                    room(R.cntp, rr + 16);
+                    room(R.fl, rr + 16);
+                    room(R.br, rr + 16);
+                    room(R.smp, rr / 64 + rr / 4096 + 16);
+                    room(R.gs, rr / 64 + 16);
+                }
             } catch (const std::bad_alloc &) {
                 tier_version = ~0ull;
                 return tier_oom();
             }
-            const void *after[7] = {trh_keys.p, trh_pre.p, trh_cntp.p, trh_fl.p, trh_br.p, trh_smp.p, trh_gs.p};
+            const void *after[7] = {H.keys.p, H.pre.p, H.cntp.p, H.fl.p, H.br.p, H.smp.p, H.gs.p};
             if (tier.has_run() && memcmp(before, after, sizeof before)) tier_version = ~0ull;  // a held run moved
         }
         return RH_OK;
@@ -1896,7 +1987,7 @@ struct rh_store {
         // compaction runs beside the copy (whose log then breaks: later batches' records are
         // relative to the new base), and a second one, which would write the buffer being copied,
         // waits for it
-        if (rf_on) {
+        if (rf_on && !rf_run) {
             if (1 - cb == rf_cb) {
                 if ((rc = settle())) return rc;
             } else {
@@ -3078,7 +3169,8 @@ static int tier_ready(rh_store *s) {
     if (s->rf_on && !s->tier_fresh() && (rc = s->poll_refresh(false))) return rc;
     if (s->tier_fresh()) return 1;
     // stale: the device answers; a refresh is under way (or starts here when that is cheap)
-    if (!s->rf_on && s->question_may_refresh() && (rc = s->start_refresh())) return rc;
+    // (a run copy costs no compaction: always; a base copy when question_may_refresh says so)
+    if (!s->rf_on && (s->run_refresh_ok() || s->question_may_refresh()) && (rc = s->refresh_now())) return rc;
     return 0;
 }
 
@@ -3415,9 +3507,9 @@ int rh_store_tier_sync(rh_store *s) {
     if ((rc = flush_locked(s))) return rc;
     if (!s->tier_on) return RH_OK;
     RH_HIP(hipSetDevice(s->device));
-    if (!s->tier_fresh() && !s->rf_on && (rc = s->start_refresh())) return rc;
+    if (!s->tier_fresh() && !s->rf_on && (rc = s->refresh_now())) return rc;
     if ((rc = s->settle())) return rc;
-    if (!s->tier_fresh() && (rc = s->start_refresh()) == RH_OK) rc = s->settle();
+    if (!s->tier_fresh() && (rc = s->refresh_now()) == RH_OK) rc = s->settle();
     return rc;
 }
 
@@ -3477,7 +3569,9 @@ int rh_store_set_host_tier(rh_store *s, int enable, uint64_t round_max) {
     if (!s->tier_on) {  // give the host memory back
         s->tier_version = ~0ull;
         s->tier.reset();
+        s->tier_epoch = ~0ull;  // no base copy held
         s->tsets[0].release(), s->tsets[1].release();
+        s->trh[0].release(), s->trh[1].release();
         s->tier_out = std::vector<uint8_t>();
         s->tier_dpre.release(), s->tier_spre.release(), s->tier_bpre.release(), s->tier_dsmp.release();
     }

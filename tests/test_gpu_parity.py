@@ -1394,6 +1394,76 @@ def test_full_size_config5_100m(gpu, oracle_lib, n):
 
 
 @pytest.mark.gpu
+def test_host_tier_nowait_run_refresh_equals_device_answers(gpu, monkeypatch):
+    """Writes that never wait (RSOS_HIP_TIER_SYNC=0, read at store creation): a batch too large for
+    the tier's tree leaves the tier stale and starts a copy of the device's delta run alone on the
+    copy engines (rsos_hip_abi.hip start_run_refresh: no compaction), into the spare run set; it
+    lands only if nothing was written meanwhile.  While it is in flight the device answers; once it
+    has landed (tier_sync) the tier -- base copy + run copy, then the tree of later small batches
+    over them -- answers ranks, selects, key-bound and rank-range aggregates and key dumps exactly
+    as the device does, and no write compacted for it."""
+    import torch
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    from rsos_hip.synth import make_records, to_host
+    monkeypatch.setenv("RSOS_HIP_TIER_TREE", "2000")
+    monkeypatch.setenv("RSOS_HIP_TIER_SYNC", "0")
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 200_000
+    base = make_records(s, n, seed=41)
+    dev, tier = GpuFingerprintStore(s, host_tier=False), GpuFingerprintStore(s, host_tier=True)
+    for st in (dev, tier):
+        st.load_bulk_device(base)
+    tier.tier_sync()
+    rng = np.random.default_rng(19)
+    seen = [to_host(base)["keys"]]
+
+    def probe():
+        assert tier.size() == dev.size() and tier.aggregate() == dev.aggregate()
+        pool = np.concatenate(seen)
+        ks = [pool[i].tobytes() for i in rng.integers(0, len(pool), 200)] + [rng.bytes(16) for _ in range(50)]
+        karr = np.frombuffer(b"".join(ks), np.uint8).reshape(-1, 16)
+        assert np.array_equal(tier.ranks(karr), dev.ranks(karr))
+        size = tier.size()
+        for r in [0, 1, size - 1] + list(rng.integers(0, size, 100)):
+            assert tier.select(int(r)) == dev.select(int(r))
+        for _ in range(80):
+            a, b = ks[rng.integers(len(ks))], ks[rng.integers(len(ks))]
+            rg = KeyRange(a, b, ["included", "excluded"][rng.integers(2)], ["included", "excluded"][rng.integers(2)])
+            assert tier.aggregate(rg) == dev.aggregate(rg)
+        lo = rng.integers(0, size, 32)
+        hi = lo + rng.integers(0, 30_000, 32)
+        assert tier.aggregates_ranks(list(lo), list(hi)) == dev.aggregates_ranks(list(lo), list(hi))
+        lo0 = int(rng.integers(0, size - 2000))
+        a0, b0 = tier.select(lo0), tier.select(lo0 + 2000)
+        assert list(tier.enumerate(KeyRange(a0, b0))) == list(dev.enumerate(KeyRange(a0, b0)))
+
+    def both(b, ops=None):
+        assert tier.apply_device(b, ops) == dev.apply_device(b, ops)
+        seen.append(to_host(b)["keys"])
+
+    c0 = tier.stats()["compactions"]
+    r0 = tier.tier_stats()["refreshes"]
+    for k in range(3):
+        b = make_records(s, 6_000, seed=700 + k, random_keys=True)
+        ops = torch.zeros(6_000, dtype=torch.uint8, device="cuda")
+        if k:  # overwrite base rows and delete some
+            b["keys"][:400] = base["keys"][torch.from_numpy(rng.choice(n, 400, replace=False)).cuda()]
+            ops[200:400] = 1
+        both(b, ops)
+        probe()  # the run copy in flight or landed: either way the answers are the device's
+        tier.tier_sync()
+        st = tier.tier_stats()
+        assert st["base_rows"] == n and st["delta_entries"] == tier.stats()["delta_rows"] > 0, st
+        probe()
+    assert tier.stats()["compactions"] == c0  # run copies: no write compacted for the tier
+    assert tier.tier_stats()["refreshes"] >= r0 + 3
+    both(make_records(s, 100, seed=710, random_keys=True))  # small: folded over base + run copy
+    assert tier.tier_stats()["base_rows"] == n
+    probe()
+
+
+@pytest.mark.gpu
 def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
     """Batches too large for the tier's tree (RSOS_HIP_TIER_TREE=2000 here, read at store creation)
     take a copy of the device's delta run instead of a refresh of the whole base

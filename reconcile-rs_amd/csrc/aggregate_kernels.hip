@@ -1323,13 +1323,13 @@ __global__ __launch_bounds__(256) void k_copy_to_host(CopyJobs j) {
     }
 }
 
-hipError_t launch_copy_to_host(const CopyJobs &jobs, hipStream_t st) {
+hipError_t launch_copy_to_host(const CopyJobs &jobs, hipStream_t st, uint32_t max_wgs) {
     uint64_t tot = 0;
     for (int k = 0; k < jobs.n; k++) tot += jobs.bytes[k];
     if (tot == 0) return hipSuccess;
     // one workgroup per CU at most: enough stores in flight for the link, and CUs left for the
     // store's own kernels while a background refresh copies
-    const uint64_t wgs = std::min<uint64_t>(256, (tot / 16 + 255) / 256 + 1);
+    const uint64_t wgs = std::min<uint64_t>(max_wgs ? max_wgs : 256, (tot / 16 + 255) / 256 + 1);
     hipLaunchKernelGGL(k_copy_to_host, dim3((uint32_t)wgs), dim3(256), 0, st, jobs);
     return hipGetLastError();
 }

@@ -150,7 +150,9 @@ struct CopyJobs {
     uint64_t bytes[8];
     int n;
 };
-hipError_t launch_copy_to_host(const CopyJobs &jobs, hipStream_t st);
+// max_wgs: the grid cap (256, one per CU, when the stores cross PCIe beside other work; more
+// for a copy within HBM)
+hipError_t launch_copy_to_host(const CopyJobs &jobs, hipStream_t st, uint32_t max_wgs = 256);
 hipError_t launch_round_copy_out(const uint64_t *hdr, uint64_t cap, uint32_t kl, const uint8_t *src, uint8_t *dst,
                                  uint64_t worst, hipStream_t st);
 // every segment's raw rank range (from the searched bound ranks) and local aggregate

@@ -1142,6 +1142,13 @@ struct rh_store {
             if (d[k].bytes) RH_HIP(hipMemcpyAsync(d[k].host, d[k].dev, d[k].bytes, hipMemcpyDeviceToHost, st));
         return RH_OK;
     }
+    // A few result bytes into page-locked memory by a one-workgroup kernel, not a copy command: a
+    // background copy on the copy engines (a no-wait run refresh) would hold it back
+    template <class T>
+    int down_small(PinnedVec<T> &v, const void *dev, size_t bytes) {
+        const Down d{v.data(), v, dev, bytes};
+        return copy_down(&d, 1, stream);
+    }
     // A refresh's device buffers, sized for the base buffers' capacity (reserve() calls it too): a
     // base grown by compactions reallocates nothing here -- a hipFree waits for every copy in
     // flight, the other store's too (no-wait drives of 40-175 ms before, profiles/r05_nowait_cycles.txt)
@@ -1225,6 +1232,7 @@ struct rh_store {
         rf_on = false;
         if (rf_run) {  // a run copy: the tier takes it if nothing was written since it started
             rf_run = false;
+            rf_tset = -1;
             if (rf_version == version && rf_epoch == tier_epoch) {
                 ract = 1 - ract;
                 tier.set_run(trh[ract].run(rf_run_n));
@@ -1360,9 +1368,19 @@ struct rh_store {
     // since: its DeltaRecs, as columns with prefix sums, are copied down instead -- O(delta run),
     // <= n / compact_div rows -- and the tier answers from base + run copy.  The next small batch
     // (or a compaction, or a run copy past a quarter of the base) refreshes the base instead.
-    DevBuf<uint8_t> trun_c, trun_fl, trun_bs, trun_ss, trun_spre, trun_bpre, trun_pre;
-    DevBuf<uint32_t> trun_cnt, trun_cntp, trun_br;
-    DevBuf<uint64_t> trun_smp, trun_gs;
+    struct RunDev {  // the delta run's columns on the device (run_columns), one version's
+        DevBuf<uint8_t> c, fl, bs, ss, spre, bpre, pre;
+        DevBuf<uint32_t> cnt, cntp, br;
+        DevBuf<uint64_t> smp, gs;
+        void release() {
+            c.release(), fl.release(), bs.release(), ss.release(), spre.release(), bpre.release(), pre.release();
+            cnt.release(), cntp.release(), br.release(), smp.release(), gs.release();
+        }
+    };
+    // two sets: run_columns fills trs[tcur]; while a no-wait run copy reads one (rf_tset), the
+    // next version's columns go to the other, so neither the copy nor the questions wait
+    RunDev trs[2];
+    int tcur = 0;
     struct RunHost {  // a run copy's page-locked columns
         PinnedVec<uint8_t> keys, fl;
         PinnedVec<uint64_t> pre, smp, gs;
@@ -1398,7 +1416,6 @@ struct rh_store {
     // trh[ract]: the run copy the tier reads; trh[1 - ract]: the one a no-wait run refresh fills
     RunHost trh[2];
     int ract = 0;
-    DevBuf<uint8_t> trun_keys;  // the run's keys staged for a no-wait run copy (batches rewrite dkeys)
     uint64_t tier_runs = 0;
     bool snap_ok = false;  // set before a batch: a run copy may replace the refresh it causes
     // with a run copy held, batches fold into the tree as deltas against base + run (mode 2: a
@@ -1413,14 +1430,13 @@ struct rh_store {
     // on the device once per version of the contents: device reads over base + run use them in
     // place (rh::RoundRun), the run copy adds the contributions' prefix sums and takes them down.
     // trun_ver: the version they hold.
-    uint64_t trun_ver = ~0ull, trun_pre_ver = ~0ull;  // the version trun_pre holds
+    uint64_t trun_ver = ~0ull, trun_pre_ver = ~0ull;  // the version trs[tcur].pre holds
     // the run's row prefix (run_columns forms it for a short run; a long run's on demand)
     int run_row_prefix() {
         int rc;
         if ((rc = run_columns())) return rc;
         if (trun_pre_ver == version) return RH_OK;
-        if ((rc = guard_run_copy())) return rc;
-        RH_HIP(rh::launch_row_prefix(trun_c.p, nd, trun_bpre.p, trun_pre.p, stream));
+        RH_HIP(rh::launch_row_prefix(trs[tcur].c.p, nd, trs[tcur].bpre.p, trs[tcur].pre.p, stream));
         trun_pre_ver = version;
         return RH_OK;
     }
@@ -1429,9 +1445,9 @@ struct rh_store {
     int run_columns() {
         int rc;
         const uint64_t n1 = nd;
-        if (trun_ver == version && trun_gs.p) return RH_OK;
-        if ((rc = guard_run_copy())) return rc;  // a no-wait run copy may still read the columns
-        trun_ver = ~0ull;
+        if (trun_ver == version && trs[tcur].gs.p) return RH_OK;
+        if (rf_on && rf_run && rf_tset == tcur) tcur = 1 - tcur;  // a run copy reads this set
+        trun_ver = trun_pre_ver = ~0ull;
         // sized for the longest run the delta run's buffers are planned for (compaction threshold +
         // a batch), not this one: a run growing batch by batch would otherwise reallocate here, and
         // the hipFree waits for everything in flight -- a background refresh copy included (no-wait
@@ -1440,17 +1456,17 @@ struct rh_store {
         const uint64_t nbk = rh_num_blocks(n1);
         {
             const uint64_t cbk = rh_num_blocks(nc), csb = rh_num_superblocks(nc), cs = (nc + 63) / 64;
-            if ((rc = trun_c.ensure(nc * 32 + 64)) || (rc = trun_cnt.ensure(nc + 16)) || (rc = trun_fl.ensure(nc + 16)) ||
-                (rc = trun_br.ensure(nc + 16)) || (rc = trun_bs.ensure(cbk * 32 + 32)) ||
-                (rc = trun_ss.ensure(csb * 32 + 32)) || (rc = trun_cntp.ensure(nc + 16)) || (rc = trun_gs.ensure(cs + 8)))
+            if ((rc = trs[tcur].c.ensure(nc * 32 + 64)) || (rc = trs[tcur].cnt.ensure(nc + 16)) || (rc = trs[tcur].fl.ensure(nc + 16)) ||
+                (rc = trs[tcur].br.ensure(nc + 16)) || (rc = trs[tcur].bs.ensure(cbk * 32 + 32)) ||
+                (rc = trs[tcur].ss.ensure(csb * 32 + 32)) || (rc = trs[tcur].cntp.ensure(nc + 16)) || (rc = trs[tcur].gs.ensure(cs + 8)))
                 return rc;
-            if ((rc = trun_spre.ensure((csb + 1) * 32 + 64)) || (rc = trun_bpre.ensure((cbk + 1) * 32 + 64)) ||
-                (rc = trun_pre.ensure((nc + 1) * 32 + 64)))
+            if ((rc = trs[tcur].spre.ensure((csb + 1) * 32 + 64)) || (rc = trs[tcur].bpre.ensure((cbk + 1) * 32 + 64)) ||
+                (rc = trs[tcur].pre.ensure((nc + 1) * 32 + 64)))
                 return rc;
         }
         if (n1 <= rh::RUNCOL_SMALL && run_cols_fused) {  // a short run: every column in one launch
-            const rh::RunCols o{trun_c.p,  trun_cnt.p,  trun_fl.p,   trun_br.p,   trun_pre.p, trun_bs.p,
-                                trun_ss.p, trun_spre.p, trun_bpre.p, trun_cntp.p, trun_gs.p};
+            const rh::RunCols o{trs[tcur].c.p,  trs[tcur].cnt.p,  trs[tcur].fl.p,   trs[tcur].br.p,   trs[tcur].pre.p, trs[tcur].bs.p,
+                                trs[tcur].ss.p, trs[tcur].spre.p, trs[tcur].bpre.p, trs[tcur].cntp.p, trs[tcur].gs.p};
             RH_HIP(rh::launch_run_columns_small(dslot[cd].p, dheap.p, n1, o, stream));
             trun_ver = trun_pre_ver = version;
             return RH_OK;
@@ -1458,13 +1474,13 @@ struct rh_store {
         // a long run: the columns with their block sums in one pass, the block prefix; its row prefix
         // (another read and write of 32 B an entry: ~0.1 ms at 10^7 entries, more than the rounds
         // of one reconciliation save with it) only for the tier's run copy (run_row_prefix)
-        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trun_c.p, trun_cnt.p, trun_fl.p, trun_br.p, stream,
-                                   trun_bs.p));
-        RH_HIP(rh::launch_reduce(trun_bs.p, nbk, trun_ss.p, stream));
-        RH_HIP(rh::launch_block_prefix(n1, trun_bs.p, trun_ss.p, trun_spre.p, trun_bpre.p, stream));
-        RH_HIP(rh::launch_exclusive_scan_u32(trun_cnt.p, trun_cntp.p, n1 + 1, scratch, stream));
+        RH_HIP(rh::launch_tier_run(dslot[cd].p, dheap.p, n1, trs[tcur].c.p, trs[tcur].cnt.p, trs[tcur].fl.p, trs[tcur].br.p, stream,
+                                   trs[tcur].bs.p));
+        RH_HIP(rh::launch_reduce(trs[tcur].bs.p, nbk, trs[tcur].ss.p, stream));
+        RH_HIP(rh::launch_block_prefix(n1, trs[tcur].bs.p, trs[tcur].ss.p, trs[tcur].spre.p, trs[tcur].bpre.p, stream));
+        RH_HIP(rh::launch_exclusive_scan_u32(trs[tcur].cnt.p, trs[tcur].cntp.p, n1 + 1, scratch, stream));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
-        RH_HIP(rh::launch_tier_gsamp(trun_br.p, trun_cntp.p, trun_fl.p, n1, trun_gs.p, stream));
+        RH_HIP(rh::launch_tier_gsamp(trs[tcur].br.p, trs[tcur].cntp.p, trs[tcur].fl.p, n1, trs[tcur].gs.p, stream));
         trun_ver = version;
         return RH_OK;
     }
@@ -1481,9 +1497,9 @@ struct rh_store {
         // the contributions' row prefix: the host walks it (HostTier::Run::prefix)
         // (the samples sized like run_columns' buffers: for the longest run planned)
         const uint64_t nc = std::max<uint64_t>(n1, dslot[cd].cap > 16 ? dslot[cd].cap - 16 : 0);
-        if ((rc = run_row_prefix()) || (rc = trun_smp.ensure((nc + 63) / 64 + (nc + 4095) / 4096 + 8))) return rc;
-        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
-        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
+        if ((rc = run_row_prefix()) || (rc = trs[tcur].smp.ensure((nc + 63) / 64 + (nc + 4095) / 4096 + 8))) return rc;
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trs[tcur].smp.p, stream));
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trs[tcur].smp.p + ns, stream));
         RunHost &H = trh[ract];  // rewritten in place: the writer holds the lock, no question reads it
         try {
             H.fit(n1, (uint32_t)kl);
@@ -1493,12 +1509,12 @@ struct rh_store {
         }
         {
             const Down d[7] = {{H.keys.data(), H.keys, dkeys[cd].p, n1 * kl},
-                               {H.pre.data(), H.pre, trun_pre.p, (n1 + 1) * 32},
-                               {H.cntp.data(), H.cntp, trun_cntp.p, (n1 + 1) * 4},
-                               {H.fl.data(), H.fl, trun_fl.p, n1},
-                               {H.br.data(), H.br, trun_br.p, n1 * 4},
-                               {H.smp.data(), H.smp, trun_smp.p, (ns + ns2) * 8},
-                               {H.gs.data(), H.gs, trun_gs.p, ns * 8}};
+                               {H.pre.data(), H.pre, trs[tcur].pre.p, (n1 + 1) * 32},
+                               {H.cntp.data(), H.cntp, trs[tcur].cntp.p, (n1 + 1) * 4},
+                               {H.fl.data(), H.fl, trs[tcur].fl.p, n1},
+                               {H.br.data(), H.br, trs[tcur].br.p, n1 * 4},
+                               {H.smp.data(), H.smp, trs[tcur].smp.p, (ns + ns2) * 8},
+                               {H.gs.data(), H.gs, trs[tcur].gs.p, ns * 8}};
             if ((rc = copy_down(d, 7, stream))) return rc;
         }
         if ((rc = sync())) {
@@ -1516,17 +1532,15 @@ struct rh_store {
     // stale tier is refreshed by a copy of the delta run alone -- O(run), no compaction (a base
     // refresh compacts first: ~3 ms per 10^8-row store) -- into the spare run set on the copy
     // engines.  It lands only if nothing was written meanwhile (it is never replayed: the next
-    // write takes another).  The copy reads the run's columns (trun_*) and its staged keys;
-    // whatever would rewrite them first waits for it on the device (guard_run_copy).
+    // write takes another).  The copy reads one of the two device column sets (the next version's
+    // columns go to the other: run_columns) and a staged copy of the run's keys.
     bool rf_run = false;  // the refresh in flight is a run copy
     uint64_t rf_run_n = 0;
+    int rf_tset = -1;               // the column set it reads
+    DevBuf<uint8_t> trun_keys;      // ... and the run's keys, staged
     bool run_refresh_ok() const {
         return tier_on && !tier_sync_writes && !rf_on && tier_epoch == base_epoch && nd > 0 &&
                nd <= tier.nb / 4 + (1u << 16);
-    }
-    int guard_run_copy() {
-        if (rf_on && rf_run) RH_HIP(hipStreamWaitEvent(stream, rf_ev, 0));
-        return RH_OK;
     }
     int refresh_streams() {
         if (cstream) return RH_OK;
@@ -1545,30 +1559,39 @@ struct rh_store {
         if ((rc = refresh_streams())) return rc;
         const uint64_t n1 = nd, ns = (n1 + 63) / 64, ns2 = (n1 + 4095) / 4096;
         const uint64_t nc = std::max<uint64_t>(n1, dslot[cd].cap > 16 ? dslot[cd].cap - 16 : 0);
-        if ((rc = run_row_prefix()) || (rc = trun_smp.ensure((nc + 63) / 64 + (nc + 4095) / 4096 + 8)) ||
-            (rc = trun_keys.ensure(nc * kl + 64)))
-            return rc;
-        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, trun_smp.p, stream));
-        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, trun_smp.p + ns, stream));
-        RH_HIP(hipMemcpyAsync(trun_keys.p, dkeys[cd].p, n1 * kl, hipMemcpyDeviceToDevice, stream));
+        if ((rc = run_row_prefix())) return rc;
+        RunDev &T = trs[tcur];
+        if ((rc = T.smp.ensure((nc + 63) / 64 + (nc + 4095) / 4096 + 8)) || (rc = trun_keys.ensure(nc * kl + 64))) return rc;
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 64, T.smp.p, stream));
+        RH_HIP(kops->sample_stride(dkeys[cd].p, n1, 4096, T.smp.p + ns, stream));
+        {  // the keys staged in HBM (the batch after next rewrites dkeys[cd]; a wait for the copy
+           // there held small writes 45 ms)
+            rh::CopyJobs j{};
+            j.src[0] = dkeys[cd].p, j.dst[0] = trun_keys.p, j.bytes[0] = n1 * kl, j.n = 1;
+            RH_HIP(rh::launch_copy_to_host(j, stream, 2048));
+        }
         RunHost &H = trh[1 - ract];
         try {
             H.fit(n1, (uint32_t)kl);
         } catch (const std::bad_alloc &) {
             return tier_oom();
         }
+        // on the copy engines (a copy kernel beside the store's work slowed its questions to
+        // milliseconds, profiles/r05_nowait_run_refresh.txt); the store's own small result copies
+        // are kernel stores (down_small), so they do not queue behind it
         RH_HIP(hipEventRecord(rf_ready, stream));
         RH_HIP(hipStreamWaitEvent(cstream, rf_ready, 0));
         const Down d[7] = {{H.keys.data(), H.keys, trun_keys.p, n1 * kl},
-                           {H.pre.data(), H.pre, trun_pre.p, (n1 + 1) * 32},
-                           {H.cntp.data(), H.cntp, trun_cntp.p, (n1 + 1) * 4},
-                           {H.fl.data(), H.fl, trun_fl.p, n1},
-                           {H.br.data(), H.br, trun_br.p, n1 * 4},
-                           {H.smp.data(), H.smp, trun_smp.p, (ns + ns2) * 8},
-                           {H.gs.data(), H.gs, trun_gs.p, ns * 8}};
+                           {H.pre.data(), H.pre, T.pre.p, (n1 + 1) * 32},
+                           {H.cntp.data(), H.cntp, T.cntp.p, (n1 + 1) * 4},
+                           {H.fl.data(), H.fl, T.fl.p, n1},
+                           {H.br.data(), H.br, T.br.p, n1 * 4},
+                           {H.smp.data(), H.smp, T.smp.p, (ns + ns2) * 8},
+                           {H.gs.data(), H.gs, T.gs.p, ns * 8}};
         if ((rc = copy_down(d, 7, cstream, false))) return rc;
         RH_HIP(hipEventRecord(rf_ev, cstream));
         rf_on = rf_run = true;
+        rf_tset = tcur;
         refresh_wanted = false;
         rf_version = version;
         rf_epoch = base_epoch;
@@ -1591,7 +1614,7 @@ struct rh_store {
         return tier_epoch == base_epoch ? 1 : 2;
     }
     // whether the batch's rows must come down at all (a fold, or a refresh in flight to log for)
-    bool fold_rows_wanted(int fmode) const { return fmode != 0 || rf_on; }
+    bool fold_rows_wanted(int fmode) const { return fmode != 0 || (rf_on && !rf_run); }
     // page-locked room for a batch's fold rows (a failure leaves the tier stale, never fails the batch)
     bool fold_room(size_t m) {
         try {
@@ -2018,7 +2041,7 @@ struct rh_store {
         // so the sums and the search table are enqueued behind the merge without a round trip; the
         // merge's own counts (pinned, asynchronous) are checked against it after the one sync
         uint64_t *c = res_host.data();
-        RH_HIP(hipMemcpyAsync(c, mcnt.p, 24, hipMemcpyDeviceToHost, stream));
+        if ((rc = down_small(res_host, mcnt.p, 24))) return rc;
         const uint64_t want = size(), nb_old = nb;
         base_epoch++;  // same contents, a new base: the tier's copy stays valid, not the device's deltas
         base_loaded = false;
@@ -2074,6 +2097,12 @@ struct rh_store {
         RH_HIP(rh::reserve_merge_scratch(scratch, plan, batch, base));
         if (scratch.err) return fail(RH_ERR_OOM, "scratch allocation failed");
         if (tier_on && (rc = refresh_room())) return rc;
+        // the row prefix's stream now, not at a later question (creating a queue takes ms)
+        if (row_prefix == 1 && !pstream) {
+            RH_HIP(create_back_stream(&pstream, device));
+            RH_HIP(hipEventCreateWithFlags(&pre_ev, hipEventDisableTiming));
+            RH_HIP(hipEventCreateWithFlags(&pre_base_ev, hipEventDisableTiming));
+        }
         tier_host_oom = false;
         // the tier's page-locked room: a failure leaves the tier stale, not the device reservation failed
         if ((rc = tier_stale_on_host_oom(tier_reserve(rows)))) return rc;
@@ -2332,7 +2361,7 @@ struct rh_store {
             if (want && (rc = fold_copies(skeys.p, sfps.p, sops.p, dheap.p + heap_len * sizeof(rh::DeltaRec), dops.p, m)))
                 return rc;
             // 5. the one round trip
-            RH_HIP(hipMemcpyAsync(host, results.p, 96, hipMemcpyDeviceToHost, stream));
+            if ((rc = down_small(res_host, results.p, 96))) return rc;
             if (full == 0 && next && next_m) {
                 if (!res_ev) RH_HIP(hipEventCreateWithFlags(&res_ev, hipEventDisableTiming));
                 RH_HIP(hipEventRecord(res_ev, stream));
@@ -2438,16 +2467,16 @@ struct rh_store {
         if ((rc = ensure_base_prefix())) return rc;
         *run = rh::RoundRun{nd,
                             dkeys[cd].p,
-                            trun_c.p,
-                            trun_bs.p,
-                            trun_ss.p,
-                            reinterpret_cast<const int32_t *>(trun_cntp.p),
-                            trun_fl.p,
-                            trun_br.p,
-                            trun_gs.p,
+                            trs[tcur].c.p,
+                            trs[tcur].bs.p,
+                            trs[tcur].ss.p,
+                            reinterpret_cast<const int32_t *>(trs[tcur].cntp.p),
+                            trs[tcur].fl.p,
+                            trs[tcur].br.p,
+                            trs[tcur].gs.p,
                             nb,
-                            trun_bpre.p,
-                            trun_pre_ver == version ? trun_pre.p : nullptr};
+                            trs[tcur].bpre.p,
+                            trun_pre_ver == version ? trs[tcur].pre.p : nullptr};
         *in = base_in();
         return RH_OK;
     }
@@ -3105,6 +3134,7 @@ struct rh_store {
         q_in.release(); q_res.release();
         stage_in.release(); stage_out.release(); stage_out2.release(); load_flag.release();
         r_in.release(); r_kind.release(); r_out.release(); r_seg.release(); r_part.release(); pr_out.release();
+        trs[0].release(); trs[1].release(); trun_keys.release();
         tsets[0].release(); tsets[1].release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release(); tier_dsmp.release();
         if (cstream) (void)hipStreamDestroy(cstream);
         if (kstream) (void)hipStreamDestroy(kstream);

@@ -2013,6 +2013,18 @@ hipError_t reserve_merge_scratch(Scratch &s, uint64_t plan, uint64_t batch, uint
     // merge_tile_bounds' tiles over a compaction's output (the base grows with every compaction:
     // a slot grown then frees the old one, and hipFree waits for every copy in flight)
     (void)s.u32(8, (std::max(base_rows, plan) + MT - 1) / MT + 1);
+    // the library scans' temporary storage (one shared slot): a delta run's count scan
+    // (run_columns, up to plan rows) and the u64 scans over up to a base
+    size_t t32 = 0, t64 = 0;
+    const uint64_t big = std::max(base_rows, plan) + 2;
+    if (rocprim::exclusive_scan(nullptr, t32, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u, plan + 2,
+                                rocprim::plus<uint32_t>(), (hipStream_t)0) != hipSuccess)
+        t32 = 0;
+    if (rocprim::exclusive_scan(nullptr, t64, (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, big,
+                                rocprim::plus<uint64_t>(), (hipStream_t)0) != hipSuccess)
+        t64 = 0;
+    (void)hipGetLastError();
+    if (std::max(t32, t64)) (void)s.bytes(std::max(t32, t64));
     return s.err;
 }
 

@@ -28,6 +28,8 @@ struct Scratch {
         Slot &s = slots[idx];
         bytes = std::max<size_t>(bytes, 256);
         if (s.bytes < bytes) {
+            static const bool dbg = getenv("RSOS_HIP_ALLOC_DBG") != nullptr;  // every regrowth, to stderr
+            if (dbg && s.p) fprintf(stderr, "rsos_hip: scratch slot %zu grows %zu -> %zu bytes\n", idx, s.bytes, bytes);
             if (s.p) {
                 (void)hipStreamSynchronize(stream);
                 (void)hipFree(s.p);

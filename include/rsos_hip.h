@@ -287,8 +287,10 @@ int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
  * second page-locked set.  By default (RSOS_HIP_TIER_SYNC unset or 1) the write or load that
  * starts a refresh waits for it, so every question is answered from a fresh tier; with
  * RSOS_HIP_TIER_SYNC=0 writes never wait -- a stale tier hands the questions to the device (which
- * reads base + delta run in place: no question compacts) and batches applied during a copy are
- * logged and replayed into it.  No question waits for an O(n) copy under either policy.
+ * reads base + delta run in place: no question compacts); while the tier's base is still the
+ * device's, its refresh is a background copy of the delta run alone (no compaction), taken if
+ * nothing was written meanwhile, else a base refresh, into which batches applied during the copy
+ * are logged and replayed.  No question waits for an O(n) copy under either policy.
  * Stats (nullable): base rows and delta entries (tree entries + run-copy entries) of a fresh tier
  * (0, 0 when stale), copies taken from the device (base refreshes and run copies) and batch folds
  * so far.
@@ -296,8 +298,9 @@ int rh_store_set_host_tier(rh_store *store, int enable, uint64_t round_max);
  * 8 B per 64 rows for the set the tier reads, with 25% headroom; the first refresh after that pins a
  * second set of the same size, which later refreshes alternate with (a failure to pin leaves the
  * tier stale and is never the write's error); the delta run's copy takes ~(key_len + 41) B per
- * delta row (up to a quarter of the rows).  At 10^8 rows of 16-byte keys: 6 GB, then 12 GB, plus
- * up to 1.4 GB.                                                                                  */
+ * delta row (up to a quarter of the rows; two such sets under RSOS_HIP_TIER_SYNC=0, one filled
+ * while the tier reads the other).  At 10^8 rows of 16-byte keys: 6 GB, then 12 GB, plus up to
+ * 1.4 GB (2.8 GB with writes never waiting).                                                     */
 int rh_store_tier_stats(rh_store *store, uint64_t *base_rows, uint64_t *delta_entries, uint64_t *refreshes,
                         uint64_t *folds);
 /* Wait until the host tier is fresh (a background refresh landed and swapped in, one started if

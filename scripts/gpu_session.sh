@@ -69,6 +69,8 @@ for step in "$@"; do
     default) run default 300 python3 bench.py ;;
     config5) run config5 300 python3 bench.py --config config5 ;;
     config5_40) run config5_40 300 python3 bench.py --config config5 --steps 40 ;;
+    config5_ab)  # the batch's result block by a kernel store (default) / a copy command, twice each
+        for k in 1a 0a 1b 0b; do run config5_ab_$k 300 env RSOS_HIP_COPY_KERNEL=${k%?} python3 bench.py --config config5 --steps 40 --cpu-baseline 0; done ;;
     rbsr) run rbsr 300 python3 bench.py --config rbsr ;;
     trace_rbsr)
         run trace_rbsr 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trrb" -o tr -- python3 bench.py --config rbsr --cpu-baseline 0 --steps 5 --warmup 2

@@ -1461,6 +1461,26 @@ def test_host_tier_nowait_run_refresh_equals_device_answers(gpu, monkeypatch):
     both(make_records(s, 100, seed=710, random_keys=True))  # small: folded over base + run copy
     assert tier.tier_stats()["base_rows"] == n
     probe()
+    # a compaction while a run copy is in flight: the copy is relative to the tier's base and the
+    # contents did not change, so it lands; the next large batch then refreshes the base
+    both(make_records(s, 6_000, seed=720, random_keys=True))
+    for st_ in (dev, tier):
+        st_.compact()
+    probe()
+    tier.tier_sync()
+    probe()
+    both(make_records(s, 6_000, seed=721, random_keys=True))
+    probe()
+    tier.tier_sync()
+    assert tier.tier_stats()["delta_entries"] == tier.stats()["delta_rows"]
+    probe()
+    # the policy switched, and the store closed, with a run copy in flight
+    both(make_records(s, 6_000, seed=722, random_keys=True))
+    tier.set_tier_policy(True)
+    probe()
+    tier.set_tier_policy(False)
+    both(make_records(s, 6_000, seed=723, random_keys=True))
+    tier.close()
 
 
 @pytest.mark.gpu

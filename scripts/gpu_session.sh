@@ -143,6 +143,9 @@ for step in "$@"; do
         python3 scripts/long_calls.py "$O/nwc" 5000 > "$O/${TAG}_nowait_long_calls.txt" 2>&1 || true ;;
     sync_cycles) run sync_cycles 400 env TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 $EX/tier_interleave 100000000 1000000 20 1 c5 2 ;;
     off_cycles) run off_cycles 400 env TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 $EX/tier_interleave 100000000 1000000 12 0 c5 2 3 ;;
+    off_drive_trace)  # tier off: per-cycle times and the kernels of each drive (scripts/drive_kernels.py)
+        run off_drive_trace 400 env TIER_INTERLEAVE_CYCLES=1 rocprofv3 --kernel-trace --output-format csv -d "$O/odt" -o tr -- $EX/tier_interleave 100000000 1000000 8 0 c5 1
+        python3 scripts/drive_kernels.py "$O/odt" "$O/off_drive_trace.log" > "$O/${TAG}_off_drive_kernels.txt" 2>&1 || true ;;
     trace_config5)
         run trace_config5 300 rocprofv3 --kernel-trace --output-format csv -d "$O/c5t" -o c5 -- python3 bench.py --config config5 --steps 40 --cpu-baseline 0
         f=$(find "$O/c5t" -name 'c5_kernel_trace.csv' | head -n 1)

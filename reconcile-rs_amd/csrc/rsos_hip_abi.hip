@@ -1442,6 +1442,7 @@ struct rh_store {
     }
     // A/B switch: RSOS_HIP_RUNCOL_FUSED=0 forms a short run's columns in the eight launches too
     int run_cols_fused = getenv("RSOS_HIP_RUNCOL_FUSED") ? atoi(getenv("RSOS_HIP_RUNCOL_FUSED")) : 1;
+    int run_prep_wait = getenv("RSOS_HIP_RUN_PREP_WAIT") ? atoi(getenv("RSOS_HIP_RUN_PREP_WAIT")) : 1;
     int run_columns() {
         int rc;
         const uint64_t n1 = nd;
@@ -1590,6 +1591,10 @@ struct rh_store {
                            {H.gs.data(), H.gs, T.gs.p, ns * 8}};
         if ((rc = copy_down(d, 7, cstream, false))) return rc;
         RH_HIP(hipEventRecord(rf_ev, cstream));
+        // the write waits for the columns and row prefix it queued (~0.4 ms at 10^7 run rows), not
+        // for the copy: the drive that follows reads them at once instead of queueing behind them
+        // (RSOS_HIP_RUN_PREP_WAIT=0: return at once)
+        if (run_prep_wait) RH_HIP(hipEventSynchronize(rf_ready));
         rf_on = rf_run = true;
         rf_tset = tcur;
         refresh_wanted = false;

@@ -141,6 +141,8 @@ for step in "$@"; do
     nowait_cycles)  # per-cycle write / drive times, and the HIP calls of the same run
         run nowait_cycles 400 env RSOS_HIP_TIER_SYNC=0 TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d "$O/nwc" -o tr -- $EX/tier_interleave 100000000 1000000 12 1 c5 2 3
         python3 scripts/long_calls.py "$O/nwc" 5000 > "$O/${TAG}_nowait_long_calls.txt" 2>&1 || true ;;
+    nowait_prep_ab)  # the no-wait write waits for its run copy's device preparation (1) or not (0)
+        for k in 1a 0a 1b 0b; do run nowait_prep_$k 400 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_RUN_PREP_WAIT=${k%?} $EX/tier_interleave 100000000 1000000 12 1 c5 2 3; done ;;
     sync_cycles) run sync_cycles 400 env TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 $EX/tier_interleave 100000000 1000000 20 1 c5 2 ;;
     off_cycles) run off_cycles 400 env TIER_INTERLEAVE_CYCLES=1 RSOS_HIP_ALLOC_DBG=1 $EX/tier_interleave 100000000 1000000 12 0 c5 2 3 ;;
     off_drive_trace)  # tier off: per-cycle times and the kernels of each drive (scripts/drive_kernels.py)

@@ -190,6 +190,13 @@ void rh_fp_sub(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
  * background kernels (the host tier's refresh scans, the row prefix) on streams whose CU mask
  * leaves the last RSOS_HIP_BG_RESERVE (default 32) compute units to the questions' kernels.     */
 typedef struct rh_store rh_store;
+/* Row cap: one rh_store holds fewer than 2^31 rows (RH_STORE_MAX_ROWS; its device ranks and counts
+ * are 32-bit).  rh_store_load / _load_device / _reserve with n >= 2^31, and rh_store_apply /
+ * _apply_device / a staged batch that would take the store to 2^31 rows, return RH_ERR_ARG
+ * ("store size limit (2^31 rows) exceeded ...") and change nothing.  Rsos::size() is a usize
+ * (rsos/src/rsos_trait.rs:44): a map of 2^31 rows or more (one MI355X holds ~2.1 x 10^9 rows of
+ * 16 B keys) is an rh_sstore (below; HipShardedMap in Rust), each shard under the cap.        */
+#define RH_STORE_MAX_ROWS 2147483648 /* 2^31 */
 
 int rh_store_create(int device, const rh_schema *schema, rh_store **out);
 int rh_store_destroy(rh_store *store);

@@ -236,6 +236,7 @@ struct DevBuf {
 
 namespace rh {
 int set_error(int code, const std::string &msg) { return fail(code, msg); }
+bool debug_fail_point(const char *name) { return fail_point(name); }
 }  // namespace rh
 
 // ---- dispatch table over the instantiated shapes (schemas.def) -------------------------------
@@ -935,7 +936,7 @@ struct rh_store {
         *done = false;
         out[0] = out[1] = out[2] = 0;
         if (m == 0 || m > small_limit()) return RH_OK;
-        if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
         if ((rc = pre_batch())) return rc;
         snap_ok = run_copy_allowed(m);
         int fmode = fold_mode(m);
@@ -1239,8 +1240,10 @@ struct rh_store {
                 tier_version = version;
                 tier_runs++;
                 tier_refreshes++;
+                run_discards = 0;
             } else {
                 refresh_wanted = true;
+                run_discards++;
             }
             return;
         }
@@ -1537,6 +1540,13 @@ struct rh_store {
     // columns go to the other: run_columns) and a staged copy of the run's keys.
     bool rf_run = false;  // the refresh in flight is a run copy
     uint64_t rf_run_n = 0;
+    // Run copies discarded in a row because a write landed during each: writes arriving faster
+    // than one O(run) copy would keep the tier stale for as long as they last.  After
+    // RUN_DISCARD_MAX of them the next refresh is a base refresh, into which the batches applied
+    // while it is in flight are logged and replayed, so it lands under a steady write stream.
+    static constexpr int RUN_DISCARD_MAX = 2;
+    int run_discards = 0;
+    uint64_t run_fallbacks = 0;  // base refreshes taken for that reason (RSOS_HIP_ROUND_DBG / tests)
     int rf_tset = -1;               // the column set it reads
     DevBuf<uint8_t> trun_keys;      // ... and the run's keys, staged
     bool run_refresh_ok() const {
@@ -1606,7 +1616,14 @@ struct rh_store {
         return RH_OK;
     }
     // the refresh a stale tier takes: a run copy when that is enough, else the base's
-    int refresh_now() { return run_refresh_ok() ? start_run_refresh() : start_refresh(); }
+    // a question's refresh (tier_ready) is only ever a run copy: no question compacts
+    bool run_refresh_next() const { return run_refresh_ok() && run_discards < RUN_DISCARD_MAX; }
+    int refresh_now() {
+        if (run_refresh_next()) return start_run_refresh();
+        if (run_refresh_ok()) run_fallbacks++;
+        run_discards = 0;
+        return start_refresh();
+    }
     // How a batch of m rows reaches the tier (decided before the batch, under the lock):
     //   0: it does not (tier off or stale, or the batch is larger than the tree takes: the tier
     //      goes stale and a refresh follows the batch),
@@ -1817,7 +1834,7 @@ struct rh_store {
         int rc;
         if ((rc = drain_prefix_build())) return rc;  // it reads bfps[cb], rewritten here
         // ranks are 32-bit on the device (searches, the protocol round): refuse what they cannot hold
-        if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
         if ((rc = settle())) return rc;  // a tier copy in flight reads the base run
         health_reset();
         version++;
@@ -1856,7 +1873,7 @@ struct rh_store {
     DevBuf<uint64_t> sbsmp, sbsmp2, sbtabp, stot;
     DevBuf<uint32_t> sbtab;
     int load_target(size_t m) {
-        if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if (m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
         const int nxt = 1 - cb;
         int rc;
         if ((rc = drain_prefix_build())) return rc;  // one from two bases ago may read bfps[nxt]
@@ -2274,7 +2291,7 @@ struct rh_store {
         out[0] = out[1] = out[2] = 0;
         if (next_prepared) *next_prepared = false;
         if (m == 0) return RH_OK;
-        if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+        if (nb + nd + m >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
         // keeping the last row of a repeated key needs the sort to order ties by input row, which
         // the batch sort does only when it carries the rows' indices (it does with ops)
         if (last_wins && !ops) return fail(RH_ERR_ARG, "last-wins batch without its op column");
@@ -3197,6 +3214,7 @@ static int tier_ready(rh_store *s) {
     const int frc = flush_locked(s);
     if (frc) return frc;
     if (!s->tier_on) return 0;
+    if (s->tier_fresh()) return 1;  // the common case: no device call at all
     RH_HIP(hipSetDevice(s->device));
     int rc;
     // a stale tier takes a landed copy now (a fresh one takes it at the next write: no log replay
@@ -3204,8 +3222,9 @@ static int tier_ready(rh_store *s) {
     if (s->rf_on && !s->tier_fresh() && (rc = s->poll_refresh(false))) return rc;
     if (s->tier_fresh()) return 1;
     // stale: the device answers; a refresh is under way (or starts here when that is cheap)
-    // (a run copy costs no compaction: always; a base copy when question_may_refresh says so)
-    if (!s->rf_on && (s->run_refresh_ok() || s->question_may_refresh()) && (rc = s->refresh_now())) return rc;
+    // (a run copy costs no compaction: always, unless copies keep being discarded; a base copy
+    // when question_may_refresh says so)
+    if (!s->rf_on && (s->run_refresh_next() || s->question_may_refresh()) && (rc = s->refresh_now())) return rc;
     return 0;
 }
 
@@ -3245,8 +3264,9 @@ int rh_store_destroy(rh_store *s) {
 }
 
 int rh_store_load(rh_store *s, const rh_columns *h, size_t n) {
+    // the row cap first: it is a property of the arguments (include/rsos_hip.h, "Row cap")
+    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
     if (!s || !h) return fail(RH_ERR_ARG, "NULL");
-    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
     RH_LOCK_NOFLUSH(s);
     s->pend.clear();  // a load replaces the contents: staged rows before it are superseded
     int rc;
@@ -3255,8 +3275,8 @@ int rh_store_load(rh_store *s, const rh_columns *h, size_t n) {
 }
 
 int rh_store_load_device(rh_store *s, const rh_columns *dev_cols, size_t n, void *after_stream) {
+    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
     if (!s) return fail(RH_ERR_ARG, "NULL");
-    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
     int rc = check_cols(s->schema, dev_cols, n);
     if (rc) return rc;
     RH_LOCK_NOFLUSH(s);
@@ -3559,8 +3579,9 @@ int rh_store_set_tier_policy(rh_store *s, int keep_fresh) {
 }
 
 int rh_store_reserve(rh_store *s, uint64_t rows, uint64_t batch_rows) {
+    if (rows >= (1ull << 31) || batch_rows >= (1ull << 31))
+        return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
     if (!s) return fail(RH_ERR_ARG, "store is NULL");
-    if (rows >= (1ull << 31) || batch_rows >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows)");
     RH_LOCK(s);
     return s->reserve(rows, batch_rows);
 }
@@ -4237,7 +4258,7 @@ int rh_estore_destroy(rh_estore *s) {
 
 int rh_estore_load(rh_estore *s, const uint8_t *bytes, const uint64_t *offsets, size_t n) {
     if (!s || (n && (!bytes || !offsets))) return fail(RH_ERR_ARG, "NULL");
-    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+    if (n >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
     std::lock_guard<std::mutex> g(s->mu);
     RH_HIP(hipSetDevice(s->device));
     int rc;
@@ -4298,7 +4319,7 @@ int rh_estore_apply(rh_estore *s, const uint64_t *pos, const uint8_t *kinds, siz
         return fail(RH_ERR_OOM, "apply: host allocation failed");
     }
     const uint64_t n_out = at;
-    if (n_out >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded");
+    if (n_out >= (1ull << 31)) return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded: use rh_sstore_* for a larger map");
     RH_HIP(hipSetDevice(s->device));
     int rc;
     const int nxt = 1 - s->cur;

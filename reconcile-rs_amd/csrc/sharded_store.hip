@@ -24,7 +24,9 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <exception>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -37,6 +39,7 @@
 
 namespace rh {
 int set_error(int code, const std::string &msg);  // rsos_hip_abi.hip: the calling thread's rh_last_error
+bool debug_fail_point(const char *name);          // rh_debug_fail_point, armed on the calling thread
 }
 
 namespace {
@@ -61,7 +64,9 @@ class ShardPool {
             w.th.join();
         }
     }
-    // fn(s) for every shard s in `idx` (distinct, ascending); returns when all have finished
+    // fn(s) for every shard s in `idx` (distinct, ascending); returns when all have finished.  An
+    // exception thrown by fn -- on the calling thread or a worker -- is rethrown here, and only
+    // after every posted task has finished (the tasks read the caller's stack).
     void run(const std::vector<int> &idx, const std::function<void(int)> &fn) {
         if (idx.empty()) return;
         if (idx.size() == 1) {
@@ -73,16 +78,24 @@ class ShardPool {
             {
                 std::lock_guard<std::mutex> g(w.mu);
                 w.fn = &fn;
+                w.err = nullptr;
                 w.state.store(1, std::memory_order_release);
             }
             w.cv.notify_one();
         }
-        fn(idx[0]);
+        std::exception_ptr err;
+        try {
+            fn(idx[0]);
+        } catch (...) {
+            err = std::current_exception();
+        }
         for (size_t k = 1; k < idx.size(); k++) {
             Slot &w = slots_[idx[k]];
             wait_for(w, 2);
             w.state.store(0, std::memory_order_relaxed);
+            if (w.err && !err) err = w.err;
         }
+        if (err) std::rethrow_exception(err);
     }
 
   private:
@@ -92,6 +105,7 @@ class ShardPool {
         std::condition_variable cv;
         std::atomic<int> state{0};  // 0 idle, 1 task posted, 2 done
         const std::function<void(int)> *fn = nullptr;
+        std::exception_ptr err;  // what the task threw, handed back to run()
         bool quit = false;
     };
     std::vector<Slot> slots_;
@@ -115,7 +129,11 @@ class ShardPool {
         for (;;) {
             wait_for(w, 1);
             if (w.quit) return;
-            (*w.fn)(i);
+            try {
+                (*w.fn)(i);
+            } catch (...) {
+                w.err = std::current_exception();
+            }
             {
                 std::lock_guard<std::mutex> g(w.mu);
                 w.state.store(2, std::memory_order_release);
@@ -139,6 +157,22 @@ struct Status {
         }
     }
 };
+
+// the status of a task that threw (no exception crosses the C ABI)
+void caught(Status &st) {
+    try {
+        throw;
+    } catch (const std::bad_alloc &) {
+        st.rc = RH_ERR_OOM;
+        st.msg = "sharded store: host allocation failed";
+    } catch (const std::exception &e) {
+        st.rc = RH_ERR_STATE;
+        st.msg = std::string("sharded store: internal error: ") + e.what();
+    } catch (...) {
+        st.rc = RH_ERR_STATE;
+        st.msg = "sharded store: internal error";
+    }
+}
 
 int key_row(const rh_schema &s) {
     switch (s.key_kind) {
@@ -174,20 +208,52 @@ struct rh_sstore {
     std::vector<uint64_t> sizes;    // rows per shard (valid while sizes_ok)
     std::vector<uint64_t> off;      // G + 1 prefix sums of sizes
     bool sizes_ok = false;
+    // each shard's root (the aggregate of its whole key range), cached until the next write: a
+    // key range spanning shards adds the roots of the shards inside it
+    std::vector<rh_aggregate> roots;
+    std::vector<uint8_t> root_ok;
+    bool tier_on = false;  // the shards' host tiers (rh_sstore_set_host_tier): their questions are
+                           // microseconds, asked on the calling thread
+    void changed() {
+        sizes_ok = false;
+        std::fill(root_ok.begin(), root_ok.end(), 0);
+    }
+    int root(int t, rh_aggregate *out) {
+        if (!root_ok[t]) {
+            if (int rc = rh_store_aggregate_keys(shards[t], 0, nullptr, 0, nullptr, &roots[t])) return rc;
+            root_ok[t] = 1;
+        }
+        *out = roots[t];
+        return RH_OK;
+    }
     std::vector<uint8_t> dirty;     // shard has staged rows not yet applied
     std::mutex mu;                  // one call at a time: every answer is one snapshot of every shard
     ShardPool *pool = nullptr;
-    std::vector<uint8_t> round_out;  // the last round's output, round_layout()
+    // Set when a write failed after some shards had committed their part (a device or allocation
+    // failure past the batch's checks): the shards then disagree with any one-store history, so
+    // every call but a load (which replaces the contents) and destroy is refused until a load.
+    std::string broken;
+    int health() const {
+        return broken.empty() ? RH_OK : rh::set_error(RH_ERR_STATE, "sharded store: " + broken + "; load to recover");
+    }
 
     // ---- key order (the key type's Ord: numeric for u32 / u64 keys stored LE, bytewise else) ----
     int cmp(const uint8_t *a, const uint8_t *b) const {
-        if (schema.key_kind == RH_KEY_U32 || schema.key_kind == RH_KEY_U64) {
-            uint64_t x = 0, y = 0;
-            memcpy(&x, a, kl);
-            memcpy(&y, b, kl);
+        switch (schema.key_kind) {
+        case RH_KEY_U64: {
+            uint64_t x, y;
+            memcpy(&x, a, 8);
+            memcpy(&y, b, 8);
             return (x > y) - (x < y);
         }
-        return kl ? memcmp(a, b, kl) : 0;
+        case RH_KEY_U32: {
+            uint32_t x, y;
+            memcpy(&x, a, 4);
+            memcpy(&y, b, 4);
+            return (x > y) - (x < y);
+        }
+        default: return kl ? memcmp(a, b, kl) : 0;
+        }
     }
     const uint8_t *splitter(int j) const { return split.data() + (size_t)j * kl; }
     // the shard holding key z: the number of splitters <= z (bisect_right)
@@ -239,7 +305,13 @@ struct rh_sstore {
         std::vector<Status> ss(G);
         std::vector<int> busy, idle;
         for (int s = 0; s < G; s++) (dirty[s] ? busy : idle).push_back(s);
-        auto len = [&](int s) { ss[s].take(rh_store_len(shards[s], &got[s])); };
+        auto len = [&](int s) {
+            try {
+                ss[s].take(rh_store_len(shards[s], &got[s]));
+            } catch (...) {
+                caught(ss[s]);
+            }
+        };
         pool->run(busy, len);
         for (int s : idle) len(s);
         for (int s = 0; s < G; s++)
@@ -266,9 +338,8 @@ struct rh_sstore {
         pool->run(idx, [&](int s) {
             try {
                 ss[s].take(fn(s));
-            } catch (const std::bad_alloc &) {
-                ss[s].rc = RH_ERR_OOM;
-                ss[s].msg = "sharded store: host allocation failed";
+            } catch (...) {
+                caught(ss[s]);
             }
         });
         for (int s : idx)
@@ -441,14 +512,11 @@ struct rh_sstore {
         });
         if (rc) return rc;
         // the roots of the shards between a segment's two boundary shards
-        std::vector<rh_aggregate> roots;
+        std::vector<rh_aggregate> mid(G, kZero);
         for (size_t t = 0; t < J.size(); t++) {
             local[t] = kZero;
-            if (B[t] > A[t] + 1 && roots.empty()) {
-                roots.assign(G, kZero);
-                for (int s = 0; s < G; s++)
-                    if ((rc = rh_store_aggregate_keys(shards[s], 0, nullptr, 0, nullptr, &roots[s]))) return rc;
-            }
+            for (int s = A[t] + 1; s < B[t]; s++)
+                if ((rc = root(s, &mid[s]))) return rc;
         }
         for (int s : idx) {
             const Job &q = jobs[s];
@@ -460,16 +528,19 @@ struct rh_sstore {
             }
         }
         for (size_t t = 0; t < J.size(); t++)
-            for (int s = A[t] + 1; s < B[t]; s++) agg_add(local[t], roots[s]);
+            for (int s = A[t] + 1; s < B[t]; s++) agg_add(local[t], mid[s]);
         return RH_OK;
     }
 
     // ---- a protocol round --------------------------------------------------------------------
-    // One piece of the round's output: the children and enumerations of a run of segments.
+    // One piece of the round's output: the children and enumerations of a run of segments, either
+    // owned (copied) or borrowed from a shard's own round output (valid until that shard's next call)
     struct Out {
         std::vector<uint8_t> csk, cek, cskeys, cekeys, esk, eek, eskeys, eekeys;
         std::vector<rh_aggregate> caggs;
         uint64_t cnt[5] = {0, 0, 0, 0, 0};  // skipped, enumerated, split, children, dropped
+        bool borrowed = false;
+        rh_segments bc{}, be{};
         void child(uint8_t s, const uint8_t *sk, uint8_t e, const uint8_t *ek, const rh_aggregate &a, size_t kl) {
             csk.push_back(s), cek.push_back(e);
             put(cskeys, s ? sk : nullptr, kl), put(cekeys, e ? ek : nullptr, kl);
@@ -484,7 +555,11 @@ struct rh_sstore {
             v.resize(o + kl, 0);
             if (k) memcpy(v.data() + o, k, kl);
         }
-        // a shard's round, copied out of the shard's buffers (valid until its next call)
+        void count(const rh_round_outcome &o) {
+            cnt[0] += o.skipped, cnt[1] += o.enumerated, cnt[2] += o.split, cnt[3] += o.children,
+                cnt[4] += o.dropped_malformed;
+        }
+        // a shard's round, copied out of the shard's buffers (a shard asked more than once per round)
         void take(const rh_segments &c, const rh_segments &e, const rh_round_outcome &o, size_t kl) {
             auto app = [](std::vector<uint8_t> &v, const void *p, size_t bytes) {
                 if (bytes) v.insert(v.end(), static_cast<const uint8_t *>(p), static_cast<const uint8_t *>(p) + bytes);
@@ -494,91 +569,274 @@ struct rh_sstore {
             if (c.n) caggs.insert(caggs.end(), c.aggregates, c.aggregates + c.n);
             app(esk, e.start_kinds, e.n), app(eek, e.end_kinds, e.n);
             app(eskeys, e.start_keys, e.n * kl), app(eekeys, e.end_keys, e.n * kl);
-            cnt[0] += o.skipped, cnt[1] += o.enumerated, cnt[2] += o.split, cnt[3] += o.children,
-                cnt[4] += o.dropped_malformed;
+            count(o);
+        }
+        // ... or left in place until the round is assembled (a shard asked once)
+        void borrow(const rh_segments &c, const rh_segments &e, const rh_round_outcome &o) {
+            borrowed = true;
+            bc = c, be = e;
+            count(o);
+        }
+        size_t nc() const { return borrowed ? bc.n : csk.size(); }
+        size_t ne() const { return borrowed ? be.n : esk.size(); }
+        // this piece's bytes into the round at children offset c, enumerations offset e
+        void put_into(uint8_t *o, const rh::RoundLayout &L, uint64_t c, uint64_t e, size_t kl) const {
+            auto cp = [](uint8_t *dst, const void *src, size_t bytes) {
+                if (!bytes) return;
+                if (src) memcpy(dst, src, bytes);
+                else memset(dst, 0, bytes);
+            };
+            const size_t pc = nc(), pe = ne();
+            if (pc) {
+                cp(o + L.csk + c, borrowed ? (const void *)bc.start_kinds : csk.data(), pc);
+                cp(o + L.cek + c, borrowed ? (const void *)bc.end_kinds : cek.data(), pc);
+                cp(o + L.cskeys + c * kl, borrowed ? bc.start_keys : cskeys.data(), pc * kl);
+                cp(o + L.cekeys + c * kl, borrowed ? bc.end_keys : cekeys.data(), pc * kl);
+                cp(o + L.caggs + c * sizeof(rh_aggregate), borrowed ? (const void *)bc.aggregates : caggs.data(),
+                   pc * sizeof(rh_aggregate));
+            }
+            if (pe) {
+                cp(o + L.esk + e, borrowed ? (const void *)be.start_kinds : esk.data(), pe);
+                cp(o + L.eek + e, borrowed ? (const void *)be.end_kinds : eek.data(), pe);
+                cp(o + L.eskeys + e * kl, borrowed ? be.start_keys : eskeys.data(), pe * kl);
+                cp(o + L.eekeys + e * kl, borrowed ? be.end_keys : eekeys.data(), pe * kl);
+            }
         }
     };
     struct Run {
         int shard;  // -1: segments that straddle shard boundaries
         size_t j0, j1;
     };
-    int protocol_round(int policy, uint64_t fan_out, const rh_segments &in, rh_segments *ch, rh_segments *en,
-                       rh_round_outcome *oc) {
-        const size_t r = in.n;
+    // The round's output buffer (round_layout()); grown, never zero-filled: every byte a caller
+    // reads through the returned arrays is written by the assembly
+    std::unique_ptr<uint8_t[]> round_buf;
+    size_t round_cap = 0;
+    uint8_t *round_room(size_t bytes) {
+        if (bytes > round_cap) {
+            round_buf.reset(new uint8_t[bytes + bytes / 4]);
+            round_cap = bytes + bytes / 4;
+        }
+        return round_buf.get();
+    }
+
+    // ---- routing a round's segments to the shards --------------------------------------------
+    // Generic: each segment's two boundary shards by binary search over the splitters -- O(r log G)
+    // key comparisons, right for any input.
+    void route_each(const rh_segments &in, std::vector<Run> &runs) const {
         const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
         const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
         const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
-        // maximal runs of consecutive segments with one owning shard
-        std::vector<Run> runs;
-        for (size_t j = 0; j < r; j++) {
+        runs.clear();
+        for (size_t j = 0; j < in.n; j++) {
             int a, b;
             span(sk[j], sk[j] ? skeys + j * kl : nullptr, ek[j], ek[j] ? ekeys + j * kl : nullptr, &a, &b);
             const int s = a == b ? a : -1;
             if (!runs.empty() && runs.back().shard == s && runs.back().j1 == j) runs.back().j1 = j + 1;
             else runs.push_back(Run{s, j, j + 1});
         }
-        std::vector<Out> outs(runs.size());
-        // the runs inside one shard: that shard's own round, the shards concurrently
-        std::vector<std::vector<size_t>> mine(G);
-        std::vector<size_t> cross;
-        for (size_t k = 0; k < runs.size(); k++) {
-            if (runs[k].shard >= 0) mine[runs[k].shard].push_back(k);
-            else
-                for (size_t j = runs[k].j0; j < runs[k].j1; j++) cross.push_back(j);
+    }
+    // Key-ordered input (a round's children are in key order, rbsr/src/protocol.rs:299-317): when
+    // the start bounds and the end bounds are each non-decreasing in j (Unbounded start = -inf,
+    // Unbounded end = +inf), both boundary shards are non-decreasing in j, so each shard's run and
+    // the straddling segments between them are found by 2 (G - 1) binary searches over the
+    // segments -- O(G log r) comparisons.  The order itself is verified in O(r), split between the
+    // shards' tasks (each checks its own run before asking its shard) and the caller (the
+    // straddling runs); any violation falls back to route_each.
+    bool pair_sorted(const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys, size_t j) const {
+        if (sk[j]) {
+            if (sk[j - 1] && cmp(skeys + (j - 1) * kl, skeys + j * kl) > 0) return false;
+        } else if (sk[j - 1]) {
+            return false;
         }
-        std::vector<int> idx;
-        for (int s = 0; s < G; s++)
-            if (!mine[s].empty()) idx.push_back(s);
-        int rc = each(idx, [&](int s) -> int {
-            for (size_t k : mine[s]) {
-                const Run &R = runs[k];
-                const size_t j = R.j0;
-                const rh_segments sub{const_cast<uint8_t *>(sk + j), skeys ? const_cast<uint8_t *>(skeys + j * kl) : nullptr,
-                                      const_cast<uint8_t *>(ek + j), ekeys ? const_cast<uint8_t *>(ekeys + j * kl) : nullptr,
-                                      in.aggregates + j, R.j1 - R.j0, R.j1 - R.j0};
-                rh_segments c{}, e{};
-                rh_round_outcome o{};
-                const int q = rh_store_protocol_round(shards[s], policy, fan_out, &sub, &c, &e, &o);
-                if (q) return q;
-                outs[k].take(c, e, o, kl);
+        if (ek[j - 1]) {
+            if (ek[j] && cmp(ekeys + (j - 1) * kl, ekeys + j * kl) > 0) return false;
+        } else if (ek[j]) {
+            return false;
+        }
+        return true;
+    }
+    // the pairs (j - 1, j) for j in [j0, j1) are ordered
+    bool pairs_sorted(const rh_segments &in, size_t j0, size_t j1) const {
+        const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
+        const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
+        const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
+        for (size_t j = std::max<size_t>(j0, 1); j < j1; j++)
+            if (!pair_sorted(sk, skeys, ek, ekeys, j)) return false;
+        return true;
+    }
+    bool route_sorted(const rh_segments &in, std::vector<Run> &runs) const {
+        const size_t r = in.n;
+        const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
+        const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
+        const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
+        auto first = [r](auto pred) {  // the first j in [0, r) with pred(j), else r (pred monotone)
+            size_t lo = 0, hi = r;
+            while (lo < hi) {
+                const size_t mid = lo + (hi - lo) / 2;
+                if (pred(mid)) hi = mid;
+                else lo = mid + 1;
             }
-            return RH_OK;
-        });
-        if (rc) return rc;
-        if (!cross.empty() && (rc = cross_round(policy, fan_out, in, runs, cross, outs))) return rc;
+            return lo;
+        };
+        // A[s]: the first segment whose start shard is >= s; B[s]: whose end shard is >= s
+        std::vector<size_t> A(G + 1, 0), B(G + 1, 0);
+        A[G] = B[G] = r;
+        for (int t = 1; t < G; t++) {
+            const uint8_t *sp = splitter(t - 1);
+            A[t] = first([&](size_t j) { return sk[j] && cmp(sp, skeys + j * kl) <= 0; });
+            B[t] = first([&](size_t j) { return !ek[j] || cmp(sp, ekeys + j * kl) < 0; });
+        }
+        runs.clear();
+        size_t cur = 0;
+        for (int t = 0; t < G; t++) {
+            const size_t lo = std::max(A[t], B[t]), hi = std::min(A[t + 1], B[t + 1]);
+            if (lo >= hi) continue;
+            if (lo < cur) return false;  // not monotone after all
+            if (cur < lo) runs.push_back(Run{-1, cur, lo});
+            runs.push_back(Run{t, lo, hi});
+            cur = hi;
+        }
+        if (cur < r) runs.push_back(Run{-1, cur, r});
+        // the straddling runs' order is checked here; each shard's by its task
+        for (const Run &R : runs)
+            if (R.shard < 0 && !pairs_sorted(in, R.j0, R.j1)) return false;
+        return true;
+    }
+
+    // RSOS_HIP_SSTORE_DBG=1: one line per protocol round on stderr -- segments, runs, straddling
+    // segments, and the host times of its phases (us): routing, the straddling segments, the
+    // shards' rounds (and the slowest shard's own call), the assembly
+    static bool dbg() {
+        static const bool on = getenv("RSOS_HIP_SSTORE_DBG") && atoi(getenv("RSOS_HIP_SSTORE_DBG")) > 0;
+        return on;
+    }
+    static double now_us() {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    // copying a round's pieces takes the shard threads past this many bytes
+    static constexpr size_t PARALLEL_COPY_BYTES = 1 << 20;
+    int protocol_round(int policy, uint64_t fan_out, const rh_segments &in, rh_segments *ch, rh_segments *en,
+                       rh_round_outcome *oc) {
+        const double t0 = dbg() ? now_us() : 0;
+        std::vector<double> shard_us(dbg() ? G : 0, 0.0);
+        std::vector<Run> runs;
+        bool fast = route_sorted(in, runs);
+        if (!fast) route_each(in, runs);
+        const double t1 = dbg() ? now_us() : 0;
+        double t2 = t1, t3 = t1;
+        std::vector<Out> outs;
+        std::vector<std::vector<size_t>> mine;
+        std::vector<int> idx;
+        const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
+        const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
+        const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
+        for (int pass = 0; pass < 2; pass++) {
+            outs.assign(runs.size(), Out{});
+            mine.assign(G, {});
+            std::vector<size_t> cross;
+            for (size_t k = 0; k < runs.size(); k++) {
+                if (runs[k].shard >= 0) mine[runs[k].shard].push_back(k);
+                else
+                    for (size_t j = runs[k].j0; j < runs[k].j1; j++) cross.push_back(j);
+            }
+            idx.clear();
+            for (int s = 0; s < G; s++)
+                if (!mine[s].empty()) idx.push_back(s);
+            // the straddling segments first: their shard calls come before the shards' own rounds,
+            // whose outputs then stay in place until the round is assembled
+            int rc;
+            if (!cross.empty() && (rc = cross_round(policy, fan_out, in, runs, cross, outs))) return rc;
+            t2 = dbg() ? now_us() : 0;
+            std::atomic<bool> unsorted{false};
+            rc = each(idx, [&](int s) -> int {
+                const double u0 = dbg() ? now_us() : 0;
+                struct Clock {  // the shard's own time, however the task ends
+                    std::vector<double> &v;
+                    int s;
+                    double u0;
+                    ~Clock() {
+                        if (!v.empty()) v[s] = now_us() - u0;
+                    }
+                } clk{shard_us, s, u0};
+                if (fast && !pairs_sorted(in, runs[mine[s][0]].j0, runs[mine[s][0]].j1)) {
+                    unsorted = true;
+                    return RH_OK;
+                }
+                for (size_t k : mine[s]) {
+                    const Run &R = runs[k];
+                    const size_t j = R.j0;
+                    const rh_segments sub{const_cast<uint8_t *>(sk + j), skeys ? const_cast<uint8_t *>(skeys + j * kl) : nullptr,
+                                          const_cast<uint8_t *>(ek + j), ekeys ? const_cast<uint8_t *>(ekeys + j * kl) : nullptr,
+                                          in.aggregates + j, R.j1 - R.j0, R.j1 - R.j0};
+                    rh_segments c{}, e{};
+                    rh_round_outcome o{};
+                    const int q = rh_store_protocol_round(shards[s], policy, fan_out, &sub, &c, &e, &o);
+                    if (q) return q;
+                    if (mine[s].size() == 1) outs[k].borrow(c, e, o);
+                    else outs[k].take(c, e, o, kl);
+                }
+                return RH_OK;
+            });
+            if (rc) return rc;
+            t3 = dbg() ? now_us() : 0;
+            if (!unsorted) break;
+            fast = false;  // the input was not key-ordered after all: route each segment
+            route_each(in, runs);
+        }
         // the pieces in segment order, in round_layout()
         uint64_t nc = 0, ne = 0, cnt[5] = {0, 0, 0, 0, 0};
         for (const Out &o : outs) {
-            nc += o.csk.size(), ne += o.esk.size();
+            nc += o.nc(), ne += o.ne();
             for (int i = 0; i < 5; i++) cnt[i] += o.cnt[i];
         }
-        const rh::RoundLayout L = rh::round_layout(nc, ne, kl);
-        round_out.assign(L.end, 0);
-        uint8_t *o = round_out.data();
-        uint64_t c = 0, e = 0;
-        for (const Out &p : outs) {
-            const size_t pc = p.csk.size(), pe = p.esk.size();
-            if (pc) {
-                memcpy(o + L.csk + c, p.csk.data(), pc);
-                memcpy(o + L.cek + c, p.cek.data(), pc);
-                memcpy(o + L.cskeys + c * kl, p.cskeys.data(), pc * kl);
-                memcpy(o + L.cekeys + c * kl, p.cekeys.data(), pc * kl);
-                memcpy(o + L.caggs + c * sizeof(rh_aggregate), p.caggs.data(), pc * sizeof(rh_aggregate));
+        if (oc) *oc = rh_round_outcome{cnt[0], cnt[1], cnt[2], cnt[3], cnt[4]};
+        if (outs.size() == 1 && outs[0].borrowed) {  // one shard's round is the whole round: in place
+            *ch = outs[0].bc;
+            *en = outs[0].be;
+            ch->cap = ch->n, en->cap = en->n;
+            if (!ch->n) *ch = rh_segments{};
+            if (!en->n) *en = rh_segments{};
+        } else {
+            const rh::RoundLayout L = rh::round_layout(nc, ne, kl);
+            uint8_t *o = round_room(L.end);
+            std::vector<uint64_t> at_c(outs.size()), at_e(outs.size());
+            uint64_t c = 0, e = 0;
+            for (size_t k = 0; k < outs.size(); k++) {
+                at_c[k] = c, at_e[k] = e;
+                c += outs[k].nc(), e += outs[k].ne();
             }
-            if (pe) {
-                memcpy(o + L.esk + e, p.esk.data(), pe);
-                memcpy(o + L.eek + e, p.eek.data(), pe);
-                memcpy(o + L.eskeys + e * kl, p.eskeys.data(), pe * kl);
-                memcpy(o + L.eekeys + e * kl, p.eekeys.data(), pe * kl);
+            memset(o, 0, 64);
+            memcpy(o, cnt, sizeof cnt);
+            if (L.end > PARALLEL_COPY_BYTES && idx.size() > 1) {
+                // each shard's thread copies its own pieces (the straddling ones go with shard 0's task)
+                int rc = each(idx, [&](int s) -> int {
+                    for (size_t k : mine[s]) outs[k].put_into(o, L, at_c[k], at_e[k], kl);
+                    if (s == idx[0])
+                        for (size_t k = 0; k < runs.size(); k++)
+                            if (runs[k].shard < 0) outs[k].put_into(o, L, at_c[k], at_e[k], kl);
+                    return RH_OK;
+                });
+                if (rc) return rc;
+            } else {
+                for (size_t k = 0; k < outs.size(); k++) outs[k].put_into(o, L, at_c[k], at_e[k], kl);
             }
-            c += pc, e += pe;
+            *ch = rh_segments{o + L.csk, o + L.cskeys, o + L.cek, o + L.cekeys, reinterpret_cast<rh_aggregate *>(o + L.caggs),
+                              (size_t)nc, (size_t)nc};
+            *en = rh_segments{o + L.esk, o + L.eskeys, o + L.eek, o + L.eekeys, nullptr, (size_t)ne, (size_t)ne};
         }
-        const uint64_t h[5] = {cnt[0], cnt[1], cnt[2], cnt[3], cnt[4]};
-        memcpy(o, h, sizeof h);
-        if (oc) *oc = rh_round_outcome{h[0], h[1], h[2], h[3], h[4]};
-        *ch = rh_segments{o + L.csk, o + L.cskeys, o + L.cek, o + L.cekeys, reinterpret_cast<rh_aggregate *>(o + L.caggs),
-                          (size_t)nc, (size_t)nc};
-        *en = rh_segments{o + L.esk, o + L.eskeys, o + L.eek, o + L.eekeys, nullptr, (size_t)ne, (size_t)ne};
+        if (dbg()) {
+            const double t4 = now_us();
+            size_t ncross = 0;
+            for (const Run &R : runs)
+                if (R.shard < 0) ncross += R.j1 - R.j0;
+            fprintf(stderr,
+                    "{\"sstore_round\": %zu, \"sorted\": %d, \"runs\": %zu, \"cross\": %zu, \"shards\": %zu, "
+                    "\"route_us\": %.1f, \"cross_us\": %.1f, \"shards_us\": %.1f, \"slowest_shard_us\": %.1f, "
+                    "\"assemble_us\": %.1f, \"children\": %llu}\n",
+                    in.n, (int)fast, runs.size(), ncross, idx.size(), t1 - t0, t2 - t1, t3 - t2,
+                    shard_us.empty() ? 0.0 : *std::max_element(shard_us.begin(), shard_us.end()), t4 - t3,
+                    (unsigned long long)nc);
+        }
         return RH_OK;
     }
     // The segments that straddle a shard boundary: resolved from their boundary shards, decided on
@@ -656,6 +914,7 @@ namespace {
 
 int lock_sizes(rh_sstore *s, std::unique_lock<std::mutex> &g) {
     g = std::unique_lock<std::mutex>(s->mu);
+    if (int rc = s->health()) return rc;
     Status st = s->flush();
     return st.rc ? fail(st.rc, st.msg) : RH_OK;
 }
@@ -685,6 +944,8 @@ int rh_sstore_create(const int *devices, int n, const rh_schema *schema, rh_ssto
     s->off.assign(n + 1, 0);
     s->sizes_ok = true;
     s->dirty.assign(n, 0);
+    s->roots.assign(n, kZero);
+    s->root_ok.assign(n, 0);
     s->even_splitters();
     try {
         s->pool = new ShardPool(n);
@@ -758,7 +1019,8 @@ int rh_sstore_load(rh_sstore *s, const rh_columns *h, size_t n) {
                           static_cast<const uint8_t *>(at(h->tags, 1)), at(h->values, vr)};
     };
     int rc = RH_OK;
-    s->sizes_ok = false;
+    s->changed();
+    s->broken.clear();
     std::fill(s->dirty.begin(), s->dirty.end(), 0);
     if (!ok) {
         rc = fail(RH_ERR_ARG, "keys must be strictly increasing (sorted, no duplicates)");
@@ -793,28 +1055,35 @@ int rh_sstore_stage(rh_sstore *s, const rh_columns *h, const uint8_t *ops, size_
     if (m == 0) return RH_OK;
     if (s->kl && !h->keys) return fail(RH_ERR_ARG, "keys column is NULL");
     std::lock_guard<std::mutex> g(s->mu);
+    int rc;
+    if ((rc = s->health())) return rc;
     const uint8_t *keys = static_cast<const uint8_t *>(h->keys);
     for (size_t i = 0; i < m; i++)
         if (ops[i] > 1) return fail(RH_ERR_ARG, "op must be 0 (insert) or 1 (delete)");
-    int rc;
     if (m == 1 || s->G == 1) {  // the Rsos::insert path: one row, no copies
         const int t = s->G == 1 ? 0 : s->owner(keys);
         if ((rc = rh_store_stage(s->shards[t], h, ops, m))) return rc;
         s->dirty[t] = 1;
-        s->sizes_ok = false;
+        s->changed();
         return RH_OK;
     }
     try {
         std::vector<std::vector<uint32_t>> rows;
         s->route(keys, m, rows);
+        std::vector<rh_sstore::Part> parts(s->G);
+        for (int t = 0; t < s->G; t++)  // every copy made before any shard takes a row
+            if (!rows[t].empty()) s->gather(*h, ops, rows[t], parts[t]);
+        int staged = 0;
         for (int t = 0; t < s->G; t++) {
             if (rows[t].empty()) continue;
-            rh_sstore::Part p;
-            s->gather(*h, ops, rows[t], p);
-            const rh_columns c = p.cols();
-            if ((rc = rh_store_stage(s->shards[t], &c, p.ops.data(), p.m))) return rc;
+            const rh_columns c = parts[t].cols();
+            if ((rc = rh_store_stage(s->shards[t], &c, parts[t].ops.data(), parts[t].m))) {
+                if (staged) s->broken = "a staged batch was refused by one shard after others had taken their rows";
+                return rc;
+            }
+            staged++;
             s->dirty[t] = 1;
-            s->sizes_ok = false;
+            s->changed();
         }
     } catch (const std::bad_alloc &) {
         return fail(RH_ERR_OOM, "stage: host allocation failed");
@@ -829,6 +1098,15 @@ int rh_sstore_apply(rh_sstore *s, const rh_columns *h, const uint8_t *ops, size_
     std::unique_lock<std::mutex> g;
     int rc = lock_sizes(s, g);  // staged rows first: they were staged before this batch
     if (rc) return rc;
+    // every check a shard's apply makes on the arguments, made here before any shard changes
+    for (size_t i = 0; i < m; i++)
+        if (ops[i] > 1) return fail(RH_ERR_ARG, "op must be 0 (insert) or 1 (delete)");
+    if (m) {
+        const rh_schema &sc = s->schema;
+        if (sc.value_kind != RH_VAL_UNIT && !h->values) return fail(RH_ERR_ARG, "values column is NULL");
+        if (sc.record_kind == RH_REC_DATED && (!h->phys || !h->logical || !h->node))
+            return fail(RH_ERR_ARG, "DATED records need phys / logical / node columns");
+    }
     uint64_t c[64][3] = {};
     try {
         std::vector<std::vector<uint32_t>> rows;
@@ -847,11 +1125,22 @@ int rh_sstore_apply(rh_sstore *s, const rh_columns *h, const uint8_t *ops, size_
             return rc;
         for (int t : idx)
             if (dup[t]) return fail(RH_ERR_ARG, "duplicate key within one batch");
-        s->sizes_ok = false;
+        for (int t : idx)  // the row cap, counting every row as new
+            if (s->sizes[t] + parts[t].m >= (1ull << 31))
+                return fail(RH_ERR_ARG, "store size limit (2^31 rows) exceeded in one shard: use more shards");
+        s->changed();
+        const bool inject = rh::debug_fail_point("sstore.apply_last_shard");
         rc = s->each(idx, [&](int t) -> int {
+            if (inject && t == idx.back()) return rh::set_error(RH_ERR_OOM, "injected failure (sstore apply)");
             const rh_columns cols = parts[t].cols();
             return rh_store_apply(s->shards[t], &cols, parts[t].ops.data(), parts[t].m, &c[t][0], &c[t][1], &c[t][2]);
         });
+        if (rc) {
+            // past the checks above only a device or allocation failure remains; with more than one
+            // shard written the others may have committed their part
+            if (idx.size() > 1) s->broken = "an apply failed in one shard after others may have committed their rows";
+            return rc;
+        }
     } catch (const std::bad_alloc &) {
         return fail(RH_ERR_OOM, "apply: host allocation failed");
     }
@@ -861,7 +1150,7 @@ int rh_sstore_apply(rh_sstore *s, const rh_columns *h, const uint8_t *ops, size_
     if (n_new) *n_new = tot[0];
     if (n_over) *n_over = tot[1];
     if (n_del) *n_del = tot[2];
-    return rc;
+    return RH_OK;
 }
 
 int rh_sstore_len(rh_sstore *s, uint64_t *out) {
@@ -901,16 +1190,26 @@ int rh_sstore_aggregate_keys(rh_sstore *s, int lo_kind, const void *lo_key, int 
     const int b = !hi_kind ? s->G - 1 : hi_kind == 1 ? s->owner(hk) : s->owner_below(hk);
     *out = kZero;
     if (a > b) return RH_OK;  // an inverted or empty range: ZERO (rbsr/src/protocol.rs:230-232)
-    std::vector<rh_aggregate> part(s->G, kZero);
-    std::vector<int> edge{a};
-    if (b != a) edge.push_back(b);
-    rc = s->each(edge, [&](int t) -> int {
-        return rh_store_aggregate_keys(s->shards[t], t == a ? lo_kind : 0, lo_key, t == b ? hi_kind : 0, hi_key, &part[t]);
-    });
-    if (rc) return rc;
-    for (int t = a + 1; t < b; t++)
-        if ((rc = rh_store_aggregate_keys(s->shards[t], 0, nullptr, 0, nullptr, &part[t]))) return rc;
-    for (int t = a; t <= b; t++) agg_add(*out, part[t]);
+    if (a == b) return rh_store_aggregate_keys(s->shards[a], lo_kind, lo_key, hi_kind, hi_key, out);
+    // the two edge shards (each asked one bound) and the cached roots of the shards between them;
+    // host-tier edges on the calling thread (a thread handoff would cost more than the question)
+    rh_aggregate part[2] = {kZero, kZero};
+    auto edge = [&](int t) -> int {
+        return t == a ? rh_store_aggregate_keys(s->shards[a], lo_kind, lo_key, 0, nullptr, &part[0])
+                      : rh_store_aggregate_keys(s->shards[b], 0, nullptr, hi_kind, hi_key, &part[1]);
+    };
+    if (s->tier_on) {
+        if ((rc = edge(a)) || (rc = edge(b))) return rc;
+    } else if ((rc = s->each({a, b}, edge))) {
+        return rc;
+    }
+    agg_add(*out, part[0]);
+    for (int t = a + 1; t < b; t++) {
+        rh_aggregate m;
+        if ((rc = s->root(t, &m))) return rc;
+        agg_add(*out, m);
+    }
+    agg_add(*out, part[1]);
     return RH_OK;
 }
 
@@ -1076,7 +1375,10 @@ int rh_sstore_protocol_round(rh_sstore *s, int policy, uint64_t fan_out, const r
 int rh_sstore_set_host_tier(rh_sstore *s, int enable, uint64_t round_max) {
     if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
     std::lock_guard<std::mutex> g(s->mu);
-    return s->each(s->all(), [&](int t) -> int { return rh_store_set_host_tier(s->shards[t], enable, round_max); });
+    if (enable < 0 || enable > 1) return fail(RH_ERR_ARG, "bad host tier setting");
+    const int rc = s->each(s->all(), [&](int t) -> int { return rh_store_set_host_tier(s->shards[t], enable, round_max); });
+    s->tier_on = rc == RH_OK ? enable == 1 : false;
+    return rc;
 }
 
 int rh_sstore_set_tier_policy(rh_sstore *s, int keep_fresh) {
@@ -1095,7 +1397,7 @@ int rh_sstore_reserve(rh_sstore *s, uint64_t rows, uint64_t batch_rows) {
 int rh_sstore_compact(rh_sstore *s) {
     if (!s) return fail(RH_ERR_ARG, "sstore is NULL");
     std::lock_guard<std::mutex> g(s->mu);
-    s->sizes_ok = false;
+    s->changed();
     return s->each(s->all(), [&](int t) -> int { return rh_store_compact(s->shards[t]); });
 }
 

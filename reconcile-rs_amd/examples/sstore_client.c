@@ -104,8 +104,15 @@ static void blob_put(blob_t *b, const void *p, size_t n) {
     b->len += n;
 }
 
+/* per-round times of `a`'s rounds in the last timed reconciliation (detail mode) */
+#define MAX_ROUNDS 64
+static double round_us[MAX_ROUNDS];
+static uint64_t round_r[MAX_ROUNDS];
+static int n_timed;
+
 /* a whole reconciliation of `a` with the peer; every round's outputs appended to `log` */
 static uint64_t reconcile(map_t a, rh_store *peer, blob_t *log) {
+    n_timed = 0;
     size_t cap = 16, n = 1;
     uint8_t *sk = calloc(cap, 1), *ek = calloc(cap, 1);
     uint64_t *skey = calloc(cap, 8), *ekey = calloc(cap, 8);
@@ -118,7 +125,11 @@ static uint64_t reconcile(map_t a, rh_store *peer, blob_t *log) {
         rh_segments ch, en;
         rh_round_outcome oc;
         if (peer_turn) CHECK(rh_store_protocol_round(peer, RH_POLICY_FIXED_FAN_OUT, 16, &in, &ch, &en, &oc));
-        else CHECK(m_round(a, &in, &ch, &en, &oc));
+        else {
+            const double t0 = now_s();
+            CHECK(m_round(a, &in, &ch, &en, &oc));
+            if (n_timed < MAX_ROUNDS) round_us[n_timed] = (now_s() - t0) * 1e6, round_r[n_timed++] = n;
+        }
         rounds++;
         if (log) {
             blob_put(log, &oc, sizeof oc);
@@ -254,14 +265,19 @@ int main(int argc, char **argv) {
     }
     compare(S, O, peer, n + bm + 6000);
     /* timing: whole reconciliations with the peer, the sharded map and the single store */
-    double ts = 0, to = 0;
+    double ts = 0, to = 0, rs[MAX_ROUNDS] = {0}, ro[MAX_ROUNDS] = {0};
+    uint64_t rr[MAX_ROUNDS] = {0};
+    int nr = 0;
     for (int r = 0; r < reps; r++) {
         double t0 = now_s();
         reconcile(S, peer, NULL);
         ts += now_s() - t0;
+        for (int i = 0; i < n_timed; i++) rs[i] += round_us[i], rr[i] = round_r[i];
+        nr = n_timed;
         t0 = now_s();
         reconcile(O, peer, NULL);
         to += now_s() - t0;
+        for (int i = 0; i < n_timed; i++) ro[i] += round_us[i];
     }
     const int q = 100000;
     double t0 = now_s();
@@ -282,6 +298,11 @@ int main(int argc, char **argv) {
            "\"aggregate_ns_sharded\": %.1f, \"aggregate_ns_single\": %.1f, \"sink\": %llu}\n",
            G, (unsigned long long)n, (unsigned long long)d, tier, reps, (unsigned long long)rounds,
            reps ? ts / reps * 1e6 : 0.0, reps ? to / reps * 1e6 : 0.0, agg_s, agg_o, (unsigned long long)(sink & 1));
+    if (getenv("SSTORE_ROUNDS")) {  /* this map's rounds: segments in, mean us sharded / single */
+        for (int i = 0; i < nr; i++)
+            printf("{\"round\": %d, \"segments\": %llu, \"us_sharded\": %.1f, \"us_single\": %.1f}\n", i,
+                   (unsigned long long)rr[i], reps ? rs[i] / reps : 0.0, reps ? ro[i] / reps : 0.0);
+    }
     CHECK(rh_sstore_destroy(ss));
     CHECK(rh_store_destroy(one));
     CHECK(rh_store_destroy(peer));

@@ -41,7 +41,12 @@ class _Shard(GpuFingerprintStore):
         self._h = handle
 
     def close(self) -> None:
-        self._h = None
+        self._h = None  # borrowed: the sharded store destroys it
+
+    def _f(self, name):
+        if self._h is None:
+            raise ValueError("shard of a closed ShardedStore")
+        return GpuFingerprintStore._f(self, name)
 
 
 class ShardedStore(GpuFingerprintStore):
@@ -63,6 +68,13 @@ class ShardedStore(GpuFingerprintStore):
             self.shards.append(_Shard(schema, sh))
         if DEFAULT_HOST_TIER if host_tier is None else host_tier:
             self.set_host_tier(True)
+
+    def close(self) -> None:
+        """Destroy the sharded store and every shard's store: the _Shard views (and any the caller
+        kept) are detached first, so a later call on one raises instead of reaching freed memory."""
+        for sh in getattr(self, "shards", []):
+            sh.close()
+        GpuFingerprintStore.close(self)
 
     # ---- the partition -------------------------------------------------------------------
     @property

@@ -7,6 +7,8 @@ use std::os::raw::{c_char, c_int, c_void};
 pub const RH_ABI_VERSION: c_int = 1;
 pub const RH_BLOCK: usize = 256;
 pub const RH_SUPER: usize = 65536;
+/// One `rh_store` holds fewer than this many rows (`include/rsos_hip.h`, "Row cap").
+pub const RH_STORE_MAX_ROWS: u64 = 2147483648;
 pub const RH_OK: c_int = 0;
 pub const RH_KEY_UNIT: i32 = 0;
 pub const RH_KEY_U32: i32 = 1;

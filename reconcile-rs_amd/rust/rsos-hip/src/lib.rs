@@ -141,6 +141,13 @@ pub fn default_device() -> i32 {
 }
 
 /// `Rsos<K>` on an MI355X.  No bounds on the type: the methods carry them.
+///
+/// Row cap: one map holds fewer than [`ffi::RH_STORE_MAX_ROWS`] (2^31) rows, the limit of one
+/// `rh_store` (`include/rsos_hip.h`, "Row cap").  A load, batch or insert that would pass it
+/// panics with the library's message (`store size limit (2^31 rows) exceeded`) and leaves the
+/// map unchanged.  `Rsos::size()` is a `usize` (`rsos/src/rsos_trait.rs:44`): a map of 2^31 rows
+/// or more is a [`HipShardedMap`], every shard under the cap (one MI355X holds ~2.1 x 10^9 rows
+/// of 16 B keys, so one device can hold several shards).
 pub struct HipFingerprintMap<K, V> {
     store: StoreHandle,
     /// rank-ordered host index (owns K and V; select / enumerate borrow from it)

@@ -13,6 +13,9 @@
 #                     one bench.py line each (the default is configs[3] at N = 1)
 #   prof_config4      rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE and VALU passes of the
 #                     default line at $RECORDS (100 M unless set), summarised into <tag>_*.json
+#   prof_cfg          the same four passes for $CFG at $RECORDS, summarised into <tag>_{traffic,valu}_$CFG.json
+#   config3_full      configs[2] at its stated size (100 M x 1 KiB) with its CPU baseline
+#   sstore_rounds     sstore_client at 4 / 8 shards, d = 100 / 1, tier on, with per-round times
 #   prof_config5      kernel stats + the per-dispatch DRAM byte passes of config5
 #   prof_rbsr         kernel stats of the rbsr line
 #   latency_tier latency_off
@@ -98,6 +101,23 @@ for step in "$@"; do
         cp "$O/stats_c4_$R/run_kernel_stats.csv" "$O/${TAG}_config4_${R}_kernel_stats.csv"
         rm -f "$O"/*_c4_$R/*_kernel_trace.csv "$O"/*_c4_$R/*_counter_collection.csv
         ;;
+    prof_cfg)  # kernel stats + FETCH_SIZE / WRITE_SIZE + VALU passes of one line: $CFG at $RECORDS
+        C=${CFG:?} R=$RECORDS
+        B="python3 bench.py --config $C --records $R --steps 10 --warmup 3 --cpu-baseline 0 --check 0 --e2e 0"
+        run stats_$C 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_$C" -o run -- $B
+        run fetch_$C 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_lift --output-format csv -d "$O/fetch_$C" -o run -- $B
+        run write_$C 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_lift --output-format csv -d "$O/write_$C" -o run -- $B
+        run valu_$C 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex k_lift --output-format csv -d "$O/valu_$C" -o run -- $B
+        python3 scripts/pmc_traffic.py "$O/fetch_$C/run_counter_collection.csv" "$O/write_$C/run_counter_collection.csv" $C "$R" "$O/${TAG}_traffic_$C.json" || exit 1
+        python3 scripts/pmc_valu.py "$O/valu_$C/run_counter_collection.csv" "$O/stats_$C/run_kernel_stats.csv" $C "$R" "$O/${TAG}_valu_$C.json" || exit 1
+        cp "$O/stats_$C/run_kernel_stats.csv" "$O/${TAG}_${C}_kernel_stats.csv"
+        rm -f "$O"/*_$C/*_kernel_trace.csv "$O"/*_$C/*_counter_collection.csv
+        ;;
+    sstore_dbg)  # 4 / 8 shards, d = 100, tier on, 3 reps: the sharded rounds' phases and every store's round times
+        for g in 4 8; do
+            run sstore_dbg_g$g 200 env SSTORE_ROUNDS=1 RSOS_HIP_SSTORE_DBG=1 RSOS_HIP_ROUND_DBG=2 $EX/sstore_client $g 2000000 100 1 3 || exit 1
+        done ;;
+    config3_full) run config3_full 600 python3 bench.py --config config3_full ;;
     prof_config5)
         run stats_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c5" -o run -- python3 bench.py --config config5 --cpu-baseline 0
         cp "$O/stats_c5/run_kernel_stats.csv" "$O/${TAG}_config5_kernel_stats.csv"
@@ -163,6 +183,12 @@ for step in "$@"; do
         rm -rf "$O/trint"
         ;;
     sstore) run sstore 300 $EX/sstore_client 4 2000000 ;;
+    sstore_rounds)  # 4 and 8 shards, d = 100 and 1, tier on: whole drives, aggregates and per-round times
+        for g in 4 8; do
+            for d in 100 1; do
+                run sstore_g${g}_d${d} 200 env SSTORE_ROUNDS=1 $EX/sstore_client $g 2000000 $d 1 20 || exit 1
+            done
+        done ;;
     sstore_ab)  # the shard threads' spin before sleeping, d = 1 and 100, tier on and off
         for sp in 50 300 2000; do
             for d in 1 100; do

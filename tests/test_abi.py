@@ -164,6 +164,31 @@ def test_apply_device_many_argument_checks(rsos_hip_lib):
     assert L.rh_store_apply_device_many(None, None, None, None, 3, None, None) == A.ERR_ARG
 
 
+def test_store_row_cap_is_refused_at_the_boundary(rsos_hip_lib):
+    """One rh_store holds fewer than 2^31 rows (include/rsos_hip.h "Row cap"; the reference's
+    Rsos::size() is a usize, rsos/src/rsos_trait.rs:44).  A reservation or load of 2^31 rows is
+    refused with RH_ERR_ARG and a message naming the sharded store, before any device is touched
+    (the cap is checked on the arguments first), and the header and the Rust FFI state it."""
+    from rsos_hip import _abi as A
+    L = A.lib()
+    for rows, batch in ((1 << 31, 0), (10, 1 << 31), (1 << 40, 0)):
+        assert L.rh_store_reserve(None, rows, batch) == A.ERR_ARG
+        msg = L.rh_last_error().decode()
+        assert "2^31 rows" in msg and "rh_sstore" in msg, msg
+    cols = A.Columns()
+    assert L.rh_store_load(None, C.byref(cols), 1 << 31) == A.ERR_ARG
+    assert "2^31 rows" in L.rh_last_error().decode()
+    assert L.rh_store_load_device(None, C.byref(cols), 1 << 31, None) == A.ERR_ARG
+    assert "2^31 rows" in L.rh_last_error().decode()
+    assert L.rh_store_reserve(None, (1 << 31) - 1, 0) == A.ERR_ARG  # under the cap: the NULL store
+    assert "NULL" in L.rh_last_error().decode()
+    header = open(HEADER).read()
+    assert "#define RH_STORE_MAX_ROWS 2147483648" in header and "Row cap" in header
+    ffi = open(os.path.join(ROOT, "reconcile-rs_amd", "rust", "rsos-hip", "src", "ffi.rs")).read()
+    assert "pub const RH_STORE_MAX_ROWS: u64 = 2147483648;" in ffi
+    assert "2³¹" in open(os.path.join(ROOT, "INTEGRATION.md")).read()
+
+
 # ---- the Rust FFI block against the header, signature by signature -------------------------------
 # (the crate cannot be compiled in this image: no cargo / rustc, SURVEY.md §0 C5; this is the check a
 # compiler would make at the boundary -- arity, pointer depth and constness, integer width)

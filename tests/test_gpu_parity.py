@@ -1484,6 +1484,49 @@ def test_host_tier_nowait_run_refresh_equals_device_answers(gpu, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_host_tier_nowait_steady_write_stream(gpu, monkeypatch):
+    """Writes that never wait, back to back with no question between them: a run copy
+    a write lands on is discarded, and after RUN_DISCARD_MAX such discards in a row the next write
+    takes a base refresh instead (its batches logged and replayed: rsos_hip_abi.hip refresh_now).
+    Whatever landed, every answer during and after the stream is the device's, and the tier is
+    fresh again once the stream stops (tier_sync)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema
+    from rsos_hip.store import KeyRange
+    from rsos_hip.synth import make_records, to_host
+    monkeypatch.setenv("RSOS_HIP_TIER_TREE", "2000")
+    monkeypatch.setenv("RSOS_HIP_TIER_SYNC", "0")
+    s = RecordSchema.dated("bytes16", "bytes64")
+    n = 300_000
+    base = make_records(s, n, seed=43)
+    dev, tier = GpuFingerprintStore(s, host_tier=False), GpuFingerprintStore(s, host_tier=True)
+    for st in (dev, tier):
+        st.load_bulk_device(base)
+    tier.tier_sync()
+    rng = np.random.default_rng(23)
+    keys = [to_host(base)["keys"]]
+    for k in range(24):
+        b = make_records(s, 8_000 + 500 * k, seed=800 + k, random_keys=True)
+        assert tier.apply_device(b) == dev.apply_device(b)
+        keys.append(to_host(b)["keys"])
+        if k % 6 == 5:  # now and then a few questions mid-stream (stale or fresh: the device's answers)
+            pool = np.concatenate(keys)
+            ks = np.ascontiguousarray(pool[rng.integers(0, len(pool), 64)])
+            assert np.array_equal(tier.ranks(ks), dev.ranks(ks))
+            assert tier.aggregate() == dev.aggregate()
+    tier.tier_sync()
+    st = tier.tier_stats()
+    assert st["base_rows"] > 0, st  # fresh (a stale tier reports 0)
+    assert tier.size() == dev.size() and tier.aggregate() == dev.aggregate()
+    for _ in range(40):
+        r = int(rng.integers(0, dev.size()))
+        assert tier.select(r) == dev.select(r)
+        a, b2 = dev.select(int(rng.integers(0, dev.size()))), dev.select(int(rng.integers(0, dev.size())))
+        assert tier.aggregate(KeyRange(a, b2)) == dev.aggregate(KeyRange(a, b2))
+    for st_ in (dev, tier):
+        st_.close()
+
+
+@pytest.mark.gpu
 def test_host_tier_run_copy_equals_device_answers(gpu, monkeypatch):
     """Batches too large for the tier's tree (RSOS_HIP_TIER_TREE=2000 here, read at store creation)
     take a copy of the device's delta run instead of a refresh of the whole base

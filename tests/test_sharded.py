@@ -257,5 +257,46 @@ def test_sharded_edge_cases(gpu, oracle_lib):
              np.zeros(40, np.uint8))
     assert sh.sizes() == [10, 10, 10, 10]
     assert sh.aggregate(KeyRange(10, 30)).size == 20 and sh.rank(25) == 25 and sh.select(31) == 31
+    # a bad op anywhere in a batch spanning every shard is refused before any shard changes
+    before = (sh.aggregate(), sh.sizes())
+    ops = np.zeros(40, np.uint8)
+    ops[33] = 2
+    with pytest.raises(A.RsosHipError) as e:
+        sh.apply({"keys": keys.view(np.uint8).reshape(-1, 8), "values": (vals + 1).view(np.uint8).reshape(-1, 8)}, ops)
+    assert e.value.code == A.ERR_ARG and (sh.aggregate(), sh.sizes()) == before
     for s in (one, peer, sh):
         s.close()
+
+
+@pytest.mark.gpu
+def test_sharded_failed_apply_is_sticky_until_a_load(gpu):
+    """A device or allocation failure in one shard's part of a batch, after the batch's checks, may
+    leave the other shards' parts committed: the sharded store then refuses every call with
+    RH_ERR_STATE (never a half-applied answer) until a load replaces the contents.  Closing the
+    store detaches the shard views."""
+    from rsos_hip import RecordSchema, _abi as A
+    from rsos_hip.sharded import ShardedStore
+    sch = RecordSchema.plain("u64", "u64")
+    sh = ShardedStore(sch, [0] * G)
+    keys = np.arange(4000, dtype=np.uint64)
+    cols = {"keys": keys.view(np.uint8).reshape(-1, 8), "values": (keys * 3).view(np.uint8).reshape(-1, 8)}
+    sh.load_bulk(cols)
+    root = sh.aggregate()
+    batch = {"keys": keys[::7].copy().view(np.uint8).reshape(-1, 8),
+             "values": (keys[::7] * 5).view(np.uint8).reshape(-1, 8)}
+    A.lib().rh_debug_fail_point(b"sstore.apply_last_shard")
+    with pytest.raises(A.RsosHipError) as e:
+        sh.apply(batch, np.zeros(len(keys[::7]), np.uint8))
+    A.lib().rh_debug_fail_point(b"")
+    assert e.value.code == A.ERR_OOM
+    for call in (sh.size, sh.aggregate, lambda: sh.rank(5), lambda: sh.select(0)):
+        with pytest.raises(A.RsosHipError) as e:
+            call()
+        assert e.value.code == A.ERR_STATE and "load to recover" in str(e.value)
+    sh.load_bulk(cols)
+    assert sh.size() == 4000 and sh.aggregate() == root
+    shard0 = sh.shards[0]
+    assert shard0.size() == 1000
+    sh.close()
+    with pytest.raises(ValueError):
+        shard0.size()

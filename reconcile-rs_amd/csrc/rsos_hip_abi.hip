@@ -2847,11 +2847,32 @@ struct rh_store {
     static constexpr size_t kDirectMax = 256ull << 20;  // mapped output sized for the worst case up to this
     int round_copyout = getenv("RSOS_HIP_ROUND_COPYOUT") ? atoi(getenv("RSOS_HIP_ROUND_COPYOUT")) : 2;
     int round_copyin = getenv("RSOS_HIP_ROUND_COPYIN") ? atoi(getenv("RSOS_HIP_ROUND_COPYIN")) : 0;
+    // A device round in two halves: round_issue queues its copies and launches, round_complete
+    // waits for it and points the outputs at it.  Several stores on one device issue their rounds
+    // back to back and then wait (rh::store_round_issue, the sharded store), so their host gaps and
+    // device work overlap; protocol_round is the two in turn.
+    struct RoundPending {
+        bool on = false, tiny = false, view = false, zero_copy = false, direct = false;
+        uint64_t seq = 0, cap = 0;
+        size_t r = 0, worst = 0;
+        rh::RoundIn din{};
+        rh::RoundRun run{};
+        rh::RoundSegs g{};
+        uint64_t *place = nullptr;
+        double h0 = 0, hv = 0, hs = 0, h1 = 0, h2 = 0, l0 = 0, l1 = 0;
+    } rp;
     int protocol_round(int policy, uint64_t param, const rh_segments &in, rh_segments *ch, rh_segments *en,
                        rh_round_outcome *oc) {
+        const int rc = round_issue(policy, param, in, ch, en, oc);
+        if (rc || !rp.on) return rc;
+        return round_complete(ch, en, oc);
+    }
+    int round_issue(int policy, uint64_t param, const rh_segments &in, rh_segments *ch, rh_segments *en,
+                    rh_round_outcome *oc) {
         int rc;
         const size_t r = in.n;
         const double h0 = round_dbg ? now_us() : 0;
+        rp.on = false;
         if (oc) *oc = rh_round_outcome{};
         *ch = rh_segments{};
         *en = rh_segments{};
@@ -2964,10 +2985,33 @@ struct rh_store {
             const double h1 = round_dbg ? now_us() : 0;
             RH_HIP(kops->round_tiny(t, stream));
             const double h2 = round_dbg ? now_us() : 0;
-            if ((rc = wait_word(reinterpret_cast<const uint64_t *>(pr_out.data()) + 7, t.seq))) return rc;
+            rp.tiny = true, rp.seq = t.seq, rp.h1 = h1, rp.h2 = h2;
+            rp.cap = cap, rp.r = r, rp.view = view, rp.din = din, rp.run = run, rp.g = g, rp.place = place;
+            rp.h0 = h0, rp.hv = hv, rp.hs = hs;
+            rp.on = true;
+            return RH_OK;
+        }
+        const double l0 = round_dbg ? now_us() : 0;
+        if ((rc = round_launch(r, b, n, sq, cap, worst, zero_copy, out_p, view, din, run, g, place, hdr, d_skeys, d_rem)))
+            return rc;
+        rp.tiny = false, rp.cap = cap, rp.r = r, rp.worst = worst, rp.zero_copy = zero_copy, rp.direct = rq_direct;
+        rp.view = view, rp.din = din, rp.run = run, rp.g = g, rp.place = place;
+        rp.h0 = h0, rp.l0 = l0, rp.l1 = round_dbg ? now_us() : 0;
+        rp.on = true;
+        return RH_OK;
+    }
+    int round_complete(rh_segments *ch, rh_segments *en, rh_round_outcome *oc) {
+        int rc;
+        rp.on = false;
+        uint64_t h[5];
+        const size_t r = rp.r;
+        const uint64_t cap = rp.cap;
+        if (rp.tiny) {
+            const double h0 = rp.h0, hv = rp.hv, hs = rp.hs, h1 = rp.h1, h2 = rp.h2;
+            if ((rc = wait_word(reinterpret_cast<const uint64_t *>(pr_out.data()) + 7, rp.seq))) return rc;
             const double h3 = round_dbg ? now_us() : 0;
             memcpy(h, pr_out.data(), sizeof h);
-            rc = round_finish(h, cap, r, view, din, run, g, place, false, ch, en, oc);
+            rc = round_finish(h, cap, r, rp.view, rp.din, rp.run, rp.g, rp.place, false, ch, en, oc);
             if (round_dbg) {  // phase times of this round (10 ns ticks), summed until the store is destroyed
                 const double h4 = now_us();
                 if (round_dbg == 1) {
@@ -2984,6 +3028,30 @@ struct rh_store {
             }
             return rc;
         }
+        const double h0 = rp.h0, l0 = rp.l0, l1 = rp.l1;
+        const bool zero_copy = rp.zero_copy, direct = rp.direct;
+        const size_t worst = rp.worst;
+        if ((rc = sync())) return rc;
+        memcpy(h, pr_out.data(), sizeof h);
+        if ((zero_copy || direct) && round_dbg && r > 1024) {  // the large rounds' host times: prep, launches, wait
+            const double l2 = now_us();
+            dbg_large[0] += l0 - h0, dbg_large[1] += l1 - l0, dbg_large[2] += l2 - l1;
+            if (dbg_large_last > 0 && h0 - dbg_large_last < 5000) dbg_large[3] += h0 - dbg_large_last;
+            dbg_large_n++;
+        }
+        rc = round_finish(h, cap, r, rp.view, rp.din, rp.run, rp.g, rp.place, worst > kRoundSmall && !direct, ch, en, oc);
+        if (round_dbg) dbg_large_last = now_us();
+        return rc;
+    }
+    bool rq_direct = false;  // round_launch: the round goes straight to mapped memory
+    // a round's device work after its input is staged (the multi-launch path), up to the copy of
+    // its header (or the whole small round) to the host: queued, not waited for
+    int round_launch(size_t r, uint64_t b, uint64_t n, int sq, uint64_t cap, size_t worst, bool zero_copy,
+                     uint8_t *out_p, bool view, const rh::RoundIn &din, const rh::RoundRun &run,
+                     const rh::RoundSegs &g, uint64_t *place, uint64_t *hdr, const uint8_t *d_skeys,
+                     const uint64_t *d_rem) {
+        int rc;
+        uint64_t *nch = g.nch, *choff = g.choff, *nen = g.nen, *enoff = g.enoff;
         const double l0 = round_dbg ? now_us() : 0;
         if (nb)
             RH_HIP(kops->search_sampled(bkeys[cb].p, nb, bsmp.p, bsmp2.p, d_skeys, 2 * r, q_rank.p, nullptr, stream,
@@ -3041,30 +3109,13 @@ struct rh_store {
         if (direct)  // the round (or, emitted in place, its header alone)
             RH_HIP(rh::launch_round_copy_out(hdr, cap, (uint32_t)kl, r_out.p, dout, round_copyout == 2 ? 64 : worst,
                                              stream));
-        const double l1 = round_dbg ? now_us() : 0;
-        if (zero_copy || direct) {
-            if ((rc = sync())) return rc;
-            memcpy(h, pr_out.data(), sizeof h);
-            if (round_dbg && r > 1024) {  // the large rounds' host times: prep, launches, wait
-                const double l2 = now_us();
-                dbg_large[0] += l0 - h0, dbg_large[1] += l1 - l0, dbg_large[2] += l2 - l1;
-                if (dbg_large_last > 0 && h0 - dbg_large_last < 5000) dbg_large[3] += h0 - dbg_large_last;
-                dbg_large_n++;
-            }
-        } else if (worst <= kRoundSmall) {
-            pr_out.resize(worst);
-            RH_HIP(hipMemcpyAsync(pr_out.data(), r_out.p, worst, hipMemcpyDeviceToHost, stream));
-            if ((rc = sync())) return rc;
-            memcpy(h, pr_out.data(), sizeof h);
-        } else {
-            pr_out.resize(64);
-            RH_HIP(hipMemcpyAsync(pr_out.data(), r_out.p, 64, hipMemcpyDeviceToHost, stream));
-            if ((rc = sync())) return rc;
-            memcpy(h, pr_out.data(), sizeof h);
+        rq_direct = direct;
+        if (!zero_copy && !direct) {  // the round (small) or its header comes down behind the work
+            const size_t bytes = worst <= kRoundSmall ? worst : 64;
+            pr_out.resize(bytes);
+            RH_HIP(hipMemcpyAsync(pr_out.data(), r_out.p, bytes, hipMemcpyDeviceToHost, stream));
         }
-        rc = round_finish(h, cap, r, view, din, run, g, place, worst > kRoundSmall && !direct, ch, en, oc);
-        if (round_dbg) dbg_large_last = now_us();
-        return rc;
+        return RH_OK;
     }
     // the round's header is in h (and pr_out): emit again if its children outnumber cap (a wide
     // fan-out; the per-segment arrays are in g / place), copy the rest down if it is still on the
@@ -3207,6 +3258,9 @@ static int flush_locked(rh_store *s) {
     RH_HIP(hipSetDevice(s->device));
     return s->flush();
 }
+
+static int round_entry(rh_store *s, int policy, uint64_t fan_out, const rh_segments *active, rh_segments *children,
+                       rh_segments *enumerations, rh_round_outcome *outcome, bool *pending);
 
 // Under the store's lock: 1 if the host tier answers (refreshing it first if the store changed
 // since; only then is the device touched), 0 if the tier is off, < 0 on error
@@ -3453,6 +3507,16 @@ int rh_store_split_segments(rh_store *s, size_t m, const uint64_t *select_ranks,
 
 int rh_store_protocol_round(rh_store *s, int policy, uint64_t fan_out, const rh_segments *active,
                             rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome) {
+    return round_entry(s, policy, fan_out, active, children, enumerations, outcome, nullptr);
+}
+
+}  // extern "C"
+
+// rh_store_protocol_round; with `pending` non-NULL a device round is only issued: *pending = true,
+// the store stays locked, and rh::store_round_complete finishes it (on the same thread)
+static int round_entry(rh_store *s, int policy, uint64_t fan_out, const rh_segments *active, rh_segments *children,
+                       rh_segments *enumerations, rh_round_outcome *outcome, bool *pending) {
+    if (pending) *pending = false;
     if (!s || !active || !children || !enumerations) return fail(RH_ERR_ARG, "NULL");
     if (policy != RH_POLICY_FIXED_FAN_OUT && policy != RH_POLICY_SQRT_FAN_OUT) return fail(RH_ERR_ARG, "unknown policy");
     const size_t r = active->n;
@@ -3492,6 +3556,24 @@ int rh_store_protocol_round(rh_store *s, int policy, uint64_t fan_out, const rh_
             return fail(RH_ERR_OOM, "protocol round: host allocation failed");
         }
     }
+    if (pending) {
+        std::unique_lock<std::mutex> g(s->mu);
+        RH_HIP(hipSetDevice(s->device));
+        int rc = s->flush();
+        if (rc) return rc;
+        try {
+            rc = s->round_issue(policy, fan_out, *active, children, enumerations, outcome);
+        } catch (const std::bad_alloc &) {
+            s->rp.on = false;
+            *children = rh_segments{};
+            *enumerations = rh_segments{};
+            return fail(RH_ERR_OOM, "protocol round: host allocation failed");
+        }
+        if (rc || !s->rp.on) return rc;
+        g.release();  // held until rh::store_round_complete
+        *pending = true;
+        return RH_OK;
+    }
     RH_LOCK(s);
     try {  // no exception crosses the C ABI
         return s->protocol_round(policy, fan_out, *active, children, enumerations, outcome);
@@ -3501,6 +3583,27 @@ int rh_store_protocol_round(rh_store *s, int policy, uint64_t fan_out, const rh_
         return fail(RH_ERR_OOM, "protocol round: host allocation failed");
     }
 }
+
+namespace rh {
+int store_round_issue(rh_store *s, int policy, uint64_t fan_out, const rh_segments *active, rh_segments *children,
+                      rh_segments *enumerations, rh_round_outcome *outcome, bool *pending) {
+    return round_entry(s, policy, fan_out, active, children, enumerations, outcome, pending);
+}
+int store_round_complete(rh_store *s, rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome) {
+    std::unique_lock<std::mutex> g(s->mu, std::adopt_lock);  // taken by store_round_issue
+    try {
+        const int rc = s->round_complete(children, enumerations, outcome);
+        if (rc) *children = rh_segments{}, *enumerations = rh_segments{};
+        return rc;
+    } catch (const std::bad_alloc &) {
+        *children = rh_segments{};
+        *enumerations = rh_segments{};
+        return fail(RH_ERR_OOM, "protocol round: host allocation failed");
+    }
+}
+}  // namespace rh
+
+extern "C" {
 
 int rh_store_fingerprints(rh_store *s, uint64_t lo, uint64_t hi, uint8_t *host_out) {
     if (!s) return fail(RH_ERR_ARG, "store is NULL");

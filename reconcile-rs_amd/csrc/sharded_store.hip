@@ -28,6 +28,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <numeric>
 #include <new>
 #include <string>
 #include <thread>
@@ -40,6 +41,11 @@
 namespace rh {
 int set_error(int code, const std::string &msg);  // rsos_hip_abi.hip: the calling thread's rh_last_error
 bool debug_fail_point(const char *name);          // rh_debug_fail_point, armed on the calling thread
+// rh_store_protocol_round in two halves (rsos_hip_abi.hip round_entry): a device round issued
+// (*pending: the store stays locked) and completed later on the same thread
+int store_round_issue(rh_store *s, int policy, uint64_t fan_out, const rh_segments *active, rh_segments *children,
+                      rh_segments *enumerations, rh_round_outcome *outcome, bool *pending);
+int store_round_complete(rh_store *s, rh_segments *children, rh_segments *enumerations, rh_round_outcome *outcome);
 }
 
 namespace {
@@ -214,6 +220,7 @@ struct rh_sstore {
     std::vector<uint8_t> root_ok;
     bool tier_on = false;  // the shards' host tiers (rh_sstore_set_host_tier): their questions are
                            // microseconds, asked on the calling thread
+    uint64_t round_max = 128;  // ... and rounds of up to this many segments per shard go to them
     void changed() {
         sizes_ok = false;
         std::fill(root_ok.begin(), root_ok.end(), 0);
@@ -333,18 +340,62 @@ struct rh_sstore {
         return (int)(std::upper_bound(off.begin() + 1, off.begin() + G, r) - (off.begin() + 1));
     }
     // run fn over shards concurrently and collect the first error (with its message)
-    int each(const std::vector<int> &idx, const std::function<int(int)> &fn) {
+    // Shards on one device: their calls from concurrent threads contend for that device's queues
+    // and the runtime's locks, so by default one thread per device runs its shards' calls in turn
+    // (RSOS_HIP_SSTORE_GROUP=0: one thread per shard whatever the devices)
+    std::vector<int> dev;  // each shard's device
+    bool shared_devices = false;
+    static bool group_env() {
+        static const bool on = !(getenv("RSOS_HIP_SSTORE_GROUP") && atoi(getenv("RSOS_HIP_SSTORE_GROUP")) == 0);
+        return on;
+    }
+    // group = false: one thread per shard even on a shared device (host-only work: the host tiers'
+    // answers, copies)
+    int each(const std::vector<int> &idx, const std::function<int(int)> &fn, bool group = true) {
         std::vector<Status> ss(G);
-        pool->run(idx, [&](int s) {
+        auto one = [&](int s) {
             try {
                 ss[s].take(fn(s));
             } catch (...) {
                 caught(ss[s]);
             }
-        });
+        };
+        if (group && shared_devices && group_env() && idx.size() > 1) {
+            // the first shard of each device in idx leads its device's group
+            std::vector<int> lead;
+            std::vector<std::vector<int>> grp(G);
+            for (int s : idx) {
+                int l = -1;
+                for (int t : lead)
+                    if (dev[t] == dev[s]) l = t;
+                if (l < 0) lead.push_back(l = s);
+                grp[l].push_back(s);
+            }
+            pool->run(lead, [&](int l) {
+                for (int s : grp[l]) one(s);
+            });
+        } else {
+            pool->run(idx, one);
+        }
         for (int s : idx)
             if (ss[s].rc) return fail(ss[s].rc, ss[s].msg);
         return RH_OK;
+    }
+    // fn(group) per device: the shards of idx on one device together (in idx order), the devices
+    // concurrently (every shard its own group when no device holds two)
+    int each_device(const std::vector<int> &idx, const std::function<int(const std::vector<int> &)> &fn,
+                    bool group = true) {
+        std::vector<int> lead;
+        std::vector<std::vector<int>> grp(G);
+        for (int s : idx) {
+            int l = -1;
+            if (group && shared_devices && group_env())
+                for (int t : lead)
+                    if (dev[t] == dev[s]) l = t;
+            if (l < 0) lead.push_back(l = s);
+            grp[l].push_back(s);
+        }
+        return each(lead, [&](int l) { return fn(grp[l]); }, group);
     }
     std::vector<int> all() const {
         std::vector<int> v(G);
@@ -718,7 +769,7 @@ struct rh_sstore {
     int protocol_round(int policy, uint64_t fan_out, const rh_segments &in, rh_segments *ch, rh_segments *en,
                        rh_round_outcome *oc) {
         const double t0 = dbg() ? now_us() : 0;
-        std::vector<double> shard_us(dbg() ? G : 0, 0.0);
+        std::vector<double> shard_us(dbg() ? G : 0, 0.0), verify_us(dbg() ? G : 0, 0.0);
         std::vector<Run> runs;
         bool fast = route_sorted(in, runs);
         if (!fast) route_each(in, runs);
@@ -748,35 +799,70 @@ struct rh_sstore {
             if (!cross.empty() && (rc = cross_round(policy, fan_out, in, runs, cross, outs))) return rc;
             t2 = dbg() ? now_us() : 0;
             std::atomic<bool> unsorted{false};
-            rc = each(idx, [&](int s) -> int {
+            auto sub_of = [&](size_t k) {
+                const Run &R = runs[k];
+                const size_t j = R.j0;
+                return rh_segments{const_cast<uint8_t *>(sk + j), skeys ? const_cast<uint8_t *>(skeys + j * kl) : nullptr,
+                                   const_cast<uint8_t *>(ek + j), ekeys ? const_cast<uint8_t *>(ekeys + j * kl) : nullptr,
+                                   in.aggregates + j, R.j1 - R.j0, R.j1 - R.j0};
+            };
+            // per device: every shard's round issued, then each completed -- the device runs one
+            // shard's round while the host issues the next, and the host waits once per shard at
+            // the end instead of between them
+            // every shard's piece within its host tier's round size: host work only, one thread
+            // per shard whatever the devices
+            bool host_only = tier_on;
+            for (int s : idx)
+                for (size_t k : mine[s]) host_only = host_only && runs[k].j1 - runs[k].j0 <= round_max;
+            rc = each_device(idx, [&](const std::vector<int> &gs) -> int {
                 const double u0 = dbg() ? now_us() : 0;
-                struct Clock {  // the shard's own time, however the task ends
-                    std::vector<double> &v;
-                    int s;
-                    double u0;
-                    ~Clock() {
-                        if (!v.empty()) v[s] = now_us() - u0;
+                int first = RH_OK;
+                std::string msg;
+                auto keep = [&](int q) {
+                    if (q && !first) first = q, msg = rh_last_error() ? rh_last_error() : "";
+                };
+                std::vector<std::pair<int, size_t>> pend;  // (shard, run) issued, to complete
+                for (int s : gs) {
+                    if (first) break;
+                    const double v0 = dbg() ? now_us() : 0;
+                    if (fast && !pairs_sorted(in, runs[mine[s][0]].j0, runs[mine[s][0]].j1)) {
+                        unsorted = true;
+                        continue;
                     }
-                } clk{shard_us, s, u0};
-                if (fast && !pairs_sorted(in, runs[mine[s][0]].j0, runs[mine[s][0]].j1)) {
-                    unsorted = true;
-                    return RH_OK;
+                    if (!verify_us.empty()) verify_us[s] = now_us() - v0;
+                    if (mine[s].size() == 1) {
+                        const size_t k = mine[s][0];
+                        const rh_segments sub = sub_of(k);
+                        rh_segments c{}, e{};
+                        rh_round_outcome o{};
+                        bool pending = false;
+                        const int q = rh::store_round_issue(shards[s], policy, fan_out, &sub, &c, &e, &o, &pending);
+                        keep(q);
+                        if (!q && pending) pend.emplace_back(s, k);
+                        else if (!q) outs[k].borrow(c, e, o);
+                        continue;
+                    }
+                    for (size_t k : mine[s]) {  // a shard asked for several runs: one at a time, copied
+                        const rh_segments sub = sub_of(k);
+                        rh_segments c{}, e{};
+                        rh_round_outcome o{};
+                        const int q = rh_store_protocol_round(shards[s], policy, fan_out, &sub, &c, &e, &o);
+                        keep(q);
+                        if (q) break;
+                        outs[k].take(c, e, o, kl);
+                    }
                 }
-                for (size_t k : mine[s]) {
-                    const Run &R = runs[k];
-                    const size_t j = R.j0;
-                    const rh_segments sub{const_cast<uint8_t *>(sk + j), skeys ? const_cast<uint8_t *>(skeys + j * kl) : nullptr,
-                                          const_cast<uint8_t *>(ek + j), ekeys ? const_cast<uint8_t *>(ekeys + j * kl) : nullptr,
-                                          in.aggregates + j, R.j1 - R.j0, R.j1 - R.j0};
+                for (const auto &p : pend) {  // every issued round completes (it holds its store's lock)
                     rh_segments c{}, e{};
                     rh_round_outcome o{};
-                    const int q = rh_store_protocol_round(shards[s], policy, fan_out, &sub, &c, &e, &o);
-                    if (q) return q;
-                    if (mine[s].size() == 1) outs[k].borrow(c, e, o);
-                    else outs[k].take(c, e, o, kl);
+                    const int q = rh::store_round_complete(shards[p.first], &c, &e, &o);
+                    keep(q);
+                    if (!q) outs[p.second].borrow(c, e, o);
                 }
-                return RH_OK;
-            });
+                if (!shard_us.empty())
+                    for (int s : gs) shard_us[s] = now_us() - u0;
+                return first ? rh::set_error(first, msg) : RH_OK;
+            }, !host_only);
             if (rc) return rc;
             t3 = dbg() ? now_us() : 0;
             if (!unsorted) break;
@@ -815,7 +901,7 @@ struct rh_sstore {
                         for (size_t k = 0; k < runs.size(); k++)
                             if (runs[k].shard < 0) outs[k].put_into(o, L, at_c[k], at_e[k], kl);
                     return RH_OK;
-                });
+                }, false);
                 if (rc) return rc;
             } else {
                 for (size_t k = 0; k < outs.size(); k++) outs[k].put_into(o, L, at_c[k], at_e[k], kl);
@@ -832,10 +918,10 @@ struct rh_sstore {
             fprintf(stderr,
                     "{\"sstore_round\": %zu, \"sorted\": %d, \"runs\": %zu, \"cross\": %zu, \"shards\": %zu, "
                     "\"route_us\": %.1f, \"cross_us\": %.1f, \"shards_us\": %.1f, \"slowest_shard_us\": %.1f, "
-                    "\"assemble_us\": %.1f, \"children\": %llu}\n",
+                    "\"assemble_us\": %.1f, \"verify_us_sum\": %.1f, \"children\": %llu}\n",
                     in.n, (int)fast, runs.size(), ncross, idx.size(), t1 - t0, t2 - t1, t3 - t2,
                     shard_us.empty() ? 0.0 : *std::max_element(shard_us.begin(), shard_us.end()), t4 - t3,
-                    (unsigned long long)nc);
+                    std::accumulate(verify_us.begin(), verify_us.end(), 0.0), (unsigned long long)nc);
         }
         return RH_OK;
     }
@@ -931,6 +1017,9 @@ int rh_sstore_create(const int *devices, int n, const rh_schema *schema, rh_ssto
     s->G = n;
     s->kl = (size_t)key_row(*schema);
     s->shards.assign(n, nullptr);
+    s->dev.assign(devices, devices + n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < i; j++) s->shared_devices |= devices[i] == devices[j];
     for (int i = 0; i < n; i++) {
         const int rc = rh_store_create(devices[i], schema, &s->shards[i]);
         if (rc) {
@@ -1378,6 +1467,7 @@ int rh_sstore_set_host_tier(rh_sstore *s, int enable, uint64_t round_max) {
     if (enable < 0 || enable > 1) return fail(RH_ERR_ARG, "bad host tier setting");
     const int rc = s->each(s->all(), [&](int t) -> int { return rh_store_set_host_tier(s->shards[t], enable, round_max); });
     s->tier_on = rc == RH_OK ? enable == 1 : false;
+    s->round_max = round_max ? round_max : 128;
     return rc;
 }
 

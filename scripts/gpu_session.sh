@@ -117,6 +117,22 @@ for step in "$@"; do
         for g in 4 8; do
             run sstore_dbg_g$g 200 env SSTORE_ROUNDS=1 RSOS_HIP_SSTORE_DBG=1 RSOS_HIP_ROUND_DBG=2 $EX/sstore_client $g 2000000 100 1 3 || exit 1
         done ;;
+    sstore_group_ab)  # shards sharing a device: one thread per device (default) / per shard
+        for gr in 1 0; do
+            for g in 4 8; do
+                run sstore_grp${gr}_g$g 200 env RSOS_HIP_SSTORE_GROUP=$gr SSTORE_ROUNDS=1 $EX/sstore_client $g 2000000 100 1 20 || exit 1
+            done
+        done ;;
+    sstore_dbg8)  # 8 shards, d = 100, 10 warm reps: the rounds' phases and every store's large-round host times
+        run sstore_dbg8 200 env SSTORE_ROUNDS=1 RSOS_HIP_SSTORE_DBG=1 RSOS_HIP_ROUND_DBG=2 $EX/sstore_client 8 2000000 100 1 10 ;;
+    trace_sstore)  # 4 shards, d = 100, 4 reps under a kernel + memory-copy trace (the raw CSVs kept)
+        run trace_sstore 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trss" -o tr -- $EX/sstore_client 4 2000000 100 1 4 ;;
+    sstore_prio_ab)  # 4 / 8 shards on one device: the stores' streams at high priority (default) / plain
+        for pr in 1 0; do
+            for g in 4 8; do
+                run sstore_prio${pr}_g$g 200 env RSOS_HIP_FORE_PRIORITY=$pr SSTORE_ROUNDS=1 $EX/sstore_client $g 2000000 100 1 20 || exit 1
+            done
+        done ;;
     config3_full) run config3_full 600 python3 bench.py --config config3_full ;;
     prof_config5)
         run stats_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c5" -o run -- python3 bench.py --config config5 --cpu-baseline 0

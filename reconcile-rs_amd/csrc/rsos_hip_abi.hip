@@ -272,16 +272,18 @@ hipError_t launch_lift_schema(int kk, int kl, int vk, int vl, int rk, bool tags,
 #define X(name, kk, kl, vk, vl)                                                                               \
     hipError_t launch_lift_search_##name(int rk, bool tags, const DevCols &c, uint64_t n, uint8_t *fps,          \
                                          const uint8_t *q, const SearchJob &jb, const SearchJob &jd,             \
-                                         const NextMinmax &nx, hipStream_t st, bool *supported);
+                                         const NextMinmax &nx, hipStream_t st, bool *supported, hipEvent_t ev0,  \
+                                         hipEvent_t ev1);
 #include "schemas.def"
 #undef X
 
 hipError_t launch_lift_search_schema(int kk, int kl, int vk, int vl, int rk, bool tags, const DevCols &c, uint64_t n,
                                      uint8_t *fps, const uint8_t *q, const SearchJob &jb, const SearchJob &jd,
-                                     const NextMinmax &nx, hipStream_t st, bool *supported) {
+                                     const NextMinmax &nx, hipStream_t st, bool *supported, hipEvent_t ev0,
+                                     hipEvent_t ev1) {
 #define X(name, KK, KL, VK, VL)                           \
     if (kk == KK && kl == KL && vk == VK && vl == VL)     \
-        return launch_lift_search_##name(rk, tags, c, n, fps, q, jb, jd, nx, st, supported);
+        return launch_lift_search_##name(rk, tags, c, n, fps, q, jb, jd, nx, st, supported, ev0, ev1);
 #include "schemas.def"
 #undef X
     *supported = false;
@@ -2232,21 +2234,17 @@ struct rh_store {
             }
             bool supported = false;
             const bool timed = g_time_batch.load() != 0;
-            if (timed) {
-                if (!ls_ev[0]) {
-                    RH_HIP(hipEventCreate(&ls_ev[0]));
-                    RH_HIP(hipEventCreate(&ls_ev[1]));
-                }
-                RH_HIP(hipEventRecord(ls_ev[0], stream));
+            if (timed && !ls_ev[0]) {
+                RH_HIP(hipEventCreate(&ls_ev[0]));
+                RH_HIP(hipEventCreate(&ls_ev[1]));
             }
+            // timed: the launch stamps the events itself (hipExtLaunchKernel), so timing it adds
+            // no marker packets -- and no ~6 us gaps -- around the kernel
             const hipError_t e =
                 rh::launch_lift_search_schema(schema.key_kind, (int)schema.key_len, schema.value_kind, (int)schema.value_len,
                                               schema.record_kind, c.tags != nullptr, dc, m, sfps.p, skeys.p, jb, jd, nx,
-                                              stream, &supported);
-            if (timed && supported && e == hipSuccess) {
-                RH_HIP(hipEventRecord(ls_ev[1], stream));
-                ls_pending = true;
-            }
+                                              stream, &supported, timed ? ls_ev[0] : nullptr, timed ? ls_ev[1] : nullptr);
+            if (timed && supported && e == hipSuccess) ls_pending = true;
             if (e != hipSuccess) return fail(RH_ERR_HIP, std::string("lift + search launch: ") + hipGetErrorString(e));
             if (supported) {
                 if (pre_minmax) *pre_minmax = nx.keys != nullptr;

@@ -300,3 +300,59 @@ def test_sharded_failed_apply_is_sticky_until_a_load(gpu):
     sh.close()
     with pytest.raises(ValueError):
         shard0.size()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tier", [False, True], ids=["device", "host_tier"])
+def test_sharded_rounds_any_segment_order(gpu, tier):
+    """A round's segments normally arrive in key order (a peer's children), which the sharded store
+    routes by 2 (G - 1) binary searches and then verifies (csrc/sharded_store.hip route_sorted).  Out
+    of order -- shuffled children, overlapping and inverted segments, unbounded ones in the middle,
+    as a malformed or hostile peer may send -- the verification fails and every segment is routed on
+    its own (route_each); either way the round equals one store's segment for segment, in the input
+    order, for rounds small enough for the host tier and large enough for the device (the shards'
+    device rounds issued together and completed together on the shared device)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
+    from rsos_hip.sharded import ShardedStore
+    sch = RecordSchema.plain("u64", "u64")
+    rng = np.random.default_rng(31)
+    keys = np.unique(rng.integers(0, 1 << 40, 60000, dtype=np.uint64))
+    cols = {"keys": keys.view(np.uint8).reshape(-1, 8), "values": (keys * 7).view(np.uint8).reshape(-1, 8)}
+    one = GpuFingerprintStore(sch, host_tier=tier)
+    sh = ShardedStore(sch, [0] * G, host_tier=tier)
+    peer = GpuFingerprintStore(sch, host_tier=tier)
+    for st in (one, sh):
+        st.load_bulk(cols)
+    pv = cols["values"].copy()
+    pv[rng.random(len(keys)) < 0.01] ^= 3
+    peer.load_bulk({"keys": cols["keys"], "values": pv})
+    # three rounds in (peer, one, peer): hundreds of key-ordered children from the peer
+    active = R.initial_ranges(sh)
+    for side in (peer, one, peer):
+        ch, en = [], []
+        R.protocol_round_with_policy(side, R.FixedFanOut(16), active, ch, en)
+        active = ch
+    assert len(active) > 200
+
+    def same(segs):
+        a_ch, a_en, b_ch, b_en = [], [], [], []
+        oa = R.protocol_round_with_policy(sh, R.FixedFanOut(16), segs, a_ch, a_en)
+        ob = R.protocol_round_with_policy(one, R.FixedFanOut(16), segs, b_ch, b_en)
+        assert oa == ob
+        assert [(c.start, c.end, c.aggregate) for c in a_ch] == [(c.start, c.end, c.aggregate) for c in b_ch]
+        assert a_en == b_en
+
+    same(active)  # key-ordered: the fast routing
+    for m in (12, 100, len(active)):  # host-tier sized and device sized
+        segs = [active[i] for i in rng.permutation(len(active))[:m]]
+        same(segs)
+        # overlapping, inverted and unbounded segments mixed in
+        extra = []
+        for s in segs[:5]:
+            extra.append(R.RangeAggregate(s.end, s.start, s.aggregate) if s.start is not None and s.end is not None
+                         else s)
+            extra.append(R.RangeAggregate(None, s.end, s.aggregate))
+            extra.append(R.RangeAggregate(s.start, None, s.aggregate))
+        same(segs[: m // 2] + extra + segs[m // 2:])
+    for st in (one, sh, peer):
+        st.close()

@@ -339,17 +339,37 @@ struct rh_sstore {
     int shard_of_rank(uint64_t r) const {
         return (int)(std::upper_bound(off.begin() + 1, off.begin() + G, r) - (off.begin() + 1));
     }
-    // run fn over shards concurrently and collect the first error (with its message)
     // Shards on one device: their calls from concurrent threads contend for that device's queues
-    // and the runtime's locks, so by default one thread per device runs its shards' calls in turn
-    // (RSOS_HIP_SSTORE_GROUP=0: one thread per shard whatever the devices)
+    // and the runtime's locks, so a thread runs up to RSOS_HIP_SSTORE_GROUP shards of one device in
+    // turn (default: all of them; 0 or 1: one thread per shard whatever the devices)
     std::vector<int> dev;  // each shard's device
     bool shared_devices = false;
-    static bool group_env() {
-        static const bool on = !(getenv("RSOS_HIP_SSTORE_GROUP") && atoi(getenv("RSOS_HIP_SSTORE_GROUP")) == 0);
-        return on;
+    static int group_size() {
+        static const int k = [] {
+            const char *e = getenv("RSOS_HIP_SSTORE_GROUP");
+            const int v = e ? atoi(e) : 64;
+            return v < 1 ? 1 : v;
+        }();
+        return k;
     }
-    // group = false: one thread per shard even on a shared device (host-only work: the host tiers'
+    // the shards of idx in groups: a group is up to group_size() shards of one device, in idx order
+    // (every shard its own group with group = false or when no device holds two); lead[i] names
+    // group i by its first shard, grp[lead[i]] its members
+    void grouping(const std::vector<int> &idx, bool group, std::vector<int> &lead,
+                  std::vector<std::vector<int>> &grp) const {
+        lead.clear();
+        grp.assign(G, {});
+        const int k = group && shared_devices ? group_size() : 1;
+        for (int s : idx) {
+            int l = -1;
+            for (int t : lead)
+                if (dev[t] == dev[s] && (int)grp[t].size() < k) l = t;
+            if (l < 0) lead.push_back(l = s);
+            grp[l].push_back(s);
+        }
+    }
+    // run fn over shards concurrently and collect the first error (with its message).  group =
+    // false: one thread per shard even on a shared device (host-only work: the host tiers'
     // answers, copies)
     int each(const std::vector<int> &idx, const std::function<int(int)> &fn, bool group = true) {
         std::vector<Status> ss(G);
@@ -360,42 +380,23 @@ struct rh_sstore {
                 caught(ss[s]);
             }
         };
-        if (group && shared_devices && group_env() && idx.size() > 1) {
-            // the first shard of each device in idx leads its device's group
-            std::vector<int> lead;
-            std::vector<std::vector<int>> grp(G);
-            for (int s : idx) {
-                int l = -1;
-                for (int t : lead)
-                    if (dev[t] == dev[s]) l = t;
-                if (l < 0) lead.push_back(l = s);
-                grp[l].push_back(s);
-            }
-            pool->run(lead, [&](int l) {
-                for (int s : grp[l]) one(s);
-            });
-        } else {
-            pool->run(idx, one);
-        }
+        std::vector<int> lead;
+        std::vector<std::vector<int>> grp;
+        grouping(idx, group, lead, grp);
+        pool->run(lead, [&](int l) {
+            for (int s : grp[l]) one(s);
+        });
         for (int s : idx)
             if (ss[s].rc) return fail(ss[s].rc, ss[s].msg);
         return RH_OK;
     }
-    // fn(group) per device: the shards of idx on one device together (in idx order), the devices
-    // concurrently (every shard its own group when no device holds two)
+    // fn(group) per group of shards (grouping): a device's shards together, the groups concurrently
     int each_device(const std::vector<int> &idx, const std::function<int(const std::vector<int> &)> &fn,
                     bool group = true) {
         std::vector<int> lead;
-        std::vector<std::vector<int>> grp(G);
-        for (int s : idx) {
-            int l = -1;
-            if (group && shared_devices && group_env())
-                for (int t : lead)
-                    if (dev[t] == dev[s]) l = t;
-            if (l < 0) lead.push_back(l = s);
-            grp[l].push_back(s);
-        }
-        return each(lead, [&](int l) { return fn(grp[l]); }, group);
+        std::vector<std::vector<int>> grp;
+        grouping(idx, group, lead, grp);
+        return each(lead, [&](int l) { return fn(grp[l]); }, false);
     }
     std::vector<int> all() const {
         std::vector<int> v(G);

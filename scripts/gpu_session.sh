@@ -117,8 +117,8 @@ for step in "$@"; do
         for g in 4 8; do
             run sstore_dbg_g$g 200 env SSTORE_ROUNDS=1 RSOS_HIP_SSTORE_DBG=1 RSOS_HIP_ROUND_DBG=2 $EX/sstore_client $g 2000000 100 1 3 || exit 1
         done ;;
-    sstore_group_ab)  # shards sharing a device: one thread per device (default) / per shard
-        for gr in 1 0; do
+    sstore_group_ab)  # shards sharing a device: up to 8 / 4 / 2 / 1 shards per thread (RSOS_HIP_SSTORE_GROUP)
+        for gr in 8 4 2 1; do
             for g in 4 8; do
                 run sstore_grp${gr}_g$g 200 env RSOS_HIP_SSTORE_GROUP=$gr SSTORE_ROUNDS=1 $EX/sstore_client $g 2000000 100 1 20 || exit 1
             done

@@ -823,6 +823,19 @@ struct rh_sstore {
                     if (q && !first) first = q, msg = rh_last_error() ? rh_last_error() : "";
                 };
                 std::vector<std::pair<int, size_t>> pend;  // (shard, run) issued, to complete
+                pend.reserve(gs.size());
+                // every issued round completes, however this task ends: it holds its store's lock
+                struct Drain {
+                    std::vector<std::pair<int, size_t>> &pend;
+                    rh_sstore *self;
+                    ~Drain() {
+                        for (const auto &p : pend) {
+                            rh_segments c{}, e{};
+                            rh_round_outcome o{};
+                            (void)rh::store_round_complete(self->shards[p.first], &c, &e, &o);
+                        }
+                    }
+                } drain{pend, this};
                 for (int s : gs) {
                     if (first) break;
                     const double v0 = dbg() ? now_us() : 0;
@@ -853,7 +866,9 @@ struct rh_sstore {
                         outs[k].take(c, e, o, kl);
                     }
                 }
-                for (const auto &p : pend) {  // every issued round completes (it holds its store's lock)
+                while (!pend.empty()) {  // completed in issue order; the rest by `drain` if one throws
+                    const auto p = pend.front();
+                    pend.erase(pend.begin());
                     rh_segments c{}, e{};
                     rh_round_outcome o{};
                     const int q = rh::store_round_complete(shards[p.first], &c, &e, &o);

@@ -9,7 +9,12 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 mark = "k_cs_hist<" if any("k_cs_hist<" in r["Kernel_Name"] for r in rows) and any(
     "k_lift_search<" in r["Kernel_Name"] for r in rows) else "k_lift<"
 lifts = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"] and int(r["Grid_Size_X"]) < 2_000_000]
-batches = [int(b) for b in sys.argv[2:]] or [len(lifts) - 3]
+# "longest": the two batches with the longest spans (the compacting ones), then the arguments
+args = sys.argv[2:]
+if args and args[0] == "longest":
+    spans = sorted(range(len(lifts) - 1), key=lambda b: int(rows[lifts[b + 1]]["Start_Timestamp"]) - int(rows[lifts[b]]["Start_Timestamp"]))
+    args = [str(b) for b in sorted(spans[-2:])] + args[1:]
+batches = [int(b) for b in args] or [len(lifts) - 3]
 for b in batches:
     i0, i1 = lifts[b], lifts[b + 1]
     t0 = int(rows[i0]["Start_Timestamp"])

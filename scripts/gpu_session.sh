@@ -188,6 +188,7 @@ for step in "$@"; do
         run trace_config5 300 rocprofv3 --kernel-trace --output-format csv -d "$O/c5t" -o c5 -- python3 bench.py --config config5 --steps 40 --cpu-baseline 0
         f=$(find "$O/c5t" -name 'c5_kernel_trace.csv' | head -n 1)
         python3 scripts/c5_timeline.py "$f" 20 21 35 36 > "$O/${TAG}_config5_timeline.txt" 2>&1 || true
+        python3 scripts/c5_timeline.py "$f" longest > "$O/${TAG}_config5_compaction_timeline.txt" 2>&1 || true
         rm -f "$f" ;;
     trace_interleave_off)
         run trace_interleave_off 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trio" -o tr -- $EX/tier_interleave 100000000 1000000 6 0 c5 1

@@ -13,7 +13,8 @@
 #                     one bench.py line each (the default is configs[3] at N = 1)
 #   prof_config4      rocprofv3 kernel stats, FETCH_SIZE / WRITE_SIZE and VALU passes of the
 #                     default line at $RECORDS (100 M unless set), summarised into <tag>_*.json
-#   prof_cfg          the same four passes for $CFG at $RECORDS, summarised into <tag>_{traffic,valu}_$CFG.json
+#   prof_cfg          the same four passes for $CFG at $RECORDS (kernel $KRE, default k_lift),
+#                     summarised into <tag>_{traffic,valu}_$CFG.json
 #   config3_full      configs[2] at its stated size (100 M x 1 KiB) with its CPU baseline
 #   sstore_rounds     sstore_client at 4 / 8 shards, d = 100 / 1, tier on, with per-round times
 #   prof_config5      kernel stats + the per-dispatch DRAM byte passes of config5
@@ -102,14 +103,15 @@ for step in "$@"; do
         rm -f "$O"/*_c4_$R/*_kernel_trace.csv "$O"/*_c4_$R/*_counter_collection.csv
         ;;
     prof_cfg)  # kernel stats + FETCH_SIZE / WRITE_SIZE + VALU passes of one line: $CFG at $RECORDS
-        C=${CFG:?} R=$RECORDS
+        # (KRE: the kernel profiled, k_lift unless set; k_snap_lift for CFG=snapshot)
+        C=${CFG:?} R=$RECORDS K=${KRE:-k_lift}
         B="python3 bench.py --config $C --records $R --steps 10 --warmup 3 --cpu-baseline 0 --check 0 --e2e 0"
         run stats_$C 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_$C" -o run -- $B
-        run fetch_$C 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_lift --output-format csv -d "$O/fetch_$C" -o run -- $B
-        run write_$C 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_lift --output-format csv -d "$O/write_$C" -o run -- $B
-        run valu_$C 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex k_lift --output-format csv -d "$O/valu_$C" -o run -- $B
-        python3 scripts/pmc_traffic.py "$O/fetch_$C/run_counter_collection.csv" "$O/write_$C/run_counter_collection.csv" $C "$R" "$O/${TAG}_traffic_$C.json" || exit 1
-        python3 scripts/pmc_valu.py "$O/valu_$C/run_counter_collection.csv" "$O/stats_$C/run_kernel_stats.csv" $C "$R" "$O/${TAG}_valu_$C.json" || exit 1
+        run fetch_$C 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $K --output-format csv -d "$O/fetch_$C" -o run -- $B
+        run write_$C 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex $K --output-format csv -d "$O/write_$C" -o run -- $B
+        run valu_$C 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex $K --output-format csv -d "$O/valu_$C" -o run -- $B
+        python3 scripts/pmc_traffic.py "$O/fetch_$C/run_counter_collection.csv" "$O/write_$C/run_counter_collection.csv" $C "$R" "$O/${TAG}_traffic_$C.json" $K || exit 1
+        python3 scripts/pmc_valu.py "$O/valu_$C/run_counter_collection.csv" "$O/stats_$C/run_kernel_stats.csv" $C "$R" "$O/${TAG}_valu_$C.json" $K || exit 1
         cp "$O/stats_$C/run_kernel_stats.csv" "$O/${TAG}_${C}_kernel_stats.csv"
         rm -f "$O"/*_$C/*_kernel_trace.csv "$O"/*_$C/*_counter_collection.csv
         ;;

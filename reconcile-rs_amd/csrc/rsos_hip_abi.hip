@@ -88,6 +88,32 @@ static hipError_t create_back_stream(hipStream_t *st, int device) {
     (void)hipGetLastError();
     return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
 }
+// The background streams every store on a device shares, one per role (0: the tier refresh's
+// kernels, 1: the row prefix), created once and kept for the process.  A CU mask is a property of
+// a hardware queue, so each CU-masked stream takes a queue of its own: one pair per store made 20
+// queues for 8 shards + their peers on one GPU, and device rounds stalled 8-20 ms behind the queue
+// scheduler (profiles/r06_sstore8_stalls.txt).  The stores' work on them is ordered by events;
+// sharing only serialises background work of different stores.  RSOS_HIP_SHARED_BG=0: per store.
+static bool shared_back_streams() {
+    static const bool on = !getenv("RSOS_HIP_SHARED_BG") || atoi(getenv("RSOS_HIP_SHARED_BG")) != 0;
+    return on;
+}
+static hipError_t back_stream(int device, int role, hipStream_t *st) {
+    if (!shared_back_streams()) return create_back_stream(st, device);
+    static std::mutex mu;
+    static std::vector<hipStream_t> made;  // [2 device + role]
+    std::lock_guard<std::mutex> g(mu);
+    const size_t k = 2 * (size_t)device + (size_t)role;
+    if (k < made.size() && made[k]) {
+        *st = made[k];
+        return hipSuccess;
+    }
+    const hipError_t e = create_back_stream(st, device);
+    if (e != hipSuccess) return e;
+    if (made.size() <= k) made.resize(k + 1, nullptr);
+    made[k] = *st;
+    return hipSuccess;
+}
 
 // rh_debug_batch_timing: HIP events around every large batch's fused lift + search launch
 std::atomic<int> g_time_batch{0};
@@ -1561,7 +1587,7 @@ struct rh_store {
         // copies, on a CU-masked one (create_back_stream): a copy issued on a CU-masked stream
         // held the next write's uploads behind it (write p50 7 -> 100 ms, 10^8 rows)
         RH_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-        RH_HIP(create_back_stream(&kstream, device));
+        RH_HIP(back_stream(device, 0, &kstream));
         RH_HIP(hipEventCreateWithFlags(&rf_ready, hipEventDisableTiming));
         RH_HIP(hipEventCreateWithFlags(&rf_ev, hipEventDisableTiming));
         RH_HIP(hipEventCreateWithFlags(&rf_kdone, hipEventDisableTiming));
@@ -2123,7 +2149,7 @@ struct rh_store {
         if (tier_on && (rc = refresh_room())) return rc;
         // the row prefix's stream now, not at a later question (creating a queue takes ms)
         if (row_prefix == 1 && !pstream) {
-            RH_HIP(create_back_stream(&pstream, device));
+            RH_HIP(back_stream(device, 1, &pstream));
             RH_HIP(hipEventCreateWithFlags(&pre_ev, hipEventDisableTiming));
             RH_HIP(hipEventCreateWithFlags(&pre_base_ev, hipEventDisableTiming));
         }
@@ -2560,7 +2586,7 @@ struct rh_store {
                 }
             }
             if (row_prefix == 1 && pre_b.p && !pstream) {  // its stream too (a queue: milliseconds)
-                RH_HIP(create_back_stream(&pstream, device));
+                RH_HIP(back_stream(device, 1, &pstream));
                 RH_HIP(hipEventCreateWithFlags(&pre_ev, hipEventDisableTiming));
                 RH_HIP(hipEventCreateWithFlags(&pre_base_ev, hipEventDisableTiming));
             }
@@ -2857,7 +2883,7 @@ struct rh_store {
         rh::RoundRun run{};
         rh::RoundSegs g{};
         uint64_t *place = nullptr;
-        double h0 = 0, hv = 0, hs = 0, h1 = 0, h2 = 0, l0 = 0, l1 = 0;
+        double h0 = 0, hv = 0, hs = 0, h1 = 0, h2 = 0, l0 = 0, l1 = 0, c0 = 0;
     } rp;
     int protocol_round(int policy, uint64_t param, const rh_segments &in, rh_segments *ch, rh_segments *en,
                        rh_round_outcome *oc) {
@@ -2994,7 +3020,7 @@ struct rh_store {
             return rc;
         rp.tiny = false, rp.cap = cap, rp.r = r, rp.worst = worst, rp.zero_copy = zero_copy, rp.direct = rq_direct;
         rp.view = view, rp.din = din, rp.run = run, rp.g = g, rp.place = place;
-        rp.h0 = h0, rp.l0 = l0, rp.l1 = round_dbg ? now_us() : 0;
+        rp.h0 = h0, rp.hv = hv, rp.hs = hs, rp.l0 = l0, rp.l1 = round_dbg ? now_us() : 0;
         rp.on = true;
         return RH_OK;
     }
@@ -3026,11 +3052,20 @@ struct rh_store {
             }
             return rc;
         }
+        rp.c0 = round_dbg ? now_us() : 0;
         const double h0 = rp.h0, l0 = rp.l0, l1 = rp.l1;
         const bool zero_copy = rp.zero_copy, direct = rp.direct;
         const size_t worst = rp.worst;
         if ((rc = sync())) return rc;
         memcpy(h, pr_out.data(), sizeof h);
+        if (round_dbg == 3) {  // any multi-launch round over 1 ms, phase by phase (us)
+            const double l2 = now_us();
+            if (l2 - h0 > 1000)
+                fprintf(stderr,
+                        "{\"slow_round_us\": {\"r\": %zu, \"total\": %.1f, \"view\": %.1f, \"stage\": %.1f, "
+                        "\"args\": %.1f, \"launches\": %.1f, \"issue_to_complete\": %.1f, \"wait\": %.1f}}\n",
+                        r, l2 - h0, rp.hv - h0, rp.hs - rp.hv, l0 - rp.hs, l1 - l0, rp.c0 - l1, l2 - rp.c0);
+        }
         if ((zero_copy || direct) && round_dbg && r > 1024) {  // the large rounds' host times: prep, launches, wait
             const double l2 = now_us();
             dbg_large[0] += l0 - h0, dbg_large[1] += l1 - l0, dbg_large[2] += l2 - l1;
@@ -3150,7 +3185,8 @@ struct rh_store {
     int round_fused = getenv("RSOS_HIP_ROUND_FUSED") ? atoi(getenv("RSOS_HIP_ROUND_FUSED")) : 1;
     uint64_t round_seq = 0;
     // RSOS_HIP_ROUND_DBG=1: k_round_tiny's phase clocks and the host's times per round, averaged to
-    // stderr when the store is destroyed; 2: the host's times only (no clock copy per round)
+    // stderr when the store is destroyed; 2: the host's times only (no clock copy per round); 3: as
+    // 2, plus a line for every multi-launch round that took over 1 ms
     int round_dbg = getenv("RSOS_HIP_ROUND_DBG") ? atoi(getenv("RSOS_HIP_ROUND_DBG")) : 0;
     DevBuf<uint64_t> dbg_clk;
     double dbg_sum[6] = {0, 0, 0, 0, 0, 0};
@@ -3208,7 +3244,7 @@ struct rh_store {
         trs[0].release(); trs[1].release(); trun_keys.release();
         tsets[0].release(); tsets[1].release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release(); tier_dsmp.release();
         if (cstream) (void)hipStreamDestroy(cstream);
-        if (kstream) (void)hipStreamDestroy(kstream);
+        if (kstream && !shared_back_streams()) (void)hipStreamDestroy(kstream);
         if (rf_ready) (void)hipEventDestroy(rf_ready);
         if (rf_ev) (void)hipEventDestroy(rf_ev);
         if (rf_kdone) (void)hipEventDestroy(rf_kdone);
@@ -3216,7 +3252,7 @@ struct rh_store {
         snap.release();
         if (pstream) {
             (void)hipStreamSynchronize(pstream);
-            (void)hipStreamDestroy(pstream);
+            if (!shared_back_streams()) (void)hipStreamDestroy(pstream);
             (void)hipEventDestroy(pre_ev);
             (void)hipEventDestroy(pre_base_ev);
             pstream = nullptr, pre_ev = pre_base_ev = nullptr;

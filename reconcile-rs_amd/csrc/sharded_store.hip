@@ -340,17 +340,25 @@ struct rh_sstore {
         return (int)(std::upper_bound(off.begin() + 1, off.begin() + G, r) - (off.begin() + 1));
     }
     // Shards on one device: their calls from concurrent threads contend for that device's queues
-    // and the runtime's locks, so a thread runs up to RSOS_HIP_SSTORE_GROUP shards of one device in
-    // turn (default: all of them; 0 or 1: one thread per shard whatever the devices)
+    // and the runtime's locks, while one thread issuing every shard's device work in turn serialises
+    // the host side of it.  Measured with 4 and 8 shards on one GPU (profiles/r06_sstore_group_ab*:
+    // 1 / 2 / 4 / 8 shards per thread, three boxes): at most 4 threads per device is best at both, so
+    // a thread takes ceil(shards on its device / 4) of them.  RSOS_HIP_SSTORE_GROUP=<k>: k per thread.
     std::vector<int> dev;  // each shard's device
     bool shared_devices = false;
-    static int group_size() {
+    static constexpr int THREADS_PER_DEVICE = 4;
+    static int group_env() {
         static const int k = [] {
             const char *e = getenv("RSOS_HIP_SSTORE_GROUP");
-            const int v = e ? atoi(e) : 64;
-            return v < 1 ? 1 : v;
+            const int v = e ? atoi(e) : 0;
+            return e ? (v < 1 ? 1 : v) : 0;  // 0: automatic
         }();
         return k;
+    }
+    int group_size(int device) const {
+        if (group_env()) return group_env();
+        const int on = (int)std::count(dev.begin(), dev.end(), device);
+        return std::max(1, (on + THREADS_PER_DEVICE - 1) / THREADS_PER_DEVICE);
     }
     // the shards of idx in groups: a group is up to group_size() shards of one device, in idx order
     // (every shard its own group with group = false or when no device holds two); lead[i] names
@@ -359,8 +367,8 @@ struct rh_sstore {
                   std::vector<std::vector<int>> &grp) const {
         lead.clear();
         grp.assign(G, {});
-        const int k = group && shared_devices ? group_size() : 1;
         for (int s : idx) {
+            const int k = group && shared_devices ? group_size(dev[s]) : 1;
             int l = -1;
             for (int t : lead)
                 if (dev[t] == dev[s] && (int)grp[t].size() < k) l = t;
@@ -660,16 +668,36 @@ struct rh_sstore {
         size_t j0, j1;
     };
     // The round's output buffer (round_layout()); grown, never zero-filled: every byte a caller
-    // reads through the returned arrays is written by the assembly
-    std::unique_ptr<uint8_t[]> round_buf;
-    size_t round_cap = 0;
-    uint8_t *round_room(size_t bytes) {
-        if (bytes > round_cap) {
-            round_buf.reset(new uint8_t[bytes + bytes / 4]);
-            round_cap = bytes + bytes / 4;
+    // reads through the returned arrays is written by the assembly.  Page-locked: the peer's next
+    // round reads it, and its shards copy their pieces of it to their devices -- from pageable
+    // memory each such copy went through the runtime's staging buffers and stalled 8-17 ms now and
+    // then under eight shards (profiles/r06_sstore8_stalls.txt).  Pageable if that allocation fails.
+    struct RoundBuf {
+        uint8_t *p = nullptr;
+        size_t cap = 0;
+        bool pinned = false;
+        ~RoundBuf() { drop(); }
+        void drop() {
+            if (p && pinned) (void)hipHostFree(p);
+            else delete[] p;
+            p = nullptr, cap = 0, pinned = false;
         }
-        return round_buf.get();
-    }
+        uint8_t *room(size_t bytes) {
+            if (bytes <= cap) return p;
+            const size_t c = bytes + bytes / 4;
+            drop();
+            void *q = nullptr;
+            if (hipHostMalloc(&q, c, hipHostMallocPortable) == hipSuccess && q) {
+                p = static_cast<uint8_t *>(q), pinned = true;
+            } else {
+                (void)hipGetLastError();
+                p = new uint8_t[c];  // std::bad_alloc: the round's caller reports RH_ERR_OOM
+            }
+            cap = c;
+            return p;
+        }
+    } round_buf;
+    uint8_t *round_room(size_t bytes) { return round_buf.room(bytes); }
 
     // ---- routing a round's segments to the shards --------------------------------------------
     // Generic: each segment's two boundary shards by binary search over the splitters -- O(r log G)
@@ -1468,6 +1496,8 @@ int rh_sstore_protocol_round(rh_sstore *s, int policy, uint64_t fan_out, const r
         rc = s->protocol_round(policy, fan_out, *active, children, enumerations, outcome);
     } catch (const std::bad_alloc &) {
         rc = fail(RH_ERR_OOM, "protocol round: host allocation failed");
+    } catch (...) {  // nothing crosses the C ABI
+        rc = fail(RH_ERR_STATE, "protocol round: internal error");
     }
     if (rc) {
         *children = rh_segments{};

@@ -126,7 +126,7 @@ for step in "$@"; do
             done
         done ;;
     sstore_dbg8)  # 8 shards, d = 100, 10 warm reps: the rounds' phases and every store's large-round host times
-        run sstore_dbg8 200 env SSTORE_ROUNDS=1 RSOS_HIP_SSTORE_DBG=1 RSOS_HIP_ROUND_DBG=2 $EX/sstore_client 8 2000000 100 1 10 ;;
+        run sstore_dbg8 200 env SSTORE_ROUNDS=1 RSOS_HIP_SSTORE_DBG=1 RSOS_HIP_ROUND_DBG=${RDBG:-2} $EX/sstore_client 8 2000000 ${D:-100} 1 10 ;;
     trace_sstore)  # 4 shards, d = 100, 4 reps under a kernel + memory-copy trace (the raw CSVs kept)
         run trace_sstore 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trss" -o tr -- $EX/sstore_client ${SHARDS:-4} 2000000 100 1 4 ;;
     sstore_prio_ab)  # 4 / 8 shards on one device: the stores' streams at high priority (default) / plain

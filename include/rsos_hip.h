@@ -520,8 +520,12 @@ int rh_sstore_compact(rh_sstore *store);
  * "snapshot.load_finish" (the dated store's), "tier.run_copy" (the host tier's copy of the delta
  * run after a large batch: the batch still succeeds, the tier goes stale), "small_batch.merge"
  * (the next small batch's delta merge is reported failed when the store is next entered: that call
- * and every later one return RH_ERR_HIP naming it, until a load replaces the contents).  For tests
- * of error paths only.                                                                       */
+ * and every later one return RH_ERR_HIP naming it, until a load replaces the contents),
+ * "sstore.apply_last_shard" (a sharded apply's last shard).  Three points instead make the next
+ * launch waited for through a sequence word find that word already holding the number it will
+ * store, as a reused buffer may: "round.stale_seq" (a one-launch device round), "query.stale_seq"
+ * (a one-launch device rank / select / aggregate), "small_batch.stale_seq" (a small batch); the
+ * answer must not change.  For tests only.                                                   */
 int rh_debug_fail_point(const char *name);
 
 /* ---- measurement -----------------------------------------------------------------------

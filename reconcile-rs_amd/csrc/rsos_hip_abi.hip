@@ -1001,7 +1001,9 @@ struct rh_store {
         a.upos = upos, a.usrc = usrc, a.rlist = rlist;
         a.mcnt = mcnt.p;
         a.res = res;
+        if (fail_point("small_batch.stale_seq")) sb_res.data()[13] = small_seq + 1;  // a test's stale word
         a.seq = ++small_seq;
+        disarm(sb_res.data() + 13);
         a.fkeys = fk, a.frecs = fr, a.fdrop = fd, a.ffps = ff, a.fops = fo;
         bool supported = false;
         hipError_t e = rh::launch_small_batch_schema(schema.key_kind, (int)schema.key_len, schema.value_kind,
@@ -1050,6 +1052,16 @@ struct rh_store {
     // command on the stream is ordered after -- so a small batch returns without the merge's time
     // and the stream's completion signal.  A stream that fails or drains without the word is an error.
     int wait_small(uint64_t seq) { return wait_word(sb_res.data() + 13, seq); }
+    // A sequence word is cleared before every launch that stores it: the buffer holding it may hold
+    // anything the same sequence number could match -- a larger round's header copied over it (the
+    // round output buffer), or an earlier owner's words (page-locked memory is reused by the runtime
+    // after a store is destroyed) -- and a match would return the previous answer still in place.
+    // (The kernel that last wrote it has been waited for: nothing else writes it meanwhile.)
+    // (RSOS_HIP_SEQ_DISARM=0 skips it: the regression test's control run)
+    static void disarm(uint64_t *w) {
+        static const bool on = !getenv("RSOS_HIP_SEQ_DISARM") || atoi(getenv("RSOS_HIP_SEQ_DISARM")) != 0;
+        if (on) __atomic_store_n(w, 0ull, __ATOMIC_RELEASE);
+    }
     // Poll a word a kernel stores last (after a system-scope fence) into mapped page-locked memory
     int wait_word(const uint64_t *w, uint64_t seq) {
         const auto t0 = std::chrono::steady_clock::now();
@@ -1344,8 +1356,24 @@ struct rh_store {
     // it would make the caller think the batch failed.  Device errors still propagate.
     int post_batch() {
         tier_host_oom = false;
-        const int rc = post_batch_tier();
-        return tier_stale_on_host_oom(rc);
+        const int rc = tier_stale_on_host_oom(post_batch_tier());
+        if (rc == RH_OK) prefetch_run_columns();
+        return rc;
+    }
+    // When the next question is the device's (tier off, or stale until a copy lands), the delta
+    // run's columns for this version are formed now, queued behind the batch on the store's
+    // stream, instead of by that question (a drive's first round paid them: a long run's five
+    // launches over the whole run, both stores).  A failure is left for the question to meet
+    // again.  RSOS_HIP_RUN_PREFETCH=0: at the question, as before.
+    int run_prefetch = getenv("RSOS_HIP_RUN_PREFETCH") ? atoi(getenv("RSOS_HIP_RUN_PREFETCH")) : 1;
+    void prefetch_run_columns() {
+        if (!run_prefetch || nd == 0 || (tier_on && tier_fresh())) return;
+        const std::string keep = g_err;
+        if (run_columns() != RH_OK) {
+            trun_ver = trun_pre_ver = ~0ull;
+            g_err = keep;
+            (void)hipGetLastError();
+        }
     }
     // A failure to pin host memory for the tier leaves the tier stale (questions go to the device;
     // the next write tries again) and is not the caller's error: the write or load has committed.
@@ -2724,7 +2752,9 @@ struct rh_store {
         q.run = run;
         q.bsmp = bsmp.p, q.bsmp2 = bsmp2.p, q.btab = (!bsmp2.p || nb == 0) ? rh::SearchTable{} : base_table();
         q.dsmp = nd ? dsmp[cd].p : nullptr, q.dsmp2 = nd ? dsmp2[cd].p : nullptr;
+        if (fail_point("query.stale_seq")) *reinterpret_cast<uint64_t *>(qt_buf.data() + o_seq) = qt_seq + 1;
         q.out = d + o_out, q.seq_word = reinterpret_cast<uint64_t *>(d + o_seq), q.seq = ++qt_seq;
+        disarm(reinterpret_cast<uint64_t *>(qt_buf.data() + o_seq));
         RH_HIP(kops->query_tiny(q, stream));
         if ((rc = wait_word(reinterpret_cast<const uint64_t *>(qt_buf.data() + o_seq), q.seq))) return rc;
         memcpy(out, qt_buf.data() + o_out, out_bytes);
@@ -3001,7 +3031,9 @@ struct rh_store {
             t.bsmp = bsmp.p, t.bsmp2 = bsmp2.p, t.btab = (!bsmp2.p || nb == 0) ? rh::SearchTable{} : base_table();
             t.dsmp = view ? dsmp[cd].p : nullptr, t.dsmp2 = view ? dsmp2[cd].p : nullptr;
             t.g = g, t.gplace = place, t.r = r, t.n = n, t.sqrt_policy = sq, t.b = b, t.cap = cap, t.out = out_p;
+            if (fail_point("round.stale_seq")) reinterpret_cast<uint64_t *>(pr_out.data())[7] = round_seq + 1;
             t.seq = ++round_seq;
+            disarm(reinterpret_cast<uint64_t *>(pr_out.data()) + 7);
             if (round_dbg == 1) {  // 2: the host's times only (no copy of the clocks after each round)
                 if ((rc = dbg_clk.ensure(8))) return rc;
                 t.dbg = dbg_clk.p;

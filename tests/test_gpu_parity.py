@@ -1716,3 +1716,85 @@ def test_tier_policy_switch(gpu):
     same()
     dev.close()
     tier.close()
+
+
+@pytest.mark.gpu
+def test_waited_launches_ignore_a_stale_sequence_word(gpu):
+    """The one-launch device paths -- a tiny protocol round (k_round_tiny), a tiny rank / select /
+    aggregate (k_query_tiny), a small batch (k_small_batch) -- return when the kernel's sequence
+    word lands in page-locked memory.  That memory may already hold the very number the next
+    launch will store: a larger round's header is copied over the round buffer, and page-locked
+    memory the runtime reuses after a store is destroyed keeps its last owner's words (a sharded
+    round once read a shard's previous answer this way).  So the word is cleared before every such
+    launch.  The fail points put the next number there first; every answer must still equal an
+    identical store's (host tiers off: the device answers)."""
+    from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R, _abi as A
+    from rsos_hip.store import KeyRange
+    sch = RecordSchema.plain("u64", "u64")
+    rng = np.random.default_rng(77)
+    keys = np.unique(rng.integers(0, 1 << 40, 50000, dtype=np.uint64))
+    cols = {"keys": keys.view(np.uint8).reshape(-1, 8), "values": (keys * 3).view(np.uint8).reshape(-1, 8)}
+    a = GpuFingerprintStore(sch, host_tier=False)
+    b = GpuFingerprintStore(sch, host_tier=False)
+    peer = GpuFingerprintStore(sch, host_tier=False)
+    for st in (a, b):
+        st.load_bulk(cols)
+    pv = cols["values"].copy()
+    pv[rng.random(len(keys)) < 0.02] ^= 5
+    peer.load_bulk({"keys": cols["keys"], "values": pv})
+
+    def rounds_equal(segs, point):
+        ch_b, en_b = [], []
+        ob = R.protocol_round_with_policy(b, R.FixedFanOut(16), segs, ch_b, en_b)
+        ch_a, en_a = [], []
+        if point:
+            A.check(A.lib().rh_debug_fail_point(point), "fail point")
+        try:
+            oa = R.protocol_round_with_policy(a, R.FixedFanOut(16), segs, ch_a, en_a)
+        finally:
+            A.lib().rh_debug_fail_point(b"")
+        assert oa == ob
+        assert [(c.start, c.end, c.aggregate) for c in ch_a] == [(c.start, c.end, c.aggregate) for c in ch_b]
+        assert en_a == en_b
+        return ch_b
+
+    # the peer's children of the whole range, then of those: hundreds of segments
+    active = R.initial_ranges(a)
+    for side in (peer, b):
+        ch, en = [], []
+        R.protocol_round_with_policy(side, R.FixedFanOut(16), active, ch, en)
+        active = ch
+    assert len(active) > 100
+    for t in range(12):
+        if t % 3 == 0:
+            rounds_equal(active, None)  # a large round: its header lands in the round buffer
+        m = int(rng.integers(1, 13))
+        rounds_equal([active[i] for i in rng.permutation(len(active))[:m]], b"round.stale_seq")
+    # tiny questions
+    for t in range(8):
+        z = int(keys[int(rng.integers(0, len(keys)))]) + int(rng.integers(0, 2))
+        A.check(A.lib().rh_debug_fail_point(b"query.stale_seq"), "fail point")
+        assert a.rank(z) == b.rank(z)
+        r = int(rng.integers(0, len(keys)))
+        A.check(A.lib().rh_debug_fail_point(b"query.stale_seq"), "fail point")
+        assert a.select(r) == b.select(r)
+        lo, hi = sorted(int(x) for x in rng.integers(0, 1 << 40, 2))
+        A.check(A.lib().rh_debug_fail_point(b"query.stale_seq"), "fail point")
+        assert a.aggregate(KeyRange(lo, hi)) == b.aggregate(KeyRange(lo, hi))
+    A.lib().rh_debug_fail_point(b"")
+    # small batches
+    for t in range(6):
+        k = rng.integers(0, 1 << 40, 3, dtype=np.uint64)
+        one = {"keys": k.view(np.uint8).reshape(-1, 8), "values": (k * 11).view(np.uint8).reshape(-1, 8)}
+        ops = np.zeros(3, np.uint8)
+        counts_b = b.apply(one, ops)
+        A.check(A.lib().rh_debug_fail_point(b"small_batch.stale_seq"), "fail point")
+        try:
+            counts_a = a.apply(one, ops)
+        finally:
+            A.lib().rh_debug_fail_point(b"")
+        assert counts_a == counts_b
+        assert a.size() == b.size() and a.aggregate() == b.aggregate()
+    assert a.batch_stats()["small"] >= 6
+    for st in (a, b, peer):
+        st.close()

@@ -1363,13 +1363,17 @@ struct rh_store {
     // When the next question is the device's (tier off, or stale until a copy lands), the delta
     // run's columns for this version are formed now, queued behind the batch on the store's
     // stream, instead of by that question (a drive's first round paid them: a long run's five
-    // launches over the whole run, both stores).  A failure is left for the question to meet
-    // again.  RSOS_HIP_RUN_PREFETCH=0: at the question, as before.
+    // launches over the whole run, both stores) -- if questions read them after the previous
+    // batch (a stream of batches with no questions between, config5, never pays for them).  A
+    // failure is left for the question to meet again.  RSOS_HIP_RUN_PREFETCH=0: at the question.
     int run_prefetch = getenv("RSOS_HIP_RUN_PREFETCH") ? atoi(getenv("RSOS_HIP_RUN_PREFETCH")) : 1;
+    bool run_cols_asked = false;  // a question read the run's columns since the last batch
     void prefetch_run_columns() {
-        if (!run_prefetch || nd == 0 || (tier_on && tier_fresh())) return;
+        const bool asked = run_cols_asked;
+        run_cols_asked = false;
+        if (!run_prefetch || !asked || nd == 0 || (tier_on && tier_fresh())) return;
         const std::string keep = g_err;
-        if (run_columns() != RH_OK) {
+        if (run_columns(false) != RH_OK) {
             trun_ver = trun_pre_ver = ~0ull;
             g_err = keep;
             (void)hipGetLastError();
@@ -1502,9 +1506,10 @@ struct rh_store {
     // A/B switch: RSOS_HIP_RUNCOL_FUSED=0 forms a short run's columns in the eight launches too
     int run_cols_fused = getenv("RSOS_HIP_RUNCOL_FUSED") ? atoi(getenv("RSOS_HIP_RUNCOL_FUSED")) : 1;
     int run_prep_wait = getenv("RSOS_HIP_RUN_PREP_WAIT") ? atoi(getenv("RSOS_HIP_RUN_PREP_WAIT")) : 1;
-    int run_columns() {
+    int run_columns(bool question = true) {
         int rc;
         const uint64_t n1 = nd;
+        run_cols_asked = run_cols_asked || question;
         if (trun_ver == version && trs[tcur].gs.p) return RH_OK;
         if (rf_on && rf_run && rf_tset == tcur) tcur = 1 - tcur;  // a run copy reads this set
         trun_ver = trun_pre_ver = ~0ull;

@@ -303,15 +303,17 @@ def test_sharded_failed_apply_is_sticky_until_a_load(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shards", [4, 8])
 @pytest.mark.parametrize("tier", [False, True], ids=["device", "host_tier"])
-def test_sharded_rounds_any_segment_order(gpu, tier):
+def test_sharded_rounds_any_segment_order(gpu, tier, shards):
     """A round's segments normally arrive in key order (a peer's children), which the sharded store
     routes by 2 (G - 1) binary searches and then verifies (csrc/sharded_store.hip route_sorted).  Out
     of order -- shuffled children, overlapping and inverted segments, unbounded ones in the middle,
     as a malformed or hostile peer may send -- the verification fails and every segment is routed on
     its own (route_each); either way the round equals one store's segment for segment, in the input
-    order, for rounds small enough for the host tier and large enough for the device (the shards'
-    device rounds issued together and completed together on the shared device)."""
+    order, for rounds small enough for the host tier and large enough for the device.  With 8
+    shards on the one device a thread drives two of them (at most 4 threads per device), issuing
+    both device rounds before completing either."""
     from rsos_hip import GpuFingerprintStore, RecordSchema, rbsr as R
     from rsos_hip.sharded import ShardedStore
     sch = RecordSchema.plain("u64", "u64")
@@ -319,7 +321,7 @@ def test_sharded_rounds_any_segment_order(gpu, tier):
     keys = np.unique(rng.integers(0, 1 << 40, 60000, dtype=np.uint64))
     cols = {"keys": keys.view(np.uint8).reshape(-1, 8), "values": (keys * 7).view(np.uint8).reshape(-1, 8)}
     one = GpuFingerprintStore(sch, host_tier=tier)
-    sh = ShardedStore(sch, [0] * G, host_tier=tier)
+    sh = ShardedStore(sch, [0] * shards, host_tier=tier)
     peer = GpuFingerprintStore(sch, host_tier=tier)
     for st in (one, sh):
         st.load_bulk(cols)

@@ -735,12 +735,36 @@ struct rh_sstore {
         }
         return true;
     }
-    // the pairs (j - 1, j) for j in [j0, j1) are ordered
+    // the pairs (j - 1, j) for j in [j0, j1) are ordered (pair_sorted's rule; integer keys
+    // compared as integers in one tight loop: this check runs over every segment of a round on
+    // the shard threads, ~1.6 ns a segment through cmp())
+    template <class T>
+    static bool pairs_sorted_int(const uint8_t *sk, const uint8_t *skeys, const uint8_t *ek, const uint8_t *ekeys,
+                                 size_t j0, size_t j1) {
+        bool ok = true;
+        for (size_t j = j0; j < j1; j++) {
+            T s0 = 0, s1 = 0, e0 = 0, e1 = 0;
+            if (sk[j - 1]) memcpy(&s0, skeys + (j - 1) * sizeof(T), sizeof(T));
+            if (sk[j]) memcpy(&s1, skeys + j * sizeof(T), sizeof(T));
+            if (ek[j - 1]) memcpy(&e0, ekeys + (j - 1) * sizeof(T), sizeof(T));
+            if (ek[j]) memcpy(&e1, ekeys + j * sizeof(T), sizeof(T));
+            // starts: Unbounded (-inf) only before bounded ones; ends: bounded only before Unbounded (+inf)
+            ok &= sk[j] ? (!sk[j - 1] || s0 <= s1) : !sk[j - 1];
+            ok &= ek[j - 1] ? (!ek[j] || e0 <= e1) : !ek[j];
+        }
+        return ok;
+    }
     bool pairs_sorted(const rh_segments &in, size_t j0, size_t j1) const {
         const uint8_t *sk = in.start_kinds, *ek = in.end_kinds;
         const uint8_t *skeys = static_cast<const uint8_t *>(in.start_keys);
         const uint8_t *ekeys = static_cast<const uint8_t *>(in.end_keys);
-        for (size_t j = std::max<size_t>(j0, 1); j < j1; j++)
+        j0 = std::max<size_t>(j0, 1);
+        if (j0 >= j1) return true;
+        static const uint8_t zkey[64] = {0};
+        const uint8_t *sp = skeys ? skeys : zkey, *ep = ekeys ? ekeys : zkey;  // all-unbounded sides
+        if (schema.key_kind == RH_KEY_U64 && skeys && ekeys) return pairs_sorted_int<uint64_t>(sk, sp, ek, ep, j0, j1);
+        if (schema.key_kind == RH_KEY_U32 && skeys && ekeys) return pairs_sorted_int<uint32_t>(sk, sp, ek, ep, j0, j1);
+        for (size_t j = j0; j < j1; j++)
             if (!pair_sorted(sk, skeys, ek, ekeys, j)) return false;
         return true;
     }

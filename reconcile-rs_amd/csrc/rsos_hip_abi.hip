@@ -98,21 +98,49 @@ static bool shared_back_streams() {
     static const bool on = !getenv("RSOS_HIP_SHARED_BG") || atoi(getenv("RSOS_HIP_SHARED_BG")) != 0;
     return on;
 }
+// Counted by the stores holding them: the last store of a device to let go destroys the stream, so
+// none outlives its stores into the runtime's teardown (a profiler's tool had already finalised
+// there and crashed on one left over).
+struct BackStreams {
+    std::mutex mu;
+    std::vector<hipStream_t> made;  // [2 device + role]
+    std::vector<int> users;
+};
+static BackStreams &back_streams() {
+    static BackStreams *b = new BackStreams();  // never destroyed: stores may outlive static teardown
+    return *b;
+}
 static hipError_t back_stream(int device, int role, hipStream_t *st) {
     if (!shared_back_streams()) return create_back_stream(st, device);
-    static std::mutex mu;
-    static std::vector<hipStream_t> made;  // [2 device + role]
-    std::lock_guard<std::mutex> g(mu);
+    BackStreams &b = back_streams();
+    std::lock_guard<std::mutex> g(b.mu);
     const size_t k = 2 * (size_t)device + (size_t)role;
-    if (k < made.size() && made[k]) {
-        *st = made[k];
-        return hipSuccess;
+    if (b.made.size() <= k) b.made.resize(k + 1, nullptr), b.users.resize(k + 1, 0);
+    if (!b.made[k]) {
+        const hipError_t e = create_back_stream(&b.made[k], device);
+        if (e != hipSuccess) {
+            b.made[k] = nullptr;
+            return e;
+        }
     }
-    const hipError_t e = create_back_stream(st, device);
-    if (e != hipSuccess) return e;
-    if (made.size() <= k) made.resize(k + 1, nullptr);
-    made[k] = *st;
+    b.users[k]++;
+    *st = b.made[k];
     return hipSuccess;
+}
+// a store lets go of its background stream (its work on it has been waited for)
+static void back_stream_put(int device, int role, hipStream_t st) {
+    if (!st) return;
+    if (!shared_back_streams()) {
+        (void)hipStreamDestroy(st);
+        return;
+    }
+    BackStreams &b = back_streams();
+    std::lock_guard<std::mutex> g(b.mu);
+    const size_t k = 2 * (size_t)device + (size_t)role;
+    if (k < b.made.size() && b.made[k] == st && --b.users[k] == 0) {
+        (void)hipStreamDestroy(st);
+        b.made[k] = nullptr;
+    }
 }
 
 // rh_debug_batch_timing: HIP events around every large batch's fused lift + search launch
@@ -3281,7 +3309,7 @@ struct rh_store {
         trs[0].release(); trs[1].release(); trun_keys.release();
         tsets[0].release(); tsets[1].release(); tier_dpre.release(); tier_spre.release(); tier_bpre.release(); tier_dsmp.release();
         if (cstream) (void)hipStreamDestroy(cstream);
-        if (kstream && !shared_back_streams()) (void)hipStreamDestroy(kstream);
+        back_stream_put(device, 0, kstream);
         if (rf_ready) (void)hipEventDestroy(rf_ready);
         if (rf_ev) (void)hipEventDestroy(rf_ev);
         if (rf_kdone) (void)hipEventDestroy(rf_kdone);
@@ -3289,7 +3317,7 @@ struct rh_store {
         snap.release();
         if (pstream) {
             (void)hipStreamSynchronize(pstream);
-            if (!shared_back_streams()) (void)hipStreamDestroy(pstream);
+            back_stream_put(device, 1, pstream);
             (void)hipEventDestroy(pre_ev);
             (void)hipEventDestroy(pre_base_ev);
             pstream = nullptr, pre_ev = pre_base_ev = nullptr;

@@ -471,7 +471,8 @@ int rh_estore_set_host_tier(rh_estore *store, int enable);
  * add over a key-range partition, aggregate.rs:79-89; select goes to the shard holding its rank;
  * a round's segments inside one shard's range are that shard's own round, a segment straddling a
  * boundary is resolved from its two boundary shards and cut on the host), and the shards are
- * driven concurrently by one host thread each.  Every call is synchronous and takes the map's
+ * driven concurrently by host threads (one per shard; at most 4 per device when shards share
+ * one, RSOS_HIP_SSTORE_GROUP overriding).  Every call is synchronous and takes the map's
  * lock: each answer is one snapshot of every shard (rbsr/src/rsos_view.rs:36).
  * Splitters: until the first load the key space is cut evenly (u32 / u64 keys at multiples of
  * 2^32 / n and 2^64 / n, byte keys by their leading 8 bytes), so single inserts spread over the

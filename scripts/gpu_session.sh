@@ -172,6 +172,8 @@ for step in "$@"; do
         run nowait_w1024 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_BG_PREFIX_WGS=1024 $EX/tier_interleave 100000000 1000000 12 1 c5 2 &&
         run nowait_w256 300 env RSOS_HIP_TIER_SYNC=0 RSOS_HIP_BG_PREFIX_WGS=256 $EX/tier_interleave 100000000 1000000 12 1 c5 2 ;;
     interleave_off) run interleave_off 400 $EX/tier_interleave 100000000 1000000 12 0 c5 2 3 ;;
+    trace_nowait_small)  # the no-wait interleave with 3 small cycles after each large batch, under a kernel trace (raw CSVs kept)
+        run trace_nowait_small 400 env RSOS_HIP_TIER_SYNC=0 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/trns" -o tr -- $EX/tier_interleave 100000000 1000000 4 1 c5 1 3 ;;
     trace_interleave_nowait)
         run trace_interleave_nowait 400 env RSOS_HIP_TIER_SYNC=0 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/trinw" -o tr -- $EX/tier_interleave 100000000 1000000 6 1 c5 1
         python3 scripts/copy_summary.py "$O/trinw" > "$O/${TAG}_interleave_nowait_trace_summary.txt" 2>&1 || true
